@@ -1,0 +1,141 @@
+#!/usr/bin/env python
+"""Flagship training-step benchmark: ResNet-50, bf16, synthetic 3x224x224, DDP.
+
+Metric (BASELINE.json): images/sec for the whole job (all ranks), ResNet-50
+on synthetic 3x224x224 data with random-init weights, one process per GPU over
+RCCL (xGMI) when N > 1. Weak scaling: the per-GPU batch is fixed.
+
+Each timed step is a full training step: forward, softmax-cross-entropy,
+backward (DDP bucketed all-reduce over RCCL overlapped with it), optimizer
+step (SGD momentum + weight decay). Nothing is skipped or cached.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B]
+                    [--model resnet50|resnet152|vit_b_16] [--backend native|torch]
+
+For N > 1 launch with torch.distributed.run (one rank per GPU); rank 0 prints
+one JSON line.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+
+BASELINE_METRIC = "images/sec (whole node) ResNet-50 synthetic 3x224x224 at 1/2/4/8 MI355X"
+# Reference-equivalent stack (stock PyTorch-ROCm: autocast bf16, channels_last,
+# MIOpen convs/BN, torch SGD) measured on one MI355X with this same harness
+# (`bench.py --backend torch`), see BASELINE.md. Scaled by N for N GPUs.
+STOCK_1GPU_IMG_S = {"resnet50": 6605.0}
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=30)
+    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--batch", type=int, default=256, help="per-GPU batch")
+    ap.add_argument("--model", default="resnet50")
+    ap.add_argument("--backend", default="native", choices=["native", "torch"])
+    ap.add_argument("--bucket-mb", type=float, default=64.0)
+    ap.add_argument("--comm-hook", default=None, choices=[None, "bf16"])
+    ap.add_argument("--json-out", default=None)
+    return ap.parse_args()
+
+
+def main():
+    args = parse()
+    from pytorch_distributed_template_amd.utils import dist as pdist
+    from pytorch_distributed_template_amd.ops import fused
+    from pytorch_distributed_template_amd import models
+    from pytorch_distributed_template_amd.parallel import wrap_ddp
+    from pytorch_distributed_template_amd.data.synthetic import SyntheticImageLoader
+
+    device = pdist.init_distributed()
+    world = pdist.get_world_size()
+    rank = pdist.get_rank()
+    if device.type != "cuda":
+        raise SystemExit("bench.py needs a GPU")
+    fused.set_backend(args.backend)
+    torch.backends.cudnn.benchmark = True
+
+    torch.manual_seed(1234)
+    ctor = {"resnet50": models.resnet50, "resnet152": models.resnet152, "vit_b_16": models.vit_b_16}[args.model]
+    model = ctor(num_classes=1000).to(device).to(memory_format=torch.channels_last)
+    if args.backend == "native":
+        from pytorch_distributed_template_amd.optim import FusedSGD
+        opt = FusedSGD(model.parameters(), lr=0.1, momentum=0.9, weight_decay=5e-5)
+    else:
+        opt = torch.optim.SGD(model.parameters(), lr=0.1, momentum=0.9, weight_decay=5e-5)
+    model = wrap_ddp(model, device, bucket_cap_mb=args.bucket_mb, broadcast_buffers=False,
+                     gradient_as_bucket_view=True, comm_hook=args.comm_hook)
+
+    loader = SyntheticImageLoader(args.batch, num_samples=args.batch * (args.steps + args.warmup + 2) * world,
+                                  dtype="bfloat16", pool=2, device=device)
+    batches = list(iter(loader))[:2]
+    autocast = args.backend == "torch"
+
+    def step(i):
+        x, y = batches[i % 2]
+        opt.zero_grad(set_to_none=True)
+        with torch.autocast("cuda", dtype=torch.bfloat16, enabled=autocast):
+            out = model(x)
+            loss = fused.softmax_cross_entropy(out, y)
+        loss.backward()
+        opt.step()
+        return loss
+
+    for i in range(args.warmup):
+        loss = step(i)
+    pdist.synchronize()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        loss = step(i)
+    pdist.synchronize()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    t = torch.tensor([elapsed], dtype=torch.float64, device=device)
+    if world > 1:
+        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
+    elapsed = float(t.item())
+    final_loss = float(loss.item())
+
+    ms = elapsed / args.steps * 1e3
+    value = world * args.batch * args.steps / elapsed
+    stock = STOCK_1GPU_IMG_S.get(args.model)
+    rec = {
+        "metric": BASELINE_METRIC if args.model == "resnet50" else f"images/sec (whole node) {args.model} synthetic",
+        "value": round(value, 2),
+        "unit": "images/sec",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(ms, 3),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": round(value / (stock * world), 4) if stock else None,
+        "dtype": "bf16",
+        "data": "synthetic (device-resident random 3x224x224, random-init weights)",
+        "config": {"model": args.model, "global_batch": args.batch * world, "per_gpu_batch": args.batch,
+                   "seq_len": None, "image_size": 224, "parallelism": f"dp{world}",
+                   "backend": args.backend, "optimizer": "SGD(momentum=0.9, wd=5e-5)",
+                   "bucket_cap_mb": args.bucket_mb, "final_loss": round(final_loss, 4),
+                   "max_mem_gib": round(torch.cuda.max_memory_allocated() / 2 ** 30, 2)},
+    }
+    if rank == 0:
+        line = json.dumps(rec)
+        print(line, flush=True)
+        if args.json_out:
+            with open(args.json_out, "w") as f:
+                f.write(line + "\n")
+    pdist.cleanup()
+
+
+if __name__ == "__main__":
+    main()

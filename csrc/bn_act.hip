@@ -1,0 +1,374 @@
+// Fused training-mode BatchNorm(+residual)(+ReLU) for NHWC bf16 activations.
+//
+// Replaces the stock chain  BN-fwd(mean/var, norm) -> add -> relu  and its
+// backward  relu-bwd -> add-bwd -> BN-bwd(dscale/dbias, dx)  (SURVEY §2.6(b):
+// these memory-bound passes cost about as much as the convs at 8 TB/s).
+//
+// Forward : y (conv output) -> per-channel partial (sum, sumsq)   [bn_stats]
+//           (or taken from the conv epilogue)  -> finalize         [bn_finalize]
+//           a = act(y * scale + shift (+ res))  one read, one write [bn_apply]
+// Backward: dz = dA * relu'(.)  ; partial (sum dz, sum dz*(y-mean)) [bn_bwd_reduce]
+//           -> dgamma, dbeta, and dy = k1*dz + k2*y + k3            [bn_bwd_finalize]
+//           dy (and dres = dz for the residual branch) in one pass   [bn_bwd_apply]
+//
+// All element passes move 16 B per lane (8 channels); channel parameters are
+// read as 2x f32x4. Partial sums are [2][R][C] fp32 (R partial rows) and are
+// combined in fp64 by the finalize kernels (deterministic, no atomics).
+#include "pdt_common.h"
+
+namespace {
+
+constexpr int NT = 256;
+
+__device__ __forceinline__ void unpack8(const u32x4& v, float* f) {
+  f[0] = lo_bf(v[0]); f[1] = hi_bf(v[0]);
+  f[2] = lo_bf(v[1]); f[3] = hi_bf(v[1]);
+  f[4] = lo_bf(v[2]); f[5] = hi_bf(v[2]);
+  f[6] = lo_bf(v[3]); f[7] = hi_bf(v[3]);
+}
+
+__device__ __forceinline__ u32x4 pack8(const float* f) {
+  return u32x4{pack2bf(f[0], f[1]), pack2bf(f[2], f[3]), pack2bf(f[4], f[5]), pack2bf(f[6], f[7])};
+}
+
+__device__ __forceinline__ void load8f(const float* p, float* f) {
+  f32x4 a = *reinterpret_cast<const f32x4*>(p);
+  f32x4 b = *reinterpret_cast<const f32x4*>(p + 4);
+  f[0] = a[0]; f[1] = a[1]; f[2] = a[2]; f[3] = a[3];
+  f[4] = b[0]; f[5] = b[1]; f[6] = b[2]; f[7] = b[3];
+}
+
+// -------------------------------------------------------------------- stats
+// grid: G blocks; block b handles rows b, b+G, ... in passes of RP rows.
+__global__ void __launch_bounds__(NT) bn_stats_kernel(const u16* __restrict__ y, float* __restrict__ part, long M,
+                                                      int C) {
+  __shared__ float red[2][NT][8];
+  const int cpr = C / 8;               // chunks per row
+  const int rp = NT / cpr;             // rows per pass
+  const int t = threadIdx.x;
+  const int ch = t % cpr, rr = t / cpr;
+  float s[8] = {0, 0, 0, 0, 0, 0, 0, 0}, q[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  if (rr < rp) {
+    for (long r = (long)blockIdx.x * rp + rr; r < M; r += (long)gridDim.x * rp) {
+      u32x4 v = *reinterpret_cast<const u32x4*>(y + r * C + ch * 8);
+      float f[8];
+      unpack8(v, f);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        s[k] += f[k];
+        q[k] += f[k] * f[k];
+      }
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    red[0][t][k] = s[k];
+    red[1][t][k] = q[k];
+  }
+  __syncthreads();
+  // reduce over rr for each ch
+  if (t < cpr) {
+    float as[8] = {0, 0, 0, 0, 0, 0, 0, 0}, aq[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    for (int j = 0; j < rp; ++j) {
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        as[k] += red[0][j * cpr + t][k];
+        aq[k] += red[1][j * cpr + t][k];
+      }
+    }
+    const long R = gridDim.x;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      part[(long)blockIdx.x * C + t * 8 + k] = as[k];
+      part[(R + blockIdx.x) * C + t * 8 + k] = aq[k];
+    }
+  }
+}
+
+// one thread per channel: combine R partial rows in fp64.
+// outputs: mean, invstd (saved for backward), scale = gamma*invstd, shift = beta - mean*scale,
+// running stats updated in place (unbiased variance), if running_mean != null.
+__global__ void bn_finalize_kernel(const float* __restrict__ part, int R, int C, double count, float eps,
+                                   float momentum, const float* __restrict__ gamma, const float* __restrict__ beta,
+                                   float* __restrict__ mean_out, float* __restrict__ invstd_out,
+                                   float* __restrict__ scale, float* __restrict__ shift,
+                                   float* __restrict__ running_mean, float* __restrict__ running_var) {
+  int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  double s = 0, q = 0;
+  for (int r = 0; r < R; ++r) {
+    s += part[(long)r * C + c];
+    q += part[(long)(R + r) * C + c];
+  }
+  double mean = s / count;
+  double var = q / count - mean * mean;
+  if (var < 0) var = 0;
+  float invstd = (float)(1.0 / sqrt(var + (double)eps));
+  float g = gamma ? gamma[c] : 1.f, b = beta ? beta[c] : 0.f;
+  mean_out[c] = (float)mean;
+  invstd_out[c] = invstd;
+  scale[c] = g * invstd;
+  shift[c] = b - (float)mean * g * invstd;
+  if (running_mean) {
+    double unb = count > 1 ? var * count / (count - 1) : var;
+    running_mean[c] = (1.f - momentum) * running_mean[c] + momentum * (float)mean;
+    running_var[c] = (1.f - momentum) * running_var[c] + momentum * (float)unb;
+  }
+}
+
+// -------------------------------------------------------------------- apply
+template <bool RES, bool RELU>
+__global__ void __launch_bounds__(NT) bn_apply_kernel(const u16* __restrict__ y, const u16* __restrict__ res,
+                                                      u16* __restrict__ out, const float* __restrict__ scale,
+                                                      const float* __restrict__ shift, long n8, int C) {
+  const int cpr = C / 8;
+  for (uint32_t i = blockIdx.x * NT + threadIdx.x; i < (uint32_t)n8; i += gridDim.x * NT) {
+    const int ch = (int)(i % (uint32_t)cpr) * 8;
+    float f[8], sc[8], sh[8];
+    unpack8(reinterpret_cast<const u32x4*>(y)[i], f);
+    load8f(scale + ch, sc);
+    load8f(shift + ch, sh);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) f[k] = f[k] * sc[k] + sh[k];
+    if (RES) {
+      float r[8];
+      unpack8(reinterpret_cast<const u32x4*>(res)[i], r);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) f[k] += r[k];
+    }
+    if (RELU) {
+#pragma unroll
+      for (int k = 0; k < 8; ++k) f[k] = fmaxf(f[k], 0.f);
+    }
+    reinterpret_cast<u32x4*>(out)[i] = pack8(f);
+  }
+}
+
+// -------------------------------------------------------------------- backward
+// relu mask: if `act` (saved output) is given, mask = act > 0; else if RELU,
+// mask = y*scale+shift > 0 (exact when there is no residual).
+template <bool RELU, bool USE_ACT>
+__global__ void __launch_bounds__(NT) bn_bwd_reduce_kernel(const u16* __restrict__ dA, const u16* __restrict__ y,
+                                                           const u16* __restrict__ act,
+                                                           const float* __restrict__ mean,
+                                                           const float* __restrict__ scale,
+                                                           const float* __restrict__ shift,
+                                                           float* __restrict__ part, long M, int C) {
+  __shared__ float red[2][NT][8];
+  const int cpr = C / 8;
+  const int rp = NT / cpr;
+  const int t = threadIdx.x;
+  const int ch = t % cpr, rr = t / cpr;
+  float s[8] = {0, 0, 0, 0, 0, 0, 0, 0}, q[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  if (rr < rp) {
+    float mu[8], sc[8], sh[8];
+    load8f(mean + ch * 8, mu);
+    if (RELU && !USE_ACT) {
+      load8f(scale + ch * 8, sc);
+      load8f(shift + ch * 8, sh);
+    }
+    for (long r = (long)blockIdx.x * rp + rr; r < M; r += (long)gridDim.x * rp) {
+      const long off = r * C + ch * 8;
+      float g[8], yv[8];
+      unpack8(*reinterpret_cast<const u32x4*>(dA + off), g);
+      unpack8(*reinterpret_cast<const u32x4*>(y + off), yv);
+      if (RELU) {
+        if (USE_ACT) {
+          float a[8];
+          unpack8(*reinterpret_cast<const u32x4*>(act + off), a);
+#pragma unroll
+          for (int k = 0; k < 8; ++k) g[k] = a[k] > 0.f ? g[k] : 0.f;
+        } else {
+#pragma unroll
+          for (int k = 0; k < 8; ++k) g[k] = (yv[k] * sc[k] + sh[k]) > 0.f ? g[k] : 0.f;
+        }
+      }
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        s[k] += g[k];
+        q[k] += g[k] * (yv[k] - mu[k]);
+      }
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    red[0][t][k] = s[k];
+    red[1][t][k] = q[k];
+  }
+  __syncthreads();
+  if (t < cpr) {
+    float as[8] = {0, 0, 0, 0, 0, 0, 0, 0}, aq[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    for (int j = 0; j < rp; ++j) {
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        as[k] += red[0][j * cpr + t][k];
+        aq[k] += red[1][j * cpr + t][k];
+      }
+    }
+    const long R = gridDim.x;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      part[(long)blockIdx.x * C + t * 8 + k] = as[k];
+      part[(R + blockIdx.x) * C + t * 8 + k] = aq[k];
+    }
+  }
+}
+
+// dgamma = sum(dz*(y-mean))*invstd, dbeta = sum(dz)
+// dy = k1*dz + k2*y + k3
+__global__ void bn_bwd_finalize_kernel(const float* __restrict__ part, int R, int C, double count,
+                                       const float* __restrict__ gamma, const float* __restrict__ mean,
+                                       const float* __restrict__ invstd, float* __restrict__ dgamma,
+                                       float* __restrict__ dbeta, float* __restrict__ k1, float* __restrict__ k2,
+                                       float* __restrict__ k3, int accumulate) {
+  int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  double s = 0, q = 0;
+  for (int r = 0; r < R; ++r) {
+    s += part[(long)r * C + c];
+    q += part[(long)(R + r) * C + c];
+  }
+  double is = invstd[c], g = gamma ? gamma[c] : 1.0, mu = mean[c];
+  double dg = q * is, db = s;
+  if (dgamma) dgamma[c] = (float)(accumulate ? dgamma[c] + dg : dg);
+  if (dbeta) dbeta[c] = (float)(accumulate ? dbeta[c] + db : db);
+  double a1 = g * is;
+  double a2 = -g * is * is * is * q / count;
+  double a3 = -g * is * s / count - a2 * mu;
+  k1[c] = (float)a1;
+  k2[c] = (float)a2;
+  k3[c] = (float)a3;
+}
+
+template <bool RELU, bool USE_ACT, bool DRES>
+__global__ void __launch_bounds__(NT) bn_bwd_apply_kernel(const u16* __restrict__ dA, const u16* __restrict__ y,
+                                                          const u16* __restrict__ act,
+                                                          const float* __restrict__ scale,
+                                                          const float* __restrict__ shift,
+                                                          const float* __restrict__ k1, const float* __restrict__ k2,
+                                                          const float* __restrict__ k3, u16* __restrict__ dy,
+                                                          u16* __restrict__ dres, long n8, int C) {
+  const int cpr = C / 8;
+  for (uint32_t i = blockIdx.x * NT + threadIdx.x; i < (uint32_t)n8; i += gridDim.x * NT) {
+    const int ch = (int)(i % (uint32_t)cpr) * 8;
+    float g[8], yv[8], a1[8], a2[8], a3[8];
+    unpack8(reinterpret_cast<const u32x4*>(dA)[i], g);
+    unpack8(reinterpret_cast<const u32x4*>(y)[i], yv);
+    if (RELU) {
+      if (USE_ACT) {
+        float a[8];
+        unpack8(reinterpret_cast<const u32x4*>(act)[i], a);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) g[k] = a[k] > 0.f ? g[k] : 0.f;
+      } else {
+        float sc[8], sh[8];
+        load8f(scale + ch, sc);
+        load8f(shift + ch, sh);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) g[k] = (yv[k] * sc[k] + sh[k]) > 0.f ? g[k] : 0.f;
+      }
+    }
+    if (DRES) reinterpret_cast<u32x4*>(dres)[i] = pack8(g);
+    load8f(k1 + ch, a1);
+    load8f(k2 + ch, a2);
+    load8f(k3 + ch, a3);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) g[k] = a1[k] * g[k] + a2[k] * yv[k] + a3[k];
+    reinterpret_cast<u32x4*>(dy)[i] = pack8(g);
+  }
+}
+
+int grid_for(long n8) {
+  long b = (n8 + NT - 1) / NT;
+  if (b > 4096) b = 4096;
+  if (b < 1) b = 1;
+  return (int)b;
+}
+
+}  // namespace
+
+PDT_API int pdt_bn_stats_blocks(long M, int C) {
+  int cpr = C / 8;
+  int rp = NT / cpr;
+  long b = (M + rp - 1) / rp;
+  // ~2 blocks per CU, each streaming many rows
+  if (b > 512) b = 512;
+  if (b < 1) b = 1;
+  return (int)b;
+}
+
+PDT_API int pdt_bn_stats(const void* y, float* part, long M, int C, int blocks, hipStream_t st) {
+  if (C % 8 || C / 8 > NT) return -1;
+  hipLaunchKernelGGL(bn_stats_kernel, dim3(blocks), dim3(NT), 0, st, (const u16*)y, part, M, C);
+  PDT_RETURN_LAUNCH();
+}
+
+PDT_API int pdt_bn_finalize(const float* part, int R, int C, double count, float eps, float momentum,
+                            const float* gamma, const float* beta, float* mean, float* invstd, float* scale,
+                            float* shift, float* running_mean, float* running_var, hipStream_t st) {
+  hipLaunchKernelGGL(bn_finalize_kernel, dim3((C + 255) / 256), dim3(256), 0, st, part, R, C, count, eps, momentum,
+                     gamma, beta, mean, invstd, scale, shift, running_mean, running_var);
+  PDT_RETURN_LAUNCH();
+}
+
+PDT_API int pdt_bn_apply(const void* y, const void* res, void* out, const float* scale, const float* shift, long M,
+                         int C, int relu, hipStream_t st) {
+  if (C % 8) return -1;
+  long n8 = M * C / 8;
+  dim3 g(grid_for(n8)), b(NT);
+  const u16* Y = (const u16*)y;
+  const u16* R = (const u16*)res;
+  u16* O = (u16*)out;
+  if (res) {
+    if (relu) hipLaunchKernelGGL((bn_apply_kernel<true, true>), g, b, 0, st, Y, R, O, scale, shift, n8, C);
+    else hipLaunchKernelGGL((bn_apply_kernel<true, false>), g, b, 0, st, Y, R, O, scale, shift, n8, C);
+  } else {
+    if (relu) hipLaunchKernelGGL((bn_apply_kernel<false, true>), g, b, 0, st, Y, R, O, scale, shift, n8, C);
+    else hipLaunchKernelGGL((bn_apply_kernel<false, false>), g, b, 0, st, Y, R, O, scale, shift, n8, C);
+  }
+  PDT_RETURN_LAUNCH();
+}
+
+PDT_API int pdt_bn_bwd_reduce(const void* dA, const void* y, const void* act, const float* mean,
+                              const float* scale, const float* shift, float* part, long M, int C, int relu,
+                              int blocks, hipStream_t st) {
+  if (C % 8 || C / 8 > NT) return -1;
+  const u16 *G = (const u16*)dA, *Y = (const u16*)y, *A = (const u16*)act;
+  dim3 g(blocks), b(NT);
+  if (!relu)
+    hipLaunchKernelGGL((bn_bwd_reduce_kernel<false, false>), g, b, 0, st, G, Y, A, mean, scale, shift, part, M, C);
+  else if (act)
+    hipLaunchKernelGGL((bn_bwd_reduce_kernel<true, true>), g, b, 0, st, G, Y, A, mean, scale, shift, part, M, C);
+  else
+    hipLaunchKernelGGL((bn_bwd_reduce_kernel<true, false>), g, b, 0, st, G, Y, A, mean, scale, shift, part, M, C);
+  PDT_RETURN_LAUNCH();
+}
+
+PDT_API int pdt_bn_bwd_finalize(const float* part, int R, int C, double count, const float* gamma,
+                                const float* mean, const float* invstd, float* dgamma, float* dbeta, float* k1,
+                                float* k2, float* k3, int accumulate, hipStream_t st) {
+  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + 255) / 256), dim3(256), 0, st, part, R, C, count, gamma,
+                     mean, invstd, dgamma, dbeta, k1, k2, k3, accumulate);
+  PDT_RETURN_LAUNCH();
+}
+
+PDT_API int pdt_bn_bwd_apply(const void* dA, const void* y, const void* act, const float* scale,
+                             const float* shift, const float* k1, const float* k2, const float* k3, void* dy,
+                             void* dres, long M, int C, int relu, hipStream_t st) {
+  if (C % 8) return -1;
+  long n8 = M * C / 8;
+  dim3 g(grid_for(n8)), b(NT);
+  const u16 *G = (const u16*)dA, *Y = (const u16*)y, *A = (const u16*)act;
+  u16 *DY = (u16*)dy, *DR = (u16*)dres;
+#define BWD_APPLY(R_, U_, D_) \
+  hipLaunchKernelGGL((bn_bwd_apply_kernel<R_, U_, D_>), g, b, 0, st, G, Y, A, scale, shift, k1, k2, k3, DY, DR, n8, C)
+  if (!relu) {
+    if (dres) BWD_APPLY(false, false, true); else BWD_APPLY(false, false, false);
+  } else if (act) {
+    if (dres) BWD_APPLY(true, true, true); else BWD_APPLY(true, true, false);
+  } else {
+    if (dres) BWD_APPLY(true, false, true); else BWD_APPLY(true, false, false);
+  }
+#undef BWD_APPLY
+  PDT_RETURN_LAUNCH();
+}

@@ -1,0 +1,350 @@
+// Implicit-GEMM convolution (forward and data-gradient) for NHWC bf16 on
+// MI355X (gfx950) MFMA.  Also serves plain "NT" GEMMs (nn.Linear forward).
+//
+//   C[m, n] = sum_k A[m, k] * B[n, k]            (fp32 accumulate)
+//   A[m, k] = src[n_img, ih, iw, c]  gathered on the fly (zero outside)
+//   k = tap * Cs + c,  tap = (th, tw) on a (nth x ntw) tap grid
+//   ih = oh * sh + oh0 + dh * th,  iw = ow * sw + ow0 + dw * tw
+//
+// forward conv : M-grid = output (Ho, Wo), taps = (kh, kw), oh0 = -pad, dh = 1,
+//                B = weight [Cout][KH][KW][Cin]
+// dgrad conv   : one launch per stride phase (ph, pw): M-grid = (H/s, W/s),
+//                taps = {kh : (ph+pad-kh) % s == 0}, source = dY, dh = -1,
+//                B = phase-sliced transposed weight [Cin][nth][ntw][Cout];
+//                output row (n, ph + s*hh, pw + s*ww) of dX.
+//
+// Tile: BM x BN x 64, 256 threads = 4 wave64s in 2x2, each wave (BM/2)x(BN/2)
+// built from 16x16x32 bf16 MFMAs.  Operands are register-staged
+// (global_load_dwordx4 -> ds_write_b128) into a double-buffered LDS ring with
+// one barrier per K-tile; the next tile's global loads are in flight while
+// the current tile's MFMAs run.  LDS rows are 128 B; 16-B chunks are
+// XOR-swizzled with ((row >> 1) & 7) so every ds_read_b128 lane group hits 16
+// distinct bank slots.
+//
+// The MFMA is issued with operands swapped (D = B·Aᵀ) so each lane holds four
+// *consecutive output channels* of one output row: the epilogue packs them to
+// 8-byte bf16 words, stages the tile through LDS and writes 16-B coalesced rows.
+// Epilogue options: per-channel BatchNorm partial statistics (sum, sum of
+// squares over the tile's rows, from the fp32 accumulators), bias, ReLU.
+#include "pdt_common.h"
+
+namespace {
+
+struct NTParams {
+  const u16* src;
+  const u16* b;
+  u16* out;
+  float* stats;        // optional: [2][nstat_rows][Ncol] partial sums (sum, sumsq)
+  const float* bias;   // optional: [Ncol]
+  int Hs, Ws, Cs;      // source geometry (NHWC, batch implied by M-grid)
+  int Hm, Wm;          // M-grid per image
+  int M, Ncol, K, ldb;
+  int sh, sw, oh0, ow0, dh, dw, nth, ntw;
+  int Ho, Wo, osh, osw, oph, opw, ldo;
+  int relu;
+  int nstat_rows;
+  FastDiv div_Wm, div_HWm, div_Cs8, div_ntw;
+};
+
+constexpr int BK = 64;
+constexpr int NT = 256;
+
+__device__ __forceinline__ int swz(int row, int chunk) { return chunk ^ ((row >> 1) & 7); }
+
+template <int BM, int BN, bool CS64>
+__global__ void __launch_bounds__(NT, 2) conv_nt_kernel(NTParams p) {
+  constexpr int MI = BM / 32;  // 16-row MFMA tiles per wave (wave covers BM/2 rows)
+  constexpr int NI = BN / 32;
+  constexpr int A_BYTES = BM * BK * 2;
+  constexpr int B_BYTES = BN * BK * 2;
+  constexpr int STAGE = A_BYTES + B_BYTES;
+  constexpr int C_STRIDE = BN * 2 + 16;  // bytes per staged output row
+  constexpr int SMEM = (2 * STAGE > BM * C_STRIDE) ? 2 * STAGE : BM * C_STRIDE;
+  __shared__ __attribute__((aligned(16))) char smem[SMEM];
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = tid >> 6;
+  const int wm = wave >> 1, wn = wave & 1;
+
+  const int ntm = (p.M + BM - 1) / BM;
+  const int ntn = (p.Ncol + BN - 1) / BN;
+  const uint32_t logical = xcd_remap(blockIdx.x, ntm * ntn);
+  const int tm = logical / ntn, tn = logical % ntn;
+  const int m0 = tm * BM, n0 = tn * BN;
+
+  // ---- per-thread A rows: r = tid/8 + 32*i, chunk column ca = tid%8
+  const int ca = tid & 7;
+  int a_base[MI], a_ih[MI], a_iw[MI];
+  bool a_ok[MI];
+#pragma unroll
+  for (int i = 0; i < MI; ++i) {
+    int m = m0 + (tid >> 3) + 32 * i;
+    a_ok[i] = m < p.M;
+    uint32_t mm = a_ok[i] ? m : 0;
+    uint32_t img = fdiv(mm, p.div_HWm);
+    uint32_t rem = mm - img * (uint32_t)(p.Hm * p.Wm);
+    uint32_t oh = fdiv(rem, p.div_Wm);
+    uint32_t ow = rem - oh * p.Wm;
+    a_base[i] = img * p.Hs * p.Ws;
+    a_ih[i] = oh * p.sh + p.oh0;
+    a_iw[i] = ow * p.sw + p.ow0;
+  }
+  // ---- per-thread B rows
+  int b_row[NI];
+  bool b_ok[NI];
+#pragma unroll
+  for (int j = 0; j < NI; ++j) {
+    int n = n0 + (tid >> 3) + 32 * j;
+    b_ok[j] = n < p.Ncol;
+    b_row[j] = b_ok[j] ? n : 0;
+  }
+
+  u32x4 ra[MI], rb[NI];
+  const int nk = (p.K + BK - 1) / BK;
+
+  auto load_tile = [&](int kt) {
+    const int k0 = kt * BK;
+    if (CS64) {
+      const int tap = k0 / p.Cs;
+      const int c0 = k0 - tap * p.Cs + ca * 8;
+      const int th = fdiv(tap, p.div_ntw);
+      const int tw = tap - th * p.ntw;
+      const int dho = p.dh * th, dwo = p.dw * tw;
+#pragma unroll
+      for (int i = 0; i < MI; ++i) {
+        int ih = a_ih[i] + dho, iw = a_iw[i] + dwo;
+        bool ok = a_ok[i] && (unsigned)ih < (unsigned)p.Hs && (unsigned)iw < (unsigned)p.Ws;
+        if (ok) {
+          ra[i] = *reinterpret_cast<const u32x4*>(p.src + (size_t)(a_base[i] + ih * p.Ws + iw) * p.Cs + c0);
+        } else {
+          ra[i] = u32x4{0, 0, 0, 0};
+        }
+      }
+    } else {
+      const int kc = k0 / 8 + ca;  // global 8-channel chunk index
+      const bool kin = kc * 8 < p.K;
+      const int tap = fdiv(kc, p.div_Cs8);
+      const int c0 = (kc - tap * (p.Cs / 8)) * 8;
+      const int th = fdiv(tap, p.div_ntw);
+      const int tw = tap - th * p.ntw;
+      const int dho = p.dh * th, dwo = p.dw * tw;
+#pragma unroll
+      for (int i = 0; i < MI; ++i) {
+        int ih = a_ih[i] + dho, iw = a_iw[i] + dwo;
+        bool ok = kin && a_ok[i] && (unsigned)ih < (unsigned)p.Hs && (unsigned)iw < (unsigned)p.Ws;
+        if (ok) {
+          ra[i] = *reinterpret_cast<const u32x4*>(p.src + (size_t)(a_base[i] + ih * p.Ws + iw) * p.Cs + c0);
+        } else {
+          ra[i] = u32x4{0, 0, 0, 0};
+        }
+      }
+    }
+    const int kb = k0 + ca * 8;
+#pragma unroll
+    for (int j = 0; j < NI; ++j) {
+      if (b_ok[j] && kb < p.K) {
+        rb[j] = *reinterpret_cast<const u32x4*>(p.b + (size_t)b_row[j] * p.ldb + kb);
+      } else {
+        rb[j] = u32x4{0, 0, 0, 0};
+      }
+    }
+  };
+
+  auto store_tile = [&](int buf) {
+    char* sa = smem + buf * STAGE;
+    char* sb = sa + A_BYTES;
+#pragma unroll
+    for (int i = 0; i < MI; ++i) {
+      int r = (tid >> 3) + 32 * i;
+      *reinterpret_cast<u32x4*>(sa + r * 128 + swz(r, ca) * 16) = ra[i];
+    }
+#pragma unroll
+    for (int j = 0; j < NI; ++j) {
+      int r = (tid >> 3) + 32 * j;
+      *reinterpret_cast<u32x4*>(sb + r * 128 + swz(r, ca) * 16) = rb[j];
+    }
+  };
+
+  f32x4 acc[MI][NI];
+#pragma unroll
+  for (int i = 0; i < MI; ++i)
+#pragma unroll
+    for (int j = 0; j < NI; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  if (nk > 0) {
+    load_tile(0);
+    store_tile(0);
+  }
+  __syncthreads();
+
+  for (int kt = 0; kt < nk; ++kt) {
+    const int cur = kt & 1;
+    if (kt + 1 < nk) load_tile(kt + 1);
+    const char* sa = smem + cur * STAGE;
+    const char* sb = sa + A_BYTES;
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      const int kch = kk * 4 + (lane >> 4);
+      bf16x8 af[MI], bfr[NI];
+#pragma unroll
+      for (int i = 0; i < MI; ++i) {
+        int r = wm * (BM / 2) + i * 16 + (lane & 15);
+        af[i] = *reinterpret_cast<const bf16x8*>(sa + r * 128 + swz(r, kch) * 16);
+      }
+#pragma unroll
+      for (int j = 0; j < NI; ++j) {
+        int r = wn * (BN / 2) + j * 16 + (lane & 15);
+        bfr[j] = *reinterpret_cast<const bf16x8*>(sb + r * 128 + swz(r, kch) * 16);
+      }
+#pragma unroll
+      for (int i = 0; i < MI; ++i)
+#pragma unroll
+        for (int j = 0; j < NI; ++j)
+          // swapped operands: lane holds 4 consecutive output channels of one row
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[j], af[i], acc[i][j], 0, 0, 0);
+    }
+    if (kt + 1 < nk) store_tile(cur ^ 1);
+    __syncthreads();
+  }
+
+  // ---------------------------------------------------------------- epilogue
+  // acc[i][j][r] = C[row = wm*BM/2 + i*16 + (lane&15)][col = wn*BN/2 + j*16 + (lane>>4)*4 + r]
+  const int lrow = lane & 15;
+  const int lcol = (lane >> 4) * 4;
+  if (p.bias != nullptr || p.relu) {
+#pragma unroll
+    for (int j = 0; j < NI; ++j) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        int col = n0 + wn * (BN / 2) + j * 16 + lcol + r;
+        float bv = (p.bias != nullptr && col < p.Ncol) ? p.bias[col] : 0.f;
+#pragma unroll
+        for (int i = 0; i < MI; ++i) {
+          float v = acc[i][j][r] + bv;
+          acc[i][j][r] = p.relu ? fmaxf(v, 0.f) : v;
+        }
+      }
+    }
+  }
+
+  if (p.stats != nullptr) {
+    // per-wave column partials over its BM/2 rows (invalid rows hold zeros)
+    const int srow = tm * 2 + wm;
+#pragma unroll
+    for (int j = 0; j < NI; ++j) {
+      float s[4], q[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        float a = 0.f, b = 0.f;
+#pragma unroll
+        for (int i = 0; i < MI; ++i) {
+          float v = acc[i][j][r];
+          a += v;
+          b += v * v;
+        }
+        s[r] = a;
+        q[r] = b;
+      }
+#pragma unroll
+      for (int o = 1; o < 16; o <<= 1) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          s[r] += __shfl_xor(s[r], o, 64);
+          q[r] += __shfl_xor(q[r], o, 64);
+        }
+      }
+      if (lrow == 0) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          int col = n0 + wn * (BN / 2) + j * 16 + lcol + r;
+          if (col < p.Ncol) {
+            p.stats[(size_t)srow * p.Ncol + col] = s[r];
+            p.stats[(size_t)(p.nstat_rows + srow) * p.Ncol + col] = q[r];
+          }
+        }
+      }
+    }
+  }
+
+  // stage bf16 tile through LDS: row-major [BM][BN] with a 16-B row pad
+#pragma unroll
+  for (int i = 0; i < MI; ++i) {
+#pragma unroll
+    for (int j = 0; j < NI; ++j) {
+      int r = wm * (BM / 2) + i * 16 + lrow;
+      int c = wn * (BN / 2) + j * 16 + lcol;
+      uint2 w;
+      w.x = pack2bf(acc[i][j][0], acc[i][j][1]);
+      w.y = pack2bf(acc[i][j][2], acc[i][j][3]);
+      *reinterpret_cast<uint2*>(smem + r * C_STRIDE + c * 2) = w;
+    }
+  }
+  __syncthreads();
+  constexpr int CPR = BN / 8;  // 16-B chunks per row
+#pragma unroll
+  for (int it = 0; it < (BM * CPR) / NT; ++it) {
+    int q = tid + it * NT;
+    int r = q / CPR, cc = q % CPR;
+    int m = m0 + r;
+    int col = n0 + cc * 8;
+    if (m < p.M && col < p.Ncol) {
+      u32x4 v = *reinterpret_cast<const u32x4*>(smem + r * C_STRIDE + cc * 16);
+      uint32_t img = fdiv(m, p.div_HWm);
+      uint32_t rem = m - img * (uint32_t)(p.Hm * p.Wm);
+      uint32_t oh = fdiv(rem, p.div_Wm);
+      uint32_t ow = rem - oh * p.Wm;
+      size_t orow = ((size_t)img * p.Ho + oh * p.osh + p.oph) * p.Wo + ow * p.osw + p.opw;
+      *reinterpret_cast<u32x4*>(p.out + orow * p.ldo + col) = v;
+    }
+  }
+}
+
+template <int BM, int BN, bool CS64>
+int launch(const NTParams& p, hipStream_t st) {
+  int ntm = (p.M + BM - 1) / BM, ntn = (p.Ncol + BN - 1) / BN;
+  hipLaunchKernelGGL((conv_nt_kernel<BM, BN, CS64>), dim3(ntm * ntn), dim3(NT), 0, st, p);
+  PDT_RETURN_LAUNCH();
+}
+
+}  // namespace
+
+// Returns the number of BN-statistics partial rows the launch will write for
+// a given M / Ncol (needed to size the stats buffer).
+PDT_API int pdt_conv_nt_stat_rows(int M, int Ncol) {
+  int BM = (Ncol <= 64) ? 256 : 128;
+  return ((M + BM - 1) / BM) * 2;
+}
+
+// Generic launch: see header comment for the meaning of every argument.
+PDT_API int pdt_conv_nt(const void* src, const void* b, void* out, float* stats, const float* bias,
+                        int Hs, int Ws, int Cs, int Nimg, int Hm, int Wm, int Ncol, int K, int ldb,
+                        int sh, int sw, int oh0, int ow0, int dh, int dw, int nth, int ntw,
+                        int Ho, int Wo, int osh, int osw, int oph, int opw, int ldo, int relu,
+                        hipStream_t stream) {
+  if (Cs % 8 != 0 || K % 8 != 0 || Ncol % 8 != 0 || ldo % 8 != 0 || ldb % 8 != 0) return -1;
+  if (K != nth * ntw * Cs) return -2;
+  NTParams p;
+  p.src = (const u16*)src;
+  p.b = (const u16*)b;
+  p.out = (u16*)out;
+  p.stats = stats;
+  p.bias = bias;
+  p.Hs = Hs; p.Ws = Ws; p.Cs = Cs;
+  p.Hm = Hm; p.Wm = Wm;
+  p.M = Nimg * Hm * Wm;
+  p.Ncol = Ncol; p.K = K; p.ldb = ldb;
+  p.sh = sh; p.sw = sw; p.oh0 = oh0; p.ow0 = ow0; p.dh = dh; p.dw = dw; p.nth = nth; p.ntw = ntw;
+  p.Ho = Ho; p.Wo = Wo; p.osh = osh; p.osw = osw; p.oph = oph; p.opw = opw; p.ldo = ldo;
+  p.relu = relu;
+  p.div_Wm = make_fastdiv(Wm);
+  p.div_HWm = make_fastdiv(Hm * Wm);
+  p.div_Cs8 = make_fastdiv(Cs / 8);
+  p.div_ntw = make_fastdiv(ntw > 0 ? ntw : 1);
+  p.nstat_rows = pdt_conv_nt_stat_rows(p.M, Ncol);
+  const bool cs64 = (Cs % 64) == 0;
+  if (Ncol <= 64) {
+    return cs64 ? launch<256, 64, true>(p, stream) : launch<256, 64, false>(p, stream);
+  }
+  return cs64 ? launch<128, 128, true>(p, stream) : launch<128, 128, false>(p, stream);
+}

@@ -1,0 +1,276 @@
+// Weight-gradient implicit GEMM for NHWC bf16 convolutions (and plain "TN"
+// GEMMs such as nn.Linear's dW) on MI355X MFMA, split over the pixel (K)
+// dimension.
+//
+//   dW[co, tap*C + c] = sum_m dY[m, co] * X[n, oh*sh + oh0 + dh*th, ow*sw + ow0 + dw*tw, c]
+//
+// Both operands arrive "K-outer" (pixel rows, channels contiguous), so tiles
+// are staged into LDS exactly as they come from HBM -- [64 pixel rows][BM|BN
+// channels] -- and MFMA fragments are read with the CDNA4 hardware-transpose
+// LDS read (ds_read_b64_tr_b16): per 16-lane group a 4-row x 16-column block
+// is delivered column-major, i.e. four consecutive k of one channel per lane;
+// two such reads give the 8-element bf16 fragment of mfma_f32_16x16x32_bf16.
+// 32-byte segments of each LDS row are XOR-swizzled by a function of the row
+// so the eight rows a 32-lane half touches fall on distinct banks.
+//
+// Each workgroup computes a BM x 128 tile over a contiguous slice of the
+// pixels and writes an fp32 partial slab; pdt_wgrad_reduce sums the slabs in
+// a fixed order (bitwise deterministic, no atomics) and writes / accumulates
+// the fp32 gradient.
+#include "pdt_common.h"
+
+namespace {
+
+struct WGParams {
+  const u16* dy;     // [M][ldy] (co contiguous)
+  const u16* x;      // NHWC source [N][Hs][Ws][C]
+  float* slab;       // [splits][Mo][No]
+  int M;             // pixels (K of the GEMM)
+  int Mo, No;        // Mo = Cout, No = ntaps*C
+  int ldy;
+  int Hs, Ws, C;
+  int Hm, Wm;        // output grid of the forward conv
+  int sh, sw, oh0, ow0, dh, dw, ntw;
+  int ktiles_per_split, splits;
+  FastDiv div_Wm, div_HWm, div_C, div_ntw;
+};
+
+constexpr int BK = 64;
+constexpr int NT = 256;
+constexpr int BN = 128;
+
+template <int RB>
+__device__ __forceinline__ int seg_swz(int row) {
+  if (RB == 256) return (row & 3) | ((row >> 1) & 4);
+  return ((row >> 1) & 1) | ((row >> 2) & 2);  // RB == 128
+}
+
+template <int RB>
+__device__ __forceinline__ int lds_off(int row, int byte_in_row) {
+  int seg = byte_in_row >> 5;
+  return row * RB + ((seg ^ seg_swz<RB>(row)) << 5) + (byte_in_row & 31);
+}
+
+template <int RB>
+__device__ __forceinline__ bf16x8 tr_frag(const char* base, int krow0, int col0, int lane) {
+  // lane = 16*g + 4*q + p :  rows krow0 + 8g + q (+4), columns col0 + 4p .. +3
+  const int g = lane >> 4, q = (lane >> 2) & 3, pp = lane & 3;
+  const int r1 = krow0 + 8 * g + q;
+  const int cb = (col0 + 4 * pp) * 2;
+  typedef __bf16 __attribute__((address_space(3))) * lptr;
+  const char* a1 = base + lds_off<RB>(r1, cb);
+  const char* a2 = base + lds_off<RB>(r1 + 4, cb);
+  bf16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((bf16x4 __attribute__((address_space(3)))*)(
+      (__attribute__((address_space(3))) char*)(uintptr_t)(uint32_t)(uintptr_t)a1));
+  bf16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((bf16x4 __attribute__((address_space(3)))*)(
+      (__attribute__((address_space(3))) char*)(uintptr_t)(uint32_t)(uintptr_t)a2));
+  (void)sizeof(lptr);
+  bf16x8 r;
+  r[0] = lo[0]; r[1] = lo[1]; r[2] = lo[2]; r[3] = lo[3];
+  r[4] = hi[0]; r[5] = hi[1]; r[6] = hi[2]; r[7] = hi[3];
+  return r;
+}
+
+template <int BM>
+__global__ void __launch_bounds__(NT, 2) wgrad_kernel(WGParams p) {
+  constexpr int RBA = BM * 2;   // bytes per A row (co)
+  constexpr int RBB = BN * 2;   // bytes per B row (tap,c)
+  constexpr int A_BYTES = BK * RBA;
+  constexpr int B_BYTES = BK * RBB;
+  constexpr int STAGE = A_BYTES + B_BYTES;
+  constexpr int ACH = BM / 8;          // 16-B chunks per A row
+  constexpr int AROWS = NT / ACH;      // rows covered per pass
+  constexpr int NA = BK / AROWS;       // A chunks per thread
+  constexpr int BCH = BN / 8;
+  constexpr int BROWS = NT / BCH;
+  constexpr int NB = BK / BROWS;
+  constexpr int MI = BM / 32;          // co 16-tiles per wave
+  constexpr int NI = BN / 32;          // tc 16-tiles per wave
+  __shared__ __attribute__((aligned(16))) char smem[2 * STAGE];
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave >> 1, wn = wave & 1;
+
+  const int ntm = (p.Mo + BM - 1) / BM, ntn = (p.No + BN - 1) / BN;
+  const int ntiles = ntm * ntn;
+  const int bid = blockIdx.x;
+  const int tile = bid % ntiles;  // consecutive blocks: same split, different tiles
+  const int split = bid / ntiles;
+  const int tm = tile / ntn, tn = tile % ntn;
+  const int co0 = tm * BM, tc0 = tn * BN;
+
+  const int nk_total = (p.M + BK - 1) / BK;
+  const int kt_begin = split * p.ktiles_per_split;
+  const int kt_end = min(nk_total, kt_begin + p.ktiles_per_split);
+
+  // A (dY) chunk of this thread: column chunk cA, rows rA0 + AROWS*i
+  const int cA = tid % ACH, rA0 = tid / ACH;
+  const int coA = co0 + cA * 8;
+  const bool okA = coA < p.Mo;
+  // B (X gather) chunk: fixed column -> fixed (tap, c)
+  const int cB = tid % BCH, rB0 = tid / BCH;
+  const int colB = tc0 + cB * 8;
+  const bool okB = colB < p.No;
+  int tap = fdiv(okB ? colB : 0, p.div_C);
+  const int cB_ch = (okB ? colB : 0) - tap * p.C;
+  const int th = fdiv(tap, p.div_ntw), tw = tap - th * p.ntw;
+  const int offh = p.oh0 + p.dh * th, offw = p.ow0 + p.dw * tw;
+
+  u32x4 ra[NA], rb[NB];
+
+  auto load_tile = [&](int kt) {
+    const int k0 = kt * BK;
+#pragma unroll
+    for (int i = 0; i < NA; ++i) {
+      int m = k0 + rA0 + AROWS * i;
+      if (okA && m < p.M)
+        ra[i] = *reinterpret_cast<const u32x4*>(p.dy + (size_t)m * p.ldy + coA);
+      else
+        ra[i] = u32x4{0, 0, 0, 0};
+    }
+#pragma unroll
+    for (int i = 0; i < NB; ++i) {
+      int m = k0 + rB0 + BROWS * i;
+      bool ok = okB && m < p.M;
+      uint32_t mm = ok ? m : 0;
+      uint32_t img = fdiv(mm, p.div_HWm);
+      uint32_t rem = mm - img * (uint32_t)(p.Hm * p.Wm);
+      uint32_t oh = fdiv(rem, p.div_Wm);
+      uint32_t ow = rem - oh * p.Wm;
+      int ih = (int)(oh * p.sh) + offh, iw = (int)(ow * p.sw) + offw;
+      ok = ok && (unsigned)ih < (unsigned)p.Hs && (unsigned)iw < (unsigned)p.Ws;
+      if (ok)
+        rb[i] = *reinterpret_cast<const u32x4*>(p.x + ((size_t)(img * p.Hs + ih) * p.Ws + iw) * p.C + cB_ch);
+      else
+        rb[i] = u32x4{0, 0, 0, 0};
+    }
+  };
+  auto store_tile = [&](int buf) {
+    char* sa = smem + buf * STAGE;
+    char* sb = sa + A_BYTES;
+#pragma unroll
+    for (int i = 0; i < NA; ++i)
+      *reinterpret_cast<u32x4*>(sa + lds_off<RBA>(rA0 + AROWS * i, cA * 16)) = ra[i];
+#pragma unroll
+    for (int i = 0; i < NB; ++i)
+      *reinterpret_cast<u32x4*>(sb + lds_off<RBB>(rB0 + BROWS * i, cB * 16)) = rb[i];
+  };
+
+  f32x4 acc[MI][NI];
+#pragma unroll
+  for (int i = 0; i < MI; ++i)
+#pragma unroll
+    for (int j = 0; j < NI; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  if (kt_begin < kt_end) {
+    load_tile(kt_begin);
+    store_tile(0);
+  }
+  __syncthreads();
+  for (int kt = kt_begin; kt < kt_end; ++kt) {
+    const int cur = (kt - kt_begin) & 1;
+    if (kt + 1 < kt_end) load_tile(kt + 1);
+    const char* sa = smem + cur * STAGE;
+    const char* sb = sa + A_BYTES;
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      bf16x8 af[MI], bfr[NI];
+#pragma unroll
+      for (int i = 0; i < MI; ++i) af[i] = tr_frag<RBA>(sa, kk * 32, wm * (BM / 2) + i * 16, lane);
+#pragma unroll
+      for (int j = 0; j < NI; ++j) bfr[j] = tr_frag<RBB>(sb, kk * 32, wn * (BN / 2) + j * 16, lane);
+#pragma unroll
+      for (int i = 0; i < MI; ++i)
+#pragma unroll
+        for (int j = 0; j < NI; ++j)
+          // D[tc][co]: lane holds 4 consecutive tc of one co
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[j], af[i], acc[i][j], 0, 0, 0);
+    }
+    if (kt + 1 < kt_end) store_tile(cur ^ 1);
+    __syncthreads();
+  }
+
+  float* out = p.slab + (size_t)split * p.Mo * p.No;
+#pragma unroll
+  for (int i = 0; i < MI; ++i) {
+    int co = co0 + wm * (BM / 2) + i * 16 + (lane & 15);
+#pragma unroll
+    for (int j = 0; j < NI; ++j) {
+      int tc = tc0 + wn * (BN / 2) + j * 16 + (lane >> 4) * 4;
+      if (co < p.Mo && tc < p.No) {
+        *reinterpret_cast<f32x4*>(out + (size_t)co * p.No + tc) = acc[i][j];
+      }
+    }
+  }
+}
+
+// out[i] = (accumulate ? out[i] : 0) + scale * sum_s slab[s][i]
+__global__ void wgrad_reduce_kernel(const float* __restrict__ slab, float* __restrict__ out, long n4,
+                                    int splits, long stride4, float scale, int accumulate) {
+  long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  for (; i < n4; i += (long)gridDim.x * blockDim.x) {
+    const f32x4* s = reinterpret_cast<const f32x4*>(slab) + i;
+    f32x4 a = s[0];
+    for (int k = 1; k < splits; ++k) a += s[(long)k * stride4];
+    a *= scale;
+    f32x4* o = reinterpret_cast<f32x4*>(out) + i;
+    if (accumulate) a += *o;
+    *o = a;
+  }
+}
+
+}  // namespace
+
+// Plan: number of splits for a given problem so the grid covers the chip
+// (~4 workgroups per CU); returns splits and writes ktiles_per_split.
+PDT_API int pdt_wgrad_plan(int M, int Mo, int No, int* ktiles_per_split) {
+  int BM = Mo <= 64 ? 64 : 128;
+  int tiles = ((Mo + BM - 1) / BM) * ((No + BN - 1) / BN);
+  int nk = (M + BK - 1) / BK;
+  int target = 1024;
+  int splits = (target + tiles - 1) / tiles;
+  if (splits > nk) splits = nk;
+  if (splits < 1) splits = 1;
+  // at least 8 k-tiles per split so the pipeline amortises
+  while (splits > 1 && (nk + splits - 1) / splits < 8) --splits;
+  int kps = (nk + splits - 1) / splits;
+  splits = (nk + kps - 1) / kps;
+  *ktiles_per_split = kps;
+  return splits;
+}
+
+PDT_API int pdt_conv_wgrad(const void* dy, const void* x, float* slab, float* out, int M, int Mo, int No,
+                           int ldy, int Hs, int Ws, int C, int Hm, int Wm, int sh, int sw, int oh0, int ow0,
+                           int dh, int dw, int ntw, int splits, int ktiles_per_split, float scale,
+                           int accumulate, hipStream_t stream) {
+  if (C % 8 != 0 || Mo % 8 != 0 || No % 8 != 0 || ldy % 8 != 0) return -1;
+  WGParams p;
+  p.dy = (const u16*)dy;
+  p.x = (const u16*)x;
+  p.slab = slab;
+  p.M = M; p.Mo = Mo; p.No = No; p.ldy = ldy;
+  p.Hs = Hs; p.Ws = Ws; p.C = C; p.Hm = Hm; p.Wm = Wm;
+  p.sh = sh; p.sw = sw; p.oh0 = oh0; p.ow0 = ow0; p.dh = dh; p.dw = dw; p.ntw = ntw;
+  p.ktiles_per_split = ktiles_per_split; p.splits = splits;
+  p.div_Wm = make_fastdiv(Wm);
+  p.div_HWm = make_fastdiv(Hm * Wm);
+  p.div_C = make_fastdiv(C);
+  p.div_ntw = make_fastdiv(ntw);
+  int BM = Mo <= 64 ? 64 : 128;
+  int tiles = ((Mo + BM - 1) / BM) * ((No + BN - 1) / BN);
+  dim3 grid(tiles * splits);
+  if (BM == 64)
+    hipLaunchKernelGGL(wgrad_kernel<64>, grid, dim3(NT), 0, stream, p);
+  else
+    hipLaunchKernelGGL(wgrad_kernel<128>, grid, dim3(NT), 0, stream, p);
+  int e = (int)hipGetLastError();
+  if (e) return e;
+  long n = (long)Mo * No;
+  long n4 = n / 4;
+  int blocks = (int)((n4 + 255) / 256);
+  if (blocks > 2048) blocks = 2048;
+  if (blocks < 1) blocks = 1;
+  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(blocks), dim3(256), 0, stream, slab, out, n4, splits, n4, scale,
+                     accumulate);
+  PDT_RETURN_LAUNCH();
+}

@@ -1,0 +1,79 @@
+// Common definitions for the MI355X (gfx950 / CDNA4) kernel library.
+//
+// All kernels are plain HIP C++ written for wave64 + MFMA; the library exposes
+// a C ABI (PDT_API) that the Python layer calls through ctypes with raw device
+// pointers and the current HIP stream (no torch headers, no hipify).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+typedef unsigned short u16;
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+#define PDT_API extern "C" __attribute__((visibility("default")))
+#define LDS_PTR(T) T __attribute__((address_space(3)))*
+
+__device__ __forceinline__ float bf2f(u16 v) { return __uint_as_float(((uint32_t)v) << 16); }
+
+__device__ __forceinline__ u16 f2bf(float f) {
+  __bf16 b = (__bf16)f;  // v_cvt_pk_bf16_f32 (RNE, NaN-preserving) on gfx950
+  return __builtin_bit_cast(u16, b);
+}
+
+__device__ __forceinline__ uint32_t pack2bf(float lo, float hi) {
+  return (uint32_t)f2bf(lo) | ((uint32_t)f2bf(hi) << 16);
+}
+
+// low / high bf16 of a packed 32-bit word
+__device__ __forceinline__ float lo_bf(uint32_t w) { return __uint_as_float(w << 16); }
+__device__ __forceinline__ float hi_bf(uint32_t w) { return __uint_as_float(w & 0xffff0000u); }
+
+__device__ __forceinline__ float warp_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+__device__ __forceinline__ float warp_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+// Fast unsigned division by a runtime-constant divisor (Granlund-Montgomery).
+struct FastDiv {
+  uint32_t d, m, s;
+};
+
+static inline FastDiv make_fastdiv(uint32_t d) {
+  FastDiv f;
+  f.d = d;
+  if (d == 1) { f.m = 0; f.s = 0; return f; }
+  uint32_t s = 0;
+  while ((1ull << s) < d) ++s;
+  f.s = s;
+  f.m = (uint32_t)((((1ull << 32) * ((1ull << s) - d)) / d) + 1);
+  return f;
+}
+
+__device__ __forceinline__ uint32_t fdiv(uint32_t n, const FastDiv& f) {
+  if (f.d == 1) return n;
+  uint32_t t = __umulhi(n, f.m);
+  return (t + ((n - t) >> 1)) >> (f.s - 1);
+}
+
+// Bijective XCD-aware remap of a 1-D block id: consecutive *logical* ids land
+// on the same XCD (blocks b, b+8, b+16.. share one XCD under round-robin
+// dispatch), so tiles that share an operand panel share that XCD's L2.
+// Speed only -- never relied on for correctness.
+__device__ __forceinline__ uint32_t xcd_remap(uint32_t bid, uint32_t nwg) {
+  const uint32_t NX = 8;
+  if (nwg < NX) return bid;
+  uint32_t q = nwg / NX, r = nwg % NX, x = bid % NX, k = bid / NX;
+  return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + k;
+}
+
+#define PDT_RETURN_LAUNCH() return (int)hipGetLastError()

@@ -1,0 +1,167 @@
+// Pooling for NHWC bf16: max-pool (k x k, stride s, pad p) with a saved uint8
+// argmax, gather-form backward (no atomics), and global average pool.
+// Reference op: F.max_pool2d in the LeNet (/root/reference/model/model.py:16-17);
+// ResNet stem max-pool 3x3 s2 p1 and the final global average pool.
+#include "pdt_common.h"
+
+namespace {
+constexpr int NT = 256;
+
+__device__ __forceinline__ void unpack8(const u32x4& v, float* f) {
+  f[0] = lo_bf(v[0]); f[1] = hi_bf(v[0]); f[2] = lo_bf(v[1]); f[3] = hi_bf(v[1]);
+  f[4] = lo_bf(v[2]); f[5] = hi_bf(v[2]); f[6] = lo_bf(v[3]); f[7] = hi_bf(v[3]);
+}
+__device__ __forceinline__ u32x4 pack8(const float* f) {
+  return u32x4{pack2bf(f[0], f[1]), pack2bf(f[2], f[3]), pack2bf(f[4], f[5]), pack2bf(f[6], f[7])};
+}
+
+// one thread = 8 channels of one output pixel
+__global__ void maxpool_fwd_kernel(const u16* __restrict__ x, u16* __restrict__ y, uint8_t* __restrict__ idx,
+                                   int N, int H, int W, int C, int Ho, int Wo, int k, int s, int p) {
+  const int cpr = C / 8;
+  long total = (long)N * Ho * Wo * cpr;
+  for (long t = (long)blockIdx.x * NT + threadIdx.x; t < total; t += (long)gridDim.x * NT) {
+    int cc = t % cpr;
+    long pix = t / cpr;
+    int ow = pix % Wo;
+    long r = pix / Wo;
+    int oh = r % Ho;
+    int n = r / Ho;
+    float best[8];
+    uint8_t bi[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) { best[j] = -INFINITY; bi[j] = 0; }
+    for (int kh = 0; kh < k; ++kh) {
+      int ih = oh * s - p + kh;
+      if ((unsigned)ih >= (unsigned)H) continue;
+      for (int kw = 0; kw < k; ++kw) {
+        int iw = ow * s - p + kw;
+        if ((unsigned)iw >= (unsigned)W) continue;
+        float f[8];
+        unpack8(*reinterpret_cast<const u32x4*>(x + (((long)n * H + ih) * W + iw) * C + cc * 8), f);
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+          if (f[j] > best[j] || (f[j] != f[j])) { best[j] = f[j]; bi[j] = (uint8_t)(kh * k + kw); }
+      }
+    }
+    reinterpret_cast<u32x4*>(y)[t] = pack8(best);
+    uint2 packed;
+    packed.x = bi[0] | (bi[1] << 8) | (bi[2] << 16) | ((uint32_t)bi[3] << 24);
+    packed.y = bi[4] | (bi[5] << 8) | (bi[6] << 16) | ((uint32_t)bi[7] << 24);
+    reinterpret_cast<uint2*>(idx)[t] = packed;
+  }
+}
+
+// gather: each input pixel sums the gradients of the windows whose argmax it is
+__global__ void maxpool_bwd_kernel(const u16* __restrict__ dy, const uint8_t* __restrict__ idx, u16* __restrict__ dx,
+                                   int N, int H, int W, int C, int Ho, int Wo, int k, int s, int p) {
+  const int cpr = C / 8;
+  long total = (long)N * H * W * cpr;
+  for (long t = (long)blockIdx.x * NT + threadIdx.x; t < total; t += (long)gridDim.x * NT) {
+    int cc = t % cpr;
+    long pix = t / cpr;
+    int w = pix % W;
+    long r = pix / W;
+    int h = r % H;
+    int n = r / H;
+    float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    int oh_lo = (h + p - k + s) / s; if (h + p - k + 1 < 0) oh_lo = 0;
+    int oh_hi = (h + p) / s;
+    int ow_lo = (w + p - k + s) / s; if (w + p - k + 1 < 0) ow_lo = 0;
+    int ow_hi = (w + p) / s;
+    for (int oh = max(oh_lo, 0); oh <= min(oh_hi, Ho - 1); ++oh) {
+      int kh = h + p - oh * s;
+      if (kh < 0 || kh >= k) continue;
+      for (int ow = max(ow_lo, 0); ow <= min(ow_hi, Wo - 1); ++ow) {
+        int kw = w + p - ow * s;
+        if (kw < 0 || kw >= k) continue;
+        long o = ((((long)n * Ho + oh) * Wo + ow) * cpr + cc);
+        uint2 bi = reinterpret_cast<const uint2*>(idx)[o];
+        float g[8];
+        unpack8(reinterpret_cast<const u32x4*>(dy)[o], g);
+        const uint8_t me = (uint8_t)(kh * k + kw);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          uint32_t word = j < 4 ? bi.x : bi.y;
+          uint8_t b = (word >> (8 * (j & 3))) & 0xff;
+          if (b == me) acc[j] += g[j];
+        }
+      }
+    }
+    reinterpret_cast<u32x4*>(dx)[t] = pack8(acc);
+  }
+}
+
+// x [N][HW][C] -> y [N][C]  (bf16 out, fp32 sum)
+__global__ void avgpool_fwd_kernel(const u16* __restrict__ x, u16* __restrict__ y, int N, int HW, int C) {
+  const int cpr = C / 8;
+  int t = blockIdx.x * NT + threadIdx.x;
+  if (t >= N * cpr) return;
+  int n = t / cpr, cc = t % cpr;
+  float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  for (int i = 0; i < HW; ++i) {
+    float f[8];
+    unpack8(*reinterpret_cast<const u32x4*>(x + ((long)n * HW + i) * C + cc * 8), f);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[j] += f[j];
+  }
+  const float inv = 1.f / HW;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) acc[j] *= inv;
+  reinterpret_cast<u32x4*>(y)[t] = pack8(acc);
+}
+
+__global__ void avgpool_bwd_kernel(const u16* __restrict__ dy, u16* __restrict__ dx, int N, int HW, int C) {
+  const int cpr = C / 8;
+  long total = (long)N * HW * cpr;
+  const float inv = 1.f / HW;
+  for (long t = (long)blockIdx.x * NT + threadIdx.x; t < total; t += (long)gridDim.x * NT) {
+    int cc = t % cpr;
+    long n = t / ((long)HW * cpr);
+    float g[8];
+    unpack8(reinterpret_cast<const u32x4*>(dy)[n * cpr + cc], g);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) g[j] *= inv;
+    reinterpret_cast<u32x4*>(dx)[t] = pack8(g);
+  }
+}
+
+int grid_for(long n) {
+  long b = (n + NT - 1) / NT;
+  return (int)(b > 8192 ? 8192 : (b < 1 ? 1 : b));
+}
+}  // namespace
+
+PDT_API int pdt_maxpool_fwd(const void* x, void* y, void* idx, int N, int H, int W, int C, int Ho, int Wo, int k,
+                            int s, int p, hipStream_t st) {
+  if (C % 8 || k * k > 255) return -1;
+  long total = (long)N * Ho * Wo * (C / 8);
+  hipLaunchKernelGGL(maxpool_fwd_kernel, dim3(grid_for(total)), dim3(NT), 0, st, (const u16*)x, (u16*)y,
+                     (uint8_t*)idx, N, H, W, C, Ho, Wo, k, s, p);
+  PDT_RETURN_LAUNCH();
+}
+
+PDT_API int pdt_maxpool_bwd(const void* dy, const void* idx, void* dx, int N, int H, int W, int C, int Ho, int Wo,
+                            int k, int s, int p, hipStream_t st) {
+  if (C % 8) return -1;
+  long total = (long)N * H * W * (C / 8);
+  hipLaunchKernelGGL(maxpool_bwd_kernel, dim3(grid_for(total)), dim3(NT), 0, st, (const u16*)dy,
+                     (const uint8_t*)idx, (u16*)dx, N, H, W, C, Ho, Wo, k, s, p);
+  PDT_RETURN_LAUNCH();
+}
+
+PDT_API int pdt_avgpool_fwd(const void* x, void* y, int N, int HW, int C, hipStream_t st) {
+  if (C % 8) return -1;
+  int total = N * (C / 8);
+  hipLaunchKernelGGL(avgpool_fwd_kernel, dim3((total + NT - 1) / NT), dim3(NT), 0, st, (const u16*)x, (u16*)y, N,
+                     HW, C);
+  PDT_RETURN_LAUNCH();
+}
+
+PDT_API int pdt_avgpool_bwd(const void* dy, void* dx, int N, int HW, int C, hipStream_t st) {
+  if (C % 8) return -1;
+  long total = (long)N * HW * (C / 8);
+  hipLaunchKernelGGL(avgpool_bwd_kernel, dim3(grid_for(total)), dim3(NT), 0, st, (const u16*)dy, (u16*)dx, N, HW,
+                     C);
+  PDT_RETURN_LAUNCH();
+}

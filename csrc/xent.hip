@@ -1,0 +1,123 @@
+// Fused softmax cross-entropy (mean reduction, optional label smoothing),
+// plus a column-sum kernel (bias gradients of nn.Linear).
+// Reference op: log_softmax + nll_loss (/root/reference/model/model.py:22,
+// /root/reference/model/loss.py:5) -- here a single online-softmax pass per row.
+//
+// forward : one wave per row: running max / sum-exp over V (16-B bf16 loads),
+//           lse[row], loss[row] = lse - (1-eps)*x[t] - eps*mean(x)
+//           then a one-block deterministic mean over rows.
+// backward: dlogits = g/B * (softmax - (1-eps)*onehot - eps/V), bf16 out.
+#include "pdt_common.h"
+
+namespace {
+
+__device__ __forceinline__ float ldx(const u16* p, long i) { return bf2f(p[i]); }
+
+template <bool BF16>
+__device__ __forceinline__ float ldv(const void* p, long i) {
+  if (BF16) return bf2f(reinterpret_cast<const u16*>(p)[i]);
+  return reinterpret_cast<const float*>(p)[i];
+}
+
+template <bool BF16>
+__global__ void xent_fwd_kernel(const void* __restrict__ logits, const long* __restrict__ target,
+                                float* __restrict__ lse, float* __restrict__ loss, int B, int V, float eps) {
+  const int lane = threadIdx.x & 63;
+  const int row = blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6);
+  if (row >= B) return;
+  const long base = (long)row * V;
+  float m = -INFINITY, s = 0.f, sx = 0.f;
+  for (int j = lane; j < V; j += 64) {
+    float v = ldv<BF16>(logits, base + j);
+    sx += v;
+    if (v > m) {
+      s = s * __expf(m - v) + 1.f;
+      m = v;
+    } else {
+      s += __expf(v - m);
+    }
+  }
+  // combine (m, s) across lanes
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    float m2 = __shfl_xor(m, o, 64), s2 = __shfl_xor(s, o, 64);
+    float mm = fmaxf(m, m2);
+    s = (m == -INFINITY ? 0.f : s * __expf(m - mm)) + (m2 == -INFINITY ? 0.f : s2 * __expf(m2 - mm));
+    m = mm;
+  }
+  sx = warp_sum(sx);
+  if (lane == 0) {
+    float l = m + __logf(s);
+    lse[row] = l;
+    long t = target[row];
+    float xt = (t >= 0 && t < V) ? ldv<BF16>(logits, base + t) : 0.f;
+    loss[row] = (t >= 0 && t < V) ? (l - (1.f - eps) * xt - eps * (sx / V)) : 0.f;
+  }
+}
+
+__global__ void mean_kernel(const float* __restrict__ x, float* __restrict__ out, int n, float scale) {
+  __shared__ float red[256];
+  float a = 0.f;
+  for (int i = threadIdx.x; i < n; i += 256) a += x[i];
+  red[threadIdx.x] = a;
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if ((int)threadIdx.x < o) red[threadIdx.x] += red[threadIdx.x + o];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) out[0] = red[0] * scale;
+}
+
+template <bool BF16>
+__global__ void xent_bwd_kernel(const void* __restrict__ logits, const long* __restrict__ target,
+                                const float* __restrict__ lse, const float* __restrict__ gout, u16* __restrict__ dlogits,
+                                int B, int V, float eps) {
+  const int row = blockIdx.y;
+  const float g = gout[0] / B;
+  const float l = lse[row];
+  const long t = target[row];
+  const long base = (long)row * V;
+  for (int j = blockIdx.x * blockDim.x + threadIdx.x; j < V; j += gridDim.x * blockDim.x) {
+    float p = __expf(ldv<BF16>(logits, base + j) - l);
+    float d = p - eps / V - (j == t ? (1.f - eps) : 0.f);
+    dlogits[base + j] = f2bf(t >= 0 && t < V ? g * d : 0.f);
+  }
+}
+
+// out[c] = (acc ? out[c] : 0) + sum_r x[r][c]   (bf16 x, fp32 out)
+__global__ void colsum_kernel(const u16* __restrict__ x, float* __restrict__ out, int R, int C, int acc) {
+  int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  float s = 0.f;
+  for (int r = 0; r < R; ++r) s += bf2f(x[(long)r * C + c]);
+  out[c] = acc ? out[c] + s : s;
+}
+
+}  // namespace
+
+PDT_API int pdt_xent_fwd(const void* logits, int bf16, const long* target, float* lse, float* loss_rows,
+                         float* loss_out, int B, int V, float eps, hipStream_t st) {
+  dim3 blk(256), grd((B + 3) / 4);
+  if (bf16)
+    hipLaunchKernelGGL(xent_fwd_kernel<true>, grd, blk, 0, st, logits, target, lse, loss_rows, B, V, eps);
+  else
+    hipLaunchKernelGGL(xent_fwd_kernel<false>, grd, blk, 0, st, logits, target, lse, loss_rows, B, V, eps);
+  hipLaunchKernelGGL(mean_kernel, dim3(1), dim3(256), 0, st, loss_rows, loss_out, B, 1.f / B);
+  PDT_RETURN_LAUNCH();
+}
+
+PDT_API int pdt_xent_bwd(const void* logits, int bf16, const long* target, const float* lse, const float* gout,
+                         void* dlogits, int B, int V, float eps, hipStream_t st) {
+  dim3 blk(256), grd((V + 255) / 256, B);
+  if (bf16)
+    hipLaunchKernelGGL(xent_bwd_kernel<true>, grd, blk, 0, st, logits, target, lse, gout, (u16*)dlogits, B, V, eps);
+  else
+    hipLaunchKernelGGL(xent_bwd_kernel<false>, grd, blk, 0, st, logits, target, lse, gout, (u16*)dlogits, B, V,
+                       eps);
+  PDT_RETURN_LAUNCH();
+}
+
+PDT_API int pdt_colsum(const void* x, float* out, int R, int C, int acc, hipStream_t st) {
+  hipLaunchKernelGGL(colsum_kernel, dim3((C + 255) / 256), dim3(256), 0, st, (const u16*)x, out, R, C, acc);
+  PDT_RETURN_LAUNCH();
+}

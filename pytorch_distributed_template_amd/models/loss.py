@@ -1,0 +1,21 @@
+"""Loss registry (``"loss"`` key in config). Reference: ``/root/reference/model/loss.py:4-5``.
+
+``cross_entropy`` routes to the fused softmax-cross-entropy HIP kernel
+(``csrc/softmax_xent.hip``) for GPU tensors; ``nll_loss`` matches the
+reference (model emits log-probabilities).
+"""
+import torch.nn.functional as F
+
+from ..ops import fused
+
+
+def nll_loss(output, target):
+    return F.nll_loss(output, target)
+
+
+def cross_entropy(output, target):
+    return fused.softmax_cross_entropy(output, target)
+
+
+def label_smoothing_cross_entropy(output, target, smoothing=0.1):
+    return fused.softmax_cross_entropy(output, target, label_smoothing=smoothing)

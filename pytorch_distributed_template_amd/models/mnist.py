@@ -1,0 +1,28 @@
+"""LeNet-style MNIST demo model (reference: ``/root/reference/model/model.py:6-22``).
+
+Same layers and parameter names (conv1 1->10 k5, conv2 10->20 k5, channel
+dropout, fc1 320->50, fc2 50->classes, log-softmax output; 21,840 params),
+so state_dicts line up with the reference's ``MnistModel``.
+"""
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from ..base.base_model import BaseModel
+
+
+class MnistModel(BaseModel):
+    def __init__(self, num_classes: int = 10):
+        super().__init__()
+        self.conv1 = nn.Conv2d(1, 10, kernel_size=5)
+        self.conv2 = nn.Conv2d(10, 20, kernel_size=5)
+        self.conv2_drop = nn.Dropout2d()
+        self.fc1 = nn.Linear(20 * 4 * 4, 50)
+        self.fc2 = nn.Linear(50, num_classes)
+
+    def forward(self, x):
+        h = F.max_pool2d(self.conv1(x), 2).relu()
+        h = F.max_pool2d(self.conv2_drop(self.conv2(h)), 2).relu()
+        h = torch.flatten(h, 1)
+        h = F.dropout(self.fc1(h).relu(), training=self.training)
+        return F.log_softmax(self.fc2(h), dim=1)

@@ -1,0 +1,104 @@
+"""ViT-B/16 (image 224, patch 16, d=768, 12 heads, MLP 3072, depth 12).
+
+Not present in the reference; BASELINE.json config #5 ("ViT-B/16 fp8
+synthetic 3x224x224") defines it. Shapes per SURVEY §2.6(b).
+
+The model is written against ``ops.fused`` entry points so the native HIP
+path (LayerNorm, bias+GELU epilogue, fused attention, and fp8 GEMMs with
+per-tensor amax scaling when ``fp8=True``) and the torch reference path share
+one module tree. Parameter names follow the common ``patch_embed / cls_token /
+pos_embed / blocks.N.{norm1,attn.qkv,attn.proj,norm2,mlp.fc1,mlp.fc2} / norm /
+head`` scheme.
+"""
+from __future__ import annotations
+
+import math
+
+import torch
+import torch.nn as nn
+
+from ..base.base_model import BaseModel
+from ..ops import fused
+
+
+class Attention(nn.Module):
+    def __init__(self, dim, num_heads):
+        super().__init__()
+        self.num_heads = num_heads
+        self.head_dim = dim // num_heads
+        self.qkv = nn.Linear(dim, dim * 3)
+        self.proj = nn.Linear(dim, dim)
+
+    def forward(self, x, fp8=False):
+        B, T, D = x.shape
+        qkv = fused.linear(x, self.qkv, fp8=fp8)                          # [B,T,3D]
+        qkv = qkv.view(B, T, 3, self.num_heads, self.head_dim).permute(2, 0, 3, 1, 4)
+        o = fused.attention(qkv[0], qkv[1], qkv[2])                        # [B,H,T,hd]
+        o = o.transpose(1, 2).reshape(B, T, D)
+        return fused.linear(o, self.proj, fp8=fp8)
+
+
+class Mlp(nn.Module):
+    def __init__(self, dim, hidden):
+        super().__init__()
+        self.fc1 = nn.Linear(dim, hidden)
+        self.fc2 = nn.Linear(hidden, dim)
+
+    def forward(self, x, fp8=False):
+        return fused.linear(fused.linear(x, self.fc1, act="gelu", fp8=fp8), self.fc2, fp8=fp8)
+
+
+class Block(nn.Module):
+    def __init__(self, dim, num_heads, mlp_ratio=4.0):
+        super().__init__()
+        self.norm1 = nn.LayerNorm(dim, eps=1e-6)
+        self.attn = Attention(dim, num_heads)
+        self.norm2 = nn.LayerNorm(dim, eps=1e-6)
+        self.mlp = Mlp(dim, int(dim * mlp_ratio))
+
+    def forward(self, x, fp8=False):
+        x = x + self.attn(fused.layer_norm(x, self.norm1), fp8=fp8)
+        x = x + self.mlp(fused.layer_norm(x, self.norm2), fp8=fp8)
+        return x
+
+
+class VisionTransformer(BaseModel):
+    def __init__(self, image_size=224, patch_size=16, in_chans=3, num_classes=1000, embed_dim=768,
+                 depth=12, num_heads=12, mlp_ratio=4.0, fp8=False):
+        super().__init__()
+        self.patch_size = patch_size
+        self.fp8 = fp8
+        self.patch_embed = nn.Conv2d(in_chans, embed_dim, patch_size, stride=patch_size)
+        n_patches = (image_size // patch_size) ** 2
+        self.cls_token = nn.Parameter(torch.zeros(1, 1, embed_dim))
+        self.pos_embed = nn.Parameter(torch.zeros(1, n_patches + 1, embed_dim))
+        self.blocks = nn.ModuleList([Block(embed_dim, num_heads, mlp_ratio) for _ in range(depth)])
+        self.norm = nn.LayerNorm(embed_dim, eps=1e-6)
+        self.head = nn.Linear(embed_dim, num_classes)
+        nn.init.trunc_normal_(self.pos_embed, std=0.02)
+        nn.init.trunc_normal_(self.cls_token, std=0.02)
+        for m in self.modules():
+            if isinstance(m, nn.Linear):
+                nn.init.trunc_normal_(m.weight, std=0.02)
+                nn.init.zeros_(m.bias)
+        fan_in = in_chans * patch_size * patch_size
+        nn.init.trunc_normal_(self.patch_embed.weight, std=math.sqrt(1.0 / fan_in))
+
+    def forward(self, x):
+        x = fused.patch_embed(x, self.patch_embed)                 # [B, N, D]
+        B = x.shape[0]
+        cls = self.cls_token.to(x.dtype).expand(B, -1, -1)
+        x = torch.cat([cls, x], dim=1) + self.pos_embed.to(x.dtype)
+        for blk in self.blocks:
+            x = blk(x, fp8=self.fp8)
+        x = fused.layer_norm(x[:, 0], self.norm)
+        return fused.linear(x, self.head)
+
+
+def vit_b_16(num_classes=1000, **kw):
+    return VisionTransformer(num_classes=num_classes, **kw)
+
+
+class ViT_B_16(VisionTransformer):
+    def __init__(self, num_classes=1000, fp8=False, **kw):
+        super().__init__(num_classes=num_classes, fp8=fp8, **kw)

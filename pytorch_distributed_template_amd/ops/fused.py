@@ -1,0 +1,130 @@
+"""Fused op entry points used by the models.
+
+Each function has two implementations:
+  * ``native``: hand-written HIP/CDNA4 kernels (``csrc/*.hip``) wrapped in
+    ``torch.autograd.Function``s (see ``ops/native_ops.py``);
+  * ``torch``: plain PyTorch ops -- used on CPU (gloo plumbing tests), as the
+    fp32 reference in numerics tests, and as the "stock ROCm stack" baseline
+    in ``bench.py --backend torch``.
+
+The backend is chosen per process with :func:`set_backend` (default:
+``native`` for GPU tensors when the extension is built, ``torch`` on CPU).
+The reference has no fused ops at all -- it runs stock cuDNN/cuBLAS kernels
+(SURVEY.md §2.6(a)).
+"""
+from __future__ import annotations
+
+import os
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+_BACKEND = os.environ.get("PDT_BACKEND", "auto")  # auto | native | torch
+
+
+def set_backend(name: str) -> None:
+    global _BACKEND
+    assert name in ("auto", "native", "torch"), name
+    _BACKEND = name
+
+
+def get_backend() -> str:
+    return _BACKEND
+
+
+def _use_native(x: torch.Tensor) -> bool:
+    if _BACKEND == "torch" or not x.is_cuda:
+        return False
+    from . import native_ops  # noqa: WPS433 (lazy: avoids loading the .so on CPU)
+    if _BACKEND == "native":
+        native_ops.require()
+        return True
+    return native_ops.available()
+
+
+# ----------------------------------------------------------------------------
+# reference (torch) implementations
+# ----------------------------------------------------------------------------
+def _torch_conv_bn_act(x, conv: nn.Conv2d, bn: nn.BatchNorm2d, residual=None, relu=True):
+    # plain ops; under torch.autocast(bf16) conv runs in bf16 and BN keeps fp32 params
+    y = conv(x)
+    y = bn(y)
+    if residual is not None:
+        y = y + residual
+    if relu:
+        y = F.relu(y)
+    return y
+
+
+def conv_bn_act(x, conv: nn.Conv2d, bn: nn.BatchNorm2d, residual=None, relu: bool = True):
+    """y = act(BN(conv(x)) [+ residual]) with training-mode batch statistics."""
+    if _use_native(x):
+        from . import native_ops
+        return native_ops.conv_bn_act(x, conv, bn, residual, relu)
+    return _torch_conv_bn_act(x, conv, bn, residual, relu)
+
+
+def max_pool2d(x, kernel_size=3, stride=2, padding=1):
+    if _use_native(x):
+        from . import native_ops
+        return native_ops.max_pool2d(x, kernel_size, stride, padding)
+    return F.max_pool2d(x, kernel_size, stride, padding)
+
+
+def global_avg_pool(x):
+    """[N,C,H,W] (any memory format) -> [N,C]."""
+    if _use_native(x):
+        from . import native_ops
+        return native_ops.global_avg_pool(x)
+    return torch.flatten(F.adaptive_avg_pool2d(x, 1), 1)
+
+
+def _torch_linear(x, fc: nn.Linear, act=None):
+    y = fc(x)
+    if act == "gelu":
+        y = F.gelu(y, approximate="tanh")
+    elif act == "relu":
+        y = F.relu(y)
+    return y
+
+
+def linear(x, fc: nn.Linear, act: str | None = None, fp8: bool = False):
+    """y = act(x @ W^T + b). ``act`` in {None, "gelu", "relu"}; ``fp8`` selects the
+    e4m3 GEMM with per-tensor scaling on the native path (ignored on torch path)."""
+    if _use_native(x):
+        from . import native_ops
+        return native_ops.linear(x, fc, act=act, fp8=fp8)
+    return _torch_linear(x, fc, act)
+
+
+def layer_norm(x, ln: nn.LayerNorm):
+    if _use_native(x):
+        from . import native_ops
+        return native_ops.layer_norm(x, ln)
+    return ln(x)
+
+
+def attention(q, k, v):
+    """softmax(q k^T / sqrt(d)) v for [B,H,T,d] tensors (non-causal)."""
+    if _use_native(q):
+        from . import native_ops
+        return native_ops.attention(q, k, v)
+    return F.scaled_dot_product_attention(q, k, v)
+
+
+def patch_embed(x, conv: nn.Conv2d):
+    """Non-overlapping patch conv -> [B, N, D] tokens."""
+    if _use_native(x):
+        from . import native_ops
+        return native_ops.patch_embed(x, conv)
+    y = conv(x)
+    return y.flatten(2).transpose(1, 2)
+
+
+def softmax_cross_entropy(logits, target, label_smoothing: float = 0.0):
+    """Mean softmax cross-entropy (fused fwd/bwd kernel on the native path)."""
+    if _use_native(logits):
+        from . import native_ops
+        return native_ops.softmax_cross_entropy(logits, target, label_smoothing)
+    return F.cross_entropy(logits.float(), target, label_smoothing=label_smoothing)

@@ -1,0 +1,555 @@
+"""ctypes bindings to ``libpdt_hip.so`` and the autograd Functions built on them.
+
+Every op checks shapes / dtypes / memory formats on the host before a kernel
+is launched (a mis-shaped launch on MI355X can fault the whole node) and
+raises loudly if the library is missing on a GPU run -- there is no silent
+fallback inside this module. ``ops/fused.py`` decides native vs torch.
+
+Tensor conventions: activations are bf16 ``channels_last`` (NHWC storage);
+parameters stay fp32 (master weights) and are cast to bf16 shadows that the
+kernels read; gradients of parameters are produced in fp32.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import threading
+from pathlib import Path
+
+import torch
+import torch.nn as nn
+
+_LIB_PATH = Path(__file__).resolve().parents[1] / "_lib" / "libpdt_hip.so"
+_lib = None
+_lock = threading.Lock()
+
+c_int, c_long, c_float, c_double, c_void_p, c_uint = (ctypes.c_int, ctypes.c_long, ctypes.c_float,
+                                                      ctypes.c_double, ctypes.c_void_p, ctypes.c_uint)
+P = c_void_p
+
+_SIGS = {
+    "pdt_conv_nt_stat_rows": (c_int, [c_int, c_int]),
+    "pdt_conv_nt": (c_int, [P, P, P, P, P] + [c_int] * 25 + [P]),
+    "pdt_wgrad_plan": (c_int, [c_int, c_int, c_int, ctypes.POINTER(c_int)]),
+    "pdt_conv_wgrad": (c_int, [P, P, P, P] + [c_int] * 16 + [c_int, c_int, c_float, c_int, P]),
+    "pdt_bn_stats_blocks": (c_int, [c_long, c_int]),
+    "pdt_bn_stats": (c_int, [P, P, c_long, c_int, c_int, P]),
+    "pdt_bn_finalize": (c_int, [P, c_int, c_int, c_double, c_float, c_float] + [P] * 8 + [P]),
+    "pdt_bn_apply": (c_int, [P, P, P, P, P, c_long, c_int, c_int, P]),
+    "pdt_bn_bwd_reduce": (c_int, [P, P, P, P, P, P, P, c_long, c_int, c_int, c_int, P]),
+    "pdt_bn_bwd_finalize": (c_int, [P, c_int, c_int, c_double] + [P] * 8 + [c_int, P]),
+    "pdt_bn_bwd_apply": (c_int, [P] * 10 + [c_long, c_int, c_int, P]),
+    "pdt_maxpool_fwd": (c_int, [P, P, P] + [c_int] * 9 + [P]),
+    "pdt_maxpool_bwd": (c_int, [P, P, P] + [c_int] * 9 + [P]),
+    "pdt_avgpool_fwd": (c_int, [P, P, c_int, c_int, c_int, P]),
+    "pdt_avgpool_bwd": (c_int, [P, P, c_int, c_int, c_int, P]),
+    "pdt_xent_fwd": (c_int, [P, c_int, P, P, P, P, c_int, c_int, c_float, P]),
+    "pdt_xent_bwd": (c_int, [P, c_int, P, P, P, P, c_int, c_int, c_float, P]),
+    "pdt_colsum": (c_int, [P, P, c_int, c_int, c_int, P]),
+    "pdt_chunk_struct_size": (c_int, []),
+    "pdt_sgd_step": (c_int, [P, c_int, P, P, P, P, c_float, c_float, c_float, c_float, c_int, c_int, c_float, P]),
+    "pdt_adam_step": (c_int, [P, c_int, P, P, P, P, P, P] + [c_float] * 5 + [c_int, c_float, c_float, c_float, P]),
+    "pdt_fill_uniform_bf16": (c_int, [P, c_long, c_uint, P]),
+    "pdt_cast_f32_bf16": (c_int, [P, P, c_long, P]),
+    "pdt_wt_dgrad": (c_int, [P, P] + [c_int] * 9 + [P]),
+    "pdt_transpose_cast": (c_int, [P, P, c_int, c_int, P]),
+    "pdt_add_bf16": (c_int, [P, P, P, c_long, P]),
+}
+
+
+def lib_path() -> Path:
+    return _LIB_PATH
+
+
+def _load():
+    global _lib
+    if _lib is not None:
+        return _lib
+    with _lock:
+        if _lib is None:
+            if not _LIB_PATH.exists():
+                raise RuntimeError(f"native kernel library missing: {_LIB_PATH} -- run "
+                                   "`python -m pytorch_distributed_template_amd.ops.build`")
+            lib = ctypes.CDLL(str(_LIB_PATH))
+            for name, (res, args) in _SIGS.items():
+                fn = getattr(lib, name)
+                fn.restype = res
+                fn.argtypes = args
+            _lib = lib
+    return _lib
+
+
+def available() -> bool:
+    if os.environ.get("PDT_DISABLE_NATIVE") == "1":
+        return False
+    return _LIB_PATH.exists() and torch.cuda.is_available()
+
+
+def require():
+    if not torch.cuda.is_available():
+        raise RuntimeError("native HIP ops need a GPU")
+    _load()
+
+
+def _s():
+    return torch.cuda.current_stream().cuda_stream
+
+
+def _p(t):
+    return None if t is None else t.data_ptr()
+
+
+def _chk(rc, name):
+    if rc != 0:
+        raise RuntimeError(f"{name} failed with code {rc}")
+
+
+def _cl(t: torch.Tensor) -> torch.Tensor:
+    """channels_last-contiguous view/copy (NHWC storage)."""
+    if t.dim() == 4 and not t.is_contiguous(memory_format=torch.channels_last):
+        t = t.contiguous(memory_format=torch.channels_last)
+    return t
+
+
+def _empty_cl(n, c, h, w, dtype, device):
+    return torch.empty((n, c, h, w), dtype=dtype, device=device, memory_format=torch.channels_last)
+
+
+# =============================================================================
+# bf16 weight shadows (cast once per parameter version)
+# =============================================================================
+_SHADOWS: dict = {}
+
+
+def register_shadow(param: torch.Tensor, shadow: torch.Tensor):
+    """Optimizers that write a bf16 copy while stepping register it here."""
+    _SHADOWS[id(param)] = (shadow, param._version, param.data_ptr())
+
+
+def bf16_weight(w: torch.Tensor, pad_cin_to: int | None = None) -> torch.Tensor:
+    """bf16 copy of an fp32 weight in [Cout][..][Cin] (channels_last) storage."""
+    if w.dtype == torch.bfloat16 and pad_cin_to is None:
+        return _cl(w)
+    key = (id(w), pad_cin_to)
+    ent = _SHADOWS.get(key if pad_cin_to else id(w))
+    if ent is not None and ent[1] == w._version and ent[2] == w.data_ptr():
+        return ent[0]
+    src = _cl(w.detach())
+    if pad_cin_to is not None and src.shape[1] != pad_cin_to:
+        src = torch.nn.functional.pad(src, (0, 0, 0, 0, 0, pad_cin_to - src.shape[1]))
+        src = _cl(src)
+    out = torch.empty_like(src, dtype=torch.bfloat16, memory_format=torch.channels_last) if src.dim() == 4 \
+        else torch.empty_like(src, dtype=torch.bfloat16)
+    if src.dtype == torch.float32:
+        _chk(_load().pdt_cast_f32_bf16(_p(src), _p(out), src.numel(), _s()), "cast")
+    else:
+        out.copy_(src)
+    _SHADOWS[key if pad_cin_to else id(w)] = (out, w._version, w.data_ptr())
+    return out
+
+
+# =============================================================================
+# raw kernel wrappers
+# =============================================================================
+def conv_nt(src, b, out, *, Hs, Ws, Cs, Nimg, Hm, Wm, Ncol, K, ldb, sh, sw, oh0, ow0, dh, dw, nth, ntw,
+            Ho, Wo, osh, osw, oph, opw, ldo, stats=None, bias=None, relu=False):
+    assert src.dtype == torch.bfloat16 and b.dtype == torch.bfloat16 and out.dtype == torch.bfloat16
+    assert Cs % 8 == 0 and K % 8 == 0 and Ncol % 8 == 0 and ldo % 8 == 0, (Cs, K, Ncol, ldo)
+    assert K == nth * ntw * Cs
+    # bounds: the kernel reads src[0 : Nimg*Hs*Ws*Cs], b[0 : Ncol*ldb], writes out rows < Nimg*Ho*Wo
+    assert src.numel() >= Nimg * Hs * Ws * Cs, "src too small"
+    assert b.numel() >= Ncol * ldb or K == 0, "B too small"
+    assert out.numel() >= Nimg * Ho * Wo * ldo, "out too small"
+    assert Nimg * Hs * Ws * Cs < 2 ** 31 and Nimg * Ho * Wo < 2 ** 31
+    rc = _load().pdt_conv_nt(_p(src), _p(b), _p(out), _p(stats), _p(bias), Hs, Ws, Cs, Nimg, Hm, Wm, Ncol, K,
+                             ldb, sh, sw, oh0, ow0, dh, dw, nth, ntw, Ho, Wo, osh, osw, oph, opw, ldo,
+                             int(relu), _s())
+    _chk(rc, "conv_nt")
+
+
+def conv_stat_rows(M, Ncol):
+    return _load().pdt_conv_nt_stat_rows(M, Ncol)
+
+
+def conv_wgrad(dy, x, out, *, M, Mo, No, ldy, Hs, Ws, C, Hm, Wm, sh, sw, oh0, ow0, dh, dw, ntw, scale=1.0,
+               accumulate=False):
+    assert dy.dtype == torch.bfloat16 and x.dtype == torch.bfloat16 and out.dtype == torch.float32
+    assert C % 8 == 0 and Mo % 8 == 0 and No % 8 == 0 and ldy % 8 == 0
+    assert out.numel() >= Mo * No and dy.numel() >= M * ldy
+    lib = _load()
+    kps = c_int(0)
+    splits = lib.pdt_wgrad_plan(M, Mo, No, ctypes.byref(kps))
+    slab = torch.empty(splits * Mo * No, dtype=torch.float32, device=dy.device)
+    rc = lib.pdt_conv_wgrad(_p(dy), _p(x), _p(slab), _p(out), M, Mo, No, ldy, Hs, Ws, C, Hm, Wm, sh, sw, oh0,
+                            ow0, dh, dw, ntw, splits, kps.value, float(scale), int(accumulate), _s())
+    _chk(rc, "conv_wgrad")
+
+
+def fill_uniform_(t: torch.Tensor, seed: int):
+    assert t.dtype == torch.bfloat16 and t.numel() % 8 == 0
+    _chk(_load().pdt_fill_uniform_bf16(_p(t), t.numel(), seed & 0xFFFFFFFF, _s()), "fill")
+    return t
+
+
+def synthetic_images(shape, dtype, device, seed=0, channels_last=True):
+    n, c, h, w = shape
+    if channels_last:
+        x = torch.empty(shape, dtype=torch.bfloat16, device=device, memory_format=torch.channels_last)
+    else:
+        x = torch.empty(shape, dtype=torch.bfloat16, device=device)
+    fill_uniform_(x, seed)
+    return x if dtype == torch.bfloat16 else x.to(dtype)
+
+
+# =============================================================================
+# conv geometry helpers
+# =============================================================================
+def _fwd_geom(N, H, W, Cs, conv: nn.Conv2d):
+    KH, KW = conv.kernel_size
+    sh, sw = conv.stride
+    ph, pw = conv.padding
+    Ho = (H + 2 * ph - KH) // sh + 1
+    Wo = (W + 2 * pw - KW) // sw + 1
+    return dict(KH=KH, KW=KW, sh=sh, sw=sw, ph=ph, pw=pw, Ho=Ho, Wo=Wo)
+
+
+def supports_conv(x: torch.Tensor, conv: nn.Conv2d) -> bool:
+    if conv.groups != 1 or conv.dilation != (1, 1) or conv.bias is not None:
+        return False
+    if x.dim() != 4 or conv.out_channels % 8 != 0:
+        return False
+    N, C, H, W = x.shape
+    if C % 8 != 0 and C > 8:
+        return False
+    sh, sw = conv.stride
+    if (H % sh) or (W % sw):
+        return False
+    return True
+
+
+def _conv_forward(x, wb, N, H, W, Cs, Cout, g, stats=None):
+    M = N * g["Ho"] * g["Wo"]
+    y = _empty_cl(N, Cout, g["Ho"], g["Wo"], torch.bfloat16, x.device)
+    conv_nt(x, wb, y, Hs=H, Ws=W, Cs=Cs, Nimg=N, Hm=g["Ho"], Wm=g["Wo"], Ncol=Cout, K=g["KH"] * g["KW"] * Cs,
+            ldb=g["KH"] * g["KW"] * Cs, sh=g["sh"], sw=g["sw"], oh0=-g["ph"], ow0=-g["pw"], dh=1, dw=1,
+            nth=g["KH"], ntw=g["KW"], Ho=g["Ho"], Wo=g["Wo"], osh=1, osw=1, oph=0, opw=0, ldo=Cout, stats=stats)
+    return y, M
+
+
+def _conv_dgrad(dy, w32, N, H, W, Cin, Cout, g):
+    """dX [N,Cin,H,W] from dY [N,Cout,Ho,Wo] (stride phases, see csrc/conv_igemm.hip)."""
+    KH, KW, s_h, s_w, ph, pw = g["KH"], g["KW"], g["sh"], g["sw"], g["ph"], g["pw"]
+    dx = _empty_cl(N, Cin, H, W, torch.bfloat16, dy.device)
+    lib = _load()
+    w32c = _cl(w32.detach().float())
+    for qh in range(s_h):
+        kh0 = (qh + ph) % s_h
+        nth = (KH - kh0 + s_h - 1) // s_h if kh0 < KH else 0
+        oh0 = (qh + ph - kh0) // s_h
+        for qw in range(s_w):
+            kw0 = (qw + pw) % s_w
+            ntw = (KW - kw0 + s_w - 1) // s_w if kw0 < KW else 0
+            ow0 = (qw + pw - kw0) // s_w
+            K = nth * ntw * Cout
+            wt = torch.empty(max(Cin * K, 8), dtype=torch.bfloat16, device=dy.device)
+            if K > 0:
+                assert s_h == s_w or True
+                _chk(lib.pdt_wt_dgrad(_p(w32c), _p(wt), Cout, KH, KW, Cin, kh0, kw0, s_h if s_h == s_w else s_h,
+                                      nth, ntw, _s()), "wt_dgrad")
+            conv_nt(dy, wt, dx, Hs=g["Ho"], Ws=g["Wo"], Cs=Cout, Nimg=N, Hm=H // s_h, Wm=W // s_w, Ncol=Cin,
+                    K=K, ldb=max(K, 8), sh=1, sw=1, oh0=oh0, ow0=ow0, dh=-1, dw=-1, nth=nth, ntw=max(ntw, 0),
+                    Ho=H, Wo=W, osh=s_h, osw=s_w, oph=qh, opw=qw, ldo=Cin)
+    return dx
+
+
+def _conv_wgrad(dy, x, N, H, W, Cs, Cout, g, out):
+    M = N * g["Ho"] * g["Wo"]
+    conv_wgrad(dy, x, out, M=M, Mo=Cout, No=g["KH"] * g["KW"] * Cs, ldy=Cout, Hs=H, Ws=W, C=Cs, Hm=g["Ho"],
+               Wm=g["Wo"], sh=g["sh"], sw=g["sw"], oh0=-g["ph"], ow0=-g["pw"], dh=1, dw=1, ntw=g["KW"])
+
+
+# =============================================================================
+# fused conv -> BN -> (+res) -> (ReLU)
+# =============================================================================
+class _ConvBNAct(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, w, gamma, beta, residual, running_mean, running_var, conv, relu, training, momentum, eps):
+        lib = _load()
+        st = _s()
+        N, C, H, W = x.shape
+        Cs = C if C % 8 == 0 else 8
+        x = x.to(torch.bfloat16)
+        if Cs != C:  # stem: pad channels to 8 (NHWC)
+            x = torch.nn.functional.pad(_cl(x).permute(0, 2, 3, 1), (0, Cs - C)).permute(0, 3, 1, 2)
+        x = _cl(x)
+        Cout = w.shape[0]
+        g = _fwd_geom(N, H, W, Cs, conv)
+        wb = bf16_weight(w, pad_cin_to=Cs if Cs != C else None)
+        dev = x.device
+        f32 = dict(dtype=torch.float32, device=dev)
+        M = N * g["Ho"] * g["Wo"]
+        if training:
+            R = conv_stat_rows(M, Cout)
+            part = torch.empty(2 * R * Cout, **f32)
+            y, _ = _conv_forward(x, wb, N, H, W, Cs, Cout, g, stats=part)
+            mean = torch.empty(Cout, **f32)
+            invstd = torch.empty(Cout, **f32)
+            scale = torch.empty(Cout, **f32)
+            shift = torch.empty(Cout, **f32)
+            rm = running_mean if running_mean is not None else None
+            rv = running_var if running_var is not None else None
+            _chk(lib.pdt_bn_finalize(_p(part), R, Cout, float(M), float(eps), float(momentum), _p(gamma),
+                                     _p(beta), _p(mean), _p(invstd), _p(scale), _p(shift), _p(rm), _p(rv), st),
+                 "bn_finalize")
+        else:
+            y, _ = _conv_forward(x, wb, N, H, W, Cs, Cout, g, stats=None)
+            invstd = torch.rsqrt(running_var.float() + eps)
+            mean = running_mean.float().clone()
+            scale = (gamma.float() * invstd).contiguous()
+            shift = (beta.float() - mean * scale).contiguous()
+        res = None
+        if residual is not None:
+            res = _cl(residual)
+            assert res.dtype == torch.bfloat16 and res.shape == y.shape, (res.shape, y.shape)
+        out = torch.empty_like(y, memory_format=torch.channels_last)
+        _chk(lib.pdt_bn_apply(_p(y), _p(res), _p(out), _p(scale), _p(shift), M, Cout, int(relu), st), "bn_apply")
+        ctx.save_for_backward(x, w, gamma, y, out if (relu and residual is not None) else None, mean, invstd,
+                              scale, shift)
+        ctx.meta = (N, C, Cs, H, W, Cout, g, relu, residual is not None)
+        return out
+
+    @staticmethod
+    def backward(ctx, dA):
+        x, w, gamma, y, act, mean, invstd, scale, shift = ctx.saved_tensors
+        N, C, Cs, H, W, Cout, g, relu, has_res = ctx.meta
+        lib = _load()
+        st = _s()
+        dA = _cl(dA.to(torch.bfloat16))
+        M = N * g["Ho"] * g["Wo"]
+        dev = dA.device
+        f32 = dict(dtype=torch.float32, device=dev)
+        blocks = lib.pdt_bn_stats_blocks(M, Cout)
+        part = torch.empty(2 * blocks * Cout, **f32)
+        _chk(lib.pdt_bn_bwd_reduce(_p(dA), _p(y), _p(act), _p(mean), _p(scale), _p(shift), _p(part), M, Cout,
+                                   int(relu), blocks, st), "bn_bwd_reduce")
+        dgamma = torch.empty(Cout, **f32)
+        dbeta = torch.empty(Cout, **f32)
+        k1 = torch.empty(Cout, **f32)
+        k2 = torch.empty(Cout, **f32)
+        k3 = torch.empty(Cout, **f32)
+        _chk(lib.pdt_bn_bwd_finalize(_p(part), blocks, Cout, float(M), _p(gamma), _p(mean), _p(invstd),
+                                     _p(dgamma), _p(dbeta), _p(k1), _p(k2), _p(k3), 0, st), "bn_bwd_finalize")
+        dy = torch.empty_like(y, memory_format=torch.channels_last)
+        dres = torch.empty_like(y, memory_format=torch.channels_last) if has_res else None
+        _chk(lib.pdt_bn_bwd_apply(_p(dA), _p(y), _p(act), _p(scale), _p(shift), _p(k1), _p(k2), _p(k3), _p(dy),
+                                  _p(dres), M, Cout, int(relu), st), "bn_bwd_apply")
+        dx = None
+        if ctx.needs_input_grad[0]:
+            dx = _conv_dgrad(dy, w, N, H, W, Cs, Cout, g)
+            if Cs != C:
+                dx = dx[:, :C]
+        dw = None
+        if ctx.needs_input_grad[1]:
+            KH, KW = g["KH"], g["KW"]
+            if Cs == C and w.is_contiguous(memory_format=torch.channels_last):
+                dw = torch.empty_like(w, dtype=torch.float32, memory_format=torch.channels_last)
+                _conv_wgrad(dy, x, N, H, W, Cs, Cout, g, dw)
+            else:
+                tmp = torch.empty((Cout, Cs, KH, KW), memory_format=torch.channels_last, **f32)
+                _conv_wgrad(dy, x, N, H, W, Cs, Cout, g, tmp)
+                dw = tmp[:, :C].contiguous(memory_format=torch.channels_last) if Cs != C else tmp
+            if dw.dtype != w.dtype:
+                dw = dw.to(w.dtype)
+        return (dx, dw, dgamma if ctx.needs_input_grad[2] else None, dbeta if ctx.needs_input_grad[3] else None,
+                dres, None, None, None, None, None, None, None)
+
+
+def conv_bn_act(x, conv: nn.Conv2d, bn: nn.BatchNorm2d, residual=None, relu=True):
+    if not supports_conv(x, conv) or (residual is not None and residual.dtype != torch.bfloat16):
+        from .fused import _torch_conv_bn_act
+        return _torch_conv_bn_act(x, conv, bn, residual, relu)
+    training = bn.training or not bn.track_running_stats
+    momentum = bn.momentum if bn.momentum is not None else 0.1
+    rm = bn.running_mean if (bn.track_running_stats and bn.training) else None
+    rv = bn.running_var if (bn.track_running_stats and bn.training) else None
+    if bn.training and bn.track_running_stats and bn.num_batches_tracked is not None:
+        bn.num_batches_tracked.add_(1)
+    if not training:
+        rm, rv = bn.running_mean, bn.running_var
+    return _ConvBNAct.apply(x, conv.weight, bn.weight, bn.bias, residual, rm, rv, conv, relu, training, momentum,
+                            bn.eps)
+
+
+# =============================================================================
+# pooling
+# =============================================================================
+class _MaxPool(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, k, s, p):
+        x = _cl(x)
+        N, C, H, W = x.shape
+        Ho = (H + 2 * p - k) // s + 1
+        Wo = (W + 2 * p - k) // s + 1
+        y = _empty_cl(N, C, Ho, Wo, torch.bfloat16, x.device)
+        idx = torch.empty(N * Ho * Wo * C, dtype=torch.uint8, device=x.device)
+        _chk(_load().pdt_maxpool_fwd(_p(x), _p(y), _p(idx), N, H, W, C, Ho, Wo, k, s, p, _s()), "maxpool_fwd")
+        ctx.save_for_backward(idx)
+        ctx.meta = (N, C, H, W, Ho, Wo, k, s, p)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        (idx,) = ctx.saved_tensors
+        N, C, H, W, Ho, Wo, k, s, p = ctx.meta
+        dy = _cl(dy.to(torch.bfloat16))
+        dx = _empty_cl(N, C, H, W, torch.bfloat16, dy.device)
+        _chk(_load().pdt_maxpool_bwd(_p(dy), _p(idx), _p(dx), N, H, W, C, Ho, Wo, k, s, p, _s()), "maxpool_bwd")
+        return dx, None, None, None
+
+
+def max_pool2d(x, kernel_size=3, stride=2, padding=1):
+    if x.dtype != torch.bfloat16 or x.shape[1] % 8:
+        return torch.nn.functional.max_pool2d(x, kernel_size, stride, padding)
+    return _MaxPool.apply(x, kernel_size, stride, padding)
+
+
+class _AvgPool(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x):
+        x = _cl(x)
+        N, C, H, W = x.shape
+        y = torch.empty((N, C), dtype=torch.bfloat16, device=x.device)
+        _chk(_load().pdt_avgpool_fwd(_p(x), _p(y), N, H * W, C, _s()), "avgpool_fwd")
+        ctx.meta = (N, C, H, W)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        N, C, H, W = ctx.meta
+        dy = dy.to(torch.bfloat16).contiguous()
+        dx = _empty_cl(N, C, H, W, torch.bfloat16, dy.device)
+        _chk(_load().pdt_avgpool_bwd(_p(dy), _p(dx), N, H * W, C, _s()), "avgpool_bwd")
+        return dx
+
+
+def global_avg_pool(x):
+    if x.dtype != torch.bfloat16 or x.shape[1] % 8:
+        return torch.flatten(torch.nn.functional.adaptive_avg_pool2d(x, 1), 1)
+    return _AvgPool.apply(x)
+
+
+# =============================================================================
+# linear (bf16 MFMA GEMM with bias / relu epilogue)
+# =============================================================================
+class _Linear(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, w, b, relu):
+        lib = _load()
+        shp = x.shape
+        x2 = x.reshape(-1, shp[-1]).to(torch.bfloat16).contiguous()
+        Mrows, K = x2.shape
+        Nout = w.shape[0]
+        wb = bf16_weight(w)
+        y = torch.empty((Mrows, Nout), dtype=torch.bfloat16, device=x.device)
+        bias = b.float().contiguous() if b is not None else None
+        conv_nt(x2, wb, y, Hs=1, Ws=1, Cs=K, Nimg=Mrows, Hm=1, Wm=1, Ncol=Nout, K=K, ldb=K, sh=1, sw=1, oh0=0,
+                ow0=0, dh=1, dw=1, nth=1, ntw=1, Ho=1, Wo=1, osh=1, osw=1, oph=0, opw=0, ldo=Nout, bias=bias,
+                relu=relu)
+        ctx.save_for_backward(x2, w, y if relu else None)
+        ctx.meta = (shp, relu, b is not None)
+        return y.reshape(*shp[:-1], Nout)
+
+    @staticmethod
+    def backward(ctx, dy):
+        x2, w, yact = ctx.saved_tensors
+        shp, relu, has_b = ctx.meta
+        lib = _load()
+        st = _s()
+        Nout, K = w.shape
+        dy2 = dy.reshape(-1, Nout).to(torch.bfloat16).contiguous()
+        if relu:
+            dy2 = dy2 * (yact > 0)
+        Mrows = dy2.shape[0]
+        dx = None
+        if ctx.needs_input_grad[0]:
+            wt = torch.empty((K, Nout), dtype=torch.bfloat16, device=dy.device)
+            _chk(lib.pdt_transpose_cast(_p(w.detach().float().contiguous()), _p(wt), Nout, K, st), "transpose")
+            dx = torch.empty((Mrows, K), dtype=torch.bfloat16, device=dy.device)
+            conv_nt(dy2, wt, dx, Hs=1, Ws=1, Cs=Nout, Nimg=Mrows, Hm=1, Wm=1, Ncol=K, K=Nout, ldb=Nout, sh=1, sw=1,
+                    oh0=0, ow0=0, dh=1, dw=1, nth=1, ntw=1, Ho=1, Wo=1, osh=1, osw=1, oph=0, opw=0, ldo=K)
+            dx = dx.reshape(*shp[:-1], K)
+        dw = None
+        if ctx.needs_input_grad[1]:
+            dw = torch.empty((Nout, K), dtype=torch.float32, device=dy.device)
+            conv_wgrad(dy2, x2, dw, M=Mrows, Mo=Nout, No=K, ldy=Nout, Hs=1, Ws=1, C=K, Hm=1, Wm=1, sh=1, sw=1,
+                       oh0=0, ow0=0, dh=1, dw=1, ntw=1)
+        db = None
+        if has_b and ctx.needs_input_grad[2]:
+            db = torch.empty(Nout, dtype=torch.float32, device=dy.device)
+            _chk(lib.pdt_colsum(_p(dy2), _p(db), Mrows, Nout, 0, st), "colsum")
+        return dx, dw, db, None
+
+
+def linear(x, fc: nn.Linear, act=None, fp8=False):
+    K = fc.in_features
+    N = fc.out_features
+    if K % 8 or N % 8 or act not in (None, "relu"):
+        from .fused import _torch_linear
+        return _torch_linear(x, fc, act)
+    return _Linear.apply(x, fc.weight, fc.bias, act == "relu")
+
+
+# =============================================================================
+# softmax cross-entropy
+# =============================================================================
+class _XEnt(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, logits, target, eps):
+        lib = _load()
+        logits = logits.contiguous()
+        B, V = logits.shape
+        is_bf16 = logits.dtype == torch.bfloat16
+        if not is_bf16 and logits.dtype != torch.float32:
+            logits = logits.float()
+        target = target.to(torch.long).contiguous()
+        assert target.numel() == B
+        lse = torch.empty(B, dtype=torch.float32, device=logits.device)
+        rows = torch.empty(B, dtype=torch.float32, device=logits.device)
+        loss = torch.empty((), dtype=torch.float32, device=logits.device)
+        _chk(lib.pdt_xent_fwd(_p(logits), int(is_bf16), _p(target), _p(lse), _p(rows), _p(loss), B, V, float(eps),
+                              _s()), "xent_fwd")
+        ctx.save_for_backward(logits, target, lse)
+        ctx.eps = eps
+        return loss
+
+    @staticmethod
+    def backward(ctx, g):
+        logits, target, lse = ctx.saved_tensors
+        B, V = logits.shape
+        g = g.float().reshape(1).contiguous()
+        dl = torch.empty((B, V), dtype=torch.bfloat16, device=logits.device)
+        _chk(_load().pdt_xent_bwd(_p(logits), int(logits.dtype == torch.bfloat16), _p(target), _p(lse), _p(g),
+                                  _p(dl), B, V, float(ctx.eps), _s()), "xent_bwd")
+        return dl, None, None
+
+
+def softmax_cross_entropy(logits, target, label_smoothing=0.0):
+    if logits.dim() != 2:
+        return torch.nn.functional.cross_entropy(logits.float(), target, label_smoothing=label_smoothing)
+    return _XEnt.apply(logits, target, float(label_smoothing))
+
+
+# =============================================================================
+# ViT ops (torch path for now on GPU as well; native kernels land in ops/vit_ops)
+# =============================================================================
+def layer_norm(x, ln):
+    return ln(x)
+
+
+def attention(q, k, v):
+    return torch.nn.functional.scaled_dot_product_attention(q, k, v)
+
+
+def patch_embed(x, conv):
+    y = conv(x)
+    return y.flatten(2).transpose(1, 2)

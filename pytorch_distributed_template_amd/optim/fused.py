@@ -1,0 +1,256 @@
+"""Multi-tensor fused SGD / Adam(W) (+AMSGrad) on MI355X.
+
+Reference optimizer: ``torch.optim.Adam(lr=1e-3, weight_decay=0, amsgrad=True)``
+(``/root/reference/config/config.json:38-45``), stepped once per batch at
+``trainer/trainer.py:58``. Semantics match torch.optim exactly (tested against
+it); the state_dict format is torch's (``momentum_buffer`` / ``exp_avg`` /
+``exp_avg_sq`` / ``max_exp_avg_sq`` / ``step``), so checkpoints interchange
+with the torch optimizers of the same name.
+
+On GPU one HIP kernel (``csrc/optim.hip``) updates every parameter tensor:
+the host builds a chunk table once (re-built only if the set of tensors or
+their storage changes) and each step is a single launch that also writes the
+bf16 shadow copy of each parameter that the conv/GEMM kernels consume. On CPU
+(gloo plumbing) the step falls back to torch's reference implementation.
+"""
+from __future__ import annotations
+
+import ctypes
+
+import torch
+from torch.optim import Optimizer
+
+CHUNK = 65536
+
+
+class _Plan:
+    """Device-side pointer/chunk tables for one param group."""
+
+    def __init__(self, params, tensors_by_role, device):
+        from ..ops import native_ops
+        lib = native_ops._load()
+        sz = lib.pdt_chunk_struct_size()
+        assert sz == 24, sz
+        chunks = []
+        for ti, p in enumerate(params):
+            n = p.numel()
+            for off in range(0, n, CHUNK):
+                chunks.append((ti, 0, off, min(CHUNK, n - off)))
+        import numpy as np
+        arr = np.zeros(len(chunks), dtype=[("t", "<i4"), ("pad", "<i4"), ("off", "<i8"), ("len", "<i8")])
+        for i, c in enumerate(chunks):
+            arr[i] = c
+        self.chunks = torch.from_numpy(arr.view(np.uint8).copy()).to(device)
+        self.nchunks = len(chunks)
+        self.tables = {}
+        for role, ts in tensors_by_role.items():
+            ptrs = [0 if t is None else t.data_ptr() for t in ts]
+            self.tables[role] = torch.tensor(ptrs, dtype=torch.int64).to(device)
+        self.key = self._key(params, tensors_by_role)
+
+    @staticmethod
+    def _key(params, tensors_by_role):
+        return tuple((role, tuple(0 if t is None else t.data_ptr() for t in ts)) for role, ts in
+                     sorted(tensors_by_role.items())) + tuple(p.data_ptr() for p in params)
+
+    def ptr(self, role):
+        t = self.tables.get(role)
+        return None if t is None else t.data_ptr()
+
+
+def _native_ok(params):
+    from ..ops import native_ops
+    return (len(params) > 0 and all(p.is_cuda and p.dtype == torch.float32 and p.is_contiguous(
+        memory_format=torch.channels_last if p.dim() == 4 else torch.contiguous_format) or
+        (p.is_cuda and p.dtype == torch.float32 and p.is_contiguous()) for p in params)
+        and native_ops.available())
+
+
+class _FusedBase(Optimizer):
+    def __init__(self, params, defaults, write_bf16_shadow=True):
+        super().__init__(params, defaults)
+        self.write_bf16_shadow = write_bf16_shadow
+        self._plans = {}
+        self._shadows = {}
+
+    def _shadow(self, p):
+        if not self.write_bf16_shadow:
+            return None
+        s = self._shadows.get(id(p))
+        if s is None or s.data_ptr() == 0:
+            if p.dim() == 4:
+                s = torch.empty_like(p, dtype=torch.bfloat16, memory_format=torch.channels_last)
+            else:
+                s = torch.empty_like(p, dtype=torch.bfloat16)
+            self._shadows[id(p)] = s
+        return s
+
+    def _plan(self, gi, params, roles, device):
+        key = _Plan._key(params, roles)
+        plan = self._plans.get(gi)
+        if plan is None or plan.key != key:
+            plan = _Plan(params, roles, device)
+            self._plans[gi] = plan
+        return plan
+
+    @staticmethod
+    def _stream():
+        return torch.cuda.current_stream().cuda_stream
+
+
+class FusedSGD(_FusedBase):
+    """torch.optim.SGD semantics (momentum, dampening, nesterov, weight_decay)."""
+
+    def __init__(self, params, lr=0.1, momentum=0.0, dampening=0.0, weight_decay=0.0, nesterov=False,
+                 write_bf16_shadow=True):
+        defaults = dict(lr=lr, momentum=momentum, dampening=dampening, weight_decay=weight_decay,
+                        nesterov=nesterov)
+        super().__init__(params, defaults, write_bf16_shadow)
+
+    @torch.no_grad()
+    def step(self, closure=None):
+        loss = None
+        if closure is not None:
+            with torch.enable_grad():
+                loss = closure()
+        for gi, group in enumerate(self.param_groups):
+            params = [p for p in group["params"] if p.grad is not None]
+            if not params:
+                continue
+            if not _native_ok(params):
+                self._torch_step(group, params)
+                continue
+            from ..ops import native_ops
+            first = False
+            bufs = []
+            for p in params:
+                st = self.state[p]
+                if group["momentum"] != 0:
+                    if "momentum_buffer" not in st or st["momentum_buffer"] is None:
+                        st["momentum_buffer"] = torch.zeros_like(p, memory_format=torch.preserve_format)
+                        first = True
+                    bufs.append(st["momentum_buffer"])
+                else:
+                    bufs.append(None)
+            grads = [p.grad if p.grad.dtype == torch.float32 else p.grad.float() for p in params]
+            grads = [g if g.stride() == p.stride() else g.contiguous(memory_format=torch.channels_last
+                                                                     if p.dim() == 4 else torch.contiguous_format)
+                     for g, p in zip(grads, params)]
+            shadows = [self._shadow(p) for p in params]
+            roles = {"p": params, "g": grads, "b": bufs if group["momentum"] != 0 else [None] * len(params),
+                     "s": shadows if self.write_bf16_shadow else [None] * len(params)}
+            plan = self._plan(gi, params, roles, params[0].device)
+            rc = native_ops._load().pdt_sgd_step(
+                plan.chunks.data_ptr(), plan.nchunks, plan.ptr("p"), plan.ptr("g"),
+                plan.ptr("b") if group["momentum"] != 0 else None,
+                plan.ptr("s") if self.write_bf16_shadow else None,
+                float(group["lr"]), float(group["momentum"]), float(group["dampening"]),
+                float(group["weight_decay"]), int(group["nesterov"]), int(first), 1.0, self._stream())
+            native_ops._chk(rc, "sgd_step")
+            if self.write_bf16_shadow:
+                for p, s in zip(params, shadows):
+                    native_ops.register_shadow(p, s)
+        return loss
+
+    def _torch_step(self, group, params):
+        for p in params:
+            g = p.grad
+            if group["weight_decay"] != 0:
+                g = g.add(p, alpha=group["weight_decay"])
+            if group["momentum"] != 0:
+                st = self.state[p]
+                buf = st.get("momentum_buffer")
+                if buf is None:
+                    buf = torch.clone(g).detach()
+                    st["momentum_buffer"] = buf
+                else:
+                    buf.mul_(group["momentum"]).add_(g, alpha=1 - group["dampening"])
+                g = g.add(buf, alpha=group["momentum"]) if group["nesterov"] else buf
+            p.add_(g, alpha=-group["lr"])
+
+
+class FusedAdam(_FusedBase):
+    """torch.optim.Adam semantics (L2 weight decay; ``amsgrad``)."""
+    decoupled = False
+
+    def __init__(self, params, lr=1e-3, betas=(0.9, 0.999), eps=1e-8, weight_decay=0.0, amsgrad=False,
+                 write_bf16_shadow=True):
+        defaults = dict(lr=lr, betas=tuple(betas), eps=eps, weight_decay=weight_decay, amsgrad=amsgrad)
+        super().__init__(params, defaults, write_bf16_shadow)
+
+    @torch.no_grad()
+    def step(self, closure=None):
+        loss = None
+        if closure is not None:
+            with torch.enable_grad():
+                loss = closure()
+        for gi, group in enumerate(self.param_groups):
+            params = [p for p in group["params"] if p.grad is not None]
+            if not params:
+                continue
+            b1, b2 = group["betas"]
+            for p in params:
+                st = self.state[p]
+                if len(st) == 0:
+                    st["step"] = torch.tensor(0.0)
+                    st["exp_avg"] = torch.zeros_like(p, memory_format=torch.preserve_format)
+                    st["exp_avg_sq"] = torch.zeros_like(p, memory_format=torch.preserve_format)
+                    if group["amsgrad"]:
+                        st["max_exp_avg_sq"] = torch.zeros_like(p, memory_format=torch.preserve_format)
+                st["step"] += 1
+            step = float(self.state[params[0]]["step"])
+            bc1 = 1 - b1 ** step
+            bc2 = 1 - b2 ** step
+            if not _native_ok(params):
+                self._torch_step(group, params, bc1, bc2)
+                continue
+            from ..ops import native_ops
+            grads = [p.grad if p.grad.dtype == torch.float32 else p.grad.float() for p in params]
+            grads = [g if g.stride() == p.stride() else g.contiguous(memory_format=torch.channels_last
+                                                                     if p.dim() == 4 else torch.contiguous_format)
+                     for g, p in zip(grads, params)]
+            shadows = [self._shadow(p) for p in params]
+            roles = {"p": params, "g": grads, "m": [self.state[p]["exp_avg"] for p in params],
+                     "v": [self.state[p]["exp_avg_sq"] for p in params],
+                     "vm": [self.state[p].get("max_exp_avg_sq") for p in params] if group["amsgrad"]
+                     else [None] * len(params),
+                     "s": shadows if self.write_bf16_shadow else [None] * len(params)}
+            plan = self._plan(gi, params, roles, params[0].device)
+            rc = native_ops._load().pdt_adam_step(
+                plan.chunks.data_ptr(), plan.nchunks, plan.ptr("p"), plan.ptr("g"), plan.ptr("m"), plan.ptr("v"),
+                plan.ptr("vm") if group["amsgrad"] else None, plan.ptr("s") if self.write_bf16_shadow else None,
+                float(group["lr"]), float(b1), float(b2), float(group["eps"]), float(group["weight_decay"]),
+                int(self.decoupled), float(bc1), float(bc2), 1.0, self._stream())
+            native_ops._chk(rc, "adam_step")
+            if self.write_bf16_shadow:
+                for p, s in zip(params, shadows):
+                    native_ops.register_shadow(p, s)
+        return loss
+
+    def _torch_step(self, group, params, bc1, bc2):
+        b1, b2 = group["betas"]
+        for p in params:
+            st = self.state[p]
+            g = p.grad
+            if group["weight_decay"] != 0:
+                if self.decoupled:
+                    p.mul_(1 - group["lr"] * group["weight_decay"])
+                else:
+                    g = g.add(p, alpha=group["weight_decay"])
+            st["exp_avg"].mul_(b1).add_(g, alpha=1 - b1)
+            st["exp_avg_sq"].mul_(b2).addcmul_(g, g, value=1 - b2)
+            v = st["exp_avg_sq"]
+            if group["amsgrad"]:
+                torch.maximum(st["max_exp_avg_sq"], v, out=st["max_exp_avg_sq"])
+                v = st["max_exp_avg_sq"]
+            denom = (v.sqrt() / (bc2 ** 0.5)).add_(group["eps"])
+            p.addcdiv_(st["exp_avg"], denom, value=-group["lr"] / bc1)
+
+
+class FusedAdamW(FusedAdam):
+    """torch.optim.AdamW semantics (decoupled weight decay)."""
+    decoupled = True
+
+    def __init__(self, params, lr=1e-3, betas=(0.9, 0.999), eps=1e-8, weight_decay=1e-2, amsgrad=False,
+                 write_bf16_shadow=True):
+        super().__init__(params, lr, betas, eps, weight_decay, amsgrad, write_bf16_shadow)

@@ -1,0 +1,64 @@
+"""Data parallelism over RCCL/xGMI.
+
+Reference: ``/root/reference/train.py:45-52`` wraps the model in
+``DistributedDataParallel(device_ids=[local_rank], output_device=local_rank)``
+with the defaults (25 MiB buckets, ``broadcast_buffers=True``).
+
+Here the same DDP reducer (bucketed all-reduce issued from autograd hooks on
+RCCL's own HIP stream, overlapping the rest of backward) is configured for the
+MI355X node instead of NVSwitch defaults:
+
+* ``bucket_cap_mb``: xGMI is a full mesh of 7 point-to-point links per GPU;
+  RCCL's ring/tree channels are per-link bound, so a handful of large buckets
+  keeps every channel streaming. Default 64 MiB for fp32 grads: ResNet-50's
+  97.5 MiB of gradients become 2 buckets (the tail bucket, issued when
+  backward finishes layer1/stem, is the only exposed one) instead of 5.
+* ``gradient_as_bucket_view=True``: gradients live inside the buckets -- no
+  per-step copy into/out of the flat buffers (saves 2x gradient bytes of HBM
+  traffic per step).
+* ``broadcast_buffers``: the reference broadcasts BN running stats from rank 0
+  every forward (its own comment says to remove it). Configurable; the
+  benchmark disables it (running stats are not used by training-mode BN).
+* ``comm_hook="bf16"``: optional bf16-compressed all-reduce (half the xGMI bytes).
+"""
+from __future__ import annotations
+
+import torch
+from torch.nn.parallel import DistributedDataParallel
+
+from ..utils.dist import get_world_size
+
+DEFAULT_BUCKET_MB = 64
+
+
+def wrap_ddp(model: torch.nn.Module, device: torch.device, bucket_cap_mb: float = DEFAULT_BUCKET_MB,
+             broadcast_buffers: bool = True, gradient_as_bucket_view: bool = True,
+             comm_hook: str | None = None, static_graph: bool = False,
+             find_unused_parameters: bool = False):
+    """Wrap in DDP when world_size > 1, else return the model unchanged."""
+    if get_world_size() <= 1:
+        return model
+    kwargs = dict(bucket_cap_mb=bucket_cap_mb, broadcast_buffers=broadcast_buffers,
+                  gradient_as_bucket_view=gradient_as_bucket_view, static_graph=static_graph,
+                  find_unused_parameters=find_unused_parameters)
+    if device.type == "cuda":
+        kwargs.update(device_ids=[device.index], output_device=device.index)
+    ddp = DistributedDataParallel(model, **kwargs)
+    if comm_hook in ("bf16", "fp16"):
+        from torch.distributed.algorithms.ddp_comm_hooks import default_hooks
+        hook = default_hooks.bf16_compress_hook if comm_hook == "bf16" else default_hooks.fp16_compress_hook
+        ddp.register_comm_hook(state=None, hook=hook)
+    return ddp
+
+
+def bucket_plan(model: torch.nn.Module, bucket_cap_mb: float = DEFAULT_BUCKET_MB):
+    """Return the bucket sizes (bytes) DDP will build, for docs/tests."""
+    import torch.distributed as dist
+    params = [p for p in model.parameters() if p.requires_grad]
+    limit = int(bucket_cap_mb * 1024 * 1024)
+    idx, _ = dist._compute_bucket_assignment_by_size(list(reversed(params)), [1024 * 1024, limit])
+    sizes = []
+    rev = list(reversed(params))
+    for bucket in idx:
+        sizes.append(sum(rev[i].numel() * rev[i].element_size() for i in bucket))
+    return sizes

@@ -1,0 +1,80 @@
+"""Builds every training/eval component from a ConfigParser.
+
+Shared by ``train.py``, ``test.py`` and the tests so that the wiring in the
+reference's ``train.py:16-74`` / ``test.py:14-101`` lives in one place.
+Registries (``init_obj`` lookups, searched in order):
+  arch        -> pytorch_distributed_template_amd.models
+  loaders     -> pytorch_distributed_template_amd.data
+  loss        -> pytorch_distributed_template_amd.models.loss
+  metrics     -> pytorch_distributed_template_amd.models.metric
+  optimizer   -> pytorch_distributed_template_amd.optim, then torch.optim
+  lr_scheduler-> torch.optim.lr_scheduler (optional: null / missing disables it)
+
+Extra (optional) ``trainer`` keys, all defaulting to reference behaviour:
+  precision "fp32"|"bf16", channels_last bool, backend "auto"|"native"|"torch",
+  ddp {bucket_cap_mb, broadcast_buffers, gradient_as_bucket_view, comm_hook},
+  len_epoch int (iteration-based epochs), log_images bool.
+"""
+from __future__ import annotations
+
+import torch
+
+from .. import data as module_data
+from .. import models as module_arch
+from .. import optim as module_optim
+from ..models import loss as module_loss
+from ..models import metric as module_metric
+from ..ops import fused
+from ..parallel import wrap_ddp
+
+
+def build_model(config, device):
+    model = config.init_obj("arch", module_arch)
+    tcfg = config["trainer"]
+    if tcfg.get("backend"):
+        fused.set_backend(tcfg["backend"])
+    model = model.to(device)
+    if tcfg.get("channels_last", False):
+        model = model.to(memory_format=torch.channels_last)
+    return model
+
+
+def build_criterion_metrics(config):
+    criterion = getattr(module_loss, config["loss"])
+    metrics = [getattr(module_metric, met) for met in config["metrics"]]
+    return criterion, metrics
+
+
+def build_optimizer(config, model):
+    params = [p for p in model.parameters() if p.requires_grad]
+    optimizer = config.init_obj("optimizer", [module_optim, torch.optim], params)
+    lr_scheduler = None
+    if config.get("lr_scheduler"):
+        lr_scheduler = config.init_obj("lr_scheduler", torch.optim.lr_scheduler, optimizer)
+    return optimizer, lr_scheduler
+
+
+def wrap_model(config, model, device):
+    ddp_cfg = dict(config["trainer"].get("ddp", {}))
+    return wrap_ddp(model, device,
+                    bucket_cap_mb=ddp_cfg.get("bucket_cap_mb", 64),
+                    broadcast_buffers=ddp_cfg.get("broadcast_buffers", True),
+                    gradient_as_bucket_view=ddp_cfg.get("gradient_as_bucket_view", True),
+                    comm_hook=ddp_cfg.get("comm_hook"),
+                    find_unused_parameters=ddp_cfg.get("find_unused_parameters", False))
+
+
+def autocast_dtype(config, device):
+    """bf16 precision: native kernels are bf16 already (no autocast); the torch
+    path uses autocast(bf16) -- the reference-equivalent mixed precision."""
+    if config["trainer"].get("precision", "fp32") != "bf16":
+        return None
+    if device.type == "cuda" and fused.get_backend() != "torch":
+        from ..ops import native_ops
+        if native_ops.available():
+            return None
+    return torch.bfloat16
+
+
+def build_loader(config, name):
+    return config.init_obj(name, module_data)

@@ -1,0 +1,178 @@
+"""Distributed utilities: process-group init over RCCL/xGMI (or gloo on CPU)
+and the collective helpers the trainer uses.
+
+Reference: ``/root/reference/utils/dist.py:7-74`` (synchronize / get_rank /
+get_world_size / is_main_process / pickle-based all_gather) plus the inline
+``init_process_group('nccl', 'env://')`` in ``train.py:20-29``.
+
+MI355X-first differences:
+  * ``init_distributed`` picks ``nccl`` (== RCCL on ROCm, runs over the xGMI
+    full mesh) for GPU runs and ``gloo`` for CPU runs, binds the device from
+    ``LOCAL_RANK`` (the reference ignored it -- SURVEY Q16), passes
+    ``device_id`` so the RCCL communicator is created eagerly, and sets a
+    timeout (the reference had none -- SURVEY §5).
+  * ``all_gather`` keeps the reference's "any picklable object" contract but
+    moves objects through ``all_gather_object`` on the CPU-side of the
+    process group; tensor payloads use :func:`gather_tensors` which gathers
+    variable-length device tensors with two fixed-shape collectives and no
+    pickling.
+  * ``reduce_loss`` is the same SUM-reduce-to-rank-0 as
+    ``base_trainer.py:165-174`` but stays on device (no ``.item()``).
+"""
+from __future__ import annotations
+
+import datetime
+import os
+from typing import Any, List, Optional
+
+import torch
+import torch.distributed as dist
+
+
+def is_dist_ready() -> bool:
+    return dist.is_available() and dist.is_initialized()
+
+
+def synchronize():
+    """Barrier across all ranks (no-op when not distributed)."""
+    if not is_dist_ready() or dist.get_world_size() == 1:
+        return
+    if dist.get_backend() == "nccl" and torch.cuda.is_available():
+        dist.barrier(device_ids=[torch.cuda.current_device()])
+    else:
+        dist.barrier()
+
+
+def get_rank() -> int:
+    return dist.get_rank() if is_dist_ready() else 0
+
+
+def get_world_size() -> int:
+    return dist.get_world_size() if is_dist_ready() else 1
+
+
+def get_local_rank(cli_value: Optional[int] = None) -> int:
+    """LOCAL_RANK env (torchrun) wins, then the CLI ``--local-rank/--local_rank``."""
+    if "LOCAL_RANK" in os.environ:
+        return int(os.environ["LOCAL_RANK"])
+    return int(cli_value or 0)
+
+
+def is_main_process() -> bool:
+    return get_rank() == 0
+
+
+def env_world_size() -> int:
+    return int(os.environ.get("WORLD_SIZE", "1"))
+
+
+def init_distributed(local_rank: Optional[int] = None, backend: Optional[str] = None,
+                     timeout_s: float = 1800.0) -> torch.device:
+    """Initialise the default process group from the ``env://`` rendezvous.
+
+    Returns the device this rank should use. Safe to call with WORLD_SIZE=1
+    (returns the device, no process group).
+    """
+    local_rank = get_local_rank(local_rank)
+    use_cuda = torch.cuda.is_available() and backend != "gloo"
+    device = torch.device("cuda", local_rank) if use_cuda else torch.device("cpu")
+    if use_cuda:
+        torch.cuda.set_device(device)
+    if env_world_size() > 1 and not is_dist_ready():
+        backend = backend or ("nccl" if use_cuda else "gloo")
+        kwargs = dict(backend=backend, init_method="env://",
+                      timeout=datetime.timedelta(seconds=timeout_s))
+        if backend == "nccl":
+            kwargs["device_id"] = device  # eager RCCL communicator creation
+        dist.init_process_group(**kwargs)
+        synchronize()
+    return device
+
+
+def cleanup():
+    if is_dist_ready():
+        dist.destroy_process_group()
+
+
+def broadcast_object(obj: Any, src: int = 0) -> Any:
+    """Broadcast a picklable object from ``src`` to every rank."""
+    if not is_dist_ready() or get_world_size() == 1:
+        return obj
+    lst = [obj if get_rank() == src else None]
+    dist.broadcast_object_list(lst, src=src)
+    return lst[0]
+
+
+def all_gather(data: Any) -> List[Any]:
+    """All-gather arbitrary picklable data; returns a list (one entry per rank).
+
+    Same contract as the reference ``utils/dist.py:34-74``. Tensors inside
+    ``data`` are moved to CPU before pickling so the receiver never
+    materialises them on the sender's device.
+    """
+    world_size = get_world_size()
+    if world_size == 1:
+        return [data]
+    data = _to_cpu(data)
+    out: List[Any] = [None] * world_size
+    dist.all_gather_object(out, data)
+    return out
+
+
+def _to_cpu(obj):
+    if isinstance(obj, torch.Tensor):
+        return obj.detach().cpu()
+    if isinstance(obj, (list, tuple)):
+        return type(obj)(_to_cpu(o) for o in obj)
+    if isinstance(obj, dict):
+        return {k: _to_cpu(v) for k, v in obj.items()}
+    return obj
+
+
+def gather_tensors(t: torch.Tensor, dst: Optional[int] = 0) -> Optional[List[torch.Tensor]]:
+    """Gather variable-length (dim 0) tensors from every rank without pickling.
+
+    Two collectives: an all-gather of the lengths, then an all-gather of the
+    payload padded to the max length (fixed shape, runs on RCCL for device
+    tensors). Returns the list on ``dst`` (or on every rank if ``dst`` is
+    None) and None elsewhere.
+    """
+    world_size = get_world_size()
+    if world_size == 1:
+        return [t]
+    n = torch.tensor([t.shape[0]], dtype=torch.long, device=t.device)
+    sizes = [torch.zeros_like(n) for _ in range(world_size)]
+    dist.all_gather(sizes, n)
+    sizes = [int(s.item()) for s in sizes]
+    maxn = max(sizes)
+    if t.shape[0] < maxn:
+        pad = t.new_zeros((maxn - t.shape[0],) + tuple(t.shape[1:]))
+        t = torch.cat([t, pad], 0)
+    bufs = [torch.empty_like(t) for _ in range(world_size)]
+    dist.all_gather(bufs, t.contiguous())
+    if dst is not None and get_rank() != dst:
+        return None
+    return [b[:s] for b, s in zip(bufs, sizes)]
+
+
+def reduce_loss(loss: torch.Tensor) -> torch.Tensor:
+    """SUM-reduce a scalar to rank 0 and divide by world size there
+    (reference ``base/base_trainer.py:165-174``); stays on device."""
+    world_size = get_world_size()
+    if world_size < 2:
+        return loss.detach()
+    with torch.no_grad():
+        all_loss = loss.detach().clone()
+        dist.reduce(all_loss, dst=0)
+        if get_rank() == 0:
+            all_loss /= world_size
+    return all_loss
+
+
+def all_reduce_mean(t: torch.Tensor) -> torch.Tensor:
+    if get_world_size() < 2:
+        return t
+    t = t.clone()
+    dist.all_reduce(t)
+    t /= get_world_size()
+    return t

@@ -1,0 +1,241 @@
+"""Numerics of every HIP kernel against a plain PyTorch fp32 reference of the
+same op (inputs rounded to bf16 first, so only accumulation / output rounding
+differ). Run on an MI355X: ``pytest -m gpu tests/test_kernels_gpu.py``."""
+import pytest
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+from pytorch_distributed_template_amd.ops import native_ops as no  # noqa: E402
+
+
+def relerr(a, b):
+    a = a.float()
+    b = b.float()
+    return ((a - b).abs().max() / b.abs().max().clamp_min(1e-6)).item()
+
+
+def _cl(t):
+    return t.contiguous(memory_format=torch.channels_last)
+
+
+def setup_module(module):
+    assert no.available(), "native library must be built and loaded on GPU runs"
+    no.require()
+
+
+CONV_SHAPES = [
+    # N, Cin, H, W, Cout, k, s, p
+    (4, 64, 56, 56, 64, 1, 1, 0),
+    (4, 64, 56, 56, 64, 3, 1, 1),
+    (2, 128, 56, 56, 128, 3, 2, 1),
+    (2, 256, 56, 56, 512, 1, 2, 0),
+    (2, 512, 14, 14, 2048, 1, 1, 0),
+    (2, 256, 14, 14, 256, 3, 1, 1),
+    (2, 3, 224, 224, 64, 7, 2, 3),
+    (3, 24, 10, 12, 40, 3, 1, 1),
+]
+
+
+@pytest.mark.parametrize("shape", CONV_SHAPES)
+def test_conv_fwd_dgrad_wgrad(shape):
+    torch.manual_seed(0)
+    N, Cin, H, W, Cout, k, s, p = shape
+    dev = "cuda"
+    conv = nn.Conv2d(Cin, Cout, k, s, p, bias=False).to(dev)
+    x = _cl(torch.randn(N, Cin, H, W, device=dev).to(torch.bfloat16))
+    w32 = _cl(conv.weight.detach().float())
+    Cs = Cin if Cin % 8 == 0 else 8
+    xs = x
+    if Cs != Cin:
+        xs = _cl(F.pad(x.permute(0, 2, 3, 1), (0, Cs - Cin)).permute(0, 3, 1, 2))
+    g = no._fwd_geom(N, H, W, Cs, conv)
+    wb = no.bf16_weight(conv.weight, pad_cin_to=Cs if Cs != Cin else None)
+    R = no.conv_stat_rows(N * g["Ho"] * g["Wo"], Cout)
+    part = torch.empty(2 * R * Cout, device=dev)
+    y, M = no._conv_forward(xs, wb, N, H, W, Cs, Cout, g, stats=part)
+    wr = conv.weight.detach().to(torch.bfloat16).float()
+    ref = F.conv2d(x.float(), wr, None, s, p)
+    assert relerr(y, ref) < 1e-2
+    # BN partial statistics from the epilogue
+    ps = part.view(2, R, Cout).sum(1)
+    rs = ref.sum((0, 2, 3))
+    rq = (ref * ref).sum((0, 2, 3))
+    assert relerr(ps[0], rs) < 1e-3 + 1e-2 * 0
+    assert relerr(ps[1], rq) < 1e-3
+    # dgrad / wgrad
+    dy = _cl(torch.randn_like(ref).to(torch.bfloat16))
+    if Cin % 8 == 0:
+        dx = no._conv_dgrad(dy, w32, N, H, W, Cs, Cout, g)
+        rdx = torch.nn.grad.conv2d_input(x.shape, wr, dy.float(), s, p)
+        assert relerr(dx, rdx) < 1e-2
+    dw = torch.empty((Cout, Cs, k, k), device=dev, memory_format=torch.channels_last)
+    no._conv_wgrad(dy, xs, N, H, W, Cs, Cout, g, dw)
+    rdw = torch.nn.grad.conv2d_weight(x.float(), wr.shape, dy.float(), s, p)
+    assert relerr(dw[:, :Cin], rdw) < 1e-2
+
+
+@pytest.mark.parametrize("relu,res", [(True, False), (True, True), (False, False)])
+def test_conv_bn_act_autograd(relu, res):
+    torch.manual_seed(1)
+    dev = "cuda"
+    N, C, H, W, Co = 4, 64, 28, 28, 128
+    conv = nn.Conv2d(C, Co, 3, 1, 1, bias=False).to(dev).to(memory_format=torch.channels_last)
+    bn = nn.BatchNorm2d(Co).to(dev)
+    with torch.no_grad():
+        bn.weight.uniform_(0.5, 1.5)
+        bn.bias.uniform_(-0.5, 0.5)
+    conv_r = nn.Conv2d(C, Co, 3, 1, 1, bias=False).to(dev)
+    bn_r = nn.BatchNorm2d(Co).to(dev)
+    conv_r.load_state_dict(conv.state_dict())
+    bn_r.load_state_dict(bn.state_dict())
+    with torch.no_grad():
+        conv_r.weight.copy_(conv.weight.to(torch.bfloat16).float())
+    x = _cl(torch.randn(N, C, H, W, device=dev).to(torch.bfloat16)).requires_grad_(True)
+    r = _cl(torch.randn(N, Co, H, W, device=dev).to(torch.bfloat16)).requires_grad_(True) if res else None
+    out = no.conv_bn_act(x, conv, bn, r, relu)
+    xr = x.detach().float().requires_grad_(True)
+    rr = r.detach().float().requires_grad_(True) if res else None
+    ref = bn_r(conv_r(xr))
+    if res:
+        ref = ref + rr
+    if relu:
+        ref = F.relu(ref)
+    assert relerr(out, ref) < 2e-2
+    assert relerr(bn.running_mean, bn_r.running_mean) < 1e-2
+    assert relerr(bn.running_var, bn_r.running_var) < 1e-2
+    go = torch.randn_like(ref)
+    out.backward(go.to(torch.bfloat16))
+    ref.backward(go.to(torch.bfloat16).float())
+    assert relerr(x.grad, xr.grad) < 3e-2
+    assert relerr(conv.weight.grad, conv_r.weight.grad) < 3e-2
+    assert relerr(bn.weight.grad, bn_r.weight.grad) < 3e-2
+    assert relerr(bn.bias.grad, bn_r.bias.grad) < 3e-2
+    if res:
+        assert relerr(r.grad, rr.grad) < 3e-2
+
+
+def test_maxpool_avgpool():
+    torch.manual_seed(2)
+    x = _cl(torch.randn(4, 64, 112, 112, device="cuda").to(torch.bfloat16)).requires_grad_(True)
+    y = no.max_pool2d(x, 3, 2, 1)
+    xr = x.detach().float().requires_grad_(True)
+    yr = F.max_pool2d(xr, 3, 2, 1)
+    assert relerr(y, yr) == 0.0
+    g = torch.randn_like(yr)
+    y.backward(g.to(torch.bfloat16))
+    yr.backward(g.to(torch.bfloat16).float())
+    assert relerr(x.grad, xr.grad) < 1e-2
+    z = _cl(torch.randn(8, 2048, 7, 7, device="cuda").to(torch.bfloat16)).requires_grad_(True)
+    a = no.global_avg_pool(z)
+    zr = z.detach().float().requires_grad_(True)
+    ar = zr.mean((2, 3))
+    assert relerr(a, ar) < 1e-2
+    g = torch.randn_like(ar)
+    a.backward(g.to(torch.bfloat16))
+    ar.backward(g.to(torch.bfloat16).float())
+    assert relerr(z.grad, zr.grad) < 1e-2
+
+
+def test_linear_and_xent():
+    torch.manual_seed(3)
+    fc = nn.Linear(2048, 1000).cuda()
+    x = torch.randn(64, 2048, device="cuda").to(torch.bfloat16).requires_grad_(True)
+    t = torch.randint(0, 1000, (64,), device="cuda")
+    logits = no.linear(x, fc)
+    loss = no.softmax_cross_entropy(logits, t)
+    fcr = nn.Linear(2048, 1000).cuda()
+    fcr.load_state_dict(fc.state_dict())
+    with torch.no_grad():
+        fcr.weight.copy_(fc.weight.to(torch.bfloat16).float())
+    xr = x.detach().float().requires_grad_(True)
+    lr = fcr(xr)
+    assert relerr(logits, lr) < 1e-2
+    lossr = F.cross_entropy(lr, t)
+    assert abs(loss.item() - lossr.item()) < 2e-2
+    loss.backward()
+    lossr.backward()
+    assert relerr(x.grad, xr.grad) < 3e-2
+    assert relerr(fc.weight.grad, fcr.weight.grad) < 3e-2
+    assert relerr(fc.bias.grad, fcr.bias.grad) < 3e-2
+
+
+def test_xent_label_smoothing_fp32():
+    torch.manual_seed(4)
+    lg = torch.randn(33, 1000, device="cuda").requires_grad_(True)
+    t = torch.randint(0, 1000, (33,), device="cuda")
+    l1 = no.softmax_cross_entropy(lg, t, 0.1)
+    lr = lg.detach().clone().requires_grad_(True)
+    l2 = F.cross_entropy(lr, t, label_smoothing=0.1)
+    assert abs(l1.item() - l2.item()) < 1e-4
+    l1.backward()
+    l2.backward()
+    assert relerr(lg.grad, lr.grad) < 1e-2
+
+
+@pytest.mark.parametrize("opt", ["sgd", "sgd_nesterov", "adam_amsgrad", "adamw"])
+def test_fused_optimizers_match_torch(opt):
+    from pytorch_distributed_template_amd.optim import FusedSGD, FusedAdam, FusedAdamW
+    torch.manual_seed(5)
+    shapes = [(64, 3, 7, 7), (1000, 2048), (1000,), (10,), (3,)]
+    ps = [torch.randn(s, device="cuda") for s in shapes]
+    qs = [p.clone() for p in ps]
+    for p in ps + qs:
+        p.requires_grad_(True)
+    if opt == "sgd":
+        a, b = FusedSGD(ps, lr=0.1, momentum=0.9, weight_decay=1e-4), torch.optim.SGD(qs, lr=0.1, momentum=0.9,
+                                                                                       weight_decay=1e-4)
+    elif opt == "sgd_nesterov":
+        a = FusedSGD(ps, lr=0.05, momentum=0.9, nesterov=True)
+        b = torch.optim.SGD(qs, lr=0.05, momentum=0.9, nesterov=True)
+    elif opt == "adam_amsgrad":
+        a, b = FusedAdam(ps, lr=1e-3, amsgrad=True, weight_decay=1e-2), torch.optim.Adam(qs, lr=1e-3, amsgrad=True,
+                                                                                          weight_decay=1e-2)
+    else:
+        a, b = FusedAdamW(ps, lr=1e-3, weight_decay=0.05), torch.optim.AdamW(qs, lr=1e-3, weight_decay=0.05)
+    for step in range(4):
+        for p, q in zip(ps, qs):
+            g = torch.randn_like(p)
+            p.grad = g.clone()
+            q.grad = g.clone()
+        a.step()
+        b.step()
+    for p, q in zip(ps, qs):
+        assert torch.allclose(p, q, rtol=1e-5, atol=1e-6), (p - q).abs().max()
+    # state_dict is interchangeable with torch's
+    b.load_state_dict(a.state_dict())
+
+
+def test_synthetic_fill_deterministic():
+    a = torch.empty(1024, device="cuda", dtype=torch.bfloat16)
+    b = torch.empty(1024, device="cuda", dtype=torch.bfloat16)
+    no.fill_uniform_(a, 7)
+    no.fill_uniform_(b, 7)
+    assert torch.equal(a, b)
+    assert a.float().abs().max() <= 1.0 and a.float().std() > 0.4
+
+
+def test_resnet50_native_matches_torch_small_batch():
+    from pytorch_distributed_template_amd.models import resnet50
+    from pytorch_distributed_template_amd.ops import fused
+    torch.manual_seed(6)
+    m = resnet50(num_classes=1000).cuda().to(memory_format=torch.channels_last)
+    x = _cl(torch.randn(8, 3, 224, 224, device="cuda").to(torch.bfloat16))
+    t = torch.randint(0, 1000, (8,), device="cuda")
+    fused.set_backend("native")
+    out = m(x)
+    loss = fused.softmax_cross_entropy(out, t)
+    loss.backward()
+    g_native = m.conv1.weight.grad.clone()
+    m.zero_grad()
+    fused.set_backend("torch")
+    with torch.autocast("cuda", dtype=torch.bfloat16):
+        out_r = m(x)
+        loss_r = F.cross_entropy(out_r.float(), t)
+    loss_r.backward()
+    fused.set_backend("auto")
+    assert torch.isfinite(loss) and abs(loss.item() - loss_r.item()) < 0.05 * abs(loss_r.item()) + 0.05
+    cos = F.cosine_similarity(g_native.flatten(), m.conv1.weight.grad.flatten(), dim=0)
+    assert cos > 0.9, cos
