@@ -85,6 +85,31 @@ __global__ void __launch_bounds__(NT) bn_stats_kernel(const u16* __restrict__ y,
   }
 }
 
+// Parallel first stage of the partial-row reduction: [2][R][C] -> [2][G][C].
+// grid (ceil(C/64), G); 256 threads = 64 channels x 4 row groups; each thread
+// sums rows y*4+rg, y*4+rg + 4G, ... in fp32, then the 4 row groups combine in LDS.
+__global__ void __launch_bounds__(256) rows_reduce_kernel(const float* __restrict__ part, float* __restrict__ out,
+                                                          int R, int C, int G) {
+  __shared__ float red[2][4][64];
+  const int t = threadIdx.x, cl = t & 63, rg = t >> 6;
+  const int c = blockIdx.x * 64 + cl;
+  const int g = blockIdx.y;
+  float s = 0.f, q = 0.f;
+  if (c < C) {
+    for (int r = g * 4 + rg; r < R; r += 4 * G) {
+      s += part[(long)r * C + c];
+      q += part[(long)(R + r) * C + c];
+    }
+  }
+  red[0][rg][cl] = s;
+  red[1][rg][cl] = q;
+  __syncthreads();
+  if (rg == 0 && c < C) {
+    out[(long)g * C + c] = red[0][0][cl] + red[0][1][cl] + red[0][2][cl] + red[0][3][cl];
+    out[(long)(G + g) * C + c] = red[1][0][cl] + red[1][1][cl] + red[1][2][cl] + red[1][3][cl];
+  }
+}
+
 // one thread per channel: combine R partial rows in fp64.
 // outputs: mean, invstd (saved for backward), scale = gamma*invstd, shift = beta - mean*scale,
 // running stats updated in place (unbiased variance), if running_mean != null.
@@ -303,9 +328,26 @@ PDT_API int pdt_bn_stats(const void* y, float* part, long M, int C, int blocks, 
   PDT_RETURN_LAUNCH();
 }
 
+// Number of floats of extra workspace the finalize calls need after the
+// [2][R][C] partial block (stage-1 output of the parallel row reduction).
+PDT_API long pdt_rows_reduce_workspace(int R, int C) {
+  int G = R > 256 ? 64 : 0;
+  return G ? 2L * G * C : 0;
+}
+
+static const float* rows_reduce(const float* part, int* R, int C, hipStream_t st) {
+  if (*R <= 256) return part;
+  const int G = 64;
+  float* out = const_cast<float*>(part) + 2L * (*R) * C;  // workspace tail
+  hipLaunchKernelGGL(rows_reduce_kernel, dim3((C + 63) / 64, G), dim3(256), 0, st, part, out, *R, C, G);
+  *R = G;
+  return out;
+}
+
 PDT_API int pdt_bn_finalize(const float* part, int R, int C, double count, float eps, float momentum,
                             const float* gamma, const float* beta, float* mean, float* invstd, float* scale,
                             float* shift, float* running_mean, float* running_var, hipStream_t st) {
+  part = rows_reduce(part, &R, C, st);
   hipLaunchKernelGGL(bn_finalize_kernel, dim3((C + 255) / 256), dim3(256), 0, st, part, R, C, count, eps, momentum,
                      gamma, beta, mean, invstd, scale, shift, running_mean, running_var);
   PDT_RETURN_LAUNCH();
@@ -347,6 +389,7 @@ PDT_API int pdt_bn_bwd_reduce(const void* dA, const void* y, const void* act, co
 PDT_API int pdt_bn_bwd_finalize(const float* part, int R, int C, double count, const float* gamma,
                                 const float* mean, const float* invstd, float* dgamma, float* dbeta, float* k1,
                                 float* k2, float* k3, int accumulate, hipStream_t st) {
+  part = rows_reduce(part, &R, C, st);
   hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + 255) / 256), dim3(256), 0, st, part, R, C, count, gamma,
                      mean, invstd, dgamma, dbeta, k1, k2, k3, accumulate);
   PDT_RETURN_LAUNCH();

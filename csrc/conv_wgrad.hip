@@ -37,7 +37,6 @@ struct WGParams {
 
 constexpr int BK = 64;
 constexpr int NT = 256;
-constexpr int BN = 128;
 
 template <int RB>
 __device__ __forceinline__ int seg_swz(int row) {
@@ -71,7 +70,7 @@ __device__ __forceinline__ bf16x8 tr_frag(const char* base, int krow0, int col0,
   return r;
 }
 
-template <int BM>
+template <int BM, int BN>
 __global__ void __launch_bounds__(NT, 2) wgrad_kernel(WGParams p) {
   constexpr int RBA = BM * 2;   // bytes per A row (co)
   constexpr int RBB = BN * 2;   // bytes per B row (tap,c)
@@ -204,19 +203,30 @@ __global__ void __launch_bounds__(NT, 2) wgrad_kernel(WGParams p) {
   }
 }
 
-// out[i] = (accumulate ? out[i] : 0) + scale * sum_s slab[s][i]
-__global__ void wgrad_reduce_kernel(const float* __restrict__ slab, float* __restrict__ out, long n4,
-                                    int splits, long stride4, float scale, int accumulate) {
+// Two-stage deterministic slab reduction.
+// stage 1: grid (ceil(n4/256), G): block (x, g) sums slabs g, g+G, g+2G, ... for
+//          256 float4 columns -> part[g][n4]   (G = 1 writes the output directly)
+// stage 2: out = (accumulate ? out : 0) + scale * sum_g part[g]
+__global__ void wgrad_reduce1_kernel(const float* __restrict__ slab, float* __restrict__ dst, long n4, int splits,
+                                     int G, float scale, int accumulate, int final_stage) {
   long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
-  for (; i < n4; i += (long)gridDim.x * blockDim.x) {
-    const f32x4* s = reinterpret_cast<const f32x4*>(slab) + i;
-    f32x4 a = s[0];
-    for (int k = 1; k < splits; ++k) a += s[(long)k * stride4];
-    a *= scale;
-    f32x4* o = reinterpret_cast<f32x4*>(out) + i;
-    if (accumulate) a += *o;
-    *o = a;
+  if (i >= n4) return;
+  const int g = blockIdx.y;
+  const f32x4* s = reinterpret_cast<const f32x4*>(slab) + i;
+  f32x4 a = {0.f, 0.f, 0.f, 0.f}, b = {0.f, 0.f, 0.f, 0.f};
+  int k = g;
+  for (; k + G < splits; k += 2 * G) {
+    a += s[(long)k * n4];
+    b += s[(long)(k + G) * n4];
   }
+  if (k < splits) a += s[(long)k * n4];
+  a += b;
+  f32x4* o = reinterpret_cast<f32x4*>(dst) + (final_stage ? i : (long)g * n4 + i);
+  if (final_stage) {
+    a *= scale;
+    if (accumulate) a += *o;
+  }
+  *o = a;
 }
 
 }  // namespace
@@ -225,6 +235,7 @@ __global__ void wgrad_reduce_kernel(const float* __restrict__ slab, float* __res
 // (~4 workgroups per CU); returns splits and writes ktiles_per_split.
 PDT_API int pdt_wgrad_plan(int M, int Mo, int No, int* ktiles_per_split) {
   int BM = Mo <= 64 ? 64 : 128;
+  int BN = No <= 64 ? 64 : 128;
   int tiles = ((Mo + BM - 1) / BM) * ((No + BN - 1) / BN);
   int nk = (M + BK - 1) / BK;
   int target = 1024;
@@ -237,6 +248,16 @@ PDT_API int pdt_wgrad_plan(int M, int Mo, int No, int* ktiles_per_split) {
   splits = (nk + kps - 1) / kps;
   *ktiles_per_split = kps;
   return splits;
+}
+
+// floats of workspace pdt_conv_wgrad needs for `splits` slabs (slabs + stage-1 partials)
+PDT_API long pdt_wgrad_workspace(int splits, int Mo, int No) {
+  long n4 = (long)Mo * No / 4;
+  int xb = (int)((n4 + 255) / 256);
+  long G = splits < 2 ? 1 : 1024 / xb;
+  if (G > splits / 4) G = splits / 4;
+  if (G < 1) G = 1;
+  return (long)splits * Mo * No + (G > 1 ? G * Mo * No : 0);
 }
 
 PDT_API int pdt_conv_wgrad(const void* dy, const void* x, float* slab, float* out, int M, int Mo, int No,
@@ -257,20 +278,36 @@ PDT_API int pdt_conv_wgrad(const void* dy, const void* x, float* slab, float* ou
   p.div_C = make_fastdiv(C);
   p.div_ntw = make_fastdiv(ntw);
   int BM = Mo <= 64 ? 64 : 128;
+  int BN = No <= 64 ? 64 : 128;
   int tiles = ((Mo + BM - 1) / BM) * ((No + BN - 1) / BN);
   dim3 grid(tiles * splits);
-  if (BM == 64)
-    hipLaunchKernelGGL(wgrad_kernel<64>, grid, dim3(NT), 0, stream, p);
+  if (BM == 64 && BN == 64)
+    hipLaunchKernelGGL((wgrad_kernel<64, 64>), grid, dim3(NT), 0, stream, p);
+  else if (BM == 64)
+    hipLaunchKernelGGL((wgrad_kernel<64, 128>), grid, dim3(NT), 0, stream, p);
+  else if (BN == 64)
+    hipLaunchKernelGGL((wgrad_kernel<128, 64>), grid, dim3(NT), 0, stream, p);
   else
-    hipLaunchKernelGGL(wgrad_kernel<128>, grid, dim3(NT), 0, stream, p);
+    hipLaunchKernelGGL((wgrad_kernel<128, 128>), grid, dim3(NT), 0, stream, p);
   int e = (int)hipGetLastError();
   if (e) return e;
-  long n = (long)Mo * No;
-  long n4 = n / 4;
-  int blocks = (int)((n4 + 255) / 256);
-  if (blocks > 2048) blocks = 2048;
-  if (blocks < 1) blocks = 1;
-  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(blocks), dim3(256), 0, stream, slab, out, n4, splits, n4, scale,
-                     accumulate);
+  long n4 = (long)Mo * No / 4;
+  int xb = (int)((n4 + 255) / 256);
+  // enough (column-block x slab-group) blocks to stream the slabs at full rate
+  int G = splits < 2 ? 1 : (int)(1024 / xb);
+  if (G > splits / 4) G = splits / 4;
+  if (G < 1) G = 1;
+  if (G == 1) {
+    hipLaunchKernelGGL(wgrad_reduce1_kernel, dim3(xb, 1), dim3(256), 0, stream, slab, out, n4, splits, 1, scale,
+                       accumulate, 1);
+  } else {
+    // stage-1 partials reuse the head of the slab buffer region past the live slabs? no: use slab[0..G) rows
+    // in place is unsafe (read while written), so partials go to the tail workspace provided by the caller.
+    float* part = slab + (long)splits * Mo * No;
+    hipLaunchKernelGGL(wgrad_reduce1_kernel, dim3(xb, G), dim3(256), 0, stream, slab, part, n4, splits, G, 1.f, 0,
+                       0);
+    hipLaunchKernelGGL(wgrad_reduce1_kernel, dim3(xb, 1), dim3(256), 0, stream, part, out, n4, G, 1, scale,
+                       accumulate, 1);
+  }
   PDT_RETURN_LAUNCH();
 }

@@ -31,8 +31,10 @@ _SIGS = {
     "pdt_conv_nt_stat_rows": (c_int, [c_int, c_int]),
     "pdt_conv_nt": (c_int, [P, P, P, P, P] + [c_int] * 25 + [P]),
     "pdt_wgrad_plan": (c_int, [c_int, c_int, c_int, ctypes.POINTER(c_int)]),
+    "pdt_wgrad_workspace": (c_long, [c_int, c_int, c_int]),
     "pdt_conv_wgrad": (c_int, [P, P, P, P] + [c_int] * 16 + [c_int, c_int, c_float, c_int, P]),
     "pdt_bn_stats_blocks": (c_int, [c_long, c_int]),
+    "pdt_rows_reduce_workspace": (c_long, [c_int, c_int]),
     "pdt_bn_stats": (c_int, [P, P, c_long, c_int, c_int, P]),
     "pdt_bn_finalize": (c_int, [P, c_int, c_int, c_double, c_float, c_float] + [P] * 8 + [P]),
     "pdt_bn_apply": (c_int, [P, P, P, P, P, c_long, c_int, c_int, P]),
@@ -179,7 +181,7 @@ def conv_wgrad(dy, x, out, *, M, Mo, No, ldy, Hs, Ws, C, Hm, Wm, sh, sw, oh0, ow
     lib = _load()
     kps = c_int(0)
     splits = lib.pdt_wgrad_plan(M, Mo, No, ctypes.byref(kps))
-    slab = torch.empty(splits * Mo * No, dtype=torch.float32, device=dy.device)
+    slab = torch.empty(lib.pdt_wgrad_workspace(splits, Mo, No), dtype=torch.float32, device=dy.device)
     rc = lib.pdt_conv_wgrad(_p(dy), _p(x), _p(slab), _p(out), M, Mo, No, ldy, Hs, Ws, C, Hm, Wm, sh, sw, oh0,
                             ow0, dh, dw, ntw, splits, kps.value, float(scale), int(accumulate), _s())
     _chk(rc, "conv_wgrad")
@@ -290,7 +292,7 @@ class _ConvBNAct(torch.autograd.Function):
         M = N * g["Ho"] * g["Wo"]
         if training:
             R = conv_stat_rows(M, Cout)
-            part = torch.empty(2 * R * Cout, **f32)
+            part = torch.empty(2 * R * Cout + lib.pdt_rows_reduce_workspace(R, Cout), **f32)
             y, _ = _conv_forward(x, wb, N, H, W, Cs, Cout, g, stats=part)
             mean = torch.empty(Cout, **f32)
             invstd = torch.empty(Cout, **f32)
@@ -329,7 +331,7 @@ class _ConvBNAct(torch.autograd.Function):
         dev = dA.device
         f32 = dict(dtype=torch.float32, device=dev)
         blocks = lib.pdt_bn_stats_blocks(M, Cout)
-        part = torch.empty(2 * blocks * Cout, **f32)
+        part = torch.empty(2 * blocks * Cout + lib.pdt_rows_reduce_workspace(blocks, Cout), **f32)
         _chk(lib.pdt_bn_bwd_reduce(_p(dA), _p(y), _p(act), _p(mean), _p(scale), _p(shift), _p(part), M, Cout,
                                    int(relu), blocks, st), "bn_bwd_reduce")
         dgamma = torch.empty(Cout, **f32)
