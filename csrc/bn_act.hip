@@ -110,21 +110,40 @@ __global__ void __launch_bounds__(256) rows_reduce_kernel(const float* __restric
   }
 }
 
-// one thread per channel: combine R partial rows in fp64.
-// outputs: mean, invstd (saved for backward), scale = gamma*invstd, shift = beta - mean*scale,
-// running stats updated in place (unbiased variance), if running_mean != null.
-__global__ void bn_finalize_kernel(const float* __restrict__ part, int R, int C, double count, float eps,
-                                   float momentum, const float* __restrict__ gamma, const float* __restrict__ beta,
-                                   float* __restrict__ mean_out, float* __restrict__ invstd_out,
-                                   float* __restrict__ scale, float* __restrict__ shift,
-                                   float* __restrict__ running_mean, float* __restrict__ running_var) {
-  int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= C) return;
-  double s = 0, q = 0;
-  for (int r = 0; r < R; ++r) {
-    s += part[(long)r * C + c];
-    q += part[(long)(R + r) * C + c];
+// Block-parallel finalize: 256 threads = 64 channels x 4 row groups; rows are
+// summed in fp64 and combined through LDS (R <= 256 after rows_reduce).
+__device__ __forceinline__ void sum_rows64(const float* __restrict__ part, int R, int C, int c, int rg,
+                                           double* sh_s, double* sh_q, double& s, double& q) {
+  const int cl = threadIdx.x & 63;
+  double a = 0, b = 0;
+  if (c < C) {
+    for (int r = rg; r < R; r += 4) {
+      a += part[(long)r * C + c];
+      b += part[(long)(R + r) * C + c];
+    }
   }
+  sh_s[rg * 64 + cl] = a;
+  sh_q[rg * 64 + cl] = b;
+  __syncthreads();
+  s = sh_s[cl] + sh_s[64 + cl] + sh_s[128 + cl] + sh_s[192 + cl];
+  q = sh_q[cl] + sh_q[64 + cl] + sh_q[128 + cl] + sh_q[192 + cl];
+}
+
+// outputs: mean, invstd (saved for backward), scale = gamma*invstd, shift = beta - mean*scale,
+// running stats updated in place (unbiased variance) and num_batches_tracked += 1.
+__global__ void __launch_bounds__(256) bn_finalize_kernel(const float* __restrict__ part, int R, int C,
+                                                          double count, float eps, float momentum,
+                                                          const float* __restrict__ gamma,
+                                                          const float* __restrict__ beta, float* __restrict__ mean_out,
+                                                          float* __restrict__ invstd_out, float* __restrict__ scale,
+                                                          float* __restrict__ shift, float* __restrict__ running_mean,
+                                                          float* __restrict__ running_var, long* __restrict__ nbt) {
+  __shared__ double sh_s[256], sh_q[256];
+  const int c = blockIdx.x * 64 + (threadIdx.x & 63), rg = threadIdx.x >> 6;
+  double s, q;
+  sum_rows64(part, R, C, c, rg, sh_s, sh_q, s, q);
+  if (blockIdx.x == 0 && threadIdx.x == 0 && nbt) nbt[0] += 1;
+  if (rg != 0 || c >= C) return;
   double mean = s / count;
   double var = q / count - mean * mean;
   if (var < 0) var = 0;
@@ -241,18 +260,18 @@ __global__ void __launch_bounds__(NT) bn_bwd_reduce_kernel(const u16* __restrict
 
 // dgamma = sum(dz*(y-mean))*invstd, dbeta = sum(dz)
 // dy = k1*dz + k2*y + k3
-__global__ void bn_bwd_finalize_kernel(const float* __restrict__ part, int R, int C, double count,
-                                       const float* __restrict__ gamma, const float* __restrict__ mean,
-                                       const float* __restrict__ invstd, float* __restrict__ dgamma,
-                                       float* __restrict__ dbeta, float* __restrict__ k1, float* __restrict__ k2,
-                                       float* __restrict__ k3, int accumulate) {
-  int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= C) return;
-  double s = 0, q = 0;
-  for (int r = 0; r < R; ++r) {
-    s += part[(long)r * C + c];
-    q += part[(long)(R + r) * C + c];
-  }
+__global__ void __launch_bounds__(256) bn_bwd_finalize_kernel(const float* __restrict__ part, int R, int C,
+                                                              double count, const float* __restrict__ gamma,
+                                                              const float* __restrict__ mean,
+                                                              const float* __restrict__ invstd,
+                                                              float* __restrict__ dgamma, float* __restrict__ dbeta,
+                                                              float* __restrict__ k1, float* __restrict__ k2,
+                                                              float* __restrict__ k3, int accumulate) {
+  __shared__ double sh_s[256], sh_q[256];
+  const int c = blockIdx.x * 64 + (threadIdx.x & 63), rg = threadIdx.x >> 6;
+  double s, q;
+  sum_rows64(part, R, C, c, rg, sh_s, sh_q, s, q);
+  if (rg != 0 || c >= C) return;
   double is = invstd[c], g = gamma ? gamma[c] : 1.0, mu = mean[c];
   double dg = q * is, db = s;
   if (dgamma) dgamma[c] = (float)(accumulate ? dgamma[c] + dg : dg);
@@ -346,10 +365,11 @@ static const float* rows_reduce(const float* part, int* R, int C, hipStream_t st
 
 PDT_API int pdt_bn_finalize(const float* part, int R, int C, double count, float eps, float momentum,
                             const float* gamma, const float* beta, float* mean, float* invstd, float* scale,
-                            float* shift, float* running_mean, float* running_var, hipStream_t st) {
+                            float* shift, float* running_mean, float* running_var, long* num_batches_tracked,
+                            hipStream_t st) {
   part = rows_reduce(part, &R, C, st);
-  hipLaunchKernelGGL(bn_finalize_kernel, dim3((C + 255) / 256), dim3(256), 0, st, part, R, C, count, eps, momentum,
-                     gamma, beta, mean, invstd, scale, shift, running_mean, running_var);
+  hipLaunchKernelGGL(bn_finalize_kernel, dim3((C + 63) / 64), dim3(256), 0, st, part, R, C, count, eps, momentum,
+                     gamma, beta, mean, invstd, scale, shift, running_mean, running_var, num_batches_tracked);
   PDT_RETURN_LAUNCH();
 }
 
@@ -390,7 +410,7 @@ PDT_API int pdt_bn_bwd_finalize(const float* part, int R, int C, double count, c
                                 const float* mean, const float* invstd, float* dgamma, float* dbeta, float* k1,
                                 float* k2, float* k3, int accumulate, hipStream_t st) {
   part = rows_reduce(part, &R, C, st);
-  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + 255) / 256), dim3(256), 0, st, part, R, C, count, gamma,
+  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + 63) / 64), dim3(256), 0, st, part, R, C, count, gamma,
                      mean, invstd, dgamma, dbeta, k1, k2, k3, accumulate);
   PDT_RETURN_LAUNCH();
 }

@@ -36,7 +36,7 @@ _SIGS = {
     "pdt_bn_stats_blocks": (c_int, [c_long, c_int]),
     "pdt_rows_reduce_workspace": (c_long, [c_int, c_int]),
     "pdt_bn_stats": (c_int, [P, P, c_long, c_int, c_int, P]),
-    "pdt_bn_finalize": (c_int, [P, c_int, c_int, c_double, c_float, c_float] + [P] * 8 + [P]),
+    "pdt_bn_finalize": (c_int, [P, c_int, c_int, c_double, c_float, c_float] + [P] * 9 + [P]),
     "pdt_bn_apply": (c_int, [P, P, P, P, P, c_long, c_int, c_int, P]),
     "pdt_bn_bwd_reduce": (c_int, [P, P, P, P, P, P, P, c_long, c_int, c_int, c_int, P]),
     "pdt_bn_bwd_finalize": (c_int, [P, c_int, c_int, c_double] + [P] * 8 + [c_int, P]),
@@ -178,6 +178,8 @@ def conv_wgrad(dy, x, out, *, M, Mo, No, ldy, Hs, Ws, C, Hm, Wm, sh, sw, oh0, ow
     assert dy.dtype == torch.bfloat16 and x.dtype == torch.bfloat16 and out.dtype == torch.float32
     assert C % 8 == 0 and Mo % 8 == 0 and No % 8 == 0 and ldy % 8 == 0
     assert out.numel() >= Mo * No and dy.numel() >= M * ldy
+    assert M % (Hm * Wm) == 0 and x.numel() >= (M // (Hm * Wm)) * Hs * Ws * C, "wgrad source too small"
+    assert ntw >= 1 and No % C == 0
     lib = _load()
     kps = c_int(0)
     splits = lib.pdt_wgrad_plan(M, Mo, No, ctypes.byref(kps))
@@ -241,6 +243,8 @@ def _conv_forward(x, wb, N, H, W, Cs, Cout, g, stats=None):
 def _conv_dgrad(dy, w32, N, H, W, Cin, Cout, g):
     """dX [N,Cin,H,W] from dY [N,Cout,Ho,Wo] (stride phases, see csrc/conv_igemm.hip)."""
     KH, KW, s_h, s_w, ph, pw = g["KH"], g["KW"], g["sh"], g["sw"], g["ph"], g["pw"]
+    assert w32.shape[0] == Cout and w32.shape[1] == Cin, (tuple(w32.shape), Cout, Cin)
+    assert dy.shape[1] == Cout and dy.numel() == N * Cout * g["Ho"] * g["Wo"]
     dx = _empty_cl(N, Cin, H, W, torch.bfloat16, dy.device)
     lib = _load()
     w32c = _cl(w32.detach().float())
@@ -275,7 +279,8 @@ def _conv_wgrad(dy, x, N, H, W, Cs, Cout, g, out):
 # =============================================================================
 class _ConvBNAct(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, w, gamma, beta, residual, running_mean, running_var, conv, relu, training, momentum, eps):
+    def forward(ctx, x, w, gamma, beta, residual, running_mean, running_var, conv, relu, training, momentum, eps,
+                nbt):
         lib = _load()
         st = _s()
         N, C, H, W = x.shape
@@ -301,7 +306,8 @@ class _ConvBNAct(torch.autograd.Function):
             rm = running_mean if running_mean is not None else None
             rv = running_var if running_var is not None else None
             _chk(lib.pdt_bn_finalize(_p(part), R, Cout, float(M), float(eps), float(momentum), _p(gamma),
-                                     _p(beta), _p(mean), _p(invstd), _p(scale), _p(shift), _p(rm), _p(rv), st),
+                                     _p(beta), _p(mean), _p(invstd), _p(scale), _p(shift), _p(rm), _p(rv),
+                                     _p(nbt), st),
                  "bn_finalize")
         else:
             y, _ = _conv_forward(x, wb, N, H, W, Cs, Cout, g, stats=None)
@@ -309,6 +315,7 @@ class _ConvBNAct(torch.autograd.Function):
             mean = running_mean.float().clone()
             scale = (gamma.float() * invstd).contiguous()
             shift = (beta.float() - mean * scale).contiguous()
+        assert y.numel() == M * Cout
         res = None
         if residual is not None:
             res = _cl(residual)
@@ -347,7 +354,10 @@ class _ConvBNAct(torch.autograd.Function):
                                   _p(dres), M, Cout, int(relu), st), "bn_bwd_apply")
         dx = None
         if ctx.needs_input_grad[0]:
-            dx = _conv_dgrad(dy, w, N, H, W, Cs, Cout, g)
+            wd = w
+            if Cs != C:  # stem: dgrad against the channel-padded weight, then drop the pad
+                wd = torch.nn.functional.pad(w.detach().float(), (0, 0, 0, 0, 0, Cs - C))
+            dx = _conv_dgrad(dy, wd, N, H, W, Cs, Cout, g)
             if Cs != C:
                 dx = dx[:, :C]
         dw = None
@@ -363,7 +373,7 @@ class _ConvBNAct(torch.autograd.Function):
             if dw.dtype != w.dtype:
                 dw = dw.to(w.dtype)
         return (dx, dw, dgamma if ctx.needs_input_grad[2] else None, dbeta if ctx.needs_input_grad[3] else None,
-                dres, None, None, None, None, None, None, None)
+                dres, None, None, None, None, None, None, None, None)
 
 
 def conv_bn_act(x, conv: nn.Conv2d, bn: nn.BatchNorm2d, residual=None, relu=True):
@@ -374,12 +384,17 @@ def conv_bn_act(x, conv: nn.Conv2d, bn: nn.BatchNorm2d, residual=None, relu=True
     momentum = bn.momentum if bn.momentum is not None else 0.1
     rm = bn.running_mean if (bn.track_running_stats and bn.training) else None
     rv = bn.running_var if (bn.track_running_stats and bn.training) else None
+    nbt = None
     if bn.training and bn.track_running_stats and bn.num_batches_tracked is not None:
-        bn.num_batches_tracked.add_(1)
+        nbt = bn.num_batches_tracked  # incremented inside the finalize kernel
+        if bn.momentum is None:  # cumulative moving average needs the host-side count
+            nbt.add_(1)
+            momentum = 1.0 / float(nbt.item())
+            nbt = None
     if not training:
         rm, rv = bn.running_mean, bn.running_var
     return _ConvBNAct.apply(x, conv.weight, bn.weight, bn.bias, residual, rm, rv, conv, relu, training, momentum,
-                            bn.eps)
+                            bn.eps, nbt)
 
 
 # =============================================================================
