@@ -51,7 +51,7 @@ constexpr int NT = 256;
 
 __device__ __forceinline__ int swz(int row, int chunk) { return chunk ^ ((row >> 1) & 7); }
 
-template <int BM, int BN, bool CS64>
+template <int BM, int BN, int NSTAGE, bool CS64>
 __global__ void __launch_bounds__(NT, 2) conv_nt_kernel(NTParams p) {
   constexpr int MI = BM / 32;  // 16-row MFMA tiles per wave (wave covers BM/2 rows)
   constexpr int NI = BN / 32;
@@ -59,7 +59,7 @@ __global__ void __launch_bounds__(NT, 2) conv_nt_kernel(NTParams p) {
   constexpr int B_BYTES = BN * BK * 2;
   constexpr int STAGE = A_BYTES + B_BYTES;
   constexpr int C_STRIDE = BN * 2 + 16;  // bytes per staged output row
-  constexpr int SMEM = (2 * STAGE > BM * C_STRIDE) ? 2 * STAGE : BM * C_STRIDE;
+  constexpr int SMEM = (NSTAGE * STAGE > BM * C_STRIDE) ? NSTAGE * STAGE : BM * C_STRIDE;
   __shared__ __attribute__((aligned(16))) char smem[SMEM];
 
   const int tid = threadIdx.x;
@@ -179,7 +179,7 @@ __global__ void __launch_bounds__(NT, 2) conv_nt_kernel(NTParams p) {
   __syncthreads();
 
   for (int kt = 0; kt < nk; ++kt) {
-    const int cur = kt & 1;
+    const int cur = NSTAGE == 2 ? (kt & 1) : 0;
     if (kt + 1 < nk) load_tile(kt + 1);
     const char* sa = smem + cur * STAGE;
     const char* sb = sa + A_BYTES;
@@ -204,9 +204,16 @@ __global__ void __launch_bounds__(NT, 2) conv_nt_kernel(NTParams p) {
           // swapped operands: lane holds 4 consecutive output channels of one row
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[j], af[i], acc[i][j], 0, 0, 0);
     }
-    if (kt + 1 < nk) store_tile(cur ^ 1);
-    __syncthreads();
+    if (NSTAGE == 2) {
+      if (kt + 1 < nk) store_tile(cur ^ 1);
+      __syncthreads();
+    } else if (kt + 1 < nk) {
+      __syncthreads();  // everyone is done reading the single buffer
+      store_tile(0);
+      __syncthreads();
+    }
   }
+  if (NSTAGE == 1) __syncthreads();  // before the epilogue reuses LDS
 
   // ---------------------------------------------------------------- epilogue
   // acc[i][j][r] = C[row = wm*BM/2 + i*16 + (lane&15)][col = wn*BN/2 + j*16 + (lane>>4)*4 + r]
@@ -300,19 +307,54 @@ __global__ void __launch_bounds__(NT, 2) conv_nt_kernel(NTParams p) {
   }
 }
 
-template <int BM, int BN, bool CS64>
+template <int BM, int BN, int NS, bool CS64>
 int launch(const NTParams& p, hipStream_t st) {
   int ntm = (p.M + BM - 1) / BM, ntn = (p.Ncol + BN - 1) / BN;
-  hipLaunchKernelGGL((conv_nt_kernel<BM, BN, CS64>), dim3(ntm * ntn), dim3(NT), 0, st, p);
+  hipLaunchKernelGGL((conv_nt_kernel<BM, BN, NS, CS64>), dim3(ntm * ntn), dim3(NT), 0, st, p);
   PDT_RETURN_LAUNCH();
+}
+
+// Tile variants (autotuned per shape from Python; -1 = built-in heuristic).
+//   id : BM x BN, LDS stages
+constexpr int NVAR = 10;
+constexpr int VAR_BM[NVAR] = {128, 256, 64, 128, 64, 128, 256, 64, 128, 64};
+constexpr int VAR_BN[NVAR] = {128, 64, 128, 64, 64, 128, 64, 128, 64, 64};
+
+int heuristic_variant(int M, int Ncol, int K) {
+  (void)M;
+  if (Ncol <= 64) return K <= 64 ? 6 : 1;
+  return K <= 64 ? 5 : 0;
+}
+
+template <bool CS64>
+int launch_variant(int v, const NTParams& p, hipStream_t st) {
+  switch (v) {
+    case 0: return launch<128, 128, 2, CS64>(p, st);
+    case 1: return launch<256, 64, 2, CS64>(p, st);
+    case 2: return launch<64, 128, 2, CS64>(p, st);
+    case 3: return launch<128, 64, 2, CS64>(p, st);
+    case 4: return launch<64, 64, 2, CS64>(p, st);
+    case 5: return launch<128, 128, 1, CS64>(p, st);
+    case 6: return launch<256, 64, 1, CS64>(p, st);
+    case 7: return launch<64, 128, 1, CS64>(p, st);
+    case 8: return launch<128, 64, 1, CS64>(p, st);
+    case 9: return launch<64, 64, 1, CS64>(p, st);
+  }
+  return -3;
 }
 
 }  // namespace
 
-// Returns the number of BN-statistics partial rows the launch will write for
-// a given M / Ncol (needed to size the stats buffer).
-PDT_API int pdt_conv_nt_stat_rows(int M, int Ncol) {
-  int BM = (Ncol <= 64) ? 256 : 128;
+PDT_API int pdt_conv_nt_num_variants() { return NVAR; }
+
+PDT_API int pdt_conv_nt_resolve_variant(int variant, int M, int Ncol, int K) {
+  return (variant >= 0 && variant < NVAR) ? variant : heuristic_variant(M, Ncol, K);
+}
+
+// Number of BN-statistics partial rows a launch of `variant` writes (sizes the stats buffer).
+PDT_API int pdt_conv_nt_stat_rows(int M, int Ncol, int K, int variant) {
+  int v = pdt_conv_nt_resolve_variant(variant, M, Ncol, K);
+  int BM = VAR_BM[v];
   return ((M + BM - 1) / BM) * 2;
 }
 
@@ -321,7 +363,7 @@ PDT_API int pdt_conv_nt(const void* src, const void* b, void* out, float* stats,
                         int Hs, int Ws, int Cs, int Nimg, int Hm, int Wm, int Ncol, int K, int ldb,
                         int sh, int sw, int oh0, int ow0, int dh, int dw, int nth, int ntw,
                         int Ho, int Wo, int osh, int osw, int oph, int opw, int ldo, int relu,
-                        hipStream_t stream) {
+                        int variant, hipStream_t stream) {
   if (Cs % 8 != 0 || K % 8 != 0 || Ncol % 8 != 0 || ldo % 8 != 0 || ldb % 8 != 0) return -1;
   if (K != nth * ntw * Cs) return -2;
   NTParams p;
@@ -341,10 +383,8 @@ PDT_API int pdt_conv_nt(const void* src, const void* b, void* out, float* stats,
   p.div_HWm = make_fastdiv(Hm * Wm);
   p.div_Cs8 = make_fastdiv(Cs / 8);
   p.div_ntw = make_fastdiv(ntw > 0 ? ntw : 1);
-  p.nstat_rows = pdt_conv_nt_stat_rows(p.M, Ncol);
+  const int v = pdt_conv_nt_resolve_variant(variant, p.M, Ncol, K);
+  p.nstat_rows = pdt_conv_nt_stat_rows(p.M, Ncol, K, v);
   const bool cs64 = (Cs % 64) == 0;
-  if (Ncol <= 64) {
-    return cs64 ? launch<256, 64, true>(p, stream) : launch<256, 64, false>(p, stream);
-  }
-  return cs64 ? launch<128, 128, true>(p, stream) : launch<128, 128, false>(p, stream);
+  return cs64 ? launch_variant<true>(v, p, stream) : launch_variant<false>(v, p, stream);
 }

@@ -28,8 +28,10 @@ c_int, c_long, c_float, c_double, c_void_p, c_uint = (ctypes.c_int, ctypes.c_lon
 P = c_void_p
 
 _SIGS = {
-    "pdt_conv_nt_stat_rows": (c_int, [c_int, c_int]),
-    "pdt_conv_nt": (c_int, [P, P, P, P, P] + [c_int] * 25 + [P]),
+    "pdt_conv_nt_stat_rows": (c_int, [c_int, c_int, c_int, c_int]),
+    "pdt_conv_nt_num_variants": (c_int, []),
+    "pdt_conv_nt_resolve_variant": (c_int, [c_int, c_int, c_int, c_int]),
+    "pdt_conv_nt": (c_int, [P, P, P, P, P] + [c_int] * 26 + [P]),
     "pdt_wgrad_plan": (c_int, [c_int, c_int, c_int, ctypes.POINTER(c_int)]),
     "pdt_wgrad_workspace": (c_long, [c_int, c_int, c_int]),
     "pdt_conv_wgrad": (c_int, [P, P, P, P] + [c_int] * 16 + [c_int, c_int, c_float, c_int, P]),
@@ -153,24 +155,103 @@ def bf16_weight(w: torch.Tensor, pad_cin_to: int | None = None) -> torch.Tensor:
 # =============================================================================
 # raw kernel wrappers
 # =============================================================================
-def conv_nt(src, b, out, *, Hs, Ws, Cs, Nimg, Hm, Wm, Ncol, K, ldb, sh, sw, oh0, ow0, dh, dw, nth, ntw,
-            Ho, Wo, osh, osw, oph, opw, ldo, stats=None, bias=None, relu=False):
+# -----------------------------------------------------------------------------
+# conv_nt tile-variant autotuner: the first eager call of every distinct
+# geometry times each tile variant (csrc/conv_igemm.hip) with HIP events and
+# keeps the fastest; choices persist in a JSON table (shipped tuned table:
+# _lib/autotune_gfx950.json; PDT_AUTOTUNE=0 disables tuning -> heuristic).
+# -----------------------------------------------------------------------------
+_TUNE_PATH = Path(os.environ.get("PDT_AUTOTUNE_CACHE", str(_LIB_PATH.parent / "autotune_gfx950.json")))
+_TUNED: dict | None = None
+
+
+def _tuned() -> dict:
+    global _TUNED
+    if _TUNED is None:
+        _TUNED = {}
+        try:
+            import json
+            _TUNED = json.loads(_TUNE_PATH.read_text())
+        except Exception:
+            _TUNED = {}
+    return _TUNED
+
+
+def _save_tuned():
+    if os.environ.get("RANK", "0") != "0":
+        return
+    try:
+        import json
+        tmp = str(_TUNE_PATH) + f".tmp{os.getpid()}"
+        with open(tmp, "w") as f:
+            json.dump(_TUNED, f, indent=0, sort_keys=True)
+        os.replace(tmp, _TUNE_PATH)
+    except Exception:
+        pass
+
+
+def _nt_args(src, b, out, stats, bias, a, relu, variant):
+    return (_p(src), _p(b), _p(out), _p(stats), _p(bias), a["Hs"], a["Ws"], a["Cs"], a["Nimg"], a["Hm"], a["Wm"],
+            a["Ncol"], a["K"], a["ldb"], a["sh"], a["sw"], a["oh0"], a["ow0"], a["dh"], a["dw"], a["nth"], a["ntw"],
+            a["Ho"], a["Wo"], a["osh"], a["osw"], a["oph"], a["opw"], a["ldo"], int(relu), int(variant), _s())
+
+
+def _check_nt(src, b, out, a):
     assert src.dtype == torch.bfloat16 and b.dtype == torch.bfloat16 and out.dtype == torch.bfloat16
+    Cs, K, Ncol, ldo, ldb = a["Cs"], a["K"], a["Ncol"], a["ldo"], a["ldb"]
     assert Cs % 8 == 0 and K % 8 == 0 and Ncol % 8 == 0 and ldo % 8 == 0, (Cs, K, Ncol, ldo)
-    assert K == nth * ntw * Cs
+    assert K == a["nth"] * a["ntw"] * Cs
     # bounds: the kernel reads src[0 : Nimg*Hs*Ws*Cs], b[0 : Ncol*ldb], writes out rows < Nimg*Ho*Wo
-    assert src.numel() >= Nimg * Hs * Ws * Cs, "src too small"
+    assert src.numel() >= a["Nimg"] * a["Hs"] * a["Ws"] * Cs, "src too small"
     assert b.numel() >= Ncol * ldb or K == 0, "B too small"
-    assert out.numel() >= Nimg * Ho * Wo * ldo, "out too small"
-    assert Nimg * Hs * Ws * Cs < 2 ** 31 and Nimg * Ho * Wo < 2 ** 31
-    rc = _load().pdt_conv_nt(_p(src), _p(b), _p(out), _p(stats), _p(bias), Hs, Ws, Cs, Nimg, Hm, Wm, Ncol, K,
-                             ldb, sh, sw, oh0, ow0, dh, dw, nth, ntw, Ho, Wo, osh, osw, oph, opw, ldo,
-                             int(relu), _s())
-    _chk(rc, "conv_nt")
+    assert out.numel() >= a["Nimg"] * a["Ho"] * a["Wo"] * ldo, "out too small"
+    assert a["Hm"] * a["osh"] <= a["Ho"] and a["Wm"] * a["osw"] <= a["Wo"]
+    assert a["Nimg"] * a["Hs"] * a["Ws"] * Cs < 2 ** 31 and a["Nimg"] * a["Ho"] * a["Wo"] < 2 ** 31
 
 
-def conv_stat_rows(M, Ncol):
-    return _load().pdt_conv_nt_stat_rows(M, Ncol)
+def select_nt_variant(src, b, out, *, with_stats=False, bias=None, relu=False, **a):
+    """Variant id for this geometry (tuning it on first use when allowed)."""
+    M = a["Nimg"] * a["Hm"] * a["Wm"]
+    key = "nt:" + ",".join(str(a[k]) for k in ("Hs", "Ws", "Cs", "Nimg", "Hm", "Wm", "Ncol", "K", "sh", "sw",
+                                                 "nth", "ntw", "osh")) + f",{int(with_stats)},{int(bias is not None)}"
+    table = _tuned()
+    if key in table:
+        return int(table[key])
+    lib = _load()
+    if (os.environ.get("PDT_AUTOTUNE", "1") == "0" or torch.cuda.is_current_stream_capturing()):
+        return lib.pdt_conv_nt_resolve_variant(-1, M, a["Ncol"], a["K"])
+    _check_nt(src, b, out, a)
+    nvar = lib.pdt_conv_nt_num_variants()
+    stats = torch.empty(2 * ((M + 63) // 64) * 2 * a["Ncol"], dtype=torch.float32, device=src.device) \
+        if with_stats else None
+    best, best_t = -1, float("inf")
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    for v in range(nvar):
+        args = _nt_args(src, b, out, stats, bias, a, relu, v)
+        _chk(lib.pdt_conv_nt(*args), "conv_nt(tune)")
+        ev0.record()
+        for _ in range(3):
+            lib.pdt_conv_nt(*args)
+        ev1.record()
+        ev1.synchronize()
+        t = ev0.elapsed_time(ev1)
+        if t < best_t:
+            best, best_t = v, t
+    table[key] = best
+    _save_tuned()
+    return best
+
+
+def conv_nt(src, b, out, *, stats=None, bias=None, relu=False, variant=None, **a):
+    """C[m, n] = sum_k A[m, k] B[n, k] with the implicit-GEMM gather (see csrc/conv_igemm.hip)."""
+    _check_nt(src, b, out, a)
+    if variant is None:
+        variant = select_nt_variant(src, b, out, with_stats=stats is not None, bias=bias, relu=relu, **a)
+    _chk(_load().pdt_conv_nt(*_nt_args(src, b, out, stats, bias, a, relu, variant)), "conv_nt")
+
+
+def conv_stat_rows(M, Ncol, K, variant):
+    return _load().pdt_conv_nt_stat_rows(M, Ncol, K, variant)
 
 
 def conv_wgrad(dy, x, out, *, M, Mo, No, ldy, Hs, Ws, C, Hm, Wm, sh, sw, oh0, ow0, dh, dw, ntw, scale=1.0,
@@ -231,13 +312,27 @@ def supports_conv(x: torch.Tensor, conv: nn.Conv2d) -> bool:
     return True
 
 
-def _conv_forward(x, wb, N, H, W, Cs, Cout, g, stats=None):
+def _fwd_nt_geom(N, H, W, Cs, Cout, g):
+    K = g["KH"] * g["KW"] * Cs
+    return dict(Hs=H, Ws=W, Cs=Cs, Nimg=N, Hm=g["Ho"], Wm=g["Wo"], Ncol=Cout, K=K, ldb=K, sh=g["sh"], sw=g["sw"],
+                oh0=-g["ph"], ow0=-g["pw"], dh=1, dw=1, nth=g["KH"], ntw=g["KW"], Ho=g["Ho"], Wo=g["Wo"], osh=1,
+                osw=1, oph=0, opw=0, ldo=Cout)
+
+
+def _conv_forward(x, wb, N, H, W, Cs, Cout, g, with_stats=False):
+    """Forward conv; returns (y, M, stats_partials or None, stats_rows)."""
     M = N * g["Ho"] * g["Wo"]
     y = _empty_cl(N, Cout, g["Ho"], g["Wo"], torch.bfloat16, x.device)
-    conv_nt(x, wb, y, Hs=H, Ws=W, Cs=Cs, Nimg=N, Hm=g["Ho"], Wm=g["Wo"], Ncol=Cout, K=g["KH"] * g["KW"] * Cs,
-            ldb=g["KH"] * g["KW"] * Cs, sh=g["sh"], sw=g["sw"], oh0=-g["ph"], ow0=-g["pw"], dh=1, dw=1,
-            nth=g["KH"], ntw=g["KW"], Ho=g["Ho"], Wo=g["Wo"], osh=1, osw=1, oph=0, opw=0, ldo=Cout, stats=stats)
-    return y, M
+    a = _fwd_nt_geom(N, H, W, Cs, Cout, g)
+    v = select_nt_variant(x, wb, y, with_stats=with_stats, **a)
+    part, R = None, 0
+    if with_stats:
+        lib = _load()
+        R = conv_stat_rows(M, Cout, a["K"], v)
+        part = torch.empty(2 * R * Cout + lib.pdt_rows_reduce_workspace(R, Cout), dtype=torch.float32,
+                           device=x.device)
+    conv_nt(x, wb, y, stats=part, variant=v, **a)
+    return y, M, part, R
 
 
 def _conv_dgrad(dy, w32, N, H, W, Cin, Cout, g):
@@ -296,9 +391,7 @@ class _ConvBNAct(torch.autograd.Function):
         f32 = dict(dtype=torch.float32, device=dev)
         M = N * g["Ho"] * g["Wo"]
         if training:
-            R = conv_stat_rows(M, Cout)
-            part = torch.empty(2 * R * Cout + lib.pdt_rows_reduce_workspace(R, Cout), **f32)
-            y, _ = _conv_forward(x, wb, N, H, W, Cs, Cout, g, stats=part)
+            y, _, part, R = _conv_forward(x, wb, N, H, W, Cs, Cout, g, with_stats=True)
             mean = torch.empty(Cout, **f32)
             invstd = torch.empty(Cout, **f32)
             scale = torch.empty(Cout, **f32)
@@ -310,7 +403,7 @@ class _ConvBNAct(torch.autograd.Function):
                                      _p(nbt), st),
                  "bn_finalize")
         else:
-            y, _ = _conv_forward(x, wb, N, H, W, Cs, Cout, g, stats=None)
+            y, _, _, _ = _conv_forward(x, wb, N, H, W, Cs, Cout, g, with_stats=False)
             invstd = torch.rsqrt(running_var.float() + eps)
             mean = running_mean.float().clone()
             scale = (gamma.float() * invstd).contiguous()

@@ -58,10 +58,8 @@ def main():
             memory_format=torch.channels_last)
         g = no._fwd_geom(N, H, H, Cs, conv)
         wb = no.bf16_weight(conv.weight, pad_cin_to=Cs if Cs != Cin else None)
-        R = no.conv_stat_rows(N * g["Ho"] * g["Wo"], Cout)
-        part = torch.empty(2 * R * Cout, device="cuda")
         wbt = conv.weight.detach().to(torch.bfloat16)
-        nf = timeit(lambda: no._conv_forward(xs, wb, N, H, H, Cs, Cout, g, stats=part), a.iters)
+        nf = timeit(lambda: no._conv_forward(xs, wb, N, H, H, Cs, Cout, g, with_stats=True), a.iters)
         sf = timeit(lambda: F.conv2d(x, wbt, None, s, p), a.iters)
         y = F.conv2d(x, wbt, None, s, p)
         dy = torch.randn_like(y)

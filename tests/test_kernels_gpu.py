@@ -62,14 +62,18 @@ def test_conv_fwd_dgrad_wgrad(shape):
         xs = _cl(F.pad(x.permute(0, 2, 3, 1), (0, Cs - Cin)).permute(0, 3, 1, 2))
     g = no._fwd_geom(N, H, W, Cs, conv)
     wb = no.bf16_weight(conv.weight, pad_cin_to=Cs if Cs != Cin else None)
-    R = no.conv_stat_rows(N * g["Ho"] * g["Wo"], Cout)
-    part = torch.empty(2 * R * Cout, device=dev)
-    y, M = no._conv_forward(xs, wb, N, H, W, Cs, Cout, g, stats=part)
+    y, M, part, R = no._conv_forward(xs, wb, N, H, W, Cs, Cout, g, with_stats=True)
     wr = conv.weight.detach().to(torch.bfloat16).float()
     ref = F.conv2d(x.float(), wr, None, s, p)
     assert relerr(y, ref) < 1e-2
+    # every tile variant the autotuner may pick computes the same conv
+    a = no._fwd_nt_geom(N, H, W, Cs, Cout, g)
+    for v in range(no._load().pdt_conv_nt_num_variants()):
+        yv = torch.empty_like(y)
+        no.conv_nt(xs, wb, yv, variant=v, **a)
+        assert relerr(yv, ref) < 1e-2, v
     # BN partial statistics from the epilogue
-    ps = part.view(2, R, Cout).sum(1)
+    ps = part[:2 * R * Cout].view(2, R, Cout).sum(1)
     rs = ref.sum((0, 2, 3))
     rq = (ref * ref).sum((0, 2, 3))
     assert relerr(ps[0], rs) < 1e-3 + 1e-2 * 0
