@@ -36,6 +36,7 @@ struct NTParams {
   u16* out;
   float* stats;        // optional: [2][nstat_rows][Ncol] partial sums (sum, sumsq)
   const float* bias;   // optional: [Ncol]
+  const u16* addend;   // optional: out = conv + addend (same layout as out)
   int Hs, Ws, Cs;      // source geometry (NHWC, batch implied by M-grid)
   int Hm, Wm;          // M-grid per image
   int M, Ncol, K, ldb;
@@ -302,6 +303,11 @@ __global__ void __launch_bounds__(NT, 2) conv_nt_kernel(NTParams p) {
       uint32_t oh = fdiv(rem, p.div_Wm);
       uint32_t ow = rem - oh * p.Wm;
       size_t orow = ((size_t)img * p.Ho + oh * p.osh + p.oph) * p.Wo + ow * p.osw + p.opw;
+      if (p.addend != nullptr) {
+        u32x4 a = *reinterpret_cast<const u32x4*>(p.addend + orow * p.ldo + col);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[e] = pack2bf(lo_bf(v[e]) + lo_bf(a[e]), hi_bf(v[e]) + hi_bf(a[e]));
+      }
       *reinterpret_cast<u32x4*>(p.out + orow * p.ldo + col) = v;
     }
   }
@@ -360,6 +366,7 @@ PDT_API int pdt_conv_nt_stat_rows(int M, int Ncol, int K, int variant) {
 
 // Generic launch: see header comment for the meaning of every argument.
 PDT_API int pdt_conv_nt(const void* src, const void* b, void* out, float* stats, const float* bias,
+                        const void* addend,
                         int Hs, int Ws, int Cs, int Nimg, int Hm, int Wm, int Ncol, int K, int ldb,
                         int sh, int sw, int oh0, int ow0, int dh, int dw, int nth, int ntw,
                         int Ho, int Wo, int osh, int osw, int oph, int opw, int ldo, int relu,
@@ -372,6 +379,7 @@ PDT_API int pdt_conv_nt(const void* src, const void* b, void* out, float* stats,
   p.out = (u16*)out;
   p.stats = stats;
   p.bias = bias;
+  p.addend = (const u16*)addend;
   p.Hs = Hs; p.Ws = Ws; p.Cs = Cs;
   p.Hm = Hm; p.Wm = Wm;
   p.M = Nimg * Hm * Wm;

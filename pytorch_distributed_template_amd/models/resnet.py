@@ -44,15 +44,9 @@ class Bottleneck(nn.Module):
             self.downsample = None
 
     def forward(self, x):
-        if self.downsample is not None:
-            identity = fused.conv_bn_act(x, self.downsample[0], self.downsample[1], relu=False)
-        else:
-            identity = x
-        out = fused.conv_bn_act(x, self.conv1, self.bn1, relu=True)
-        out = fused.conv_bn_act(out, self.conv2, self.bn2, relu=True)
-        # BN3 + residual add + ReLU in one pass
-        out = fused.conv_bn_act(out, self.conv3, self.bn3, residual=identity, relu=True)
-        return out
+        # conv-BN-ReLU x3 with BN3 + residual add + ReLU in one pass; on the
+        # native path the whole block is one autograd node (ops.native_ops._Bottleneck)
+        return fused.bottleneck(x, self)
 
 
 class ResNet(BaseModel):

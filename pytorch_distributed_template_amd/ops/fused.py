@@ -65,6 +65,22 @@ def conv_bn_act(x, conv: nn.Conv2d, bn: nn.BatchNorm2d, residual=None, relu: boo
     return _torch_conv_bn_act(x, conv, bn, residual, relu)
 
 
+def bottleneck(x, blk):
+    """ResNet bottleneck block; the native path runs it as one fused autograd node."""
+    if _use_native(x):
+        from . import native_ops
+        out = native_ops.bottleneck(x, blk)
+        if out is not None:
+            return out
+    if blk.downsample is not None:
+        identity = conv_bn_act(x, blk.downsample[0], blk.downsample[1], relu=False)
+    else:
+        identity = x
+    out = conv_bn_act(x, blk.conv1, blk.bn1, relu=True)
+    out = conv_bn_act(out, blk.conv2, blk.bn2, relu=True)
+    return conv_bn_act(out, blk.conv3, blk.bn3, residual=identity, relu=True)
+
+
 def max_pool2d(x, kernel_size=3, stride=2, padding=1):
     if _use_native(x):
         from . import native_ops

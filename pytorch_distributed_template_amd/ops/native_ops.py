@@ -31,7 +31,7 @@ _SIGS = {
     "pdt_conv_nt_stat_rows": (c_int, [c_int, c_int, c_int, c_int]),
     "pdt_conv_nt_num_variants": (c_int, []),
     "pdt_conv_nt_resolve_variant": (c_int, [c_int, c_int, c_int, c_int]),
-    "pdt_conv_nt": (c_int, [P, P, P, P, P] + [c_int] * 26 + [P]),
+    "pdt_conv_nt": (c_int, [P, P, P, P, P, P] + [c_int] * 26 + [P]),
     "pdt_wgrad_plan": (c_int, [c_int, c_int, c_int, ctypes.POINTER(c_int)]),
     "pdt_wgrad_workspace": (c_long, [c_int, c_int, c_int]),
     "pdt_conv_wgrad": (c_int, [P, P, P, P] + [c_int] * 16 + [c_int, c_int, c_float, c_int, P]),
@@ -190,8 +190,8 @@ def _save_tuned():
         pass
 
 
-def _nt_args(src, b, out, stats, bias, a, relu, variant):
-    return (_p(src), _p(b), _p(out), _p(stats), _p(bias), a["Hs"], a["Ws"], a["Cs"], a["Nimg"], a["Hm"], a["Wm"],
+def _nt_args(src, b, out, stats, bias, a, relu, variant, addend=None):
+    return (_p(src), _p(b), _p(out), _p(stats), _p(bias), _p(addend), a["Hs"], a["Ws"], a["Cs"], a["Nimg"], a["Hm"], a["Wm"],
             a["Ncol"], a["K"], a["ldb"], a["sh"], a["sw"], a["oh0"], a["ow0"], a["dh"], a["dw"], a["nth"], a["ntw"],
             a["Ho"], a["Wo"], a["osh"], a["osw"], a["oph"], a["opw"], a["ldo"], int(relu), int(variant), _s())
 
@@ -242,12 +242,15 @@ def select_nt_variant(src, b, out, *, with_stats=False, bias=None, relu=False, *
     return best
 
 
-def conv_nt(src, b, out, *, stats=None, bias=None, relu=False, variant=None, **a):
-    """C[m, n] = sum_k A[m, k] B[n, k] with the implicit-GEMM gather (see csrc/conv_igemm.hip)."""
+def conv_nt(src, b, out, *, stats=None, bias=None, relu=False, variant=None, addend=None, **a):
+    """C[m, n] = sum_k A[m, k] B[n, k] (+ addend) with the implicit-GEMM gather (see csrc/conv_igemm.hip)."""
     _check_nt(src, b, out, a)
+    if addend is not None:
+        assert addend.dtype == torch.bfloat16 and addend.numel() == out.numel() and addend.is_contiguous(
+            memory_format=torch.channels_last if addend.dim() == 4 else torch.contiguous_format)
     if variant is None:
         variant = select_nt_variant(src, b, out, with_stats=stats is not None, bias=bias, relu=relu, **a)
-    _chk(_load().pdt_conv_nt(*_nt_args(src, b, out, stats, bias, a, relu, variant)), "conv_nt")
+    _chk(_load().pdt_conv_nt(*_nt_args(src, b, out, stats, bias, a, relu, variant, addend)), "conv_nt")
 
 
 def conv_stat_rows(M, Ncol, K, variant):
@@ -335,8 +338,8 @@ def _conv_forward(x, wb, N, H, W, Cs, Cout, g, with_stats=False):
     return y, M, part, R
 
 
-def _conv_dgrad(dy, w32, N, H, W, Cin, Cout, g):
-    """dX [N,Cin,H,W] from dY [N,Cout,Ho,Wo] (stride phases, see csrc/conv_igemm.hip)."""
+def _conv_dgrad(dy, w32, N, H, W, Cin, Cout, g, addend=None):
+    """dX [N,Cin,H,W] (+ addend) from dY [N,Cout,Ho,Wo] (stride phases, see csrc/conv_igemm.hip)."""
     KH, KW, s_h, s_w, ph, pw = g["KH"], g["KW"], g["sh"], g["sw"], g["ph"], g["pw"]
     assert w32.shape[0] == Cout and w32.shape[1] == Cin, (tuple(w32.shape), Cout, Cin)
     assert dy.shape[1] == Cout and dy.numel() == N * Cout * g["Ho"] * g["Wo"]
@@ -359,7 +362,7 @@ def _conv_dgrad(dy, w32, N, H, W, Cin, Cout, g):
                                       nth, ntw, _s()), "wt_dgrad")
             conv_nt(dy, wt, dx, Hs=g["Ho"], Ws=g["Wo"], Cs=Cout, Nimg=N, Hm=H // s_h, Wm=W // s_w, Ncol=Cin,
                     K=K, ldb=max(K, 8), sh=1, sw=1, oh0=oh0, ow0=ow0, dh=-1, dw=-1, nth=nth, ntw=max(ntw, 0),
-                    Ho=H, Wo=W, osh=s_h, osw=s_w, oph=qh, opw=qw, ldo=Cin)
+                    Ho=H, Wo=W, osh=s_h, osw=s_w, oph=qh, opw=qw, ldo=Cin, addend=addend)
     return dx
 
 
@@ -370,124 +373,211 @@ def _conv_wgrad(dy, x, N, H, W, Cs, Cout, g, out):
 
 
 # =============================================================================
-# fused conv -> BN -> (+res) -> (ReLU)
+# fused conv -> BN -> (+res) -> (ReLU): one "unit"
 # =============================================================================
+class _BNArgs:
+    """BatchNorm module state resolved for one call (training vs eval, running
+    stats, num_batches_tracked handled inside the finalize kernel)."""
+    __slots__ = ("training", "momentum", "eps", "rm", "rv", "nbt")
+
+    def __init__(self, bn: nn.BatchNorm2d):
+        self.training = bn.training or not bn.track_running_stats
+        self.momentum = bn.momentum if bn.momentum is not None else 0.1
+        self.eps = bn.eps
+        self.rm = bn.running_mean if (bn.track_running_stats and bn.training) else None
+        self.rv = bn.running_var if (bn.track_running_stats and bn.training) else None
+        self.nbt = None
+        if bn.training and bn.track_running_stats and bn.num_batches_tracked is not None:
+            self.nbt = bn.num_batches_tracked
+            if bn.momentum is None:  # cumulative moving average needs the host-side count
+                self.nbt.add_(1)
+                self.momentum = 1.0 / float(self.nbt.item())
+                self.nbt = None
+        if not self.training:
+            self.rm, self.rv = bn.running_mean, bn.running_var
+
+
+class _Unit:
+    """Saved state of one conv->BN->act unit between forward and backward."""
+    __slots__ = ("x", "w", "gamma", "y", "act", "mean", "invstd", "scale", "shift", "N", "C", "Cs", "H", "W",
+                 "Cout", "g", "relu", "has_res")
+
+
+def _unit_fwd(x, w, gamma, beta, residual, conv, relu, bna: _BNArgs):
+    lib = _load()
+    st = _s()
+    N, C, H, W = x.shape
+    Cs = C if C % 8 == 0 else 8
+    x = x.to(torch.bfloat16)
+    if Cs != C:  # stem: pad channels to 8 (NHWC)
+        x = torch.nn.functional.pad(_cl(x).permute(0, 2, 3, 1), (0, Cs - C)).permute(0, 3, 1, 2)
+    x = _cl(x)
+    Cout = w.shape[0]
+    g = _fwd_geom(N, H, W, Cs, conv)
+    wb = bf16_weight(w, pad_cin_to=Cs if Cs != C else None)
+    f32 = dict(dtype=torch.float32, device=x.device)
+    M = N * g["Ho"] * g["Wo"]
+    if bna.training:
+        y, _, part, R = _conv_forward(x, wb, N, H, W, Cs, Cout, g, with_stats=True)
+        vec = torch.empty((4, Cout), **f32)
+        mean, invstd, scale, shift = vec[0], vec[1], vec[2], vec[3]
+        _chk(lib.pdt_bn_finalize(_p(part), R, Cout, float(M), float(bna.eps), float(bna.momentum), _p(gamma),
+                                 _p(beta), _p(mean), _p(invstd), _p(scale), _p(shift), _p(bna.rm), _p(bna.rv),
+                                 _p(bna.nbt), st), "bn_finalize")
+    else:
+        y, _, _, _ = _conv_forward(x, wb, N, H, W, Cs, Cout, g, with_stats=False)
+        invstd = torch.rsqrt(bna.rv.float() + bna.eps)
+        mean = bna.rm.float().clone()
+        scale = (gamma.float() * invstd).contiguous()
+        shift = (beta.float() - mean * scale).contiguous()
+    assert y.numel() == M * Cout
+    res = None
+    if residual is not None:
+        res = _cl(residual)
+        assert res.dtype == torch.bfloat16 and res.shape == y.shape, (res.shape, y.shape)
+    out = torch.empty_like(y, memory_format=torch.channels_last)
+    _chk(lib.pdt_bn_apply(_p(y), _p(res), _p(out), _p(scale), _p(shift), M, Cout, int(relu), st), "bn_apply")
+    u = _Unit()
+    u.x, u.w, u.gamma, u.y = x, w, gamma, y
+    u.act = out if (relu and residual is not None) else None
+    u.mean, u.invstd, u.scale, u.shift = mean, invstd, scale, shift
+    u.N, u.C, u.Cs, u.H, u.W, u.Cout, u.g, u.relu, u.has_res = N, C, Cs, H, W, Cout, g, relu, residual is not None
+    return out, u
+
+
+def _bn_bwd(dA, u: _Unit, want_dres: bool):
+    """BN(+res)(+ReLU) backward: returns (dy, dres, dgamma, dbeta)."""
+    lib = _load()
+    st = _s()
+    dA = _cl(dA.to(torch.bfloat16))
+    Cout = u.Cout
+    M = u.N * u.g["Ho"] * u.g["Wo"]
+    f32 = dict(dtype=torch.float32, device=dA.device)
+    blocks = lib.pdt_bn_stats_blocks(M, Cout)
+    part = torch.empty(2 * blocks * Cout + lib.pdt_rows_reduce_workspace(blocks, Cout), **f32)
+    _chk(lib.pdt_bn_bwd_reduce(_p(dA), _p(u.y), _p(u.act), _p(u.mean), _p(u.scale), _p(u.shift), _p(part), M,
+                               Cout, int(u.relu), blocks, st), "bn_bwd_reduce")
+    vec = torch.empty((5, Cout), **f32)
+    dgamma, dbeta, k1, k2, k3 = vec[0], vec[1], vec[2], vec[3], vec[4]
+    _chk(lib.pdt_bn_bwd_finalize(_p(part), blocks, Cout, float(M), _p(u.gamma), _p(u.mean), _p(u.invstd),
+                                 _p(dgamma), _p(dbeta), _p(k1), _p(k2), _p(k3), 0, st), "bn_bwd_finalize")
+    dy = torch.empty_like(u.y, memory_format=torch.channels_last)
+    dres = torch.empty_like(u.y, memory_format=torch.channels_last) if want_dres else None
+    _chk(lib.pdt_bn_bwd_apply(_p(dA), _p(u.y), _p(u.act), _p(u.scale), _p(u.shift), _p(k1), _p(k2), _p(k3),
+                              _p(dy), _p(dres), M, Cout, int(u.relu), st), "bn_bwd_apply")
+    return dy, dres, dgamma, dbeta
+
+
+def _unit_dx(dy, u: _Unit, addend=None):
+    wd = u.w
+    if u.Cs != u.C:  # stem: dgrad against the channel-padded weight, then drop the pad
+        wd = torch.nn.functional.pad(u.w.detach().float(), (0, 0, 0, 0, 0, u.Cs - u.C))
+        assert addend is None
+    dx = _conv_dgrad(dy, wd, u.N, u.H, u.W, u.Cs, u.Cout, u.g, addend=addend)
+    return dx[:, :u.C] if u.Cs != u.C else dx
+
+
+def _unit_dw(dy, u: _Unit):
+    w = u.w
+    KH, KW = u.g["KH"], u.g["KW"]
+    if u.Cs == u.C and w.is_contiguous(memory_format=torch.channels_last):
+        dw = torch.empty_like(w, dtype=torch.float32, memory_format=torch.channels_last)
+        _conv_wgrad(dy, u.x, u.N, u.H, u.W, u.Cs, u.Cout, u.g, dw)
+    else:
+        tmp = torch.empty((u.Cout, u.Cs, KH, KW), dtype=torch.float32, device=dy.device,
+                          memory_format=torch.channels_last)
+        _conv_wgrad(dy, u.x, u.N, u.H, u.W, u.Cs, u.Cout, u.g, tmp)
+        dw = tmp[:, :u.C].contiguous(memory_format=torch.channels_last) if u.Cs != u.C else tmp
+    return dw.to(w.dtype) if dw.dtype != w.dtype else dw
+
+
 class _ConvBNAct(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, w, gamma, beta, residual, running_mean, running_var, conv, relu, training, momentum, eps,
-                nbt):
-        lib = _load()
-        st = _s()
-        N, C, H, W = x.shape
-        Cs = C if C % 8 == 0 else 8
-        x = x.to(torch.bfloat16)
-        if Cs != C:  # stem: pad channels to 8 (NHWC)
-            x = torch.nn.functional.pad(_cl(x).permute(0, 2, 3, 1), (0, Cs - C)).permute(0, 3, 1, 2)
-        x = _cl(x)
-        Cout = w.shape[0]
-        g = _fwd_geom(N, H, W, Cs, conv)
-        wb = bf16_weight(w, pad_cin_to=Cs if Cs != C else None)
-        dev = x.device
-        f32 = dict(dtype=torch.float32, device=dev)
-        M = N * g["Ho"] * g["Wo"]
-        if training:
-            y, _, part, R = _conv_forward(x, wb, N, H, W, Cs, Cout, g, with_stats=True)
-            mean = torch.empty(Cout, **f32)
-            invstd = torch.empty(Cout, **f32)
-            scale = torch.empty(Cout, **f32)
-            shift = torch.empty(Cout, **f32)
-            rm = running_mean if running_mean is not None else None
-            rv = running_var if running_var is not None else None
-            _chk(lib.pdt_bn_finalize(_p(part), R, Cout, float(M), float(eps), float(momentum), _p(gamma),
-                                     _p(beta), _p(mean), _p(invstd), _p(scale), _p(shift), _p(rm), _p(rv),
-                                     _p(nbt), st),
-                 "bn_finalize")
-        else:
-            y, _, _, _ = _conv_forward(x, wb, N, H, W, Cs, Cout, g, with_stats=False)
-            invstd = torch.rsqrt(running_var.float() + eps)
-            mean = running_mean.float().clone()
-            scale = (gamma.float() * invstd).contiguous()
-            shift = (beta.float() - mean * scale).contiguous()
-        assert y.numel() == M * Cout
-        res = None
-        if residual is not None:
-            res = _cl(residual)
-            assert res.dtype == torch.bfloat16 and res.shape == y.shape, (res.shape, y.shape)
-        out = torch.empty_like(y, memory_format=torch.channels_last)
-        _chk(lib.pdt_bn_apply(_p(y), _p(res), _p(out), _p(scale), _p(shift), M, Cout, int(relu), st), "bn_apply")
-        ctx.save_for_backward(x, w, gamma, y, out if (relu and residual is not None) else None, mean, invstd,
-                              scale, shift)
-        ctx.meta = (N, C, Cs, H, W, Cout, g, relu, residual is not None)
+    def forward(ctx, x, w, gamma, beta, residual, conv, relu, bna):
+        out, u = _unit_fwd(x, w, gamma, beta, residual, conv, relu, bna)
+        ctx.u = u
+        ctx.save_for_backward(u.x, u.y, u.act)  # version-checked activations
         return out
 
     @staticmethod
     def backward(ctx, dA):
-        x, w, gamma, y, act, mean, invstd, scale, shift = ctx.saved_tensors
-        N, C, Cs, H, W, Cout, g, relu, has_res = ctx.meta
-        lib = _load()
-        st = _s()
-        dA = _cl(dA.to(torch.bfloat16))
-        M = N * g["Ho"] * g["Wo"]
-        dev = dA.device
-        f32 = dict(dtype=torch.float32, device=dev)
-        blocks = lib.pdt_bn_stats_blocks(M, Cout)
-        part = torch.empty(2 * blocks * Cout + lib.pdt_rows_reduce_workspace(blocks, Cout), **f32)
-        _chk(lib.pdt_bn_bwd_reduce(_p(dA), _p(y), _p(act), _p(mean), _p(scale), _p(shift), _p(part), M, Cout,
-                                   int(relu), blocks, st), "bn_bwd_reduce")
-        dgamma = torch.empty(Cout, **f32)
-        dbeta = torch.empty(Cout, **f32)
-        k1 = torch.empty(Cout, **f32)
-        k2 = torch.empty(Cout, **f32)
-        k3 = torch.empty(Cout, **f32)
-        _chk(lib.pdt_bn_bwd_finalize(_p(part), blocks, Cout, float(M), _p(gamma), _p(mean), _p(invstd),
-                                     _p(dgamma), _p(dbeta), _p(k1), _p(k2), _p(k3), 0, st), "bn_bwd_finalize")
-        dy = torch.empty_like(y, memory_format=torch.channels_last)
-        dres = torch.empty_like(y, memory_format=torch.channels_last) if has_res else None
-        _chk(lib.pdt_bn_bwd_apply(_p(dA), _p(y), _p(act), _p(scale), _p(shift), _p(k1), _p(k2), _p(k3), _p(dy),
-                                  _p(dres), M, Cout, int(relu), st), "bn_bwd_apply")
-        dx = None
-        if ctx.needs_input_grad[0]:
-            wd = w
-            if Cs != C:  # stem: dgrad against the channel-padded weight, then drop the pad
-                wd = torch.nn.functional.pad(w.detach().float(), (0, 0, 0, 0, 0, Cs - C))
-            dx = _conv_dgrad(dy, wd, N, H, W, Cs, Cout, g)
-            if Cs != C:
-                dx = dx[:, :C]
-        dw = None
-        if ctx.needs_input_grad[1]:
-            KH, KW = g["KH"], g["KW"]
-            if Cs == C and w.is_contiguous(memory_format=torch.channels_last):
-                dw = torch.empty_like(w, dtype=torch.float32, memory_format=torch.channels_last)
-                _conv_wgrad(dy, x, N, H, W, Cs, Cout, g, dw)
-            else:
-                tmp = torch.empty((Cout, Cs, KH, KW), memory_format=torch.channels_last, **f32)
-                _conv_wgrad(dy, x, N, H, W, Cs, Cout, g, tmp)
-                dw = tmp[:, :C].contiguous(memory_format=torch.channels_last) if Cs != C else tmp
-            if dw.dtype != w.dtype:
-                dw = dw.to(w.dtype)
+        u = ctx.u
+        dy, dres, dgamma, dbeta = _bn_bwd(dA, u, u.has_res)
+        dx = _unit_dx(dy, u) if ctx.needs_input_grad[0] else None
+        dw = _unit_dw(dy, u) if ctx.needs_input_grad[1] else None
+        del ctx.u
         return (dx, dw, dgamma if ctx.needs_input_grad[2] else None, dbeta if ctx.needs_input_grad[3] else None,
-                dres, None, None, None, None, None, None, None, None)
+                dres, None, None, None)
 
 
 def conv_bn_act(x, conv: nn.Conv2d, bn: nn.BatchNorm2d, residual=None, relu=True):
     if not supports_conv(x, conv) or (residual is not None and residual.dtype != torch.bfloat16):
         from .fused import _torch_conv_bn_act
         return _torch_conv_bn_act(x, conv, bn, residual, relu)
-    training = bn.training or not bn.track_running_stats
-    momentum = bn.momentum if bn.momentum is not None else 0.1
-    rm = bn.running_mean if (bn.track_running_stats and bn.training) else None
-    rv = bn.running_var if (bn.track_running_stats and bn.training) else None
-    nbt = None
-    if bn.training and bn.track_running_stats and bn.num_batches_tracked is not None:
-        nbt = bn.num_batches_tracked  # incremented inside the finalize kernel
-        if bn.momentum is None:  # cumulative moving average needs the host-side count
-            nbt.add_(1)
-            momentum = 1.0 / float(nbt.item())
-            nbt = None
-    if not training:
-        rm, rv = bn.running_mean, bn.running_var
-    return _ConvBNAct.apply(x, conv.weight, bn.weight, bn.bias, residual, rm, rv, conv, relu, training, momentum,
-                            bn.eps, nbt)
+    return _ConvBNAct.apply(x, conv.weight, bn.weight, bn.bias, residual, conv, relu, _BNArgs(bn))
+
+
+# =============================================================================
+# fused ResNet bottleneck: conv1-bn1-relu -> conv2-bn2-relu -> conv3-bn3 (+ identity
+# or downsample conv-bn) -> relu, with a hand-scheduled backward: the block-input
+# gradient is produced by ONE data-gradient GEMM whose epilogue adds the
+# identity / downsample branch gradient (no separate add pass).
+# =============================================================================
+class _Bottleneck(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, blk, has_ds, *params):
+        if has_ds:
+            idn, ud = _unit_fwd(x, blk.downsample[0].weight, blk.downsample[1].weight, blk.downsample[1].bias, None,
+                                blk.downsample[0], False, _BNArgs(blk.downsample[1]))
+        else:
+            idn, ud = _cl(x.to(torch.bfloat16)), None
+        a1, u1 = _unit_fwd(x, blk.conv1.weight, blk.bn1.weight, blk.bn1.bias, None, blk.conv1, True,
+                           _BNArgs(blk.bn1))
+        a2, u2 = _unit_fwd(a1, blk.conv2.weight, blk.bn2.weight, blk.bn2.bias, None, blk.conv2, True,
+                           _BNArgs(blk.bn2))
+        out, u3 = _unit_fwd(a2, blk.conv3.weight, blk.bn3.weight, blk.bn3.bias, idn, blk.conv3, True,
+                            _BNArgs(blk.bn3))
+        ctx.units = (u1, u2, u3, ud)
+        ctx.has_ds = has_ds
+        ctx.save_for_backward(u1.x, u1.y, u2.y, u3.y, u3.act)
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        u1, u2, u3, ud = ctx.units
+        need = ctx.needs_input_grad
+        dy3, dres, dg3, db3 = _bn_bwd(dout, u3, True)
+        da2 = _unit_dx(dy3, u3)
+        dw3 = _unit_dw(dy3, u3)
+        dy2, _, dg2, db2 = _bn_bwd(da2, u2, False)
+        da1 = _unit_dx(dy2, u2)
+        dw2 = _unit_dw(dy2, u2)
+        dy1, _, dg1, db1 = _bn_bwd(da1, u1, False)
+        grads_ds = ()
+        if ctx.has_ds:
+            dyd, _, dgd, dbd = _bn_bwd(dres, ud, False)
+            addend = _unit_dx(dyd, ud) if need[0] else None
+            dwd = _unit_dw(dyd, ud)
+            grads_ds = (dwd, dgd, dbd)
+        else:
+            addend = dres
+        dx = _unit_dx(dy1, u1, addend=addend) if need[0] else None
+        dw1 = _unit_dw(dy1, u1)
+        del ctx.units
+        return (dx, None, None, dw1, dg1, db1, dw2, dg2, db2, dw3, dg3, db3) + grads_ds
+
+
+def bottleneck(x, blk):
+    convs = [blk.conv1, blk.conv2, blk.conv3] + ([blk.downsample[0]] if blk.downsample is not None else [])
+    if x.dtype != torch.bfloat16 or not all(supports_conv(x if c is blk.conv1 else x, c) for c in convs) \
+            or x.shape[1] % 8:
+        return None
+    has_ds = blk.downsample is not None
+    params = [blk.conv1.weight, blk.bn1.weight, blk.bn1.bias, blk.conv2.weight, blk.bn2.weight, blk.bn2.bias,
+              blk.conv3.weight, blk.bn3.weight, blk.bn3.bias]
+    if has_ds:
+        params += [blk.downsample[0].weight, blk.downsample[1].weight, blk.downsample[1].bias]
+    return _Bottleneck.apply(x, blk, has_ds, *params)
 
 
 # =============================================================================

@@ -304,3 +304,36 @@ def test_resnet50_native_matches_torch_small_batch():
     fused.set_backend("auto")
     assert torch.isfinite(loss) and abs(loss.item() - loss_r.item()) < 0.05 * abs(loss_r.item()) + 0.05
     assert torch.isfinite(g_native).all()
+
+
+@pytest.mark.parametrize("stride,ds", [(1, False), (2, True), (1, True)])
+def test_fused_bottleneck_matches_unit_composition(stride, ds):
+    """The fused bottleneck node (dgrad epilogue adds the shortcut gradient)
+    must equal the composition of single conv-BN-act units."""
+    from pytorch_distributed_template_amd.models.resnet import Bottleneck
+    torch.manual_seed(7)
+    inpl = 256 if not ds else 128
+    blk = Bottleneck(inpl, 64, stride=stride, downsample=ds).cuda().to(memory_format=torch.channels_last)
+    x = _cl(torch.randn(4, inpl, 16, 16, device="cuda").to(torch.bfloat16))
+
+    def unfused(xx):
+        idn = no.conv_bn_act(xx, blk.downsample[0], blk.downsample[1], relu=False) if ds else xx
+        o = no.conv_bn_act(xx, blk.conv1, blk.bn1, relu=True)
+        o = no.conv_bn_act(o, blk.conv2, blk.bn2, relu=True)
+        return no.conv_bn_act(o, blk.conv3, blk.bn3, residual=idn, relu=True)
+
+    outs = []
+    for fn in (lambda xx: no.bottleneck(xx, blk), unfused):
+        for p in blk.parameters():
+            p.grad = None
+        xi = x.detach().clone().requires_grad_(True)
+        y = fn(xi)
+        g = torch.ones_like(y) * 0.01 + _cl(torch.randn(y.shape, device="cuda", generator=torch.Generator(
+            "cuda").manual_seed(3)).to(torch.bfloat16))
+        y.backward(g)
+        outs.append((y.float(), xi.grad.float(), [p.grad.float().clone() for p in blk.parameters()]))
+    (y1, dx1, g1), (y2, dx2, g2) = outs
+    assert nrmerr(y1, y2) < 1e-3
+    assert nrmerr(dx1, dx2) < 1e-2
+    for a, b in zip(g1, g2):
+        assert nrmerr(a, b) < 1e-2
