@@ -68,11 +68,15 @@ def main():
     torch.manual_seed(1234)
     ctor = {"resnet50": models.resnet50, "resnet152": models.resnet152, "vit_b_16": models.vit_b_16}[args.model]
     model = ctor(num_classes=1000).to(device).to(memory_format=torch.channels_last)
-    if args.backend == "native":
-        from pytorch_distributed_template_amd.optim import FusedSGD
-        opt = FusedSGD(model.parameters(), lr=0.1, momentum=0.9, weight_decay=5e-5)
+    from pytorch_distributed_template_amd.optim import FusedAdamW, FusedSGD
+    if args.model.startswith("vit"):
+        opt_name = "AdamW(lr=1e-3, wd=0.05)"
+        opt = (FusedAdamW if args.backend == "native" else torch.optim.AdamW)(model.parameters(), lr=1e-3,
+                                                                              weight_decay=0.05)
     else:
-        opt = torch.optim.SGD(model.parameters(), lr=0.1, momentum=0.9, weight_decay=5e-5)
+        opt_name = "SGD(momentum=0.9, wd=5e-5)"
+        opt = (FusedSGD if args.backend == "native" else torch.optim.SGD)(model.parameters(), lr=0.1, momentum=0.9,
+                                                                          weight_decay=5e-5)
     model = wrap_ddp(model, device, bucket_cap_mb=args.bucket_mb, broadcast_buffers=False,
                      gradient_as_bucket_view=True, comm_hook=args.comm_hook)
 
@@ -160,7 +164,7 @@ def main():
         "data": "synthetic (device-resident random 3x224x224, random-init weights)",
         "config": {"model": args.model, "global_batch": args.batch * world, "per_gpu_batch": args.batch,
                    "seq_len": None, "image_size": 224, "parallelism": f"dp{world}",
-                   "backend": args.backend, "optimizer": "SGD(momentum=0.9, wd=5e-5)",
+                   "backend": args.backend, "optimizer": opt_name,
                    "bucket_cap_mb": args.bucket_mb, "final_loss": round(final_loss, 4), "hip_graph": args.graph,
                    "cpu_issue_ms_per_step": round(cpu_issue / args.steps * 1e3, 3),
                    "max_mem_gib": round(torch.cuda.max_memory_allocated() / 2 ** 30, 2)},

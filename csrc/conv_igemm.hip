@@ -42,7 +42,8 @@ struct NTParams {
   int M, Ncol, K, ldb;
   int sh, sw, oh0, ow0, dh, dw, nth, ntw;
   int Ho, Wo, osh, osw, oph, opw, ldo;
-  int relu;
+  int act;             // 0 none, 1 relu, 2 gelu(tanh)
+  u16* aux;            // optional: pre-activation copy of the output (same layout)
   int nstat_rows;
   FastDiv div_Wm, div_HWm, div_Cs8, div_ntw;
 };
@@ -220,18 +221,15 @@ __global__ void __launch_bounds__(NT, 2) conv_nt_kernel(NTParams p) {
   // acc[i][j][r] = C[row = wm*BM/2 + i*16 + (lane&15)][col = wn*BN/2 + j*16 + (lane>>4)*4 + r]
   const int lrow = lane & 15;
   const int lcol = (lane >> 4) * 4;
-  if (p.bias != nullptr || p.relu) {
+  if (p.bias != nullptr) {
 #pragma unroll
     for (int j = 0; j < NI; ++j) {
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         int col = n0 + wn * (BN / 2) + j * 16 + lcol + r;
-        float bv = (p.bias != nullptr && col < p.Ncol) ? p.bias[col] : 0.f;
+        float bv = col < p.Ncol ? p.bias[col] : 0.f;
 #pragma unroll
-        for (int i = 0; i < MI; ++i) {
-          float v = acc[i][j][r] + bv;
-          acc[i][j][r] = p.relu ? fmaxf(v, 0.f) : v;
-        }
+        for (int i = 0; i < MI; ++i) acc[i][j][r] += bv;
       }
     }
   }
@@ -275,42 +273,68 @@ __global__ void __launch_bounds__(NT, 2) conv_nt_kernel(NTParams p) {
     }
   }
 
-  // stage bf16 tile through LDS: row-major [BM][BN] with a 16-B row pad
-#pragma unroll
-  for (int i = 0; i < MI; ++i) {
-#pragma unroll
-    for (int j = 0; j < NI; ++j) {
-      int r = wm * (BM / 2) + i * 16 + lrow;
-      int c = wn * (BN / 2) + j * 16 + lcol;
-      uint2 w;
-      w.x = pack2bf(acc[i][j][0], acc[i][j][1]);
-      w.y = pack2bf(acc[i][j][2], acc[i][j][3]);
-      *reinterpret_cast<uint2*>(smem + r * C_STRIDE + c * 2) = w;
-    }
-  }
-  __syncthreads();
+  // stage the bf16 tile through LDS (row-major [BM][BN], 16-B row pad) and
+  // write 16-B coalesced rows; `pre` = pre-activation copy (aux output)
   constexpr int CPR = BN / 8;  // 16-B chunks per row
+  auto stage_store = [&](u16* dst, const u16* addend) {
 #pragma unroll
-  for (int it = 0; it < (BM * CPR) / NT; ++it) {
-    int q = tid + it * NT;
-    int r = q / CPR, cc = q % CPR;
-    int m = m0 + r;
-    int col = n0 + cc * 8;
-    if (m < p.M && col < p.Ncol) {
-      u32x4 v = *reinterpret_cast<const u32x4*>(smem + r * C_STRIDE + cc * 16);
-      uint32_t img = fdiv(m, p.div_HWm);
-      uint32_t rem = m - img * (uint32_t)(p.Hm * p.Wm);
-      uint32_t oh = fdiv(rem, p.div_Wm);
-      uint32_t ow = rem - oh * p.Wm;
-      size_t orow = ((size_t)img * p.Ho + oh * p.osh + p.oph) * p.Wo + ow * p.osw + p.opw;
-      if (p.addend != nullptr) {
-        u32x4 a = *reinterpret_cast<const u32x4*>(p.addend + orow * p.ldo + col);
+    for (int i = 0; i < MI; ++i) {
 #pragma unroll
-        for (int e = 0; e < 4; ++e) v[e] = pack2bf(lo_bf(v[e]) + lo_bf(a[e]), hi_bf(v[e]) + hi_bf(a[e]));
+      for (int j = 0; j < NI; ++j) {
+        int r = wm * (BM / 2) + i * 16 + lrow;
+        int c = wn * (BN / 2) + j * 16 + lcol;
+        uint2 w;
+        w.x = pack2bf(acc[i][j][0], acc[i][j][1]);
+        w.y = pack2bf(acc[i][j][2], acc[i][j][3]);
+        *reinterpret_cast<uint2*>(smem + r * C_STRIDE + c * 2) = w;
       }
-      *reinterpret_cast<u32x4*>(p.out + orow * p.ldo + col) = v;
     }
+    __syncthreads();
+#pragma unroll
+    for (int it = 0; it < (BM * CPR) / NT; ++it) {
+      int q = tid + it * NT;
+      int r = q / CPR, cc = q % CPR;
+      int m = m0 + r;
+      int col = n0 + cc * 8;
+      if (m < p.M && col < p.Ncol) {
+        u32x4 v = *reinterpret_cast<const u32x4*>(smem + r * C_STRIDE + cc * 16);
+        uint32_t img = fdiv(m, p.div_HWm);
+        uint32_t rem = m - img * (uint32_t)(p.Hm * p.Wm);
+        uint32_t oh = fdiv(rem, p.div_Wm);
+        uint32_t ow = rem - oh * p.Wm;
+        size_t orow = ((size_t)img * p.Ho + oh * p.osh + p.oph) * p.Wo + ow * p.osw + p.opw;
+        if (addend != nullptr) {
+          u32x4 a = *reinterpret_cast<const u32x4*>(addend + orow * p.ldo + col);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) v[e] = pack2bf(lo_bf(v[e]) + lo_bf(a[e]), hi_bf(v[e]) + hi_bf(a[e]));
+        }
+        *reinterpret_cast<u32x4*>(dst + orow * p.ldo + col) = v;
+      }
+    }
+  };
+
+  if (p.aux != nullptr) {
+    stage_store(p.aux, nullptr);
+    __syncthreads();
   }
+  if (p.act != 0) {
+#pragma unroll
+    for (int i = 0; i < MI; ++i)
+#pragma unroll
+      for (int j = 0; j < NI; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          float x = acc[i][j][r];
+          if (p.act == 1) {
+            x = fmaxf(x, 0.f);
+          } else {
+            float u = 0.7978845608f * (x + 0.044715f * x * x * x);
+            x = 0.5f * x * (1.f + tanhf(u));
+          }
+          acc[i][j][r] = x;
+        }
+  }
+  stage_store(p.out, p.addend);
 }
 
 template <int BM, int BN, int NS, bool CS64>
@@ -369,8 +393,8 @@ PDT_API int pdt_conv_nt(const void* src, const void* b, void* out, float* stats,
                         const void* addend,
                         int Hs, int Ws, int Cs, int Nimg, int Hm, int Wm, int Ncol, int K, int ldb,
                         int sh, int sw, int oh0, int ow0, int dh, int dw, int nth, int ntw,
-                        int Ho, int Wo, int osh, int osw, int oph, int opw, int ldo, int relu,
-                        int variant, hipStream_t stream) {
+                        int Ho, int Wo, int osh, int osw, int oph, int opw, int ldo, int act,
+                        void* aux, int variant, hipStream_t stream) {
   if (Cs % 8 != 0 || K % 8 != 0 || Ncol % 8 != 0 || ldo % 8 != 0 || ldb % 8 != 0) return -1;
   if (K != nth * ntw * Cs) return -2;
   NTParams p;
@@ -386,7 +410,8 @@ PDT_API int pdt_conv_nt(const void* src, const void* b, void* out, float* stats,
   p.Ncol = Ncol; p.K = K; p.ldb = ldb;
   p.sh = sh; p.sw = sw; p.oh0 = oh0; p.ow0 = ow0; p.dh = dh; p.dw = dw; p.nth = nth; p.ntw = ntw;
   p.Ho = Ho; p.Wo = Wo; p.osh = osh; p.osw = osw; p.oph = oph; p.opw = opw; p.ldo = ldo;
-  p.relu = relu;
+  p.act = act;
+  p.aux = (u16*)aux;
   p.div_Wm = make_fastdiv(Wm);
   p.div_HWm = make_fastdiv(Hm * Wm);
   p.div_Cs8 = make_fastdiv(Cs / 8);

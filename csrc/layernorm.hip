@@ -1,0 +1,239 @@
+// LayerNorm (bf16 in/out, fp32 statistics) and GELU(tanh) backward for the
+// ViT-B/16 path (BASELINE config #5).
+//
+// Forward: one wave64 per row; each lane owns D/256 chunks of four bf16
+// (8-byte loads), row mean / rstd by wave shuffles; y = (x-mean)*rstd*g + b.
+// Backward: same row mapping; dx = rstd * (dxhat - mean(dxhat) - xhat*mean(dxhat*xhat)),
+// dxhat = dy*g; per-block column partials of (dy*xhat, dy) are written to a
+// [2][blocks][D] buffer and summed by a second, deterministic pass.
+#include "pdt_common.h"
+
+namespace {
+
+constexpr int WPB = 4;  // waves (rows) per block
+
+__device__ __forceinline__ void ld4(const u16* p, float* f) {
+  uint2 v = *reinterpret_cast<const uint2*>(p);
+  f[0] = lo_bf(v.x); f[1] = hi_bf(v.x); f[2] = lo_bf(v.y); f[3] = hi_bf(v.y);
+}
+__device__ __forceinline__ void st4(u16* p, const float* f) {
+  uint2 v;
+  v.x = pack2bf(f[0], f[1]);
+  v.y = pack2bf(f[2], f[3]);
+  *reinterpret_cast<uint2*>(p) = v;
+}
+
+template <int CH>  // chunks of 4 per lane: D = 256*CH
+__global__ void __launch_bounds__(64 * WPB) ln_fwd_kernel(const u16* __restrict__ x, const float* __restrict__ g,
+                                                          const float* __restrict__ b, u16* __restrict__ y,
+                                                          float* __restrict__ mean_out, float* __restrict__ rstd_out,
+                                                          int rows, float eps) {
+  const int lane = threadIdx.x & 63;
+  const int row = blockIdx.x * WPB + (threadIdx.x >> 6);
+  if (row >= rows) return;
+  constexpr int D = 256 * CH;
+  const u16* xr = x + (long)row * D;
+  float v[CH][4];
+  float s = 0.f;
+#pragma unroll
+  for (int c = 0; c < CH; ++c) {
+    ld4(xr + (c * 64 + lane) * 4, v[c]);
+    s += v[c][0] + v[c][1] + v[c][2] + v[c][3];
+  }
+  const float mean = warp_sum(s) * (1.f / D);
+  float q = 0.f;
+#pragma unroll
+  for (int c = 0; c < CH; ++c)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      float d = v[c][e] - mean;
+      q += d * d;
+    }
+  const float rstd = rsqrtf(warp_sum(q) * (1.f / D) + eps);
+  u16* yr = y + (long)row * D;
+#pragma unroll
+  for (int c = 0; c < CH; ++c) {
+    const int col = (c * 64 + lane) * 4;
+    f32x4 gg = *reinterpret_cast<const f32x4*>(g + col);
+    f32x4 bb = *reinterpret_cast<const f32x4*>(b + col);
+    float o[4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) o[e] = (v[c][e] - mean) * rstd * gg[e] + bb[e];
+    st4(yr + col, o);
+  }
+  if (lane == 0) {
+    mean_out[row] = mean;
+    rstd_out[row] = rstd;
+  }
+}
+
+template <int CH>
+__global__ void __launch_bounds__(64 * WPB) ln_bwd_kernel(const u16* __restrict__ dy, const u16* __restrict__ x,
+                                                          const float* __restrict__ g,
+                                                          const float* __restrict__ mean_in,
+                                                          const float* __restrict__ rstd_in, u16* __restrict__ dx,
+                                                          float* __restrict__ part, int rows, int rows_per_block) {
+  constexpr int D = 256 * CH;
+  __shared__ float red[2][WPB][D];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  float dg[CH][4], db[CH][4];
+#pragma unroll
+  for (int c = 0; c < CH; ++c)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) dg[c][e] = db[c][e] = 0.f;
+  const int r0 = blockIdx.x * rows_per_block;
+  const int r1 = min(rows, r0 + rows_per_block);
+  for (int row = r0 + w; row < r1; row += WPB) {
+    const float mean = mean_in[row], rstd = rstd_in[row];
+    float xh[CH][4], gy[CH][4];
+    float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+    for (int c = 0; c < CH; ++c) {
+      const int col = (c * 64 + lane) * 4;
+      float xv[4], dv[4];
+      ld4(x + (long)row * D + col, xv);
+      ld4(dy + (long)row * D + col, dv);
+      f32x4 gg = *reinterpret_cast<const f32x4*>(g + col);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        xh[c][e] = (xv[e] - mean) * rstd;
+        gy[c][e] = dv[e] * gg[e];
+        s1 += gy[c][e];
+        s2 += gy[c][e] * xh[c][e];
+        dg[c][e] += dv[e] * xh[c][e];
+        db[c][e] += dv[e];
+      }
+    }
+    const float m1 = warp_sum(s1) * (1.f / D), m2 = warp_sum(s2) * (1.f / D);
+#pragma unroll
+    for (int c = 0; c < CH; ++c) {
+      float o[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) o[e] = rstd * (gy[c][e] - m1 - xh[c][e] * m2);
+      st4(dx + (long)row * D + (c * 64 + lane) * 4, o);
+    }
+  }
+#pragma unroll
+  for (int c = 0; c < CH; ++c)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      red[0][w][(c * 64 + lane) * 4 + e] = dg[c][e];
+      red[1][w][(c * 64 + lane) * 4 + e] = db[c][e];
+    }
+  __syncthreads();
+  for (int col = threadIdx.x; col < D; col += 64 * WPB) {
+    float a = 0.f, bsum = 0.f;
+#pragma unroll
+    for (int k = 0; k < WPB; ++k) {
+      a += red[0][k][col];
+      bsum += red[1][k][col];
+    }
+    part[(long)blockIdx.x * D + col] = a;
+    part[(long)(gridDim.x + blockIdx.x) * D + col] = bsum;
+  }
+}
+
+// out[c] (+)= sum_r part[r][c]  for the two halves (dgamma, dbeta);
+// 256 threads = 64 columns x 4 row groups, combined through LDS.
+__global__ void __launch_bounds__(256) colsum_f32_kernel(const float* __restrict__ part, float* __restrict__ dg,
+                                                         float* __restrict__ db, int R, int D, int accumulate) {
+  __shared__ float sa[4][64], sb[4][64];
+  const int cl = threadIdx.x & 63, rg = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + cl;
+  float a = 0.f, b = 0.f;
+  if (c < D) {
+    for (int r = rg; r < R; r += 4) {
+      a += part[(long)r * D + c];
+      b += part[(long)(R + r) * D + c];
+    }
+  }
+  sa[rg][cl] = a;
+  sb[rg][cl] = b;
+  __syncthreads();
+  if (rg == 0 && c < D) {
+    a = sa[0][cl] + sa[1][cl] + sa[2][cl] + sa[3][cl];
+    b = sb[0][cl] + sb[1][cl] + sb[2][cl] + sb[3][cl];
+    dg[c] = accumulate ? dg[c] + a : a;
+    db[c] = accumulate ? db[c] + b : b;
+  }
+}
+
+// GELU (tanh approximation) backward: dz = dy * gelu'(z)
+__global__ void gelu_bwd_kernel(const u16* __restrict__ dy, const u16* __restrict__ z, u16* __restrict__ dz,
+                                long n8) {
+  for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < n8; i += (long)gridDim.x * 256) {
+    u32x4 a = reinterpret_cast<const u32x4*>(dy)[i], b = reinterpret_cast<const u32x4*>(z)[i], o;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      float r[2];
+      float gv[2] = {lo_bf(a[k]), hi_bf(a[k])}, zv[2] = {lo_bf(b[k]), hi_bf(b[k])};
+#pragma unroll
+      for (int e = 0; e < 2; ++e) {
+        const float x = zv[e];
+        const float u = 0.7978845608f * (x + 0.044715f * x * x * x);
+        const float t = tanhf(u);
+        const float du = 0.7978845608f * (1.f + 3.f * 0.044715f * x * x);
+        r[e] = gv[e] * (0.5f * (1.f + t) + 0.5f * x * (1.f - t * t) * du);
+      }
+      o[k] = pack2bf(r[0], r[1]);
+    }
+    reinterpret_cast<u32x4*>(dz)[i] = o;
+  }
+}
+
+}  // namespace
+
+PDT_API int pdt_ln_fwd(const void* x, const float* g, const float* b, void* y, float* mean, float* rstd, int rows,
+                       int D, float eps, hipStream_t st) {
+  dim3 grid((rows + WPB - 1) / WPB), blk(64 * WPB);
+  switch (D) {
+    case 256: hipLaunchKernelGGL(ln_fwd_kernel<1>, grid, blk, 0, st, (const u16*)x, g, b, (u16*)y, mean, rstd, rows, eps); break;
+    case 512: hipLaunchKernelGGL(ln_fwd_kernel<2>, grid, blk, 0, st, (const u16*)x, g, b, (u16*)y, mean, rstd, rows, eps); break;
+    case 768: hipLaunchKernelGGL(ln_fwd_kernel<3>, grid, blk, 0, st, (const u16*)x, g, b, (u16*)y, mean, rstd, rows, eps); break;
+    case 1024: hipLaunchKernelGGL(ln_fwd_kernel<4>, grid, blk, 0, st, (const u16*)x, g, b, (u16*)y, mean, rstd, rows, eps); break;
+    default: return -1;
+  }
+  PDT_RETURN_LAUNCH();
+}
+
+static int ln_rows_per_block(int rows) {
+  int rpb = 64;
+  while ((rows + rpb - 1) / rpb > 512) rpb *= 2;
+  return rpb;
+}
+
+PDT_API int pdt_ln_bwd_blocks(int rows) {
+  int rpb = ln_rows_per_block(rows);
+  int b = (rows + rpb - 1) / rpb;
+  return b < 1 ? 1 : b;
+}
+
+PDT_API int pdt_ln_bwd(const void* dy, const void* x, const float* g, const float* mean, const float* rstd, void* dx,
+                       float* dg, float* db, float* part, int rows, int D, int accumulate, hipStream_t st) {
+  const int blocks = pdt_ln_bwd_blocks(rows);
+  const int rpb = ln_rows_per_block(rows);
+  dim3 grid(blocks), blk(64 * WPB);
+  const u16 *DY = (const u16*)dy, *X = (const u16*)x;
+  u16* DX = (u16*)dx;
+  switch (D) {
+    case 256: hipLaunchKernelGGL(ln_bwd_kernel<1>, grid, blk, 0, st, DY, X, g, mean, rstd, DX, part, rows, rpb); break;
+    case 512: hipLaunchKernelGGL(ln_bwd_kernel<2>, grid, blk, 0, st, DY, X, g, mean, rstd, DX, part, rows, rpb); break;
+    case 768: hipLaunchKernelGGL(ln_bwd_kernel<3>, grid, blk, 0, st, DY, X, g, mean, rstd, DX, part, rows, rpb); break;
+    case 1024: hipLaunchKernelGGL(ln_bwd_kernel<4>, grid, blk, 0, st, DY, X, g, mean, rstd, DX, part, rows, rpb); break;
+    default: return -1;
+  }
+  int e = (int)hipGetLastError();
+  if (e) return e;
+  hipLaunchKernelGGL(colsum_f32_kernel, dim3((D + 63) / 64), dim3(256), 0, st, part, dg, db, blocks, D,
+                     accumulate);
+  PDT_RETURN_LAUNCH();
+}
+
+PDT_API int pdt_gelu_bwd(const void* dy, const void* z, void* dz, long n, hipStream_t st) {
+  if (n % 8) return -1;
+  long n8 = n / 8;
+  long b = (n8 + 255) / 256;
+  if (b > 8192) b = 8192;
+  hipLaunchKernelGGL(gelu_bwd_kernel, dim3((int)b), dim3(256), 0, st, (const u16*)dy, (const u16*)z, (u16*)dz, n8);
+  PDT_RETURN_LAUNCH();
+}

@@ -31,7 +31,11 @@ _SIGS = {
     "pdt_conv_nt_stat_rows": (c_int, [c_int, c_int, c_int, c_int]),
     "pdt_conv_nt_num_variants": (c_int, []),
     "pdt_conv_nt_resolve_variant": (c_int, [c_int, c_int, c_int, c_int]),
-    "pdt_conv_nt": (c_int, [P, P, P, P, P, P] + [c_int] * 26 + [P]),
+    "pdt_conv_nt": (c_int, [P, P, P, P, P, P] + [c_int] * 25 + [P, c_int, P]),
+    "pdt_ln_fwd": (c_int, [P, P, P, P, P, P, c_int, c_int, c_float, P]),
+    "pdt_ln_bwd_blocks": (c_int, [c_int]),
+    "pdt_ln_bwd": (c_int, [P] * 9 + [c_int, c_int, c_int, P]),
+    "pdt_gelu_bwd": (c_int, [P, P, P, c_long, P]),
     "pdt_wgrad_plan": (c_int, [c_int, c_int, c_int, ctypes.POINTER(c_int)]),
     "pdt_wgrad_workspace": (c_long, [c_int, c_int, c_int]),
     "pdt_conv_wgrad": (c_int, [P, P, P, P] + [c_int] * 16 + [c_int, c_int, c_float, c_int, P]),
@@ -190,10 +194,10 @@ def _save_tuned():
         pass
 
 
-def _nt_args(src, b, out, stats, bias, a, relu, variant, addend=None):
+def _nt_args(src, b, out, stats, bias, a, act, variant, addend=None, aux=None):
     return (_p(src), _p(b), _p(out), _p(stats), _p(bias), _p(addend), a["Hs"], a["Ws"], a["Cs"], a["Nimg"], a["Hm"], a["Wm"],
             a["Ncol"], a["K"], a["ldb"], a["sh"], a["sw"], a["oh0"], a["ow0"], a["dh"], a["dw"], a["nth"], a["ntw"],
-            a["Ho"], a["Wo"], a["osh"], a["osw"], a["oph"], a["opw"], a["ldo"], int(relu), int(variant), _s())
+            a["Ho"], a["Wo"], a["osh"], a["osw"], a["oph"], a["opw"], a["ldo"], int(act), _p(aux), int(variant), _s())
 
 
 def _check_nt(src, b, out, a):
@@ -209,7 +213,7 @@ def _check_nt(src, b, out, a):
     assert a["Nimg"] * a["Hs"] * a["Ws"] * Cs < 2 ** 31 and a["Nimg"] * a["Ho"] * a["Wo"] < 2 ** 31
 
 
-def select_nt_variant(src, b, out, *, with_stats=False, bias=None, relu=False, **a):
+def select_nt_variant(src, b, out, *, with_stats=False, bias=None, act=0, **a):
     """Variant id for this geometry (tuning it on first use when allowed)."""
     M = a["Nimg"] * a["Hm"] * a["Wm"]
     key = "nt:" + ",".join(str(a[k]) for k in ("Hs", "Ws", "Cs", "Nimg", "Hm", "Wm", "Ncol", "K", "sh", "sw",
@@ -227,7 +231,7 @@ def select_nt_variant(src, b, out, *, with_stats=False, bias=None, relu=False, *
     best, best_t = -1, float("inf")
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     for v in range(nvar):
-        args = _nt_args(src, b, out, stats, bias, a, relu, v)
+        args = _nt_args(src, b, out, stats, bias, a, act, v)
         _chk(lib.pdt_conv_nt(*args), "conv_nt(tune)")
         ev0.record()
         for _ in range(3):
@@ -242,15 +246,22 @@ def select_nt_variant(src, b, out, *, with_stats=False, bias=None, relu=False, *
     return best
 
 
-def conv_nt(src, b, out, *, stats=None, bias=None, relu=False, variant=None, addend=None, **a):
+ACT = {None: 0, "none": 0, "relu": 1, "gelu": 2}
+
+
+def conv_nt(src, b, out, *, stats=None, bias=None, relu=False, act=None, variant=None, addend=None, aux=None,
+            **a):
     """C[m, n] = sum_k A[m, k] B[n, k] (+ addend) with the implicit-GEMM gather (see csrc/conv_igemm.hip)."""
     _check_nt(src, b, out, a)
     if addend is not None:
         assert addend.dtype == torch.bfloat16 and addend.numel() == out.numel() and addend.is_contiguous(
             memory_format=torch.channels_last if addend.dim() == 4 else torch.contiguous_format)
+    act_id = ACT[act] if act is not None else (1 if relu else 0)
+    if aux is not None:
+        assert aux.dtype == torch.bfloat16 and aux.numel() == out.numel()
     if variant is None:
-        variant = select_nt_variant(src, b, out, with_stats=stats is not None, bias=bias, relu=relu, **a)
-    _chk(_load().pdt_conv_nt(*_nt_args(src, b, out, stats, bias, a, relu, variant, addend)), "conv_nt")
+        variant = select_nt_variant(src, b, out, with_stats=stats is not None, bias=bias, act=act_id, **a)
+    _chk(_load().pdt_conv_nt(*_nt_args(src, b, out, stats, bias, a, act_id, variant, addend, aux)), "conv_nt")
 
 
 def conv_stat_rows(M, Ncol, K, variant):
@@ -643,32 +654,36 @@ def global_avg_pool(x):
 # =============================================================================
 class _Linear(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, w, b, relu):
-        lib = _load()
+    def forward(ctx, x, w, b, act):
         shp = x.shape
         x2 = x.reshape(-1, shp[-1]).to(torch.bfloat16).contiguous()
         Mrows, K = x2.shape
         Nout = w.shape[0]
         wb = bf16_weight(w)
         y = torch.empty((Mrows, Nout), dtype=torch.bfloat16, device=x.device)
+        z = torch.empty_like(y) if act == "gelu" else None  # pre-activation for GELU backward
         bias = b.float().contiguous() if b is not None else None
         conv_nt(x2, wb, y, Hs=1, Ws=1, Cs=K, Nimg=Mrows, Hm=1, Wm=1, Ncol=Nout, K=K, ldb=K, sh=1, sw=1, oh0=0,
                 ow0=0, dh=1, dw=1, nth=1, ntw=1, Ho=1, Wo=1, osh=1, osw=1, oph=0, opw=0, ldo=Nout, bias=bias,
-                relu=relu)
-        ctx.save_for_backward(x2, w, y if relu else None)
-        ctx.meta = (shp, relu, b is not None)
+                act=act, aux=z)
+        ctx.save_for_backward(x2, w, y if act == "relu" else z)
+        ctx.meta = (shp, act, b is not None)
         return y.reshape(*shp[:-1], Nout)
 
     @staticmethod
     def backward(ctx, dy):
-        x2, w, yact = ctx.saved_tensors
-        shp, relu, has_b = ctx.meta
+        x2, w, saved = ctx.saved_tensors
+        shp, act, has_b = ctx.meta
         lib = _load()
         st = _s()
         Nout, K = w.shape
         dy2 = dy.reshape(-1, Nout).to(torch.bfloat16).contiguous()
-        if relu:
-            dy2 = dy2 * (yact > 0)
+        if act == "relu":
+            dy2 = dy2 * (saved > 0)
+        elif act == "gelu":
+            dz = torch.empty_like(dy2)
+            _chk(lib.pdt_gelu_bwd(_p(dy2), _p(saved), _p(dz), dz.numel(), st), "gelu_bwd")
+            dy2 = dz
         Mrows = dy2.shape[0]
         dx = None
         if ctx.needs_input_grad[0]:
@@ -693,10 +708,53 @@ class _Linear(torch.autograd.Function):
 def linear(x, fc: nn.Linear, act=None, fp8=False):
     K = fc.in_features
     N = fc.out_features
-    if K % 8 or N % 8 or act not in (None, "relu"):
+    if K % 8 or N % 8 or act not in (None, "relu", "gelu"):
         from .fused import _torch_linear
         return _torch_linear(x, fc, act)
-    return _Linear.apply(x, fc.weight, fc.bias, act == "relu")
+    return _Linear.apply(x, fc.weight, fc.bias, act)
+
+
+# =============================================================================
+# LayerNorm (bf16 activations, fp32 affine params)
+# =============================================================================
+class _LayerNorm(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, g, b, eps):
+        shp = x.shape
+        D = shp[-1]
+        x2 = x.reshape(-1, D).to(torch.bfloat16).contiguous()
+        rows = x2.shape[0]
+        y = torch.empty_like(x2)
+        stats = torch.empty((2, rows), dtype=torch.float32, device=x.device)
+        gf = g.float().contiguous()
+        bf = b.float().contiguous()
+        _chk(_load().pdt_ln_fwd(_p(x2), _p(gf), _p(bf), _p(y), _p(stats[0]), _p(stats[1]), rows, D, float(eps),
+                                _s()), "ln_fwd")
+        ctx.save_for_backward(x2, gf, stats)
+        ctx.shp = shp
+        return y.reshape(shp)
+
+    @staticmethod
+    def backward(ctx, dy):
+        x2, gf, stats = ctx.saved_tensors
+        rows, D = x2.shape
+        lib = _load()
+        dy2 = dy.reshape(rows, D).to(torch.bfloat16).contiguous()
+        dx = torch.empty_like(x2)
+        blocks = lib.pdt_ln_bwd_blocks(rows)
+        part = torch.empty(2 * blocks * D, dtype=torch.float32, device=dy.device)
+        dg = torch.empty(D, dtype=torch.float32, device=dy.device)
+        db = torch.empty(D, dtype=torch.float32, device=dy.device)
+        _chk(lib.pdt_ln_bwd(_p(dy2), _p(x2), _p(gf), _p(stats[0]), _p(stats[1]), _p(dx), _p(dg), _p(db), _p(part),
+                            rows, D, 0, _s()), "ln_bwd")
+        return dx.reshape(ctx.shp), dg, db, None
+
+
+def layer_norm(x, ln):
+    D = ln.normalized_shape[-1]
+    if len(ln.normalized_shape) != 1 or D not in (256, 512, 768, 1024) or not ln.elementwise_affine:
+        return ln(x)
+    return _LayerNorm.apply(x, ln.weight, ln.bias, ln.eps)
 
 
 # =============================================================================
@@ -742,14 +800,57 @@ def softmax_cross_entropy(logits, target, label_smoothing=0.0):
 # =============================================================================
 # ViT ops (torch path for now on GPU as well; native kernels land in ops/vit_ops)
 # =============================================================================
-def layer_norm(x, ln):
-    return ln(x)
-
-
 def attention(q, k, v):
     return torch.nn.functional.scaled_dot_product_attention(q, k, v)
 
 
+class _PatchEmbed(torch.autograd.Function):
+    """Non-overlapping patch conv as an implicit GEMM whose NHWC output IS the
+    [B, N_patches, D] token matrix (no transpose pass)."""
+
+    @staticmethod
+    def forward(ctx, x, w, b, conv):
+        N, C, H, W = x.shape
+        Cs = C if C % 8 == 0 else 8
+        x = x.to(torch.bfloat16)
+        if Cs != C:
+            x = torch.nn.functional.pad(_cl(x).permute(0, 2, 3, 1), (0, Cs - C)).permute(0, 3, 1, 2)
+        x = _cl(x)
+        Cout = w.shape[0]
+        g = _fwd_geom(N, H, W, Cs, conv)
+        wb = bf16_weight(w, pad_cin_to=Cs if Cs != C else None)
+        y = _empty_cl(N, Cout, g["Ho"], g["Wo"], torch.bfloat16, x.device)
+        conv_nt(x, wb, y, bias=b.float().contiguous() if b is not None else None,
+                **_fwd_nt_geom(N, H, W, Cs, Cout, g))
+        u = _Unit()
+        u.x, u.w, u.N, u.C, u.Cs, u.H, u.W, u.Cout, u.g = x, w, N, C, Cs, H, W, Cout, g
+        ctx.u = u
+        ctx.has_b = b is not None
+        return y.permute(0, 2, 3, 1).reshape(N, g["Ho"] * g["Wo"], Cout)
+
+    @staticmethod
+    def backward(ctx, dtok):
+        u = ctx.u
+        N, Cout = u.N, u.Cout
+        dy = dtok.to(torch.bfloat16).reshape(N, u.g["Ho"], u.g["Wo"], Cout).permute(0, 3, 1, 2)
+        dy = _cl(dy)
+        dw = _unit_dw(dy, u) if ctx.needs_input_grad[1] else None
+        db = None
+        if ctx.has_b and ctx.needs_input_grad[2]:
+            db = torch.empty(Cout, dtype=torch.float32, device=dy.device)
+            _chk(_load().pdt_colsum(_p(dy), _p(db), N * u.g["Ho"] * u.g["Wo"], Cout, 0, _s()), "colsum")
+        dx = None
+        if ctx.needs_input_grad[0]:
+            dx = _unit_dx(dy, u)
+        del ctx.u
+        return dx, dw, db, None
+
+
 def patch_embed(x, conv):
-    y = conv(x)
-    return y.flatten(2).transpose(1, 2)
+    KH, KW = conv.kernel_size
+    if (conv.stride != conv.kernel_size or conv.padding != (0, 0) or conv.out_channels % 8 or conv.groups != 1
+            or conv.dilation != (1, 1) or x.dim() != 4 or x.shape[2] % KH or x.shape[3] % KW
+            or (x.shape[1] % 8 and x.shape[1] > 8)):
+        y = conv(x)
+        return y.flatten(2).transpose(1, 2)
+    return _PatchEmbed.apply(x, conv.weight, conv.bias, conv)

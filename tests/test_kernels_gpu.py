@@ -337,3 +337,58 @@ def test_fused_bottleneck_matches_unit_composition(stride, ds):
     assert nrmerr(dx1, dx2) < 1e-2
     for a, b in zip(g1, g2):
         assert nrmerr(a, b) < 1e-2
+
+
+def test_layernorm_gelu_linear_patch_embed():
+    torch.manual_seed(8)
+    ln = nn.LayerNorm(768, eps=1e-6).cuda()
+    with torch.no_grad():
+        ln.weight.uniform_(0.5, 1.5)
+        ln.bias.uniform_(-0.2, 0.2)
+    x = torch.randn(2, 197, 768, device="cuda").to(torch.bfloat16).requires_grad_(True)
+    y = no.layer_norm(x, ln)
+    xr = x.detach().float().requires_grad_(True)
+    yr = F.layer_norm(xr, (768,), ln.weight, ln.bias, 1e-6)
+    assert nrmerr(y, yr) < 1e-2
+    g = torch.randn_like(yr).to(torch.bfloat16)
+    y.backward(g)
+    gw = ln.weight.grad.clone()
+    ln.weight.grad = None
+    yr.backward(g.float())
+    assert nrmerr(x.grad, xr.grad) < 2e-2
+    assert nrmerr(gw, ln.weight.grad) < 2e-2
+    # GEMM + bias + GELU epilogue (pre-activation kept for backward)
+    fc = nn.Linear(768, 3072).cuda()
+    h = torch.randn(394, 768, device="cuda").to(torch.bfloat16).requires_grad_(True)
+    o = no.linear(h, fc, act="gelu")
+    hr = h.detach().float().requires_grad_(True)
+    w_r = fc.weight.detach().to(torch.bfloat16).float().requires_grad_(True)
+    orf = F.gelu(F.linear(hr, w_r, fc.bias.detach()), approximate="tanh")
+    assert nrmerr(o, orf) < 1e-2
+    go = torch.randn_like(orf).to(torch.bfloat16)
+    o.backward(go)
+    orf.backward(go.float())
+    assert nrmerr(h.grad, hr.grad) < 2e-2
+    assert nrmerr(fc.weight.grad, w_r.grad) < 2e-2
+    # patch embedding (16x16 stride 16, 3 -> 768 channels, bias)
+    pe = nn.Conv2d(3, 768, 16, 16).cuda()
+    img = _cl(torch.randn(2, 3, 224, 224, device="cuda").to(torch.bfloat16))
+    tok = no.patch_embed(img, pe)
+    ref = F.conv2d(img.float(), pe.weight.detach().to(torch.bfloat16).float(), pe.bias.detach(), 16)
+    ref = ref.flatten(2).transpose(1, 2)
+    assert tok.shape == (2, 196, 768) and nrmerr(tok, ref) < 1e-2
+
+
+def test_vit_native_train_step():
+    from pytorch_distributed_template_amd.models.vit import VisionTransformer
+    from pytorch_distributed_template_amd.ops import fused
+    torch.manual_seed(9)
+    m = VisionTransformer(depth=2).cuda()
+    x = _cl(torch.randn(4, 3, 224, 224, device="cuda").to(torch.bfloat16))
+    t = torch.randint(0, 1000, (4,), device="cuda")
+    fused.set_backend("native")
+    loss = fused.softmax_cross_entropy(m(x), t)
+    loss.backward()
+    fused.set_backend("auto")
+    assert torch.isfinite(loss)
+    assert all(p.grad is not None and torch.isfinite(p.grad).all() for p in m.parameters() if p.requires_grad)
