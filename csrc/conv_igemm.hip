@@ -53,7 +53,7 @@ constexpr int NT = 256;
 
 __device__ __forceinline__ int swz(int row, int chunk) { return chunk ^ ((row >> 1) & 7); }
 
-template <int BM, int BN, int NSTAGE, bool CS64>
+template <int BM, int BN, int NSTAGE, bool CS64, bool DIRECT>
 __global__ void __launch_bounds__(NT, 2) conv_nt_kernel(NTParams p) {
   constexpr int MI = BM / 32;  // 16-row MFMA tiles per wave (wave covers BM/2 rows)
   constexpr int NI = BN / 32;
@@ -61,7 +61,8 @@ __global__ void __launch_bounds__(NT, 2) conv_nt_kernel(NTParams p) {
   constexpr int B_BYTES = BN * BK * 2;
   constexpr int STAGE = A_BYTES + B_BYTES;
   constexpr int C_STRIDE = BN * 2 + 16;  // bytes per staged output row
-  constexpr int SMEM = (NSTAGE * STAGE > BM * C_STRIDE) ? NSTAGE * STAGE : BM * C_STRIDE;
+  constexpr int CST = DIRECT ? 0 : BM * C_STRIDE;  // epilogue staging bytes
+  constexpr int SMEM = (NSTAGE * STAGE > CST) ? NSTAGE * STAGE : CST;
   __shared__ __attribute__((aligned(16))) char smem[SMEM];
 
   const int tid = threadIdx.x;
@@ -215,7 +216,7 @@ __global__ void __launch_bounds__(NT, 2) conv_nt_kernel(NTParams p) {
       __syncthreads();
     }
   }
-  if (NSTAGE == 1) __syncthreads();  // before the epilogue reuses LDS
+  if (NSTAGE == 1 && !DIRECT) __syncthreads();  // before the epilogue reuses LDS
 
   // ---------------------------------------------------------------- epilogue
   // acc[i][j][r] = C[row = wm*BM/2 + i*16 + (lane&15)][col = wn*BN/2 + j*16 + (lane>>4)*4 + r]
@@ -276,7 +277,40 @@ __global__ void __launch_bounds__(NT, 2) conv_nt_kernel(NTParams p) {
   // stage the bf16 tile through LDS (row-major [BM][BN], 16-B row pad) and
   // write 16-B coalesced rows; `pre` = pre-activation copy (aux output)
   constexpr int CPR = BN / 8;  // 16-B chunks per row
+  // DIRECT: each lane stores its 4 consecutive channels (8 B) straight to HBM
+  // (no LDS round trip / barrier); L2 merges the 32-B row pieces into lines.
+  auto direct_store = [&](u16* dst, const u16* addend) {
+#pragma unroll
+    for (int i = 0; i < MI; ++i) {
+      int m = m0 + wm * (BM / 2) + i * 16 + lrow;
+      if (m >= p.M) continue;
+      uint32_t img = fdiv(m, p.div_HWm);
+      uint32_t rem = m - img * (uint32_t)(p.Hm * p.Wm);
+      uint32_t oh = fdiv(rem, p.div_Wm);
+      uint32_t ow = rem - oh * p.Wm;
+      size_t orow = ((size_t)img * p.Ho + oh * p.osh + p.oph) * p.Wo + ow * p.osw + p.opw;
+#pragma unroll
+      for (int j = 0; j < NI; ++j) {
+        int col = n0 + wn * (BN / 2) + j * 16 + lcol;
+        if (col >= p.Ncol) continue;
+        float v0 = acc[i][j][0], v1 = acc[i][j][1], v2 = acc[i][j][2], v3 = acc[i][j][3];
+        if (addend != nullptr) {
+          uint2 a = *reinterpret_cast<const uint2*>(addend + orow * p.ldo + col);
+          v0 += lo_bf(a.x); v1 += hi_bf(a.x); v2 += lo_bf(a.y); v3 += hi_bf(a.y);
+        }
+        uint2 w;
+        w.x = pack2bf(v0, v1);
+        w.y = pack2bf(v2, v3);
+        *reinterpret_cast<uint2*>(dst + orow * p.ldo + col) = w;
+      }
+    }
+  };
+
   auto stage_store = [&](u16* dst, const u16* addend) {
+    if (DIRECT) {
+      direct_store(dst, addend);
+      return;
+    }
 #pragma unroll
     for (int i = 0; i < MI; ++i) {
 #pragma unroll
@@ -315,7 +349,7 @@ __global__ void __launch_bounds__(NT, 2) conv_nt_kernel(NTParams p) {
 
   if (p.aux != nullptr) {
     stage_store(p.aux, nullptr);
-    __syncthreads();
+    if (!DIRECT) __syncthreads();
   }
   if (p.act != 0) {
 #pragma unroll
@@ -337,18 +371,21 @@ __global__ void __launch_bounds__(NT, 2) conv_nt_kernel(NTParams p) {
   stage_store(p.out, p.addend);
 }
 
-template <int BM, int BN, int NS, bool CS64>
+template <int BM, int BN, int NS, bool CS64, bool DIRECT>
 int launch(const NTParams& p, hipStream_t st) {
   int ntm = (p.M + BM - 1) / BM, ntn = (p.Ncol + BN - 1) / BN;
-  hipLaunchKernelGGL((conv_nt_kernel<BM, BN, NS, CS64>), dim3(ntm * ntn), dim3(NT), 0, st, p);
+  hipLaunchKernelGGL((conv_nt_kernel<BM, BN, NS, CS64, DIRECT>), dim3(ntm * ntn), dim3(NT), 0, st, p);
   PDT_RETURN_LAUNCH();
 }
 
 // Tile variants (autotuned per shape from Python; -1 = built-in heuristic).
 //   id : BM x BN, LDS stages
-constexpr int NVAR = 10;
-constexpr int VAR_BM[NVAR] = {128, 256, 64, 128, 64, 128, 256, 64, 128, 64};
-constexpr int VAR_BN[NVAR] = {128, 64, 128, 64, 64, 128, 64, 128, 64, 64};
+//   ids 10..19 : the same tiles with the direct (no LDS staging) epilogue
+constexpr int NVAR = 20;
+constexpr int VAR_BM[NVAR] = {128, 256, 64, 128, 64, 128, 256, 64, 128, 64,
+                              128, 256, 64, 128, 64, 128, 256, 64, 128, 64};
+constexpr int VAR_BN[NVAR] = {128, 64, 128, 64, 64, 128, 64, 128, 64, 64,
+                              128, 64, 128, 64, 64, 128, 64, 128, 64, 64};
 
 int heuristic_variant(int M, int Ncol, int K) {
   (void)M;
@@ -359,16 +396,26 @@ int heuristic_variant(int M, int Ncol, int K) {
 template <bool CS64>
 int launch_variant(int v, const NTParams& p, hipStream_t st) {
   switch (v) {
-    case 0: return launch<128, 128, 2, CS64>(p, st);
-    case 1: return launch<256, 64, 2, CS64>(p, st);
-    case 2: return launch<64, 128, 2, CS64>(p, st);
-    case 3: return launch<128, 64, 2, CS64>(p, st);
-    case 4: return launch<64, 64, 2, CS64>(p, st);
-    case 5: return launch<128, 128, 1, CS64>(p, st);
-    case 6: return launch<256, 64, 1, CS64>(p, st);
-    case 7: return launch<64, 128, 1, CS64>(p, st);
-    case 8: return launch<128, 64, 1, CS64>(p, st);
-    case 9: return launch<64, 64, 1, CS64>(p, st);
+    case 0: return launch<128, 128, 2, CS64, false>(p, st);
+    case 1: return launch<256, 64, 2, CS64, false>(p, st);
+    case 2: return launch<64, 128, 2, CS64, false>(p, st);
+    case 3: return launch<128, 64, 2, CS64, false>(p, st);
+    case 4: return launch<64, 64, 2, CS64, false>(p, st);
+    case 5: return launch<128, 128, 1, CS64, false>(p, st);
+    case 6: return launch<256, 64, 1, CS64, false>(p, st);
+    case 7: return launch<64, 128, 1, CS64, false>(p, st);
+    case 8: return launch<128, 64, 1, CS64, false>(p, st);
+    case 9: return launch<64, 64, 1, CS64, false>(p, st);
+    case 10: return launch<128, 128, 2, CS64, true>(p, st);
+    case 11: return launch<256, 64, 2, CS64, true>(p, st);
+    case 12: return launch<64, 128, 2, CS64, true>(p, st);
+    case 13: return launch<128, 64, 2, CS64, true>(p, st);
+    case 14: return launch<64, 64, 2, CS64, true>(p, st);
+    case 15: return launch<128, 128, 1, CS64, true>(p, st);
+    case 16: return launch<256, 64, 1, CS64, true>(p, st);
+    case 17: return launch<64, 128, 1, CS64, true>(p, st);
+    case 18: return launch<128, 64, 1, CS64, true>(p, st);
+    case 19: return launch<64, 64, 1, CS64, true>(p, st);
   }
   return -3;
 }

@@ -70,7 +70,7 @@ __device__ __forceinline__ bf16x8 tr_frag(const char* base, int krow0, int col0,
   return r;
 }
 
-template <int BM, int BN>
+template <int BM, int BN, int NSTAGE>
 __global__ void __launch_bounds__(NT, 2) wgrad_kernel(WGParams p) {
   constexpr int RBA = BM * 2;   // bytes per A row (co)
   constexpr int RBB = BN * 2;   // bytes per B row (tap,c)
@@ -85,7 +85,7 @@ __global__ void __launch_bounds__(NT, 2) wgrad_kernel(WGParams p) {
   constexpr int NB = BK / BROWS;
   constexpr int MI = BM / 32;          // co 16-tiles per wave
   constexpr int NI = BN / 32;          // tc 16-tiles per wave
-  __shared__ __attribute__((aligned(16))) char smem[2 * STAGE];
+  __shared__ __attribute__((aligned(16))) char smem[NSTAGE * STAGE];
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave >> 1, wn = wave & 1;
@@ -167,7 +167,7 @@ __global__ void __launch_bounds__(NT, 2) wgrad_kernel(WGParams p) {
   }
   __syncthreads();
   for (int kt = kt_begin; kt < kt_end; ++kt) {
-    const int cur = (kt - kt_begin) & 1;
+    const int cur = NSTAGE == 2 ? ((kt - kt_begin) & 1) : 0;
     if (kt + 1 < kt_end) load_tile(kt + 1);
     const char* sa = smem + cur * STAGE;
     const char* sb = sa + A_BYTES;
@@ -185,8 +185,14 @@ __global__ void __launch_bounds__(NT, 2) wgrad_kernel(WGParams p) {
           // D[tc][co]: lane holds 4 consecutive tc of one co
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[j], af[i], acc[i][j], 0, 0, 0);
     }
-    if (kt + 1 < kt_end) store_tile(cur ^ 1);
-    __syncthreads();
+    if (NSTAGE == 2) {
+      if (kt + 1 < kt_end) store_tile(cur ^ 1);
+      __syncthreads();
+    } else if (kt + 1 < kt_end) {
+      __syncthreads();
+      store_tile(0);
+      __syncthreads();
+    }
   }
 
   float* out = p.slab + (size_t)split * p.Mo * p.No;
@@ -231,14 +237,34 @@ __global__ void wgrad_reduce1_kernel(const float* __restrict__ slab, float* __re
 
 }  // namespace
 
-// Plan: number of splits for a given problem so the grid covers the chip
-// (~4 workgroups per CU); returns splits and writes ktiles_per_split.
-PDT_API int pdt_wgrad_plan(int M, int Mo, int No, int* ktiles_per_split) {
-  int BM = Mo <= 64 ? 64 : 128;
-  int BN = No <= 64 ? 64 : 128;
+// Variants: v = tile * 3 + cfg; tile in {64x64, 64x128, 128x64, 128x128} (Mo x No),
+// cfg: 0 = 2 LDS stages / ~1024 workgroups, 1 = 1 stage / ~1024, 2 = 1 stage / ~2048.
+// -1 = heuristic (tile from Mo/No, cfg 0). Autotuned per shape from Python.
+constexpr int WG_NVAR = 12;
+static void wg_variant(int v, int Mo, int No, int* BM, int* BN, int* NS, int* target) {
+  if (v < 0 || v >= WG_NVAR) {
+    *BM = Mo <= 64 ? 64 : 128;
+    *BN = No <= 64 ? 64 : 128;
+    *NS = 2;
+    *target = 1024;
+    return;
+  }
+  const int tile = v / 3, cfg = v % 3;
+  *BM = (tile >= 2) ? 128 : 64;
+  *BN = (tile & 1) ? 128 : 64;
+  *NS = cfg == 0 ? 2 : 1;
+  *target = cfg == 2 ? 2048 : 1024;
+}
+
+PDT_API int pdt_wgrad_num_variants() { return WG_NVAR; }
+
+// Plan: number of splits so the grid covers the chip; returns splits and
+// writes ktiles_per_split.
+PDT_API int pdt_wgrad_plan(int M, int Mo, int No, int variant, int* ktiles_per_split) {
+  int BM, BN, NS, target;
+  wg_variant(variant, Mo, No, &BM, &BN, &NS, &target);
   int tiles = ((Mo + BM - 1) / BM) * ((No + BN - 1) / BN);
   int nk = (M + BK - 1) / BK;
-  int target = 1024;
   int splits = (target + tiles - 1) / tiles;
   if (splits > nk) splits = nk;
   if (splits < 1) splits = 1;
@@ -263,7 +289,7 @@ PDT_API long pdt_wgrad_workspace(int splits, int Mo, int No) {
 PDT_API int pdt_conv_wgrad(const void* dy, const void* x, float* slab, float* out, int M, int Mo, int No,
                            int ldy, int Hs, int Ws, int C, int Hm, int Wm, int sh, int sw, int oh0, int ow0,
                            int dh, int dw, int ntw, int splits, int ktiles_per_split, float scale,
-                           int accumulate, hipStream_t stream) {
+                           int accumulate, int variant, hipStream_t stream) {
   if (C % 8 != 0 || Mo % 8 != 0 || No % 8 != 0 || ldy % 8 != 0) return -1;
   WGParams p;
   p.dy = (const u16*)dy;
@@ -277,18 +303,23 @@ PDT_API int pdt_conv_wgrad(const void* dy, const void* x, float* slab, float* ou
   p.div_HWm = make_fastdiv(Hm * Wm);
   p.div_C = make_fastdiv(C);
   p.div_ntw = make_fastdiv(ntw);
-  int BM = Mo <= 64 ? 64 : 128;
-  int BN = No <= 64 ? 64 : 128;
+  int BM, BN, NS, target;
+  wg_variant(variant, Mo, No, &BM, &BN, &NS, &target);
   int tiles = ((Mo + BM - 1) / BM) * ((No + BN - 1) / BN);
   dim3 grid(tiles * splits);
-  if (BM == 64 && BN == 64)
-    hipLaunchKernelGGL((wgrad_kernel<64, 64>), grid, dim3(NT), 0, stream, p);
-  else if (BM == 64)
-    hipLaunchKernelGGL((wgrad_kernel<64, 128>), grid, dim3(NT), 0, stream, p);
-  else if (BN == 64)
-    hipLaunchKernelGGL((wgrad_kernel<128, 64>), grid, dim3(NT), 0, stream, p);
-  else
-    hipLaunchKernelGGL((wgrad_kernel<128, 128>), grid, dim3(NT), 0, stream, p);
+#define WG_LAUNCH(a, b, c) hipLaunchKernelGGL((wgrad_kernel<a, b, c>), grid, dim3(NT), 0, stream, p)
+  if (NS == 2) {
+    if (BM == 64 && BN == 64) WG_LAUNCH(64, 64, 2);
+    else if (BM == 64) WG_LAUNCH(64, 128, 2);
+    else if (BN == 64) WG_LAUNCH(128, 64, 2);
+    else WG_LAUNCH(128, 128, 2);
+  } else {
+    if (BM == 64 && BN == 64) WG_LAUNCH(64, 64, 1);
+    else if (BM == 64) WG_LAUNCH(64, 128, 1);
+    else if (BN == 64) WG_LAUNCH(128, 64, 1);
+    else WG_LAUNCH(128, 128, 1);
+  }
+#undef WG_LAUNCH
   int e = (int)hipGetLastError();
   if (e) return e;
   long n4 = (long)Mo * No / 4;

@@ -36,9 +36,10 @@ _SIGS = {
     "pdt_ln_bwd_blocks": (c_int, [c_int]),
     "pdt_ln_bwd": (c_int, [P] * 9 + [c_int, c_int, c_int, P]),
     "pdt_gelu_bwd": (c_int, [P, P, P, c_long, P]),
-    "pdt_wgrad_plan": (c_int, [c_int, c_int, c_int, ctypes.POINTER(c_int)]),
+    "pdt_wgrad_plan": (c_int, [c_int, c_int, c_int, c_int, ctypes.POINTER(c_int)]),
+    "pdt_wgrad_num_variants": (c_int, []),
     "pdt_wgrad_workspace": (c_long, [c_int, c_int, c_int]),
-    "pdt_conv_wgrad": (c_int, [P, P, P, P] + [c_int] * 16 + [c_int, c_int, c_float, c_int, P]),
+    "pdt_conv_wgrad": (c_int, [P, P, P, P] + [c_int] * 16 + [c_int, c_int, c_float, c_int, c_int, P]),
     "pdt_bn_stats_blocks": (c_int, [c_long, c_int]),
     "pdt_rows_reduce_workspace": (c_long, [c_int, c_int]),
     "pdt_bn_stats": (c_int, [P, P, c_long, c_int, c_int, P]),
@@ -216,7 +217,7 @@ def _check_nt(src, b, out, a):
 def select_nt_variant(src, b, out, *, with_stats=False, bias=None, act=0, **a):
     """Variant id for this geometry (tuning it on first use when allowed)."""
     M = a["Nimg"] * a["Hm"] * a["Wm"]
-    key = "nt:" + ",".join(str(a[k]) for k in ("Hs", "Ws", "Cs", "Nimg", "Hm", "Wm", "Ncol", "K", "sh", "sw",
+    key = "nt2:" + ",".join(str(a[k]) for k in ("Hs", "Ws", "Cs", "Nimg", "Hm", "Wm", "Ncol", "K", "sh", "sw",
                                                  "nth", "ntw", "osh")) + f",{int(with_stats)},{int(bias is not None)}"
     table = _tuned()
     if key in table:
@@ -268,20 +269,49 @@ def conv_stat_rows(M, Ncol, K, variant):
     return _load().pdt_conv_nt_stat_rows(M, Ncol, K, variant)
 
 
-def conv_wgrad(dy, x, out, *, M, Mo, No, ldy, Hs, Ws, C, Hm, Wm, sh, sw, oh0, ow0, dh, dw, ntw, scale=1.0,
-               accumulate=False):
+def _wgrad_launch(lib, dy, x, out, v, scale, accumulate, a):
+    kps = c_int(0)
+    splits = lib.pdt_wgrad_plan(a["M"], a["Mo"], a["No"], v, ctypes.byref(kps))
+    slab = torch.empty(lib.pdt_wgrad_workspace(splits, a["Mo"], a["No"]), dtype=torch.float32, device=dy.device)
+    rc = lib.pdt_conv_wgrad(_p(dy), _p(x), _p(slab), _p(out), a["M"], a["Mo"], a["No"], a["ldy"], a["Hs"], a["Ws"],
+                            a["C"], a["Hm"], a["Wm"], a["sh"], a["sw"], a["oh0"], a["ow0"], a["dh"], a["dw"],
+                            a["ntw"], splits, kps.value, float(scale), int(accumulate), int(v), _s())
+    _chk(rc, "conv_wgrad")
+
+
+def conv_wgrad(dy, x, out, *, scale=1.0, accumulate=False, variant=None, **a):
+    """dW[co, tap*C + c] = sum_m dY[m, co] X_gather[m, (tap, c)] (see csrc/conv_wgrad.hip)."""
+    M, Mo, No, ldy, C, Hm, Wm = a["M"], a["Mo"], a["No"], a["ldy"], a["C"], a["Hm"], a["Wm"]
     assert dy.dtype == torch.bfloat16 and x.dtype == torch.bfloat16 and out.dtype == torch.float32
     assert C % 8 == 0 and Mo % 8 == 0 and No % 8 == 0 and ldy % 8 == 0
     assert out.numel() >= Mo * No and dy.numel() >= M * ldy
-    assert M % (Hm * Wm) == 0 and x.numel() >= (M // (Hm * Wm)) * Hs * Ws * C, "wgrad source too small"
-    assert ntw >= 1 and No % C == 0
+    assert M % (Hm * Wm) == 0 and x.numel() >= (M // (Hm * Wm)) * a["Hs"] * a["Ws"] * C, "wgrad source too small"
+    assert a["ntw"] >= 1 and No % C == 0
     lib = _load()
-    kps = c_int(0)
-    splits = lib.pdt_wgrad_plan(M, Mo, No, ctypes.byref(kps))
-    slab = torch.empty(lib.pdt_wgrad_workspace(splits, Mo, No), dtype=torch.float32, device=dy.device)
-    rc = lib.pdt_conv_wgrad(_p(dy), _p(x), _p(slab), _p(out), M, Mo, No, ldy, Hs, Ws, C, Hm, Wm, sh, sw, oh0,
-                            ow0, dh, dw, ntw, splits, kps.value, float(scale), int(accumulate), _s())
-    _chk(rc, "conv_wgrad")
+    if variant is None:
+        key = "wg:" + ",".join(str(a[k]) for k in ("M", "Mo", "No", "Hs", "Ws", "C", "Hm", "Wm", "sh", "ntw"))
+        table = _tuned()
+        if key in table:
+            variant = int(table[key])
+        elif os.environ.get("PDT_AUTOTUNE", "1") == "0" or torch.cuda.is_current_stream_capturing():
+            variant = -1
+        else:
+            ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            best, best_t = -1, float("inf")
+            for v in range(lib.pdt_wgrad_num_variants()):
+                _wgrad_launch(lib, dy, x, out, v, scale, False, a)
+                ev0.record()
+                for _ in range(3):
+                    _wgrad_launch(lib, dy, x, out, v, scale, False, a)
+                ev1.record()
+                ev1.synchronize()
+                t = ev0.elapsed_time(ev1)
+                if t < best_t:
+                    best, best_t = v, t
+            table[key] = best
+            _save_tuned()
+            variant = best
+    _wgrad_launch(lib, dy, x, out, variant, scale, accumulate, a)
 
 
 def fill_uniform_(t: torch.Tensor, seed: int):

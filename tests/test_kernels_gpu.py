@@ -88,6 +88,13 @@ def test_conv_fwd_dgrad_wgrad(shape):
     no._conv_wgrad(dy, xs, N, H, W, Cs, Cout, g, dw)
     rdw = torch.nn.grad.conv2d_weight(x.float(), wr.shape, dy.float(), s, p)
     assert relerr(dw[:, :Cin], rdw) < 1e-2
+    # every wgrad variant the autotuner may pick
+    wa = dict(M=N * g["Ho"] * g["Wo"], Mo=Cout, No=k * k * Cs, ldy=Cout, Hs=H, Ws=W, C=Cs, Hm=g["Ho"], Wm=g["Wo"],
+              sh=s, sw=s, oh0=-p, ow0=-p, dh=1, dw=1, ntw=k)
+    for v in range(no._load().pdt_wgrad_num_variants()):
+        dwv = torch.zeros_like(dw)
+        no.conv_wgrad(dy, xs, dwv, variant=v, **wa)
+        assert relerr(dwv[:, :Cin], rdw) < 1e-2, v
 
 
 @pytest.mark.parametrize("relu,res", [(True, False), (True, True), (False, False)])
