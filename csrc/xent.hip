@@ -84,12 +84,29 @@ __global__ void xent_bwd_kernel(const void* __restrict__ logits, const long* __r
   }
 }
 
-// out[c] = (acc ? out[c] : 0) + sum_r x[r][c]   (bf16 x, fp32 out)
-__global__ void colsum_kernel(const u16* __restrict__ x, float* __restrict__ out, int R, int C, int acc) {
+// Column sums of a bf16 [R][C] matrix into fp32 (bias gradients):
+// stage 1: grid (ceil(C/64), G) blocks of 256 threads = 64 columns x 4 row
+//          lanes; block (x, g) sums rows g*rpb .. (g+1)*rpb -> part[g][C]
+// stage 2: out[c] = (acc ? out[c] : 0) + sum_g part[g][c]
+__global__ void __launch_bounds__(256) colsum1_kernel(const u16* __restrict__ x, float* __restrict__ part, int R,
+                                                      int C, int rpb) {
+  __shared__ float red[4][64];
+  const int cl = threadIdx.x & 63, rg = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + cl;
+  const int r0 = blockIdx.y * rpb, r1 = min(R, r0 + rpb);
+  float s = 0.f;
+  if (c < C)
+    for (int r = r0 + rg; r < r1; r += 4) s += bf2f(x[(long)r * C + c]);
+  red[rg][cl] = s;
+  __syncthreads();
+  if (rg == 0 && c < C) part[(long)blockIdx.y * C + c] = red[0][cl] + red[1][cl] + red[2][cl] + red[3][cl];
+}
+
+__global__ void colsum2_kernel(const float* __restrict__ part, float* __restrict__ out, int G, int C, int acc) {
   int c = blockIdx.x * blockDim.x + threadIdx.x;
   if (c >= C) return;
   float s = 0.f;
-  for (int r = 0; r < R; ++r) s += bf2f(x[(long)r * C + c]);
+  for (int g = 0; g < G; ++g) s += part[(long)g * C + c];
   out[c] = acc ? out[c] + s : s;
 }
 
@@ -117,7 +134,20 @@ PDT_API int pdt_xent_bwd(const void* logits, int bf16, const long* target, const
   PDT_RETURN_LAUNCH();
 }
 
-PDT_API int pdt_colsum(const void* x, float* out, int R, int C, int acc, hipStream_t st) {
-  hipLaunchKernelGGL(colsum_kernel, dim3((C + 255) / 256), dim3(256), 0, st, (const u16*)x, out, R, C, acc);
+// workspace floats pdt_colsum needs
+PDT_API long pdt_colsum_workspace(int R, int C) {
+  int G = (R + 255) / 256;
+  if (G > 128) G = 128;
+  if (G < 1) G = 1;
+  return (long)G * C;
+}
+
+PDT_API int pdt_colsum(const void* x, float* out, float* work, int R, int C, int acc, hipStream_t st) {
+  int G = (R + 255) / 256;
+  if (G > 128) G = 128;
+  if (G < 1) G = 1;
+  int rpb = (R + G - 1) / G;
+  hipLaunchKernelGGL(colsum1_kernel, dim3((C + 63) / 64, G), dim3(256), 0, st, (const u16*)x, work, R, C, rpb);
+  hipLaunchKernelGGL(colsum2_kernel, dim3((C + 255) / 256), dim3(256), 0, st, work, out, G, C, acc);
   PDT_RETURN_LAUNCH();
 }

@@ -54,7 +54,8 @@ _SIGS = {
     "pdt_avgpool_bwd": (c_int, [P, P, c_int, c_int, c_int, P]),
     "pdt_xent_fwd": (c_int, [P, c_int, P, P, P, P, c_int, c_int, c_float, P]),
     "pdt_xent_bwd": (c_int, [P, c_int, P, P, P, P, c_int, c_int, c_float, P]),
-    "pdt_colsum": (c_int, [P, P, c_int, c_int, c_int, P]),
+    "pdt_colsum": (c_int, [P, P, P, c_int, c_int, c_int, P]),
+    "pdt_colsum_workspace": (c_long, [c_int, c_int]),
     "pdt_chunk_struct_size": (c_int, []),
     "pdt_sgd_step": (c_int, [P, c_int, P, P, P, P, c_float, c_float, c_float, c_float, c_int, c_int, c_float, P]),
     "pdt_adam_step": (c_int, [P, c_int, P, P, P, P, P, P] + [c_float] * 5 + [c_int, c_float, c_float, c_float, P]),
@@ -312,6 +313,16 @@ def conv_wgrad(dy, x, out, *, scale=1.0, accumulate=False, variant=None, **a):
             _save_tuned()
             variant = best
     _wgrad_launch(lib, dy, x, out, variant, scale, accumulate, a)
+
+
+def colsum(x, R, C):
+    """fp32 column sums of a bf16 [R][C] matrix (bias gradients)."""
+    assert x.dtype == torch.bfloat16 and x.numel() >= R * C
+    lib = _load()
+    out = torch.empty(C, dtype=torch.float32, device=x.device)
+    work = torch.empty(lib.pdt_colsum_workspace(R, C), dtype=torch.float32, device=x.device)
+    _chk(lib.pdt_colsum(_p(x), _p(out), _p(work), R, C, 0, _s()), "colsum")
+    return out
 
 
 def fill_uniform_(t: torch.Tensor, seed: int):
@@ -730,8 +741,7 @@ class _Linear(torch.autograd.Function):
                        oh0=0, ow0=0, dh=1, dw=1, ntw=1)
         db = None
         if has_b and ctx.needs_input_grad[2]:
-            db = torch.empty(Nout, dtype=torch.float32, device=dy.device)
-            _chk(lib.pdt_colsum(_p(dy2), _p(db), Mrows, Nout, 0, st), "colsum")
+            db = colsum(dy2, Mrows, Nout)
         return dx, dw, db, None
 
 
@@ -867,8 +877,7 @@ class _PatchEmbed(torch.autograd.Function):
         dw = _unit_dw(dy, u) if ctx.needs_input_grad[1] else None
         db = None
         if ctx.has_b and ctx.needs_input_grad[2]:
-            db = torch.empty(Cout, dtype=torch.float32, device=dy.device)
-            _chk(_load().pdt_colsum(_p(dy), _p(db), N * u.g["Ho"] * u.g["Wo"], Cout, 0, _s()), "colsum")
+            db = colsum(dy, N * u.g["Ho"] * u.g["Wo"], Cout)
         dx = None
         if ctx.needs_input_grad[0]:
             dx = _unit_dx(dy, u)
