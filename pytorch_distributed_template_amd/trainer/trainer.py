@@ -32,6 +32,7 @@ import torch
 from ..base.base_trainer import BaseTrainer
 from ..utils import MetricTracker, inf_loop
 from ..utils import dist as pdist
+from ..utils.profiling import PhaseTimer
 
 
 class Trainer(BaseTrainer):
@@ -57,6 +58,9 @@ class Trainer(BaseTrainer):
         self.train_metrics = MetricTracker("loss", writer=self.writer)
         self.valid_metrics = MetricTracker("loss", *[m.__name__ for m in self.metric_ftns], writer=self.writer)
         self.last_throughput = None
+        # optional per-phase device timing (HIP events + ROCTx ranges): trainer.profile_phases
+        self.phase_timer = PhaseTimer(enabled=bool(config["trainer"].get("profile_phases", False))
+                                      and device.type == "cuda")
 
     # ------------------------------------------------------------------ helpers
     def _on_epoch_start(self, epoch):
@@ -96,12 +100,15 @@ class Trainer(BaseTrainer):
                 n_images = 0
             data, target = self._to_device(data, target)
 
+            pt = self.phase_timer
             self.optimizer.zero_grad(set_to_none=True)
-            with self._autocast():
+            with pt.phase("forward"), self._autocast():
                 output = self.model(data)
                 loss = self.criterion(output, target)
-            loss.backward()
-            self.optimizer.step()
+            with pt.phase("backward"):
+                loss.backward()
+            with pt.phase("optimizer"):
+                self.optimizer.step()
 
             loss_sum += loss.detach().float()
             n_iter += 1
@@ -132,6 +139,8 @@ class Trainer(BaseTrainer):
         log = self.train_metrics.result()
         if self.last_throughput is not None:
             log["images_per_sec"] = round(self.last_throughput, 2)
+        if self.phase_timer.enabled:
+            log.update({f"ms_{k}": round(v, 3) for k, v in self.phase_timer.summary().items()})
 
         if self.do_validation:
             val_log = self._valid_epoch(epoch)

@@ -65,7 +65,12 @@ def test_conv_fwd_dgrad_wgrad(shape):
     y, M, part, R = no._conv_forward(xs, wb, N, H, W, Cs, Cout, g, with_stats=True)
     wr = conv.weight.detach().to(torch.bfloat16).float()
     ref = F.conv2d(x.float(), wr, None, s, p)
-    assert relerr(y, ref) < 1e-2
+    if relerr(y, ref) >= 1e-2:  # diagnose: which input/variant disagrees
+        ref2 = F.conv2d(x.float(), wr, None, s, p)
+        y2, _, _, _ = no._conv_forward(xs, wb, N, H, W, Cs, Cout, g, with_stats=True)
+        raise AssertionError(f"conv fwd mismatch: err={relerr(y, ref):.4f} rerun_native={relerr(y2, ref):.4f} "
+                             f"ref_vs_ref2={relerr(ref2, ref):.4f} weight_bf16_ok="
+                             f"{torch.equal(wb.float()[:, :Cin] if Cs != Cin else wb.float(), wr)}")
     # every tile variant the autotuner may pick computes the same conv
     a = no._fwd_nt_geom(N, H, W, Cs, Cout, g)
     for v in range(no._load().pdt_conv_nt_num_variants()):
