@@ -27,6 +27,7 @@
 // Epilogue options: per-channel BatchNorm partial statistics (sum, sum of
 // squares over the tile's rows, from the fp32 accumulators), bias, ReLU.
 #include "pdt_common.h"
+#include <stdlib.h>
 
 namespace {
 
@@ -45,6 +46,8 @@ struct NTParams {
   int act;             // 0 none, 1 relu, 2 gelu(tanh)
   u16* aux;            // optional: pre-activation copy of the output (same layout)
   int nstat_rows;
+  int nt_store;        // 1: non-temporal (streaming) output stores
+  int ident_out;       // 1: output row == m (no stride-phase remap) -> skip the index math
   FastDiv div_Wm, div_HWm, div_Cs8, div_ntw;
 };
 
@@ -284,11 +287,14 @@ __global__ void __launch_bounds__(NT, 2) conv_nt_kernel(NTParams p) {
     for (int i = 0; i < MI; ++i) {
       int m = m0 + wm * (BM / 2) + i * 16 + lrow;
       if (m >= p.M) continue;
-      uint32_t img = fdiv(m, p.div_HWm);
-      uint32_t rem = m - img * (uint32_t)(p.Hm * p.Wm);
-      uint32_t oh = fdiv(rem, p.div_Wm);
-      uint32_t ow = rem - oh * p.Wm;
-      size_t orow = ((size_t)img * p.Ho + oh * p.osh + p.oph) * p.Wo + ow * p.osw + p.opw;
+      size_t orow = m;
+      if (!p.ident_out) {
+        uint32_t img = fdiv(m, p.div_HWm);
+        uint32_t rem = m - img * (uint32_t)(p.Hm * p.Wm);
+        uint32_t oh = fdiv(rem, p.div_Wm);
+        uint32_t ow = rem - oh * p.Wm;
+        orow = ((size_t)img * p.Ho + oh * p.osh + p.oph) * p.Wo + ow * p.osw + p.opw;
+      }
 #pragma unroll
       for (int j = 0; j < NI; ++j) {
         int col = n0 + wn * (BN / 2) + j * 16 + lcol;
@@ -301,7 +307,11 @@ __global__ void __launch_bounds__(NT, 2) conv_nt_kernel(NTParams p) {
         uint2 w;
         w.x = pack2bf(v0, v1);
         w.y = pack2bf(v2, v3);
-        *reinterpret_cast<uint2*>(dst + orow * p.ldo + col) = w;
+        typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+        u32x2 w2 = {w.x, w.y};
+        u32x2* dp = reinterpret_cast<u32x2*>(dst + orow * p.ldo + col);
+        if (p.nt_store) __builtin_nontemporal_store(w2, dp);
+        else *dp = w2;
       }
     }
   };
@@ -332,17 +342,22 @@ __global__ void __launch_bounds__(NT, 2) conv_nt_kernel(NTParams p) {
       int col = n0 + cc * 8;
       if (m < p.M && col < p.Ncol) {
         u32x4 v = *reinterpret_cast<const u32x4*>(smem + r * C_STRIDE + cc * 16);
-        uint32_t img = fdiv(m, p.div_HWm);
-        uint32_t rem = m - img * (uint32_t)(p.Hm * p.Wm);
-        uint32_t oh = fdiv(rem, p.div_Wm);
-        uint32_t ow = rem - oh * p.Wm;
-        size_t orow = ((size_t)img * p.Ho + oh * p.osh + p.oph) * p.Wo + ow * p.osw + p.opw;
+        size_t orow = m;
+        if (!p.ident_out) {
+          uint32_t img = fdiv(m, p.div_HWm);
+          uint32_t rem = m - img * (uint32_t)(p.Hm * p.Wm);
+          uint32_t oh = fdiv(rem, p.div_Wm);
+          uint32_t ow = rem - oh * p.Wm;
+          orow = ((size_t)img * p.Ho + oh * p.osh + p.oph) * p.Wo + ow * p.osw + p.opw;
+        }
         if (addend != nullptr) {
           u32x4 a = *reinterpret_cast<const u32x4*>(addend + orow * p.ldo + col);
 #pragma unroll
           for (int e = 0; e < 4; ++e) v[e] = pack2bf(lo_bf(v[e]) + lo_bf(a[e]), hi_bf(v[e]) + hi_bf(a[e]));
         }
-        *reinterpret_cast<u32x4*>(dst + orow * p.ldo + col) = v;
+        u32x4* dp = reinterpret_cast<u32x4*>(dst + orow * p.ldo + col);
+        if (p.nt_store) __builtin_nontemporal_store(v, dp);
+        else *dp = v;
       }
     }
   };
@@ -463,6 +478,15 @@ PDT_API int pdt_conv_nt(const void* src, const void* b, void* out, float* stats,
   p.div_HWm = make_fastdiv(Hm * Wm);
   p.div_Cs8 = make_fastdiv(Cs / 8);
   p.div_ntw = make_fastdiv(ntw > 0 ? ntw : 1);
+  p.ident_out = (Hm == Ho && Wm == Wo && osh == 1 && osw == 1 && oph == 0 && opw == 0) ? 1 : 0;
+  {
+    static int nt_env = -1;
+    if (nt_env < 0) {
+      const char* e = getenv("PDT_NT_STORE");
+      nt_env = (e && e[0] == '1') ? 1 : 0;
+    }
+    p.nt_store = nt_env;
+  }
   const int v = pdt_conv_nt_resolve_variant(variant, p.M, Ncol, K);
   p.nstat_rows = pdt_conv_nt_stat_rows(p.M, Ncol, K, v);
   const bool cs64 = (Cs % 64) == 0;
