@@ -56,7 +56,10 @@ constexpr int NT = 256;
 
 __device__ __forceinline__ int swz(int row, int chunk) { return chunk ^ ((row >> 1) & 7); }
 
-template <int BM, int BN, int NSTAGE, bool CS64, bool DIRECT>
+// 16 zero bytes: the global_load_lds source for padding / out-of-range rows
+__device__ __attribute__((aligned(64))) u32x4 pdt_zero_chunk[4];
+
+template <int BM, int BN, int NSTAGE, bool CS64, bool DIRECT, bool GLDS>
 __global__ void __launch_bounds__(NT, 2) conv_nt_kernel(NTParams p) {
   constexpr int MI = BM / 32;  // 16-row MFMA tiles per wave (wave covers BM/2 rows)
   constexpr int NI = BN / 32;
@@ -172,13 +175,61 @@ __global__ void __launch_bounds__(NT, 2) conv_nt_kernel(NTParams p) {
     }
   };
 
+  // GLDS: global_load_lds_dwordx4 straight into LDS (no VGPR staging). The
+  // LDS image stays lane-linear per wave instruction (8 rows x 128 B), so the
+  // XOR swizzle moves to the SOURCE: lane (row r, physical chunk ca) fetches
+  // logical chunk ca ^ swz(r). Padding / out-of-range rows read a zero page.
+  auto glds_tile = [&](int kt, int buf) {
+    char* sa = smem + buf * STAGE;
+    char* sb = sa + A_BYTES;
+    const int k0 = kt * BK;
+#pragma unroll
+    for (int i = 0; i < MI; ++i) {
+      const int r = (tid >> 3) + 32 * i;
+      const int c = swz(r, ca);  // logical chunk for this lane's LDS slot
+      const void* g = pdt_zero_chunk;
+      if (CS64) {
+        const int tap = k0 / p.Cs;
+        const int c0 = k0 - tap * p.Cs + c * 8;
+        const int th = fdiv(tap, p.div_ntw);
+        const int tw = tap - th * p.ntw;
+        const int ih = a_ih[i] + p.dh * th, iw = a_iw[i] + p.dw * tw;
+        if (a_ok[i] && (unsigned)ih < (unsigned)p.Hs && (unsigned)iw < (unsigned)p.Ws)
+          g = p.src + (size_t)(a_base[i] + ih * p.Ws + iw) * p.Cs + c0;
+      } else {
+        const int kc = k0 / 8 + c;
+        const int tap = fdiv(kc, p.div_Cs8);
+        const int c0 = (kc - tap * (p.Cs / 8)) * 8;
+        const int th = fdiv(tap, p.div_ntw);
+        const int tw = tap - th * p.ntw;
+        const int ih = a_ih[i] + p.dh * th, iw = a_iw[i] + p.dw * tw;
+        if (kc * 8 < p.K && a_ok[i] && (unsigned)ih < (unsigned)p.Hs && (unsigned)iw < (unsigned)p.Ws)
+          g = p.src + (size_t)(a_base[i] + ih * p.Ws + iw) * p.Cs + c0;
+      }
+      __builtin_amdgcn_global_load_lds(
+          g, (__attribute__((address_space(3))) void*)(sa + (8 * wave + 32 * i) * 128), 16, 0, 0);
+    }
+#pragma unroll
+    for (int j = 0; j < NI; ++j) {
+      const int r = (tid >> 3) + 32 * j;
+      const int kb = k0 + swz(r, ca) * 8;
+      const void* g = (b_ok[j] && kb < p.K) ? (const void*)(p.b + (size_t)b_row[j] * p.ldb + kb)
+                                            : (const void*)pdt_zero_chunk;
+      __builtin_amdgcn_global_load_lds(
+          g, (__attribute__((address_space(3))) void*)(sb + (8 * wave + 32 * j) * 128), 16, 0, 0);
+    }
+  };
+
   f32x4 acc[MI][NI];
 #pragma unroll
   for (int i = 0; i < MI; ++i)
 #pragma unroll
     for (int j = 0; j < NI; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  if (nk > 0) {
+  if (GLDS) {
+    if (nk > 0) glds_tile(0, 0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  } else if (nk > 0) {
     load_tile(0);
     store_tile(0);
   }
@@ -186,7 +237,11 @@ __global__ void __launch_bounds__(NT, 2) conv_nt_kernel(NTParams p) {
 
   for (int kt = 0; kt < nk; ++kt) {
     const int cur = NSTAGE == 2 ? (kt & 1) : 0;
-    if (kt + 1 < nk) load_tile(kt + 1);
+    if (GLDS) {
+      if (NSTAGE == 2 && kt + 1 < nk) glds_tile(kt + 1, cur ^ 1);
+    } else if (kt + 1 < nk) {
+      load_tile(kt + 1);
+    }
     const char* sa = smem + cur * STAGE;
     const char* sb = sa + A_BYTES;
 #pragma unroll
@@ -210,7 +265,17 @@ __global__ void __launch_bounds__(NT, 2) conv_nt_kernel(NTParams p) {
           // swapped operands: lane holds 4 consecutive output channels of one row
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[j], af[i], acc[i][j], 0, 0, 0);
     }
-    if (NSTAGE == 2) {
+    if (GLDS) {
+      if (NSTAGE == 2) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // my DMA into the other buffer landed
+        __syncthreads();                                   // ... and everyone's; buffer cur is free
+      } else if (kt + 1 < nk) {
+        __syncthreads();
+        glds_tile(kt + 1, 0);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+      }
+    } else if (NSTAGE == 2) {
       if (kt + 1 < nk) store_tile(cur ^ 1);
       __syncthreads();
     } else if (kt + 1 < nk) {
@@ -386,20 +451,23 @@ __global__ void __launch_bounds__(NT, 2) conv_nt_kernel(NTParams p) {
   stage_store(p.out, p.addend);
 }
 
-template <int BM, int BN, int NS, bool CS64, bool DIRECT>
+template <int BM, int BN, int NS, bool CS64, bool DIRECT, bool GLDS = false>
 int launch(const NTParams& p, hipStream_t st) {
   int ntm = (p.M + BM - 1) / BM, ntn = (p.Ncol + BN - 1) / BN;
-  hipLaunchKernelGGL((conv_nt_kernel<BM, BN, NS, CS64, DIRECT>), dim3(ntm * ntn), dim3(NT), 0, st, p);
+  hipLaunchKernelGGL((conv_nt_kernel<BM, BN, NS, CS64, DIRECT, GLDS>), dim3(ntm * ntn), dim3(NT), 0, st, p);
   PDT_RETURN_LAUNCH();
 }
 
 // Tile variants (autotuned per shape from Python; -1 = built-in heuristic).
 //   id : BM x BN, LDS stages
 //   ids 10..19 : the same tiles with the direct (no LDS staging) epilogue
-constexpr int NVAR = 20;
+//   ids 20..29 : the same tiles loaded by global_load_lds (LDS-DMA)
+constexpr int NVAR = 30;
 constexpr int VAR_BM[NVAR] = {128, 256, 64, 128, 64, 128, 256, 64, 128, 64,
+                              128, 256, 64, 128, 64, 128, 256, 64, 128, 64,
                               128, 256, 64, 128, 64, 128, 256, 64, 128, 64};
 constexpr int VAR_BN[NVAR] = {128, 64, 128, 64, 64, 128, 64, 128, 64, 64,
+                              128, 64, 128, 64, 64, 128, 64, 128, 64, 64,
                               128, 64, 128, 64, 64, 128, 64, 128, 64, 64};
 
 int heuristic_variant(int M, int Ncol, int K) {
@@ -431,6 +499,16 @@ int launch_variant(int v, const NTParams& p, hipStream_t st) {
     case 17: return launch<64, 128, 1, CS64, true>(p, st);
     case 18: return launch<128, 64, 1, CS64, true>(p, st);
     case 19: return launch<64, 64, 1, CS64, true>(p, st);
+    case 20: return launch<128, 128, 2, CS64, false, true>(p, st);
+    case 21: return launch<256, 64, 2, CS64, false, true>(p, st);
+    case 22: return launch<64, 128, 2, CS64, false, true>(p, st);
+    case 23: return launch<128, 64, 2, CS64, false, true>(p, st);
+    case 24: return launch<64, 64, 2, CS64, false, true>(p, st);
+    case 25: return launch<128, 128, 1, CS64, false, true>(p, st);
+    case 26: return launch<256, 64, 1, CS64, false, true>(p, st);
+    case 27: return launch<64, 128, 1, CS64, false, true>(p, st);
+    case 28: return launch<128, 64, 1, CS64, false, true>(p, st);
+    case 29: return launch<64, 64, 1, CS64, false, true>(p, st);
   }
   return -3;
 }
