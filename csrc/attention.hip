@@ -1,0 +1,443 @@
+// Fused (flash-style) multi-head attention for ViT on MI355X MFMA, bf16 in /
+// fp32 softmax, head dim 64, non-causal, any sequence length (ViT-B/16: 197).
+//
+// Layout: Q, K, V are read in place from the qkv projection output
+// [B, T, 3, H, 64] (row stride ld elements), O is written as [B, T, H*64]
+// (the proj GEMM's input, no transpose pass), gradients dQ/dK/dV are written
+// into a [B, T, 3, H, 64] buffer (the qkv GEMM's output gradient).
+//
+// Forward, one workgroup = 64 queries of one (b, h), one wave = 16 queries:
+//   S^T = K Q^T with mfma_f32_16x16x32_bf16 (K rows = A operand, Q = B operand)
+//   puts 4 keys x 1 query in every lane (query = lane & 15), so the running
+//   row max / sum reduce over the 4 lanes {l, l^16, l^32, l^48} only; the
+//   exponentiated probabilities are ALREADY the B operand of O^T = V^T P^T
+//   (k index permuted consistently on both operands), and V^T comes from the
+//   hardware-transposing LDS read ds_read_b64_tr_b16. The O^T accumulator has
+//   the same query-per-lane layout as the softmax state: rescales need no
+//   cross-lane traffic.
+// Backward: dK/dV kernel (one workgroup per 64 keys, 16 keys per wave, loops
+// over all query tiles) and a dQ kernel (one workgroup per 64 queries) -- the
+// probabilities are recomputed from Q, K and the saved log-sum-exp, no atomics.
+#include "pdt_common.h"
+
+namespace {
+
+constexpr int D = 64;     // head dim
+constexpr int TILE = 64;  // keys (or queries) per LDS tile
+
+typedef __attribute__((address_space(3))) bf16x4 lds_bf16x4;
+
+// [64 rows][64 bf16] tile, 128-B rows. Two images:
+//  * row image (ds_read_b128 of 8 contiguous d): chunk XOR ((row >> 1) & 7)
+//  * transposed image (ds_read_b64_tr_b16): 32-B segment XOR seg_swz(row)
+__device__ __forceinline__ int row_off(int row, int chunk) { return row * 128 + ((chunk ^ ((row >> 1) & 7)) << 4); }
+__device__ __forceinline__ int seg_swz(int row) { return ((row >> 1) & 1) | ((row >> 2) & 2); }
+__device__ __forceinline__ int tr_off(int row, int byte_in_row) {
+  int seg = byte_in_row >> 5;
+  return row * 128 + ((seg ^ seg_swz(row)) << 5) + (byte_in_row & 31);
+}
+
+// stage a [64][64] bf16 tile (rows r0.., valid rows < nvalid, zero otherwise) into LDS
+template <bool TR>
+__device__ __forceinline__ void stage_tile(char* lds, const u16* src, long ld, int r0, int nvalid, int tid) {
+#pragma unroll
+  for (int it = 0; it < 2; ++it) {  // 512 chunks of 16 B over 256 threads
+    const int q = tid + it * 256;
+    const int row = q >> 3, ch = q & 7;
+    u32x4 v = {0, 0, 0, 0};
+    if (r0 + row < nvalid) v = *reinterpret_cast<const u32x4*>(src + (long)(r0 + row) * ld + ch * 8);
+    const int off = TR ? tr_off(row, ch * 16) : row_off(row, ch);
+    *reinterpret_cast<u32x4*>(lds + off) = v;
+  }
+}
+
+__device__ __forceinline__ bf16x8 ld_row_frag(const char* lds, int row, int chunk) {
+  return *reinterpret_cast<const bf16x8*>(lds + row_off(row, chunk));
+}
+
+// A/B fragment whose 8 k-elements are rows {kb0 + 0..3} and {kb1 + 0..3} (per
+// 16-lane group: kb += 4*g) of column block col0..col0+15 of a transposed image.
+__device__ __forceinline__ bf16x8 tr_frag2(const char* lds, int kb0, int kb1, int col0, int lane) {
+  const int g = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
+  const int cb = (col0 + 4 * p) * 2;
+  bf16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4bf16(
+      (lds_bf16x4*)((__attribute__((address_space(3))) char*)(uintptr_t)(uint32_t)(uintptr_t)(
+          lds + tr_off(kb0 + 4 * g + q, cb))));
+  bf16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4bf16(
+      (lds_bf16x4*)((__attribute__((address_space(3))) char*)(uintptr_t)(uint32_t)(uintptr_t)(
+          lds + tr_off(kb1 + 4 * g + q, cb))));
+  bf16x8 r;
+  r[0] = lo[0]; r[1] = lo[1]; r[2] = lo[2]; r[3] = lo[3];
+  r[4] = hi[0]; r[5] = hi[1]; r[6] = hi[2]; r[7] = hi[3];
+  return r;
+}
+
+__device__ __forceinline__ float xor_max4(float v) {
+  v = fmaxf(v, __shfl_xor(v, 16, 64));
+  return fmaxf(v, __shfl_xor(v, 32, 64));
+}
+__device__ __forceinline__ float xor_sum4(float v) {
+  v += __shfl_xor(v, 16, 64);
+  return v + __shfl_xor(v, 32, 64);
+}
+
+__device__ __forceinline__ bf16x8 pack_p(const f32x4& a, const f32x4& b) {
+  bf16x8 r;
+  r[0] = (__bf16)a[0]; r[1] = (__bf16)a[1]; r[2] = (__bf16)a[2]; r[3] = (__bf16)a[3];
+  r[4] = (__bf16)b[0]; r[5] = (__bf16)b[1]; r[6] = (__bf16)b[2]; r[7] = (__bf16)b[3];
+  return r;
+}
+
+struct AttnParams {
+  const u16* qkv;   // [B, T, 3, H, 64]
+  u16* out;         // [B, T, H*64]
+  float* lse;       // [B*H, T]  (log2-domain of scaled scores)
+  int B, T, H;
+  long ld;          // row stride of qkv (3*H*64)
+  long ldo;         // row stride of out (H*64)
+  float c;          // softmax scale * log2(e)
+};
+
+__global__ void __launch_bounds__(256) attn_fwd_kernel(AttnParams p) {
+  __shared__ __attribute__((aligned(16))) char smem[2 * TILE * D * 2];
+  char* Ks = smem;
+  char* Vs = smem + TILE * D * 2;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, g = lane >> 4;
+  const int bh = blockIdx.y, b = bh / p.H, h = bh % p.H;
+  const int q0 = blockIdx.x * TILE + wave * 16;
+  const u16* base = p.qkv + (long)b * p.T * p.ld + h * D;
+  const u16* Qg = base;
+  const u16* Kg = base + p.H * D;
+  const u16* Vg = base + 2 * p.H * D;
+  // Q fragments (B operand of S^T): Q[q0 + (lane&15)][32kk + 8g .. +7]
+  const int qrow = q0 + (lane & 15);
+  bf16x8 qf[2];
+#pragma unroll
+  for (int kk = 0; kk < 2; ++kk) {
+    u32x4 v = {0, 0, 0, 0};
+    if (qrow < p.T) v = *reinterpret_cast<const u32x4*>(Qg + (long)qrow * p.ld + 32 * kk + 8 * g);
+    qf[kk] = __builtin_bit_cast(bf16x8, v);
+  }
+  float m = -INFINITY, l = 0.f;
+  f32x4 o[4];
+#pragma unroll
+  for (int dt = 0; dt < 4; ++dt) o[dt] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  for (int k0 = 0; k0 < p.T; k0 += TILE) {
+    __syncthreads();
+    stage_tile<false>(Ks, Kg, p.ld, k0, p.T, tid);
+    stage_tile<true>(Vs, Vg, p.ld, k0, p.T, tid);
+    __syncthreads();
+    f32x4 s[4];
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      s[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk)
+        s[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ld_row_frag(Ks, 16 * t + (lane & 15), 4 * kk + g), qf[kk],
+                                                       s[t], 0, 0, 0);
+    }
+    // s[t][r] = S[key = k0 + 16t + 4g + r][q = qrow]
+    float mt = -INFINITY;
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int key = k0 + 16 * t + 4 * g + r;
+        float v = key < p.T ? s[t][r] * p.c : -INFINITY;
+        s[t][r] = v;
+        mt = fmaxf(mt, v);
+      }
+    mt = xor_max4(mt);
+    const float mn = fmaxf(m, mt);
+    const float alpha = exp2f(m - mn);  // m = -inf first: exp2(-inf) = 0
+    float ls = 0.f;
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        float e = exp2f(s[t][r] - mn);
+        s[t][r] = e;
+        ls += e;
+      }
+    l = l * alpha + xor_sum4(ls);
+    m = mn;
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt) o[dt] *= alpha;
+    // O^T[d][q] += sum_key V^T[d][key] P^T[key][q]  (two 32-key steps)
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      const bf16x8 pf = pack_p(s[2 * ks], s[2 * ks + 1]);
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt)
+        o[dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(tr_frag2(Vs, 32 * ks, 32 * ks + 16, 16 * dt, lane), pf,
+                                                        o[dt], 0, 0, 0);
+    }
+  }
+  // o[dt][r] = O^T[d = 16dt + 4g + r][q = qrow]
+  if (qrow < p.T) {
+    const float inv = 1.f / l;
+    u16* orow = p.out + ((long)b * p.T + qrow) * p.ldo + h * D;
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt) {
+      uint2 w;
+      w.x = pack2bf(o[dt][0] * inv, o[dt][1] * inv);
+      w.y = pack2bf(o[dt][2] * inv, o[dt][3] * inv);
+      *reinterpret_cast<uint2*>(orow + 16 * dt + 4 * g) = w;
+    }
+    if (g == 0) p.lse[(long)bh * p.T + qrow] = m + log2f(l);
+  }
+}
+
+struct AttnBwdParams {
+  const u16* qkv;   // [B, T, 3, H, 64]
+  const u16* dout;  // [B, T, H*64]
+  const float* lse; // [B*H, T]
+  const float* delta;  // [B*H, T] = rowsum(dO * O)
+  u16* dqkv;        // [B, T, 3, H, 64]
+  int B, T, H;
+  long ld, ldo;
+  float c;          // scale * log2(e)
+  float scale;
+};
+
+// delta[bh][q] = sum_d dO[q][d] * O[q][d]
+__global__ void attn_delta_kernel(const u16* __restrict__ dout, const u16* __restrict__ out, float* __restrict__ delta,
+                                  int B, int T, int H, long ldo) {
+  const int lane = threadIdx.x & 63;
+  const long row = (long)blockIdx.x * 4 + (threadIdx.x >> 6);  // over B*T*H (b, t, h)
+  if (row >= (long)B * T * H) return;
+  const int h = row % H;
+  const long bt = row / H;
+  const long off = bt * ldo + h * D + lane;
+  float v = bf2f(dout[off]) * bf2f(out[off]);
+  v = warp_sum(v);
+  if (lane == 0) {
+    const int b = bt / T, t = bt % T;
+    delta[((long)b * H + h) * T + t] = v;
+  }
+}
+
+// dK, dV: one workgroup per 64 keys of one (b, h); wave = 16 keys.
+// S = Q K^T with Q rows as A operand -> lane holds S[q = 16u + 4g + r][key = lane&15]
+__global__ void __launch_bounds__(256) attn_bwd_dkdv_kernel(AttnBwdParams p) {
+  __shared__ __attribute__((aligned(16))) char smem[2 * TILE * D * 2];
+  char* Qs = smem;                    // transposed image (B operand of dK via tr reads)
+  char* dOs = smem + TILE * D * 2;    // row image + tr image? -> two separate uses below
+  __shared__ __attribute__((aligned(16))) char dOt[TILE * D * 2];
+  __shared__ __attribute__((aligned(16))) char Qr[TILE * D * 2];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, g = lane >> 4;
+  const int bh = blockIdx.y, b = bh / p.H, h = bh % p.H;
+  const int kbase = blockIdx.x * TILE + wave * 16;
+  const int key = kbase + (lane & 15);
+  const u16* base = p.qkv + (long)b * p.T * p.ld + h * D;
+  const u16* Qg = base;
+  const u16* Kg = base + p.H * D;
+  const u16* Vg = base + 2 * p.H * D;
+  const u16* dOg = p.dout + (long)b * p.T * p.ldo + h * D;
+  // K, V fragments as B operands (k = d): K[key][8g + j + 32kk]
+  bf16x8 kf[2], vf[2];
+#pragma unroll
+  for (int kk = 0; kk < 2; ++kk) {
+    u32x4 a = {0, 0, 0, 0}, c = {0, 0, 0, 0};
+    if (key < p.T) {
+      a = *reinterpret_cast<const u32x4*>(Kg + (long)key * p.ld + 32 * kk + 8 * g);
+      c = *reinterpret_cast<const u32x4*>(Vg + (long)key * p.ld + 32 * kk + 8 * g);
+    }
+    kf[kk] = __builtin_bit_cast(bf16x8, a);
+    vf[kk] = __builtin_bit_cast(bf16x8, c);
+  }
+  f32x4 dk[4], dv[4];
+#pragma unroll
+  for (int dt = 0; dt < 4; ++dt) dk[dt] = dv[dt] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const float* lse = p.lse + (long)bh * p.T;
+  const float* dl = p.delta + (long)bh * p.T;
+
+  for (int q0 = 0; q0 < p.T; q0 += TILE) {
+    __syncthreads();
+    stage_tile<false>(Qr, Qg, p.ld, q0, p.T, tid);     // rows: A operand of S
+    stage_tile<true>(Qs, Qg, p.ld, q0, p.T, tid);      // transposed: B operand of dK
+    stage_tile<false>(dOs, dOg, p.ldo, q0, p.T, tid);  // rows: A operand of dP
+    stage_tile<true>(dOt, dOg, p.ldo, q0, p.T, tid);   // transposed: B operand of dV
+    __syncthreads();
+    f32x4 s[4], dp[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      s[u] = dp[u] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) {
+        s[u] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ld_row_frag(Qr, 16 * u + (lane & 15), 4 * kk + g), kf[kk],
+                                                       s[u], 0, 0, 0);
+        dp[u] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ld_row_frag(dOs, 16 * u + (lane & 15), 4 * kk + g),
+                                                        vf[kk], dp[u], 0, 0, 0);
+      }
+    }
+    // s[u][r] = S[q = q0 + 16u + 4g + r][key], same for dp
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int q = q0 + 16 * u + 4 * g + r;
+        float pr = 0.f, ds = 0.f;
+        if (q < p.T && key < p.T) {
+          pr = exp2f(s[u][r] * p.c - lse[q]);
+          ds = pr * (dp[u][r] - dl[q]);
+        }
+        s[u][r] = pr;
+        dp[u][r] = ds;
+      }
+    // dV^T[d][key] += dO^T[d][q] P[q][key] ; dK^T[d][key] += Q^T[d][q] dS[q][key]
+    // A operand = transposed dO / Q tile (rows d, k = q permuted), B = P / dS (k = q, col = key)
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      const bf16x8 pf = pack_p(s[2 * ks], s[2 * ks + 1]);
+      const bf16x8 sf = pack_p(dp[2 * ks], dp[2 * ks + 1]);
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt) {
+        dv[dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(tr_frag2(dOt, 32 * ks, 32 * ks + 16, 16 * dt, lane), pf,
+                                                         dv[dt], 0, 0, 0);
+        dk[dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(tr_frag2(Qs, 32 * ks, 32 * ks + 16, 16 * dt, lane), sf,
+                                                         dk[dt], 0, 0, 0);
+      }
+    }
+  }
+  // dk[dt][r] = dK^T[d = 16dt + 4g + r][key]
+  if (key < p.T) {
+    u16* drow = p.dqkv + ((long)b * p.T + key) * p.ld + h * D;
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt) {
+      uint2 wk, wv;
+      wk.x = pack2bf(dk[dt][0] * p.scale, dk[dt][1] * p.scale);
+      wk.y = pack2bf(dk[dt][2] * p.scale, dk[dt][3] * p.scale);
+      wv.x = pack2bf(dv[dt][0], dv[dt][1]);
+      wv.y = pack2bf(dv[dt][2], dv[dt][3]);
+      *reinterpret_cast<uint2*>(drow + p.H * D + 16 * dt + 4 * g) = wk;
+      *reinterpret_cast<uint2*>(drow + 2 * p.H * D + 16 * dt + 4 * g) = wv;
+    }
+  }
+}
+
+// dQ: one workgroup per 64 queries; wave = 16 queries; S^T orientation (as forward).
+__global__ void __launch_bounds__(256) attn_bwd_dq_kernel(AttnBwdParams p) {
+  __shared__ __attribute__((aligned(16))) char smem[3 * TILE * D * 2];
+  char* Kr = smem;                    // row image (A operand of S^T)
+  char* Kt = smem + TILE * D * 2;     // transposed (A operand of dQ^T)
+  char* Vr = smem + 2 * TILE * D * 2; // row image (A operand of dP^T)
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, g = lane >> 4;
+  const int bh = blockIdx.y, b = bh / p.H, h = bh % p.H;
+  const int qrow = blockIdx.x * TILE + wave * 16 + (lane & 15);
+  const u16* base = p.qkv + (long)b * p.T * p.ld + h * D;
+  const u16* Qg = base;
+  const u16* Kg = base + p.H * D;
+  const u16* Vg = base + 2 * p.H * D;
+  const u16* dOg = p.dout + (long)b * p.T * p.ldo + h * D;
+  bf16x8 qf[2], of[2];
+#pragma unroll
+  for (int kk = 0; kk < 2; ++kk) {
+    u32x4 a = {0, 0, 0, 0}, c = {0, 0, 0, 0};
+    if (qrow < p.T) {
+      a = *reinterpret_cast<const u32x4*>(Qg + (long)qrow * p.ld + 32 * kk + 8 * g);
+      c = *reinterpret_cast<const u32x4*>(dOg + (long)qrow * p.ldo + 32 * kk + 8 * g);
+    }
+    qf[kk] = __builtin_bit_cast(bf16x8, a);
+    of[kk] = __builtin_bit_cast(bf16x8, c);
+  }
+  const float lq = qrow < p.T ? p.lse[(long)bh * p.T + qrow] : 0.f;
+  const float dq_delta = qrow < p.T ? p.delta[(long)bh * p.T + qrow] : 0.f;
+  f32x4 dq[4];
+#pragma unroll
+  for (int dt = 0; dt < 4; ++dt) dq[dt] = f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int k0 = 0; k0 < p.T; k0 += TILE) {
+    __syncthreads();
+    stage_tile<false>(Kr, Kg, p.ld, k0, p.T, tid);
+    stage_tile<true>(Kt, Kg, p.ld, k0, p.T, tid);
+    stage_tile<false>(Vr, Vg, p.ld, k0, p.T, tid);
+    __syncthreads();
+    f32x4 s[4], dp[4];
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      s[t] = dp[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) {
+        s[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ld_row_frag(Kr, 16 * t + (lane & 15), 4 * kk + g), qf[kk],
+                                                       s[t], 0, 0, 0);
+        dp[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ld_row_frag(Vr, 16 * t + (lane & 15), 4 * kk + g), of[kk],
+                                                        dp[t], 0, 0, 0);
+      }
+    }
+    // s[t][r] = S[key = k0 + 16t + 4g + r][q = qrow]
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int k = k0 + 16 * t + 4 * g + r;
+        float ds = 0.f;
+        if (k < p.T && qrow < p.T) {
+          float pr = exp2f(s[t][r] * p.c - lq);
+          ds = pr * (dp[t][r] - dq_delta);
+        }
+        s[t][r] = ds;
+      }
+    // dQ^T[d][q] += K^T[d][key] dS^T[key][q]
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      const bf16x8 sf = pack_p(s[2 * ks], s[2 * ks + 1]);
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt)
+        dq[dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(tr_frag2(Kt, 32 * ks, 32 * ks + 16, 16 * dt, lane), sf,
+                                                         dq[dt], 0, 0, 0);
+    }
+  }
+  if (qrow < p.T) {
+    u16* drow = p.dqkv + ((long)b * p.T + qrow) * p.ld + h * D;
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt) {
+      uint2 w;
+      w.x = pack2bf(dq[dt][0] * p.scale, dq[dt][1] * p.scale);
+      w.y = pack2bf(dq[dt][2] * p.scale, dq[dt][3] * p.scale);
+      *reinterpret_cast<uint2*>(drow + 16 * dt + 4 * g) = w;
+    }
+  }
+}
+
+}  // namespace
+
+PDT_API int pdt_attn_fwd(const void* qkv, void* out, float* lse, int B, int T, int H, float scale, hipStream_t st) {
+  AttnParams p;
+  p.qkv = (const u16*)qkv;
+  p.out = (u16*)out;
+  p.lse = lse;
+  p.B = B; p.T = T; p.H = H;
+  p.ld = 3L * H * D;
+  p.ldo = (long)H * D;
+  p.c = scale * 1.4426950408889634f;
+  dim3 grid((T + TILE - 1) / TILE, B * H);
+  hipLaunchKernelGGL(attn_fwd_kernel, grid, dim3(256), 0, st, p);
+  PDT_RETURN_LAUNCH();
+}
+
+PDT_API int pdt_attn_bwd(const void* qkv, const void* out, const void* dout, const float* lse, float* delta,
+                         void* dqkv, int B, int T, int H, float scale, hipStream_t st) {
+  const long rows = (long)B * T * H;
+  hipLaunchKernelGGL(attn_delta_kernel, dim3((unsigned)((rows + 3) / 4)), dim3(256), 0, st, (const u16*)dout,
+                     (const u16*)out, delta, B, T, H, (long)H * D);
+  int e = (int)hipGetLastError();
+  if (e) return e;
+  AttnBwdParams p;
+  p.qkv = (const u16*)qkv;
+  p.dout = (const u16*)dout;
+  p.lse = lse;
+  p.delta = delta;
+  p.dqkv = (u16*)dqkv;
+  p.B = B; p.T = T; p.H = H;
+  p.ld = 3L * H * D;
+  p.ldo = (long)H * D;
+  p.c = scale * 1.4426950408889634f;
+  p.scale = scale;
+  dim3 grid((T + TILE - 1) / TILE, B * H);
+  hipLaunchKernelGGL(attn_bwd_dkdv_kernel, grid, dim3(256), 0, st, p);
+  e = (int)hipGetLastError();
+  if (e) return e;
+  hipLaunchKernelGGL(attn_bwd_dq_kernel, grid, dim3(256), 0, st, p);
+  PDT_RETURN_LAUNCH();
+}

@@ -59,10 +59,14 @@ __device__ __forceinline__ int swz(int row, int chunk) { return chunk ^ ((row >>
 // 16 zero bytes: the global_load_lds source for padding / out-of-range rows
 __device__ __attribute__((aligned(64))) u32x4 pdt_zero_chunk[4];
 
-template <int BM, int BN, int NSTAGE, bool CS64, bool DIRECT, bool GLDS>
-__global__ void __launch_bounds__(NT, 2) conv_nt_kernel(NTParams p) {
-  constexpr int MI = BM / 32;  // 16-row MFMA tiles per wave (wave covers BM/2 rows)
-  constexpr int NI = BN / 32;
+template <int BM, int BN, int NSTAGE, bool CS64, bool DIRECT, bool GLDS, int NTH = 256, int WM = 2>
+__global__ void __launch_bounds__(NTH, 2) conv_nt_kernel(NTParams p) {
+  constexpr int WN = NTH / 64 / WM;       // waves along N
+  constexpr int MI = BM / (WM * 16);      // 16-row MFMA tiles per wave
+  constexpr int NI = BN / (WN * 16);
+  constexpr int LA = BM * 8 / NTH;        // 16-B A chunks each thread stages per K-tile
+  constexpr int LB = BN * 8 / NTH;
+  constexpr int RS = NTH / 8;             // rows covered by one staging pass
   constexpr int A_BYTES = BM * BK * 2;
   constexpr int B_BYTES = BN * BK * 2;
   constexpr int STAGE = A_BYTES + B_BYTES;
@@ -74,7 +78,7 @@ __global__ void __launch_bounds__(NT, 2) conv_nt_kernel(NTParams p) {
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wave = tid >> 6;
-  const int wm = wave >> 1, wn = wave & 1;
+  const int wm = wave / WN, wn = wave % WN;
 
   const int ntm = (p.M + BM - 1) / BM;
   const int ntn = (p.Ncol + BN - 1) / BN;
@@ -84,11 +88,11 @@ __global__ void __launch_bounds__(NT, 2) conv_nt_kernel(NTParams p) {
 
   // ---- per-thread A rows: r = tid/8 + 32*i, chunk column ca = tid%8
   const int ca = tid & 7;
-  int a_base[MI], a_ih[MI], a_iw[MI];
-  bool a_ok[MI];
+  int a_base[LA], a_ih[LA], a_iw[LA];
+  bool a_ok[LA];
 #pragma unroll
-  for (int i = 0; i < MI; ++i) {
-    int m = m0 + (tid >> 3) + 32 * i;
+  for (int i = 0; i < LA; ++i) {
+    int m = m0 + (tid >> 3) + RS * i;
     a_ok[i] = m < p.M;
     uint32_t mm = a_ok[i] ? m : 0;
     uint32_t img = fdiv(mm, p.div_HWm);
@@ -100,16 +104,16 @@ __global__ void __launch_bounds__(NT, 2) conv_nt_kernel(NTParams p) {
     a_iw[i] = ow * p.sw + p.ow0;
   }
   // ---- per-thread B rows
-  int b_row[NI];
-  bool b_ok[NI];
+  int b_row[LB];
+  bool b_ok[LB];
 #pragma unroll
-  for (int j = 0; j < NI; ++j) {
-    int n = n0 + (tid >> 3) + 32 * j;
+  for (int j = 0; j < LB; ++j) {
+    int n = n0 + (tid >> 3) + RS * j;
     b_ok[j] = n < p.Ncol;
     b_row[j] = b_ok[j] ? n : 0;
   }
 
-  u32x4 ra[MI], rb[NI];
+  u32x4 ra[LA], rb[LB];
   const int nk = (p.K + BK - 1) / BK;
 
   auto load_tile = [&](int kt) {
@@ -121,7 +125,7 @@ __global__ void __launch_bounds__(NT, 2) conv_nt_kernel(NTParams p) {
       const int tw = tap - th * p.ntw;
       const int dho = p.dh * th, dwo = p.dw * tw;
 #pragma unroll
-      for (int i = 0; i < MI; ++i) {
+      for (int i = 0; i < LA; ++i) {
         int ih = a_ih[i] + dho, iw = a_iw[i] + dwo;
         bool ok = a_ok[i] && (unsigned)ih < (unsigned)p.Hs && (unsigned)iw < (unsigned)p.Ws;
         if (ok) {
@@ -139,7 +143,7 @@ __global__ void __launch_bounds__(NT, 2) conv_nt_kernel(NTParams p) {
       const int tw = tap - th * p.ntw;
       const int dho = p.dh * th, dwo = p.dw * tw;
 #pragma unroll
-      for (int i = 0; i < MI; ++i) {
+      for (int i = 0; i < LA; ++i) {
         int ih = a_ih[i] + dho, iw = a_iw[i] + dwo;
         bool ok = kin && a_ok[i] && (unsigned)ih < (unsigned)p.Hs && (unsigned)iw < (unsigned)p.Ws;
         if (ok) {
@@ -151,7 +155,7 @@ __global__ void __launch_bounds__(NT, 2) conv_nt_kernel(NTParams p) {
     }
     const int kb = k0 + ca * 8;
 #pragma unroll
-    for (int j = 0; j < NI; ++j) {
+    for (int j = 0; j < LB; ++j) {
       if (b_ok[j] && kb < p.K) {
         rb[j] = *reinterpret_cast<const u32x4*>(p.b + (size_t)b_row[j] * p.ldb + kb);
       } else {
@@ -164,13 +168,13 @@ __global__ void __launch_bounds__(NT, 2) conv_nt_kernel(NTParams p) {
     char* sa = smem + buf * STAGE;
     char* sb = sa + A_BYTES;
 #pragma unroll
-    for (int i = 0; i < MI; ++i) {
-      int r = (tid >> 3) + 32 * i;
+    for (int i = 0; i < LA; ++i) {
+      int r = (tid >> 3) + RS * i;
       *reinterpret_cast<u32x4*>(sa + r * 128 + swz(r, ca) * 16) = ra[i];
     }
 #pragma unroll
-    for (int j = 0; j < NI; ++j) {
-      int r = (tid >> 3) + 32 * j;
+    for (int j = 0; j < LB; ++j) {
+      int r = (tid >> 3) + RS * j;
       *reinterpret_cast<u32x4*>(sb + r * 128 + swz(r, ca) * 16) = rb[j];
     }
   };
@@ -184,8 +188,8 @@ __global__ void __launch_bounds__(NT, 2) conv_nt_kernel(NTParams p) {
     char* sb = sa + A_BYTES;
     const int k0 = kt * BK;
 #pragma unroll
-    for (int i = 0; i < MI; ++i) {
-      const int r = (tid >> 3) + 32 * i;
+    for (int i = 0; i < LA; ++i) {
+      const int r = (tid >> 3) + RS * i;
       const int c = swz(r, ca);  // logical chunk for this lane's LDS slot
       const void* g = pdt_zero_chunk;
       if (CS64) {
@@ -207,16 +211,16 @@ __global__ void __launch_bounds__(NT, 2) conv_nt_kernel(NTParams p) {
           g = p.src + (size_t)(a_base[i] + ih * p.Ws + iw) * p.Cs + c0;
       }
       __builtin_amdgcn_global_load_lds(
-          g, (__attribute__((address_space(3))) void*)(sa + (8 * wave + 32 * i) * 128), 16, 0, 0);
+          g, (__attribute__((address_space(3))) void*)(sa + (8 * wave + RS * i) * 128), 16, 0, 0);
     }
 #pragma unroll
-    for (int j = 0; j < NI; ++j) {
-      const int r = (tid >> 3) + 32 * j;
+    for (int j = 0; j < LB; ++j) {
+      const int r = (tid >> 3) + RS * j;
       const int kb = k0 + swz(r, ca) * 8;
       const void* g = (b_ok[j] && kb < p.K) ? (const void*)(p.b + (size_t)b_row[j] * p.ldb + kb)
                                             : (const void*)pdt_zero_chunk;
       __builtin_amdgcn_global_load_lds(
-          g, (__attribute__((address_space(3))) void*)(sb + (8 * wave + 32 * j) * 128), 16, 0, 0);
+          g, (__attribute__((address_space(3))) void*)(sb + (8 * wave + RS * j) * 128), 16, 0, 0);
     }
   };
 
@@ -250,12 +254,12 @@ __global__ void __launch_bounds__(NT, 2) conv_nt_kernel(NTParams p) {
       bf16x8 af[MI], bfr[NI];
 #pragma unroll
       for (int i = 0; i < MI; ++i) {
-        int r = wm * (BM / 2) + i * 16 + (lane & 15);
+        int r = wm * (BM / WM) + i * 16 + (lane & 15);
         af[i] = *reinterpret_cast<const bf16x8*>(sa + r * 128 + swz(r, kch) * 16);
       }
 #pragma unroll
       for (int j = 0; j < NI; ++j) {
-        int r = wn * (BN / 2) + j * 16 + (lane & 15);
+        int r = wn * (BN / WN) + j * 16 + (lane & 15);
         bfr[j] = *reinterpret_cast<const bf16x8*>(sb + r * 128 + swz(r, kch) * 16);
       }
 #pragma unroll
@@ -295,7 +299,7 @@ __global__ void __launch_bounds__(NT, 2) conv_nt_kernel(NTParams p) {
     for (int j = 0; j < NI; ++j) {
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        int col = n0 + wn * (BN / 2) + j * 16 + lcol + r;
+        int col = n0 + wn * (BN / WN) + j * 16 + lcol + r;
         float bv = col < p.Ncol ? p.bias[col] : 0.f;
 #pragma unroll
         for (int i = 0; i < MI; ++i) acc[i][j][r] += bv;
@@ -305,7 +309,7 @@ __global__ void __launch_bounds__(NT, 2) conv_nt_kernel(NTParams p) {
 
   if (p.stats != nullptr) {
     // per-wave column partials over its BM/2 rows (invalid rows hold zeros)
-    const int srow = tm * 2 + wm;
+    const int srow = tm * WM + wm;
 #pragma unroll
     for (int j = 0; j < NI; ++j) {
       float s[4], q[4];
@@ -332,7 +336,7 @@ __global__ void __launch_bounds__(NT, 2) conv_nt_kernel(NTParams p) {
       if (lrow == 0) {
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          int col = n0 + wn * (BN / 2) + j * 16 + lcol + r;
+          int col = n0 + wn * (BN / WN) + j * 16 + lcol + r;
           if (col < p.Ncol) {
             p.stats[(size_t)srow * p.Ncol + col] = s[r];
             p.stats[(size_t)(p.nstat_rows + srow) * p.Ncol + col] = q[r];
@@ -350,7 +354,7 @@ __global__ void __launch_bounds__(NT, 2) conv_nt_kernel(NTParams p) {
   auto direct_store = [&](u16* dst, const u16* addend) {
 #pragma unroll
     for (int i = 0; i < MI; ++i) {
-      int m = m0 + wm * (BM / 2) + i * 16 + lrow;
+      int m = m0 + wm * (BM / WM) + i * 16 + lrow;
       if (m >= p.M) continue;
       size_t orow = m;
       if (!p.ident_out) {
@@ -362,7 +366,7 @@ __global__ void __launch_bounds__(NT, 2) conv_nt_kernel(NTParams p) {
       }
 #pragma unroll
       for (int j = 0; j < NI; ++j) {
-        int col = n0 + wn * (BN / 2) + j * 16 + lcol;
+        int col = n0 + wn * (BN / WN) + j * 16 + lcol;
         if (col >= p.Ncol) continue;
         float v0 = acc[i][j][0], v1 = acc[i][j][1], v2 = acc[i][j][2], v3 = acc[i][j][3];
         if (addend != nullptr) {
@@ -390,8 +394,8 @@ __global__ void __launch_bounds__(NT, 2) conv_nt_kernel(NTParams p) {
     for (int i = 0; i < MI; ++i) {
 #pragma unroll
       for (int j = 0; j < NI; ++j) {
-        int r = wm * (BM / 2) + i * 16 + lrow;
-        int c = wn * (BN / 2) + j * 16 + lcol;
+        int r = wm * (BM / WM) + i * 16 + lrow;
+        int c = wn * (BN / WN) + j * 16 + lcol;
         uint2 w;
         w.x = pack2bf(acc[i][j][0], acc[i][j][1]);
         w.y = pack2bf(acc[i][j][2], acc[i][j][3]);
@@ -400,8 +404,8 @@ __global__ void __launch_bounds__(NT, 2) conv_nt_kernel(NTParams p) {
     }
     __syncthreads();
 #pragma unroll
-    for (int it = 0; it < (BM * CPR) / NT; ++it) {
-      int q = tid + it * NT;
+    for (int it = 0; it < (BM * CPR) / NTH; ++it) {
+      int q = tid + it * NTH;
       int r = q / CPR, cc = q % CPR;
       int m = m0 + r;
       int col = n0 + cc * 8;
@@ -451,10 +455,11 @@ __global__ void __launch_bounds__(NT, 2) conv_nt_kernel(NTParams p) {
   stage_store(p.out, p.addend);
 }
 
-template <int BM, int BN, int NS, bool CS64, bool DIRECT, bool GLDS = false>
+template <int BM, int BN, int NS, bool CS64, bool DIRECT, bool GLDS = false, int NTH = 256, int WM = 2>
 int launch(const NTParams& p, hipStream_t st) {
   int ntm = (p.M + BM - 1) / BM, ntn = (p.Ncol + BN - 1) / BN;
-  hipLaunchKernelGGL((conv_nt_kernel<BM, BN, NS, CS64, DIRECT, GLDS>), dim3(ntm * ntn), dim3(NT), 0, st, p);
+  hipLaunchKernelGGL((conv_nt_kernel<BM, BN, NS, CS64, DIRECT, GLDS, NTH, WM>), dim3(ntm * ntn), dim3(NTH), 0, st,
+                     p);
   PDT_RETURN_LAUNCH();
 }
 
@@ -462,13 +467,20 @@ int launch(const NTParams& p, hipStream_t st) {
 //   id : BM x BN, LDS stages
 //   ids 10..19 : the same tiles with the direct (no LDS staging) epilogue
 //   ids 20..29 : the same tiles loaded by global_load_lds (LDS-DMA)
-constexpr int NVAR = 30;
+//   ids 30..33 : 512-thread (8-wave) tiles, 2 stages, 64x64 per wave:
+//                256x128 (4x2 waves) and 128x256 (2x4 waves), each LDS-DMA
+//                and register-staged
+constexpr int NVAR = 34;
 constexpr int VAR_BM[NVAR] = {128, 256, 64, 128, 64, 128, 256, 64, 128, 64,
                               128, 256, 64, 128, 64, 128, 256, 64, 128, 64,
-                              128, 256, 64, 128, 64, 128, 256, 64, 128, 64};
+                              128, 256, 64, 128, 64, 128, 256, 64, 128, 64,
+                              256, 128, 256, 128};
 constexpr int VAR_BN[NVAR] = {128, 64, 128, 64, 64, 128, 64, 128, 64, 64,
                               128, 64, 128, 64, 64, 128, 64, 128, 64, 64,
-                              128, 64, 128, 64, 64, 128, 64, 128, 64, 64};
+                              128, 64, 128, 64, 64, 128, 64, 128, 64, 64,
+                              128, 256, 128, 256};
+constexpr int VAR_WM[NVAR] = {2, 2, 2, 2, 2, 2, 2, 2, 2, 2, 2, 2, 2, 2, 2, 2, 2, 2, 2, 2,
+                              2, 2, 2, 2, 2, 2, 2, 2, 2, 2, 4, 2, 4, 2};
 
 int heuristic_variant(int M, int Ncol, int K) {
   (void)M;
@@ -509,6 +521,10 @@ int launch_variant(int v, const NTParams& p, hipStream_t st) {
     case 27: return launch<64, 128, 1, CS64, false, true>(p, st);
     case 28: return launch<128, 64, 1, CS64, false, true>(p, st);
     case 29: return launch<64, 64, 1, CS64, false, true>(p, st);
+    case 30: return launch<256, 128, 2, CS64, false, true, 512, 4>(p, st);
+    case 31: return launch<128, 256, 2, CS64, false, true, 512, 2>(p, st);
+    case 32: return launch<256, 128, 2, CS64, false, false, 512, 4>(p, st);
+    case 33: return launch<128, 256, 2, CS64, false, false, 512, 2>(p, st);
   }
   return -3;
 }
@@ -525,7 +541,7 @@ PDT_API int pdt_conv_nt_resolve_variant(int variant, int M, int Ncol, int K) {
 PDT_API int pdt_conv_nt_stat_rows(int M, int Ncol, int K, int variant) {
   int v = pdt_conv_nt_resolve_variant(variant, M, Ncol, K);
   int BM = VAR_BM[v];
-  return ((M + BM - 1) / BM) * 2;
+  return ((M + BM - 1) / BM) * VAR_WM[v];
 }
 
 // Generic launch: see header comment for the meaning of every argument.
