@@ -32,9 +32,7 @@ class Attention(nn.Module):
     def forward(self, x, fp8=False):
         B, T, D = x.shape
         qkv = fused.linear(x, self.qkv, fp8=fp8)                          # [B,T,3D]
-        qkv = qkv.view(B, T, 3, self.num_heads, self.head_dim).permute(2, 0, 3, 1, 4)
-        o = fused.attention(qkv[0], qkv[1], qkv[2])                        # [B,H,T,hd]
-        o = o.transpose(1, 2).reshape(B, T, D)
+        o = fused.qkv_attention(qkv, self.num_heads)                       # [B,T,D]
         return fused.linear(o, self.proj, fp8=fp8)
 
 

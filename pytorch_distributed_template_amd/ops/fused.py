@@ -129,6 +129,19 @@ def attention(q, k, v):
     return F.scaled_dot_product_attention(q, k, v)
 
 
+def qkv_attention(qkv, num_heads: int):
+    """Multi-head attention on a packed qkv projection [B, T, 3*H*hd] -> [B, T, H*hd].
+    Native path: one fused MFMA kernel (hd = 64); torch path: SDPA."""
+    B, T, D3 = qkv.shape
+    hd = D3 // (3 * num_heads)
+    if _use_native(qkv) and hd == 64:
+        from . import native_ops
+        return native_ops.qkv_attention(qkv, num_heads)
+    q, k, v = qkv.view(B, T, 3, num_heads, hd).permute(2, 0, 3, 1, 4)
+    o = F.scaled_dot_product_attention(q, k, v)
+    return o.transpose(1, 2).reshape(B, T, num_heads * hd)
+
+
 def patch_embed(x, conv: nn.Conv2d):
     """Non-overlapping patch conv -> [B, N, D] tokens."""
     if _use_native(x):

@@ -64,6 +64,8 @@ _SIGS = {
     "pdt_wt_dgrad": (c_int, [P, P] + [c_int] * 9 + [P]),
     "pdt_transpose_cast": (c_int, [P, P, c_int, c_int, P]),
     "pdt_add_bf16": (c_int, [P, P, P, c_long, P]),
+    "pdt_attn_fwd": (c_int, [P, P, P, c_int, c_int, c_int, c_float, P]),
+    "pdt_attn_bwd": (c_int, [P, P, P, P, P, P, c_int, c_int, c_int, c_float, P]),
 }
 
 
@@ -228,8 +230,9 @@ def select_nt_variant(src, b, out, *, with_stats=False, bias=None, act=0, **a):
         return lib.pdt_conv_nt_resolve_variant(-1, M, a["Ncol"], a["K"])
     _check_nt(src, b, out, a)
     nvar = lib.pdt_conv_nt_num_variants()
-    stats = torch.empty(2 * ((M + 63) // 64) * 2 * a["Ncol"], dtype=torch.float32, device=src.device) \
-        if with_stats else None
+    # partial-stat rows depend on the variant's BM and waves-along-M: size for the largest
+    rows = max(lib.pdt_conv_nt_stat_rows(M, a["Ncol"], a["K"], v) for v in range(nvar))
+    stats = torch.empty(2 * rows * a["Ncol"], dtype=torch.float32, device=src.device) if with_stats else None
     best, best_t = -1, float("inf")
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     for v in range(nvar):
@@ -840,6 +843,42 @@ def softmax_cross_entropy(logits, target, label_smoothing=0.0):
 # =============================================================================
 # ViT ops (torch path for now on GPU as well; native kernels land in ops/vit_ops)
 # =============================================================================
+class _QKVAttention(torch.autograd.Function):
+    """Fused multi-head attention straight off the qkv projection output
+    (csrc/attention.hip): qkv [B, T, 3*H*64] -> out [B, T, H*64] (the proj
+    GEMM's input layout) with the log-sum-exp saved for the recomputing
+    backward, which writes d(qkv) in the qkv layout (the qkv GEMM's dY)."""
+
+    @staticmethod
+    def forward(ctx, qkv, H):
+        B, T, D3 = qkv.shape
+        assert D3 == 3 * H * 64 and qkv.dtype == torch.bfloat16, "head_dim must be 64, bf16"
+        qkv = qkv.contiguous()
+        out = torch.empty((B, T, H * 64), dtype=torch.bfloat16, device=qkv.device)
+        lse = torch.empty((B * H, T), dtype=torch.float32, device=qkv.device)
+        scale = 64 ** -0.5
+        _chk(_load().pdt_attn_fwd(_p(qkv), _p(out), _p(lse), B, T, H, scale, _s()), "attn_fwd")
+        ctx.save_for_backward(qkv, out, lse)
+        ctx.H, ctx.scale = H, scale
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        qkv, out, lse = ctx.saved_tensors
+        B, T, _ = qkv.shape
+        dout = dout.to(torch.bfloat16).contiguous()
+        delta = torch.empty_like(lse)
+        dqkv = torch.empty_like(qkv)
+        _chk(_load().pdt_attn_bwd(_p(qkv), _p(out), _p(dout), _p(lse), _p(delta), _p(dqkv), B, T, ctx.H,
+                                  ctx.scale, _s()), "attn_bwd")
+        return dqkv, None
+
+
+def qkv_attention(qkv, num_heads):
+    """softmax(q k^T / 8) v over heads of 64 for a packed [B, T, 3*H*64] qkv."""
+    return _QKVAttention.apply(qkv, num_heads)
+
+
 def attention(q, k, v):
     return torch.nn.functional.scaled_dot_product_attention(q, k, v)
 

@@ -6,7 +6,8 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import torch, torch.nn as nn, torch.nn.functional as F
 from pytorch_distributed_template_amd.ops import native_ops as no
 
-shapes = [(2, 256, 56, 56, 512, 1, 2, 0), (2, 128, 56, 56, 128, 3, 2, 1), (4, 64, 56, 56, 64, 1, 1, 0)]
+shapes = [(2, 256, 56, 56, 512, 1, 2, 0), (2, 128, 56, 56, 128, 3, 2, 1), (4, 64, 56, 56, 64, 1, 1, 0),
+          (4, 1024, 4, 4, 2048, 1, 2, 0), (4, 512, 2, 2, 512, 3, 1, 1), (4, 256, 8, 8, 256, 3, 1, 1)]
 for (N, Cin, H, W, Cout, k, s, p) in shapes:
     torch.manual_seed(0)
     conv = nn.Conv2d(Cin, Cout, k, s, p, bias=False).cuda()

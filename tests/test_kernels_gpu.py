@@ -404,3 +404,28 @@ def test_vit_native_train_step():
     fused.set_backend("auto")
     assert torch.isfinite(loss)
     assert all(p.grad is not None and torch.isfinite(p.grad).all() for p in m.parameters() if p.requires_grad)
+
+
+@pytest.mark.parametrize("B,T,H", [(3, 197, 4), (2, 64, 2), (1, 50, 12), (2, 300, 3)])
+def test_fused_qkv_attention(B, T, H):
+    """Fused MFMA attention (fwd + recomputing bwd) vs an fp32 softmax reference."""
+    torch.manual_seed(B * 1000 + T)
+    qkv = (torch.randn(B, T, 3 * H * 64, device="cuda") * 1.5).to(torch.bfloat16)
+    dout = torch.randn(B, T, H * 64, device="cuda").to(torch.bfloat16)
+
+    x = qkv.float().requires_grad_(True)
+    q, k, v = x.view(B, T, 3, H, 64).permute(2, 0, 3, 1, 4)
+    p = torch.softmax(q @ k.transpose(-1, -2) / 8.0, dim=-1)
+    ref = (p @ v).transpose(1, 2).reshape(B, T, H * 64)
+    ref.backward(dout.float())
+
+    xn = qkv.clone().requires_grad_(True)
+    out = no.qkv_attention(xn, H)
+    out.backward(dout)
+    torch.cuda.synchronize()
+    assert out.shape == ref.shape and out.dtype == torch.bfloat16
+    assert nrmerr(out, ref) < 1e-2, nrmerr(out, ref)
+    g, gr = xn.grad.view(B, T, 3, H * 64), x.grad.view(B, T, 3, H * 64)
+    for i, name in enumerate("qkv"):
+        e = nrmerr(g[:, :, i], gr[:, :, i])
+        assert e < 2e-2, (name, e)
