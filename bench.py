@@ -41,6 +41,7 @@ def parse():
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--batch", type=int, default=256, help="per-GPU batch")
     ap.add_argument("--model", default="resnet50")
+    ap.add_argument("--fp8", action="store_true", help="ViT: fp8 (e4m3/e5m2) GEMMs on the native path")
     ap.add_argument("--backend", default="native", choices=["native", "torch"])
     ap.add_argument("--bucket-mb", type=float, default=64.0)
     ap.add_argument("--comm-hook", default=None, choices=[None, "bf16"])
@@ -67,7 +68,8 @@ def main():
 
     torch.manual_seed(1234)
     ctor = {"resnet50": models.resnet50, "resnet152": models.resnet152, "vit_b_16": models.vit_b_16}[args.model]
-    model = ctor(num_classes=1000).to(device).to(memory_format=torch.channels_last)
+    kw = {"fp8": True} if args.fp8 else {}
+    model = ctor(num_classes=1000, **kw).to(device).to(memory_format=torch.channels_last)
     from pytorch_distributed_template_amd.optim import FusedAdamW, FusedSGD
     if args.model.startswith("vit"):
         opt_name = "AdamW(lr=1e-3, wd=0.05)"
@@ -160,7 +162,7 @@ def main():
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": round(value / (stock * world), 4) if stock else None,
-        "dtype": "bf16",
+        "dtype": "fp8(e4m3 fwd, e5m2 dgrad)+bf16" if args.fp8 else "bf16",
         "data": "synthetic (device-resident random 3x224x224, random-init weights)",
         "config": {"model": args.model, "global_batch": args.batch * world, "per_gpu_batch": args.batch,
                    "seq_len": None, "image_size": 224, "parallelism": f"dp{world}",

@@ -48,6 +48,8 @@ struct NTParams {
   int nstat_rows;
   int nt_store;        // 1: non-temporal (streaming) output stores
   int ident_out;       // 1: output row == m (no stride-phase remap) -> skip the index math
+  const float* dq_a;   // fp8 only: dequant scale of the A (src) operand (device scalar)
+  const float* dq_b;   // fp8 only: dequant scale of the B operand
   FastDiv div_Wm, div_HWm, div_Cs8, div_ntw;
 };
 
@@ -56,10 +58,23 @@ constexpr int NT = 256;
 
 __device__ __forceinline__ int swz(int row, int chunk) { return chunk ^ ((row >> 1) & 7); }
 
+typedef int i32x8 __attribute__((ext_vector_type(8)));
+__device__ __forceinline__ i32x8 cat8(const bf16x8& lo, const bf16x8& hi) {
+  const u32x4 a = __builtin_bit_cast(u32x4, lo), b = __builtin_bit_cast(u32x4, hi);
+  return i32x8{(int)a[0], (int)a[1], (int)a[2], (int)a[3], (int)b[0], (int)b[1], (int)b[2], (int)b[3]};
+}
+
 // 16 zero bytes: the global_load_lds source for padding / out-of-range rows
 __device__ __attribute__((aligned(64))) u32x4 pdt_zero_chunk[4];
 
-template <int BM, int BN, int NSTAGE, bool CS64, bool DIRECT, bool GLDS, int NTH = 256, int WM = 2>
+// F8 = 0: bf16 operands. F8 = 1 / 2: fp8 operands (B = OCP e4m3; src = e4m3 / e5m2)
+// handled as byte PAIRS -- every index below is in 2-byte units, so staging,
+// swizzle and gather are unchanged -- and one block-scaled
+// mfma_scale_f32_16x16x128_f8f6f4 (2x the bf16 MFMA rate, unit block scales)
+// consumes a whole 128-byte LDS k-row: the two bf16 k-step fragments of a lane
+// ARE its 32-byte fp8 fragment (a k permutation shared by both operands).
+// The per-tensor dequant scales multiply the accumulators in the epilogue.
+template <int BM, int BN, int NSTAGE, bool CS64, bool DIRECT, bool GLDS, int NTH = 256, int WM = 2, int F8 = 0>
 __global__ void __launch_bounds__(NTH, 2) conv_nt_kernel(NTParams p) {
   constexpr int WN = NTH / 64 / WM;       // waves along N
   constexpr int MI = BM / (WM * 16);      // 16-row MFMA tiles per wave
@@ -248,6 +263,29 @@ __global__ void __launch_bounds__(NTH, 2) conv_nt_kernel(NTParams p) {
     }
     const char* sa = smem + cur * STAGE;
     const char* sb = sa + A_BYTES;
+    if constexpr (F8 != 0) {
+      bf16x8 af[2][MI], bfr[2][NI];
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) {
+        const int kch = kk * 4 + (lane >> 4);
+#pragma unroll
+        for (int i = 0; i < MI; ++i) {
+          int r = wm * (BM / WM) + i * 16 + (lane & 15);
+          af[kk][i] = *reinterpret_cast<const bf16x8*>(sa + r * 128 + swz(r, kch) * 16);
+        }
+#pragma unroll
+        for (int j = 0; j < NI; ++j) {
+          int r = wn * (BN / WN) + j * 16 + (lane & 15);
+          bfr[kk][j] = *reinterpret_cast<const bf16x8*>(sb + r * 128 + swz(r, kch) * 16);
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < MI; ++i)
+#pragma unroll
+        for (int j = 0; j < NI; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(
+              cat8(bfr[0][j], bfr[1][j]), cat8(af[0][i], af[1][i]), acc[i][j], 0, F8 == 2 ? 1 : 0, 0, 127, 0, 127);
+    } else
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk) {
       const int kch = kk * 4 + (lane >> 4);
@@ -294,6 +332,13 @@ __global__ void __launch_bounds__(NTH, 2) conv_nt_kernel(NTParams p) {
   // acc[i][j][r] = C[row = wm*BM/2 + i*16 + (lane&15)][col = wn*BN/2 + j*16 + (lane>>4)*4 + r]
   const int lrow = lane & 15;
   const int lcol = (lane >> 4) * 4;
+  if constexpr (F8 != 0) {
+    const float alpha = p.dq_a[0] * p.dq_b[0];
+#pragma unroll
+    for (int i = 0; i < MI; ++i)
+#pragma unroll
+      for (int j = 0; j < NI; ++j) acc[i][j] *= alpha;
+  }
   if (p.bias != nullptr) {
 #pragma unroll
     for (int j = 0; j < NI; ++j) {
@@ -455,11 +500,11 @@ __global__ void __launch_bounds__(NTH, 2) conv_nt_kernel(NTParams p) {
   stage_store(p.out, p.addend);
 }
 
-template <int BM, int BN, int NS, bool CS64, bool DIRECT, bool GLDS = false, int NTH = 256, int WM = 2>
+template <int BM, int BN, int NS, bool CS64, bool DIRECT, bool GLDS = false, int NTH = 256, int WM = 2, int F8 = 0>
 int launch(const NTParams& p, hipStream_t st) {
   int ntm = (p.M + BM - 1) / BM, ntn = (p.Ncol + BN - 1) / BN;
-  hipLaunchKernelGGL((conv_nt_kernel<BM, BN, NS, CS64, DIRECT, GLDS, NTH, WM>), dim3(ntm * ntn), dim3(NTH), 0, st,
-                     p);
+  hipLaunchKernelGGL((conv_nt_kernel<BM, BN, NS, CS64, DIRECT, GLDS, NTH, WM, F8>), dim3(ntm * ntn), dim3(NTH), 0,
+                     st, p);
   PDT_RETURN_LAUNCH();
 }
 
@@ -568,6 +613,7 @@ PDT_API int pdt_conv_nt(const void* src, const void* b, void* out, float* stats,
   p.Ho = Ho; p.Wo = Wo; p.osh = osh; p.osw = osw; p.oph = oph; p.opw = opw; p.ldo = ldo;
   p.act = act;
   p.aux = (u16*)aux;
+  p.dq_a = p.dq_b = nullptr;
   p.div_Wm = make_fastdiv(Wm);
   p.div_HWm = make_fastdiv(Hm * Wm);
   p.div_Cs8 = make_fastdiv(Cs / 8);
@@ -585,4 +631,64 @@ PDT_API int pdt_conv_nt(const void* src, const void* b, void* out, float* stats,
   p.nstat_rows = pdt_conv_nt_stat_rows(p.M, Ncol, K, v);
   const bool cs64 = (Cs % 64) == 0;
   return cs64 ? launch_variant<true>(v, p, stream) : launch_variant<false>(v, p, stream);
+}
+
+// ---------------------------------------------------------------------------
+// fp8 GEMM  out[m, n] = dq_a * dq_b * sum_k A[m, k] B[n, k] (+ bias, act, aux)
+// A: [M][lda] fp8 (e4m3 if fmt_a == 0, e5m2 if 1), B: [N][ldb] e4m3, out bf16 [M][ldo].
+// K, lda, ldb in BYTES (= elements), multiples of 128 / 16 / 16.
+namespace {
+constexpr int NVAR_F8 = 8;
+constexpr int VAR_F8_BM[NVAR_F8] = {128, 128, 256, 128, 64, 128, 256, 128};
+constexpr int VAR_F8_BN[NVAR_F8] = {128, 128, 128, 256, 128, 64, 64, 128};
+
+template <int F8>
+int launch_f8(int v, const NTParams& p, hipStream_t st) {
+  switch (v) {
+    case 0: return launch<128, 128, 2, true, false, false, 256, 2, F8>(p, st);
+    case 1: return launch<128, 128, 2, true, false, true, 256, 2, F8>(p, st);
+    case 2: return launch<256, 128, 2, true, false, true, 512, 4, F8>(p, st);
+    case 3: return launch<128, 256, 2, true, false, true, 512, 2, F8>(p, st);
+    case 4: return launch<64, 128, 2, true, false, true, 256, 2, F8>(p, st);
+    case 5: return launch<128, 64, 2, true, false, true, 256, 2, F8>(p, st);
+    case 6: return launch<256, 64, 2, true, false, true, 256, 2, F8>(p, st);
+    case 7: return launch<128, 128, 2, true, true, true, 256, 2, F8>(p, st);
+  }
+  return -3;
+}
+}  // namespace
+
+PDT_API int pdt_gemm_f8_num_variants() { return NVAR_F8; }
+
+PDT_API int pdt_gemm_f8(const void* a, const void* b, void* out, const float* bias, const float* dq_a,
+                        const float* dq_b, int M, int N, int K, int lda, int ldb, int ldo, int fmt_a, int act,
+                        void* aux, int variant, hipStream_t stream) {
+  if (K % 128 != 0 || lda % 16 != 0 || ldb % 16 != 0 || N % 8 != 0 || ldo % 8 != 0) return -1;
+  if (lda != K) return -2;  // rows of A are dense (the gather's source row stride is Cs)
+  NTParams p;
+  p.src = (const u16*)a;
+  p.b = (const u16*)b;
+  p.out = (u16*)out;
+  p.stats = nullptr;
+  p.bias = bias;
+  p.addend = nullptr;
+  p.Hs = 1; p.Ws = 1; p.Cs = K / 2;
+  p.Hm = 1; p.Wm = 1;
+  p.M = M;
+  p.Ncol = N; p.K = K / 2; p.ldb = ldb / 2;
+  p.sh = 1; p.sw = 1; p.oh0 = 0; p.ow0 = 0; p.dh = 1; p.dw = 1; p.nth = 1; p.ntw = 1;
+  p.Ho = 1; p.Wo = 1; p.osh = 1; p.osw = 1; p.oph = 0; p.opw = 0; p.ldo = ldo;
+  p.act = act;
+  p.aux = (u16*)aux;
+  p.nstat_rows = 0;
+  p.nt_store = 0;
+  p.ident_out = 1;
+  p.dq_a = dq_a;
+  p.dq_b = dq_b;
+  p.div_Wm = make_fastdiv(1);
+  p.div_HWm = make_fastdiv(1);
+  p.div_Cs8 = make_fastdiv(K / 16);
+  p.div_ntw = make_fastdiv(1);
+  const int v = (variant >= 0 && variant < NVAR_F8) ? variant : 1;
+  return fmt_a == 1 ? launch_f8<2>(v, p, stream) : launch_f8<1>(v, p, stream);
 }

@@ -1,0 +1,182 @@
+// FP8 (OCP e4m3fn / e5m2) quantization for the fp8 GEMM path with per-tensor
+// "current" scaling, no host round trip:
+//
+//   pdt_amax_partial : grid-stride |x| max -> partial[nblk]   (no atomics, no memset)
+//   pdt_cast_fp8     : every block re-reduces the <= 1024 partials (4 KB, L2),
+//                      scale = FP8_MAX / amax, writes q = sat(x * scale) as fp8
+//                      and block 0 writes dq = 1 / scale (the GEMM epilogue's
+//                      dequant factor); optional [R][C] -> [C][R] transpose
+//                      (weights for the dgrad GEMM) through a 64x64 LDS tile.
+//
+// The conversions are the gfx950 packed converts v_cvt_pk_fp8_f32 /
+// v_cvt_pk_bf8_f32 (round to nearest even); inputs are clamped to the format's
+// finite range first, so nothing overflows to NaN.
+#include "pdt_common.h"
+
+namespace {
+
+constexpr int AMAX_BLOCKS = 1024;
+
+template <bool BF16>
+__device__ __forceinline__ float ld(const void* p, long i) {
+  if (BF16) return bf2f(reinterpret_cast<const u16*>(p)[i]);
+  return reinterpret_cast<const float*>(p)[i];
+}
+
+template <bool BF16>
+__global__ void __launch_bounds__(256) amax_partial_kernel(const void* __restrict__ x, long n,
+                                                           float* __restrict__ partial) {
+  __shared__ float red[4];
+  float m = 0.f;
+  const long stride = (long)gridDim.x * 256 * 8;
+  for (long base = ((long)blockIdx.x * 256 + threadIdx.x) * 8; base < n; base += stride) {
+    if (BF16 && base + 8 <= n) {
+      const u32x4 v = *reinterpret_cast<const u32x4*>(reinterpret_cast<const u16*>(x) + base);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) m = fmaxf(m, fmaxf(fabsf(lo_bf(v[e])), fabsf(hi_bf(v[e]))));
+    } else {
+      for (long i = base; i < base + 8 && i < n; ++i) m = fmaxf(m, fabsf(ld<BF16>(x, i)));
+    }
+  }
+  m = warp_max(m);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = m;
+  __syncthreads();
+  if (threadIdx.x == 0) partial[blockIdx.x] = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
+}
+
+// amax from the partials; every thread of the block gets it
+__device__ __forceinline__ float block_amax(const float* __restrict__ partial, int nblk) {
+  __shared__ float red[4];
+  float m = 0.f;
+  for (int i = threadIdx.x; i < nblk; i += blockDim.x) m = fmaxf(m, partial[i]);
+  m = warp_max(m);
+  __syncthreads();
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = m;
+  __syncthreads();
+  return fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
+}
+
+template <int FMT>
+__device__ __forceinline__ uint32_t cvt4(float a, float b, float c, float d) {
+  constexpr float FMAX = FMT == 0 ? 448.f : 57344.f;
+  a = fminf(fmaxf(a, -FMAX), FMAX);
+  b = fminf(fmaxf(b, -FMAX), FMAX);
+  c = fminf(fmaxf(c, -FMAX), FMAX);
+  d = fminf(fmaxf(d, -FMAX), FMAX);
+  int r;
+  if (FMT == 0) {
+    r = __builtin_amdgcn_cvt_pk_fp8_f32(a, b, 0, false);
+    r = __builtin_amdgcn_cvt_pk_fp8_f32(c, d, r, true);
+  } else {
+    r = __builtin_amdgcn_cvt_pk_bf8_f32(a, b, 0, false);
+    r = __builtin_amdgcn_cvt_pk_bf8_f32(c, d, r, true);
+  }
+  return (uint32_t)r;
+}
+
+template <int FMT>
+__device__ __forceinline__ float scale_from(float amax) {
+  constexpr float FMAX = FMT == 0 ? 448.f : 57344.f;
+  return amax > 0.f ? FMAX / amax : 1.f;
+}
+
+template <bool BF16, int FMT>
+__global__ void __launch_bounds__(256) cast_fp8_kernel(const void* __restrict__ x, long n,
+                                                       const float* __restrict__ partial, int nblk,
+                                                       uint8_t* __restrict__ q, float* __restrict__ dq) {
+  const float s = scale_from<FMT>(block_amax(partial, nblk));
+  if (blockIdx.x == 0 && threadIdx.x == 0) dq[0] = 1.f / s;
+  const long stride = (long)gridDim.x * 256 * 8;
+  for (long base = ((long)blockIdx.x * 256 + threadIdx.x) * 8; base < n; base += stride) {
+    float v[8];
+    if (BF16 && base + 8 <= n) {
+      const u32x4 w = *reinterpret_cast<const u32x4*>(reinterpret_cast<const u16*>(x) + base);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        v[2 * e] = lo_bf(w[e]);
+        v[2 * e + 1] = hi_bf(w[e]);
+      }
+    } else {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] = base + e < n ? ld<BF16>(x, base + e) : 0.f;
+    }
+    if (base + 8 <= n) {
+      uint2 o;
+      o.x = cvt4<FMT>(v[0] * s, v[1] * s, v[2] * s, v[3] * s);
+      o.y = cvt4<FMT>(v[4] * s, v[5] * s, v[6] * s, v[7] * s);
+      *reinterpret_cast<uint2*>(q + base) = o;
+    } else {
+      for (long i = base; i < n; ++i) q[i] = (uint8_t)(cvt4<FMT>(v[i - base] * s, 0.f, 0.f, 0.f) & 0xff);
+    }
+  }
+}
+
+// [R][C] fp32 -> fp8 [C][R] with the tensor's scale (64x64 tiles, 256 threads)
+template <int FMT>
+__global__ void __launch_bounds__(256) cast_fp8_t_kernel(const float* __restrict__ x, int R, int C,
+                                                         const float* __restrict__ partial, int nblk,
+                                                         uint8_t* __restrict__ q) {
+  __shared__ float tile[64][65];
+  const float s = scale_from<FMT>(block_amax(partial, nblk));
+  const int r0 = blockIdx.y * 64, c0 = blockIdx.x * 64;
+  const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+  for (int i = ty; i < 64; i += 4) {
+    const int r = r0 + i, c = c0 + tx;
+    tile[i][tx] = (r < R && c < C) ? x[(long)r * C + c] * s : 0.f;
+  }
+  __syncthreads();
+  // out row = c (64 of them), 64 bytes each: thread -> (row, 4-byte group)
+  for (int i = threadIdx.x; i < 64 * 16; i += 256) {
+    const int oc = i >> 4, g = (i & 15) * 4;
+    const int c = c0 + oc, r = r0 + g;
+    if (c < C && r + 3 < R) {
+      *reinterpret_cast<uint32_t*>(q + (long)c * R + r) =
+          cvt4<FMT>(tile[g][oc], tile[g + 1][oc], tile[g + 2][oc], tile[g + 3][oc]);
+    } else if (c < C) {
+      for (int e = 0; e < 4 && r + e < R; ++e)
+        q[(long)c * R + r + e] = (uint8_t)(cvt4<FMT>(tile[g + e][oc], 0.f, 0.f, 0.f) & 0xff);
+    }
+  }
+}
+
+int nblocks(long n) {
+  long b = (n + 256 * 8 - 1) / (256 * 8);
+  if (b > AMAX_BLOCKS) b = AMAX_BLOCKS;
+  return b < 1 ? 1 : (int)b;
+}
+
+}  // namespace
+
+PDT_API int pdt_amax_blocks(long n) { return nblocks(n); }
+
+PDT_API int pdt_amax_partial(const void* x, int bf16, long n, float* partial, hipStream_t st) {
+  const int nb = nblocks(n);
+  if (bf16)
+    hipLaunchKernelGGL(amax_partial_kernel<true>, dim3(nb), dim3(256), 0, st, x, n, partial);
+  else
+    hipLaunchKernelGGL(amax_partial_kernel<false>, dim3(nb), dim3(256), 0, st, x, n, partial);
+  PDT_RETURN_LAUNCH();
+}
+
+// fmt: 0 = e4m3fn, 1 = e5m2
+PDT_API int pdt_cast_fp8(const void* x, int bf16, long n, const float* partial, int fmt, void* q, float* dq,
+                         hipStream_t st) {
+  const int nb = nblocks(n);
+  uint8_t* qo = (uint8_t*)q;
+  if (bf16) {
+    if (fmt == 0) hipLaunchKernelGGL((cast_fp8_kernel<true, 0>), dim3(nb), dim3(256), 0, st, x, n, partial, nb, qo, dq);
+    else hipLaunchKernelGGL((cast_fp8_kernel<true, 1>), dim3(nb), dim3(256), 0, st, x, n, partial, nb, qo, dq);
+  } else {
+    if (fmt == 0) hipLaunchKernelGGL((cast_fp8_kernel<false, 0>), dim3(nb), dim3(256), 0, st, x, n, partial, nb, qo, dq);
+    else hipLaunchKernelGGL((cast_fp8_kernel<false, 1>), dim3(nb), dim3(256), 0, st, x, n, partial, nb, qo, dq);
+  }
+  PDT_RETURN_LAUNCH();
+}
+
+// fp32 [R][C] -> e4m3 [C][R]; the partials must come from pdt_amax_partial over the same R*C values
+PDT_API int pdt_cast_fp8_t(const float* x, int R, int C, const float* partial, void* q, hipStream_t st) {
+  const int nb = nblocks((long)R * C);
+  dim3 grid((C + 63) / 64, (R + 63) / 64);
+  hipLaunchKernelGGL(cast_fp8_t_kernel<0>, grid, dim3(256), 0, st, x, R, C, partial, nb, (uint8_t*)q);
+  PDT_RETURN_LAUNCH();
+}

@@ -65,6 +65,12 @@ _SIGS = {
     "pdt_transpose_cast": (c_int, [P, P, c_int, c_int, P]),
     "pdt_add_bf16": (c_int, [P, P, P, c_long, P]),
     "pdt_attn_fwd": (c_int, [P, P, P, c_int, c_int, c_int, c_float, P]),
+    "pdt_gemm_f8_num_variants": (c_int, []),
+    "pdt_gemm_f8": (c_int, [P, P, P, P, P, P] + [c_int] * 8 + [P, c_int, P]),
+    "pdt_amax_blocks": (c_int, [c_long]),
+    "pdt_amax_partial": (c_int, [P, c_int, c_long, P, P]),
+    "pdt_cast_fp8": (c_int, [P, c_int, c_long, P, c_int, P, P, P]),
+    "pdt_cast_fp8_t": (c_int, [P, c_int, c_int, P, P, P]),
     "pdt_attn_bwd": (c_int, [P, P, P, P, P, P, c_int, c_int, c_int, c_float, P]),
 }
 
@@ -198,6 +204,54 @@ def _save_tuned():
         pass
 
 
+def _tune_allowed() -> bool:
+    return os.environ.get("PDT_AUTOTUNE", "1") != "0" and not torch.cuda.is_current_stream_capturing()
+
+
+def _time_variants(nvar, launch, allowed=None):
+    """Fastest variant id: one warm launch, then the best of two 3-launch HIP-event trials."""
+    best, best_t = -1, float("inf")
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    for v in range(nvar):
+        if allowed is not None and v not in allowed:
+            continue
+        _chk(launch(v), f"tune variant {v}")
+        t = float("inf")
+        for _ in range(2):
+            ev0.record()
+            for _ in range(3):
+                launch(v)
+            ev1.record()
+            ev1.synchronize()
+            t = min(t, ev0.elapsed_time(ev1))
+        if t < best_t:
+            best, best_t = v, t
+    return best
+
+
+def _autotune(key, nvar, launch, default=0):
+    table = _tuned()
+    if key in table:
+        return int(table[key])
+    if not _tune_allowed():
+        return default
+    table[key] = _time_variants(nvar, launch)
+    _save_tuned()
+    return table[key]
+
+
+def _variant_filter():
+    """PDT_NT_VARIANTS="0-29,31" restricts the conv_nt variants the tuner may pick."""
+    spec = os.environ.get("PDT_NT_VARIANTS")
+    if not spec:
+        return None
+    out = set()
+    for part in spec.split(","):
+        lo, _, hi = part.partition("-")
+        out.update(range(int(lo), int(hi or lo) + 1))
+    return out
+
+
 def _nt_args(src, b, out, stats, bias, a, act, variant, addend=None, aux=None):
     return (_p(src), _p(b), _p(out), _p(stats), _p(bias), _p(addend), a["Hs"], a["Ws"], a["Cs"], a["Nimg"], a["Hm"], a["Wm"],
             a["Ncol"], a["K"], a["ldb"], a["sh"], a["sw"], a["oh0"], a["ow0"], a["dh"], a["dw"], a["nth"], a["ntw"],
@@ -233,19 +287,8 @@ def select_nt_variant(src, b, out, *, with_stats=False, bias=None, act=0, **a):
     # partial-stat rows depend on the variant's BM and waves-along-M: size for the largest
     rows = max(lib.pdt_conv_nt_stat_rows(M, a["Ncol"], a["K"], v) for v in range(nvar))
     stats = torch.empty(2 * rows * a["Ncol"], dtype=torch.float32, device=src.device) if with_stats else None
-    best, best_t = -1, float("inf")
-    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    for v in range(nvar):
-        args = _nt_args(src, b, out, stats, bias, a, act, v)
-        _chk(lib.pdt_conv_nt(*args), "conv_nt(tune)")
-        ev0.record()
-        for _ in range(3):
-            lib.pdt_conv_nt(*args)
-        ev1.record()
-        ev1.synchronize()
-        t = ev0.elapsed_time(ev1)
-        if t < best_t:
-            best, best_t = v, t
+    best = _time_variants(nvar, lambda v: lib.pdt_conv_nt(*_nt_args(src, b, out, stats, bias, a, act, v)),
+                          _variant_filter())
     table[key] = best
     _save_tuned()
     return best
@@ -748,12 +791,128 @@ class _Linear(torch.autograd.Function):
         return dx, dw, db, None
 
 
+# =============================================================================
+# FP8 linear (OCP e4m3 forward operands, e5m2 output gradients) -- csrc/fp8.hip
+# quantizes with per-tensor current scaling entirely on device; the GEMMs are
+# the block-scaled fp8 MFMA instantiation of conv_nt (csrc/conv_igemm.hip,
+# pdt_gemm_f8). Weight gradients stay bf16 (the wgrad kernel), as in common
+# fp8 training recipes.
+# =============================================================================
+E4M3, E5M2 = 0, 1
+
+
+def quantize_fp8(x: torch.Tensor, fmt: int = E4M3):
+    """(q uint8 same shape, dq fp32[1]) with x ~= q.float() * dq (per-tensor scale)."""
+    lib = _load()
+    x = x.contiguous()
+    assert x.dtype in (torch.bfloat16, torch.float32)
+    n = x.numel()
+    part = torch.empty(lib.pdt_amax_blocks(n), dtype=torch.float32, device=x.device)
+    q = torch.empty(x.shape, dtype=torch.uint8, device=x.device)
+    dq = torch.empty(1, dtype=torch.float32, device=x.device)
+    bf = int(x.dtype == torch.bfloat16)
+    _chk(lib.pdt_amax_partial(_p(x), bf, n, _p(part), _s()), "amax")
+    _chk(lib.pdt_cast_fp8(_p(x), bf, n, _p(part), fmt, _p(q), _p(dq), _s()), "cast_fp8")
+    return q, dq
+
+
+_F8W: dict = {}
+
+
+def fp8_weight(w: torch.Tensor):
+    """(wq [N][K] e4m3, wqt [K][N] e4m3, dq) of an fp32 [N][K] weight, cached per optimizer version."""
+    ent = _F8W.get(id(w))
+    if ent is not None and ent[0] == w._version and ent[1] == w.data_ptr():
+        return ent[2]
+    lib = _load()
+    src = w.detach().float().contiguous()
+    N, K = src.shape
+    part = torch.empty(lib.pdt_amax_blocks(src.numel()), dtype=torch.float32, device=w.device)
+    wq = torch.empty((N, K), dtype=torch.uint8, device=w.device)
+    wqt = torch.empty((K, N), dtype=torch.uint8, device=w.device)
+    dq = torch.empty(1, dtype=torch.float32, device=w.device)
+    st = _s()
+    _chk(lib.pdt_amax_partial(_p(src), 0, src.numel(), _p(part), st), "amax")
+    _chk(lib.pdt_cast_fp8(_p(src), 0, src.numel(), _p(part), E4M3, _p(wq), _p(dq), st), "cast_fp8")
+    _chk(lib.pdt_cast_fp8_t(_p(src), N, K, _p(part), _p(wqt), st), "cast_fp8_t")
+    val = (wq, wqt, dq)
+    _F8W[id(w)] = (w._version, w.data_ptr(), val)
+    return val
+
+
+def gemm_f8(a, b, out, dq_a, dq_b, *, fmt_a=E4M3, bias=None, act=0, aux=None, variant=None):
+    """out[M, N] (bf16) = dq_a*dq_b * a[M, K] @ b[N, K]^T (+bias, act); a, b uint8 fp8 codes."""
+    M, K = a.shape
+    N = b.shape[0]
+    assert a.dtype == torch.uint8 and b.dtype == torch.uint8 and b.shape[1] == K and K % 128 == 0
+    assert out.dtype == torch.bfloat16 and out.numel() == M * N and a.is_contiguous() and b.is_contiguous()
+    lib = _load()
+    args = lambda v: (_p(a), _p(b), _p(out), _p(bias), _p(dq_a), _p(dq_b), M, N, K, K, K, N, fmt_a, act,  # noqa
+                      _p(aux), v, _s())
+    if variant is None:
+        key = f"f8:{M},{N},{K},{fmt_a},{act},{int(bias is not None)}"
+        variant = _autotune(key, lib.pdt_gemm_f8_num_variants(), lambda v: lib.pdt_gemm_f8(*args(v)))
+    _chk(lib.pdt_gemm_f8(*args(variant)), "gemm_f8")
+    return out
+
+
+class _LinearF8(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, w, b, act):
+        shp = x.shape
+        x2 = x.reshape(-1, shp[-1]).to(torch.bfloat16).contiguous()
+        Mrows, K = x2.shape
+        Nout = w.shape[0]
+        xq, dqx = quantize_fp8(x2, E4M3)
+        wq, _, dqw = fp8_weight(w)
+        y = torch.empty((Mrows, Nout), dtype=torch.bfloat16, device=x.device)
+        z = torch.empty_like(y) if act == "gelu" else None
+        bias = b.float().contiguous() if b is not None else None
+        gemm_f8(xq, wq, y, dqx, dqw, bias=bias, act=ACT[act], aux=z)
+        ctx.save_for_backward(x2, w, y if act == "relu" else z)
+        ctx.meta = (shp, act, b is not None)
+        return y.reshape(*shp[:-1], Nout)
+
+    @staticmethod
+    def backward(ctx, dy):
+        x2, w, saved = ctx.saved_tensors
+        shp, act, has_b = ctx.meta
+        lib = _load()
+        Nout, K = w.shape
+        dy2 = dy.reshape(-1, Nout).to(torch.bfloat16).contiguous()
+        if act == "relu":
+            dy2 = dy2 * (saved > 0)
+        elif act == "gelu":
+            dz = torch.empty_like(dy2)
+            _chk(lib.pdt_gelu_bwd(_p(dy2), _p(saved), _p(dz), dz.numel(), _s()), "gelu_bwd")
+            dy2 = dz
+        Mrows = dy2.shape[0]
+        dx = None
+        if ctx.needs_input_grad[0]:
+            dyq, dqdy = quantize_fp8(dy2, E5M2)
+            _, wqt, dqw = fp8_weight(w)
+            dx = torch.empty((Mrows, K), dtype=torch.bfloat16, device=dy.device)
+            gemm_f8(dyq, wqt, dx, dqdy, dqw, fmt_a=E5M2)
+            dx = dx.reshape(*shp[:-1], K)
+        dw = None
+        if ctx.needs_input_grad[1]:
+            dw = torch.empty((Nout, K), dtype=torch.float32, device=dy.device)
+            conv_wgrad(dy2, x2, dw, M=Mrows, Mo=Nout, No=K, ldy=Nout, Hs=1, Ws=1, C=K, Hm=1, Wm=1, sh=1, sw=1,
+                       oh0=0, ow0=0, dh=1, dw=1, ntw=1)
+        db = None
+        if has_b and ctx.needs_input_grad[2]:
+            db = colsum(dy2, Mrows, Nout)
+        return dx, dw, db, None
+
+
 def linear(x, fc: nn.Linear, act=None, fp8=False):
     K = fc.in_features
     N = fc.out_features
     if K % 8 or N % 8 or act not in (None, "relu", "gelu"):
         from .fused import _torch_linear
         return _torch_linear(x, fc, act)
+    if fp8 and K % 128 == 0 and N % 128 == 0:
+        return _LinearF8.apply(x, fc.weight, fc.bias, act)
     return _Linear.apply(x, fc.weight, fc.bias, act)
 
 

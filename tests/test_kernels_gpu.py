@@ -429,3 +429,84 @@ def test_fused_qkv_attention(B, T, H):
     for i, name in enumerate("qkv"):
         e = nrmerr(g[:, :, i], gr[:, :, i])
         assert e < 2e-2, (name, e)
+
+
+def _f8(q, fmt):
+    return q.view(torch.float8_e4m3fn if fmt == no.E4M3 else torch.float8_e5m2).float()
+
+
+@pytest.mark.parametrize("fmt", [0, 1])
+def test_fp8_quantize_matches_torch_cast(fmt):
+    torch.manual_seed(11)
+    x = (torch.randn(1000, 384, device="cuda") * 3).to(torch.bfloat16)
+    x[3, 5] = 17.0  # amax
+    q, dq = no.quantize_fp8(x, fmt)
+    torch.cuda.synchronize()
+    fmax = 448.0 if fmt == 0 else 57344.0
+    assert abs(dq.item() - 17.0 / fmax) < 1e-6 * 17.0 / fmax + 1e-12
+    ref = (x.float() / dq).to(torch.float8_e4m3fn if fmt == 0 else torch.float8_e5m2)
+    same = (ref.view(torch.uint8) == q).float().mean().item()
+    assert same > 0.999, same
+    assert nrmerr(_f8(q, fmt) * dq, x) < (0.03 if fmt == 0 else 0.06)
+
+
+def test_fp8_weight_transpose_copy():
+    w = torch.randn(256, 384, device="cuda")
+    wq, wqt, dq = no.fp8_weight(w)
+    assert torch.equal(wq.t().contiguous(), wqt)
+    assert nrmerr(_f8(wq, 0) * dq, w) < 0.03
+
+
+@pytest.mark.parametrize("M,N,K", [(300, 256, 384), (1024, 768, 768), (64, 128, 128)])
+@pytest.mark.parametrize("fmt", [0, 1])
+def test_gemm_f8_all_variants(M, N, K, fmt):
+    """fp8 MFMA GEMM vs an fp32 GEMM of the same (dequantized) fp8 operands."""
+    torch.manual_seed(M + N + K)
+    a = torch.randn(M, K, device="cuda").to(torch.bfloat16)
+    b = torch.randn(N, K, device="cuda")
+    qa, dqa = no.quantize_fp8(a, fmt)
+    qb, dqb = no.quantize_fp8(b, 0)
+    bias = torch.randn(N, device="cuda")
+    ref = (_f8(qa, fmt) * dqa) @ (_f8(qb, 0) * dqb).t() + bias
+    for v in range(no._load().pdt_gemm_f8_num_variants()):
+        out = torch.empty(M, N, dtype=torch.bfloat16, device="cuda")
+        no.gemm_f8(qa, qb, out, dqa, dqb, fmt_a=fmt, bias=bias, variant=v)
+        torch.cuda.synchronize()
+        assert relerr(out, ref) < 1e-2, (v, relerr(out, ref))
+
+
+def test_linear_fp8_autograd():
+    torch.manual_seed(12)
+    fc = nn.Linear(768, 3072).cuda()
+    x = torch.randn(4, 197, 768, device="cuda").to(torch.bfloat16).requires_grad_(True)
+    y = no.linear(x, fc, act="gelu", fp8=True)
+    fcr = nn.Linear(768, 3072).cuda()
+    fcr.load_state_dict(fc.state_dict())
+    xr = x.detach().float().requires_grad_(True)
+    yr = F.gelu(fcr(xr), approximate="tanh")
+    assert nrmerr(y, yr) < 6e-2, nrmerr(y, yr)
+    g = torch.randn_like(yr).to(torch.bfloat16)
+    y.backward(g)
+    yr.backward(g.float())
+    assert nrmerr(x.grad, xr.grad) < 1e-1, nrmerr(x.grad, xr.grad)
+    assert nrmerr(fc.weight.grad, fcr.weight.grad) < 3e-2
+    assert nrmerr(fc.bias.grad, fcr.bias.grad) < 3e-2
+
+
+def test_vit_fp8_train_step():
+    from pytorch_distributed_template_amd.models import vit_b_16
+    from pytorch_distributed_template_amd.optim import FusedAdamW
+    torch.manual_seed(13)
+    m = vit_b_16(num_classes=10, fp8=True, depth=2).cuda()
+    opt = FusedAdamW(m.parameters(), lr=1e-3)
+    x = torch.randn(4, 3, 224, 224, device="cuda").to(torch.bfloat16)
+    t = torch.randint(0, 10, (4,), device="cuda")
+    losses = []
+    for _ in range(3):
+        opt.zero_grad(set_to_none=True)
+        loss = no.softmax_cross_entropy(m(x), t)
+        loss.backward()
+        opt.step()
+        losses.append(loss.item())
+    assert all(torch.isfinite(torch.tensor(losses)))
+    assert losses[-1] < losses[0]
