@@ -97,6 +97,8 @@ def global_avg_pool(x):
 
 
 def _torch_linear(x, fc: nn.Linear, act=None):
+    if x.dtype != fc.weight.dtype and not torch.is_autocast_enabled(x.device.type):
+        x = x.to(fc.weight.dtype)
     y = fc(x)
     if act == "gelu":
         y = F.gelu(y, approximate="tanh")

@@ -23,6 +23,15 @@ from torch.optim import Optimizer
 CHUNK = 65536
 
 
+def _bump_versions(params):
+    """The step kernel writes parameters through raw pointers, invisible to
+    autograd's version counters: bump them so caches keyed on ``_version``
+    (fp8 weight copies, saved-tensor checks) see the update."""
+    from torch.autograd.graph import increment_version
+    for p in params:
+        increment_version(p)
+
+
 class _Plan:
     """Device-side pointer/chunk tables for one param group."""
 
@@ -147,6 +156,7 @@ class FusedSGD(_FusedBase):
                 float(group["lr"]), float(group["momentum"]), float(group["dampening"]),
                 float(group["weight_decay"]), int(group["nesterov"]), int(first), 1.0, self._stream())
             native_ops._chk(rc, "sgd_step")
+            _bump_versions(params)
             if self.write_bf16_shadow:
                 for p, s in zip(params, shadows):
                     native_ops.register_shadow(p, s)
@@ -222,6 +232,7 @@ class FusedAdam(_FusedBase):
                 float(group["lr"]), float(b1), float(b2), float(group["eps"]), float(group["weight_decay"]),
                 int(self.decoupled), float(bc1), float(bc2), 1.0, self._stream())
             native_ops._chk(rc, "adam_step")
+            _bump_versions(params)
             if self.write_bf16_shadow:
                 for p, s in zip(params, shadows):
                     native_ops.register_shadow(p, s)

@@ -510,3 +510,17 @@ def test_vit_fp8_train_step():
         losses.append(loss.item())
     assert all(torch.isfinite(torch.tensor(losses)))
     assert losses[-1] < losses[0]
+
+
+def test_fused_optimizer_bumps_versions_and_fp8_cache():
+    """In-place native steps must invalidate weight caches keyed on _version."""
+    from pytorch_distributed_template_amd.optim import FusedAdamW, FusedSGD
+    for cls in (FusedSGD, FusedAdamW):
+        w = nn.Parameter(torch.randn(256, 384, device="cuda"))
+        opt = cls([w], lr=0.1)
+        q0 = no.fp8_weight(w)[0].clone()
+        v0 = w._version
+        w.grad = torch.randn_like(w)
+        opt.step()
+        assert w._version > v0
+        assert not torch.equal(no.fp8_weight(w)[0], q0)
