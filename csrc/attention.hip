@@ -201,18 +201,27 @@ struct AttnBwdParams {
   float scale;
 };
 
-// delta[bh][q] = sum_d dO[q][d] * O[q][d]
-__global__ void attn_delta_kernel(const u16* __restrict__ dout, const u16* __restrict__ out, float* __restrict__ delta,
-                                  int B, int T, int H, long ldo) {
-  const int lane = threadIdx.x & 63;
-  const long row = (long)blockIdx.x * 4 + (threadIdx.x >> 6);  // over B*T*H (b, t, h)
-  if (row >= (long)B * T * H) return;
-  const int h = row % H;
-  const long bt = row / H;
-  const long off = bt * ldo + h * D + lane;
-  float v = bf2f(dout[off]) * bf2f(out[off]);
-  v = warp_sum(v);
-  if (lane == 0) {
+// delta[bh][q] = sum_d dO[q][d] * O[q][d]; 8 lanes (16 B each) per (b, t, h) row
+__global__ void __launch_bounds__(256) attn_delta_kernel(const u16* __restrict__ dout, const u16* __restrict__ out,
+                                                         float* __restrict__ delta, int B, int T, int H, long ldo) {
+  const long row = ((long)blockIdx.x * 256 + threadIdx.x) >> 3;  // over B*T*H (b, t, h)
+  const int part = threadIdx.x & 7;
+  const bool ok = row < (long)B * T * H;
+  const long rr = ok ? row : 0;
+  const int h = rr % H;
+  const long bt = rr / H;
+  const long off = bt * ldo + h * D + part * 8;
+  float v = 0.f;
+  if (ok) {
+    const u32x4 a = *reinterpret_cast<const u32x4*>(dout + off);
+    const u32x4 b = *reinterpret_cast<const u32x4*>(out + off);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) v += lo_bf(a[e]) * lo_bf(b[e]) + hi_bf(a[e]) * hi_bf(b[e]);
+  }
+  v += __shfl_xor(v, 1, 64);
+  v += __shfl_xor(v, 2, 64);
+  v += __shfl_xor(v, 4, 64);
+  if (ok && part == 0) {
     const int b = bt / T, t = bt % T;
     delta[((long)b * H + h) * T + t] = v;
   }
@@ -226,6 +235,7 @@ __global__ void __launch_bounds__(256) attn_bwd_dkdv_kernel(AttnBwdParams p) {
   char* dOs = smem + TILE * D * 2;    // row image + tr image? -> two separate uses below
   __shared__ __attribute__((aligned(16))) char dOt[TILE * D * 2];
   __shared__ __attribute__((aligned(16))) char Qr[TILE * D * 2];
+  __shared__ float lse_s[TILE], dl_s[TILE];  // per-query softmax stats of the current q tile
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, g = lane >> 4;
   const int bh = blockIdx.y, b = bh / p.H, h = bh % p.H;
   const int kbase = blockIdx.x * TILE + wave * 16;
@@ -259,6 +269,11 @@ __global__ void __launch_bounds__(256) attn_bwd_dkdv_kernel(AttnBwdParams p) {
     stage_tile<true>(Qs, Qg, p.ld, q0, p.T, tid);      // transposed: B operand of dK
     stage_tile<false>(dOs, dOg, p.ldo, q0, p.T, tid);  // rows: A operand of dP
     stage_tile<true>(dOt, dOg, p.ldo, q0, p.T, tid);   // transposed: B operand of dV
+    if (tid < TILE) {
+      const int q = q0 + tid;
+      lse_s[tid] = q < p.T ? lse[q] : 0.f;
+      dl_s[tid] = q < p.T ? dl[q] : 0.f;
+    }
     __syncthreads();
     f32x4 s[4], dp[4];
 #pragma unroll
@@ -277,11 +292,11 @@ __global__ void __launch_bounds__(256) attn_bwd_dkdv_kernel(AttnBwdParams p) {
     for (int u = 0; u < 4; ++u)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const int q = q0 + 16 * u + 4 * g + r;
+        const int ql = 16 * u + 4 * g + r;
         float pr = 0.f, ds = 0.f;
-        if (q < p.T && key < p.T) {
-          pr = exp2f(s[u][r] * p.c - lse[q]);
-          ds = pr * (dp[u][r] - dl[q]);
+        if (q0 + ql < p.T && key < p.T) {
+          pr = exp2f(s[u][r] * p.c - lse_s[ql]);
+          ds = pr * (dp[u][r] - dl_s[ql]);
         }
         s[u][r] = pr;
         dp[u][r] = ds;
@@ -419,7 +434,7 @@ PDT_API int pdt_attn_fwd(const void* qkv, void* out, float* lse, int B, int T, i
 PDT_API int pdt_attn_bwd(const void* qkv, const void* out, const void* dout, const float* lse, float* delta,
                          void* dqkv, int B, int T, int H, float scale, hipStream_t st) {
   const long rows = (long)B * T * H;
-  hipLaunchKernelGGL(attn_delta_kernel, dim3((unsigned)((rows + 3) / 4)), dim3(256), 0, st, (const u16*)dout,
+  hipLaunchKernelGGL(attn_delta_kernel, dim3((unsigned)((rows * 8 + 255) / 256)), dim3(256), 0, st, (const u16*)dout,
                      (const u16*)out, delta, B, T, H, (long)H * D);
   int e = (int)hipGetLastError();
   if (e) return e;

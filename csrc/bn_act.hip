@@ -161,10 +161,13 @@ __global__ void __launch_bounds__(256) bn_finalize_kernel(const float* __restric
 }
 
 // -------------------------------------------------------------------- apply
-template <bool RES, bool RELU>
+// MASK: also write the ReLU mask as one bit per element (byte i = chunk i's 8
+// channels): the backward then reads 1/16 of the bytes instead of `out`.
+template <bool RES, bool RELU, bool MASK = false>
 __global__ void __launch_bounds__(NT) bn_apply_kernel(const u16* __restrict__ y, const u16* __restrict__ res,
                                                       u16* __restrict__ out, const float* __restrict__ scale,
-                                                      const float* __restrict__ shift, long n8, int C) {
+                                                      const float* __restrict__ shift, long n8, int C,
+                                                      uint8_t* __restrict__ mask) {
   const int cpr = C / 8;
   for (uint32_t i = blockIdx.x * NT + threadIdx.x; i < (uint32_t)n8; i += gridDim.x * NT) {
     const int ch = (int)(i % (uint32_t)cpr) * 8;
@@ -184,20 +187,32 @@ __global__ void __launch_bounds__(NT) bn_apply_kernel(const u16* __restrict__ y,
 #pragma unroll
       for (int k = 0; k < 8; ++k) f[k] = fmaxf(f[k], 0.f);
     }
-    reinterpret_cast<u32x4*>(out)[i] = pack8(f);
+    const u32x4 o = pack8(f);
+    reinterpret_cast<u32x4*>(out)[i] = o;
+    if (MASK) {
+      uint32_t m = 0;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {  // mask of the ROUNDED output (what backward's act > 0 saw)
+        m |= ((o[e] & 0x7fffu) != 0 && !(o[e] & 0x8000u)) ? (1u << (2 * e)) : 0u;
+        m |= ((o[e] & 0x7fff0000u) != 0 && !(o[e] & 0x80000000u)) ? (1u << (2 * e + 1)) : 0u;
+      }
+      mask[i] = (uint8_t)m;
+    }
   }
 }
 
 // -------------------------------------------------------------------- backward
 // relu mask: if `act` (saved output) is given, mask = act > 0; else if RELU,
 // mask = y*scale+shift > 0 (exact when there is no residual).
-template <bool RELU, bool USE_ACT>
+// USE_MASK: the ReLU mask comes from the forward's bit mask (takes precedence over USE_ACT)
+template <bool RELU, bool USE_ACT, bool USE_MASK = false>
 __global__ void __launch_bounds__(NT) bn_bwd_reduce_kernel(const u16* __restrict__ dA, const u16* __restrict__ y,
                                                            const u16* __restrict__ act,
                                                            const float* __restrict__ mean,
                                                            const float* __restrict__ scale,
                                                            const float* __restrict__ shift,
-                                                           float* __restrict__ part, long M, int C) {
+                                                           float* __restrict__ part, long M, int C,
+                                                           const uint8_t* __restrict__ mask) {
   __shared__ float red[2][NT][8];
   const int cpr = C / 8;
   const int rp = NT / cpr;
@@ -207,7 +222,7 @@ __global__ void __launch_bounds__(NT) bn_bwd_reduce_kernel(const u16* __restrict
   if (rr < rp) {
     float mu[8], sc[8], sh[8];
     load8f(mean + ch * 8, mu);
-    if (RELU && !USE_ACT) {
+    if (RELU && !USE_ACT && !USE_MASK) {
       load8f(scale + ch * 8, sc);
       load8f(shift + ch * 8, sh);
     }
@@ -217,7 +232,11 @@ __global__ void __launch_bounds__(NT) bn_bwd_reduce_kernel(const u16* __restrict
       unpack8(*reinterpret_cast<const u32x4*>(dA + off), g);
       unpack8(*reinterpret_cast<const u32x4*>(y + off), yv);
       if (RELU) {
-        if (USE_ACT) {
+        if (USE_MASK) {
+          const uint32_t m = mask[off >> 3];
+#pragma unroll
+          for (int k = 0; k < 8; ++k) g[k] = (m >> k) & 1u ? g[k] : 0.f;
+        } else if (USE_ACT) {
           float a[8];
           unpack8(*reinterpret_cast<const u32x4*>(act + off), a);
 #pragma unroll
@@ -284,14 +303,15 @@ __global__ void __launch_bounds__(256) bn_bwd_finalize_kernel(const float* __res
   k3[c] = (float)a3;
 }
 
-template <bool RELU, bool USE_ACT, bool DRES>
+template <bool RELU, bool USE_ACT, bool DRES, bool USE_MASK = false>
 __global__ void __launch_bounds__(NT) bn_bwd_apply_kernel(const u16* __restrict__ dA, const u16* __restrict__ y,
                                                           const u16* __restrict__ act,
                                                           const float* __restrict__ scale,
                                                           const float* __restrict__ shift,
                                                           const float* __restrict__ k1, const float* __restrict__ k2,
                                                           const float* __restrict__ k3, u16* __restrict__ dy,
-                                                          u16* __restrict__ dres, long n8, int C) {
+                                                          u16* __restrict__ dres, long n8, int C,
+                                                          const uint8_t* __restrict__ mask) {
   const int cpr = C / 8;
   for (uint32_t i = blockIdx.x * NT + threadIdx.x; i < (uint32_t)n8; i += gridDim.x * NT) {
     const int ch = (int)(i % (uint32_t)cpr) * 8;
@@ -299,7 +319,11 @@ __global__ void __launch_bounds__(NT) bn_bwd_apply_kernel(const u16* __restrict_
     unpack8(reinterpret_cast<const u32x4*>(dA)[i], g);
     unpack8(reinterpret_cast<const u32x4*>(y)[i], yv);
     if (RELU) {
-      if (USE_ACT) {
+      if (USE_MASK) {
+        const uint32_t m = mask[i];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) g[k] = (m >> k) & 1u ? g[k] : 0.f;
+      } else if (USE_ACT) {
         float a[8];
         unpack8(reinterpret_cast<const u32x4*>(act)[i], a);
 #pragma unroll
@@ -373,36 +397,45 @@ PDT_API int pdt_bn_finalize(const float* part, int R, int C, double count, float
   PDT_RETURN_LAUNCH();
 }
 
+// mask (optional, relu only): [M*C/8] bytes, bit k of byte i = (out[8i+k] > 0)
 PDT_API int pdt_bn_apply(const void* y, const void* res, void* out, const float* scale, const float* shift, long M,
-                         int C, int relu, hipStream_t st) {
+                         int C, int relu, void* mask, hipStream_t st) {
   if (C % 8) return -1;
+  if (mask && !relu) return -2;
   long n8 = M * C / 8;
   dim3 g(grid_for(n8)), b(NT);
   const u16* Y = (const u16*)y;
   const u16* R = (const u16*)res;
   u16* O = (u16*)out;
+  uint8_t* MK = (uint8_t*)mask;
+#define APPLY(R_, U_, M_) \
+  hipLaunchKernelGGL((bn_apply_kernel<R_, U_, M_>), g, b, 0, st, Y, R, O, scale, shift, n8, C, MK)
   if (res) {
-    if (relu) hipLaunchKernelGGL((bn_apply_kernel<true, true>), g, b, 0, st, Y, R, O, scale, shift, n8, C);
-    else hipLaunchKernelGGL((bn_apply_kernel<true, false>), g, b, 0, st, Y, R, O, scale, shift, n8, C);
+    if (relu) { if (mask) APPLY(true, true, true); else APPLY(true, true, false); }
+    else APPLY(true, false, false);
   } else {
-    if (relu) hipLaunchKernelGGL((bn_apply_kernel<false, true>), g, b, 0, st, Y, R, O, scale, shift, n8, C);
-    else hipLaunchKernelGGL((bn_apply_kernel<false, false>), g, b, 0, st, Y, R, O, scale, shift, n8, C);
+    if (relu) { if (mask) APPLY(false, true, true); else APPLY(false, true, false); }
+    else APPLY(false, false, false);
   }
+#undef APPLY
   PDT_RETURN_LAUNCH();
 }
 
+// ReLU mask source (relu != 0): bit mask if given, else act > 0 if given, else recomputed from y
 PDT_API int pdt_bn_bwd_reduce(const void* dA, const void* y, const void* act, const float* mean,
                               const float* scale, const float* shift, float* part, long M, int C, int relu,
-                              int blocks, hipStream_t st) {
+                              int blocks, const void* mask, hipStream_t st) {
   if (C % 8 || C / 8 > NT) return -1;
   const u16 *G = (const u16*)dA, *Y = (const u16*)y, *A = (const u16*)act;
+  const uint8_t* MK = (const uint8_t*)mask;
   dim3 g(blocks), b(NT);
-  if (!relu)
-    hipLaunchKernelGGL((bn_bwd_reduce_kernel<false, false>), g, b, 0, st, G, Y, A, mean, scale, shift, part, M, C);
-  else if (act)
-    hipLaunchKernelGGL((bn_bwd_reduce_kernel<true, true>), g, b, 0, st, G, Y, A, mean, scale, shift, part, M, C);
-  else
-    hipLaunchKernelGGL((bn_bwd_reduce_kernel<true, false>), g, b, 0, st, G, Y, A, mean, scale, shift, part, M, C);
+#define RED(R_, U_, M_) \
+  hipLaunchKernelGGL((bn_bwd_reduce_kernel<R_, U_, M_>), g, b, 0, st, G, Y, A, mean, scale, shift, part, M, C, MK)
+  if (!relu) RED(false, false, false);
+  else if (mask) RED(true, false, true);
+  else if (act) RED(true, true, false);
+  else RED(true, false, false);
+#undef RED
   PDT_RETURN_LAUNCH();
 }
 
@@ -417,21 +450,29 @@ PDT_API int pdt_bn_bwd_finalize(const float* part, int R, int C, double count, c
 
 PDT_API int pdt_bn_bwd_apply(const void* dA, const void* y, const void* act, const float* scale,
                              const float* shift, const float* k1, const float* k2, const float* k3, void* dy,
-                             void* dres, long M, int C, int relu, hipStream_t st) {
+                             void* dres, long M, int C, int relu, const void* mask, hipStream_t st) {
   if (C % 8) return -1;
   long n8 = M * C / 8;
   dim3 g(grid_for(n8)), b(NT);
   const u16 *G = (const u16*)dA, *Y = (const u16*)y, *A = (const u16*)act;
   u16 *DY = (u16*)dy, *DR = (u16*)dres;
+  const uint8_t* MK = (const uint8_t*)mask;
 #define BWD_APPLY(R_, U_, D_) \
-  hipLaunchKernelGGL((bn_bwd_apply_kernel<R_, U_, D_>), g, b, 0, st, G, Y, A, scale, shift, k1, k2, k3, DY, DR, n8, C)
+  hipLaunchKernelGGL((bn_bwd_apply_kernel<R_, U_, D_>), g, b, 0, st, G, Y, A, scale, shift, k1, k2, k3, DY, DR, n8, C, \
+                     MK)
+#define BWD_APPLY_M(D_) \
+  hipLaunchKernelGGL((bn_bwd_apply_kernel<true, false, D_, true>), g, b, 0, st, G, Y, A, scale, shift, k1, k2, k3, DY, \
+                     DR, n8, C, MK)
   if (!relu) {
     if (dres) BWD_APPLY(false, false, true); else BWD_APPLY(false, false, false);
+  } else if (mask) {
+    if (dres) BWD_APPLY_M(true); else BWD_APPLY_M(false);
   } else if (act) {
     if (dres) BWD_APPLY(true, true, true); else BWD_APPLY(true, true, false);
   } else {
     if (dres) BWD_APPLY(true, false, true); else BWD_APPLY(true, false, false);
   }
 #undef BWD_APPLY
+#undef BWD_APPLY_M
   PDT_RETURN_LAUNCH();
 }

@@ -48,6 +48,7 @@ struct NTParams {
   int nstat_rows;
   int nt_store;        // 1: non-temporal (streaming) output stores
   int ident_out;       // 1: output row == m (no stride-phase remap) -> skip the index math
+  const uint8_t* addend_mask;  // optional: addend is masked by this ReLU bit mask (1 bit / element)
   const float* dq_a;   // fp8 only: dequant scale of the A (src) operand (device scalar)
   const float* dq_b;   // fp8 only: dequant scale of the B operand
   FastDiv div_Wm, div_HWm, div_Cs8, div_ntw;
@@ -416,6 +417,12 @@ __global__ void __launch_bounds__(NTH, 2) conv_nt_kernel(NTParams p) {
         float v0 = acc[i][j][0], v1 = acc[i][j][1], v2 = acc[i][j][2], v3 = acc[i][j][3];
         if (addend != nullptr) {
           uint2 a = *reinterpret_cast<const uint2*>(addend + orow * p.ldo + col);
+          if (p.addend_mask != nullptr) {
+            const size_t e = orow * p.ldo + col;
+            const uint32_t mb = p.addend_mask[e >> 3] >> (e & 7);
+            a.x &= ((mb & 1u) ? 0xffffu : 0u) | ((mb & 2u) ? 0xffff0000u : 0u);
+            a.y &= ((mb & 4u) ? 0xffffu : 0u) | ((mb & 8u) ? 0xffff0000u : 0u);
+          }
           v0 += lo_bf(a.x); v1 += hi_bf(a.x); v2 += lo_bf(a.y); v3 += hi_bf(a.y);
         }
         uint2 w;
@@ -466,6 +473,12 @@ __global__ void __launch_bounds__(NTH, 2) conv_nt_kernel(NTParams p) {
         }
         if (addend != nullptr) {
           u32x4 a = *reinterpret_cast<const u32x4*>(addend + orow * p.ldo + col);
+          if (p.addend_mask != nullptr) {
+            const uint32_t mb = p.addend_mask[(orow * p.ldo + col) >> 3];
+#pragma unroll
+            for (int e = 0; e < 4; ++e)
+              a[e] &= ((mb >> (2 * e)) & 1u ? 0xffffu : 0u) | ((mb >> (2 * e + 1)) & 1u ? 0xffff0000u : 0u);
+          }
 #pragma unroll
           for (int e = 0; e < 4; ++e) v[e] = pack2bf(lo_bf(v[e]) + lo_bf(a[e]), hi_bf(v[e]) + hi_bf(a[e]));
         }
@@ -591,7 +604,7 @@ PDT_API int pdt_conv_nt_stat_rows(int M, int Ncol, int K, int variant) {
 
 // Generic launch: see header comment for the meaning of every argument.
 PDT_API int pdt_conv_nt(const void* src, const void* b, void* out, float* stats, const float* bias,
-                        const void* addend,
+                        const void* addend, const void* addend_mask,
                         int Hs, int Ws, int Cs, int Nimg, int Hm, int Wm, int Ncol, int K, int ldb,
                         int sh, int sw, int oh0, int ow0, int dh, int dw, int nth, int ntw,
                         int Ho, int Wo, int osh, int osw, int oph, int opw, int ldo, int act,
@@ -605,6 +618,8 @@ PDT_API int pdt_conv_nt(const void* src, const void* b, void* out, float* stats,
   p.stats = stats;
   p.bias = bias;
   p.addend = (const u16*)addend;
+  p.addend_mask = (const uint8_t*)addend_mask;
+  if (addend_mask && (!addend || ldo != Ncol)) return -4;  // mask indexes the dense [M][Ncol] addend
   p.Hs = Hs; p.Ws = Ws; p.Cs = Cs;
   p.Hm = Hm; p.Wm = Wm;
   p.M = Nimg * Hm * Wm;
@@ -672,6 +687,7 @@ PDT_API int pdt_gemm_f8(const void* a, const void* b, void* out, const float* bi
   p.stats = nullptr;
   p.bias = bias;
   p.addend = nullptr;
+  p.addend_mask = nullptr;
   p.Hs = 1; p.Ws = 1; p.Cs = K / 2;
   p.Hm = 1; p.Wm = 1;
   p.M = M;

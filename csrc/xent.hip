@@ -102,6 +102,40 @@ __global__ void __launch_bounds__(256) colsum1_kernel(const u16* __restrict__ x,
   if (rg == 0 && c < C) part[(long)blockIdx.y * C + c] = red[0][cl] + red[1][cl] + red[2][cl] + red[3][cl];
 }
 
+// vectorised stage 1 for C % 8 == 0: thread = one 16-B chunk (8 columns) of a
+// row; a block covers rp rows per pass of up to 256 chunks (blockIdx.y picks
+// the chunk range) and strides over rows; rows combine in LDS -> part[g][C]
+__global__ void __launch_bounds__(256) colsum1v_kernel(const u16* __restrict__ x, float* __restrict__ part, int R,
+                                                       int C, int cpb) {
+  __shared__ float red[256][9];
+  const int t = threadIdx.x;
+  const int cpr = C / 8;
+  const int rp = 256 / cpb;
+  const int ch = blockIdx.y * cpb + t % cpb, rr = t / cpb;
+  float s[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  if (rr < rp && ch < cpr) {
+    for (long r = (long)blockIdx.x * rp + rr; r < R; r += (long)gridDim.x * rp) {
+      const u32x4 v = *reinterpret_cast<const u32x4*>(x + r * C + ch * 8);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        s[2 * e] += lo_bf(v[e]);
+        s[2 * e + 1] += hi_bf(v[e]);
+      }
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < 8; ++k) red[t][k] = s[k];
+  __syncthreads();
+  if (t < cpb && blockIdx.y * cpb + t < cpr) {
+    float a[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    for (int j = 0; j < rp; ++j)
+#pragma unroll
+      for (int k = 0; k < 8; ++k) a[k] += red[j * cpb + t][k];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) part[(long)blockIdx.x * C + (blockIdx.y * cpb + t) * 8 + k] = a[k];
+  }
+}
+
 __global__ void colsum2_kernel(const float* __restrict__ part, float* __restrict__ out, int G, int C, int acc) {
   int c = blockIdx.x * blockDim.x + threadIdx.x;
   if (c >= C) return;
@@ -147,7 +181,14 @@ PDT_API int pdt_colsum(const void* x, float* out, float* work, int R, int C, int
   if (G > 128) G = 128;
   if (G < 1) G = 1;
   int rpb = (R + G - 1) / G;
-  hipLaunchKernelGGL(colsum1_kernel, dim3((C + 63) / 64, G), dim3(256), 0, st, (const u16*)x, work, R, C, rpb);
+  if (C % 8 == 0) {
+    const int cpr = C / 8;
+    const int cpb = cpr < 256 ? cpr : 256;
+    hipLaunchKernelGGL(colsum1v_kernel, dim3(G, (cpr + cpb - 1) / cpb), dim3(256), 0, st, (const u16*)x, work, R, C,
+                       cpb);
+  } else {
+    hipLaunchKernelGGL(colsum1_kernel, dim3((C + 63) / 64, G), dim3(256), 0, st, (const u16*)x, work, R, C, rpb);
+  }
   hipLaunchKernelGGL(colsum2_kernel, dim3((C + 255) / 256), dim3(256), 0, st, work, out, G, C, acc);
   PDT_RETURN_LAUNCH();
 }

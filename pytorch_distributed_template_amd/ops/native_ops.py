@@ -31,7 +31,7 @@ _SIGS = {
     "pdt_conv_nt_stat_rows": (c_int, [c_int, c_int, c_int, c_int]),
     "pdt_conv_nt_num_variants": (c_int, []),
     "pdt_conv_nt_resolve_variant": (c_int, [c_int, c_int, c_int, c_int]),
-    "pdt_conv_nt": (c_int, [P, P, P, P, P, P] + [c_int] * 25 + [P, c_int, P]),
+    "pdt_conv_nt": (c_int, [P, P, P, P, P, P, P] + [c_int] * 25 + [P, c_int, P]),
     "pdt_ln_fwd": (c_int, [P, P, P, P, P, P, c_int, c_int, c_float, P]),
     "pdt_ln_bwd_blocks": (c_int, [c_int]),
     "pdt_ln_bwd": (c_int, [P] * 9 + [c_int, c_int, c_int, P]),
@@ -44,10 +44,10 @@ _SIGS = {
     "pdt_rows_reduce_workspace": (c_long, [c_int, c_int]),
     "pdt_bn_stats": (c_int, [P, P, c_long, c_int, c_int, P]),
     "pdt_bn_finalize": (c_int, [P, c_int, c_int, c_double, c_float, c_float] + [P] * 9 + [P]),
-    "pdt_bn_apply": (c_int, [P, P, P, P, P, c_long, c_int, c_int, P]),
-    "pdt_bn_bwd_reduce": (c_int, [P, P, P, P, P, P, P, c_long, c_int, c_int, c_int, P]),
+    "pdt_bn_apply": (c_int, [P, P, P, P, P, c_long, c_int, c_int, P, P]),
+    "pdt_bn_bwd_reduce": (c_int, [P, P, P, P, P, P, P, c_long, c_int, c_int, c_int, P, P]),
     "pdt_bn_bwd_finalize": (c_int, [P, c_int, c_int, c_double] + [P] * 8 + [c_int, P]),
-    "pdt_bn_bwd_apply": (c_int, [P] * 10 + [c_long, c_int, c_int, P]),
+    "pdt_bn_bwd_apply": (c_int, [P] * 10 + [c_long, c_int, c_int, P, P]),
     "pdt_maxpool_fwd": (c_int, [P, P, P] + [c_int] * 9 + [P]),
     "pdt_maxpool_bwd": (c_int, [P, P, P] + [c_int] * 9 + [P]),
     "pdt_avgpool_fwd": (c_int, [P, P, c_int, c_int, c_int, P]),
@@ -252,8 +252,8 @@ def _variant_filter():
     return out
 
 
-def _nt_args(src, b, out, stats, bias, a, act, variant, addend=None, aux=None):
-    return (_p(src), _p(b), _p(out), _p(stats), _p(bias), _p(addend), a["Hs"], a["Ws"], a["Cs"], a["Nimg"], a["Hm"], a["Wm"],
+def _nt_args(src, b, out, stats, bias, a, act, variant, addend=None, aux=None, addend_mask=None):
+    return (_p(src), _p(b), _p(out), _p(stats), _p(bias), _p(addend), _p(addend_mask), a["Hs"], a["Ws"], a["Cs"], a["Nimg"], a["Hm"], a["Wm"],
             a["Ncol"], a["K"], a["ldb"], a["sh"], a["sw"], a["oh0"], a["ow0"], a["dh"], a["dw"], a["nth"], a["ntw"],
             a["Ho"], a["Wo"], a["osh"], a["osw"], a["oph"], a["opw"], a["ldo"], int(act), _p(aux), int(variant), _s())
 
@@ -298,7 +298,7 @@ ACT = {None: 0, "none": 0, "relu": 1, "gelu": 2}
 
 
 def conv_nt(src, b, out, *, stats=None, bias=None, relu=False, act=None, variant=None, addend=None, aux=None,
-            **a):
+            addend_mask=None, **a):
     """C[m, n] = sum_k A[m, k] B[n, k] (+ addend) with the implicit-GEMM gather (see csrc/conv_igemm.hip)."""
     _check_nt(src, b, out, a)
     if addend is not None:
@@ -309,7 +309,11 @@ def conv_nt(src, b, out, *, stats=None, bias=None, relu=False, act=None, variant
         assert aux.dtype == torch.bfloat16 and aux.numel() == out.numel()
     if variant is None:
         variant = select_nt_variant(src, b, out, with_stats=stats is not None, bias=bias, act=act_id, **a)
-    _chk(_load().pdt_conv_nt(*_nt_args(src, b, out, stats, bias, a, act_id, variant, addend, aux)), "conv_nt")
+    if addend_mask is not None:
+        assert addend is not None and addend_mask.dtype == torch.uint8 and addend_mask.numel() * 8 == addend.numel()
+        assert a["ldo"] == a["Ncol"]
+    _chk(_load().pdt_conv_nt(*_nt_args(src, b, out, stats, bias, a, act_id, variant, addend, aux, addend_mask)),
+         "conv_nt")
 
 
 def conv_stat_rows(M, Ncol, K, variant):
@@ -436,7 +440,7 @@ def _conv_forward(x, wb, N, H, W, Cs, Cout, g, with_stats=False):
     return y, M, part, R
 
 
-def _conv_dgrad(dy, w32, N, H, W, Cin, Cout, g, addend=None):
+def _conv_dgrad(dy, w32, N, H, W, Cin, Cout, g, addend=None, addend_mask=None):
     """dX [N,Cin,H,W] (+ addend) from dY [N,Cout,Ho,Wo] (stride phases, see csrc/conv_igemm.hip)."""
     KH, KW, s_h, s_w, ph, pw = g["KH"], g["KW"], g["sh"], g["sw"], g["ph"], g["pw"]
     assert w32.shape[0] == Cout and w32.shape[1] == Cin, (tuple(w32.shape), Cout, Cin)
@@ -460,7 +464,7 @@ def _conv_dgrad(dy, w32, N, H, W, Cin, Cout, g, addend=None):
                                       nth, ntw, _s()), "wt_dgrad")
             conv_nt(dy, wt, dx, Hs=g["Ho"], Ws=g["Wo"], Cs=Cout, Nimg=N, Hm=H // s_h, Wm=W // s_w, Ncol=Cin,
                     K=K, ldb=max(K, 8), sh=1, sw=1, oh0=oh0, ow0=ow0, dh=-1, dw=-1, nth=nth, ntw=max(ntw, 0),
-                    Ho=H, Wo=W, osh=s_h, osw=s_w, oph=qh, opw=qw, ldo=Cin, addend=addend)
+                    Ho=H, Wo=W, osh=s_h, osw=s_w, oph=qh, opw=qw, ldo=Cin, addend=addend, addend_mask=addend_mask)
     return dx
 
 
@@ -497,8 +501,8 @@ class _BNArgs:
 
 class _Unit:
     """Saved state of one conv->BN->act unit between forward and backward."""
-    __slots__ = ("x", "w", "gamma", "y", "act", "mean", "invstd", "scale", "shift", "N", "C", "Cs", "H", "W",
-                 "Cout", "g", "relu", "has_res")
+    __slots__ = ("x", "w", "gamma", "y", "act", "mask", "mean", "invstd", "scale", "shift", "N", "C", "Cs", "H",
+                 "W", "Cout", "g", "relu", "has_res")
 
 
 def _unit_fwd(x, w, gamma, beta, residual, conv, relu, bna: _BNArgs):
@@ -534,17 +538,25 @@ def _unit_fwd(x, w, gamma, beta, residual, conv, relu, bna: _BNArgs):
         res = _cl(residual)
         assert res.dtype == torch.bfloat16 and res.shape == y.shape, (res.shape, y.shape)
     out = torch.empty_like(y, memory_format=torch.channels_last)
-    _chk(lib.pdt_bn_apply(_p(y), _p(res), _p(out), _p(scale), _p(shift), M, Cout, int(relu), st), "bn_apply")
+    # residual + ReLU: the backward's ReLU mask cannot be recomputed from y alone; keep it
+    # as one bit per element instead of re-reading the bf16 output (1/16 of the bytes)
+    mask = torch.empty(M * Cout // 8, dtype=torch.uint8, device=x.device) if (relu and residual is not None) \
+        else None
+    _chk(lib.pdt_bn_apply(_p(y), _p(res), _p(out), _p(scale), _p(shift), M, Cout, int(relu), _p(mask), st),
+         "bn_apply")
     u = _Unit()
     u.x, u.w, u.gamma, u.y = x, w, gamma, y
-    u.act = out if (relu and residual is not None) else None
+    u.act = None
+    u.mask = mask
     u.mean, u.invstd, u.scale, u.shift = mean, invstd, scale, shift
     u.N, u.C, u.Cs, u.H, u.W, u.Cout, u.g, u.relu, u.has_res = N, C, Cs, H, W, Cout, g, relu, residual is not None
     return out, u
 
 
-def _bn_bwd(dA, u: _Unit, want_dres: bool):
-    """BN(+res)(+ReLU) backward: returns (dy, dres, dgamma, dbeta)."""
+def _bn_bwd(dA, u: _Unit, want_dres: bool, mask=None):
+    """BN(+res)(+ReLU) backward: returns (dy, dres, dgamma, dbeta). ``mask`` (a ReLU bit
+    mask of another unit's output) gates dA first -- the downsample branch of a bottleneck
+    sees the block's ReLU exactly as the main branch does."""
     lib = _load()
     st = _s()
     dA = _cl(dA.to(torch.bfloat16))
@@ -553,8 +565,11 @@ def _bn_bwd(dA, u: _Unit, want_dres: bool):
     f32 = dict(dtype=torch.float32, device=dA.device)
     blocks = lib.pdt_bn_stats_blocks(M, Cout)
     part = torch.empty(2 * blocks * Cout + lib.pdt_rows_reduce_workspace(blocks, Cout), **f32)
+    if mask is None:
+        mask = u.mask
+    relu = u.relu or mask is not None
     _chk(lib.pdt_bn_bwd_reduce(_p(dA), _p(u.y), _p(u.act), _p(u.mean), _p(u.scale), _p(u.shift), _p(part), M,
-                               Cout, int(u.relu), blocks, st), "bn_bwd_reduce")
+                               Cout, int(relu), blocks, _p(mask), st), "bn_bwd_reduce")
     vec = torch.empty((5, Cout), **f32)
     dgamma, dbeta, k1, k2, k3 = vec[0], vec[1], vec[2], vec[3], vec[4]
     _chk(lib.pdt_bn_bwd_finalize(_p(part), blocks, Cout, float(M), _p(u.gamma), _p(u.mean), _p(u.invstd),
@@ -562,16 +577,16 @@ def _bn_bwd(dA, u: _Unit, want_dres: bool):
     dy = torch.empty_like(u.y, memory_format=torch.channels_last)
     dres = torch.empty_like(u.y, memory_format=torch.channels_last) if want_dres else None
     _chk(lib.pdt_bn_bwd_apply(_p(dA), _p(u.y), _p(u.act), _p(u.scale), _p(u.shift), _p(k1), _p(k2), _p(k3),
-                              _p(dy), _p(dres), M, Cout, int(u.relu), st), "bn_bwd_apply")
+                              _p(dy), _p(dres), M, Cout, int(relu), _p(mask), st), "bn_bwd_apply")
     return dy, dres, dgamma, dbeta
 
 
-def _unit_dx(dy, u: _Unit, addend=None):
+def _unit_dx(dy, u: _Unit, addend=None, addend_mask=None):
     wd = u.w
     if u.Cs != u.C:  # stem: dgrad against the channel-padded weight, then drop the pad
         wd = torch.nn.functional.pad(u.w.detach().float(), (0, 0, 0, 0, 0, u.Cs - u.C))
         assert addend is None
-    dx = _conv_dgrad(dy, wd, u.N, u.H, u.W, u.Cs, u.Cout, u.g, addend=addend)
+    dx = _conv_dgrad(dy, wd, u.N, u.H, u.W, u.Cs, u.Cout, u.g, addend=addend, addend_mask=addend_mask)
     return dx[:, :u.C] if u.Cs != u.C else dx
 
 
@@ -594,7 +609,7 @@ class _ConvBNAct(torch.autograd.Function):
     def forward(ctx, x, w, gamma, beta, residual, conv, relu, bna):
         out, u = _unit_fwd(x, w, gamma, beta, residual, conv, relu, bna)
         ctx.u = u
-        ctx.save_for_backward(u.x, u.y, u.act)  # version-checked activations
+        ctx.save_for_backward(u.x, u.y, u.mask)  # version-checked activations
         return out
 
     @staticmethod
@@ -637,14 +652,15 @@ class _Bottleneck(torch.autograd.Function):
                             _BNArgs(blk.bn3))
         ctx.units = (u1, u2, u3, ud)
         ctx.has_ds = has_ds
-        ctx.save_for_backward(u1.x, u1.y, u2.y, u3.y, u3.act)
+        ctx.save_for_backward(u1.x, u1.y, u2.y, u3.y, u3.mask)
         return out
 
     @staticmethod
     def backward(ctx, dout):
         u1, u2, u3, ud = ctx.units
         need = ctx.needs_input_grad
-        dy3, dres, dg3, db3 = _bn_bwd(dout, u3, True)
+        dout = _cl(dout.to(torch.bfloat16))
+        dy3, _, dg3, db3 = _bn_bwd(dout, u3, False)
         da2 = _unit_dx(dy3, u3)
         dw3 = _unit_dw(dy3, u3)
         dy2, _, dg2, db2 = _bn_bwd(da2, u2, False)
@@ -652,14 +668,18 @@ class _Bottleneck(torch.autograd.Function):
         dw2 = _unit_dw(dy2, u2)
         dy1, _, dg1, db1 = _bn_bwd(da1, u1, False)
         grads_ds = ()
+        # shortcut gradient = dout * relu_mask(out): never materialised -- the downsample
+        # BN backward gates dout with the mask itself, and an identity shortcut is added
+        # (masked) by the epilogue of the block-input dgrad GEMM
+        addend_mask = None
         if ctx.has_ds:
-            dyd, _, dgd, dbd = _bn_bwd(dres, ud, False)
+            dyd, _, dgd, dbd = _bn_bwd(dout, ud, False, mask=u3.mask)
             addend = _unit_dx(dyd, ud) if need[0] else None
             dwd = _unit_dw(dyd, ud)
             grads_ds = (dwd, dgd, dbd)
         else:
-            addend = dres
-        dx = _unit_dx(dy1, u1, addend=addend) if need[0] else None
+            addend, addend_mask = dout, u3.mask
+        dx = _unit_dx(dy1, u1, addend=addend, addend_mask=addend_mask) if need[0] else None
         dw1 = _unit_dw(dy1, u1)
         del ctx.units
         return (dx, None, None, dw1, dg1, db1, dw2, dg2, db2, dw3, dg3, db3) + grads_ds
