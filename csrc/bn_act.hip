@@ -15,6 +15,7 @@
 // read as 2x f32x4. Partial sums are [2][R][C] fp32 (R partial rows) and are
 // combined in fp64 by the finalize kernels (deterministic, no atomics).
 #include "pdt_common.h"
+#include <stdlib.h>
 
 namespace {
 
@@ -359,8 +360,14 @@ PDT_API int pdt_bn_stats_blocks(long M, int C) {
   int cpr = C / 8;
   int rp = NT / cpr;
   long b = (M + rp - 1) / rp;
-  // ~2 blocks per CU, each streaming many rows
-  if (b > 512) b = 512;
+  // several blocks per CU, each streaming many rows (PDT_BN_BLOCKS overrides the cap)
+  static int cap = -1;
+  if (cap < 0) {
+    const char* e = getenv("PDT_BN_BLOCKS");
+    cap = e ? atoi(e) : 1024;
+    if (cap < 1) cap = 1024;
+  }
+  if (b > cap) b = cap;
   if (b < 1) b = 1;
   return (int)b;
 }

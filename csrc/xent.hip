@@ -136,12 +136,21 @@ __global__ void __launch_bounds__(256) colsum1v_kernel(const u16* __restrict__ x
   }
 }
 
-__global__ void colsum2_kernel(const float* __restrict__ part, float* __restrict__ out, int G, int C, int acc) {
-  int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= C) return;
+// stage 2: 256 threads = 64 columns x 4 row groups (fixed order -> deterministic)
+__global__ void __launch_bounds__(256) colsum2_kernel(const float* __restrict__ part, float* __restrict__ out, int G,
+                                                      int C, int acc) {
+  __shared__ float red[4][64];
+  const int cl = threadIdx.x & 63, rg = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + cl;
   float s = 0.f;
-  for (int g = 0; g < G; ++g) s += part[(long)g * C + c];
-  out[c] = acc ? out[c] + s : s;
+  if (c < C)
+    for (int g = rg; g < G; g += 4) s += part[(long)g * C + c];
+  red[rg][cl] = s;
+  __syncthreads();
+  if (rg == 0 && c < C) {
+    const float t = (red[0][cl] + red[1][cl]) + (red[2][cl] + red[3][cl]);
+    out[c] = acc ? out[c] + t : t;
+  }
 }
 
 }  // namespace
@@ -169,17 +178,19 @@ PDT_API int pdt_xent_bwd(const void* logits, int bf16, const long* target, const
 }
 
 // workspace floats pdt_colsum needs
-PDT_API long pdt_colsum_workspace(int R, int C) {
-  int G = (R + 255) / 256;
-  if (G > 128) G = 128;
+// row groups of stage 1: enough blocks to fill 256 CUs several times over
+static int colsum_groups(int R, int C) {
+  int G = (R + 31) / 32;
+  const int cap = C % 8 == 0 ? 512 : 128;
+  if (G > cap) G = cap;
   if (G < 1) G = 1;
-  return (long)G * C;
+  return G;
 }
 
+PDT_API long pdt_colsum_workspace(int R, int C) { return (long)colsum_groups(R, C) * C; }
+
 PDT_API int pdt_colsum(const void* x, float* out, float* work, int R, int C, int acc, hipStream_t st) {
-  int G = (R + 255) / 256;
-  if (G > 128) G = 128;
-  if (G < 1) G = 1;
+  const int G = colsum_groups(R, C);
   int rpb = (R + G - 1) / G;
   if (C % 8 == 0) {
     const int cpr = C / 8;
@@ -189,6 +200,6 @@ PDT_API int pdt_colsum(const void* x, float* out, float* work, int R, int C, int
   } else {
     hipLaunchKernelGGL(colsum1_kernel, dim3((C + 63) / 64, G), dim3(256), 0, st, (const u16*)x, work, R, C, rpb);
   }
-  hipLaunchKernelGGL(colsum2_kernel, dim3((C + 255) / 256), dim3(256), 0, st, work, out, G, C, acc);
+  hipLaunchKernelGGL(colsum2_kernel, dim3((C + 63) / 64), dim3(256), 0, st, work, out, G, C, acc);
   PDT_RETURN_LAUNCH();
 }
