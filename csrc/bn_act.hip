@@ -364,8 +364,8 @@ PDT_API int pdt_bn_stats_blocks(long M, int C) {
   static int cap = -1;
   if (cap < 0) {
     const char* e = getenv("PDT_BN_BLOCKS");
-    cap = e ? atoi(e) : 1024;
-    if (cap < 1) cap = 1024;
+    cap = e ? atoi(e) : 512;
+    if (cap < 1) cap = 512;
   }
   if (b > cap) b = cap;
   if (b < 1) b = 1;

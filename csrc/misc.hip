@@ -53,6 +53,39 @@ __global__ void wt_dgrad_kernel(const float* __restrict__ w, u16* __restrict__ o
   }
 }
 
+// Many wt_dgrad jobs in one launch (all conv weights of a model after an
+// optimizer step): job j covers elements [start_j, start_{j+1}) of the flat
+// index space; a thread finds its job by binary search over the starts.
+struct WtJob {
+  const float* w;
+  u16* out;
+  long start;
+  int Cout, KH, KW, Cin, kh0, kw0, s, nth, ntw, pad;
+};
+
+__global__ void wt_dgrad_multi_kernel(const WtJob* __restrict__ jobs, int njobs, long total) {
+  __shared__ long starts[512];  // job starts staged once per block (njobs <= 512 checked on the host)
+  for (int i = threadIdx.x; i < njobs; i += NT) starts[i] = jobs[i].start;
+  __syncthreads();
+  for (long t = (long)blockIdx.x * NT + threadIdx.x; t < total; t += (long)gridDim.x * NT) {
+    int lo = 0, hi = njobs - 1;
+    while (lo < hi) {
+      const int mid = (lo + hi + 1) >> 1;
+      if (starts[mid] <= t) lo = mid; else hi = mid - 1;
+    }
+    const WtJob& J = jobs[lo];
+    long e = t - J.start;
+    const int co = e % J.Cout;
+    long r = e / J.Cout;
+    const int tw = r % J.ntw;
+    r /= J.ntw;
+    const int th = r % J.nth;
+    const int ci = r / J.nth;
+    const int kh = J.kh0 + J.s * th, kw = J.kw0 + J.s * tw;
+    J.out[e] = f2bf(J.w[(((long)co * J.KH + kh) * J.KW + kw) * J.Cin + ci]);
+  }
+}
+
 // out[r][c] = W[c][r] for a [R][C] fp32 matrix -> bf16 [C][R]
 __global__ void transpose_cast_kernel(const float* __restrict__ w, u16* __restrict__ out, int R, int C) {
   __shared__ float tile[32][33];
@@ -103,6 +136,18 @@ PDT_API int pdt_wt_dgrad(const float* w, void* out, int Cout, int KH, int KW, in
   if (total == 0) return 0;
   hipLaunchKernelGGL(wt_dgrad_kernel, dim3(grid_for(total)), dim3(NT), 0, st, w, (u16*)out, Cout, KH, KW, Cin, kh0,
                      kw0, s, nth, ntw);
+  PDT_RETURN_LAUNCH();
+}
+
+PDT_API int pdt_wt_job_size() { return (int)sizeof(WtJob); }
+
+// jobs: device array of WtJob (host-packed, see native_ops._DgradWeights)
+PDT_API int pdt_wt_dgrad_multi(const void* jobs, int njobs, long total, hipStream_t st) {
+  if (njobs <= 0 || total <= 0) return 0;
+  if (njobs > 512) return -1;
+  long g = (total + NT - 1) / NT;
+  if (g > 8192) g = 8192;
+  hipLaunchKernelGGL(wt_dgrad_multi_kernel, dim3((unsigned)g), dim3(NT), 0, st, (const WtJob*)jobs, njobs, total);
   PDT_RETURN_LAUNCH();
 }
 

@@ -63,6 +63,8 @@ _SIGS = {
     "pdt_cast_f32_bf16": (c_int, [P, P, c_long, P]),
     "pdt_wt_dgrad": (c_int, [P, P] + [c_int] * 9 + [P]),
     "pdt_transpose_cast": (c_int, [P, P, c_int, c_int, P]),
+    "pdt_wt_job_size": (c_int, []),
+    "pdt_wt_dgrad_multi": (c_int, [P, c_int, c_long, P]),
     "pdt_add_bf16": (c_int, [P, P, P, c_long, P]),
     "pdt_attn_fwd": (c_int, [P, P, P, c_int, c_int, c_int, c_float, P]),
     "pdt_gemm_f8_num_variants": (c_int, []),
@@ -440,6 +442,62 @@ def _conv_forward(x, wb, N, H, W, Cs, Cout, g, with_stats=False):
     return y, M, part, R
 
 
+class _DgradWeights:
+    """Cache of the transposed, stride-phase-sliced bf16 weights the dgrad GEMMs
+    consume (pdt_wt_dgrad layout), keyed per (parameter, phase). When the
+    optimizer has stepped (parameter version changed), the FIRST request
+    rebuilds every registered entry in ONE multi-tensor launch
+    (pdt_wt_dgrad_multi) instead of one small kernel per conv and phase."""
+
+    def __init__(self):
+        self.entries = {}   # key -> [weakref(param), buf, version, job-tuple, data_ptr]
+        self.table = None   # device job table (uint8) for the current entry set
+        self.total = 0
+
+    def get(self, param, Cout, KH, KW, Cin, kh0, kw0, s, nth, ntw):
+        key = (id(param), param.data_ptr(), kh0, kw0, s, nth, ntw)
+        ent = self.entries.get(key)
+        if ent is not None and ent[0]() is param and ent[2] == param._version:
+            return ent[1]
+        lib = _load()
+        if (ent is None or ent[0]() is not param) and len(self.entries) >= 512:
+            self.entries.clear()  # device job table holds at most 512 entries
+            self.table = None
+        if ent is None or ent[0]() is not param:
+            import weakref
+            buf = torch.empty(max(Cin * nth * ntw * Cout, 8), dtype=torch.bfloat16, device=param.device)
+            _chk(lib.pdt_wt_dgrad(_p(param), _p(buf), Cout, KH, KW, Cin, kh0, kw0, s, nth, ntw, _s()), "wt_dgrad")
+            self.entries[key] = [weakref.ref(param), buf, param._version, (Cout, KH, KW, Cin, kh0, kw0, s, nth, ntw),
+                                 param.data_ptr()]
+            self.table = None
+            return buf
+        self._rebuild_all(lib)
+        return ent[1]
+
+    def _rebuild_all(self, lib):
+        # drop entries whose parameter died or moved (their pointers must never reach the kernel)
+        dead = [k for k, e in self.entries.items() if e[0]() is None or e[0]().data_ptr() != e[4]]
+        for k in dead:
+            del self.entries[k]
+            self.table = None
+        if self.table is None:
+            import struct
+            assert lib.pdt_wt_job_size() == 64
+            blob, start = bytearray(), 0
+            for ref, buf, _, j, ptr in self.entries.values():
+                blob += struct.pack("<QQq10i", ptr, buf.data_ptr(), start, *j, 0)
+                start += j[3] * j[7] * j[8] * j[0]
+            dev = next(iter(self.entries.values()))[1].device
+            self.table = torch.frombuffer(bytearray(blob), dtype=torch.uint8).to(dev)
+            self.total = start
+        _chk(lib.pdt_wt_dgrad_multi(_p(self.table), len(self.entries), self.total, _s()), "wt_dgrad_multi")
+        for ent in self.entries.values():
+            ent[2] = ent[0]()._version
+
+
+_DGRAD_W = _DgradWeights()
+
+
 def _conv_dgrad(dy, w32, N, H, W, Cin, Cout, g, addend=None, addend_mask=None):
     """dX [N,Cin,H,W] (+ addend) from dY [N,Cout,Ho,Wo] (stride phases, see csrc/conv_igemm.hip)."""
     KH, KW, s_h, s_w, ph, pw = g["KH"], g["KW"], g["sh"], g["sw"], g["ph"], g["pw"]
@@ -447,7 +505,10 @@ def _conv_dgrad(dy, w32, N, H, W, Cin, Cout, g, addend=None, addend_mask=None):
     assert dy.shape[1] == Cout and dy.numel() == N * Cout * g["Ho"] * g["Wo"]
     dx = _empty_cl(N, Cin, H, W, torch.bfloat16, dy.device)
     lib = _load()
-    w32c = _cl(w32.detach().float())
+    # parameters (fp32, channels_last storage) get cached phase weights; temporaries do not
+    cacheable = isinstance(w32, nn.Parameter) and w32.dtype == torch.float32 and \
+        w32.is_contiguous(memory_format=torch.channels_last)
+    w32c = w32 if cacheable else _cl(w32.detach().float())
     for qh in range(s_h):
         kh0 = (qh + ph) % s_h
         nth = (KH - kh0 + s_h - 1) // s_h if kh0 < KH else 0
@@ -457,11 +518,14 @@ def _conv_dgrad(dy, w32, N, H, W, Cin, Cout, g, addend=None, addend_mask=None):
             ntw = (KW - kw0 + s_w - 1) // s_w if kw0 < KW else 0
             ow0 = (qw + pw - kw0) // s_w
             K = nth * ntw * Cout
-            wt = torch.empty(max(Cin * K, 8), dtype=torch.bfloat16, device=dy.device)
-            if K > 0:
-                assert s_h == s_w or True
-                _chk(lib.pdt_wt_dgrad(_p(w32c), _p(wt), Cout, KH, KW, Cin, kh0, kw0, s_h if s_h == s_w else s_h,
-                                      nth, ntw, _s()), "wt_dgrad")
+            assert s_h == s_w, "dgrad weight slicing assumes square strides"
+            if K > 0 and cacheable:
+                wt = _DGRAD_W.get(w32, Cout, KH, KW, Cin, kh0, kw0, s_h, nth, ntw)
+            else:
+                wt = torch.empty(max(Cin * K, 8), dtype=torch.bfloat16, device=dy.device)
+                if K > 0:
+                    _chk(lib.pdt_wt_dgrad(_p(w32c), _p(wt), Cout, KH, KW, Cin, kh0, kw0, s_h, nth, ntw, _s()),
+                         "wt_dgrad")
             conv_nt(dy, wt, dx, Hs=g["Ho"], Ws=g["Wo"], Cs=Cout, Nimg=N, Hm=H // s_h, Wm=W // s_w, Ncol=Cin,
                     K=K, ldb=max(K, 8), sh=1, sw=1, oh0=oh0, ow0=ow0, dh=-1, dw=-1, nth=nth, ntw=max(ntw, 0),
                     Ho=H, Wo=W, osh=s_h, osw=s_w, oph=qh, opw=qw, ldo=Cin, addend=addend, addend_mask=addend_mask)

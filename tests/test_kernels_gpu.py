@@ -526,3 +526,22 @@ def test_fused_optimizer_bumps_versions_and_fp8_cache():
         opt.step()
         assert w._version > v0
         assert not torch.equal(no.fp8_weight(w)[0], q0)
+
+
+def test_dgrad_weight_cache_tracks_updates():
+    """Cached phase weights are rebuilt (batched launch) after in-place parameter updates."""
+    torch.manual_seed(14)
+    convs = [nn.Conv2d(64, 128, 3, 2, 1, bias=False).cuda().to(memory_format=torch.channels_last),
+             nn.Conv2d(64, 64, 1, 1, 0, bias=False).cuda().to(memory_format=torch.channels_last)]
+    N, H, W = 2, 16, 16
+    for step in range(3):
+        for conv in convs:
+            g = no._fwd_geom(N, H, W, 64, conv)
+            dy = _cl(torch.randn(N, conv.out_channels, g["Ho"], g["Wo"], device="cuda").to(torch.bfloat16))
+            dx = no._conv_dgrad(dy, conv.weight, N, H, W, 64, conv.out_channels, g)
+            ref = torch.nn.grad.conv2d_input((N, 64, H, W), conv.weight.detach().to(torch.bfloat16).float(),
+                                             dy.float(), conv.stride, conv.padding)
+            assert relerr(dx, ref) < 1e-2, (step, relerr(dx, ref))
+        with torch.no_grad():
+            for conv in convs:
+                conv.weight.mul_(-1.5)
