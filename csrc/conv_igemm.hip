@@ -76,7 +76,7 @@ __device__ __attribute__((aligned(64))) u32x4 pdt_zero_chunk[4];
 // ARE its 32-byte fp8 fragment (a k permutation shared by both operands).
 // The per-tensor dequant scales multiply the accumulators in the epilogue.
 template <int BM, int BN, int NSTAGE, bool CS64, bool DIRECT, bool GLDS, int NTH = 256, int WM = 2, int F8 = 0>
-__global__ void __launch_bounds__(NTH, 2) conv_nt_kernel(NTParams p) {
+__global__ void __launch_bounds__(NTH, NSTAGE == 3 ? 1 : 2) conv_nt_kernel(NTParams p) {
   constexpr int WN = NTH / 64 / WM;       // waves along N
   constexpr int MI = BM / (WM * 16);      // 16-row MFMA tiles per wave
   constexpr int NI = BN / (WN * 16);
@@ -246,6 +246,79 @@ __global__ void __launch_bounds__(NTH, 2) conv_nt_kernel(NTParams p) {
 #pragma unroll
     for (int j = 0; j < NI; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
+  // one K-tile of MFMA work on the LDS stage at sa / sb
+  auto compute_tile = [&](const char* sa, const char* sb) {
+    if constexpr (F8 != 0) {
+      bf16x8 af[2][MI], bfr[2][NI];
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) {
+        const int kch = kk * 4 + (lane >> 4);
+#pragma unroll
+        for (int i = 0; i < MI; ++i) {
+          int r = wm * (BM / WM) + i * 16 + (lane & 15);
+          af[kk][i] = *reinterpret_cast<const bf16x8*>(sa + r * 128 + swz(r, kch) * 16);
+        }
+#pragma unroll
+        for (int j = 0; j < NI; ++j) {
+          int r = wn * (BN / WN) + j * 16 + (lane & 15);
+          bfr[kk][j] = *reinterpret_cast<const bf16x8*>(sb + r * 128 + swz(r, kch) * 16);
+        }
+      }
+      if (NSTAGE == 3) __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int i = 0; i < MI; ++i)
+#pragma unroll
+        for (int j = 0; j < NI; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(
+              cat8(bfr[0][j], bfr[1][j]), cat8(af[0][i], af[1][i]), acc[i][j], 0, F8 == 2 ? 1 : 0, 0, 127, 0, 127);
+      if (NSTAGE == 3) __builtin_amdgcn_s_setprio(0);
+    } else {
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) {
+        const int kch = kk * 4 + (lane >> 4);
+        bf16x8 af[MI], bfr[NI];
+#pragma unroll
+        for (int i = 0; i < MI; ++i) {
+          int r = wm * (BM / WM) + i * 16 + (lane & 15);
+          af[i] = *reinterpret_cast<const bf16x8*>(sa + r * 128 + swz(r, kch) * 16);
+        }
+#pragma unroll
+        for (int j = 0; j < NI; ++j) {
+          int r = wn * (BN / WN) + j * 16 + (lane & 15);
+          bfr[j] = *reinterpret_cast<const bf16x8*>(sb + r * 128 + swz(r, kch) * 16);
+        }
+        if (NSTAGE == 3) __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+        for (int i = 0; i < MI; ++i)
+#pragma unroll
+          for (int j = 0; j < NI; ++j)
+            // swapped operands: lane holds 4 consecutive output channels of one row
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[j], af[i], acc[i][j], 0, 0, 0);
+        if (NSTAGE == 3) __builtin_amdgcn_s_setprio(0);
+      }
+    }
+  };
+
+  if constexpr (NSTAGE == 3) {
+    // 3-stage LDS-DMA ring, ONE raw barrier per K-tile, loads stay in flight
+    // across it: tile kt+2 is issued right after the barrier that proves every
+    // wave finished reading its buffer (tile kt-1's), and the counted
+    // vmcnt(LA+LB) before the barrier retires only this thread's tile-kt DMA
+    // (tile kt+1's stays outstanding). No __syncthreads (vmcnt(0)) in the loop.
+    static_assert(GLDS, "3-stage ring is the LDS-DMA pipeline");
+    if (nk > 0) glds_tile(0, 0);
+    if (nk > 1) glds_tile(1, 1);
+    for (int kt = 0; kt < nk; ++kt) {
+      if (kt + 1 < nk) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(LA + LB) : "memory");
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+      if (kt + 2 < nk) glds_tile(kt + 2, (kt + 2) % 3);
+      const char* sa = smem + (kt % 3) * STAGE;
+      compute_tile(sa, sa + A_BYTES);
+    }
+    if (!DIRECT) __syncthreads();  // before the epilogue reuses LDS
+  } else {
   if (GLDS) {
     if (nk > 0) glds_tile(0, 0);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -263,51 +336,7 @@ __global__ void __launch_bounds__(NTH, 2) conv_nt_kernel(NTParams p) {
       load_tile(kt + 1);
     }
     const char* sa = smem + cur * STAGE;
-    const char* sb = sa + A_BYTES;
-    if constexpr (F8 != 0) {
-      bf16x8 af[2][MI], bfr[2][NI];
-#pragma unroll
-      for (int kk = 0; kk < 2; ++kk) {
-        const int kch = kk * 4 + (lane >> 4);
-#pragma unroll
-        for (int i = 0; i < MI; ++i) {
-          int r = wm * (BM / WM) + i * 16 + (lane & 15);
-          af[kk][i] = *reinterpret_cast<const bf16x8*>(sa + r * 128 + swz(r, kch) * 16);
-        }
-#pragma unroll
-        for (int j = 0; j < NI; ++j) {
-          int r = wn * (BN / WN) + j * 16 + (lane & 15);
-          bfr[kk][j] = *reinterpret_cast<const bf16x8*>(sb + r * 128 + swz(r, kch) * 16);
-        }
-      }
-#pragma unroll
-      for (int i = 0; i < MI; ++i)
-#pragma unroll
-        for (int j = 0; j < NI; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(
-              cat8(bfr[0][j], bfr[1][j]), cat8(af[0][i], af[1][i]), acc[i][j], 0, F8 == 2 ? 1 : 0, 0, 127, 0, 127);
-    } else
-#pragma unroll
-    for (int kk = 0; kk < 2; ++kk) {
-      const int kch = kk * 4 + (lane >> 4);
-      bf16x8 af[MI], bfr[NI];
-#pragma unroll
-      for (int i = 0; i < MI; ++i) {
-        int r = wm * (BM / WM) + i * 16 + (lane & 15);
-        af[i] = *reinterpret_cast<const bf16x8*>(sa + r * 128 + swz(r, kch) * 16);
-      }
-#pragma unroll
-      for (int j = 0; j < NI; ++j) {
-        int r = wn * (BN / WN) + j * 16 + (lane & 15);
-        bfr[j] = *reinterpret_cast<const bf16x8*>(sb + r * 128 + swz(r, kch) * 16);
-      }
-#pragma unroll
-      for (int i = 0; i < MI; ++i)
-#pragma unroll
-        for (int j = 0; j < NI; ++j)
-          // swapped operands: lane holds 4 consecutive output channels of one row
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[j], af[i], acc[i][j], 0, 0, 0);
-    }
+    compute_tile(sa, sa + A_BYTES);
     if (GLDS) {
       if (NSTAGE == 2) {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // my DMA into the other buffer landed
@@ -328,6 +357,7 @@ __global__ void __launch_bounds__(NTH, 2) conv_nt_kernel(NTParams p) {
     }
   }
   if (NSTAGE == 1 && !DIRECT) __syncthreads();  // before the epilogue reuses LDS
+  }
 
   // ---------------------------------------------------------------- epilogue
   // acc[i][j][r] = C[row = wm*BM/2 + i*16 + (lane&15)][col = wn*BN/2 + j*16 + (lane>>4)*4 + r]
@@ -528,17 +558,20 @@ int launch(const NTParams& p, hipStream_t st) {
 //   ids 30..33 : 512-thread (8-wave) tiles, 2 stages, 64x64 per wave:
 //                256x128 (4x2 waves) and 128x256 (2x4 waves), each LDS-DMA
 //                and register-staged
-constexpr int NVAR = 34;
+//   ids 34..35 : the 8-wave tiles on the 3-stage LDS-DMA ring (1 barrier per
+//                K-tile, counted vmcnt, s_setprio around the MFMA bursts;
+//                144 KB LDS -> one workgroup of 8 waves per CU)
+constexpr int NVAR = 36;
 constexpr int VAR_BM[NVAR] = {128, 256, 64, 128, 64, 128, 256, 64, 128, 64,
                               128, 256, 64, 128, 64, 128, 256, 64, 128, 64,
                               128, 256, 64, 128, 64, 128, 256, 64, 128, 64,
-                              256, 128, 256, 128};
+                              256, 128, 256, 128, 256, 128};
 constexpr int VAR_BN[NVAR] = {128, 64, 128, 64, 64, 128, 64, 128, 64, 64,
                               128, 64, 128, 64, 64, 128, 64, 128, 64, 64,
                               128, 64, 128, 64, 64, 128, 64, 128, 64, 64,
-                              128, 256, 128, 256};
+                              128, 256, 128, 256, 128, 256};
 constexpr int VAR_WM[NVAR] = {2, 2, 2, 2, 2, 2, 2, 2, 2, 2, 2, 2, 2, 2, 2, 2, 2, 2, 2, 2,
-                              2, 2, 2, 2, 2, 2, 2, 2, 2, 2, 4, 2, 4, 2};
+                              2, 2, 2, 2, 2, 2, 2, 2, 2, 2, 4, 2, 4, 2, 4, 2};
 
 int heuristic_variant(int M, int Ncol, int K) {
   (void)M;
@@ -583,6 +616,8 @@ int launch_variant(int v, const NTParams& p, hipStream_t st) {
     case 31: return launch<128, 256, 2, CS64, false, true, 512, 2>(p, st);
     case 32: return launch<256, 128, 2, CS64, false, false, 512, 4>(p, st);
     case 33: return launch<128, 256, 2, CS64, false, false, 512, 2>(p, st);
+    case 34: return launch<256, 128, 3, CS64, false, true, 512, 4>(p, st);
+    case 35: return launch<128, 256, 3, CS64, false, true, 512, 2>(p, st);
   }
   return -3;
 }
@@ -653,9 +688,9 @@ PDT_API int pdt_conv_nt(const void* src, const void* b, void* out, float* stats,
 // A: [M][lda] fp8 (e4m3 if fmt_a == 0, e5m2 if 1), B: [N][ldb] e4m3, out bf16 [M][ldo].
 // K, lda, ldb in BYTES (= elements), multiples of 128 / 16 / 16.
 namespace {
-constexpr int NVAR_F8 = 8;
-constexpr int VAR_F8_BM[NVAR_F8] = {128, 128, 256, 128, 64, 128, 256, 128};
-constexpr int VAR_F8_BN[NVAR_F8] = {128, 128, 128, 256, 128, 64, 64, 128};
+constexpr int NVAR_F8 = 10;
+constexpr int VAR_F8_BM[NVAR_F8] = {128, 128, 256, 128, 64, 128, 256, 128, 256, 128};
+constexpr int VAR_F8_BN[NVAR_F8] = {128, 128, 128, 256, 128, 64, 64, 128, 128, 256};
 
 template <int F8>
 int launch_f8(int v, const NTParams& p, hipStream_t st) {
@@ -668,6 +703,8 @@ int launch_f8(int v, const NTParams& p, hipStream_t st) {
     case 5: return launch<128, 64, 2, true, false, true, 256, 2, F8>(p, st);
     case 6: return launch<256, 64, 2, true, false, true, 256, 2, F8>(p, st);
     case 7: return launch<128, 128, 2, true, true, true, 256, 2, F8>(p, st);
+    case 8: return launch<256, 128, 3, true, false, true, 512, 4, F8>(p, st);
+    case 9: return launch<128, 256, 3, true, false, true, 512, 2, F8>(p, st);
   }
   return -3;
 }
