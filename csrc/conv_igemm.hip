@@ -75,8 +75,9 @@ __device__ __attribute__((aligned(64))) u32x4 pdt_zero_chunk[4];
 // consumes a whole 128-byte LDS k-row: the two bf16 k-step fragments of a lane
 // ARE its 32-byte fp8 fragment (a k permutation shared by both operands).
 // The per-tensor dequant scales multiply the accumulators in the epilogue.
-template <int BM, int BN, int NSTAGE, bool CS64, bool DIRECT, bool GLDS, int NTH = 256, int WM = 2, int F8 = 0>
-__global__ void __launch_bounds__(NTH, NSTAGE == 3 ? 1 : 2) conv_nt_kernel(NTParams p) {
+template <int BM, int BN, int NSTAGE, bool CS64, bool DIRECT, bool GLDS, int NTH = 256, int WM = 2, int F8 = 0,
+          bool PIPE = false>
+__global__ void __launch_bounds__(NTH, PIPE ? 1 : 2) conv_nt_kernel(NTParams p) {
   constexpr int WN = NTH / 64 / WM;       // waves along N
   constexpr int MI = BM / (WM * 16);      // 16-row MFMA tiles per wave
   constexpr int NI = BN / (WN * 16);
@@ -264,14 +265,14 @@ __global__ void __launch_bounds__(NTH, NSTAGE == 3 ? 1 : 2) conv_nt_kernel(NTPar
           bfr[kk][j] = *reinterpret_cast<const bf16x8*>(sb + r * 128 + swz(r, kch) * 16);
         }
       }
-      if (NSTAGE == 3) __builtin_amdgcn_s_setprio(1);
+      if (PIPE) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
       for (int i = 0; i < MI; ++i)
 #pragma unroll
         for (int j = 0; j < NI; ++j)
           acc[i][j] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(
               cat8(bfr[0][j], bfr[1][j]), cat8(af[0][i], af[1][i]), acc[i][j], 0, F8 == 2 ? 1 : 0, 0, 127, 0, 127);
-      if (NSTAGE == 3) __builtin_amdgcn_s_setprio(0);
+      if (PIPE) __builtin_amdgcn_s_setprio(0);
     } else {
 #pragma unroll
       for (int kk = 0; kk < 2; ++kk) {
@@ -287,34 +288,34 @@ __global__ void __launch_bounds__(NTH, NSTAGE == 3 ? 1 : 2) conv_nt_kernel(NTPar
           int r = wn * (BN / WN) + j * 16 + (lane & 15);
           bfr[j] = *reinterpret_cast<const bf16x8*>(sb + r * 128 + swz(r, kch) * 16);
         }
-        if (NSTAGE == 3) __builtin_amdgcn_s_setprio(1);
+        if (PIPE) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
         for (int i = 0; i < MI; ++i)
 #pragma unroll
           for (int j = 0; j < NI; ++j)
             // swapped operands: lane holds 4 consecutive output channels of one row
             acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[j], af[i], acc[i][j], 0, 0, 0);
-        if (NSTAGE == 3) __builtin_amdgcn_s_setprio(0);
+        if (PIPE) __builtin_amdgcn_s_setprio(0);
       }
     }
   };
 
-  if constexpr (NSTAGE == 3) {
-    // 3-stage LDS-DMA ring, ONE raw barrier per K-tile, loads stay in flight
-    // across it: tile kt+2 is issued right after the barrier that proves every
-    // wave finished reading its buffer (tile kt-1's), and the counted
-    // vmcnt(LA+LB) before the barrier retires only this thread's tile-kt DMA
-    // (tile kt+1's stays outstanding). No __syncthreads (vmcnt(0)) in the loop.
-    static_assert(GLDS, "3-stage ring is the LDS-DMA pipeline");
-    if (nk > 0) glds_tile(0, 0);
-    if (nk > 1) glds_tile(1, 1);
+  if constexpr (PIPE) {
+    // NSTAGE-deep LDS-DMA ring, ONE raw barrier per K-tile: tile kt+NSTAGE-1
+    // is issued right after the barrier that proves every wave finished
+    // reading its buffer (tile kt-1's); the counted vmcnt before the barrier
+    // retires only this thread's tile-kt DMA (with 3 stages tile kt+1's stays
+    // in flight across it). No __syncthreads (vmcnt(0) lgkmcnt(0)) in the loop.
+    static_assert(GLDS && (NSTAGE == 2 || NSTAGE == 3), "the ring is the LDS-DMA pipeline");
+    for (int t = 0; t < NSTAGE - 1; ++t)
+      if (t < nk) glds_tile(t, t);
     for (int kt = 0; kt < nk; ++kt) {
-      if (kt + 1 < nk) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(LA + LB) : "memory");
+      if (NSTAGE == 3 && kt + 1 < nk) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(LA + LB) : "memory");
       else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __builtin_amdgcn_s_barrier();
       asm volatile("" ::: "memory");
-      if (kt + 2 < nk) glds_tile(kt + 2, (kt + 2) % 3);
-      const char* sa = smem + (kt % 3) * STAGE;
+      if (kt + NSTAGE - 1 < nk) glds_tile(kt + NSTAGE - 1, (kt + NSTAGE - 1) % NSTAGE);
+      const char* sa = smem + (kt % NSTAGE) * STAGE;
       compute_tile(sa, sa + A_BYTES);
     }
     if (!DIRECT) __syncthreads();  // before the epilogue reuses LDS
@@ -543,11 +544,12 @@ __global__ void __launch_bounds__(NTH, NSTAGE == 3 ? 1 : 2) conv_nt_kernel(NTPar
   stage_store(p.out, p.addend);
 }
 
-template <int BM, int BN, int NS, bool CS64, bool DIRECT, bool GLDS = false, int NTH = 256, int WM = 2, int F8 = 0>
+template <int BM, int BN, int NS, bool CS64, bool DIRECT, bool GLDS = false, int NTH = 256, int WM = 2, int F8 = 0,
+          bool PIPE = false>
 int launch(const NTParams& p, hipStream_t st) {
   int ntm = (p.M + BM - 1) / BM, ntn = (p.Ncol + BN - 1) / BN;
-  hipLaunchKernelGGL((conv_nt_kernel<BM, BN, NS, CS64, DIRECT, GLDS, NTH, WM, F8>), dim3(ntm * ntn), dim3(NTH), 0,
-                     st, p);
+  hipLaunchKernelGGL((conv_nt_kernel<BM, BN, NS, CS64, DIRECT, GLDS, NTH, WM, F8, PIPE>), dim3(ntm * ntn), dim3(NTH),
+                     0, st, p);
   PDT_RETURN_LAUNCH();
 }
 
@@ -561,17 +563,20 @@ int launch(const NTParams& p, hipStream_t st) {
 //   ids 34..35 : the 8-wave tiles on the 3-stage LDS-DMA ring (1 barrier per
 //                K-tile, counted vmcnt, s_setprio around the MFMA bursts;
 //                144 KB LDS -> one workgroup of 8 waves per CU)
-constexpr int NVAR = 36;
+//   id 36      : 256x256 (2x4 waves of 128x64), 2-stage ring (128 KB LDS): the
+//                per-wave tile that lifts the LDS-bytes-per-MFMA ratio above the
+//                64x64 tiles' (LDS read bandwidth, not MFMA, bounds those)
+constexpr int NVAR = 37;
 constexpr int VAR_BM[NVAR] = {128, 256, 64, 128, 64, 128, 256, 64, 128, 64,
                               128, 256, 64, 128, 64, 128, 256, 64, 128, 64,
                               128, 256, 64, 128, 64, 128, 256, 64, 128, 64,
-                              256, 128, 256, 128, 256, 128};
+                              256, 128, 256, 128, 256, 128, 256};
 constexpr int VAR_BN[NVAR] = {128, 64, 128, 64, 64, 128, 64, 128, 64, 64,
                               128, 64, 128, 64, 64, 128, 64, 128, 64, 64,
                               128, 64, 128, 64, 64, 128, 64, 128, 64, 64,
-                              128, 256, 128, 256, 128, 256};
+                              128, 256, 128, 256, 128, 256, 256};
 constexpr int VAR_WM[NVAR] = {2, 2, 2, 2, 2, 2, 2, 2, 2, 2, 2, 2, 2, 2, 2, 2, 2, 2, 2, 2,
-                              2, 2, 2, 2, 2, 2, 2, 2, 2, 2, 4, 2, 4, 2, 4, 2};
+                              2, 2, 2, 2, 2, 2, 2, 2, 2, 2, 4, 2, 4, 2, 4, 2, 2};
 
 int heuristic_variant(int M, int Ncol, int K) {
   (void)M;
@@ -616,8 +621,9 @@ int launch_variant(int v, const NTParams& p, hipStream_t st) {
     case 31: return launch<128, 256, 2, CS64, false, true, 512, 2>(p, st);
     case 32: return launch<256, 128, 2, CS64, false, false, 512, 4>(p, st);
     case 33: return launch<128, 256, 2, CS64, false, false, 512, 2>(p, st);
-    case 34: return launch<256, 128, 3, CS64, false, true, 512, 4>(p, st);
-    case 35: return launch<128, 256, 3, CS64, false, true, 512, 2>(p, st);
+    case 34: return launch<256, 128, 3, CS64, false, true, 512, 4, 0, true>(p, st);
+    case 35: return launch<128, 256, 3, CS64, false, true, 512, 2, 0, true>(p, st);
+    case 36: return launch<256, 256, 2, CS64, false, true, 512, 2, 0, true>(p, st);
   }
   return -3;
 }
@@ -688,9 +694,9 @@ PDT_API int pdt_conv_nt(const void* src, const void* b, void* out, float* stats,
 // A: [M][lda] fp8 (e4m3 if fmt_a == 0, e5m2 if 1), B: [N][ldb] e4m3, out bf16 [M][ldo].
 // K, lda, ldb in BYTES (= elements), multiples of 128 / 16 / 16.
 namespace {
-constexpr int NVAR_F8 = 10;
-constexpr int VAR_F8_BM[NVAR_F8] = {128, 128, 256, 128, 64, 128, 256, 128, 256, 128};
-constexpr int VAR_F8_BN[NVAR_F8] = {128, 128, 128, 256, 128, 64, 64, 128, 128, 256};
+constexpr int NVAR_F8 = 11;
+constexpr int VAR_F8_BM[NVAR_F8] = {128, 128, 256, 128, 64, 128, 256, 128, 256, 128, 256};
+constexpr int VAR_F8_BN[NVAR_F8] = {128, 128, 128, 256, 128, 64, 64, 128, 128, 256, 256};
 
 template <int F8>
 int launch_f8(int v, const NTParams& p, hipStream_t st) {
@@ -703,8 +709,9 @@ int launch_f8(int v, const NTParams& p, hipStream_t st) {
     case 5: return launch<128, 64, 2, true, false, true, 256, 2, F8>(p, st);
     case 6: return launch<256, 64, 2, true, false, true, 256, 2, F8>(p, st);
     case 7: return launch<128, 128, 2, true, true, true, 256, 2, F8>(p, st);
-    case 8: return launch<256, 128, 3, true, false, true, 512, 4, F8>(p, st);
-    case 9: return launch<128, 256, 3, true, false, true, 512, 2, F8>(p, st);
+    case 8: return launch<256, 128, 3, true, false, true, 512, 4, F8, true>(p, st);
+    case 9: return launch<128, 256, 3, true, false, true, 512, 2, F8, true>(p, st);
+    case 10: return launch<256, 256, 2, true, false, true, 512, 2, F8, true>(p, st);
   }
   return -3;
 }
