@@ -14,6 +14,7 @@ from __future__ import annotations
 import ctypes
 import os
 import threading
+import weakref
 from pathlib import Path
 
 import torch
@@ -141,9 +142,15 @@ def _empty_cl(n, c, h, w, dtype, device):
 _SHADOWS: dict = {}
 
 
+def _same_tensor(ent_ref, w) -> bool:
+    # id() and data_ptr() are both recycled after a tensor dies (a new Parameter of
+    # the same size can get both): the cache entry must point at THIS object
+    return ent_ref is not None and ent_ref() is w
+
+
 def register_shadow(param: torch.Tensor, shadow: torch.Tensor):
     """Optimizers that write a bf16 copy while stepping register it here."""
-    _SHADOWS[id(param)] = (shadow, param._version, param.data_ptr())
+    _SHADOWS[id(param)] = (shadow, param._version, param.data_ptr(), weakref.ref(param))
 
 
 def bf16_weight(w: torch.Tensor, pad_cin_to: int | None = None) -> torch.Tensor:
@@ -152,7 +159,7 @@ def bf16_weight(w: torch.Tensor, pad_cin_to: int | None = None) -> torch.Tensor:
         return _cl(w)
     key = (id(w), pad_cin_to)
     ent = _SHADOWS.get(key if pad_cin_to else id(w))
-    if ent is not None and ent[1] == w._version and ent[2] == w.data_ptr():
+    if ent is not None and ent[1] == w._version and ent[2] == w.data_ptr() and _same_tensor(ent[3], w):
         return ent[0]
     src = _cl(w.detach())
     if pad_cin_to is not None and src.shape[1] != pad_cin_to:
@@ -164,8 +171,15 @@ def bf16_weight(w: torch.Tensor, pad_cin_to: int | None = None) -> torch.Tensor:
         _chk(_load().pdt_cast_f32_bf16(_p(src), _p(out), src.numel(), _s()), "cast")
     else:
         out.copy_(src)
-    _SHADOWS[key if pad_cin_to else id(w)] = (out, w._version, w.data_ptr())
+    _SHADOWS[key if pad_cin_to else id(w)] = (out, w._version, w.data_ptr(), _weak(w))
     return out
+
+
+def _weak(t):
+    try:
+        return weakref.ref(t)
+    except TypeError:
+        return None
 
 
 # =============================================================================
@@ -906,7 +920,7 @@ _F8W: dict = {}
 def fp8_weight(w: torch.Tensor):
     """(wq [N][K] e4m3, wqt [K][N] e4m3, dq) of an fp32 [N][K] weight, cached per optimizer version."""
     ent = _F8W.get(id(w))
-    if ent is not None and ent[0] == w._version and ent[1] == w.data_ptr():
+    if ent is not None and ent[0] == w._version and ent[1] == w.data_ptr() and _same_tensor(ent[3], w):
         return ent[2]
     lib = _load()
     src = w.detach().float().contiguous()
@@ -920,7 +934,7 @@ def fp8_weight(w: torch.Tensor):
     _chk(lib.pdt_cast_fp8(_p(src), 0, src.numel(), _p(part), E4M3, _p(wq), _p(dq), st), "cast_fp8")
     _chk(lib.pdt_cast_fp8_t(_p(src), N, K, _p(part), _p(wqt), st), "cast_fp8_t")
     val = (wq, wqt, dq)
-    _F8W[id(w)] = (w._version, w.data_ptr(), val)
+    _F8W[id(w)] = (w._version, w.data_ptr(), val, _weak(w))
     return val
 
 
