@@ -19,6 +19,7 @@
 // over all query tiles) and a dQ kernel (one workgroup per 64 queries) -- the
 // probabilities are recomputed from Q, K and the saved log-sum-exp, no atomics.
 #include "pdt_common.h"
+#include <stdlib.h>
 
 namespace {
 
@@ -415,7 +416,352 @@ __global__ void __launch_bounds__(256) attn_bwd_dq_kernel(AttnBwdParams p) {
   }
 }
 
+// ============================================================================
+// Whole-sequence kernels (T <= 16*NKT <= 256, e.g. ViT's 197 tokens): one
+// workgroup per (b, h) stages the ENTIRE K/V (forward), Q/dO (dK/dV) or K/V
+// (dQ) of the head into LDS once, then every wave loops over its 16-row
+// subtiles with no further barriers -- the tiled kernels above pay a
+// global->LDS round trip and two barriers per 64-row tile for 16 MFMAs.
+// The softmax of a 16-query subtile is taken over all keys at once.
+// ============================================================================
+
+// stage rows [0, 16*NKT) of a head (zero beyond T) as a row or transposed image
+template <bool TR, int NKT, int NTH>
+__device__ __forceinline__ void stage_seq(char* lds, const u16* src, long ld, int T, int tid) {
+  constexpr int CH = NKT * 16 * 8;  // 16-B chunks
+#pragma unroll
+  for (int it = 0; it < (CH + NTH - 1) / NTH; ++it) {
+    const int q = tid + it * NTH;
+    if (q < CH) {
+      const int row = q >> 3, ch = q & 7;
+      u32x4 v = {0, 0, 0, 0};
+      if (row < T) v = *reinterpret_cast<const u32x4*>(src + (long)row * ld + ch * 8);
+      *reinterpret_cast<u32x4*>(lds + (TR ? tr_off(row, ch * 16) : row_off(row, ch))) = v;
+    }
+  }
+}
+
+template <int NKT>
+__global__ void __launch_bounds__(256) attn_fwd_seq_kernel(AttnParams p) {
+  constexpr int NR = ((NKT + 1) & ~1) * 16;  // rows staged (even number of 16-row subtiles)
+  __shared__ __attribute__((aligned(16))) char smem[2 * NR * 128];
+  char* Ks = smem;
+  char* Vs = smem + NR * 128;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, g = lane >> 4;
+  const int bh = blockIdx.x, b = bh / p.H, h = bh % p.H;
+  const u16* base = p.qkv + (long)b * p.T * p.ld + h * D;
+  stage_seq<false, NR / 16, 256>(Ks, base + p.H * D, p.ld, p.T, tid);
+  stage_seq<true, NR / 16, 256>(Vs, base + 2 * p.H * D, p.ld, p.T, tid);
+  __syncthreads();
+  const int nkt = (p.T + 15) >> 4;
+  for (int qs = wave; qs < nkt; qs += 4) {
+    const int qrow = qs * 16 + (lane & 15);
+    bf16x8 qf[2];
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      u32x4 v = {0, 0, 0, 0};
+      if (qrow < p.T) v = *reinterpret_cast<const u32x4*>(base + (long)qrow * p.ld + 32 * kk + 8 * g);
+      qf[kk] = __builtin_bit_cast(bf16x8, v);
+    }
+    constexpr int NKE = (NKT + 1) & ~1;  // even: key subtiles pair up into 32-key MFMA steps
+    f32x4 s[NKE];
+    float m = -INFINITY;
+#pragma unroll
+    for (int t = 0; t < NKE; ++t) {
+      s[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+      if (t < nkt) {
+#pragma unroll
+        for (int kk = 0; kk < 2; ++kk)
+          s[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ld_row_frag(Ks, 16 * t + (lane & 15), 4 * kk + g), qf[kk],
+                                                         s[t], 0, 0, 0);
+      }
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float v = (16 * t + 4 * g + r) < p.T ? s[t][r] * p.c : -INFINITY;
+        s[t][r] = v;
+        m = fmaxf(m, v);
+      }
+    }
+    m = xor_max4(m);
+    float l = 0.f;
+#pragma unroll
+    for (int t = 0; t < NKE; ++t)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float e = exp2f(s[t][r] - m);
+        s[t][r] = e;
+        l += e;
+      }
+    l = xor_sum4(l);
+    f32x4 o[4];
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt) o[dt] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int ks = 0; ks < NKE / 2; ++ks) {
+      if (2 * ks < nkt) {
+        const bf16x8 pf = pack_p(s[2 * ks], s[2 * ks + 1]);
+#pragma unroll
+        for (int dt = 0; dt < 4; ++dt)
+          o[dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(tr_frag2(Vs, 32 * ks, 32 * ks + 16, 16 * dt, lane), pf,
+                                                          o[dt], 0, 0, 0);
+      }
+    }
+    if (qrow < p.T) {
+      const float inv = 1.f / l;
+      u16* orow = p.out + ((long)b * p.T + qrow) * p.ldo + h * D;
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt) {
+        uint2 w;
+        w.x = pack2bf(o[dt][0] * inv, o[dt][1] * inv);
+        w.y = pack2bf(o[dt][2] * inv, o[dt][3] * inv);
+        *reinterpret_cast<uint2*>(orow + 16 * dt + 4 * g) = w;
+      }
+      if (g == 0) p.lse[(long)bh * p.T + qrow] = m + log2f(l);
+    }
+  }
+}
+
+// delta[q] = sum_d dO[q][d] O[q][d] for the 16-query subtile of this lane group:
+// each of the 4 lanes sharing a query sums 16 of the 64 dims
+__device__ __forceinline__ float row_delta(const u16* dOrow, const u16* Orow, int g) {
+  float v = 0.f;
+#pragma unroll
+  for (int c = 0; c < 2; ++c) {
+    const u32x4 a = *reinterpret_cast<const u32x4*>(dOrow + 16 * g + 8 * c);
+    const u32x4 o = *reinterpret_cast<const u32x4*>(Orow + 16 * g + 8 * c);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) v += lo_bf(a[e]) * lo_bf(o[e]) + hi_bf(a[e]) * hi_bf(o[e]);
+  }
+  return xor_sum4(v);
+}
+
+struct AttnSeqBwdParams {
+  const u16* qkv;
+  const u16* out;   // forward output O [B, T, H*64]
+  const u16* dout;  // [B, T, H*64]
+  const float* lse; // [B*H, T]
+  u16* dqkv;
+  int B, T, H;
+  long ld, ldo;
+  float c, scale;
+};
+
+// dK, dV: one workgroup (8 waves) per (b, h); wave w owns key subtiles w, w+8.
+template <int NKT_>
+__global__ void __launch_bounds__(512) attn_bwd_dkdv_seq_kernel(AttnSeqBwdParams p) {
+  constexpr int NKT = (NKT_ + 1) & ~1;  // even number of 16-row subtiles staged
+  constexpr int IMG = NKT * 16 * 128;
+  __shared__ __attribute__((aligned(16))) char smem[4 * IMG + 2 * NKT * 16 * 4];
+  char* Qr = smem;
+  char* Qt = smem + IMG;
+  char* dOr = smem + 2 * IMG;
+  char* dOt = smem + 3 * IMG;
+  float* lse_s = reinterpret_cast<float*>(smem + 4 * IMG);
+  float* dl_s = lse_s + NKT * 16;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, g = lane >> 4;
+  const int bh = blockIdx.x, b = bh / p.H, h = bh % p.H;
+  const u16* base = p.qkv + (long)b * p.T * p.ld + h * D;
+  const u16* dOg = p.dout + (long)b * p.T * p.ldo + h * D;
+  const u16* Og = p.out + (long)b * p.T * p.ldo + h * D;
+  stage_seq<false, NKT, 512>(Qr, base, p.ld, p.T, tid);
+  stage_seq<true, NKT, 512>(Qt, base, p.ld, p.T, tid);
+  stage_seq<false, NKT, 512>(dOr, dOg, p.ldo, p.T, tid);
+  stage_seq<true, NKT, 512>(dOt, dOg, p.ldo, p.T, tid);
+  // per-query softmax stats: lse from the forward, delta recomputed here (8 lanes per query)
+  for (int i = tid; i < NKT * 16 * 8; i += 512) {
+    const int q = i >> 3, part = i & 7;
+    float v = 0.f;
+    if (q < p.T) {
+      const u32x4 a = *reinterpret_cast<const u32x4*>(dOg + (long)q * p.ldo + part * 8);
+      const u32x4 o = *reinterpret_cast<const u32x4*>(Og + (long)q * p.ldo + part * 8);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) v += lo_bf(a[e]) * lo_bf(o[e]) + hi_bf(a[e]) * hi_bf(o[e]);
+    }
+    v += __shfl_xor(v, 1, 64);
+    v += __shfl_xor(v, 2, 64);
+    v += __shfl_xor(v, 4, 64);
+    if (part == 0) {
+      dl_s[q] = v;
+      lse_s[q] = q < p.T ? p.lse[(long)bh * p.T + q] : 0.f;
+    }
+  }
+  __syncthreads();
+  const int nkt = (p.T + 15) >> 4;
+  for (int kt = wave; kt < nkt; kt += 8) {
+    const int key = kt * 16 + (lane & 15);
+    bf16x8 kf[2], vf[2];
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      u32x4 a = {0, 0, 0, 0}, c = {0, 0, 0, 0};
+      if (key < p.T) {
+        a = *reinterpret_cast<const u32x4*>(base + p.H * D + (long)key * p.ld + 32 * kk + 8 * g);
+        c = *reinterpret_cast<const u32x4*>(base + 2 * p.H * D + (long)key * p.ld + 32 * kk + 8 * g);
+      }
+      kf[kk] = __builtin_bit_cast(bf16x8, a);
+      vf[kk] = __builtin_bit_cast(bf16x8, c);
+    }
+    f32x4 dk[4], dv[4];
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt) dk[dt] = dv[dt] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int qp = 0; 2 * qp < nkt; ++qp) {
+      f32x4 sp[2], dsp[2];
+#pragma unroll
+      for (int h2 = 0; h2 < 2; ++h2) {
+        const int u = 2 * qp + h2;
+        f32x4 sv = f32x4{0.f, 0.f, 0.f, 0.f}, dpv = f32x4{0.f, 0.f, 0.f, 0.f};
+        if (u < nkt) {
+#pragma unroll
+          for (int kk = 0; kk < 2; ++kk) {
+            sv = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ld_row_frag(Qr, 16 * u + (lane & 15), 4 * kk + g), kf[kk],
+                                                         sv, 0, 0, 0);
+            dpv = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ld_row_frag(dOr, 16 * u + (lane & 15), 4 * kk + g),
+                                                          vf[kk], dpv, 0, 0, 0);
+          }
+        }
+        // sv[r] = S[q = 16u + 4g + r][key]
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int q = 16 * u + 4 * g + r;
+          float pr = 0.f, ds = 0.f;
+          if (q < p.T && key < p.T) {
+            pr = exp2f(sv[r] * p.c - lse_s[q]);
+            ds = pr * (dpv[r] - dl_s[q]);
+          }
+          sv[r] = pr;
+          dpv[r] = ds;
+        }
+        sp[h2] = sv;
+        dsp[h2] = dpv;
+      }
+      const bf16x8 pf = pack_p(sp[0], sp[1]);
+      const bf16x8 sf = pack_p(dsp[0], dsp[1]);
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt) {
+        dv[dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(tr_frag2(dOt, 32 * qp, 32 * qp + 16, 16 * dt, lane), pf,
+                                                         dv[dt], 0, 0, 0);
+        dk[dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(tr_frag2(Qt, 32 * qp, 32 * qp + 16, 16 * dt, lane), sf,
+                                                         dk[dt], 0, 0, 0);
+      }
+    }
+    if (key < p.T) {
+      u16* drow = p.dqkv + ((long)b * p.T + key) * p.ld + h * D;
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt) {
+        uint2 wk, wv;
+        wk.x = pack2bf(dk[dt][0] * p.scale, dk[dt][1] * p.scale);
+        wk.y = pack2bf(dk[dt][2] * p.scale, dk[dt][3] * p.scale);
+        wv.x = pack2bf(dv[dt][0], dv[dt][1]);
+        wv.y = pack2bf(dv[dt][2], dv[dt][3]);
+        *reinterpret_cast<uint2*>(drow + p.H * D + 16 * dt + 4 * g) = wk;
+        *reinterpret_cast<uint2*>(drow + 2 * p.H * D + 16 * dt + 4 * g) = wv;
+      }
+    }
+  }
+}
+
+// dQ: one workgroup (8 waves) per (b, h); wave w owns query subtiles w, w+8.
+template <int NKT_>
+__global__ void __launch_bounds__(512) attn_bwd_dq_seq_kernel(AttnSeqBwdParams p) {
+  constexpr int NKT = (NKT_ + 1) & ~1;
+  constexpr int IMG = NKT * 16 * 128;
+  __shared__ __attribute__((aligned(16))) char smem[3 * IMG];
+  char* Kr = smem;
+  char* Kt = smem + IMG;
+  char* Vr = smem + 2 * IMG;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, g = lane >> 4;
+  const int bh = blockIdx.x, b = bh / p.H, h = bh % p.H;
+  const u16* base = p.qkv + (long)b * p.T * p.ld + h * D;
+  const u16* dOg = p.dout + (long)b * p.T * p.ldo + h * D;
+  const u16* Og = p.out + (long)b * p.T * p.ldo + h * D;
+  stage_seq<false, NKT, 512>(Kr, base + p.H * D, p.ld, p.T, tid);
+  stage_seq<true, NKT, 512>(Kt, base + p.H * D, p.ld, p.T, tid);
+  stage_seq<false, NKT, 512>(Vr, base + 2 * p.H * D, p.ld, p.T, tid);
+  __syncthreads();
+  const int nkt = (p.T + 15) >> 4;
+  for (int qs = wave; qs < nkt; qs += 8) {
+    const int qrow = qs * 16 + (lane & 15);
+    const bool qok = qrow < p.T;
+    const int qr = qok ? qrow : 0;
+    bf16x8 qf[2], of[2];
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      u32x4 a = {0, 0, 0, 0}, c = {0, 0, 0, 0};
+      if (qok) {
+        a = *reinterpret_cast<const u32x4*>(base + (long)qrow * p.ld + 32 * kk + 8 * g);
+        c = *reinterpret_cast<const u32x4*>(dOg + (long)qrow * p.ldo + 32 * kk + 8 * g);
+      }
+      qf[kk] = __builtin_bit_cast(bf16x8, a);
+      of[kk] = __builtin_bit_cast(bf16x8, c);
+    }
+    const float delta = row_delta(dOg + (long)qr * p.ldo, Og + (long)qr * p.ldo, g);
+    const float lq = qok ? p.lse[(long)bh * p.T + qrow] : 0.f;
+    f32x4 dq[4];
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt) dq[dt] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int kp = 0; 2 * kp < nkt; ++kp) {
+      f32x4 dsp[2];
+#pragma unroll
+      for (int h2 = 0; h2 < 2; ++h2) {
+        const int t = 2 * kp + h2;
+        f32x4 sv = f32x4{0.f, 0.f, 0.f, 0.f}, dpv = f32x4{0.f, 0.f, 0.f, 0.f};
+        if (t < nkt) {
+#pragma unroll
+          for (int kk = 0; kk < 2; ++kk) {
+            sv = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ld_row_frag(Kr, 16 * t + (lane & 15), 4 * kk + g), qf[kk],
+                                                         sv, 0, 0, 0);
+            dpv = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ld_row_frag(Vr, 16 * t + (lane & 15), 4 * kk + g), of[kk],
+                                                          dpv, 0, 0, 0);
+          }
+        }
+        // sv[r] = S[key = 16t + 4g + r][q = qrow]
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int k = 16 * t + 4 * g + r;
+          float ds = 0.f;
+          if (k < p.T && qok) ds = exp2f(sv[r] * p.c - lq) * (dpv[r] - delta);
+          sv[r] = ds;
+        }
+        dsp[h2] = sv;
+      }
+      const bf16x8 sf = pack_p(dsp[0], dsp[1]);
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt)
+        dq[dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(tr_frag2(Kt, 32 * kp, 32 * kp + 16, 16 * dt, lane), sf,
+                                                         dq[dt], 0, 0, 0);
+    }
+    if (qok) {
+      u16* drow = p.dqkv + ((long)b * p.T + qrow) * p.ld + h * D;
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt) {
+        uint2 w;
+        w.x = pack2bf(dq[dt][0] * p.scale, dq[dt][1] * p.scale);
+        w.y = pack2bf(dq[dt][2] * p.scale, dq[dt][3] * p.scale);
+        *reinterpret_cast<uint2*>(drow + 16 * dt + 4 * g) = w;
+      }
+    }
+  }
+}
+
 }  // namespace
+
+// whole-sequence kernel instantiation for T <= 256 (16-row subtiles)
+static int seq_nkt(int T) {
+  const int n = (T + 15) / 16;
+  if (n <= 4) return 4;
+  if (n <= 8) return 8;
+  if (n <= 13) return 13;  // ViT-B/16 @ 224: 197 tokens
+  if (n <= 16) return 16;
+  return 0;
+}
+
+static int attn_seq_disabled() {
+  static int v = -1;
+  if (v < 0) {
+    const char* e = getenv("PDT_ATTN_TILED");
+    v = (e && e[0] == '1') ? 1 : 0;
+  }
+  return v;
+}
 
 PDT_API int pdt_attn_fwd(const void* qkv, void* out, float* lse, int B, int T, int H, float scale, hipStream_t st) {
   AttnParams p;
@@ -426,6 +772,17 @@ PDT_API int pdt_attn_fwd(const void* qkv, void* out, float* lse, int B, int T, i
   p.ld = 3L * H * D;
   p.ldo = (long)H * D;
   p.c = scale * 1.4426950408889634f;
+  const int nkt = attn_seq_disabled() ? 0 : seq_nkt(T);
+  if (nkt) {
+    dim3 g(B * H);
+    switch (nkt) {
+      case 4: hipLaunchKernelGGL(attn_fwd_seq_kernel<4>, g, dim3(256), 0, st, p); break;
+      case 8: hipLaunchKernelGGL(attn_fwd_seq_kernel<8>, g, dim3(256), 0, st, p); break;
+      case 13: hipLaunchKernelGGL(attn_fwd_seq_kernel<13>, g, dim3(256), 0, st, p); break;
+      default: hipLaunchKernelGGL(attn_fwd_seq_kernel<16>, g, dim3(256), 0, st, p); break;
+    }
+    PDT_RETURN_LAUNCH();
+  }
   dim3 grid((T + TILE - 1) / TILE, B * H);
   hipLaunchKernelGGL(attn_fwd_kernel, grid, dim3(256), 0, st, p);
   PDT_RETURN_LAUNCH();
@@ -433,6 +790,32 @@ PDT_API int pdt_attn_fwd(const void* qkv, void* out, float* lse, int B, int T, i
 
 PDT_API int pdt_attn_bwd(const void* qkv, const void* out, const void* dout, const float* lse, float* delta,
                          void* dqkv, int B, int T, int H, float scale, hipStream_t st) {
+  const int nkt = attn_seq_disabled() ? 0 : seq_nkt(T);
+  if (nkt) {
+    AttnSeqBwdParams q;
+    q.qkv = (const u16*)qkv;
+    q.out = (const u16*)out;
+    q.dout = (const u16*)dout;
+    q.lse = lse;
+    q.dqkv = (u16*)dqkv;
+    q.B = B; q.T = T; q.H = H;
+    q.ld = 3L * H * D;
+    q.ldo = (long)H * D;
+    q.c = scale * 1.4426950408889634f;
+    q.scale = scale;
+    dim3 g(B * H);
+#define SEQ_BWD(N)                                                                \
+  hipLaunchKernelGGL(attn_bwd_dkdv_seq_kernel<N>, g, dim3(512), 0, st, q);        \
+  hipLaunchKernelGGL(attn_bwd_dq_seq_kernel<N>, g, dim3(512), 0, st, q)
+    switch (nkt) {
+      case 4: SEQ_BWD(4); break;
+      case 8: SEQ_BWD(8); break;
+      case 13: SEQ_BWD(13); break;
+      default: SEQ_BWD(16); break;
+    }
+#undef SEQ_BWD
+    PDT_RETURN_LAUNCH();
+  }
   const long rows = (long)B * T * H;
   hipLaunchKernelGGL(attn_delta_kernel, dim3((unsigned)((rows * 8 + 255) / 256)), dim3(256), 0, st, (const u16*)dout,
                      (const u16*)out, delta, B, T, H, (long)H * D);

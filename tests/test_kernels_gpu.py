@@ -406,7 +406,7 @@ def test_vit_native_train_step():
     assert all(p.grad is not None and torch.isfinite(p.grad).all() for p in m.parameters() if p.requires_grad)
 
 
-@pytest.mark.parametrize("B,T,H", [(3, 197, 4), (2, 64, 2), (1, 50, 12), (2, 300, 3)])
+@pytest.mark.parametrize("B,T,H", [(3, 197, 4), (2, 64, 2), (1, 50, 12), (2, 300, 3), (1, 256, 2), (2, 16, 3), (1, 120, 2)])
 def test_fused_qkv_attention(B, T, H):
     """Fused MFMA attention (fwd + recomputing bwd) vs an fp32 softmax reference."""
     torch.manual_seed(B * 1000 + T)
