@@ -290,7 +290,7 @@ def _check_nt(src, b, out, a):
 def select_nt_variant(src, b, out, *, with_stats=False, bias=None, act=0, **a):
     """Variant id for this geometry (tuning it on first use when allowed)."""
     M = a["Nimg"] * a["Hm"] * a["Wm"]
-    key = "nt3:" + ",".join(str(a[k]) for k in ("Hs", "Ws", "Cs", "Nimg", "Hm", "Wm", "Ncol", "K", "sh", "sw",
+    key = "nt4:" + ",".join(str(a[k]) for k in ("Hs", "Ws", "Cs", "Nimg", "Hm", "Wm", "Ncol", "K", "sh", "sw",
                                                  "nth", "ntw", "osh")) + f",{int(with_stats)},{int(bias is not None)}"
     table = _tuned()
     if key in table:
@@ -837,6 +837,86 @@ def global_avg_pool(x):
 # =============================================================================
 # linear (bf16 MFMA GEMM with bias / relu epilogue)
 # =============================================================================
+# -----------------------------------------------------------------------------
+# Plain-GEMM backward of nn.Linear: dX = dY W (NN) and dW = dY^T X (TN). These
+# carry no fused epilogue, so per shape the first call times the native kernels
+# (conv_nt on a transposed bf16 W; the split-K wgrad kernel) against the
+# library GEMM (hipBLASLt through torch.mm, fp32-output for dW) and keeps the
+# faster one ("lg:" keys in the tuned table; PDT_LIB_GEMM=0 forces native).
+# -----------------------------------------------------------------------------
+def _lib_gemm_allowed() -> bool:
+    return os.environ.get("PDT_LIB_GEMM", "1") != "0"
+
+
+def _linear_dgrad_native(dy2, w):
+    Nout, K = w.shape
+    Mrows = dy2.shape[0]
+    wt = torch.empty((K, Nout), dtype=torch.bfloat16, device=dy2.device)
+    _chk(_load().pdt_transpose_cast(_p(w.detach().float().contiguous()), _p(wt), Nout, K, _s()), "transpose")
+    dx = torch.empty((Mrows, K), dtype=torch.bfloat16, device=dy2.device)
+    conv_nt(dy2, wt, dx, Hs=1, Ws=1, Cs=Nout, Nimg=Mrows, Hm=1, Wm=1, Ncol=K, K=Nout, ldb=Nout, sh=1, sw=1,
+            oh0=0, ow0=0, dh=1, dw=1, nth=1, ntw=1, Ho=1, Wo=1, osh=1, osw=1, oph=0, opw=0, ldo=K)
+    return dx
+
+
+def _linear_dgrad_lib(dy2, w):
+    return torch.mm(dy2, bf16_weight(w))
+
+
+def _linear_wgrad_native(dy2, x2, w):
+    Nout, K = w.shape
+    dw = torch.empty((Nout, K), dtype=torch.float32, device=dy2.device)
+    conv_wgrad(dy2, x2, dw, M=dy2.shape[0], Mo=Nout, No=K, ldy=Nout, Hs=1, Ws=1, C=K, Hm=1, Wm=1, sh=1, sw=1,
+               oh0=0, ow0=0, dh=1, dw=1, ntw=1)
+    return dw
+
+
+def _linear_wgrad_lib(dy2, x2, w):
+    return torch.mm(dy2.t(), x2, out_dtype=torch.float32)
+
+
+def _pick_impl(key, native, library):
+    """'native' or 'lib' for this GEMM shape, timed once (both produce the same result)."""
+    table = _tuned()
+    if key in table:
+        return table[key]
+    if not (_lib_gemm_allowed() and _tune_allowed()):
+        return "native"
+    native()  # warm: also runs the native kernels' own variant tuning
+    library()
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    times = {}
+    for name, fn in (("native", native), ("lib", library)):
+        t = float("inf")
+        for _ in range(2):
+            ev0.record()
+            for _ in range(3):
+                fn()
+            ev1.record()
+            ev1.synchronize()
+            t = min(t, ev0.elapsed_time(ev1))
+        times[name] = t
+    table[key] = min(times, key=times.get)
+    _save_tuned()
+    return table[key]
+
+
+def _linear_dgrad(dy2, w):
+    Nout, K = w.shape
+    key = f"lgd:{dy2.shape[0]},{Nout},{K}"
+    impl = _pick_impl(key, lambda: _linear_dgrad_native(dy2, w), lambda: _linear_dgrad_lib(dy2, w)) \
+        if _lib_gemm_allowed() else "native"
+    return _linear_dgrad_lib(dy2, w) if impl == "lib" else _linear_dgrad_native(dy2, w)
+
+
+def _linear_wgrad(dy2, x2, w):
+    Nout, K = w.shape
+    key = f"lgw:{dy2.shape[0]},{Nout},{K}"
+    impl = _pick_impl(key, lambda: _linear_wgrad_native(dy2, x2, w), lambda: _linear_wgrad_lib(dy2, x2, w)) \
+        if _lib_gemm_allowed() else "native"
+    return _linear_wgrad_lib(dy2, x2, w) if impl == "lib" else _linear_wgrad_native(dy2, x2, w)
+
+
 class _Linear(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, w, b, act):
@@ -870,19 +950,8 @@ class _Linear(torch.autograd.Function):
             _chk(lib.pdt_gelu_bwd(_p(dy2), _p(saved), _p(dz), dz.numel(), st), "gelu_bwd")
             dy2 = dz
         Mrows = dy2.shape[0]
-        dx = None
-        if ctx.needs_input_grad[0]:
-            wt = torch.empty((K, Nout), dtype=torch.bfloat16, device=dy.device)
-            _chk(lib.pdt_transpose_cast(_p(w.detach().float().contiguous()), _p(wt), Nout, K, st), "transpose")
-            dx = torch.empty((Mrows, K), dtype=torch.bfloat16, device=dy.device)
-            conv_nt(dy2, wt, dx, Hs=1, Ws=1, Cs=Nout, Nimg=Mrows, Hm=1, Wm=1, Ncol=K, K=Nout, ldb=Nout, sh=1, sw=1,
-                    oh0=0, ow0=0, dh=1, dw=1, nth=1, ntw=1, Ho=1, Wo=1, osh=1, osw=1, oph=0, opw=0, ldo=K)
-            dx = dx.reshape(*shp[:-1], K)
-        dw = None
-        if ctx.needs_input_grad[1]:
-            dw = torch.empty((Nout, K), dtype=torch.float32, device=dy.device)
-            conv_wgrad(dy2, x2, dw, M=Mrows, Mo=Nout, No=K, ldy=Nout, Hs=1, Ws=1, C=K, Hm=1, Wm=1, sh=1, sw=1,
-                       oh0=0, ow0=0, dh=1, dw=1, ntw=1)
+        dx = _linear_dgrad(dy2, w).reshape(*shp[:-1], K) if ctx.needs_input_grad[0] else None
+        dw = _linear_wgrad(dy2, x2, w) if ctx.needs_input_grad[1] else None
         db = None
         if has_b and ctx.needs_input_grad[2]:
             db = colsum(dy2, Mrows, Nout)
@@ -948,7 +1017,7 @@ def gemm_f8(a, b, out, dq_a, dq_b, *, fmt_a=E4M3, bias=None, act=0, aux=None, va
     args = lambda v: (_p(a), _p(b), _p(out), _p(bias), _p(dq_a), _p(dq_b), M, N, K, K, K, N, fmt_a, act,  # noqa
                       _p(aux), v, _s())
     if variant is None:
-        key = f"f8:{M},{N},{K},{fmt_a},{act},{int(bias is not None)}"
+        key = f"f8b:{M},{N},{K},{fmt_a},{act},{int(bias is not None)}"
         variant = _autotune(key, lib.pdt_gemm_f8_num_variants(), lambda v: lib.pdt_gemm_f8(*args(v)))
     _chk(lib.pdt_gemm_f8(*args(variant)), "gemm_f8")
     return out
@@ -969,6 +1038,9 @@ class _LinearF8(torch.autograd.Function):
         gemm_f8(xq, wq, y, dqx, dqw, bias=bias, act=ACT[act], aux=z)
         ctx.save_for_backward(x2, w, y if act == "relu" else z)
         ctx.meta = (shp, act, b is not None)
+        # e5m2 data-gradient GEMM only on request: its dY quantisation pass costs
+        # about what the fp8 GEMM saves over the bf16 one (PDT_FP8_DGRAD=1)
+        ctx.fp8_dgrad = os.environ.get("PDT_FP8_DGRAD", "0") == "1"
         return y.reshape(*shp[:-1], Nout)
 
     @staticmethod
@@ -987,16 +1059,15 @@ class _LinearF8(torch.autograd.Function):
         Mrows = dy2.shape[0]
         dx = None
         if ctx.needs_input_grad[0]:
-            dyq, dqdy = quantize_fp8(dy2, E5M2)
-            _, wqt, dqw = fp8_weight(w)
-            dx = torch.empty((Mrows, K), dtype=torch.bfloat16, device=dy.device)
-            gemm_f8(dyq, wqt, dx, dqdy, dqw, fmt_a=E5M2)
+            if ctx.fp8_dgrad:
+                dyq, dqdy = quantize_fp8(dy2, E5M2)
+                _, wqt, dqw = fp8_weight(w)
+                dx = torch.empty((Mrows, K), dtype=torch.bfloat16, device=dy.device)
+                gemm_f8(dyq, wqt, dx, dqdy, dqw, fmt_a=E5M2)
+            else:
+                dx = _linear_dgrad(dy2, w)
             dx = dx.reshape(*shp[:-1], K)
-        dw = None
-        if ctx.needs_input_grad[1]:
-            dw = torch.empty((Nout, K), dtype=torch.float32, device=dy.device)
-            conv_wgrad(dy2, x2, dw, M=Mrows, Mo=Nout, No=K, ldy=Nout, Hs=1, Ws=1, C=K, Hm=1, Wm=1, sh=1, sw=1,
-                       oh0=0, ow0=0, dh=1, dw=1, ntw=1)
+        dw = _linear_wgrad(dy2, x2, w) if ctx.needs_input_grad[1] else None
         db = None
         if has_b and ctx.needs_input_grad[2]:
             db = colsum(dy2, Mrows, Nout)
