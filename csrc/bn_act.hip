@@ -130,35 +130,124 @@ __device__ __forceinline__ void sum_rows64(const float* __restrict__ part, int R
   q = sh_q[cl] + sh_q[64 + cl] + sh_q[128 + cl] + sh_q[192 + cl];
 }
 
+struct FwdFin {
+  double count;
+  float eps, momentum;
+  const float* gamma;
+  const float* beta;
+  float *mean_out, *invstd_out, *scale, *shift, *running_mean, *running_var;
+  long* nbt;
+};
+
+struct BwdFin {
+  double count;
+  const float *gamma, *mean, *invstd;
+  float *dgamma, *dbeta, *k1, *k2, *k3;
+  int accumulate;
+};
+
 // outputs: mean, invstd (saved for backward), scale = gamma*invstd, shift = beta - mean*scale,
 // running stats updated in place (unbiased variance) and num_batches_tracked += 1.
-__global__ void __launch_bounds__(256) bn_finalize_kernel(const float* __restrict__ part, int R, int C,
-                                                          double count, float eps, float momentum,
-                                                          const float* __restrict__ gamma,
-                                                          const float* __restrict__ beta, float* __restrict__ mean_out,
-                                                          float* __restrict__ invstd_out, float* __restrict__ scale,
-                                                          float* __restrict__ shift, float* __restrict__ running_mean,
-                                                          float* __restrict__ running_var, long* __restrict__ nbt) {
+__device__ __forceinline__ void fwd_finalize_channel(const FwdFin& f, int c, double s, double q) {
+  const double count = f.count;
+  const float momentum = f.momentum;
+  const float* gamma = f.gamma;
+  const float* beta = f.beta;
+  double mean = s / count;
+  double var = q / count - mean * mean;
+  if (var < 0) var = 0;
+  float invstd = (float)(1.0 / sqrt(var + (double)f.eps));
+  float g = gamma ? gamma[c] : 1.f, b = beta ? beta[c] : 0.f;
+  f.mean_out[c] = (float)mean;
+  f.invstd_out[c] = invstd;
+  f.scale[c] = g * invstd;
+  f.shift[c] = b - (float)mean * g * invstd;
+  if (f.running_mean) {
+    double unb = count > 1 ? var * count / (count - 1) : var;
+    f.running_mean[c] = (1.f - momentum) * f.running_mean[c] + momentum * (float)mean;
+    f.running_var[c] = (1.f - momentum) * f.running_var[c] + momentum * (float)unb;
+  }
+}
+
+// dgamma = sum(dz*(y-mean))*invstd, dbeta = sum(dz); dy = k1*dz + k2*y + k3
+__device__ __forceinline__ void bwd_finalize_channel(const BwdFin& f, int c, double s, double q) {
+  double is = f.invstd[c], g = f.gamma ? f.gamma[c] : 1.0, mu = f.mean[c];
+  double dg = q * is, db = s;
+  if (f.dgamma) f.dgamma[c] = (float)(f.accumulate ? f.dgamma[c] + dg : dg);
+  if (f.dbeta) f.dbeta[c] = (float)(f.accumulate ? f.dbeta[c] + db : db);
+  double a1 = g * is;
+  double a2 = -g * is * is * is * q / f.count;
+  double a3 = -g * is * s / f.count - a2 * mu;
+  f.k1[c] = (float)a1;
+  f.k2[c] = (float)a2;
+  f.k3[c] = (float)a3;
+}
+
+__global__ void __launch_bounds__(256) bn_finalize_kernel(const float* __restrict__ part, int R, int C, FwdFin f) {
   __shared__ double sh_s[256], sh_q[256];
   const int c = blockIdx.x * 64 + (threadIdx.x & 63), rg = threadIdx.x >> 6;
   double s, q;
   sum_rows64(part, R, C, c, rg, sh_s, sh_q, s, q);
-  if (blockIdx.x == 0 && threadIdx.x == 0 && nbt) nbt[0] += 1;
+  if (blockIdx.x == 0 && threadIdx.x == 0 && f.nbt) f.nbt[0] += 1;
   if (rg != 0 || c >= C) return;
-  double mean = s / count;
-  double var = q / count - mean * mean;
-  if (var < 0) var = 0;
-  float invstd = (float)(1.0 / sqrt(var + (double)eps));
-  float g = gamma ? gamma[c] : 1.f, b = beta ? beta[c] : 0.f;
-  mean_out[c] = (float)mean;
-  invstd_out[c] = invstd;
-  scale[c] = g * invstd;
-  shift[c] = b - (float)mean * g * invstd;
-  if (running_mean) {
-    double unb = count > 1 ? var * count / (count - 1) : var;
-    running_mean[c] = (1.f - momentum) * running_mean[c] + momentum * (float)mean;
-    running_var[c] = (1.f - momentum) * running_var[c] + momentum * (float)unb;
+  fwd_finalize_channel(f, c, s, q);
+}
+
+__global__ void __launch_bounds__(256) bn_bwd_finalize_kernel(const float* __restrict__ part, int R, int C, BwdFin f) {
+  __shared__ double sh_s[256], sh_q[256];
+  const int c = blockIdx.x * 64 + (threadIdx.x & 63), rg = threadIdx.x >> 6;
+  double s, q;
+  sum_rows64(part, R, C, c, rg, sh_s, sh_q, s, q);
+  if (rg != 0 || c >= C) return;
+  bwd_finalize_channel(f, c, s, q);
+}
+
+// Arrival counters of the fused reduce+finalize (one per 64-channel block):
+// zero at load, reset by the block that consumes them. Launches on one stream
+// are serialised, so consecutive BatchNorms reuse them.
+__device__ unsigned int pdt_bn_arrivals[64];
+
+// rows_reduce (stage 1 of the partial-row reduction, [2][R][C] -> [2][G][C])
+// whose LAST-arriving block per channel block runs the finalize for those 64
+// channels over the G fresh rows (fixed order -> deterministic): one launch
+// instead of two per BatchNorm.
+template <bool BWD>
+__global__ void __launch_bounds__(256) rows_reduce_fin_kernel(const float* __restrict__ part,
+                                                              float* __restrict__ out, int R, int C, int G,
+                                                              FwdFin ff, BwdFin bf) {
+  __shared__ float red[2][4][64];
+  __shared__ double sh_s[256], sh_q[256];
+  __shared__ unsigned int is_last;
+  const int t = threadIdx.x, cl = t & 63, rg = t >> 6;
+  const int c = blockIdx.x * 64 + cl;
+  const int g = blockIdx.y;
+  float s = 0.f, q = 0.f;
+  if (c < C) {
+    for (int r = g * 4 + rg; r < R; r += 4 * G) {
+      s += part[(long)r * C + c];
+      q += part[(long)(R + r) * C + c];
+    }
   }
+  red[0][rg][cl] = s;
+  red[1][rg][cl] = q;
+  __syncthreads();
+  if (rg == 0 && c < C) {
+    out[(long)g * C + c] = red[0][0][cl] + red[0][1][cl] + red[0][2][cl] + red[0][3][cl];
+    out[(long)(G + g) * C + c] = red[1][0][cl] + red[1][1][cl] + red[1][2][cl] + red[1][3][cl];
+  }
+  __threadfence();  // this block's rows are visible device-wide before it is counted
+  __syncthreads();
+  if (t == 0) is_last = atomicAdd(&pdt_bn_arrivals[blockIdx.x], 1u) == (unsigned)(G - 1) ? 1u : 0u;
+  __syncthreads();
+  if (!is_last) return;
+  __threadfence();  // acquire: see every other block's rows
+  double ds, dq;
+  sum_rows64(out, G, C, c, rg, sh_s, sh_q, ds, dq);
+  if (t == 0) pdt_bn_arrivals[blockIdx.x] = 0u;
+  if (!BWD && blockIdx.x == 0 && t == 0 && ff.nbt) ff.nbt[0] += 1;
+  if (rg != 0 || c >= C) return;
+  if (BWD) bwd_finalize_channel(bf, c, ds, dq);
+  else fwd_finalize_channel(ff, c, ds, dq);
 }
 
 // -------------------------------------------------------------------- apply
@@ -278,32 +367,6 @@ __global__ void __launch_bounds__(NT) bn_bwd_reduce_kernel(const u16* __restrict
   }
 }
 
-// dgamma = sum(dz*(y-mean))*invstd, dbeta = sum(dz)
-// dy = k1*dz + k2*y + k3
-__global__ void __launch_bounds__(256) bn_bwd_finalize_kernel(const float* __restrict__ part, int R, int C,
-                                                              double count, const float* __restrict__ gamma,
-                                                              const float* __restrict__ mean,
-                                                              const float* __restrict__ invstd,
-                                                              float* __restrict__ dgamma, float* __restrict__ dbeta,
-                                                              float* __restrict__ k1, float* __restrict__ k2,
-                                                              float* __restrict__ k3, int accumulate) {
-  __shared__ double sh_s[256], sh_q[256];
-  const int c = blockIdx.x * 64 + (threadIdx.x & 63), rg = threadIdx.x >> 6;
-  double s, q;
-  sum_rows64(part, R, C, c, rg, sh_s, sh_q, s, q);
-  if (rg != 0 || c >= C) return;
-  double is = invstd[c], g = gamma ? gamma[c] : 1.0, mu = mean[c];
-  double dg = q * is, db = s;
-  if (dgamma) dgamma[c] = (float)(accumulate ? dgamma[c] + dg : dg);
-  if (dbeta) dbeta[c] = (float)(accumulate ? dbeta[c] + db : db);
-  double a1 = g * is;
-  double a2 = -g * is * is * is * q / count;
-  double a3 = -g * is * s / count - a2 * mu;
-  k1[c] = (float)a1;
-  k2[c] = (float)a2;
-  k3[c] = (float)a3;
-}
-
 template <bool RELU, bool USE_ACT, bool DRES, bool USE_MASK = false>
 __global__ void __launch_bounds__(NT) bn_bwd_apply_kernel(const u16* __restrict__ dA, const u16* __restrict__ y,
                                                           const u16* __restrict__ act,
@@ -385,22 +448,22 @@ PDT_API long pdt_rows_reduce_workspace(int R, int C) {
   return G ? 2L * G * C : 0;
 }
 
-static const float* rows_reduce(const float* part, int* R, int C, hipStream_t st) {
-  if (*R <= 256) return part;
-  const int G = 64;
-  float* out = const_cast<float*>(part) + 2L * (*R) * C;  // workspace tail
-  hipLaunchKernelGGL(rows_reduce_kernel, dim3((C + 63) / 64, G), dim3(256), 0, st, part, out, *R, C, G);
-  *R = G;
-  return out;
-}
 
 PDT_API int pdt_bn_finalize(const float* part, int R, int C, double count, float eps, float momentum,
                             const float* gamma, const float* beta, float* mean, float* invstd, float* scale,
                             float* shift, float* running_mean, float* running_var, long* num_batches_tracked,
                             hipStream_t st) {
-  part = rows_reduce(part, &R, C, st);
-  hipLaunchKernelGGL(bn_finalize_kernel, dim3((C + 63) / 64), dim3(256), 0, st, part, R, C, count, eps, momentum,
-                     gamma, beta, mean, invstd, scale, shift, running_mean, running_var, num_batches_tracked);
+  FwdFin f{count, eps, momentum, gamma, beta, mean, invstd, scale, shift, running_mean, running_var,
+           num_batches_tracked};
+  if (R > 256) {
+    if ((C + 63) / 64 > 64) return -1;
+    const int G = 64;
+    float* out = const_cast<float*>(part) + 2L * R * C;  // workspace tail
+    hipLaunchKernelGGL(rows_reduce_fin_kernel<false>, dim3((C + 63) / 64, G), dim3(256), 0, st, part, out, R, C, G,
+                       f, BwdFin{});
+    PDT_RETURN_LAUNCH();
+  }
+  hipLaunchKernelGGL(bn_finalize_kernel, dim3((C + 63) / 64), dim3(256), 0, st, part, R, C, f);
   PDT_RETURN_LAUNCH();
 }
 
@@ -449,9 +512,16 @@ PDT_API int pdt_bn_bwd_reduce(const void* dA, const void* y, const void* act, co
 PDT_API int pdt_bn_bwd_finalize(const float* part, int R, int C, double count, const float* gamma,
                                 const float* mean, const float* invstd, float* dgamma, float* dbeta, float* k1,
                                 float* k2, float* k3, int accumulate, hipStream_t st) {
-  part = rows_reduce(part, &R, C, st);
-  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + 63) / 64), dim3(256), 0, st, part, R, C, count, gamma,
-                     mean, invstd, dgamma, dbeta, k1, k2, k3, accumulate);
+  BwdFin f{count, gamma, mean, invstd, dgamma, dbeta, k1, k2, k3, accumulate};
+  if (R > 256) {
+    if ((C + 63) / 64 > 64) return -1;
+    const int G = 64;
+    float* out = const_cast<float*>(part) + 2L * R * C;
+    hipLaunchKernelGGL(rows_reduce_fin_kernel<true>, dim3((C + 63) / 64, G), dim3(256), 0, st, part, out, R, C, G,
+                       FwdFin{}, f);
+    PDT_RETURN_LAUNCH();
+  }
+  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + 63) / 64), dim3(256), 0, st, part, R, C, f);
   PDT_RETURN_LAUNCH();
 }
 
