@@ -139,6 +139,74 @@ __global__ void __launch_bounds__(256) cast_fp8_t_kernel(const float* __restrict
   }
 }
 
+// ---------------------------------------------------------------------------
+// Delayed scaling (one pass): quantize with the scale derived from an amax
+// history, record this tensor's amax for the next steps. Per-tensor state
+// (fp32 words):
+//   [0] scale in use         [1] dq of the LAST cast (1/scale, read by the GEMM)
+//   [2] amax of this cast    (uint bits, atomicMax; non-negative floats order as uints)
+//   [3] arrival counter      [4] history index     [5 .. 5+H) amax history
+// The last-arriving block rolls the history, sets the next scale and resets [2]/[3].
+constexpr int HIST = 16;
+
+template <bool BF16, int FMT>
+__global__ void __launch_bounds__(256) cast_fp8_delayed_kernel(const void* __restrict__ x, long n,
+                                                               float* __restrict__ meta, uint8_t* __restrict__ q) {
+  __shared__ float red[4];
+  __shared__ unsigned int last;
+  const float s = meta[0];
+  float m = 0.f;
+  const long stride = (long)gridDim.x * 256 * 8;
+  for (long base = ((long)blockIdx.x * 256 + threadIdx.x) * 8; base < n; base += stride) {
+    float v[8];
+    if (BF16 && base + 8 <= n) {
+      const u32x4 w = *reinterpret_cast<const u32x4*>(reinterpret_cast<const u16*>(x) + base);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        v[2 * e] = lo_bf(w[e]);
+        v[2 * e + 1] = hi_bf(w[e]);
+      }
+    } else {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] = base + e < n ? ld<BF16>(x, base + e) : 0.f;
+    }
+#pragma unroll
+    for (int e = 0; e < 8; ++e) m = fmaxf(m, fabsf(v[e]));
+    if (base + 8 <= n) {
+      uint2 o;
+      o.x = cvt4<FMT>(v[0] * s, v[1] * s, v[2] * s, v[3] * s);
+      o.y = cvt4<FMT>(v[4] * s, v[5] * s, v[6] * s, v[7] * s);
+      *reinterpret_cast<uint2*>(q + base) = o;
+    } else {
+      for (long i = base; i < n; ++i) q[i] = (uint8_t)(cvt4<FMT>(v[i - base] * s, 0.f, 0.f, 0.f) & 0xff);
+    }
+  }
+  m = warp_max(m);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = m;
+  __syncthreads();
+  unsigned int* mu = reinterpret_cast<unsigned int*>(meta);
+  if (threadIdx.x == 0) {
+    const float bm = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
+    atomicMax(mu + 2, __float_as_uint(bm));
+    __threadfence();
+    last = atomicAdd(mu + 3, 1u) == gridDim.x - 1 ? 1u : 0u;
+  }
+  __syncthreads();
+  if (last && threadIdx.x == 0) {
+    __threadfence();
+    const float cur = __uint_as_float(atomicAdd(mu + 2, 0u));
+    const int idx = (int)mu[4];
+    meta[5 + idx % HIST] = cur;
+    mu[4] = (unsigned)(idx + 1);
+    float h = 0.f;
+    for (int i = 0; i < HIST; ++i) h = fmaxf(h, meta[5 + i]);
+    meta[1] = 1.f / s;
+    meta[0] = scale_from<FMT>(h);
+    mu[2] = 0u;
+    mu[3] = 0u;
+  }
+}
+
 int nblocks(long n) {
   long b = (n + 256 * 8 - 1) / (256 * 8);
   if (b > AMAX_BLOCKS) b = AMAX_BLOCKS;
@@ -178,5 +246,43 @@ PDT_API int pdt_cast_fp8_t(const float* x, int R, int C, const float* partial, v
   const int nb = nblocks((long)R * C);
   dim3 grid((C + 63) / 64, (R + 63) / 64);
   hipLaunchKernelGGL(cast_fp8_t_kernel<0>, grid, dim3(256), 0, st, x, R, C, partial, nb, (uint8_t*)q);
+  PDT_RETURN_LAUNCH();
+}
+
+PDT_API int pdt_fp8_meta_words() { return 5 + HIST; }
+
+// one-pass delayed-scaling cast; meta must be initialised by pdt_fp8_meta_seed
+PDT_API int pdt_cast_fp8_delayed(const void* x, int bf16, long n, float* meta, int fmt, void* q, hipStream_t st) {
+  const int nb = nblocks(n);
+  uint8_t* qo = (uint8_t*)q;
+#define CD(B_, F_) hipLaunchKernelGGL((cast_fp8_delayed_kernel<B_, F_>), dim3(nb), dim3(256), 0, st, x, n, meta, qo)
+  if (bf16) { if (fmt == 0) CD(true, 0); else CD(true, 1); }
+  else { if (fmt == 0) CD(false, 0); else CD(false, 1); }
+#undef CD
+  PDT_RETURN_LAUNCH();
+}
+
+namespace {
+template <int FMT>
+__global__ void fp8_meta_seed_kernel(const float* __restrict__ partial, int nblk, float* __restrict__ meta) {
+  const float a = block_amax(partial, nblk);
+  if (threadIdx.x == 0) {
+    unsigned int* mu = reinterpret_cast<unsigned int*>(meta);
+    for (int i = 0; i < HIST; ++i) meta[5 + i] = 0.f;
+    meta[5] = a;
+    mu[4] = 1u;
+    mu[2] = 0u;
+    mu[3] = 0u;
+    meta[0] = scale_from<FMT>(a);
+    meta[1] = 1.f / meta[0];
+  }
+}
+}  // namespace
+
+// seed the history with the exact amax of a first tensor (from pdt_amax_partial)
+PDT_API int pdt_fp8_meta_seed(const float* partial, long n, int fmt, float* meta, hipStream_t st) {
+  const int nb = nblocks(n);
+  if (fmt == 0) hipLaunchKernelGGL(fp8_meta_seed_kernel<0>, dim3(1), dim3(256), 0, st, partial, nb, meta);
+  else hipLaunchKernelGGL(fp8_meta_seed_kernel<1>, dim3(1), dim3(256), 0, st, partial, nb, meta);
   PDT_RETURN_LAUNCH();
 }

@@ -74,6 +74,9 @@ _SIGS = {
     "pdt_amax_partial": (c_int, [P, c_int, c_long, P, P]),
     "pdt_cast_fp8": (c_int, [P, c_int, c_long, P, c_int, P, P, P]),
     "pdt_cast_fp8_t": (c_int, [P, c_int, c_int, P, P, P]),
+    "pdt_fp8_meta_words": (c_int, []),
+    "pdt_cast_fp8_delayed": (c_int, [P, c_int, c_long, P, c_int, P, P]),
+    "pdt_fp8_meta_seed": (c_int, [P, c_long, c_int, P, P]),
     "pdt_attn_bwd": (c_int, [P, P, P, P, P, P, c_int, c_int, c_int, c_float, P]),
 }
 
@@ -983,6 +986,26 @@ def quantize_fp8(x: torch.Tensor, fmt: int = E4M3):
     return q, dq
 
 
+def quantize_fp8_delayed(x: torch.Tensor, meta: torch.Tensor | None, fmt: int = E4M3):
+    """One-pass cast with delayed (amax-history) scaling; returns (q, dq, meta).
+
+    ``meta`` is the tensor's scaling state (csrc/fp8.hip: scale, dq, amax,
+    history); pass None on first use -- it is created and seeded with the
+    exact amax of ``x`` (so the first step is current-scaled)."""
+    lib = _load()
+    x = x.contiguous()
+    n = x.numel()
+    bf = int(x.dtype == torch.bfloat16)
+    if meta is None:
+        meta = torch.zeros(lib.pdt_fp8_meta_words(), dtype=torch.float32, device=x.device)
+        part = torch.empty(lib.pdt_amax_blocks(n), dtype=torch.float32, device=x.device)
+        _chk(lib.pdt_amax_partial(_p(x), bf, n, _p(part), _s()), "amax")
+        _chk(lib.pdt_fp8_meta_seed(_p(part), n, fmt, _p(meta), _s()), "fp8_meta_seed")
+    q = torch.empty(x.shape, dtype=torch.uint8, device=x.device)
+    _chk(lib.pdt_cast_fp8_delayed(_p(x), bf, n, _p(meta), fmt, _p(q), _s()), "cast_fp8_delayed")
+    return q, meta[1:2], meta
+
+
 _F8W: dict = {}
 
 
@@ -1025,12 +1048,16 @@ def gemm_f8(a, b, out, dq_a, dq_b, *, fmt_a=E4M3, bias=None, act=0, aux=None, va
 
 class _LinearF8(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, w, b, act):
+    def forward(ctx, x, w, b, act, fc):
         shp = x.shape
         x2 = x.reshape(-1, shp[-1]).to(torch.bfloat16).contiguous()
         Mrows, K = x2.shape
         Nout = w.shape[0]
-        xq, dqx = quantize_fp8(x2, E4M3)
+        if os.environ.get("PDT_FP8_SCALING", "delayed") == "current":
+            xq, dqx = quantize_fp8(x2, E4M3)
+        else:  # delayed scaling: one pass, amax history kept on the module
+            xq, dqx, meta = quantize_fp8_delayed(x2, getattr(fc, "_pdt_fp8_meta", None), E4M3)
+            fc._pdt_fp8_meta = meta
         wq, _, dqw = fp8_weight(w)
         y = torch.empty((Mrows, Nout), dtype=torch.bfloat16, device=x.device)
         z = torch.empty_like(y) if act == "gelu" else None
@@ -1071,7 +1098,7 @@ class _LinearF8(torch.autograd.Function):
         db = None
         if has_b and ctx.needs_input_grad[2]:
             db = colsum(dy2, Mrows, Nout)
-        return dx, dw, db, None
+        return dx, dw, db, None, None
 
 
 def linear(x, fc: nn.Linear, act=None, fp8=False):
@@ -1081,7 +1108,7 @@ def linear(x, fc: nn.Linear, act=None, fp8=False):
         from .fused import _torch_linear
         return _torch_linear(x, fc, act)
     if fp8 and K % 128 == 0 and N % 128 == 0:
-        return _LinearF8.apply(x, fc.weight, fc.bias, act)
+        return _LinearF8.apply(x, fc.weight, fc.bias, act, fc)
     return _Linear.apply(x, fc.weight, fc.bias, act)
 
 

@@ -545,3 +545,22 @@ def test_dgrad_weight_cache_tracks_updates():
         with torch.no_grad():
             for conv in convs:
                 conv.weight.mul_(-1.5)
+
+
+def test_fp8_delayed_scaling_history():
+    """One-pass delayed-scaling cast: seeded exactly, then scales from the amax history."""
+    torch.manual_seed(15)
+    x1 = torch.randn(513, 256, device="cuda").to(torch.bfloat16)
+    q1, dq1, meta = no.quantize_fp8_delayed(x1, None)
+    torch.cuda.synchronize()
+    amax1 = x1.float().abs().max().item()
+    assert abs(dq1.item() - amax1 / 448.0) < 1e-6 * amax1
+    assert nrmerr(_f8(q1, 0) * dq1, x1) < 0.03
+    x2 = x1 * 4  # amax grows: this step saturates at the old scale, the next one adapts
+    q2, dq2, meta = no.quantize_fp8_delayed(x2, meta)
+    torch.cuda.synchronize()
+    assert abs(dq2.item() - amax1 / 448.0) < 1e-6 * amax1  # scale from history (step 1)
+    q3, dq3, meta = no.quantize_fp8_delayed(x2, meta)
+    torch.cuda.synchronize()
+    assert abs(dq3.item() - 4 * amax1 / 448.0) < 1e-5 * amax1
+    assert nrmerr(_f8(q3, 0) * dq3, x2) < 0.03
