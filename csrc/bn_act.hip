@@ -202,54 +202,6 @@ __global__ void __launch_bounds__(256) bn_bwd_finalize_kernel(const float* __res
   bwd_finalize_channel(f, c, s, q);
 }
 
-// Arrival counters of the fused reduce+finalize (one per 64-channel block):
-// zero at load, reset by the block that consumes them. Launches on one stream
-// are serialised, so consecutive BatchNorms reuse them.
-__device__ unsigned int pdt_bn_arrivals[64];
-
-// rows_reduce (stage 1 of the partial-row reduction, [2][R][C] -> [2][G][C])
-// whose LAST-arriving block per channel block runs the finalize for those 64
-// channels over the G fresh rows (fixed order -> deterministic): one launch
-// instead of two per BatchNorm.
-template <bool BWD>
-__global__ void __launch_bounds__(256) rows_reduce_fin_kernel(const float* __restrict__ part,
-                                                              float* __restrict__ out, int R, int C, int G,
-                                                              FwdFin ff, BwdFin bf) {
-  __shared__ float red[2][4][64];
-  __shared__ double sh_s[256], sh_q[256];
-  __shared__ unsigned int is_last;
-  const int t = threadIdx.x, cl = t & 63, rg = t >> 6;
-  const int c = blockIdx.x * 64 + cl;
-  const int g = blockIdx.y;
-  float s = 0.f, q = 0.f;
-  if (c < C) {
-    for (int r = g * 4 + rg; r < R; r += 4 * G) {
-      s += part[(long)r * C + c];
-      q += part[(long)(R + r) * C + c];
-    }
-  }
-  red[0][rg][cl] = s;
-  red[1][rg][cl] = q;
-  __syncthreads();
-  if (rg == 0 && c < C) {
-    out[(long)g * C + c] = red[0][0][cl] + red[0][1][cl] + red[0][2][cl] + red[0][3][cl];
-    out[(long)(G + g) * C + c] = red[1][0][cl] + red[1][1][cl] + red[1][2][cl] + red[1][3][cl];
-  }
-  __threadfence();  // this block's rows are visible device-wide before it is counted
-  __syncthreads();
-  if (t == 0) is_last = atomicAdd(&pdt_bn_arrivals[blockIdx.x], 1u) == (unsigned)(G - 1) ? 1u : 0u;
-  __syncthreads();
-  if (!is_last) return;
-  __threadfence();  // acquire: see every other block's rows
-  double ds, dq;
-  sum_rows64(out, G, C, c, rg, sh_s, sh_q, ds, dq);
-  if (t == 0) pdt_bn_arrivals[blockIdx.x] = 0u;
-  if (!BWD && blockIdx.x == 0 && t == 0 && ff.nbt) ff.nbt[0] += 1;
-  if (rg != 0 || c >= C) return;
-  if (BWD) bwd_finalize_channel(bf, c, ds, dq);
-  else fwd_finalize_channel(ff, c, ds, dq);
-}
-
 // -------------------------------------------------------------------- apply
 // MASK: also write the ReLU mask as one bit per element (byte i = chunk i's 8
 // channels): the backward then reads 1/16 of the bytes instead of `out`.
@@ -449,20 +401,26 @@ PDT_API long pdt_rows_reduce_workspace(int R, int C) {
 }
 
 
+// Stage 1 of the partial-row reduction when R > 256 (a separate launch: a
+// single-launch "last block finalizes" variant needs a device-scope release
+// fence per block, which on the multi-XCD MI355X writes back L2 -- measured
+// ~2.4x slower than the two launches).
+static const float* rows_reduce(const float* part, int* R, int C, hipStream_t st) {
+  if (*R <= 256) return part;
+  const int G = 64;
+  float* out = const_cast<float*>(part) + 2L * (*R) * C;  // workspace tail
+  hipLaunchKernelGGL(rows_reduce_kernel, dim3((C + 63) / 64, G), dim3(256), 0, st, part, out, *R, C, G);
+  *R = G;
+  return out;
+}
+
 PDT_API int pdt_bn_finalize(const float* part, int R, int C, double count, float eps, float momentum,
                             const float* gamma, const float* beta, float* mean, float* invstd, float* scale,
                             float* shift, float* running_mean, float* running_var, long* num_batches_tracked,
                             hipStream_t st) {
   FwdFin f{count, eps, momentum, gamma, beta, mean, invstd, scale, shift, running_mean, running_var,
            num_batches_tracked};
-  if (R > 256) {
-    if ((C + 63) / 64 > 64) return -1;
-    const int G = 64;
-    float* out = const_cast<float*>(part) + 2L * R * C;  // workspace tail
-    hipLaunchKernelGGL(rows_reduce_fin_kernel<false>, dim3((C + 63) / 64, G), dim3(256), 0, st, part, out, R, C, G,
-                       f, BwdFin{});
-    PDT_RETURN_LAUNCH();
-  }
+  part = rows_reduce(part, &R, C, st);
   hipLaunchKernelGGL(bn_finalize_kernel, dim3((C + 63) / 64), dim3(256), 0, st, part, R, C, f);
   PDT_RETURN_LAUNCH();
 }
@@ -513,14 +471,7 @@ PDT_API int pdt_bn_bwd_finalize(const float* part, int R, int C, double count, c
                                 const float* mean, const float* invstd, float* dgamma, float* dbeta, float* k1,
                                 float* k2, float* k3, int accumulate, hipStream_t st) {
   BwdFin f{count, gamma, mean, invstd, dgamma, dbeta, k1, k2, k3, accumulate};
-  if (R > 256) {
-    if ((C + 63) / 64 > 64) return -1;
-    const int G = 64;
-    float* out = const_cast<float*>(part) + 2L * R * C;
-    hipLaunchKernelGGL(rows_reduce_fin_kernel<true>, dim3((C + 63) / 64, G), dim3(256), 0, st, part, out, R, C, G,
-                       FwdFin{}, f);
-    PDT_RETURN_LAUNCH();
-  }
+  part = rows_reduce(part, &R, C, st);
   hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + 63) / 64), dim3(256), 0, st, part, R, C, f);
   PDT_RETURN_LAUNCH();
 }

@@ -145,15 +145,14 @@ __global__ void __launch_bounds__(256) cast_fp8_t_kernel(const float* __restrict
 // (fp32 words):
 //   [0] scale in use         [1] dq of the LAST cast (1/scale, read by the GEMM)
 //   [2] amax of this cast    (uint bits, atomicMax; non-negative floats order as uints)
-//   [3] arrival counter      [4] history index     [5 .. 5+H) amax history
-// The last-arriving block rolls the history, sets the next scale and resets [2]/[3].
+//   [3] unused               [4] history index     [5 .. 5+H) amax history
+// A one-block roll kernel then moves [2] into the history and sets the next scale.
 constexpr int HIST = 16;
 
 template <bool BF16, int FMT>
 __global__ void __launch_bounds__(256) cast_fp8_delayed_kernel(const void* __restrict__ x, long n,
                                                                float* __restrict__ meta, uint8_t* __restrict__ q) {
   __shared__ float red[4];
-  __shared__ unsigned int last;
   const float s = meta[0];
   float m = 0.f;
   const long stride = (long)gridDim.x * 256 * 8;
@@ -184,27 +183,28 @@ __global__ void __launch_bounds__(256) cast_fp8_delayed_kernel(const void* __res
   m = warp_max(m);
   if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = m;
   __syncthreads();
-  unsigned int* mu = reinterpret_cast<unsigned int*>(meta);
   if (threadIdx.x == 0) {
     const float bm = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
-    atomicMax(mu + 2, __float_as_uint(bm));
-    __threadfence();
-    last = atomicAdd(mu + 3, 1u) == gridDim.x - 1 ? 1u : 0u;
+    atomicMax(reinterpret_cast<unsigned int*>(meta) + 2, __float_as_uint(bm));  // order-free -> deterministic
   }
-  __syncthreads();
-  if (last && threadIdx.x == 0) {
-    __threadfence();
-    const float cur = __uint_as_float(atomicAdd(mu + 2, 0u));
-    const int idx = (int)mu[4];
-    meta[5 + idx % HIST] = cur;
-    mu[4] = (unsigned)(idx + 1);
-    float h = 0.f;
-    for (int i = 0; i < HIST; ++i) h = fmaxf(h, meta[5 + i]);
-    meta[1] = 1.f / s;
-    meta[0] = scale_from<FMT>(h);
-    mu[2] = 0u;
-    mu[3] = 0u;
-  }
+}
+
+// history roll, one tiny launch after the cast (a last-block roll inside the
+// cast would need a device-scope release fence per block: an L2 write-back on
+// the multi-XCD part)
+template <int FMT>
+__global__ void fp8_meta_roll_kernel(float* __restrict__ meta) {
+  if (threadIdx.x != 0) return;
+  unsigned int* mu = reinterpret_cast<unsigned int*>(meta);
+  const float cur = __uint_as_float(mu[2]);
+  const int idx = (int)mu[4];
+  meta[5 + idx % HIST] = cur;
+  mu[4] = (unsigned)(idx + 1);
+  float h = 0.f;
+  for (int i = 0; i < HIST; ++i) h = fmaxf(h, meta[5 + i]);
+  meta[1] = 1.f / meta[0];
+  meta[0] = scale_from<FMT>(h);
+  mu[2] = 0u;
 }
 
 int nblocks(long n) {
@@ -259,6 +259,8 @@ PDT_API int pdt_cast_fp8_delayed(const void* x, int bf16, long n, float* meta, i
   if (bf16) { if (fmt == 0) CD(true, 0); else CD(true, 1); }
   else { if (fmt == 0) CD(false, 0); else CD(false, 1); }
 #undef CD
+  if (fmt == 0) hipLaunchKernelGGL(fp8_meta_roll_kernel<0>, dim3(1), dim3(64), 0, st, meta);
+  else hipLaunchKernelGGL(fp8_meta_roll_kernel<1>, dim3(1), dim3(64), 0, st, meta);
   PDT_RETURN_LAUNCH();
 }
 
