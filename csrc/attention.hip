@@ -441,20 +441,55 @@ __device__ __forceinline__ void stage_seq(char* lds, const u16* src, long ld, in
   }
 }
 
-template <int NKT>
+// Per-lane LDS offsets. A 16-row subtile's row-image fragment (rows 16t + (lane&15),
+// chunk 4kk + g) and a transposed-image fragment pair (rows 32x + 4g + q and
+// +16, column block 16dt) are a lane constant plus an immediate: the XOR
+// swizzles only see bits of (lane&15) / (g, q) -- so no per-read address math.
+__device__ __forceinline__ int row_lane_off(int lane, int kk) {
+  const int l = lane & 15, g = lane >> 4;
+  return l * 128 + (((4 * kk + g) ^ ((l >> 1) & 7)) << 4);
+}
+__device__ __forceinline__ int tr_lane_off(int lane, int dt) {
+  const int g = lane >> 4, q = (lane >> 2) & 3, pp = lane & 3;
+  const int sw = ((q >> 1) & 1) | (((g >> 1) & 1) << 1);  // seg_swz(32x + 16h + 4g + q)
+  return (4 * g + q) * 128 + ((dt ^ sw) << 5) + 8 * pp;
+}
+__device__ __forceinline__ bf16x8 frag_row(const char* img, int off, int t) {
+  return *reinterpret_cast<const bf16x8*>(img + off + t * 2048);
+}
+__device__ __forceinline__ bf16x8 frag_tr(const char* img, int off, int x) {
+  const char* a = img + off + x * 4096;
+  bf16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4bf16(
+      (lds_bf16x4*)((__attribute__((address_space(3))) char*)(uintptr_t)(uint32_t)(uintptr_t)a));
+  bf16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4bf16(
+      (lds_bf16x4*)((__attribute__((address_space(3))) char*)(uintptr_t)(uint32_t)(uintptr_t)(a + 2048)));
+  bf16x8 r;
+  r[0] = lo[0]; r[1] = lo[1]; r[2] = lo[2]; r[3] = lo[3];
+  r[4] = hi[0]; r[5] = hi[1]; r[6] = hi[2]; r[7] = hi[3];
+  return r;
+}
+__device__ __forceinline__ float fast_exp2(float x) { return __builtin_amdgcn_exp2f(x); }
+
+// forward: NT = number of 16-key subtiles (exact: ceil(T/16)); keys >= T only
+// occur in subtile NT-1, so only that one is masked
+template <int NT>
 __global__ void __launch_bounds__(256) attn_fwd_seq_kernel(AttnParams p) {
-  constexpr int NR = ((NKT + 1) & ~1) * 16;  // rows staged (even number of 16-row subtiles)
-  __shared__ __attribute__((aligned(16))) char smem[2 * NR * 128];
+  constexpr int NE = (NT + 1) & ~1;  // staged subtiles (even: 32-key PV steps)
+  __shared__ __attribute__((aligned(16))) char smem[2 * NE * 16 * 128];
   char* Ks = smem;
-  char* Vs = smem + NR * 128;
+  char* Vs = smem + NE * 16 * 128;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, g = lane >> 4;
   const int bh = blockIdx.x, b = bh / p.H, h = bh % p.H;
   const u16* base = p.qkv + (long)b * p.T * p.ld + h * D;
-  stage_seq<false, NR / 16, 256>(Ks, base + p.H * D, p.ld, p.T, tid);
-  stage_seq<true, NR / 16, 256>(Vs, base + 2 * p.H * D, p.ld, p.T, tid);
+  stage_seq<false, NE, 256>(Ks, base + p.H * D, p.ld, p.T, tid);
+  stage_seq<true, NE, 256>(Vs, base + 2 * p.H * D, p.ld, p.T, tid);
+  const int r0 = row_lane_off(lane, 0), r1 = row_lane_off(lane, 1);
+  int to[4];
+#pragma unroll
+  for (int dt = 0; dt < 4; ++dt) to[dt] = tr_lane_off(lane, dt);
+  const int klast = 16 * (NT - 1) + 4 * g;  // first key of this lane in the last subtile
   __syncthreads();
-  const int nkt = (p.T + 15) >> 4;
-  for (int qs = wave; qs < nkt; qs += 4) {
+  for (int qs = wave; qs < NT; qs += 4) {
     const int qrow = qs * 16 + (lane & 15);
     bf16x8 qf[2];
 #pragma unroll
@@ -463,32 +498,27 @@ __global__ void __launch_bounds__(256) attn_fwd_seq_kernel(AttnParams p) {
       if (qrow < p.T) v = *reinterpret_cast<const u32x4*>(base + (long)qrow * p.ld + 32 * kk + 8 * g);
       qf[kk] = __builtin_bit_cast(bf16x8, v);
     }
-    constexpr int NKE = (NKT + 1) & ~1;  // even: key subtiles pair up into 32-key MFMA steps
-    f32x4 s[NKE];
+    f32x4 s[NE];
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+      s[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(frag_row(Ks, r0, t), qf[0], f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+      s[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(frag_row(Ks, r1, t), qf[1], s[t], 0, 0, 0);
+    }
+    if (NE > NT) s[NE - 1] = f32x4{-INFINITY, -INFINITY, -INFINITY, -INFINITY};
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+      if (klast + r >= p.T) s[NT - 1][r] = -INFINITY;
     float m = -INFINITY;
 #pragma unroll
-    for (int t = 0; t < NKE; ++t) {
-      s[t] = f32x4{0.f, 0.f, 0.f, 0.f};
-      if (t < nkt) {
-#pragma unroll
-        for (int kk = 0; kk < 2; ++kk)
-          s[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ld_row_frag(Ks, 16 * t + (lane & 15), 4 * kk + g), qf[kk],
-                                                         s[t], 0, 0, 0);
-      }
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const float v = (16 * t + 4 * g + r) < p.T ? s[t][r] * p.c : -INFINITY;
-        s[t][r] = v;
-        m = fmaxf(m, v);
-      }
-    }
+    for (int t = 0; t < NT; ++t) m = fmaxf(m, fmaxf(fmaxf(s[t][0], s[t][1]), fmaxf(s[t][2], s[t][3])));
     m = xor_max4(m);
+    const float cm = m * p.c;
     float l = 0.f;
 #pragma unroll
-    for (int t = 0; t < NKE; ++t)
+    for (int t = 0; t < NE; ++t)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const float e = exp2f(s[t][r] - m);
+        const float e = fast_exp2(fmaf(s[t][r], p.c, -cm));
         s[t][r] = e;
         l += e;
       }
@@ -497,14 +527,11 @@ __global__ void __launch_bounds__(256) attn_fwd_seq_kernel(AttnParams p) {
 #pragma unroll
     for (int dt = 0; dt < 4; ++dt) o[dt] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-    for (int ks = 0; ks < NKE / 2; ++ks) {
-      if (2 * ks < nkt) {
-        const bf16x8 pf = pack_p(s[2 * ks], s[2 * ks + 1]);
+    for (int ks = 0; ks < NE / 2; ++ks) {
+      const bf16x8 pf = pack_p(s[2 * ks], s[2 * ks + 1]);
 #pragma unroll
-        for (int dt = 0; dt < 4; ++dt)
-          o[dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(tr_frag2(Vs, 32 * ks, 32 * ks + 16, 16 * dt, lane), pf,
-                                                          o[dt], 0, 0, 0);
-      }
+      for (int dt = 0; dt < 4; ++dt)
+        o[dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(frag_tr(Vs, to[dt], ks), pf, o[dt], 0, 0, 0);
     }
     if (qrow < p.T) {
       const float inv = 1.f / l;
@@ -516,7 +543,7 @@ __global__ void __launch_bounds__(256) attn_fwd_seq_kernel(AttnParams p) {
         w.y = pack2bf(o[dt][2] * inv, o[dt][3] * inv);
         *reinterpret_cast<uint2*>(orow + 16 * dt + 4 * g) = w;
       }
-      if (g == 0) p.lse[(long)bh * p.T + qrow] = m + log2f(l);
+      if (g == 0) p.lse[(long)bh * p.T + qrow] = cm + log2f(l);
     }
   }
 }
@@ -547,28 +574,31 @@ struct AttnSeqBwdParams {
 };
 
 // dK, dV: one workgroup (8 waves) per (b, h); wave w owns key subtiles w, w+8.
-template <int NKT_>
+// Per query subtile u: S = Q K^T (q on the register axis, key on the lane),
+// P = exp2(c S - lse), dS = P (dP - delta); dV^T += dO^T P, dK^T += Q^T dS.
+template <int NT>
 __global__ void __launch_bounds__(512) attn_bwd_dkdv_seq_kernel(AttnSeqBwdParams p) {
-  constexpr int NKT = (NKT_ + 1) & ~1;  // even number of 16-row subtiles staged
-  constexpr int IMG = NKT * 16 * 128;
-  __shared__ __attribute__((aligned(16))) char smem[4 * IMG + 2 * NKT * 16 * 4];
+  constexpr int NE = (NT + 1) & ~1;
+  constexpr int IMG = NE * 16 * 128;
+  __shared__ __attribute__((aligned(16))) char smem[4 * IMG + 2 * NE * 16 * 4];
   char* Qr = smem;
   char* Qt = smem + IMG;
   char* dOr = smem + 2 * IMG;
   char* dOt = smem + 3 * IMG;
-  float* lse_s = reinterpret_cast<float*>(smem + 4 * IMG);
-  float* dl_s = lse_s + NKT * 16;
+  float* lse_s = reinterpret_cast<float*>(smem + 4 * IMG);  // pre-negated: -lse
+  float* dl_s = lse_s + NE * 16;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, g = lane >> 4;
   const int bh = blockIdx.x, b = bh / p.H, h = bh % p.H;
   const u16* base = p.qkv + (long)b * p.T * p.ld + h * D;
   const u16* dOg = p.dout + (long)b * p.T * p.ldo + h * D;
   const u16* Og = p.out + (long)b * p.T * p.ldo + h * D;
-  stage_seq<false, NKT, 512>(Qr, base, p.ld, p.T, tid);
-  stage_seq<true, NKT, 512>(Qt, base, p.ld, p.T, tid);
-  stage_seq<false, NKT, 512>(dOr, dOg, p.ldo, p.T, tid);
-  stage_seq<true, NKT, 512>(dOt, dOg, p.ldo, p.T, tid);
-  // per-query softmax stats: lse from the forward, delta recomputed here (8 lanes per query)
-  for (int i = tid; i < NKT * 16 * 8; i += 512) {
+  stage_seq<false, NE, 512>(Qr, base, p.ld, p.T, tid);
+  stage_seq<true, NE, 512>(Qt, base, p.ld, p.T, tid);
+  stage_seq<false, NE, 512>(dOr, dOg, p.ldo, p.T, tid);
+  stage_seq<true, NE, 512>(dOt, dOg, p.ldo, p.T, tid);
+  // per-query stats: -lse (so P = exp2(fma(S, c, -lse))) and delta (8 lanes per query);
+  // rows >= T get -inf -> P = 0
+  for (int i = tid; i < NE * 16 * 8; i += 512) {
     const int q = i >> 3, part = i & 7;
     float v = 0.f;
     if (q < p.T) {
@@ -582,68 +612,66 @@ __global__ void __launch_bounds__(512) attn_bwd_dkdv_seq_kernel(AttnSeqBwdParams
     v += __shfl_xor(v, 4, 64);
     if (part == 0) {
       dl_s[q] = v;
-      lse_s[q] = q < p.T ? p.lse[(long)bh * p.T + q] : 0.f;
+      lse_s[q] = q < p.T ? -p.lse[(long)bh * p.T + q] : -INFINITY;
     }
   }
+  const int r0 = row_lane_off(lane, 0), r1 = row_lane_off(lane, 1);
+  int to[4];
+#pragma unroll
+  for (int dt = 0; dt < 4; ++dt) to[dt] = tr_lane_off(lane, dt);
   __syncthreads();
-  const int nkt = (p.T + 15) >> 4;
-  for (int kt = wave; kt < nkt; kt += 8) {
+  for (int kt = wave; kt < NT; kt += 8) {
     const int key = kt * 16 + (lane & 15);
+    const bool kok = key < p.T;
     bf16x8 kf[2], vf[2];
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk) {
       u32x4 a = {0, 0, 0, 0}, c = {0, 0, 0, 0};
-      if (key < p.T) {
+      if (kok) {
         a = *reinterpret_cast<const u32x4*>(base + p.H * D + (long)key * p.ld + 32 * kk + 8 * g);
         c = *reinterpret_cast<const u32x4*>(base + 2 * p.H * D + (long)key * p.ld + 32 * kk + 8 * g);
       }
       kf[kk] = __builtin_bit_cast(bf16x8, a);
       vf[kk] = __builtin_bit_cast(bf16x8, c);
     }
+    const float kmask = kok ? 1.f : 0.f;  // padded keys: P = dS = 0 (their K/V rows are zero)
     f32x4 dk[4], dv[4];
 #pragma unroll
     for (int dt = 0; dt < 4; ++dt) dk[dt] = dv[dt] = f32x4{0.f, 0.f, 0.f, 0.f};
-    for (int qp = 0; 2 * qp < nkt; ++qp) {
-      f32x4 sp[2], dsp[2];
+#pragma unroll 1
+    for (int qp = 0; qp < NE / 2; ++qp) {
+      f32x4 pp[2], dsp[2];
 #pragma unroll
       for (int h2 = 0; h2 < 2; ++h2) {
         const int u = 2 * qp + h2;
         f32x4 sv = f32x4{0.f, 0.f, 0.f, 0.f}, dpv = f32x4{0.f, 0.f, 0.f, 0.f};
-        if (u < nkt) {
-#pragma unroll
-          for (int kk = 0; kk < 2; ++kk) {
-            sv = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ld_row_frag(Qr, 16 * u + (lane & 15), 4 * kk + g), kf[kk],
-                                                         sv, 0, 0, 0);
-            dpv = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ld_row_frag(dOr, 16 * u + (lane & 15), 4 * kk + g),
-                                                          vf[kk], dpv, 0, 0, 0);
-          }
+        if (u < NT) {
+          sv = __builtin_amdgcn_mfma_f32_16x16x32_bf16(frag_row(Qr, r0, u), kf[0], sv, 0, 0, 0);
+          sv = __builtin_amdgcn_mfma_f32_16x16x32_bf16(frag_row(Qr, r1, u), kf[1], sv, 0, 0, 0);
+          dpv = __builtin_amdgcn_mfma_f32_16x16x32_bf16(frag_row(dOr, r0, u), vf[0], dpv, 0, 0, 0);
+          dpv = __builtin_amdgcn_mfma_f32_16x16x32_bf16(frag_row(dOr, r1, u), vf[1], dpv, 0, 0, 0);
         }
-        // sv[r] = S[q = 16u + 4g + r][key]
+        // sv[r] = S[q = 16u + 4g + r][key]; stats of those 4 queries in one 16-B LDS read each
+        const f32x4 nl = *reinterpret_cast<const f32x4*>(lse_s + 16 * u + 4 * g);
+        const f32x4 dl = *reinterpret_cast<const f32x4*>(dl_s + 16 * u + 4 * g);
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          const int q = 16 * u + 4 * g + r;
-          float pr = 0.f, ds = 0.f;
-          if (q < p.T && key < p.T) {
-            pr = exp2f(sv[r] * p.c - lse_s[q]);
-            ds = pr * (dpv[r] - dl_s[q]);
-          }
+          const float pr = fast_exp2(fmaf(sv[r], p.c, nl[r])) * kmask;
           sv[r] = pr;
-          dpv[r] = ds;
+          dpv[r] = pr * (dpv[r] - dl[r]);
         }
-        sp[h2] = sv;
+        pp[h2] = sv;
         dsp[h2] = dpv;
       }
-      const bf16x8 pf = pack_p(sp[0], sp[1]);
+      const bf16x8 pf = pack_p(pp[0], pp[1]);
       const bf16x8 sf = pack_p(dsp[0], dsp[1]);
 #pragma unroll
       for (int dt = 0; dt < 4; ++dt) {
-        dv[dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(tr_frag2(dOt, 32 * qp, 32 * qp + 16, 16 * dt, lane), pf,
-                                                         dv[dt], 0, 0, 0);
-        dk[dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(tr_frag2(Qt, 32 * qp, 32 * qp + 16, 16 * dt, lane), sf,
-                                                         dk[dt], 0, 0, 0);
+        dv[dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(frag_tr(dOt, to[dt], qp), pf, dv[dt], 0, 0, 0);
+        dk[dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(frag_tr(Qt, to[dt], qp), sf, dk[dt], 0, 0, 0);
       }
     }
-    if (key < p.T) {
+    if (kok) {
       u16* drow = p.dqkv + ((long)b * p.T + key) * p.ld + h * D;
 #pragma unroll
       for (int dt = 0; dt < 4; ++dt) {
@@ -660,10 +688,10 @@ __global__ void __launch_bounds__(512) attn_bwd_dkdv_seq_kernel(AttnSeqBwdParams
 }
 
 // dQ: one workgroup (8 waves) per (b, h); wave w owns query subtiles w, w+8.
-template <int NKT_>
+template <int NT>
 __global__ void __launch_bounds__(512) attn_bwd_dq_seq_kernel(AttnSeqBwdParams p) {
-  constexpr int NKT = (NKT_ + 1) & ~1;
-  constexpr int IMG = NKT * 16 * 128;
+  constexpr int NE = (NT + 1) & ~1;
+  constexpr int IMG = NE * 16 * 128;
   __shared__ __attribute__((aligned(16))) char smem[3 * IMG];
   char* Kr = smem;
   char* Kt = smem + IMG;
@@ -673,12 +701,16 @@ __global__ void __launch_bounds__(512) attn_bwd_dq_seq_kernel(AttnSeqBwdParams p
   const u16* base = p.qkv + (long)b * p.T * p.ld + h * D;
   const u16* dOg = p.dout + (long)b * p.T * p.ldo + h * D;
   const u16* Og = p.out + (long)b * p.T * p.ldo + h * D;
-  stage_seq<false, NKT, 512>(Kr, base + p.H * D, p.ld, p.T, tid);
-  stage_seq<true, NKT, 512>(Kt, base + p.H * D, p.ld, p.T, tid);
-  stage_seq<false, NKT, 512>(Vr, base + 2 * p.H * D, p.ld, p.T, tid);
+  stage_seq<false, NE, 512>(Kr, base + p.H * D, p.ld, p.T, tid);
+  stage_seq<true, NE, 512>(Kt, base + p.H * D, p.ld, p.T, tid);
+  stage_seq<false, NE, 512>(Vr, base + 2 * p.H * D, p.ld, p.T, tid);
+  const int r0 = row_lane_off(lane, 0), r1 = row_lane_off(lane, 1);
+  int to[4];
+#pragma unroll
+  for (int dt = 0; dt < 4; ++dt) to[dt] = tr_lane_off(lane, dt);
+  const int klast = 16 * (NT - 1) + 4 * g;
   __syncthreads();
-  const int nkt = (p.T + 15) >> 4;
-  for (int qs = wave; qs < nkt; qs += 8) {
+  for (int qs = wave; qs < NT; qs += 8) {
     const int qrow = qs * 16 + (lane & 15);
     const bool qok = qrow < p.T;
     const int qr = qok ? qrow : 0;
@@ -693,32 +725,29 @@ __global__ void __launch_bounds__(512) attn_bwd_dq_seq_kernel(AttnSeqBwdParams p
       qf[kk] = __builtin_bit_cast(bf16x8, a);
       of[kk] = __builtin_bit_cast(bf16x8, c);
     }
-    const float delta = row_delta(dOg + (long)qr * p.ldo, Og + (long)qr * p.ldo, g);
-    const float lq = qok ? p.lse[(long)bh * p.T + qrow] : 0.f;
+    const float delta = qok ? row_delta(dOg + (long)qr * p.ldo, Og + (long)qr * p.ldo, g) : 0.f;
+    const float nlq = qok ? -p.lse[(long)bh * p.T + qrow] : -INFINITY;
     f32x4 dq[4];
 #pragma unroll
     for (int dt = 0; dt < 4; ++dt) dq[dt] = f32x4{0.f, 0.f, 0.f, 0.f};
-    for (int kp = 0; 2 * kp < nkt; ++kp) {
+#pragma unroll 1
+    for (int kp = 0; kp < NE / 2; ++kp) {
       f32x4 dsp[2];
 #pragma unroll
       for (int h2 = 0; h2 < 2; ++h2) {
         const int t = 2 * kp + h2;
         f32x4 sv = f32x4{0.f, 0.f, 0.f, 0.f}, dpv = f32x4{0.f, 0.f, 0.f, 0.f};
-        if (t < nkt) {
-#pragma unroll
-          for (int kk = 0; kk < 2; ++kk) {
-            sv = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ld_row_frag(Kr, 16 * t + (lane & 15), 4 * kk + g), qf[kk],
-                                                         sv, 0, 0, 0);
-            dpv = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ld_row_frag(Vr, 16 * t + (lane & 15), 4 * kk + g), of[kk],
-                                                          dpv, 0, 0, 0);
-          }
+        if (t < NT) {
+          sv = __builtin_amdgcn_mfma_f32_16x16x32_bf16(frag_row(Kr, r0, t), qf[0], sv, 0, 0, 0);
+          sv = __builtin_amdgcn_mfma_f32_16x16x32_bf16(frag_row(Kr, r1, t), qf[1], sv, 0, 0, 0);
+          dpv = __builtin_amdgcn_mfma_f32_16x16x32_bf16(frag_row(Vr, r0, t), of[0], dpv, 0, 0, 0);
+          dpv = __builtin_amdgcn_mfma_f32_16x16x32_bf16(frag_row(Vr, r1, t), of[1], dpv, 0, 0, 0);
         }
         // sv[r] = S[key = 16t + 4g + r][q = qrow]
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          const int k = 16 * t + 4 * g + r;
-          float ds = 0.f;
-          if (k < p.T && qok) ds = exp2f(sv[r] * p.c - lq) * (dpv[r] - delta);
+          float ds = fast_exp2(fmaf(sv[r], p.c, nlq)) * (dpv[r] - delta);
+          if (t >= NT - 1 && (t >= NT || klast + r >= p.T)) ds = 0.f;  // padded keys (last subtile only)
           sv[r] = ds;
         }
         dsp[h2] = sv;
@@ -726,8 +755,7 @@ __global__ void __launch_bounds__(512) attn_bwd_dq_seq_kernel(AttnSeqBwdParams p
       const bf16x8 sf = pack_p(dsp[0], dsp[1]);
 #pragma unroll
       for (int dt = 0; dt < 4; ++dt)
-        dq[dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(tr_frag2(Kt, 32 * kp, 32 * kp + 16, 16 * dt, lane), sf,
-                                                         dq[dt], 0, 0, 0);
+        dq[dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(frag_tr(Kt, to[dt], kp), sf, dq[dt], 0, 0, 0);
     }
     if (qok) {
       u16* drow = p.dqkv + ((long)b * p.T + qrow) * p.ld + h * D;
@@ -747,12 +775,28 @@ __global__ void __launch_bounds__(512) attn_bwd_dq_seq_kernel(AttnSeqBwdParams p
 // whole-sequence kernel instantiation for T <= 256 (16-row subtiles)
 static int seq_nkt(int T) {
   const int n = (T + 15) / 16;
-  if (n <= 4) return 4;
-  if (n <= 8) return 8;
-  if (n <= 13) return 13;  // ViT-B/16 @ 224: 197 tokens
-  if (n <= 16) return 16;
-  return 0;
+  return n <= 16 ? n : 0;
 }
+
+#define PDT_SEQ_SWITCH(N, CALL) \
+  switch (N) {                  \
+    case 1: CALL(1); break;     \
+    case 2: CALL(2); break;     \
+    case 3: CALL(3); break;     \
+    case 4: CALL(4); break;     \
+    case 5: CALL(5); break;     \
+    case 6: CALL(6); break;     \
+    case 7: CALL(7); break;     \
+    case 8: CALL(8); break;     \
+    case 9: CALL(9); break;     \
+    case 10: CALL(10); break;   \
+    case 11: CALL(11); break;   \
+    case 12: CALL(12); break;   \
+    case 13: CALL(13); break;   \
+    case 14: CALL(14); break;   \
+    case 15: CALL(15); break;   \
+    default: CALL(16); break;   \
+  }
 
 static int attn_seq_disabled() {
   static int v = -1;
@@ -775,12 +819,9 @@ PDT_API int pdt_attn_fwd(const void* qkv, void* out, float* lse, int B, int T, i
   const int nkt = attn_seq_disabled() ? 0 : seq_nkt(T);
   if (nkt) {
     dim3 g(B * H);
-    switch (nkt) {
-      case 4: hipLaunchKernelGGL(attn_fwd_seq_kernel<4>, g, dim3(256), 0, st, p); break;
-      case 8: hipLaunchKernelGGL(attn_fwd_seq_kernel<8>, g, dim3(256), 0, st, p); break;
-      case 13: hipLaunchKernelGGL(attn_fwd_seq_kernel<13>, g, dim3(256), 0, st, p); break;
-      default: hipLaunchKernelGGL(attn_fwd_seq_kernel<16>, g, dim3(256), 0, st, p); break;
-    }
+#define FWD_SEQ(N) hipLaunchKernelGGL(attn_fwd_seq_kernel<N>, g, dim3(256), 0, st, p)
+    PDT_SEQ_SWITCH(nkt, FWD_SEQ)
+#undef FWD_SEQ
     PDT_RETURN_LAUNCH();
   }
   dim3 grid((T + TILE - 1) / TILE, B * H);
@@ -807,12 +848,7 @@ PDT_API int pdt_attn_bwd(const void* qkv, const void* out, const void* dout, con
 #define SEQ_BWD(N)                                                                \
   hipLaunchKernelGGL(attn_bwd_dkdv_seq_kernel<N>, g, dim3(512), 0, st, q);        \
   hipLaunchKernelGGL(attn_bwd_dq_seq_kernel<N>, g, dim3(512), 0, st, q)
-    switch (nkt) {
-      case 4: SEQ_BWD(4); break;
-      case 8: SEQ_BWD(8); break;
-      case 13: SEQ_BWD(13); break;
-      default: SEQ_BWD(16); break;
-    }
+    PDT_SEQ_SWITCH(nkt, SEQ_BWD)
 #undef SEQ_BWD
     PDT_RETURN_LAUNCH();
   }
