@@ -488,16 +488,25 @@ __global__ void __launch_bounds__(256) attn_fwd_seq_kernel(AttnParams p) {
 #pragma unroll
   for (int dt = 0; dt < 4; ++dt) to[dt] = tr_lane_off(lane, dt);
   const int klast = 16 * (NT - 1) + 4 * g;  // first key of this lane in the last subtile
+  // Q fragments of this wave's first subtile are fetched while K/V stage; each
+  // iteration prefetches the next subtile's before computing the current one
+  auto load_q = [&](int qs, u32x4* v) {
+    const int qrow = qs * 16 + (lane & 15);
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      v[kk] = u32x4{0, 0, 0, 0};
+      if (qs < NT && qrow < p.T) v[kk] = *reinterpret_cast<const u32x4*>(base + (long)qrow * p.ld + 32 * kk + 8 * g);
+    }
+  };
+  u32x4 qn[2];
+  load_q(wave, qn);
   __syncthreads();
   for (int qs = wave; qs < NT; qs += 4) {
     const int qrow = qs * 16 + (lane & 15);
     bf16x8 qf[2];
-#pragma unroll
-    for (int kk = 0; kk < 2; ++kk) {
-      u32x4 v = {0, 0, 0, 0};
-      if (qrow < p.T) v = *reinterpret_cast<const u32x4*>(base + (long)qrow * p.ld + 32 * kk + 8 * g);
-      qf[kk] = __builtin_bit_cast(bf16x8, v);
-    }
+    qf[0] = __builtin_bit_cast(bf16x8, qn[0]);
+    qf[1] = __builtin_bit_cast(bf16x8, qn[1]);
+    load_q(qs + 4, qn);
     f32x4 s[NE];
 #pragma unroll
     for (int t = 0; t < NT; ++t) {

@@ -210,13 +210,16 @@ __global__ void __launch_bounds__(NT) bn_apply_kernel(const u16* __restrict__ y,
                                                       u16* __restrict__ out, const float* __restrict__ scale,
                                                       const float* __restrict__ shift, long n8, int C,
                                                       uint8_t* __restrict__ mask) {
+  // the host sizes the grid so the stride is a multiple of C/8: a thread's 8
+  // channels never change, so the per-channel coefficients are loaded once
   const int cpr = C / 8;
+  const int ch = (int)((blockIdx.x * NT + threadIdx.x) % (uint32_t)cpr) * 8;
+  float sc[8], sh[8];
+  load8f(scale + ch, sc);
+  load8f(shift + ch, sh);
   for (uint32_t i = blockIdx.x * NT + threadIdx.x; i < (uint32_t)n8; i += gridDim.x * NT) {
-    const int ch = (int)(i % (uint32_t)cpr) * 8;
-    float f[8], sc[8], sh[8];
+    float f[8];
     unpack8(reinterpret_cast<const u32x4*>(y)[i], f);
-    load8f(scale + ch, sc);
-    load8f(shift + ch, sh);
 #pragma unroll
     for (int k = 0; k < 8; ++k) f[k] = f[k] * sc[k] + sh[k];
     if (RES) {
@@ -329,9 +332,17 @@ __global__ void __launch_bounds__(NT) bn_bwd_apply_kernel(const u16* __restrict_
                                                           u16* __restrict__ dres, long n8, int C,
                                                           const uint8_t* __restrict__ mask) {
   const int cpr = C / 8;
+  const int ch = (int)((blockIdx.x * NT + threadIdx.x) % (uint32_t)cpr) * 8;  // invariant (see bn_apply)
+  float a1[8], a2[8], a3[8], sc[8], sh[8];
+  load8f(k1 + ch, a1);
+  load8f(k2 + ch, a2);
+  load8f(k3 + ch, a3);
+  if (RELU && !USE_MASK && !USE_ACT) {
+    load8f(scale + ch, sc);
+    load8f(shift + ch, sh);
+  }
   for (uint32_t i = blockIdx.x * NT + threadIdx.x; i < (uint32_t)n8; i += gridDim.x * NT) {
-    const int ch = (int)(i % (uint32_t)cpr) * 8;
-    float g[8], yv[8], a1[8], a2[8], a3[8];
+    float g[8], yv[8];
     unpack8(reinterpret_cast<const u32x4*>(dA)[i], g);
     unpack8(reinterpret_cast<const u32x4*>(y)[i], yv);
     if (RELU) {
@@ -345,27 +356,28 @@ __global__ void __launch_bounds__(NT) bn_bwd_apply_kernel(const u16* __restrict_
 #pragma unroll
         for (int k = 0; k < 8; ++k) g[k] = a[k] > 0.f ? g[k] : 0.f;
       } else {
-        float sc[8], sh[8];
-        load8f(scale + ch, sc);
-        load8f(shift + ch, sh);
 #pragma unroll
         for (int k = 0; k < 8; ++k) g[k] = (yv[k] * sc[k] + sh[k]) > 0.f ? g[k] : 0.f;
       }
     }
     if (DRES) reinterpret_cast<u32x4*>(dres)[i] = pack8(g);
-    load8f(k1 + ch, a1);
-    load8f(k2 + ch, a2);
-    load8f(k3 + ch, a3);
 #pragma unroll
     for (int k = 0; k < 8; ++k) g[k] = a1[k] * g[k] + a2[k] * yv[k] + a3[k];
     reinterpret_cast<u32x4*>(dy)[i] = pack8(g);
   }
 }
 
-int grid_for(long n8) {
+int gcd_i(int a, int b) { return b ? gcd_i(b, a % b) : a; }
+
+// grid for the element passes: <= 4096 blocks, rounded so that the grid
+// stride (blocks * NT chunks) is a multiple of C/8 (channel-invariant threads)
+int grid_for(long n8, int C) {
   long b = (n8 + NT - 1) / NT;
   if (b > 4096) b = 4096;
   if (b < 1) b = 1;
+  const int cpr = C / 8;
+  const int f = cpr / gcd_i(cpr, NT);
+  b = (b + f - 1) / f * f;
   return (int)b;
 }
 
@@ -431,7 +443,7 @@ PDT_API int pdt_bn_apply(const void* y, const void* res, void* out, const float*
   if (C % 8) return -1;
   if (mask && !relu) return -2;
   long n8 = M * C / 8;
-  dim3 g(grid_for(n8)), b(NT);
+  dim3 g(grid_for(n8, C)), b(NT);
   const u16* Y = (const u16*)y;
   const u16* R = (const u16*)res;
   u16* O = (u16*)out;
@@ -481,7 +493,7 @@ PDT_API int pdt_bn_bwd_apply(const void* dA, const void* y, const void* act, con
                              void* dres, long M, int C, int relu, const void* mask, hipStream_t st) {
   if (C % 8) return -1;
   long n8 = M * C / 8;
-  dim3 g(grid_for(n8)), b(NT);
+  dim3 g(grid_for(n8, C)), b(NT);
   const u16 *G = (const u16*)dA, *Y = (const u16*)y, *A = (const u16*)act;
   u16 *DY = (u16*)dy, *DR = (u16*)dres;
   const uint8_t* MK = (const uint8_t*)mask;
