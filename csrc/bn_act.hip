@@ -217,7 +217,6 @@ __global__ void __launch_bounds__(NT) bn_apply_kernel(const u16* __restrict__ y,
   float sc[8], sh[8];
   load8f(scale + ch, sc);
   load8f(shift + ch, sh);
-#pragma unroll 2
   for (uint32_t i = blockIdx.x * NT + threadIdx.x; i < (uint32_t)n8; i += gridDim.x * NT) {
     float f[8];
     unpack8(reinterpret_cast<const u32x4*>(y)[i], f);
@@ -272,18 +271,19 @@ __global__ void __launch_bounds__(NT) bn_bwd_reduce_kernel(const u16* __restrict
       load8f(scale + ch * 8, sc);
       load8f(shift + ch * 8, sh);
     }
-    // gate + accumulate one row chunk (raw loads passed in so two rows' loads are in flight together)
-    auto accum = [&](const u32x4& gw, const u32x4& yw, uint32_t m, const u32x4& aw) {
+    for (long r = (long)blockIdx.x * rp + rr; r < M; r += (long)gridDim.x * rp) {
+      const long off = r * C + ch * 8;
       float g[8], yv[8];
-      unpack8(gw, g);
-      unpack8(yw, yv);
+      unpack8(*reinterpret_cast<const u32x4*>(dA + off), g);
+      unpack8(*reinterpret_cast<const u32x4*>(y + off), yv);
       if (RELU) {
         if (USE_MASK) {
+          const uint32_t m = mask[off >> 3];
 #pragma unroll
           for (int k = 0; k < 8; ++k) g[k] = (m >> k) & 1u ? g[k] : 0.f;
         } else if (USE_ACT) {
           float a[8];
-          unpack8(aw, a);
+          unpack8(*reinterpret_cast<const u32x4*>(act + off), a);
 #pragma unroll
           for (int k = 0; k < 8; ++k) g[k] = a[k] > 0.f ? g[k] : 0.f;
         } else {
@@ -296,29 +296,6 @@ __global__ void __launch_bounds__(NT) bn_bwd_reduce_kernel(const u16* __restrict
         s[k] += g[k];
         q[k] += g[k] * (yv[k] - mu[k]);
       }
-    };
-    auto ld = [&](long r, u32x4& gw, u32x4& yw, uint32_t& m, u32x4& aw) {
-      const long off = r * C + ch * 8;
-      gw = *reinterpret_cast<const u32x4*>(dA + off);
-      yw = *reinterpret_cast<const u32x4*>(y + off);
-      if (RELU && USE_MASK) m = mask[off >> 3];
-      if (RELU && USE_ACT && !USE_MASK) aw = *reinterpret_cast<const u32x4*>(act + off);
-    };
-    const long step = (long)gridDim.x * rp;
-    long r = (long)blockIdx.x * rp + rr;
-    for (; r + step < M; r += 2 * step) {  // two rows per trip: 2x the loads in flight
-      u32x4 g0, y0, a0 = {0, 0, 0, 0}, g1, y1, a1 = {0, 0, 0, 0};
-      uint32_t m0 = 0, m1 = 0;
-      ld(r, g0, y0, m0, a0);
-      ld(r + step, g1, y1, m1, a1);
-      accum(g0, y0, m0, a0);
-      accum(g1, y1, m1, a1);
-    }
-    if (r < M) {
-      u32x4 g0, y0, a0 = {0, 0, 0, 0};
-      uint32_t m0 = 0;
-      ld(r, g0, y0, m0, a0);
-      accum(g0, y0, m0, a0);
     }
   }
 #pragma unroll
@@ -364,7 +341,6 @@ __global__ void __launch_bounds__(NT) bn_bwd_apply_kernel(const u16* __restrict_
     load8f(scale + ch, sc);
     load8f(shift + ch, sh);
   }
-#pragma unroll 2
   for (uint32_t i = blockIdx.x * NT + threadIdx.x; i < (uint32_t)n8; i += gridDim.x * NT) {
     float g[8], yv[8];
     unpack8(reinterpret_cast<const u32x4*>(dA)[i], g);
