@@ -47,7 +47,27 @@ def parse():
     ap.add_argument("--comm-hook", default=None, choices=[None, "bf16"])
     ap.add_argument("--graph", action="store_true", help="capture the whole training step in a HIP graph")
     ap.add_argument("--json-out", default=None)
+    ap.add_argument("--dist-backend", default=None, choices=[None, "nccl", "gloo"],
+                    help="gloo: rehearse N ranks sharing GPU 0 (gradient all-reduce on the host); default RCCL")
     return ap.parse_args()
+
+
+def heartbeat(rank, state, every_s=30.0):
+    """Rank 0 prints a progress line to stderr every ``every_s`` seconds (first-step
+    autotuning / MIOpen searches can run for minutes without other output)."""
+    import threading
+    stop = threading.Event()
+    if rank != 0:
+        return stop
+    t0 = time.time()
+
+    def run():
+        while not stop.wait(every_s):
+            print(f"[bench] {time.time() - t0:.0f}s phase={state['phase']} step={state['step']}", file=sys.stderr,
+                  flush=True)
+
+    threading.Thread(target=run, daemon=True).start()
+    return stop
 
 
 def main():
@@ -58,11 +78,14 @@ def main():
     from pytorch_distributed_template_amd.parallel import wrap_ddp
     from pytorch_distributed_template_amd.data.synthetic import SyntheticImageLoader
 
-    device = pdist.init_distributed()
+    shared = args.dist_backend == "gloo"
+    device = pdist.init_distributed(backend=args.dist_backend, device_index=0 if shared else None)
     world = pdist.get_world_size()
     rank = pdist.get_rank()
     if device.type != "cuda":
         raise SystemExit("bench.py needs a GPU")
+    state = {"phase": "setup", "step": 0}
+    hb = heartbeat(rank, state)
     fused.set_backend(args.backend)
     torch.backends.cudnn.benchmark = True
 
@@ -129,19 +152,24 @@ def main():
             graph.replay()
             return static_loss
 
+    state["phase"] = "warmup"
     for i in range(args.warmup):
+        state["step"] = i
         loss = step(i)
     pdist.synchronize()
     torch.cuda.synchronize()
+    state["phase"] = "timed"
     t0 = time.perf_counter()
     cpu_issue = 0.0
     for i in range(args.steps):
+        state["step"] = i
         c0 = time.perf_counter()
         loss = step(i)
         cpu_issue += time.perf_counter() - c0
     pdist.synchronize()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
+    hb.set()
     t = torch.tensor([elapsed], dtype=torch.float64, device=device)
     if world > 1:
         torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
@@ -167,7 +195,7 @@ def main():
         "config": {"model": args.model, "global_batch": args.batch * world, "per_gpu_batch": args.batch,
                    "seq_len": None, "image_size": 224, "parallelism": f"dp{world}",
                    "backend": args.backend, "optimizer": opt_name,
-                   "bucket_cap_mb": args.bucket_mb, "final_loss": round(final_loss, 4), "hip_graph": args.graph,
+                   "bucket_cap_mb": args.bucket_mb, "dist_backend": args.dist_backend or "nccl (RCCL)","final_loss": round(final_loss, 4), "hip_graph": args.graph,
                    "cpu_issue_ms_per_step": round(cpu_issue / args.steps * 1e3, 3),
                    "max_mem_gib": round(torch.cuda.max_memory_allocated() / 2 ** 30, 2)},
     }

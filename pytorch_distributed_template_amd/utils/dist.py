@@ -67,15 +67,19 @@ def env_world_size() -> int:
 
 
 def init_distributed(local_rank: Optional[int] = None, backend: Optional[str] = None,
-                     timeout_s: float = 1800.0) -> torch.device:
+                     timeout_s: float = 1800.0, device_index: Optional[int] = None) -> torch.device:
     """Initialise the default process group from the ``env://`` rendezvous.
 
     Returns the device this rank should use. Safe to call with WORLD_SIZE=1
-    (returns the device, no process group).
+    (returns the device, no process group). ``device_index`` pins the GPU
+    (e.g. several gloo ranks sharing one GPU to rehearse a multi-rank job on a
+    one-GPU box); by default a rank uses GPU ``LOCAL_RANK`` and a ``gloo``
+    backend means a CPU run.
     """
     local_rank = get_local_rank(local_rank)
-    use_cuda = torch.cuda.is_available() and backend != "gloo"
-    device = torch.device("cuda", local_rank) if use_cuda else torch.device("cpu")
+    use_cuda = torch.cuda.is_available() and (backend != "gloo" or device_index is not None)
+    index = local_rank if device_index is None else device_index
+    device = torch.device("cuda", index) if use_cuda else torch.device("cpu")
     if use_cuda:
         torch.cuda.set_device(device)
     if env_world_size() > 1 and not is_dist_ready():
