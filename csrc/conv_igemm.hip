@@ -628,17 +628,209 @@ int launch_variant(int v, const NTParams& p, hipStream_t st) {
   return -3;
 }
 
+// ---------------------------------------------------------------------------
+// Streaming skinny-K GEMM for 1x1 convolutions (K = Cin or Cout in {64, 128, 256}):
+//   out[m, n] = sum_k A[row(m), k] * B[n, k]
+// The LDS-tiled kernel above runs ONE K-tile per output tile when K <= 64, so
+// load -> MFMA -> store never overlap inside a workgroup, and its 128-KB
+// tiles leave one workgroup per CU. These shapes (the 1x1 expansions
+// 64->256 / 128->512 / 256->1024 and their data gradients) are pure HBM
+// streams (~4-8 FLOP/B), so this kernel drops LDS and barriers entirely:
+//   * every wave owns NJ x 16 output columns; their B fragments (NJ x K/32 x
+//     16 B per lane) are loaded ONCE into registers;
+//   * the wave walks 16-row M tiles rg, rg + nrg, ... (all waves advance
+//     through A together: one streaming pass), loading each tile's A
+//     fragments straight from HBM into registers one tile ahead;
+//   * epilogue per tile: (+ ReLU-masked addend) -> bf16 -> 8-B stores; the
+//     BatchNorm partial sums stay in registers for the whole walk and are
+//     reduced once at the end (nrg partial rows instead of M/BM).
+// Waves of one workgroup take different column blocks of the same rows, so
+// an A tile is fetched from HBM once and re-read from L1/L2 by the others.
+struct SParams {
+  const u16* a;
+  const u16* b;
+  u16* out;
+  float* stats;                 // optional: [2][nrg][N]
+  const u16* addend;            // optional: [M][ldo]
+  const uint8_t* addend_mask;   // optional: 1 bit per addend element
+  int N, ldo, ntiles, ncb, nrg;
+  int Hs, Ws, Hm, Wm, sh, sw;   // strided 1x1 source geometry (STRIDED only)
+  FastDiv div_Wm, div_HWm;
+};
+
+template <int KK, int NJ, bool STRIDED>
+__global__ void __launch_bounds__(256) gemm_stream_kernel(SParams p) {
+  constexpr int KS = KK / 32;
+  const int lane = threadIdx.x & 63;
+  const uint32_t blk = xcd_remap(blockIdx.x, gridDim.x);
+  const int gw = (int)blk * 4 + (threadIdx.x >> 6);
+  const int cb = gw % p.ncb, rg = gw / p.ncb;
+  if (rg >= p.nrg) return;  // whole wave: the grid is rounded up to 4 waves
+  const int n0 = cb * NJ * 16;
+  const int lr = lane & 15, lk = (lane >> 4) * 8;
+
+  bf16x8 bf[NJ][KS];
+#pragma unroll
+  for (int j = 0; j < NJ; ++j)
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks)
+      bf[j][ks] = *reinterpret_cast<const bf16x8*>(p.b + (size_t)(n0 + j * 16 + lr) * KK + ks * 32 + lk);
+
+  auto a_row = [&](int t) -> const u16* {
+    const uint32_t m = (uint32_t)t * 16 + lr;
+    if (!STRIDED) return p.a + (size_t)m * KK;
+    const uint32_t img = fdiv(m, p.div_HWm);
+    const uint32_t rem = m - img * (uint32_t)(p.Hm * p.Wm);
+    const uint32_t oh = fdiv(rem, p.div_Wm);
+    const uint32_t ow = rem - oh * p.Wm;
+    return p.a + ((size_t)(img * p.Hs + oh * p.sh) * p.Ws + ow * p.sw) * KK;
+  };
+
+  float s[NJ][4], q[NJ][4];
+#pragma unroll
+  for (int j = 0; j < NJ; ++j)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) s[j][r] = q[j][r] = 0.f;
+
+  bf16x8 a[KS];
+  {
+    const u16* ap = a_row(rg < p.ntiles ? rg : 0);
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) a[ks] = *reinterpret_cast<const bf16x8*>(ap + ks * 32 + lk);
+  }
+  for (int t = rg; t < p.ntiles; t += p.nrg) {
+    // next tile's A (clamped: the last trip re-reads a valid tile instead of branching)
+    bf16x8 an[KS];
+    {
+      const int tn = t + p.nrg < p.ntiles ? t + p.nrg : t;
+      const u16* ap = a_row(tn);
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) an[ks] = *reinterpret_cast<const bf16x8*>(ap + ks * 32 + lk);
+    }
+    f32x4 acc[NJ];
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks)
+#pragma unroll
+      for (int j = 0; j < NJ; ++j)
+        // swapped operands: lane holds 4 consecutive output channels of row lr
+        acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bf[j][ks], a[ks], acc[j], 0, 0, 0);
+
+    const size_t m = (size_t)t * 16 + lr;
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+      const int col = n0 + j * 16 + (lane >> 4) * 4;
+      float v[4] = {acc[j][0], acc[j][1], acc[j][2], acc[j][3]};
+      if (p.stats != nullptr) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          s[j][r] += v[r];
+          q[j][r] += v[r] * v[r];
+        }
+      }
+      const size_t e = m * p.ldo + col;
+      if (p.addend != nullptr) {
+        uint2 ad = *reinterpret_cast<const uint2*>(p.addend + e);
+        if (p.addend_mask != nullptr) {
+          const uint32_t mb = p.addend_mask[e >> 3] >> (e & 7);
+          ad.x &= ((mb & 1u) ? 0xffffu : 0u) | ((mb & 2u) ? 0xffff0000u : 0u);
+          ad.y &= ((mb & 4u) ? 0xffffu : 0u) | ((mb & 8u) ? 0xffff0000u : 0u);
+        }
+        v[0] += lo_bf(ad.x); v[1] += hi_bf(ad.x); v[2] += lo_bf(ad.y); v[3] += hi_bf(ad.y);
+      }
+      typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+      *reinterpret_cast<u32x2*>(p.out + e) = u32x2{pack2bf(v[0], v[1]), pack2bf(v[2], v[3])};
+    }
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) a[ks] = an[ks];
+  }
+
+  if (p.stats != nullptr) {
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+#pragma unroll
+      for (int o = 1; o < 16; o <<= 1) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          s[j][r] += __shfl_xor(s[j][r], o, 64);
+          q[j][r] += __shfl_xor(q[j][r], o, 64);
+        }
+      }
+      if (lr == 0) {
+        const int col = n0 + j * 16 + (lane >> 4) * 4;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          p.stats[(size_t)rg * p.N + col + r] = s[j][r];
+          p.stats[(size_t)(p.nrg + rg) * p.N + col + r] = q[j][r];
+        }
+      }
+    }
+  }
+}
+
+// stream variants (conv_nt variant ids NVAR..NVAR+3): NJ in {2, 4} x ~2048 / ~4096 waves
+constexpr int NVAR_STREAM = 4;
+constexpr int STREAM_NJ[NVAR_STREAM] = {2, 2, 4, 4};
+constexpr int STREAM_WAVES[NVAR_STREAM] = {2048, 4096, 2048, 4096};
+
+// partial-stat rows (= row groups) of stream variant s; 0 if the column split does not fit
+int stream_rows(int s, int M, int Ncol) {
+  const int cols = STREAM_NJ[s] * 16;
+  if (Ncol % cols || M % 16) return 0;
+  const int ncb = Ncol / cols, ntiles = M / 16;
+  int nrg = STREAM_WAVES[s] / ncb;
+  if (nrg > ntiles / 2) nrg = ntiles / 2;  // >= 2 tiles per wave (one in flight)
+  return nrg < 1 ? 1 : nrg;
+}
+
+template <int KK, int NJ>
+int launch_stream(const SParams& p, bool strided, hipStream_t st) {
+  const int blocks = (p.ncb * p.nrg + 3) / 4;
+  if (strided)
+    hipLaunchKernelGGL((gemm_stream_kernel<KK, NJ, true>), dim3(blocks), dim3(256), 0, st, p);
+  else
+    hipLaunchKernelGGL((gemm_stream_kernel<KK, NJ, false>), dim3(blocks), dim3(256), 0, st, p);
+  PDT_RETURN_LAUNCH();
+}
+
+constexpr int NOT_APPLICABLE = -5;  // variant cannot run this geometry (the tuner skips it)
+
+int run_stream(int s, const NTParams& p, hipStream_t st) {
+  const int NJ = STREAM_NJ[s];
+  const int K = p.K;
+  // 1x1, unpadded, dense [N][K] weights, output row == m, no bias / activation / aux
+  if (p.nth != 1 || p.ntw != 1 || p.oh0 != 0 || p.ow0 != 0 || !p.ident_out || p.Cs != K || p.ldb != K ||
+      p.bias != nullptr || p.act != 0 || p.aux != nullptr)
+    return NOT_APPLICABLE;
+  if (!(K == 64 || K == 128 || K == 256) || (K == 256 && NJ == 4)) return NOT_APPLICABLE;
+  const int nrg = stream_rows(s, p.M, p.Ncol);
+  if (nrg == 0) return NOT_APPLICABLE;
+  const bool strided = !(p.sh == 1 && p.sw == 1 && p.Hs == p.Hm && p.Ws == p.Wm);
+  if (strided && ((p.Hm - 1) * p.sh >= p.Hs || (p.Wm - 1) * p.sw >= p.Ws)) return NOT_APPLICABLE;
+  SParams q;
+  q.a = p.src; q.b = p.b; q.out = p.out; q.stats = p.stats;
+  q.addend = p.addend; q.addend_mask = p.addend_mask;
+  q.N = p.Ncol; q.ldo = p.ldo; q.ntiles = p.M / 16; q.ncb = p.Ncol / (NJ * 16); q.nrg = nrg;
+  q.Hs = p.Hs; q.Ws = p.Ws; q.Hm = p.Hm; q.Wm = p.Wm; q.sh = p.sh; q.sw = p.sw;
+  q.div_Wm = p.div_Wm; q.div_HWm = p.div_HWm;
+  if (K == 64) return NJ == 2 ? launch_stream<64, 2>(q, strided, st) : launch_stream<64, 4>(q, strided, st);
+  if (K == 128) return NJ == 2 ? launch_stream<128, 2>(q, strided, st) : launch_stream<128, 4>(q, strided, st);
+  return launch_stream<256, 2>(q, strided, st);
+}
+
 }  // namespace
 
-PDT_API int pdt_conv_nt_num_variants() { return NVAR; }
+PDT_API int pdt_conv_nt_num_variants() { return NVAR + NVAR_STREAM; }
 
 PDT_API int pdt_conv_nt_resolve_variant(int variant, int M, int Ncol, int K) {
-  return (variant >= 0 && variant < NVAR) ? variant : heuristic_variant(M, Ncol, K);
+  return (variant >= 0 && variant < NVAR + NVAR_STREAM) ? variant : heuristic_variant(M, Ncol, K);
 }
 
 // Number of BN-statistics partial rows a launch of `variant` writes (sizes the stats buffer).
 PDT_API int pdt_conv_nt_stat_rows(int M, int Ncol, int K, int variant) {
   int v = pdt_conv_nt_resolve_variant(variant, M, Ncol, K);
+  if (v >= NVAR) return stream_rows(v - NVAR, M, Ncol);
   int BM = VAR_BM[v];
   return ((M + BM - 1) / BM) * VAR_WM[v];
 }
@@ -685,6 +877,7 @@ PDT_API int pdt_conv_nt(const void* src, const void* b, void* out, float* stats,
   }
   const int v = pdt_conv_nt_resolve_variant(variant, p.M, Ncol, K);
   p.nstat_rows = pdt_conv_nt_stat_rows(p.M, Ncol, K, v);
+  if (v >= NVAR) return run_stream(v - NVAR, p, stream);
   const bool cs64 = (Cs % 64) == 0;
   return cs64 ? launch_variant<true>(v, p, stream) : launch_variant<false>(v, p, stream);
 }

@@ -13,10 +13,16 @@
 // 32-byte segments of each LDS row are XOR-swizzled by a function of the row
 // so the eight rows a 32-lane half touches fall on distinct banks.
 //
-// Each workgroup computes a BM x 128 tile over a contiguous slice of the
+// Each workgroup computes a BM x BN tile over a contiguous slice of the
 // pixels and writes an fp32 partial slab; pdt_wgrad_reduce sums the slabs in
 // a fixed order (bitwise deterministic, no atomics) and writes / accumulates
 // the fp32 gradient.
+//
+// Workgroup shapes: 4 waves (2x2, up to 128x128, two workgroups per CU) or
+// 8 waves (256x128 as 4x2, 128x256 as 2x4, 256x256 as 2x4 with a 128x64 tile
+// per wave; one workgroup per CU). The 8-wave tiles halve the L2->LDS bytes
+// per MFMA of the 128x128 tile: the big 3x3 weight gradients (No = 9*Cin up
+// to 4608) are otherwise bound by the staging traffic, not the matrix cores.
 #include "pdt_common.h"
 
 namespace {
@@ -38,9 +44,13 @@ struct WGParams {
 constexpr int BK = 64;
 constexpr int NT = 256;
 
+// XOR applied to the 32-B segment index of an LDS row. A transposed read's
+// 32-lane half touches rows {8g + q : g = 0,1, q = 0..3} (+4) in one logical
+// segment; for rows of >= 256 B (a whole bank row or more) the swizzle gives
+// those 8 rows 8 distinct values mod 8 -> 8 distinct 32-B bank groups.
 template <int RB>
 __device__ __forceinline__ int seg_swz(int row) {
-  if (RB == 256) return (row & 3) | ((row >> 1) & 4);
+  if (RB >= 256) return (row & 3) | ((row >> 1) & 4);
   return ((row >> 1) & 1) | ((row >> 2) & 2);  // RB == 128
 }
 
@@ -70,25 +80,27 @@ __device__ __forceinline__ bf16x8 tr_frag(const char* base, int krow0, int col0,
   return r;
 }
 
-template <int BM, int BN, int NSTAGE>
-__global__ void __launch_bounds__(NT, 2) wgrad_kernel(WGParams p) {
+template <int BM, int BN, int NSTAGE, int NTH = NT, int WM = 2>
+__global__ void __launch_bounds__(NTH, NTH == NT ? 2 : 1) wgrad_kernel(WGParams p) {
+  constexpr int WN = NTH / 64 / WM;    // waves along the (tap, c) columns
   constexpr int RBA = BM * 2;   // bytes per A row (co)
   constexpr int RBB = BN * 2;   // bytes per B row (tap,c)
   constexpr int A_BYTES = BK * RBA;
   constexpr int B_BYTES = BK * RBB;
   constexpr int STAGE = A_BYTES + B_BYTES;
   constexpr int ACH = BM / 8;          // 16-B chunks per A row
-  constexpr int AROWS = NT / ACH;      // rows covered per pass
+  constexpr int AROWS = NTH / ACH;     // rows covered per pass
   constexpr int NA = BK / AROWS;       // A chunks per thread
   constexpr int BCH = BN / 8;
-  constexpr int BROWS = NT / BCH;
+  constexpr int BROWS = NTH / BCH;
   constexpr int NB = BK / BROWS;
-  constexpr int MI = BM / 32;          // co 16-tiles per wave
-  constexpr int NI = BN / 32;          // tc 16-tiles per wave
+  constexpr int MI = BM / (WM * 16);   // co 16-tiles per wave
+  constexpr int NI = BN / (WN * 16);   // tc 16-tiles per wave
+  static_assert(NA >= 1 && NB >= 1 && MI >= 1 && NI >= 1 && WM * WN * 64 == NTH, "wgrad tile shape");
   __shared__ __attribute__((aligned(16))) char smem[NSTAGE * STAGE];
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int wm = wave >> 1, wn = wave & 1;
+  const int wm = wave / WN, wn = wave % WN;
 
   const int ntm = (p.Mo + BM - 1) / BM, ntn = (p.No + BN - 1) / BN;
   const int ntiles = ntm * ntn;
@@ -173,17 +185,19 @@ __global__ void __launch_bounds__(NT, 2) wgrad_kernel(WGParams p) {
     const char* sb = sa + A_BYTES;
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk) {
-      bf16x8 af[MI], bfr[NI];
+      // B fragments for the whole k-step, A fragments one 16-row tile at a time
+      // (the 128x64-per-wave tile would otherwise hold 12 fragments at once)
+      bf16x8 bfr[NI];
 #pragma unroll
-      for (int i = 0; i < MI; ++i) af[i] = tr_frag<RBA>(sa, kk * 32, wm * (BM / 2) + i * 16, lane);
+      for (int j = 0; j < NI; ++j) bfr[j] = tr_frag<RBB>(sb, kk * 32, wn * (BN / WN) + j * 16, lane);
 #pragma unroll
-      for (int j = 0; j < NI; ++j) bfr[j] = tr_frag<RBB>(sb, kk * 32, wn * (BN / 2) + j * 16, lane);
-#pragma unroll
-      for (int i = 0; i < MI; ++i)
+      for (int i = 0; i < MI; ++i) {
+        const bf16x8 af = tr_frag<RBA>(sa, kk * 32, wm * (BM / WM) + i * 16, lane);
 #pragma unroll
         for (int j = 0; j < NI; ++j)
           // D[tc][co]: lane holds 4 consecutive tc of one co
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[j], af[i], acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[j], af, acc[i][j], 0, 0, 0);
+      }
     }
     if (NSTAGE == 2) {
       if (kt + 1 < kt_end) store_tile(cur ^ 1);
@@ -198,10 +212,10 @@ __global__ void __launch_bounds__(NT, 2) wgrad_kernel(WGParams p) {
   float* out = p.slab + (size_t)split * p.Mo * p.No;
 #pragma unroll
   for (int i = 0; i < MI; ++i) {
-    int co = co0 + wm * (BM / 2) + i * 16 + (lane & 15);
+    int co = co0 + wm * (BM / WM) + i * 16 + (lane & 15);
 #pragma unroll
     for (int j = 0; j < NI; ++j) {
-      int tc = tc0 + wn * (BN / 2) + j * 16 + (lane >> 4) * 4;
+      int tc = tc0 + wn * (BN / WN) + j * 16 + (lane >> 4) * 4;
       if (co < p.Mo && tc < p.No) {
         *reinterpret_cast<f32x4*>(out + (size_t)co * p.No + tc) = acc[i][j];
       }
@@ -237,23 +251,26 @@ __global__ void wgrad_reduce1_kernel(const float* __restrict__ slab, float* __re
 
 }  // namespace
 
-// Variants: v = tile * 3 + cfg; tile in {64x64, 64x128, 128x64, 128x128} (Mo x No),
-// cfg: 0 = 2 LDS stages / ~1024 workgroups, 1 = 1 stage / ~1024, 2 = 1 stage / ~2048.
-// -1 = heuristic (tile from Mo/No, cfg 0). Autotuned per shape from Python.
-constexpr int WG_NVAR = 12;
-static void wg_variant(int v, int Mo, int No, int* BM, int* BN, int* NS, int* target) {
-  if (v < 0 || v >= WG_NVAR) {
-    *BM = Mo <= 64 ? 64 : 128;
-    *BN = No <= 64 ? 64 : 128;
-    *NS = 2;
-    *target = 1024;
-    return;
-  }
-  const int tile = v / 3, cfg = v % 3;
-  *BM = (tile >= 2) ? 128 : 64;
-  *BN = (tile & 1) ? 128 : 64;
-  *NS = cfg == 0 ? 2 : 1;
-  *target = cfg == 2 ? 2048 : 1024;
+// Variants (autotuned per shape from Python; -1 = heuristic: tile from Mo/No, 2 stages, ~1024 WGs):
+//   0..11 : v = tile * 3 + cfg, 4-wave tiles {64x64, 64x128, 128x64, 128x128} (Mo x No);
+//           cfg 0 = 2 LDS stages / ~1024 workgroups, 1 = 1 stage / ~1024, 2 = 1 stage / ~2048
+//   12..17: 8-wave tiles, 2 LDS stages: 256x128 and 128x256 (64x64 per wave) at ~512 and ~1024
+//           workgroups; 256x256 (128x64 per wave, 128 KB LDS) at ~256 and ~512
+struct WGVar {
+  int BM, BN, NS, NTH, target;
+};
+constexpr int WG_NVAR = 18;
+constexpr WGVar WG_VARS[WG_NVAR] = {
+    {64, 64, 2, 256, 1024},   {64, 64, 1, 256, 1024},   {64, 64, 1, 256, 2048},
+    {64, 128, 2, 256, 1024},  {64, 128, 1, 256, 1024},  {64, 128, 1, 256, 2048},
+    {128, 64, 2, 256, 1024},  {128, 64, 1, 256, 1024},  {128, 64, 1, 256, 2048},
+    {128, 128, 2, 256, 1024}, {128, 128, 1, 256, 1024}, {128, 128, 1, 256, 2048},
+    {256, 128, 2, 512, 512},  {128, 256, 2, 512, 512},  {256, 128, 2, 512, 1024},
+    {128, 256, 2, 512, 1024}, {256, 256, 2, 512, 256},  {256, 256, 2, 512, 512},
+};
+static WGVar wg_variant(int v, int Mo, int No) {
+  if (v < 0 || v >= WG_NVAR) return WGVar{Mo <= 64 ? 64 : 128, No <= 64 ? 64 : 128, 2, 256, 1024};
+  return WG_VARS[v];
 }
 
 PDT_API int pdt_wgrad_num_variants() { return WG_NVAR; }
@@ -261,8 +278,8 @@ PDT_API int pdt_wgrad_num_variants() { return WG_NVAR; }
 // Plan: number of splits so the grid covers the chip; returns splits and
 // writes ktiles_per_split.
 PDT_API int pdt_wgrad_plan(int M, int Mo, int No, int variant, int* ktiles_per_split) {
-  int BM, BN, NS, target;
-  wg_variant(variant, Mo, No, &BM, &BN, &NS, &target);
+  const WGVar w = wg_variant(variant, Mo, No);
+  const int BM = w.BM, BN = w.BN, target = w.target;
   int tiles = ((Mo + BM - 1) / BM) * ((No + BN - 1) / BN);
   int nk = (M + BK - 1) / BK;
   int splits = (target + tiles - 1) / tiles;
@@ -303,12 +320,17 @@ PDT_API int pdt_conv_wgrad(const void* dy, const void* x, float* slab, float* ou
   p.div_HWm = make_fastdiv(Hm * Wm);
   p.div_C = make_fastdiv(C);
   p.div_ntw = make_fastdiv(ntw);
-  int BM, BN, NS, target;
-  wg_variant(variant, Mo, No, &BM, &BN, &NS, &target);
+  const WGVar w = wg_variant(variant, Mo, No);
+  const int BM = w.BM, BN = w.BN, NS = w.NS;
   int tiles = ((Mo + BM - 1) / BM) * ((No + BN - 1) / BN);
   dim3 grid(tiles * splits);
 #define WG_LAUNCH(a, b, c) hipLaunchKernelGGL((wgrad_kernel<a, b, c>), grid, dim3(NT), 0, stream, p)
-  if (NS == 2) {
+#define WG_LAUNCH8(a, b, wm) hipLaunchKernelGGL((wgrad_kernel<a, b, 2, 512, wm>), grid, dim3(512), 0, stream, p)
+  if (w.NTH == 512) {
+    if (BM == 256 && BN == 256) WG_LAUNCH8(256, 256, 2);
+    else if (BM == 256) WG_LAUNCH8(256, 128, 4);
+    else WG_LAUNCH8(128, 256, 2);
+  } else if (NS == 2) {
     if (BM == 64 && BN == 64) WG_LAUNCH(64, 64, 2);
     else if (BM == 64) WG_LAUNCH(64, 128, 2);
     else if (BN == 64) WG_LAUNCH(128, 64, 2);
@@ -320,6 +342,7 @@ PDT_API int pdt_conv_wgrad(const void* dy, const void* x, float* slab, float* ou
     else WG_LAUNCH(128, 128, 1);
   }
 #undef WG_LAUNCH
+#undef WG_LAUNCH8
   int e = (int)hipGetLastError();
   if (e) return e;
   long n4 = (long)Mo * No / 4;

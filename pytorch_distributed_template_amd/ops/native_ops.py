@@ -227,6 +227,9 @@ def _tune_allowed() -> bool:
     return os.environ.get("PDT_AUTOTUNE", "1") != "0" and not torch.cuda.is_current_stream_capturing()
 
 
+NOT_APPLICABLE = -5  # kernel return code: this variant cannot run this geometry
+
+
 def _time_variants(nvar, launch, allowed=None):
     """Fastest variant id: one warm launch, then the best of two 3-launch HIP-event trials."""
     best, best_t = -1, float("inf")
@@ -234,7 +237,10 @@ def _time_variants(nvar, launch, allowed=None):
     for v in range(nvar):
         if allowed is not None and v not in allowed:
             continue
-        _chk(launch(v), f"tune variant {v}")
+        rc = launch(v)
+        if rc == NOT_APPLICABLE:  # e.g. the streaming 1x1 kernel on a 3x3 geometry
+            continue
+        _chk(rc, f"tune variant {v}")
         t = float("inf")
         for _ in range(2):
             ev0.record()
@@ -293,7 +299,7 @@ def _check_nt(src, b, out, a):
 def select_nt_variant(src, b, out, *, with_stats=False, bias=None, act=0, **a):
     """Variant id for this geometry (tuning it on first use when allowed)."""
     M = a["Nimg"] * a["Hm"] * a["Wm"]
-    key = "nt4:" + ",".join(str(a[k]) for k in ("Hs", "Ws", "Cs", "Nimg", "Hm", "Wm", "Ncol", "K", "sh", "sw",
+    key = "nt5:" + ",".join(str(a[k]) for k in ("Hs", "Ws", "Cs", "Nimg", "Hm", "Wm", "Ncol", "K", "sh", "sw",
                                                  "nth", "ntw", "osh")) + f",{int(with_stats)},{int(bias is not None)}"
     table = _tuned()
     if key in table:
@@ -359,7 +365,7 @@ def conv_wgrad(dy, x, out, *, scale=1.0, accumulate=False, variant=None, **a):
     assert a["ntw"] >= 1 and No % C == 0
     lib = _load()
     if variant is None:
-        key = "wg:" + ",".join(str(a[k]) for k in ("M", "Mo", "No", "Hs", "Ws", "C", "Hm", "Wm", "sh", "ntw"))
+        key = "wg2:" + ",".join(str(a[k]) for k in ("M", "Mo", "No", "Hs", "Ws", "C", "Hm", "Wm", "sh", "ntw"))
         table = _tuned()
         if key in table:
             variant = int(table[key])
@@ -914,7 +920,7 @@ def _linear_dgrad(dy2, w):
 
 def _linear_wgrad(dy2, x2, w):
     Nout, K = w.shape
-    key = f"lgw:{dy2.shape[0]},{Nout},{K}"
+    key = f"lgw2:{dy2.shape[0]},{Nout},{K}"
     impl = _pick_impl(key, lambda: _linear_wgrad_native(dy2, x2, w), lambda: _linear_wgrad_lib(dy2, x2, w)) \
         if _lib_gemm_allowed() else "native"
     return _linear_wgrad_lib(dy2, x2, w) if impl == "lib" else _linear_wgrad_native(dy2, x2, w)

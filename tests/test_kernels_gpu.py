@@ -75,8 +75,10 @@ def test_conv_fwd_dgrad_wgrad(shape):
     a = no._fwd_nt_geom(N, H, W, Cs, Cout, g)
     for v in range(no._load().pdt_conv_nt_num_variants()):
         yv = torch.empty_like(y)
-        no.conv_nt(xs, wb, yv, variant=v, **a)
-        assert relerr(yv, ref) < 1e-2, v
+        rc = no._load().pdt_conv_nt(*no._nt_args(xs, wb, yv, None, None, a, 0, v))
+        if rc == no.NOT_APPLICABLE:
+            continue
+        assert rc == 0 and relerr(yv, ref) < 1e-2, v
     # BN partial statistics from the epilogue
     ps = part[:2 * R * Cout].view(2, R, Cout).sum(1)
     rs = ref.sum((0, 2, 3))
@@ -100,6 +102,54 @@ def test_conv_fwd_dgrad_wgrad(shape):
         dwv = torch.zeros_like(dw)
         no.conv_wgrad(dy, xs, dwv, variant=v, **wa)
         assert relerr(dwv[:, :Cin], rdw) < 1e-2, v
+
+
+STREAM_SHAPES = [  # Cin (= K), Cout, stride: the 1x1 convs the streaming kernel serves
+    (64, 256, 1), (128, 512, 1), (256, 128, 1), (256, 512, 2), (64, 64, 1), (128, 256, 2),
+]
+
+
+@pytest.mark.parametrize("cin,cout,s", STREAM_SHAPES)
+def test_stream_1x1_gemm(cin, cout, s):
+    """Streaming skinny-K 1x1 GEMM variants: output, BN partial statistics, and the
+    ReLU-masked addend epilogue (the block-input data gradient) vs fp32 references."""
+    torch.manual_seed(3)
+    dev = "cuda"
+    N, H = 4, 14 * s
+    conv = nn.Conv2d(cin, cout, 1, s, 0, bias=False).to(dev).to(memory_format=torch.channels_last)
+    x = _cl(torch.randn(N, cin, H, H, device=dev).to(torch.bfloat16))
+    wb = no.bf16_weight(conv.weight)
+    ref = F.conv2d(x.float(), conv.weight.detach().to(torch.bfloat16).float(), None, s, 0)
+    g = no._fwd_geom(N, H, H, cin, conv)
+    a = no._fwd_nt_geom(N, H, H, cin, cout, g)
+    M = N * g["Ho"] * g["Wo"]
+    lib = no._load()
+    nvar = lib.pdt_conv_nt_num_variants()
+    ran = 0
+    for v in range(nvar - 4, nvar):
+        rows = lib.pdt_conv_nt_stat_rows(M, cout, cin, v)
+        part = torch.full((2 * max(rows, 1) * cout,), float("nan"), device=dev)
+        y = torch.empty_like(ref, dtype=torch.bfloat16, memory_format=torch.channels_last)
+        rc = lib.pdt_conv_nt(*no._nt_args(x, wb, y, part, None, a, 0, v))
+        if rc == no.NOT_APPLICABLE:
+            continue
+        assert rc == 0, (v, rc)
+        ran += 1
+        assert relerr(y, ref) < 1e-2, v
+        ps = part.view(2, rows, cout).sum(1)
+        assert relerr(ps[0], ref.sum((0, 2, 3))) < 1e-3, v
+        assert relerr(ps[1], (ref * ref).sum((0, 2, 3))) < 1e-3, v
+        if s == 1:  # dgrad-style epilogue: + addend gated by a 1-bit ReLU mask
+            add = _cl(torch.randn_like(ref).to(torch.bfloat16))
+            mask = torch.randint(0, 256, (add.numel() // 8,), dtype=torch.uint8, device=dev)
+            bits = ((mask.view(-1, 1).int() >> torch.arange(8, device=dev)) & 1).view(-1)
+            # element e of the NHWC storage <-> bit e
+            gate = bits.view(N, g["Ho"], g["Wo"], cout).permute(0, 3, 1, 2).float()
+            y2 = torch.empty_like(y)
+            rc = lib.pdt_conv_nt(*no._nt_args(x, wb, y2, None, None, a, 0, v, add, None, mask))
+            assert rc == 0
+            assert relerr(y2, ref + add.float() * gate) < 1e-2, v
+    assert ran >= 1
 
 
 @pytest.mark.parametrize("relu,res", [(True, False), (True, True), (False, False)])
