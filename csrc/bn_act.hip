@@ -97,7 +97,23 @@ __global__ void __launch_bounds__(256) rows_reduce_kernel(const float* __restric
   const int g = blockIdx.y;
   float s = 0.f, q = 0.f;
   if (c < C) {
-    for (int r = g * 4 + rg; r < R; r += 4 * G) {
+    // 8 rows per trip, all loads issued before the adds (latency, not bandwidth, bounds this)
+    int r = g * 4 + rg;
+    const int step = 4 * G;
+    for (; r + 7 * step < R; r += 8 * step) {
+      float a[8], b[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        a[u] = part[(long)(r + u * step) * C + c];
+        b[u] = part[(long)(R + r + u * step) * C + c];
+      }
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        s += a[u];
+        q += b[u];
+      }
+    }
+    for (; r < R; r += step) {
       s += part[(long)r * C + c];
       q += part[(long)(R + r) * C + c];
     }
@@ -118,7 +134,21 @@ __device__ __forceinline__ void sum_rows64(const float* __restrict__ part, int R
   const int cl = threadIdx.x & 63;
   double a = 0, b = 0;
   if (c < C) {
-    for (int r = rg; r < R; r += 4) {
+    int r = rg;
+    for (; r + 28 < R; r += 32) {  // 8 rows per trip, loads first
+      float x[8], y[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        x[u] = part[(long)(r + 4 * u) * C + c];
+        y[u] = part[(long)(R + r + 4 * u) * C + c];
+      }
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        a += x[u];
+        b += y[u];
+      }
+    }
+    for (; r < R; r += 4) {
       a += part[(long)r * C + c];
       b += part[(long)(R + r) * C + c];
     }
@@ -407,8 +437,15 @@ PDT_API int pdt_bn_stats(const void* y, float* part, long M, int C, int blocks, 
 
 // Number of floats of extra workspace the finalize calls need after the
 // [2][R][C] partial block (stage-1 output of the parallel row reduction).
+// stage-1 row groups: enough blocks to fill the chip for narrow C, few enough
+// rows left for the finalize's single pass
+static int rows_groups(int R, int C) {
+  if (R <= 256) return 0;
+  return (R > 2048 && C <= 256) ? 128 : 64;
+}
+
 PDT_API long pdt_rows_reduce_workspace(int R, int C) {
-  int G = R > 256 ? 64 : 0;
+  const int G = rows_groups(R, C);
   return G ? 2L * G * C : 0;
 }
 
@@ -418,8 +455,8 @@ PDT_API long pdt_rows_reduce_workspace(int R, int C) {
 // fence per block, which on the multi-XCD MI355X writes back L2 -- measured
 // ~2.4x slower than the two launches).
 static const float* rows_reduce(const float* part, int* R, int C, hipStream_t st) {
-  if (*R <= 256) return part;
-  const int G = 64;
+  const int G = rows_groups(*R, C);
+  if (G == 0) return part;
   float* out = const_cast<float*>(part) + 2L * (*R) * C;  // workspace tail
   hipLaunchKernelGGL(rows_reduce_kernel, dim3((C + 63) / 64, G), dim3(256), 0, st, part, out, *R, C, G);
   *R = G;

@@ -1,0 +1,768 @@
+// Implicit-GEMM kernel template shared by conv_igemm.hip (plain epilogues) and
+// conv_igemm_bnb.hip (the fused BatchNorm-backward epilogue instantiations).
+// See conv_igemm.hip for the algorithm.
+#pragma once
+#include "pdt_common.h"
+#include <stdlib.h>
+
+namespace pdt_nt {
+
+// BatchNorm-backward reduction fused into a data-gradient epilogue. The GEMM
+// output (+ addend) is dA, the gradient arriving at a BN(+ReLU) unit's output;
+// instead of a separate pass that re-reads dA and y, the epilogue computes
+// per-channel partials of g = relu_gate(dA) over its rows:
+//   part[row0 + r][c] = sum g,   part[R + row0 + r][c] = sum g * (y - mean)
+// (the layout pdt_bn_bwd_finalize reduces). dA is stored UNGATED (it stays the
+// true gradient of the unit's output); g uses the bf16-rounded stored value,
+// exactly what the reduce pass would have read.
+struct BnbArgs {
+  const u16* y;          // the unit's pre-BN conv output, same layout as the GEMM output
+  const float* mean;     // [Ncol]
+  const float* scale;    // [Ncol] (ReLU gate recomputed from y when mask == nullptr)
+  const float* shift;
+  const uint8_t* mask;   // optional ReLU bit mask of the unit's output
+  float* part;           // nullptr = disabled
+  int relu, row0, R;
+};
+
+struct NTParams {
+  const u16* src;
+  const u16* b;
+  u16* out;
+  float* stats;        // optional: [2][nstat_rows][Ncol] partial sums (sum, sumsq)
+  const float* bias;   // optional: [Ncol]
+  const u16* addend;   // optional: out = conv + addend (same layout as out)
+  int Hs, Ws, Cs;      // source geometry (NHWC, batch implied by M-grid)
+  int Hm, Wm;          // M-grid per image
+  int M, Ncol, K, ldb;
+  int sh, sw, oh0, ow0, dh, dw, nth, ntw;
+  int Ho, Wo, osh, osw, oph, opw, ldo;
+  int act;             // 0 none, 1 relu, 2 gelu(tanh)
+  u16* aux;            // optional: pre-activation copy of the output (same layout)
+  int nstat_rows;
+  int nt_store;        // 1: non-temporal (streaming) output stores
+  int ident_out;       // 1: output row == m (no stride-phase remap) -> skip the index math
+  const uint8_t* addend_mask;  // optional: addend is masked by this ReLU bit mask (1 bit / element)
+  const float* dq_a;   // fp8 only: dequant scale of the A (src) operand (device scalar)
+  const float* dq_b;   // fp8 only: dequant scale of the B operand
+  BnbArgs bnb;         // optional: BatchNorm-backward partial sums of the unit this output feeds
+  FastDiv div_Wm, div_HWm, div_Cs8, div_ntw;
+};
+
+constexpr int BK = 64;
+constexpr int NT = 256;
+
+__device__ __forceinline__ int swz(int row, int chunk) { return chunk ^ ((row >> 1) & 7); }
+
+typedef int i32x8 __attribute__((ext_vector_type(8)));
+__device__ __forceinline__ i32x8 cat8(const bf16x8& lo, const bf16x8& hi) {
+  const u32x4 a = __builtin_bit_cast(u32x4, lo), b = __builtin_bit_cast(u32x4, hi);
+  return i32x8{(int)a[0], (int)a[1], (int)a[2], (int)a[3], (int)b[0], (int)b[1], (int)b[2], (int)b[3]};
+}
+
+// 16 zero bytes: the global_load_lds source for padding / out-of-range rows
+static __device__ __attribute__((aligned(64))) u32x4 pdt_zero_chunk[4];
+
+// F8 = 0: bf16 operands. F8 = 1 / 2: fp8 operands (B = OCP e4m3; src = e4m3 / e5m2)
+// handled as byte PAIRS -- every index below is in 2-byte units, so staging,
+// swizzle and gather are unchanged -- and one block-scaled
+// mfma_scale_f32_16x16x128_f8f6f4 (2x the bf16 MFMA rate, unit block scales)
+// consumes a whole 128-byte LDS k-row: the two bf16 k-step fragments of a lane
+// ARE its 32-byte fp8 fragment (a k permutation shared by both operands).
+// The per-tensor dequant scales multiply the accumulators in the epilogue.
+template <int BM, int BN, int NSTAGE, bool CS64, bool DIRECT, bool GLDS, int NTH = 256, int WM = 2, int F8 = 0,
+          bool PIPE = false, bool BNB = false>
+__global__ void __launch_bounds__(NTH, PIPE ? 1 : 2) conv_nt_kernel(NTParams p) {
+  constexpr int WN = NTH / 64 / WM;       // waves along N
+  constexpr int MI = BM / (WM * 16);      // 16-row MFMA tiles per wave
+  constexpr int NI = BN / (WN * 16);
+  constexpr int LA = BM * 8 / NTH;        // 16-B A chunks each thread stages per K-tile
+  constexpr int LB = BN * 8 / NTH;
+  constexpr int RS = NTH / 8;             // rows covered by one staging pass
+  constexpr int A_BYTES = BM * BK * 2;
+  constexpr int B_BYTES = BN * BK * 2;
+  constexpr int STAGE = A_BYTES + B_BYTES;
+  constexpr int C_STRIDE = BN * 2 + 16;  // bytes per staged output row
+  constexpr int CST = (DIRECT && !BNB) ? 0 : BM * C_STRIDE;  // epilogue staging bytes (BNB always stages)
+  constexpr int SMEM = (NSTAGE * STAGE > CST) ? NSTAGE * STAGE : CST;
+  __shared__ __attribute__((aligned(16))) char smem[SMEM];
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = tid >> 6;
+  const int wm = wave / WN, wn = wave % WN;
+
+  const int ntm = (p.M + BM - 1) / BM;
+  const int ntn = (p.Ncol + BN - 1) / BN;
+  const uint32_t logical = xcd_remap(blockIdx.x, ntm * ntn);
+  const int tm = logical / ntn, tn = logical % ntn;
+  const int m0 = tm * BM, n0 = tn * BN;
+
+  // ---- per-thread A rows: r = tid/8 + 32*i, chunk column ca = tid%8
+  const int ca = tid & 7;
+  int a_base[LA], a_ih[LA], a_iw[LA];
+  bool a_ok[LA];
+#pragma unroll
+  for (int i = 0; i < LA; ++i) {
+    int m = m0 + (tid >> 3) + RS * i;
+    a_ok[i] = m < p.M;
+    uint32_t mm = a_ok[i] ? m : 0;
+    uint32_t img = fdiv(mm, p.div_HWm);
+    uint32_t rem = mm - img * (uint32_t)(p.Hm * p.Wm);
+    uint32_t oh = fdiv(rem, p.div_Wm);
+    uint32_t ow = rem - oh * p.Wm;
+    a_base[i] = img * p.Hs * p.Ws;
+    a_ih[i] = oh * p.sh + p.oh0;
+    a_iw[i] = ow * p.sw + p.ow0;
+  }
+  // ---- per-thread B rows
+  int b_row[LB];
+  bool b_ok[LB];
+#pragma unroll
+  for (int j = 0; j < LB; ++j) {
+    int n = n0 + (tid >> 3) + RS * j;
+    b_ok[j] = n < p.Ncol;
+    b_row[j] = b_ok[j] ? n : 0;
+  }
+
+  u32x4 ra[LA], rb[LB];
+  const int nk = (p.K + BK - 1) / BK;
+
+  auto load_tile = [&](int kt) {
+    const int k0 = kt * BK;
+    if (CS64) {
+      const int tap = k0 / p.Cs;
+      const int c0 = k0 - tap * p.Cs + ca * 8;
+      const int th = fdiv(tap, p.div_ntw);
+      const int tw = tap - th * p.ntw;
+      const int dho = p.dh * th, dwo = p.dw * tw;
+#pragma unroll
+      for (int i = 0; i < LA; ++i) {
+        int ih = a_ih[i] + dho, iw = a_iw[i] + dwo;
+        bool ok = a_ok[i] && (unsigned)ih < (unsigned)p.Hs && (unsigned)iw < (unsigned)p.Ws;
+        if (ok) {
+          ra[i] = *reinterpret_cast<const u32x4*>(p.src + (size_t)(a_base[i] + ih * p.Ws + iw) * p.Cs + c0);
+        } else {
+          ra[i] = u32x4{0, 0, 0, 0};
+        }
+      }
+    } else {
+      const int kc = k0 / 8 + ca;  // global 8-channel chunk index
+      const bool kin = kc * 8 < p.K;
+      const int tap = fdiv(kc, p.div_Cs8);
+      const int c0 = (kc - tap * (p.Cs / 8)) * 8;
+      const int th = fdiv(tap, p.div_ntw);
+      const int tw = tap - th * p.ntw;
+      const int dho = p.dh * th, dwo = p.dw * tw;
+#pragma unroll
+      for (int i = 0; i < LA; ++i) {
+        int ih = a_ih[i] + dho, iw = a_iw[i] + dwo;
+        bool ok = kin && a_ok[i] && (unsigned)ih < (unsigned)p.Hs && (unsigned)iw < (unsigned)p.Ws;
+        if (ok) {
+          ra[i] = *reinterpret_cast<const u32x4*>(p.src + (size_t)(a_base[i] + ih * p.Ws + iw) * p.Cs + c0);
+        } else {
+          ra[i] = u32x4{0, 0, 0, 0};
+        }
+      }
+    }
+    const int kb = k0 + ca * 8;
+#pragma unroll
+    for (int j = 0; j < LB; ++j) {
+      if (b_ok[j] && kb < p.K) {
+        rb[j] = *reinterpret_cast<const u32x4*>(p.b + (size_t)b_row[j] * p.ldb + kb);
+      } else {
+        rb[j] = u32x4{0, 0, 0, 0};
+      }
+    }
+  };
+
+  auto store_tile = [&](int buf) {
+    char* sa = smem + buf * STAGE;
+    char* sb = sa + A_BYTES;
+#pragma unroll
+    for (int i = 0; i < LA; ++i) {
+      int r = (tid >> 3) + RS * i;
+      *reinterpret_cast<u32x4*>(sa + r * 128 + swz(r, ca) * 16) = ra[i];
+    }
+#pragma unroll
+    for (int j = 0; j < LB; ++j) {
+      int r = (tid >> 3) + RS * j;
+      *reinterpret_cast<u32x4*>(sb + r * 128 + swz(r, ca) * 16) = rb[j];
+    }
+  };
+
+  // GLDS: global_load_lds_dwordx4 straight into LDS (no VGPR staging). The
+  // LDS image stays lane-linear per wave instruction (8 rows x 128 B), so the
+  // XOR swizzle moves to the SOURCE: lane (row r, physical chunk ca) fetches
+  // logical chunk ca ^ swz(r). Padding / out-of-range rows read a zero page.
+  auto glds_tile = [&](int kt, int buf) {
+    char* sa = smem + buf * STAGE;
+    char* sb = sa + A_BYTES;
+    const int k0 = kt * BK;
+#pragma unroll
+    for (int i = 0; i < LA; ++i) {
+      const int r = (tid >> 3) + RS * i;
+      const int c = swz(r, ca);  // logical chunk for this lane's LDS slot
+      const void* g = pdt_zero_chunk;
+      if (CS64) {
+        const int tap = k0 / p.Cs;
+        const int c0 = k0 - tap * p.Cs + c * 8;
+        const int th = fdiv(tap, p.div_ntw);
+        const int tw = tap - th * p.ntw;
+        const int ih = a_ih[i] + p.dh * th, iw = a_iw[i] + p.dw * tw;
+        if (a_ok[i] && (unsigned)ih < (unsigned)p.Hs && (unsigned)iw < (unsigned)p.Ws)
+          g = p.src + (size_t)(a_base[i] + ih * p.Ws + iw) * p.Cs + c0;
+      } else {
+        const int kc = k0 / 8 + c;
+        const int tap = fdiv(kc, p.div_Cs8);
+        const int c0 = (kc - tap * (p.Cs / 8)) * 8;
+        const int th = fdiv(tap, p.div_ntw);
+        const int tw = tap - th * p.ntw;
+        const int ih = a_ih[i] + p.dh * th, iw = a_iw[i] + p.dw * tw;
+        if (kc * 8 < p.K && a_ok[i] && (unsigned)ih < (unsigned)p.Hs && (unsigned)iw < (unsigned)p.Ws)
+          g = p.src + (size_t)(a_base[i] + ih * p.Ws + iw) * p.Cs + c0;
+      }
+      __builtin_amdgcn_global_load_lds(
+          g, (__attribute__((address_space(3))) void*)(sa + (8 * wave + RS * i) * 128), 16, 0, 0);
+    }
+#pragma unroll
+    for (int j = 0; j < LB; ++j) {
+      const int r = (tid >> 3) + RS * j;
+      const int kb = k0 + swz(r, ca) * 8;
+      const void* g = (b_ok[j] && kb < p.K) ? (const void*)(p.b + (size_t)b_row[j] * p.ldb + kb)
+                                            : (const void*)pdt_zero_chunk;
+      __builtin_amdgcn_global_load_lds(
+          g, (__attribute__((address_space(3))) void*)(sb + (8 * wave + RS * j) * 128), 16, 0, 0);
+    }
+  };
+
+  f32x4 acc[MI][NI];
+#pragma unroll
+  for (int i = 0; i < MI; ++i)
+#pragma unroll
+    for (int j = 0; j < NI; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  // one K-tile of MFMA work on the LDS stage at sa / sb
+  auto compute_tile = [&](const char* sa, const char* sb) {
+    if constexpr (F8 != 0) {
+      bf16x8 af[2][MI], bfr[2][NI];
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) {
+        const int kch = kk * 4 + (lane >> 4);
+#pragma unroll
+        for (int i = 0; i < MI; ++i) {
+          int r = wm * (BM / WM) + i * 16 + (lane & 15);
+          af[kk][i] = *reinterpret_cast<const bf16x8*>(sa + r * 128 + swz(r, kch) * 16);
+        }
+#pragma unroll
+        for (int j = 0; j < NI; ++j) {
+          int r = wn * (BN / WN) + j * 16 + (lane & 15);
+          bfr[kk][j] = *reinterpret_cast<const bf16x8*>(sb + r * 128 + swz(r, kch) * 16);
+        }
+      }
+      if (PIPE) __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int i = 0; i < MI; ++i)
+#pragma unroll
+        for (int j = 0; j < NI; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(
+              cat8(bfr[0][j], bfr[1][j]), cat8(af[0][i], af[1][i]), acc[i][j], 0, F8 == 2 ? 1 : 0, 0, 127, 0, 127);
+      if (PIPE) __builtin_amdgcn_s_setprio(0);
+    } else {
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) {
+        const int kch = kk * 4 + (lane >> 4);
+        bf16x8 af[MI], bfr[NI];
+#pragma unroll
+        for (int i = 0; i < MI; ++i) {
+          int r = wm * (BM / WM) + i * 16 + (lane & 15);
+          af[i] = *reinterpret_cast<const bf16x8*>(sa + r * 128 + swz(r, kch) * 16);
+        }
+#pragma unroll
+        for (int j = 0; j < NI; ++j) {
+          int r = wn * (BN / WN) + j * 16 + (lane & 15);
+          bfr[j] = *reinterpret_cast<const bf16x8*>(sb + r * 128 + swz(r, kch) * 16);
+        }
+        if (PIPE) __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+        for (int i = 0; i < MI; ++i)
+#pragma unroll
+          for (int j = 0; j < NI; ++j)
+            // swapped operands: lane holds 4 consecutive output channels of one row
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[j], af[i], acc[i][j], 0, 0, 0);
+        if (PIPE) __builtin_amdgcn_s_setprio(0);
+      }
+    }
+  };
+
+  if constexpr (PIPE) {
+    // NSTAGE-deep LDS-DMA ring, ONE raw barrier per K-tile: tile kt+NSTAGE-1
+    // is issued right after the barrier that proves every wave finished
+    // reading its buffer (tile kt-1's); the counted vmcnt before the barrier
+    // retires only this thread's tile-kt DMA (with 3 stages tile kt+1's stays
+    // in flight across it). No __syncthreads (vmcnt(0) lgkmcnt(0)) in the loop.
+    static_assert(GLDS && (NSTAGE == 2 || NSTAGE == 3), "the ring is the LDS-DMA pipeline");
+    for (int t = 0; t < NSTAGE - 1; ++t)
+      if (t < nk) glds_tile(t, t);
+    for (int kt = 0; kt < nk; ++kt) {
+      if (NSTAGE == 3 && kt + 1 < nk) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(LA + LB) : "memory");
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+      if (kt + NSTAGE - 1 < nk) glds_tile(kt + NSTAGE - 1, (kt + NSTAGE - 1) % NSTAGE);
+      const char* sa = smem + (kt % NSTAGE) * STAGE;
+      compute_tile(sa, sa + A_BYTES);
+    }
+    if (!DIRECT) __syncthreads();  // before the epilogue reuses LDS
+  } else {
+  if (GLDS) {
+    if (nk > 0) glds_tile(0, 0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  } else if (nk > 0) {
+    load_tile(0);
+    store_tile(0);
+  }
+  __syncthreads();
+
+  for (int kt = 0; kt < nk; ++kt) {
+    const int cur = NSTAGE == 2 ? (kt & 1) : 0;
+    if (GLDS) {
+      if (NSTAGE == 2 && kt + 1 < nk) glds_tile(kt + 1, cur ^ 1);
+    } else if (kt + 1 < nk) {
+      load_tile(kt + 1);
+    }
+    const char* sa = smem + cur * STAGE;
+    compute_tile(sa, sa + A_BYTES);
+    if (GLDS) {
+      if (NSTAGE == 2) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // my DMA into the other buffer landed
+        __syncthreads();                                   // ... and everyone's; buffer cur is free
+      } else if (kt + 1 < nk) {
+        __syncthreads();
+        glds_tile(kt + 1, 0);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+      }
+    } else if (NSTAGE == 2) {
+      if (kt + 1 < nk) store_tile(cur ^ 1);
+      __syncthreads();
+    } else if (kt + 1 < nk) {
+      __syncthreads();  // everyone is done reading the single buffer
+      store_tile(0);
+      __syncthreads();
+    }
+  }
+  if (NSTAGE == 1 && !DIRECT) __syncthreads();  // before the epilogue reuses LDS
+  }
+
+  // ---------------------------------------------------------------- epilogue
+  // acc[i][j][r] = C[row = wm*BM/2 + i*16 + (lane&15)][col = wn*BN/2 + j*16 + (lane>>4)*4 + r]
+  const int lrow = lane & 15;
+  const int lcol = (lane >> 4) * 4;
+  if constexpr (F8 != 0) {
+    const float alpha = p.dq_a[0] * p.dq_b[0];
+#pragma unroll
+    for (int i = 0; i < MI; ++i)
+#pragma unroll
+      for (int j = 0; j < NI; ++j) acc[i][j] *= alpha;
+  }
+  if (p.bias != nullptr) {
+#pragma unroll
+    for (int j = 0; j < NI; ++j) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        int col = n0 + wn * (BN / WN) + j * 16 + lcol + r;
+        float bv = col < p.Ncol ? p.bias[col] : 0.f;
+#pragma unroll
+        for (int i = 0; i < MI; ++i) acc[i][j][r] += bv;
+      }
+    }
+  }
+
+  if constexpr (BNB) {
+    // Fused BatchNorm-backward partials (BnbArgs). The bf16 tile is staged
+    // through LDS as in the plain epilogue; each thread then owns one 16-B
+    // chunk column (8 channels) and walks rows, so y / addend are read -- and
+    // dA written -- as coalesced 16-B row chunks, exactly the bytes the
+    // separate reduce pass would have read. Loads of IB rows are issued before
+    // any is consumed. Output = bf16(bf16(acc) + masked addend): bit-identical
+    // to the plain data gradient; the partials see that stored value.
+    // Partial rows: one per M-tile (lanes, then waves, reduced in-block).
+    constexpr int CPR = BN / 8;
+    constexpr int RPI = NTH / CPR;        // rows covered per pass
+    constexpr int NIT = BM / RPI;         // passes
+    constexpr int IB = NIT < 4 ? NIT : 4;  // rows in flight per thread
+    static_assert(NTH % CPR == 0 && BM % RPI == 0, "chunk-column ownership");
+    __syncthreads();  // all waves are done with the operand stages
+#pragma unroll
+    for (int i = 0; i < MI; ++i)
+#pragma unroll
+      for (int j = 0; j < NI; ++j) {
+        int r = wm * (BM / WM) + i * 16 + lrow;
+        int c = wn * (BN / WN) + j * 16 + lcol;
+        uint2 w;
+        w.x = pack2bf(acc[i][j][0], acc[i][j][1]);
+        w.y = pack2bf(acc[i][j][2], acc[i][j][3]);
+        *reinterpret_cast<uint2*>(smem + r * C_STRIDE + c * 2) = w;
+      }
+    __syncthreads();
+    const int cc = tid % CPR, r0 = tid / CPR;
+    const int col = n0 + cc * 8;
+    const bool cok = col < p.Ncol;
+    const int colc = cok ? col : 0;
+    const bool has_add = p.addend != nullptr, has_amask = p.addend_mask != nullptr;
+    const bool has_mask = p.bnb.mask != nullptr, gate_y = p.bnb.relu && !has_mask;
+    float mu[8], sc[8], sh[8], s[8], q[8];
+    {
+      const f32x4 m0v = *reinterpret_cast<const f32x4*>(p.bnb.mean + colc);
+      const f32x4 m1v = *reinterpret_cast<const f32x4*>(p.bnb.mean + colc + 4);
+      f32x4 s0 = {0.f, 0.f, 0.f, 0.f}, s1 = s0, h0 = s0, h1 = s0;
+      if (gate_y) {
+        s0 = *reinterpret_cast<const f32x4*>(p.bnb.scale + colc);
+        s1 = *reinterpret_cast<const f32x4*>(p.bnb.scale + colc + 4);
+        h0 = *reinterpret_cast<const f32x4*>(p.bnb.shift + colc);
+        h1 = *reinterpret_cast<const f32x4*>(p.bnb.shift + colc + 4);
+      }
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        mu[k] = m0v[k]; mu[k + 4] = m1v[k];
+        sc[k] = s0[k]; sc[k + 4] = s1[k];
+        sh[k] = h0[k]; sh[k + 4] = h1[k];
+      }
+#pragma unroll
+      for (int k = 0; k < 8; ++k) s[k] = q[k] = 0.f;
+    }
+#pragma unroll
+    for (int it0 = 0; it0 < NIT; it0 += IB) {
+      uint32_t eo[IB];
+      bool rok[IB];
+      u32x4 yv4[IB], ad4[IB];
+      uint32_t amb[IB], mkb[IB];
+#pragma unroll
+      for (int b = 0; b < IB; ++b) {
+        const int m = m0 + r0 + (it0 + b) * RPI;
+        rok[b] = cok && m < p.M;
+        const uint32_t mm = m < p.M ? m : 0;
+        uint32_t orow = mm;
+        if (!p.ident_out) {
+          uint32_t img = fdiv(mm, p.div_HWm);
+          uint32_t rem = mm - img * (uint32_t)(p.Hm * p.Wm);
+          uint32_t oh = fdiv(rem, p.div_Wm);
+          uint32_t ow = rem - oh * p.Wm;
+          orow = (img * p.Ho + oh * p.osh + p.oph) * p.Wo + ow * p.osw + p.opw;
+        }
+        eo[b] = orow * (uint32_t)p.ldo + colc;  // host guarantees rows * ldo < 2^31
+        yv4[b] = *reinterpret_cast<const u32x4*>(p.bnb.y + eo[b]);
+        ad4[b] = has_add ? *reinterpret_cast<const u32x4*>(p.addend + eo[b]) : u32x4{0u, 0u, 0u, 0u};
+        amb[b] = has_amask ? (uint32_t)p.addend_mask[eo[b] >> 3] : 0xffu;
+        mkb[b] = has_mask ? (uint32_t)p.bnb.mask[eo[b] >> 3] : 0xffu;
+      }
+#pragma unroll
+      for (int b = 0; b < IB; ++b) {
+        const int r = r0 + (it0 + b) * RPI;
+        u32x4 v = *reinterpret_cast<const u32x4*>(smem + r * C_STRIDE + cc * 16);
+        if (has_add) {
+          u32x4 a = ad4[b];
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            a[e] &= ((amb[b] >> (2 * e)) & 1u ? 0xffffu : 0u) | ((amb[b] >> (2 * e + 1)) & 1u ? 0xffff0000u : 0u);
+            v[e] = pack2bf(lo_bf(v[e]) + lo_bf(a[e]), hi_bf(v[e]) + hi_bf(a[e]));
+          }
+        }
+        if (rok[b]) *reinterpret_cast<u32x4*>(p.out + eo[b]) = v;
+        float g[8], yf[8];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          g[2 * e] = lo_bf(v[e]); g[2 * e + 1] = hi_bf(v[e]);
+          yf[2 * e] = lo_bf(yv4[b][e]); yf[2 * e + 1] = hi_bf(yv4[b][e]);
+        }
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          bool on = rok[b];
+          if (p.bnb.relu) on = on && (has_mask ? ((mkb[b] >> k) & 1u) != 0 : (yf[k] * sc[k] + sh[k]) > 0.f);
+          const float gg = on ? g[k] : 0.f;
+          s[k] += gg;
+          q[k] += gg * (yf[k] - mu[k]);
+        }
+      }
+    }
+    // lanes sharing a chunk column: lane, lane ^ CPR, ... (CPR < 64)
+#pragma unroll
+    for (int o = CPR; o < 64; o <<= 1)
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        s[k] += __shfl_xor(s[k], o, 64);
+        q[k] += __shfl_xor(q[k], o, 64);
+      }
+    constexpr int NW = NTH / 64;
+    float* red = reinterpret_cast<float*>(smem);  // [NW][CPR][16], staging reads are done after the barrier
+    __syncthreads();
+    if (lane < CPR) {
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        red[(wave * CPR + lane) * 16 + k] = s[k];
+        red[(wave * CPR + lane) * 16 + 8 + k] = q[k];
+      }
+    }
+    __syncthreads();
+    const int srow = p.bnb.row0 + tm;
+    for (int t = tid; t < CPR * 16; t += NTH) {
+      const int c8 = t / 16, k = t % 16;
+      float acc_w = 0.f;
+#pragma unroll
+      for (int w = 0; w < NW; ++w) acc_w += red[(w * CPR + c8) * 16 + k];
+      const int cl = n0 + c8 * 8 + (k & 7);
+      if (cl < p.Ncol) p.bnb.part[(size_t)(k < 8 ? srow : p.bnb.R + srow) * p.Ncol + cl] = acc_w;
+    }
+    return;
+  }
+
+  if (p.stats != nullptr) {
+    // per-wave column partials over its BM/2 rows (invalid rows hold zeros)
+    const int srow = tm * WM + wm;
+#pragma unroll
+    for (int j = 0; j < NI; ++j) {
+      float s[4], q[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        float a = 0.f, b = 0.f;
+#pragma unroll
+        for (int i = 0; i < MI; ++i) {
+          float v = acc[i][j][r];
+          a += v;
+          b += v * v;
+        }
+        s[r] = a;
+        q[r] = b;
+      }
+#pragma unroll
+      for (int o = 1; o < 16; o <<= 1) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          s[r] += __shfl_xor(s[r], o, 64);
+          q[r] += __shfl_xor(q[r], o, 64);
+        }
+      }
+      if (lrow == 0) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          int col = n0 + wn * (BN / WN) + j * 16 + lcol + r;
+          if (col < p.Ncol) {
+            p.stats[(size_t)srow * p.Ncol + col] = s[r];
+            p.stats[(size_t)(p.nstat_rows + srow) * p.Ncol + col] = q[r];
+          }
+        }
+      }
+    }
+  }
+
+  // stage the bf16 tile through LDS (row-major [BM][BN], 16-B row pad) and
+  // write 16-B coalesced rows; `pre` = pre-activation copy (aux output)
+  constexpr int CPR = BN / 8;  // 16-B chunks per row
+  // DIRECT: each lane stores its 4 consecutive channels (8 B) straight to HBM
+  // (no LDS round trip / barrier); L2 merges the 32-B row pieces into lines.
+  auto direct_store = [&](u16* dst, const u16* addend) {
+#pragma unroll
+    for (int i = 0; i < MI; ++i) {
+      int m = m0 + wm * (BM / WM) + i * 16 + lrow;
+      if (m >= p.M) continue;
+      size_t orow = m;
+      if (!p.ident_out) {
+        uint32_t img = fdiv(m, p.div_HWm);
+        uint32_t rem = m - img * (uint32_t)(p.Hm * p.Wm);
+        uint32_t oh = fdiv(rem, p.div_Wm);
+        uint32_t ow = rem - oh * p.Wm;
+        orow = ((size_t)img * p.Ho + oh * p.osh + p.oph) * p.Wo + ow * p.osw + p.opw;
+      }
+#pragma unroll
+      for (int j = 0; j < NI; ++j) {
+        int col = n0 + wn * (BN / WN) + j * 16 + lcol;
+        if (col >= p.Ncol) continue;
+        float v0 = acc[i][j][0], v1 = acc[i][j][1], v2 = acc[i][j][2], v3 = acc[i][j][3];
+        if (addend != nullptr) {
+          uint2 a = *reinterpret_cast<const uint2*>(addend + orow * p.ldo + col);
+          if (p.addend_mask != nullptr) {
+            const size_t e = orow * p.ldo + col;
+            const uint32_t mb = p.addend_mask[e >> 3] >> (e & 7);
+            a.x &= ((mb & 1u) ? 0xffffu : 0u) | ((mb & 2u) ? 0xffff0000u : 0u);
+            a.y &= ((mb & 4u) ? 0xffffu : 0u) | ((mb & 8u) ? 0xffff0000u : 0u);
+          }
+          v0 += lo_bf(a.x); v1 += hi_bf(a.x); v2 += lo_bf(a.y); v3 += hi_bf(a.y);
+        }
+        uint2 w;
+        w.x = pack2bf(v0, v1);
+        w.y = pack2bf(v2, v3);
+        typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+        u32x2 w2 = {w.x, w.y};
+        u32x2* dp = reinterpret_cast<u32x2*>(dst + orow * p.ldo + col);
+        if (p.nt_store) __builtin_nontemporal_store(w2, dp);
+        else *dp = w2;
+      }
+    }
+  };
+
+  auto stage_store = [&](u16* dst, const u16* addend) {
+    if (DIRECT) {
+      direct_store(dst, addend);
+      return;
+    }
+#pragma unroll
+    for (int i = 0; i < MI; ++i) {
+#pragma unroll
+      for (int j = 0; j < NI; ++j) {
+        int r = wm * (BM / WM) + i * 16 + lrow;
+        int c = wn * (BN / WN) + j * 16 + lcol;
+        uint2 w;
+        w.x = pack2bf(acc[i][j][0], acc[i][j][1]);
+        w.y = pack2bf(acc[i][j][2], acc[i][j][3]);
+        *reinterpret_cast<uint2*>(smem + r * C_STRIDE + c * 2) = w;
+      }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int it = 0; it < (BM * CPR) / NTH; ++it) {
+      int q = tid + it * NTH;
+      int r = q / CPR, cc = q % CPR;
+      int m = m0 + r;
+      int col = n0 + cc * 8;
+      if (m < p.M && col < p.Ncol) {
+        u32x4 v = *reinterpret_cast<const u32x4*>(smem + r * C_STRIDE + cc * 16);
+        size_t orow = m;
+        if (!p.ident_out) {
+          uint32_t img = fdiv(m, p.div_HWm);
+          uint32_t rem = m - img * (uint32_t)(p.Hm * p.Wm);
+          uint32_t oh = fdiv(rem, p.div_Wm);
+          uint32_t ow = rem - oh * p.Wm;
+          orow = ((size_t)img * p.Ho + oh * p.osh + p.oph) * p.Wo + ow * p.osw + p.opw;
+        }
+        if (addend != nullptr) {
+          u32x4 a = *reinterpret_cast<const u32x4*>(addend + orow * p.ldo + col);
+          if (p.addend_mask != nullptr) {
+            const uint32_t mb = p.addend_mask[(orow * p.ldo + col) >> 3];
+#pragma unroll
+            for (int e = 0; e < 4; ++e)
+              a[e] &= ((mb >> (2 * e)) & 1u ? 0xffffu : 0u) | ((mb >> (2 * e + 1)) & 1u ? 0xffff0000u : 0u);
+          }
+#pragma unroll
+          for (int e = 0; e < 4; ++e) v[e] = pack2bf(lo_bf(v[e]) + lo_bf(a[e]), hi_bf(v[e]) + hi_bf(a[e]));
+        }
+        u32x4* dp = reinterpret_cast<u32x4*>(dst + orow * p.ldo + col);
+        if (p.nt_store) __builtin_nontemporal_store(v, dp);
+        else *dp = v;
+      }
+    }
+  };
+
+  if (p.aux != nullptr) {
+    stage_store(p.aux, nullptr);
+    if (!DIRECT) __syncthreads();
+  }
+  if (p.act != 0) {
+#pragma unroll
+    for (int i = 0; i < MI; ++i)
+#pragma unroll
+      for (int j = 0; j < NI; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          float x = acc[i][j][r];
+          if (p.act == 1) {
+            x = fmaxf(x, 0.f);
+          } else {
+            float u = 0.7978845608f * (x + 0.044715f * x * x * x);
+            x = 0.5f * x * (1.f + tanhf(u));
+          }
+          acc[i][j][r] = x;
+        }
+  }
+  stage_store(p.out, p.addend);
+}
+
+template <int BM, int BN, int NS, bool CS64, bool DIRECT, bool GLDS = false, int NTH = 256, int WM = 2, int F8 = 0,
+          bool PIPE = false, bool BNB = false>
+int launch(const NTParams& p, hipStream_t st) {
+  int ntm = (p.M + BM - 1) / BM, ntn = (p.Ncol + BN - 1) / BN;
+  hipLaunchKernelGGL((conv_nt_kernel<BM, BN, NS, CS64, DIRECT, GLDS, NTH, WM, F8, PIPE, BNB>), dim3(ntm * ntn),
+                     dim3(NTH), 0, st, p);
+  PDT_RETURN_LAUNCH();
+}
+
+// Tile variants (autotuned per shape from Python; -1 = built-in heuristic).
+//   id : BM x BN, LDS stages
+//   ids 10..19 : the same tiles with the direct (no LDS staging) epilogue
+//   ids 20..29 : the same tiles loaded by global_load_lds (LDS-DMA)
+//   ids 30..33 : 512-thread (8-wave) tiles, 2 stages, 64x64 per wave:
+//                256x128 (4x2 waves) and 128x256 (2x4 waves), each LDS-DMA
+//                and register-staged
+//   ids 34..35 : the 8-wave tiles on the 3-stage LDS-DMA ring (1 barrier per
+//                K-tile, counted vmcnt, s_setprio around the MFMA bursts;
+//                144 KB LDS -> one workgroup of 8 waves per CU)
+//   id 36      : 256x256 (2x4 waves of 128x64), 2-stage ring (128 KB LDS): the
+//                per-wave tile that lifts the LDS-bytes-per-MFMA ratio above the
+//                64x64 tiles' (LDS read bandwidth, not MFMA, bounds those)
+constexpr int NVAR = 37;
+constexpr int VAR_BM[NVAR] = {128, 256, 64, 128, 64, 128, 256, 64, 128, 64,
+                              128, 256, 64, 128, 64, 128, 256, 64, 128, 64,
+                              128, 256, 64, 128, 64, 128, 256, 64, 128, 64,
+                              256, 128, 256, 128, 256, 128, 256};
+constexpr int VAR_BN[NVAR] = {128, 64, 128, 64, 64, 128, 64, 128, 64, 64,
+                              128, 64, 128, 64, 64, 128, 64, 128, 64, 64,
+                              128, 64, 128, 64, 64, 128, 64, 128, 64, 64,
+                              128, 256, 128, 256, 128, 256, 256};
+constexpr int VAR_WM[NVAR] = {2, 2, 2, 2, 2, 2, 2, 2, 2, 2, 2, 2, 2, 2, 2, 2, 2, 2, 2, 2,
+                              2, 2, 2, 2, 2, 2, 2, 2, 2, 2, 4, 2, 4, 2, 4, 2, 2};
+
+inline int heuristic_variant(int M, int Ncol, int K) {
+  (void)M;
+  if (Ncol <= 64) return K <= 64 ? 6 : 1;
+  return K <= 64 ? 5 : 0;
+}
+
+template <bool CS64, bool BNB = false>
+int launch_variant(int v, const NTParams& p, hipStream_t st) {
+  switch (v) {
+    case 0: return launch<128, 128, 2, CS64, false, false, 256, 2, 0, false, BNB>(p, st);
+    case 1: return launch<256, 64, 2, CS64, false, false, 256, 2, 0, false, BNB>(p, st);
+    case 2: return launch<64, 128, 2, CS64, false, false, 256, 2, 0, false, BNB>(p, st);
+    case 3: return launch<128, 64, 2, CS64, false, false, 256, 2, 0, false, BNB>(p, st);
+    case 4: return launch<64, 64, 2, CS64, false, false, 256, 2, 0, false, BNB>(p, st);
+    case 5: return launch<128, 128, 1, CS64, false, false, 256, 2, 0, false, BNB>(p, st);
+    case 6: return launch<256, 64, 1, CS64, false, false, 256, 2, 0, false, BNB>(p, st);
+    case 7: return launch<64, 128, 1, CS64, false, false, 256, 2, 0, false, BNB>(p, st);
+    case 8: return launch<128, 64, 1, CS64, false, false, 256, 2, 0, false, BNB>(p, st);
+    case 9: return launch<64, 64, 1, CS64, false, false, 256, 2, 0, false, BNB>(p, st);
+    case 10: return launch<128, 128, 2, CS64, true, false, 256, 2, 0, false, BNB>(p, st);
+    case 11: return launch<256, 64, 2, CS64, true, false, 256, 2, 0, false, BNB>(p, st);
+    case 12: return launch<64, 128, 2, CS64, true, false, 256, 2, 0, false, BNB>(p, st);
+    case 13: return launch<128, 64, 2, CS64, true, false, 256, 2, 0, false, BNB>(p, st);
+    case 14: return launch<64, 64, 2, CS64, true, false, 256, 2, 0, false, BNB>(p, st);
+    case 15: return launch<128, 128, 1, CS64, true, false, 256, 2, 0, false, BNB>(p, st);
+    case 16: return launch<256, 64, 1, CS64, true, false, 256, 2, 0, false, BNB>(p, st);
+    case 17: return launch<64, 128, 1, CS64, true, false, 256, 2, 0, false, BNB>(p, st);
+    case 18: return launch<128, 64, 1, CS64, true, false, 256, 2, 0, false, BNB>(p, st);
+    case 19: return launch<64, 64, 1, CS64, true, false, 256, 2, 0, false, BNB>(p, st);
+    case 20: return launch<128, 128, 2, CS64, false, true, 256, 2, 0, false, BNB>(p, st);
+    case 21: return launch<256, 64, 2, CS64, false, true, 256, 2, 0, false, BNB>(p, st);
+    case 22: return launch<64, 128, 2, CS64, false, true, 256, 2, 0, false, BNB>(p, st);
+    case 23: return launch<128, 64, 2, CS64, false, true, 256, 2, 0, false, BNB>(p, st);
+    case 24: return launch<64, 64, 2, CS64, false, true, 256, 2, 0, false, BNB>(p, st);
+    case 25: return launch<128, 128, 1, CS64, false, true, 256, 2, 0, false, BNB>(p, st);
+    case 26: return launch<256, 64, 1, CS64, false, true, 256, 2, 0, false, BNB>(p, st);
+    case 27: return launch<64, 128, 1, CS64, false, true, 256, 2, 0, false, BNB>(p, st);
+    case 28: return launch<128, 64, 1, CS64, false, true, 256, 2, 0, false, BNB>(p, st);
+    case 29: return launch<64, 64, 1, CS64, false, true, 256, 2, 0, false, BNB>(p, st);
+    case 30: return launch<256, 128, 2, CS64, false, true, 512, 4, 0, false, BNB>(p, st);
+    case 31: return launch<128, 256, 2, CS64, false, true, 512, 2, 0, false, BNB>(p, st);
+    case 32: return launch<256, 128, 2, CS64, false, false, 512, 4, 0, false, BNB>(p, st);
+    case 33: return launch<128, 256, 2, CS64, false, false, 512, 2, 0, false, BNB>(p, st);
+    case 34: return launch<256, 128, 3, CS64, false, true, 512, 4, 0, true, BNB>(p, st);
+    case 35: return launch<128, 256, 3, CS64, false, true, 512, 2, 0, true, BNB>(p, st);
+    case 36: return launch<256, 256, 2, CS64, false, true, 512, 2, 0, true, BNB>(p, st);
+  }
+  return -3;
+}
+
+
+// the fused BatchNorm-backward instantiations (defined in conv_igemm_bnb.hip)
+int launch_variant_bnb(int v, bool cs64, const NTParams& p, hipStream_t st);
+
+}  // namespace pdt_nt

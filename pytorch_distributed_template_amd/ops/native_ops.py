@@ -30,9 +30,11 @@ P = c_void_p
 
 _SIGS = {
     "pdt_conv_nt_stat_rows": (c_int, [c_int, c_int, c_int, c_int]),
+    "pdt_conv_nt_bnb_rows": (c_int, [c_int, c_int, c_int, c_int]),
     "pdt_conv_nt_num_variants": (c_int, []),
     "pdt_conv_nt_resolve_variant": (c_int, [c_int, c_int, c_int, c_int]),
     "pdt_conv_nt": (c_int, [P, P, P, P, P, P, P] + [c_int] * 25 + [P, c_int, P]),
+    "pdt_conv_nt_bnb": (c_int, [P] * 5 + [c_int] * 25 + [P] * 6 + [c_int] * 3 + [P]),
     "pdt_ln_fwd": (c_int, [P, P, P, P, P, P, c_int, c_int, c_float, P]),
     "pdt_ln_bwd_blocks": (c_int, [c_int]),
     "pdt_ln_bwd": (c_int, [P] * 9 + [c_int, c_int, c_int, P]),
@@ -341,6 +343,13 @@ def conv_nt(src, b, out, *, stats=None, bias=None, relu=False, act=None, variant
          "conv_nt")
 
 
+def _check_addend(addend, out, addend_mask, Ncol):
+    assert addend.dtype == torch.bfloat16 and addend.numel() == out.numel() and addend.is_contiguous(
+        memory_format=torch.channels_last if addend.dim() == 4 else torch.contiguous_format)
+    if addend_mask is not None:
+        assert addend_mask.dtype == torch.uint8 and addend_mask.numel() * 8 == addend.numel()
+
+
 def conv_stat_rows(M, Ncol, K, variant):
     return _load().pdt_conv_nt_stat_rows(M, Ncol, K, variant)
 
@@ -521,8 +530,25 @@ class _DgradWeights:
 _DGRAD_W = _DgradWeights()
 
 
-def _conv_dgrad(dy, w32, N, H, W, Cin, Cout, g, addend=None, addend_mask=None):
-    """dX [N,Cin,H,W] (+ addend) from dY [N,Cout,Ho,Wo] (stride phases, see csrc/conv_igemm.hip)."""
+class _BnbPartials:
+    """BatchNorm-backward partial sums produced by a data-gradient epilogue for one
+    unit (see ``BnbArgs`` in csrc/conv_igemm.hip): [2][R][C] fp32 (+ rows_reduce tail)."""
+    __slots__ = ("part", "R", "unit")
+
+    def __init__(self, part, R, unit):
+        self.part, self.R, self.unit = part, R, unit
+
+
+def _bnb_enabled() -> bool:
+    return os.environ.get("PDT_FUSE_BN_BWD", "1") != "0"
+
+
+def _conv_dgrad(dy, w32, N, H, W, Cin, Cout, g, addend=None, addend_mask=None, bnb_unit=None, bnb_mask=None):
+    """dX [N,Cin,H,W] (+ addend) from dY [N,Cout,Ho,Wo] (stride phases, see csrc/conv_igemm.hip).
+
+    ``bnb_unit``: the conv->BN(->ReLU) unit whose output dX is the gradient of; its
+    BatchNorm-backward reduction (gated by its ReLU -- ``bnb_mask`` or recomputed
+    from y) is computed in the GEMM epilogue. Returns ``(dx, _BnbPartials)`` then."""
     KH, KW, s_h, s_w, ph, pw = g["KH"], g["KW"], g["sh"], g["sw"], g["ph"], g["pw"]
     assert w32.shape[0] == Cout and w32.shape[1] == Cin, (tuple(w32.shape), Cout, Cin)
     assert dy.shape[1] == Cout and dy.numel() == N * Cout * g["Ho"] * g["Wo"]
@@ -532,6 +558,7 @@ def _conv_dgrad(dy, w32, N, H, W, Cin, Cout, g, addend=None, addend_mask=None):
     cacheable = isinstance(w32, nn.Parameter) and w32.dtype == torch.float32 and \
         w32.is_contiguous(memory_format=torch.channels_last)
     w32c = w32 if cacheable else _cl(w32.detach().float())
+    launches = []
     for qh in range(s_h):
         kh0 = (qh + ph) % s_h
         nth = (KH - kh0 + s_h - 1) // s_h if kh0 < KH else 0
@@ -549,10 +576,66 @@ def _conv_dgrad(dy, w32, N, H, W, Cin, Cout, g, addend=None, addend_mask=None):
                 if K > 0:
                     _chk(lib.pdt_wt_dgrad(_p(w32c), _p(wt), Cout, KH, KW, Cin, kh0, kw0, s_h, nth, ntw, _s()),
                          "wt_dgrad")
-            conv_nt(dy, wt, dx, Hs=g["Ho"], Ws=g["Wo"], Cs=Cout, Nimg=N, Hm=H // s_h, Wm=W // s_w, Ncol=Cin,
-                    K=K, ldb=max(K, 8), sh=1, sw=1, oh0=oh0, ow0=ow0, dh=-1, dw=-1, nth=nth, ntw=max(ntw, 0),
-                    Ho=H, Wo=W, osh=s_h, osw=s_w, oph=qh, opw=qw, ldo=Cin, addend=addend, addend_mask=addend_mask)
-    return dx
+            a = dict(Hs=g["Ho"], Ws=g["Wo"], Cs=Cout, Nimg=N, Hm=H // s_h, Wm=W // s_w, Ncol=Cin,
+                     K=K, ldb=max(K, 8), sh=1, sw=1, oh0=oh0, ow0=ow0, dh=-1, dw=-1, nth=nth, ntw=max(ntw, 0),
+                     Ho=H, Wo=W, osh=s_h, osw=s_w, oph=qh, opw=qw, ldo=Cin)
+            if bnb_unit is None:
+                conv_nt(dy, wt, dx, addend=addend, addend_mask=addend_mask, **a)
+            else:
+                launches.append((wt, a))
+    if bnb_unit is None:
+        return dx
+    # fused BN-backward partials: every phase launch writes its own row range
+    u = bnb_unit
+    assert u.Cout == Cin and u.y.numel() == dx.numel() and u.y.is_contiguous(memory_format=torch.channels_last)
+    if addend is not None:
+        _check_addend(addend, dx, addend_mask, Cin)
+    relu = bool(u.relu or bnb_mask is not None)
+    if bnb_mask is not None:
+        assert bnb_mask.dtype == torch.uint8 and bnb_mask.numel() * 8 == dx.numel()
+
+    def launch(wt, a, v, part, row0, R):
+        return lib.pdt_conv_nt_bnb(
+            _p(dy), _p(wt), _p(dx), _p(addend), _p(addend_mask), a["Hs"], a["Ws"], a["Cs"], a["Nimg"], a["Hm"],
+            a["Wm"], a["Ncol"], a["K"], a["ldb"], a["sh"], a["sw"], a["oh0"], a["ow0"], a["dh"], a["dw"], a["nth"],
+            a["ntw"], a["Ho"], a["Wo"], a["osh"], a["osw"], a["oph"], a["opw"], a["ldo"], int(v), _p(u.y),
+            _p(u.mean), _p(u.scale), _p(u.shift), _p(bnb_mask), _p(part), int(relu), int(row0), int(R), _s())
+
+    plan, R = [], 0
+    for wt, a in launches:
+        _check_nt(dy, wt, dx, a)
+        v = _select_bnb_variant(lambda v, part, rows, wt=wt, a=a: launch(wt, a, v, part, 0, rows), a,
+                                addend is not None, bnb_mask is not None, dy.device)
+        rows = lib.pdt_conv_nt_bnb_rows(a["Nimg"] * a["Hm"] * a["Wm"], Cin, a["K"], v)
+        plan.append((wt, a, v, R))
+        R += rows
+    part = torch.empty(2 * R * Cin + lib.pdt_rows_reduce_workspace(R, Cin), dtype=torch.float32, device=dy.device)
+    for wt, a, v, row0 in plan:
+        _chk(launch(wt, a, v, part, row0, R), "conv_nt_bnb")
+    return dx, _BnbPartials(part, R, u)
+
+
+def _select_bnb_variant(launch, a, has_addend, has_mask, device):
+    """Variant for a data gradient with the fused BN-backward epilogue: its own
+    tuned-table key (the epilogue's extra loads / registers shift the best tile)."""
+    geom = ",".join(str(a[k]) for k in ("Hs", "Ws", "Cs", "Nimg", "Hm", "Wm", "Ncol", "K", "sh", "sw", "nth", "ntw",
+                                        "osh"))
+    key = f"ntb2:{geom},{int(has_addend)},{int(has_mask)}"
+    table = _tuned()
+    if key in table:
+        return int(table[key])
+    lib = _load()
+    M = a["Nimg"] * a["Hm"] * a["Wm"]
+    if not _tune_allowed():  # the plain data gradient's tuned tile, else the heuristic
+        plain = f"nt5:{geom},0,0"
+        return int(table[plain]) if plain in table else lib.pdt_conv_nt_resolve_variant(-1, M, a["Ncol"], a["K"])
+    nvar = lib.pdt_conv_nt_num_variants()
+    rows = max(lib.pdt_conv_nt_bnb_rows(M, a["Ncol"], a["K"], v) for v in range(nvar))
+    part = torch.empty(2 * rows * a["Ncol"], dtype=torch.float32, device=device)
+    table[key] = _time_variants(nvar, lambda v: launch(v, part, lib.pdt_conv_nt_bnb_rows(M, a["Ncol"], a["K"], v)),
+                                _variant_filter())
+    _save_tuned()
+    return table[key]
 
 
 def _conv_wgrad(dy, x, N, H, W, Cs, Cout, g, out):
@@ -589,7 +672,7 @@ class _BNArgs:
 class _Unit:
     """Saved state of one conv->BN->act unit between forward and backward."""
     __slots__ = ("x", "w", "gamma", "y", "act", "mask", "mean", "invstd", "scale", "shift", "N", "C", "Cs", "H",
-                 "W", "Cout", "g", "relu", "has_res")
+                 "W", "Cout", "g", "relu", "has_res", "bnb_pre", "__weakref__")
 
 
 def _unit_fwd(x, w, gamma, beta, residual, conv, relu, bna: _BNArgs):
@@ -635,28 +718,34 @@ def _unit_fwd(x, w, gamma, beta, residual, conv, relu, bna: _BNArgs):
     u.x, u.w, u.gamma, u.y = x, w, gamma, y
     u.act = None
     u.mask = mask
+    u.bnb_pre = None
     u.mean, u.invstd, u.scale, u.shift = mean, invstd, scale, shift
     u.N, u.C, u.Cs, u.H, u.W, u.Cout, u.g, u.relu, u.has_res = N, C, Cs, H, W, Cout, g, relu, residual is not None
     return out, u
 
 
-def _bn_bwd(dA, u: _Unit, want_dres: bool, mask=None):
+def _bn_bwd(dA, u: _Unit, want_dres: bool, mask=None, pre: _BnbPartials | None = None):
     """BN(+res)(+ReLU) backward: returns (dy, dres, dgamma, dbeta). ``mask`` (a ReLU bit
     mask of another unit's output) gates dA first -- the downsample branch of a bottleneck
-    sees the block's ReLU exactly as the main branch does."""
+    sees the block's ReLU exactly as the main branch does. ``pre``: the reduction was
+    already done by the epilogue of the GEMM that produced dA (no reduce pass)."""
     lib = _load()
     st = _s()
     dA = _cl(dA.to(torch.bfloat16))
     Cout = u.Cout
     M = u.N * u.g["Ho"] * u.g["Wo"]
     f32 = dict(dtype=torch.float32, device=dA.device)
-    blocks = lib.pdt_bn_stats_blocks(M, Cout)
-    part = torch.empty(2 * blocks * Cout + lib.pdt_rows_reduce_workspace(blocks, Cout), **f32)
     if mask is None:
         mask = u.mask
     relu = u.relu or mask is not None
-    _chk(lib.pdt_bn_bwd_reduce(_p(dA), _p(u.y), _p(u.act), _p(u.mean), _p(u.scale), _p(u.shift), _p(part), M,
-                               Cout, int(relu), blocks, _p(mask), st), "bn_bwd_reduce")
+    if pre is not None:
+        assert pre.unit is u
+        part, blocks = pre.part, pre.R
+    else:
+        blocks = lib.pdt_bn_stats_blocks(M, Cout)
+        part = torch.empty(2 * blocks * Cout + lib.pdt_rows_reduce_workspace(blocks, Cout), **f32)
+        _chk(lib.pdt_bn_bwd_reduce(_p(dA), _p(u.y), _p(u.act), _p(u.mean), _p(u.scale), _p(u.shift), _p(part), M,
+                                   Cout, int(relu), blocks, _p(mask), st), "bn_bwd_reduce")
     vec = torch.empty((5, Cout), **f32)
     dgamma, dbeta, k1, k2, k3 = vec[0], vec[1], vec[2], vec[3], vec[4]
     _chk(lib.pdt_bn_bwd_finalize(_p(part), blocks, Cout, float(M), _p(u.gamma), _p(u.mean), _p(u.invstd),
@@ -668,12 +757,15 @@ def _bn_bwd(dA, u: _Unit, want_dres: bool, mask=None):
     return dy, dres, dgamma, dbeta
 
 
-def _unit_dx(dy, u: _Unit, addend=None, addend_mask=None):
+def _unit_dx(dy, u: _Unit, addend=None, addend_mask=None, bnb_unit=None, bnb_mask=None):
+    """Data gradient of unit ``u``'s conv. With ``bnb_unit`` (the unit whose output
+    this gradient flows into) returns ``(dx, _BnbPartials)``."""
     wd = u.w
     if u.Cs != u.C:  # stem: dgrad against the channel-padded weight, then drop the pad
         wd = torch.nn.functional.pad(u.w.detach().float(), (0, 0, 0, 0, 0, u.Cs - u.C))
-        assert addend is None
-    dx = _conv_dgrad(dy, wd, u.N, u.H, u.W, u.Cs, u.Cout, u.g, addend=addend, addend_mask=addend_mask)
+        assert addend is None and bnb_unit is None
+    dx = _conv_dgrad(dy, wd, u.N, u.H, u.W, u.Cs, u.Cout, u.g, addend=addend, addend_mask=addend_mask,
+                     bnb_unit=bnb_unit, bnb_mask=bnb_mask)
     return dx[:, :u.C] if u.Cs != u.C else dx
 
 
@@ -723,6 +815,41 @@ def conv_bn_act(x, conv: nn.Conv2d, bn: nn.BatchNorm2d, residual=None, relu=True
 # gradient is produced by ONE data-gradient GEMM whose epilogue adds the
 # identity / downsample branch gradient (no separate add pass).
 # =============================================================================
+# Cross-block fusion of the BatchNorm-backward reduction. Block k's output is
+# block k+1's input; block k+1's backward produces that gradient with ONE dgrad
+# GEMM (+ shortcut addend), so its epilogue also computes block k's bn3
+# backward partials (gated by block k's ReLU bit mask). Forward records which
+# unit produced each block output; backward leaves the partials on that unit,
+# tagged with the gradient tensor's storage and version -- block k's backward
+# uses them only if the gradient it receives is exactly that tensor.
+_PRODUCERS: dict = {}
+
+
+def _note_producer(out, u):
+    if len(_PRODUCERS) > 64:
+        for k in [k for k, e in _PRODUCERS.items() if e[0]() is None]:
+            del _PRODUCERS[k]
+    _PRODUCERS[out.data_ptr()] = (weakref.ref(u), tuple(out.shape), out.stride(), out._version)
+
+
+def _producer_of(x):
+    e = _PRODUCERS.get(x.data_ptr())
+    if e is None:
+        return None
+    u = e[0]()
+    if u is None or e[1] != tuple(x.shape) or e[2] != x.stride() or e[3] != x._version:
+        return None
+    return u
+
+
+def _take_bnb(u, grad):
+    """Partials a later block's epilogue left for unit ``u``, if ``grad`` is that output."""
+    st, u.bnb_pre = u.bnb_pre, None
+    if st is None or st[0] != grad.data_ptr() or st[1] != grad._version or st[2] != tuple(grad.shape):
+        return None
+    return st[3]
+
+
 class _Bottleneck(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, blk, has_ds, *params):
@@ -739,7 +866,10 @@ class _Bottleneck(torch.autograd.Function):
                             _BNArgs(blk.bn3))
         ctx.units = (u1, u2, u3, ud)
         ctx.has_ds = has_ds
+        prev = _producer_of(x) if _bnb_enabled() else None
+        ctx.prev = weakref.ref(prev) if prev is not None else None
         ctx.save_for_backward(u1.x, u1.y, u2.y, u3.y, u3.mask)
+        _note_producer(out, u3)
         return out
 
     @staticmethod
@@ -747,13 +877,20 @@ class _Bottleneck(torch.autograd.Function):
         u1, u2, u3, ud = ctx.units
         need = ctx.needs_input_grad
         dout = _cl(dout.to(torch.bfloat16))
-        dy3, _, dg3, db3 = _bn_bwd(dout, u3, False)
-        da2 = _unit_dx(dy3, u3)
+        dy3, _, dg3, db3 = _bn_bwd(dout, u3, False, pre=_take_bnb(u3, dout))
+        fuse = _bnb_enabled()
+        if fuse:  # bn2 / bn1 backward reductions in the epilogues of the conv3 / conv2 dgrads
+            da2, pre2 = _unit_dx(dy3, u3, bnb_unit=u2)
+        else:
+            da2, pre2 = _unit_dx(dy3, u3), None
         dw3 = _unit_dw(dy3, u3)
-        dy2, _, dg2, db2 = _bn_bwd(da2, u2, False)
-        da1 = _unit_dx(dy2, u2)
+        dy2, _, dg2, db2 = _bn_bwd(da2, u2, False, pre=pre2)
+        if fuse:
+            da1, pre1 = _unit_dx(dy2, u2, bnb_unit=u1)
+        else:
+            da1, pre1 = _unit_dx(dy2, u2), None
         dw2 = _unit_dw(dy2, u2)
-        dy1, _, dg1, db1 = _bn_bwd(da1, u1, False)
+        dy1, _, dg1, db1 = _bn_bwd(da1, u1, False, pre=pre1)
         grads_ds = ()
         # shortcut gradient = dout * relu_mask(out): never materialised -- the downsample
         # BN backward gates dout with the mask itself, and an identity shortcut is added
@@ -766,7 +903,14 @@ class _Bottleneck(torch.autograd.Function):
             grads_ds = (dwd, dgd, dbd)
         else:
             addend, addend_mask = dout, u3.mask
-        dx = _unit_dx(dy1, u1, addend=addend, addend_mask=addend_mask) if need[0] else None
+        prev = ctx.prev() if ctx.prev is not None else None
+        dx = None
+        if need[0] and prev is not None and prev.mask is not None and prev.Cout == u1.C and u1.Cs == u1.C:
+            # the previous block's bn3 backward partials from this epilogue
+            dx, pre = _unit_dx(dy1, u1, addend=addend, addend_mask=addend_mask, bnb_unit=prev, bnb_mask=prev.mask)
+            prev.bnb_pre = (dx.data_ptr(), dx._version, tuple(dx.shape), pre)
+        elif need[0]:
+            dx = _unit_dx(dy1, u1, addend=addend, addend_mask=addend_mask)
         dw1 = _unit_dw(dy1, u1)
         del ctx.units
         return (dx, None, None, dw1, dg1, db1, dw2, dg2, db2, dw3, dg3, db3) + grads_ds

@@ -1,0 +1,113 @@
+"""BatchNorm-backward reduction fused into the data-gradient GEMM epilogue
+(``BnbArgs`` in csrc/conv_igemm.hip, ``_Bottleneck.backward`` in
+ops/native_ops.py): fused vs the separate reduce pass vs an fp32 PyTorch
+reference of the same ResNet stage. Run on an MI355X."""
+import pytest
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+from pytorch_distributed_template_amd.ops import native_ops as no  # noqa: E402
+
+
+def nrmerr(a, b):
+    a = a.float()
+    b = b.float()
+    return ((a - b).norm() / b.norm().clamp_min(1e-6)).item()
+
+
+def _cl(t):
+    return t.contiguous(memory_format=torch.channels_last)
+
+
+def setup_module(module):
+    assert no.available(), "native library must be built and loaded on GPU runs"
+    no.require()
+
+
+def _ref_bottleneck(x, blk):
+    """fp32 PyTorch reference of a training-mode bottleneck (batch statistics)."""
+    def cb(t, conv, bn, relu):
+        t = F.conv2d(t, conv.weight, None, conv.stride, conv.padding)
+        t = F.batch_norm(t, None, None, bn.weight, bn.bias, True, 0.0, bn.eps)
+        return F.relu(t) if relu else t
+    idn = cb(x, blk.downsample[0], blk.downsample[1], False) if blk.downsample is not None else x
+    o = cb(x, blk.conv1, blk.bn1, True)
+    o = cb(o, blk.conv2, blk.bn2, True)
+    return F.relu(cb(o, blk.conv3, blk.bn3, False) + idn)
+
+
+def _stage():
+    from pytorch_distributed_template_amd.models.resnet import Bottleneck
+    return nn.Sequential(Bottleneck(256, 128, stride=2, downsample=True), Bottleneck(512, 128),
+                         Bottleneck(512, 128))
+
+
+def test_bn_backward_reduction_fused_into_dgrad_epilogue(monkeypatch):
+    """A 3-block stage (stride-2 + downsample, then identity blocks): the BN
+    backward reductions computed in the data-gradient epilogues (in-block bn1/bn2,
+    and the previous block's bn3 from the next block's input-gradient GEMM) must
+    match the separate reduce pass and an fp32 PyTorch reference."""
+    torch.manual_seed(11)
+    stage = _stage().cuda().to(memory_format=torch.channels_last)
+    for m in stage.modules():
+        if isinstance(m, nn.BatchNorm2d):
+            with torch.no_grad():
+                m.weight.uniform_(0.5, 1.5)
+                m.bias.uniform_(-0.3, 0.3)
+    x = _cl(torch.randn(8, 256, 28, 28, device="cuda").to(torch.bfloat16))
+    gy = _cl(torch.randn(8, 512, 14, 14, device="cuda", generator=torch.Generator("cuda").manual_seed(5))
+             .to(torch.bfloat16))
+    lib = no._load()
+    calls = {"bnb": 0, "reduce": 0}
+    orig_bnb, orig_red = lib.pdt_conv_nt_bnb, lib.pdt_bn_bwd_reduce
+
+    def count(name, fn):
+        def w(*a):
+            calls[name] += 1
+            return fn(*a)
+        return w
+    monkeypatch.setattr(lib, "pdt_conv_nt_bnb", count("bnb", orig_bnb))
+    monkeypatch.setattr(lib, "pdt_bn_bwd_reduce", count("reduce", orig_red))
+
+    res = {}
+    for fuse in ("1", "0"):
+        monkeypatch.setenv("PDT_FUSE_BN_BWD", fuse)
+        calls.update(bnb=0, reduce=0)
+        for p in stage.parameters():
+            p.grad = None
+        xi = x.detach().clone().requires_grad_(True)
+        y = stage(xi)
+        y.backward(gy)
+        torch.cuda.synchronize()
+        res[fuse] = (y.float(), xi.grad.float(), [p.grad.float().clone() for p in stage.parameters()], dict(calls))
+    # fused: bn1/bn2 of all 3 blocks + bn3 of blocks 0 and 1 (3x3 s2 dgrad = 4 phase launches);
+    # left on the reduce pass: the last block's bn3 and the downsample BN
+    assert res["1"][3]["reduce"] == 2, res["1"][3]
+    assert res["1"][3]["bnb"] >= 8, res["1"][3]
+    assert res["0"][3]["bnb"] == 0 and res["0"][3]["reduce"] == 10, res["0"][3]
+    (y1, dx1, g1, _), (y0, dx0, g0, _) = res["1"], res["0"]
+    assert nrmerr(y1, y0) == 0.0
+    assert nrmerr(dx1, dx0) < 2e-2
+    # fp32 reference of the same stage: the fused path must be as accurate as the
+    # separate reduce pass (both differ from fp32 only by bf16 rounding, which the
+    # BN backward's mean subtraction amplifies through the 3 blocks)
+    ref = _stage().cuda()
+    with torch.no_grad():
+        for q, p in zip(ref.parameters(), stage.parameters()):
+            q.copy_(p.float())
+    xr = x.detach().float().requires_grad_(True)
+    yr = xr
+    for blk in ref:
+        yr = _ref_bottleneck(yr, blk)
+    yr.backward(gy.float())
+    e1, e0 = nrmerr(dx1, xr.grad), nrmerr(dx0, xr.grad)
+    print(f"dx err vs fp32: fused {e1:.4g} unfused {e0:.4g}; fused vs unfused {nrmerr(dx1, dx0):.4g}")
+    assert nrmerr(y1, yr) < 2e-2
+    assert e1 < 1.25 * e0 + 2e-3, (e1, e0)
+    for a, b, q in zip(g1, g0, ref.parameters()):
+        ea, eb = nrmerr(a, q.grad), nrmerr(b, q.grad)
+        print(f"  {tuple(a.shape)}: fused {ea:.4g} unfused {eb:.4g}")
+        assert ea < 1.25 * eb + 2e-3, (a.shape, ea, eb)
