@@ -30,8 +30,12 @@ sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 BASELINE_METRIC = "images/sec (whole node) ResNet-50 synthetic 3x224x224 at 1/2/4/8 MI355X"
 # Reference-equivalent stack (stock PyTorch-ROCm: autocast bf16, channels_last,
 # MIOpen convs/BN, torch SGD) measured on one MI355X with this same harness
-# (`bench.py --backend torch`), see BASELINE.md. Scaled by N for N GPUs.
-STOCK_1GPU_IMG_S = {"resnet50": 6605.0}
+# (`bench.py --backend torch --batch B`), keyed by (model, per-GPU batch), see
+# BASELINE.md. Scaled by N for N GPUs (weak scaling).
+STOCK_1GPU_IMG_S = {("resnet50", 256): 6605.4, ("resnet50", 512): 6863.8}
+# Per-GPU batch: 512 images (21 GiB of the 288 GiB HBM3E) -- the stage-3/4 GEMMs
+# (M = N*14*14, N*7*7) fill all 256 CUs only from ~512 images up.
+DEFAULT_BATCH = {"resnet50": 512}
 
 
 def parse():
@@ -39,7 +43,7 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=30)
     ap.add_argument("--warmup", type=int, default=10)
-    ap.add_argument("--batch", type=int, default=256, help="per-GPU batch")
+    ap.add_argument("--batch", type=int, default=None, help="per-GPU batch (default: 512 for resnet50, else 256)")
     ap.add_argument("--model", default="resnet50")
     ap.add_argument("--fp8", action="store_true", help="ViT: fp8 (e4m3/e5m2) GEMMs on the native path")
     ap.add_argument("--backend", default="native", choices=["native", "torch"])
@@ -49,7 +53,10 @@ def parse():
     ap.add_argument("--json-out", default=None)
     ap.add_argument("--dist-backend", default=None, choices=[None, "nccl", "gloo"],
                     help="gloo: rehearse N ranks sharing GPU 0 (gradient all-reduce on the host); default RCCL")
-    return ap.parse_args()
+    a = ap.parse_args()
+    if a.batch is None:
+        a.batch = DEFAULT_BATCH.get(a.model, 256)
+    return a
 
 
 def heartbeat(rank, state, every_s=30.0):
@@ -178,7 +185,7 @@ def main():
 
     ms = elapsed / args.steps * 1e3
     value = world * args.batch * args.steps / elapsed
-    stock = STOCK_1GPU_IMG_S.get(args.model)
+    stock = STOCK_1GPU_IMG_S.get((args.model, args.batch))
     rec = {
         "metric": BASELINE_METRIC if args.model == "resnet50" else f"images/sec (whole node) {args.model} synthetic",
         "value": round(value, 2),

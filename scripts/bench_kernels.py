@@ -75,12 +75,21 @@ def main():
         sw = timeit(lambda: torch.ops.aten.convolution_backward(dy, x, wbt, None, (s, s), (p, p), (1, 1), False,
                                                                (0, 0), 1, (False, True, False)), a.iters)
         flop = 2.0 * N * g["Ho"] * g["Wo"] * Cout * Cin * k * k
+        # roofline floor per pass: max(FLOP / 2.5 PF/s dense bf16, min bytes / 6 TB/s achievable HBM)
+        bx, by, bw = 2.0 * N * H * H * Cs, 2.0 * N * g["Ho"] * g["Wo"] * Cout, 2.0 * Cout * Cs * k * k
+        floor = lambda b: max(flop / 2.5e15, b / 6e12) * 1e6  # noqa: E731
+        ff, fd, fw = floor(bx + by + bw), floor(bx + by + bw), floor(bx + by + 2 * bw)
         print(f"{Cin:4d}x{H:3d}->{Cout:4d} k{k} s{s} x{cnt:<2d}        {nf:8.1f}/{sf:8.1f} {nd:8.1f}/{sd:8.1f} "
-              f"{nw:8.1f}/{sw:8.1f}  {flop / nf / 1e6:7.1f}", flush=True)
+              f"{nw:8.1f}/{sw:8.1f}  {flop / nf / 1e6:7.1f}  floor f/d/w {ff:6.1f}/{fd:6.1f}/{fw:6.1f} us"
+              f"  eff {ff / nf:4.0%}/{fd / max(nd, 1e-9):4.0%}/{fw / nw:4.0%}", flush=True)
+        for key, v in (("ff", ff), ("fd", fd), ("fw", fw)):
+            tot[key] = tot.get(key, 0.0) + v * cnt
         for key, v in (("nf", nf), ("sf", sf), ("nd", nd), ("sd", sd), ("nw", nw), ("sw", sw)):
             tot[key] += v * cnt
     print("weighted totals (ms, per ResNet-50 step): fwd %.2f/%.2f dgrad %.2f/%.2f wgrad %.2f/%.2f" % (
         tot["nf"] / 1e3, tot["sf"] / 1e3, tot["nd"] / 1e3, tot["sd"] / 1e3, tot["nw"] / 1e3, tot["sw"] / 1e3))
+    print("roofline floors (ms): fwd %.2f dgrad %.2f wgrad %.2f" % (tot["ff"] / 1e3, tot["fd"] / 1e3,
+                                                                    tot["fw"] / 1e3))
 
 
 if __name__ == "__main__":
