@@ -850,6 +850,54 @@ def _take_bnb(u, grad):
     return st[3]
 
 
+# Weight gradients on a side HIP stream. Inside a block's backward the
+# data-gradient chain (dgrad GEMM -> BN reduce/finalize -> BN apply -> next
+# dgrad) is serial and full of small, latency-bound launches (BN finalize runs
+# on a handful of workgroups); the weight-gradient GEMMs depend only on dy and
+# the saved input, so they run beside that chain and fill the idle CUs. The
+# block joins the side stream before returning its gradients (DDP's bucket
+# hooks and the optimizer see finished tensors on the current stream).
+# Opt-in (PDT_WGRAD_STREAM=1): measured on one MI355X the kernels do overlap
+# (53.5 ms of kernel time in a 44.0 ms ResNet-50 bs512 step) but they then
+# contend for HBM bandwidth -- the BN element passes beside a wgrad GEMM run
+# 2.5x longer -- so the step is within noise of the single-stream order
+# (+0.4 % at bs512, -0.3 % at bs256; profiles/resnet50_native_bs512_step_r44_sidestream.txt).
+_SIDE_STREAMS: dict = {}
+
+
+def _wgrad_stream_enabled() -> bool:
+    return os.environ.get("PDT_WGRAD_STREAM", "0") == "1" and not torch.cuda.is_current_stream_capturing()
+
+
+class _SideWgrad:
+    def __init__(self):
+        self.on = _wgrad_stream_enabled()
+        self.used = False
+        if self.on:
+            dev = torch.cuda.current_device()
+            if dev not in _SIDE_STREAMS:
+                _SIDE_STREAMS[dev] = torch.cuda.Stream(device=dev)
+            self.side = _SIDE_STREAMS[dev]
+            self.main = torch.cuda.current_stream()
+
+    def dw(self, dy, u):
+        if not self.on:
+            return _unit_dw(dy, u)
+        self.side.wait_stream(self.main)  # dy (and everything before it) is ready
+        with torch.cuda.stream(self.side):
+            dw = _unit_dw(dy, u)
+        # the allocator must not recycle these while the side stream still reads / writes them
+        dy.record_stream(self.side)
+        u.x.record_stream(self.side)
+        dw.record_stream(self.main)
+        self.used = True
+        return dw
+
+    def join(self):
+        if self.used:
+            self.main.wait_stream(self.side)
+
+
 class _Bottleneck(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, blk, has_ds, *params):
@@ -883,13 +931,14 @@ class _Bottleneck(torch.autograd.Function):
             da2, pre2 = _unit_dx(dy3, u3, bnb_unit=u2)
         else:
             da2, pre2 = _unit_dx(dy3, u3), None
-        dw3 = _unit_dw(dy3, u3)
+        wg = _SideWgrad()
+        dw3 = wg.dw(dy3, u3)
         dy2, _, dg2, db2 = _bn_bwd(da2, u2, False, pre=pre2)
         if fuse:
             da1, pre1 = _unit_dx(dy2, u2, bnb_unit=u1)
         else:
             da1, pre1 = _unit_dx(dy2, u2), None
-        dw2 = _unit_dw(dy2, u2)
+        dw2 = wg.dw(dy2, u2)
         dy1, _, dg1, db1 = _bn_bwd(da1, u1, False, pre=pre1)
         grads_ds = ()
         # shortcut gradient = dout * relu_mask(out): never materialised -- the downsample
@@ -899,7 +948,7 @@ class _Bottleneck(torch.autograd.Function):
         if ctx.has_ds:
             dyd, _, dgd, dbd = _bn_bwd(dout, ud, False, mask=u3.mask)
             addend = _unit_dx(dyd, ud) if need[0] else None
-            dwd = _unit_dw(dyd, ud)
+            dwd = wg.dw(dyd, ud)
             grads_ds = (dwd, dgd, dbd)
         else:
             addend, addend_mask = dout, u3.mask
@@ -911,7 +960,8 @@ class _Bottleneck(torch.autograd.Function):
             prev.bnb_pre = (dx.data_ptr(), dx._version, tuple(dx.shape), pre)
         elif need[0]:
             dx = _unit_dx(dy1, u1, addend=addend, addend_mask=addend_mask)
-        dw1 = _unit_dw(dy1, u1)
+        dw1 = wg.dw(dy1, u1)
+        wg.join()
         del ctx.units
         return (dx, None, None, dw1, dg1, db1, dw2, dg2, db2, dw3, dg3, db3) + grads_ds
 
