@@ -80,7 +80,11 @@ __device__ __forceinline__ bf16x8 tr_frag(const char* base, int krow0, int col0,
   return r;
 }
 
-template <int BM, int BN, int NSTAGE, int NTH = NT, int WM = 2>
+// PF = register prefetch slots (NSTAGE == 2 only): with PF = 2 the global loads
+// of tile k+3 are issued right after tile k's barrier and land in LDS two
+// compute phases later (PF = 1: one), so a workgroup keeps ~2x the bytes in
+// flight -- the large weight gradients are load-latency bound otherwise.
+template <int BM, int BN, int NSTAGE, int NTH = NT, int WM = 2, int PF = 1>
 __global__ void __launch_bounds__(NTH, NTH == NT ? 2 : 1) wgrad_kernel(WGParams p) {
   constexpr int WN = NTH / 64 / WM;    // waves along the (tap, c) columns
   constexpr int RBA = BM * 2;   // bytes per A row (co)
@@ -129,7 +133,7 @@ __global__ void __launch_bounds__(NTH, NTH == NT ? 2 : 1) wgrad_kernel(WGParams 
 
   u32x4 ra[NA], rb[NB];
 
-  auto load_tile = [&](int kt) {
+  auto load_into = [&](int kt, u32x4 (&ra)[NA], u32x4 (&rb)[NB]) {
     const int k0 = kt * BK;
 #pragma unroll
     for (int i = 0; i < NA; ++i) {
@@ -156,7 +160,8 @@ __global__ void __launch_bounds__(NTH, NTH == NT ? 2 : 1) wgrad_kernel(WGParams 
         rb[i] = u32x4{0, 0, 0, 0};
     }
   };
-  auto store_tile = [&](int buf) {
+  auto load_tile = [&](int kt) { load_into(kt, ra, rb); };
+  auto store_from = [&](int buf, const u32x4 (&ra)[NA], const u32x4 (&rb)[NB]) {
     char* sa = smem + buf * STAGE;
     char* sb = sa + A_BYTES;
 #pragma unroll
@@ -166,6 +171,7 @@ __global__ void __launch_bounds__(NTH, NTH == NT ? 2 : 1) wgrad_kernel(WGParams 
     for (int i = 0; i < NB; ++i)
       *reinterpret_cast<u32x4*>(sb + lds_off<RBB>(rB0 + BROWS * i, cB * 16)) = rb[i];
   };
+  auto store_tile = [&](int buf) { store_from(buf, ra, rb); };
 
   f32x4 acc[MI][NI];
 #pragma unroll
@@ -173,6 +179,49 @@ __global__ void __launch_bounds__(NTH, NTH == NT ? 2 : 1) wgrad_kernel(WGParams 
 #pragma unroll
     for (int j = 0; j < NI; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
+  auto compute = [&](const char* sa) {
+    const char* sb = sa + A_BYTES;
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      bf16x8 bfr[NI];
+#pragma unroll
+      for (int j = 0; j < NI; ++j) bfr[j] = tr_frag<RBB>(sb, kk * 32, wn * (BN / WN) + j * 16, lane);
+#pragma unroll
+      for (int i = 0; i < MI; ++i) {
+        const bf16x8 af = tr_frag<RBA>(sa, kk * 32, wm * (BM / WM) + i * 16, lane);
+#pragma unroll
+        for (int j = 0; j < NI; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[j], af, acc[i][j], 0, 0, 0);
+      }
+    }
+  };
+
+  if constexpr (PF == 2) {
+    static_assert(NSTAGE == 2, "deep prefetch uses the 2-stage LDS ring");
+    // slot A = (ra, rb), slot B = (rb2 pair); loop unrolled by 2 so slots stay compile-time
+    u32x4 ra2[NA], rb2[NB];
+    const int n = kt_end - kt_begin;
+    if (n > 0) {
+      load_into(kt_begin, ra, rb);
+      store_from(0, ra, rb);
+    }
+    if (n > 1) load_into(kt_begin + 1, ra2, rb2);
+    if (n > 2) load_into(kt_begin + 2, ra, rb);
+    __syncthreads();
+    for (int i = 0; i < n; i += 2) {
+      // tile i in LDS stage 0, tile i+1 in slot B, tile i+2 in flight to slot A
+      compute(smem);
+      if (i + 1 < n) store_from(1, ra2, rb2);
+      __syncthreads();
+      if (i + 3 < n) load_into(kt_begin + i + 3, ra2, rb2);
+      if (i + 1 >= n) break;
+      // tile i+1 in LDS stage 1, tile i+2 in slot A, tile i+3 in flight to slot B
+      compute(smem + STAGE);
+      if (i + 2 < n) store_from(0, ra, rb);
+      __syncthreads();
+      if (i + 4 < n) load_into(kt_begin + i + 4, ra, rb);
+    }
+  } else {
   if (kt_begin < kt_end) {
     load_tile(kt_begin);
     store_tile(0);
@@ -207,6 +256,7 @@ __global__ void __launch_bounds__(NTH, NTH == NT ? 2 : 1) wgrad_kernel(WGParams 
       store_tile(0);
       __syncthreads();
     }
+  }
   }
 
   float* out = p.slab + (size_t)split * p.Mo * p.No;
@@ -259,7 +309,8 @@ __global__ void wgrad_reduce1_kernel(const float* __restrict__ slab, float* __re
 struct WGVar {
   int BM, BN, NS, NTH, target;
 };
-constexpr int WG_NVAR = 18;
+//   18..27: NS = 3 marks the 2-stage ring with 2 register prefetch slots (PF = 2)
+constexpr int WG_NVAR = 28;
 constexpr WGVar WG_VARS[WG_NVAR] = {
     {64, 64, 2, 256, 1024},   {64, 64, 1, 256, 1024},   {64, 64, 1, 256, 2048},
     {64, 128, 2, 256, 1024},  {64, 128, 1, 256, 1024},  {64, 128, 1, 256, 2048},
@@ -267,6 +318,10 @@ constexpr WGVar WG_VARS[WG_NVAR] = {
     {128, 128, 2, 256, 1024}, {128, 128, 1, 256, 1024}, {128, 128, 1, 256, 2048},
     {256, 128, 2, 512, 512},  {128, 256, 2, 512, 512},  {256, 128, 2, 512, 1024},
     {128, 256, 2, 512, 1024}, {256, 256, 2, 512, 256},  {256, 256, 2, 512, 512},
+    {64, 128, 3, 256, 1024},  {128, 64, 3, 256, 1024},  {128, 128, 3, 256, 1024},
+    {128, 128, 3, 256, 2048}, {64, 64, 3, 256, 2048},   {256, 128, 3, 512, 512},
+    {128, 256, 3, 512, 512},  {256, 128, 3, 512, 1024}, {128, 256, 3, 512, 1024},
+    {256, 256, 3, 512, 512},
 };
 static WGVar wg_variant(int v, int Mo, int No) {
   if (v < 0 || v >= WG_NVAR) return WGVar{Mo <= 64 ? 64 : 128, No <= 64 ? 64 : 128, 2, 256, 1024};
@@ -326,7 +381,19 @@ PDT_API int pdt_conv_wgrad(const void* dy, const void* x, float* slab, float* ou
   dim3 grid(tiles * splits);
 #define WG_LAUNCH(a, b, c) hipLaunchKernelGGL((wgrad_kernel<a, b, c>), grid, dim3(NT), 0, stream, p)
 #define WG_LAUNCH8(a, b, wm) hipLaunchKernelGGL((wgrad_kernel<a, b, 2, 512, wm>), grid, dim3(512), 0, stream, p)
-  if (w.NTH == 512) {
+#define WG_LAUNCH_PF(a, b, t, wm) hipLaunchKernelGGL((wgrad_kernel<a, b, 2, t, wm, 2>), grid, dim3(t), 0, stream, p)
+  if (NS == 3) {
+    if (w.NTH == 512) {
+      if (BM == 256 && BN == 256) WG_LAUNCH_PF(256, 256, 512, 2);
+      else if (BM == 256) WG_LAUNCH_PF(256, 128, 512, 4);
+      else WG_LAUNCH_PF(128, 256, 512, 2);
+    } else {
+      if (BM == 64 && BN == 64) WG_LAUNCH_PF(64, 64, 256, 2);
+      else if (BM == 64) WG_LAUNCH_PF(64, 128, 256, 2);
+      else if (BN == 64) WG_LAUNCH_PF(128, 64, 256, 2);
+      else WG_LAUNCH_PF(128, 128, 256, 2);
+    }
+  } else if (w.NTH == 512) {
     if (BM == 256 && BN == 256) WG_LAUNCH8(256, 256, 2);
     else if (BM == 256) WG_LAUNCH8(256, 128, 4);
     else WG_LAUNCH8(128, 256, 2);
@@ -343,6 +410,7 @@ PDT_API int pdt_conv_wgrad(const void* dy, const void* x, float* slab, float* ou
   }
 #undef WG_LAUNCH
 #undef WG_LAUNCH8
+#undef WG_LAUNCH_PF
   int e = (int)hipGetLastError();
   if (e) return e;
   long n4 = (long)Mo * No / 4;
