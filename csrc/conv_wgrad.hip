@@ -108,7 +108,10 @@ __global__ void __launch_bounds__(NTH, NTH == NT ? 2 : 1) wgrad_kernel(WGParams 
 
   const int ntm = (p.Mo + BM - 1) / BM, ntn = (p.No + BN - 1) / BN;
   const int ntiles = ntm * ntn;
-  const int bid = blockIdx.x;
+  // XCD-aware: a contiguous run of logical ids (= the tiles of one or a few
+  // pixel splits) stays on one XCD, so the dY / X slices those tiles share are
+  // fetched into that XCD's L2 once instead of once per XCD
+  const int bid = (int)xcd_remap(blockIdx.x, gridDim.x);
   const int tile = bid % ntiles;  // consecutive blocks: same split, different tiles
   const int split = bid / ntiles;
   const int tm = tile / ntn, tn = tile % ntn;
