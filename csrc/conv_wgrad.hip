@@ -24,6 +24,7 @@
 // per MFMA of the 128x128 tile: the big 3x3 weight gradients (No = 9*Cin up
 // to 4608) are otherwise bound by the staging traffic, not the matrix cores.
 #include "pdt_common.h"
+#include <stdlib.h>
 
 namespace {
 
@@ -38,6 +39,7 @@ struct WGParams {
   int Hm, Wm;        // output grid of the forward conv
   int sh, sw, oh0, ow0, dh, dw, ntw;
   int ktiles_per_split, splits;
+  int xcd;           // 1: XCD-aware block mapping (PDT_WGRAD_XCD=0 disables, for A/B runs)
   FastDiv div_Wm, div_HWm, div_C, div_ntw;
 };
 
@@ -111,7 +113,7 @@ __global__ void __launch_bounds__(NTH, NTH == NT ? 2 : 1) wgrad_kernel(WGParams 
   // XCD-aware: a contiguous run of logical ids (= the tiles of one or a few
   // pixel splits) stays on one XCD, so the dY / X slices those tiles share are
   // fetched into that XCD's L2 once instead of once per XCD
-  const int bid = (int)xcd_remap(blockIdx.x, gridDim.x);
+  const int bid = p.xcd ? (int)xcd_remap(blockIdx.x, gridDim.x) : (int)blockIdx.x;
   const int tile = bid % ntiles;  // consecutive blocks: same split, different tiles
   const int split = bid / ntiles;
   const int tm = tile / ntn, tn = tile % ntn;
@@ -374,6 +376,14 @@ PDT_API int pdt_conv_wgrad(const void* dy, const void* x, float* slab, float* ou
   p.Hs = Hs; p.Ws = Ws; p.C = C; p.Hm = Hm; p.Wm = Wm;
   p.sh = sh; p.sw = sw; p.oh0 = oh0; p.ow0 = ow0; p.dh = dh; p.dw = dw; p.ntw = ntw;
   p.ktiles_per_split = ktiles_per_split; p.splits = splits;
+  {
+    static int xcd_env = -1;
+    if (xcd_env < 0) {
+      const char* e = getenv("PDT_WGRAD_XCD");
+      xcd_env = (e && e[0] == '0') ? 0 : 1;
+    }
+    p.xcd = xcd_env;
+  }
   p.div_Wm = make_fastdiv(Wm);
   p.div_HWm = make_fastdiv(Hm * Wm);
   p.div_C = make_fastdiv(C);
