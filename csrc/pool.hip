@@ -15,9 +15,14 @@ __device__ __forceinline__ u32x4 pack8(const float* f) {
   return u32x4{pack2bf(f[0], f[1]), pack2bf(f[2], f[3]), pack2bf(f[4], f[5]), pack2bf(f[6], f[7])};
 }
 
-// one thread = 8 channels of one output pixel
+// one thread = 8 channels of one output pixel. AFF: the input is a pre-BatchNorm
+// conv output and every window element is first mapped through the BN affine
+// + ReLU (relu(x * scale[c] + shift[c]), fp32) -- the ResNet stem's BN-apply
+// pass and its full-resolution activation are never materialised.
+template <bool AFF>
 __global__ void maxpool_fwd_kernel(const u16* __restrict__ x, u16* __restrict__ y, uint8_t* __restrict__ idx,
-                                   int N, int H, int W, int C, int Ho, int Wo, int k, int s, int p) {
+                                   int N, int H, int W, int C, int Ho, int Wo, int k, int s, int p,
+                                   const float* __restrict__ scale, const float* __restrict__ shift) {
   const int cpr = C / 8;
   long total = (long)N * Ho * Wo * cpr;
   for (long t = (long)blockIdx.x * NT + threadIdx.x; t < total; t += (long)gridDim.x * NT) {
@@ -27,10 +32,14 @@ __global__ void maxpool_fwd_kernel(const u16* __restrict__ x, u16* __restrict__ 
     long r = pix / Wo;
     int oh = r % Ho;
     int n = r / Ho;
-    float best[8];
+    float best[8], sc[8], sh[8];
     uint8_t bi[8];
 #pragma unroll
     for (int j = 0; j < 8; ++j) { best[j] = -INFINITY; bi[j] = 0; }
+    if (AFF) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) { sc[j] = scale[cc * 8 + j]; sh[j] = shift[cc * 8 + j]; }
+    }
     for (int kh = 0; kh < k; ++kh) {
       int ih = oh * s - p + kh;
       if ((unsigned)ih >= (unsigned)H) continue;
@@ -39,6 +48,10 @@ __global__ void maxpool_fwd_kernel(const u16* __restrict__ x, u16* __restrict__ 
         if ((unsigned)iw >= (unsigned)W) continue;
         float f[8];
         unpack8(*reinterpret_cast<const u32x4*>(x + (((long)n * H + ih) * W + iw) * C + cc * 8), f);
+        if (AFF) {
+#pragma unroll
+          for (int j = 0; j < 8; ++j) f[j] = fmaxf(f[j] * sc[j] + sh[j], 0.f);
+        }
 #pragma unroll
         for (int j = 0; j < 8; ++j)
           if (f[j] > best[j] || (f[j] != f[j])) { best[j] = f[j]; bi[j] = (uint8_t)(kh * k + kw); }
@@ -136,8 +149,18 @@ PDT_API int pdt_maxpool_fwd(const void* x, void* y, void* idx, int N, int H, int
                             int s, int p, hipStream_t st) {
   if (C % 8 || k * k > 255) return -1;
   long total = (long)N * Ho * Wo * (C / 8);
-  hipLaunchKernelGGL(maxpool_fwd_kernel, dim3(grid_for(total)), dim3(NT), 0, st, (const u16*)x, (u16*)y,
-                     (uint8_t*)idx, N, H, W, C, Ho, Wo, k, s, p);
+  hipLaunchKernelGGL(maxpool_fwd_kernel<false>, dim3(grid_for(total)), dim3(NT), 0, st, (const u16*)x, (u16*)y,
+                     (uint8_t*)idx, N, H, W, C, Ho, Wo, k, s, p, nullptr, nullptr);
+  PDT_RETURN_LAUNCH();
+}
+
+// max-pool of relu(x * scale + shift) (per-channel fp32 BN affine), argmax as above
+PDT_API int pdt_maxpool_fwd_affine(const void* x, void* y, void* idx, const float* scale, const float* shift, int N,
+                                   int H, int W, int C, int Ho, int Wo, int k, int s, int p, hipStream_t st) {
+  if (C % 8 || k * k > 255 || !scale || !shift) return -1;
+  long total = (long)N * Ho * Wo * (C / 8);
+  hipLaunchKernelGGL(maxpool_fwd_kernel<true>, dim3(grid_for(total)), dim3(NT), 0, st, (const u16*)x, (u16*)y,
+                     (uint8_t*)idx, N, H, W, C, Ho, Wo, k, s, p, scale, shift);
   PDT_RETURN_LAUNCH();
 }
 

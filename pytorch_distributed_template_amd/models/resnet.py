@@ -81,8 +81,7 @@ class ResNet(BaseModel):
         return nn.Sequential(*layers)
 
     def forward(self, x):
-        x = fused.conv_bn_act(x, self.conv1, self.bn1, relu=True)
-        x = fused.max_pool2d(x, 3, 2, 1)
+        x = fused.conv_bn_relu_maxpool(x, self.conv1, self.bn1, 3, 2, 1)
         x = self.layer1(x)
         x = self.layer2(x)
         x = self.layer3(x)

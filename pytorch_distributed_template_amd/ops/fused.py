@@ -81,6 +81,17 @@ def bottleneck(x, blk):
     return conv_bn_act(out, blk.conv3, blk.bn3, residual=identity, relu=True)
 
 
+def conv_bn_relu_maxpool(x, conv: nn.Conv2d, bn: nn.BatchNorm2d, kernel_size=3, stride=2, padding=1):
+    """max_pool2d(relu(BN(conv(x)))) -- the ResNet stem. Native: one node whose
+    max-pool applies the BN affine + ReLU on the fly (no full-resolution activation)."""
+    if _use_native(x):
+        from . import native_ops
+        out = native_ops.stem_pool(x, conv, bn, kernel_size, stride, padding)
+        if out is not None:
+            return out
+    return max_pool2d(conv_bn_act(x, conv, bn, relu=True), kernel_size, stride, padding)
+
+
 def max_pool2d(x, kernel_size=3, stride=2, padding=1):
     if _use_native(x):
         from . import native_ops

@@ -52,6 +52,7 @@ _SIGS = {
     "pdt_bn_bwd_finalize": (c_int, [P, c_int, c_int, c_double] + [P] * 8 + [c_int, P]),
     "pdt_bn_bwd_apply": (c_int, [P] * 10 + [c_long, c_int, c_int, P, P]),
     "pdt_maxpool_fwd": (c_int, [P, P, P] + [c_int] * 9 + [P]),
+    "pdt_maxpool_fwd_affine": (c_int, [P] * 5 + [c_int] * 9 + [P]),
     "pdt_maxpool_bwd": (c_int, [P, P, P] + [c_int] * 9 + [P]),
     "pdt_avgpool_fwd": (c_int, [P, P, c_int, c_int, c_int, P]),
     "pdt_avgpool_bwd": (c_int, [P, P, c_int, c_int, c_int, P]),
@@ -675,7 +676,7 @@ class _Unit:
                  "W", "Cout", "g", "relu", "has_res", "bnb_pre", "__weakref__")
 
 
-def _unit_fwd(x, w, gamma, beta, residual, conv, relu, bna: _BNArgs):
+def _unit_fwd(x, w, gamma, beta, residual, conv, relu, bna: _BNArgs, apply: bool = True):
     lib = _load()
     st = _s()
     N, C, H, W = x.shape
@@ -703,6 +704,13 @@ def _unit_fwd(x, w, gamma, beta, residual, conv, relu, bna: _BNArgs):
         scale = (gamma.float() * invstd).contiguous()
         shift = (beta.float() - mean * scale).contiguous()
     assert y.numel() == M * Cout
+    if not apply:  # the consumer applies the BN affine (+ReLU) itself (stem max-pool)
+        u = _Unit()
+        u.x, u.w, u.gamma, u.y = x, w, gamma, y
+        u.act, u.mask, u.bnb_pre = None, None, None
+        u.mean, u.invstd, u.scale, u.shift = mean, invstd, scale, shift
+        u.N, u.C, u.Cs, u.H, u.W, u.Cout, u.g, u.relu, u.has_res = N, C, Cs, H, W, Cout, g, relu, False
+        return None, u
     res = None
     if residual is not None:
         res = _cl(residual)
@@ -1004,6 +1012,50 @@ class _MaxPool(torch.autograd.Function):
         dx = _empty_cl(N, C, H, W, torch.bfloat16, dy.device)
         _chk(_load().pdt_maxpool_bwd(_p(dy), _p(idx), _p(dx), N, H, W, C, Ho, Wo, k, s, p, _s()), "maxpool_bwd")
         return dx, None, None, None
+
+
+class _StemPool(torch.autograd.Function):
+    """conv -> BN -> ReLU -> max-pool (the ResNet stem) with the BN apply folded into
+    the max-pool: the full-resolution post-ReLU activation is never written or read.
+    Backward: max-pool gradient (full resolution) -> BN backward (ReLU gate recomputed
+    from y) -> weight gradient (and data gradient if the input needs one)."""
+
+    @staticmethod
+    def forward(ctx, x, w, gamma, beta, conv, bna, k, s, p):
+        _, u = _unit_fwd(x, w, gamma, beta, None, conv, True, bna, apply=False)
+        N, C, H, W = u.N, u.Cout, u.g["Ho"], u.g["Wo"]
+        Ho = (H + 2 * p - k) // s + 1
+        Wo = (W + 2 * p - k) // s + 1
+        assert u.y.shape == (N, C, H, W) and u.y.is_contiguous(memory_format=torch.channels_last)
+        out = _empty_cl(N, C, Ho, Wo, torch.bfloat16, u.y.device)
+        idx = torch.empty(N * Ho * Wo * C, dtype=torch.uint8, device=u.y.device)
+        _chk(_load().pdt_maxpool_fwd_affine(_p(u.y), _p(out), _p(idx), _p(u.scale), _p(u.shift), N, H, W, C, Ho, Wo,
+                                            k, s, p, _s()), "maxpool_fwd_affine")
+        ctx.u = u
+        ctx.meta = (N, C, H, W, Ho, Wo, k, s, p)
+        ctx.save_for_backward(u.x, u.y, idx)
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        u = ctx.u
+        _, _, idx = ctx.saved_tensors
+        N, C, H, W, Ho, Wo, k, s, p = ctx.meta
+        dout = _cl(dout.to(torch.bfloat16))
+        dA = _empty_cl(N, C, H, W, torch.bfloat16, dout.device)
+        _chk(_load().pdt_maxpool_bwd(_p(dout), _p(idx), _p(dA), N, H, W, C, Ho, Wo, k, s, p, _s()), "maxpool_bwd")
+        dy, _, dgamma, dbeta = _bn_bwd(dA, u, False)
+        dx = _unit_dx(dy, u) if ctx.needs_input_grad[0] else None
+        dw = _unit_dw(dy, u) if ctx.needs_input_grad[1] else None
+        del ctx.u
+        return dx, dw, dgamma, dbeta, None, None, None, None, None
+
+
+def stem_pool(x, conv: nn.Conv2d, bn: nn.BatchNorm2d, kernel_size=3, stride=2, padding=1):
+    """max_pool2d(relu(bn(conv(x)))) as one node; None if the native path cannot run it."""
+    if not supports_conv(x, conv) or conv.out_channels % 8:
+        return None
+    return _StemPool.apply(x, conv.weight, bn.weight, bn.bias, conv, _BNArgs(bn), kernel_size, stride, padding)
 
 
 def max_pool2d(x, kernel_size=3, stride=2, padding=1):

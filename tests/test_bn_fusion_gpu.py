@@ -111,3 +111,48 @@ def test_bn_backward_reduction_fused_into_dgrad_epilogue(monkeypatch):
         ea, eb = nrmerr(a, q.grad), nrmerr(b, q.grad)
         print(f"  {tuple(a.shape)}: fused {ea:.4g} unfused {eb:.4g}")
         assert ea < 1.25 * eb + 2e-3, (a.shape, ea, eb)
+
+
+def test_stem_bn_relu_folded_into_maxpool():
+    """ResNet stem: max_pool(relu(bn(conv(x)))) with the BN apply done inside the
+    max-pool vs the unfused composition (conv_bn_act + max_pool2d) and an fp32
+    PyTorch reference. The fused pool compares fp32 values where the unfused one
+    compares bf16-rounded activations, so argmax ties resolve differently and the
+    gradient of a tied window reaches a different pixel: both are judged against
+    the fp32 reference instead of against each other."""
+    import torch.nn.functional as F
+    torch.manual_seed(3)
+    conv = nn.Conv2d(3, 64, 7, 2, 3, bias=False).cuda().to(memory_format=torch.channels_last)
+    bn = nn.BatchNorm2d(64).cuda()
+    with torch.no_grad():
+        bn.weight.uniform_(-1.0, 1.5)  # negative scales: the affine is not monotonic
+        bn.bias.uniform_(-0.3, 0.3)
+        conv.weight.copy_(conv.weight.to(torch.bfloat16).float())
+    x = _cl(torch.randn(4, 3, 64, 64, device="cuda").to(torch.bfloat16))
+    g = None
+    res = []
+    for path in ("fused", "unfused", "fp32"):
+        for p_ in (conv.weight, bn.weight, bn.bias):
+            p_.grad = None
+        if path == "fused":
+            y = no.stem_pool(x, conv, bn)
+            assert y is not None
+        elif path == "unfused":
+            y = no.max_pool2d(no.conv_bn_act(x, conv, bn, relu=True), 3, 2, 1)
+        else:
+            t = F.conv2d(x.float(), conv.weight, None, 2, 3)
+            t = F.relu(F.batch_norm(t, None, None, bn.weight, bn.bias, True, 0.0, bn.eps))
+            y = F.max_pool2d(t, 3, 2, 1)
+        if g is None:
+            g = _cl(torch.randn(y.shape, device="cuda", generator=torch.Generator("cuda").manual_seed(9))
+                    .to(torch.bfloat16))
+        y.backward(g.to(y.dtype))
+        torch.cuda.synchronize()
+        res.append((y.float(), conv.weight.grad.clone(), bn.weight.grad.clone(), bn.bias.grad.clone()))
+    fused, unfused, ref = res
+    assert fused[0].shape == (4, 64, 16, 16)
+    assert nrmerr(fused[0], unfused[0]) < 2e-3
+    for k in range(4):
+        ef, eu = nrmerr(fused[k], ref[k]), nrmerr(unfused[k], ref[k])
+        print(f"stem output/grad {k}: fused {ef:.4g} unfused {eu:.4g}")
+        assert ef < 1.25 * eu + 5e-3, (k, ef, eu)
