@@ -83,6 +83,18 @@ class SyntheticImageLoader:
         if self.device.type == "cuda":
             from ..ops import native_ops
             if native_ops.available():
+                B, C, H, W = shape
+                if channels_last and self.dtype == torch.bfloat16 and C % 8:
+                    # NHWC with the channel dim zero-padded to 8 in storage: the images are the
+                    # [B, C, H, W] view, and the stem's implicit GEMM reads the padded 16-B pixel
+                    # rows in place (no per-step pad copy; ops.native_ops.nhwc_padded_view)
+                    cp = (C + 7) // 8 * 8
+                    buf = torch.empty((B, H, W, cp), dtype=torch.bfloat16, device=self.device)
+                    native_ops.fill_uniform_(buf, seed)
+                    buf[..., C:] = 0
+                    x = buf[..., :C].permute(0, 3, 1, 2)
+                    x.pdt_nhwc_pad = cp
+                    return x
                 x = torch.empty(shape, dtype=torch.bfloat16, device=self.device, memory_format=fmt)
                 native_ops.fill_uniform_(x, seed)
                 return x if self.dtype == torch.bfloat16 else x.to(self.dtype)

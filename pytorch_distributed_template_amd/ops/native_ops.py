@@ -676,13 +676,30 @@ class _Unit:
                  "W", "Cout", "g", "relu", "has_res", "bnb_pre", "__weakref__")
 
 
+def nhwc_padded_view(x, cp):
+    """[N, cp, H, W] channels_last view of a [N, C, H, W] bf16 tensor that a loader
+    built as a view into NHWC storage zero-padded to ``cp`` channels
+    (``x.pdt_nhwc_pad == cp``); None when x is not such a view."""
+    if getattr(x, "pdt_nhwc_pad", None) != cp or x.dtype != torch.bfloat16 or x.dim() != 4:
+        return None
+    N, C, H, W = x.shape
+    if x.stride() != (H * W * cp, 1, W * cp, cp):
+        return None
+    if x.untyped_storage().nbytes() < (x.storage_offset() + N * H * W * cp) * 2:
+        return None
+    return torch.as_strided(x, (N, cp, H, W), (H * W * cp, 1, W * cp, cp))
+
+
 def _unit_fwd(x, w, gamma, beta, residual, conv, relu, bna: _BNArgs, apply: bool = True):
     lib = _load()
     st = _s()
     N, C, H, W = x.shape
     Cs = C if C % 8 == 0 else 8
+    xp = nhwc_padded_view(x, Cs) if Cs != C else None
     x = x.to(torch.bfloat16)
-    if Cs != C:  # stem: pad channels to 8 (NHWC)
+    if xp is not None:  # stem on a loader-padded NHWC batch: read in place
+        x = xp
+    elif Cs != C:  # stem: pad channels to 8 (NHWC)
         x = torch.nn.functional.pad(_cl(x).permute(0, 2, 3, 1), (0, Cs - C)).permute(0, 3, 1, 2)
     x = _cl(x)
     Cout = w.shape[0]
