@@ -280,14 +280,50 @@ __global__ void __launch_bounds__(NT) bn_apply_kernel(const u16* __restrict__ y,
 // relu mask: if `act` (saved output) is given, mask = act > 0; else if RELU,
 // mask = y*scale+shift > 0 (exact when there is no residual).
 // USE_MASK: the ReLU mask comes from the forward's bit mask (takes precedence over USE_ACT)
-template <bool RELU, bool USE_ACT, bool USE_MASK = false>
+// ResNet stem: the BN-backward passes read the BN output gradient dA straight from
+// the max-pool's output gradient and argmax bytes (csrc/pool.hip: maxpool_bwd_kernel
+// gathers the same way), so the full-resolution dA is never written or read.
+struct PoolSrc {
+  const u16* dout;     // [N][Ho][Wo][C] pool output gradient
+  const uint8_t* idx;  // [N][Ho][Wo][C] argmax (kh*k + kw) per element
+  int H, W, Ho, Wo, k, s, p;
+};
+
+__device__ inline void pool_grad8(const PoolSrc& ps, uint32_t pix, int cc, int cpr, float (&acc)[8]) {
+  const uint32_t w = pix % (uint32_t)ps.W, r = pix / (uint32_t)ps.W;
+  const int h = r % (uint32_t)ps.H, n = r / (uint32_t)ps.H;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) acc[j] = 0.f;
+  const int oh_lo = max(h + ps.p - ps.k + ps.s, 0) / ps.s, oh_hi = min((h + ps.p) / ps.s, ps.Ho - 1);
+  const int ow_lo = max((int)w + ps.p - ps.k + ps.s, 0) / ps.s, ow_hi = min(((int)w + ps.p) / ps.s, ps.Wo - 1);
+  for (int oh = oh_lo; oh <= oh_hi; ++oh) {
+    const int kh = h + ps.p - oh * ps.s;
+    if (kh < 0 || kh >= ps.k) continue;
+    for (int ow = ow_lo; ow <= ow_hi; ++ow) {
+      const int kw = (int)w + ps.p - ow * ps.s;
+      if (kw < 0 || kw >= ps.k) continue;
+      const uint32_t o = (((uint32_t)n * ps.Ho + oh) * ps.Wo + ow) * cpr + cc;
+      const uint2 bi = reinterpret_cast<const uint2*>(ps.idx)[o];
+      float g[8];
+      unpack8(reinterpret_cast<const u32x4*>(ps.dout)[o], g);
+      const uint32_t me = (uint32_t)(kh * ps.k + kw);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const uint32_t b = ((j < 4 ? bi.x : bi.y) >> (8 * (j & 3))) & 0xffu;
+        if (b == me) acc[j] += g[j];
+      }
+    }
+  }
+}
+
+template <bool RELU, bool USE_ACT, bool USE_MASK = false, bool POOL = false>
 __global__ void __launch_bounds__(NT) bn_bwd_reduce_kernel(const u16* __restrict__ dA, const u16* __restrict__ y,
                                                            const u16* __restrict__ act,
                                                            const float* __restrict__ mean,
                                                            const float* __restrict__ scale,
                                                            const float* __restrict__ shift,
                                                            float* __restrict__ part, long M, int C,
-                                                           const uint8_t* __restrict__ mask) {
+                                                           const uint8_t* __restrict__ mask, PoolSrc ps = {}) {
   __shared__ float red[2][NT][8];
   const int cpr = C / 8;
   const int rp = NT / cpr;
@@ -304,7 +340,10 @@ __global__ void __launch_bounds__(NT) bn_bwd_reduce_kernel(const u16* __restrict
     for (long r = (long)blockIdx.x * rp + rr; r < M; r += (long)gridDim.x * rp) {
       const long off = r * C + ch * 8;
       float g[8], yv[8];
-      unpack8(*reinterpret_cast<const u32x4*>(dA + off), g);
+      if (POOL)
+        pool_grad8(ps, (uint32_t)r, ch, cpr, g);
+      else
+        unpack8(*reinterpret_cast<const u32x4*>(dA + off), g);
       unpack8(*reinterpret_cast<const u32x4*>(y + off), yv);
       if (RELU) {
         if (USE_MASK) {
@@ -352,7 +391,7 @@ __global__ void __launch_bounds__(NT) bn_bwd_reduce_kernel(const u16* __restrict
   }
 }
 
-template <bool RELU, bool USE_ACT, bool DRES, bool USE_MASK = false>
+template <bool RELU, bool USE_ACT, bool DRES, bool USE_MASK = false, bool POOL = false>
 __global__ void __launch_bounds__(NT) bn_bwd_apply_kernel(const u16* __restrict__ dA, const u16* __restrict__ y,
                                                           const u16* __restrict__ act,
                                                           const float* __restrict__ scale,
@@ -360,7 +399,7 @@ __global__ void __launch_bounds__(NT) bn_bwd_apply_kernel(const u16* __restrict_
                                                           const float* __restrict__ k1, const float* __restrict__ k2,
                                                           const float* __restrict__ k3, u16* __restrict__ dy,
                                                           u16* __restrict__ dres, long n8, int C,
-                                                          const uint8_t* __restrict__ mask) {
+                                                          const uint8_t* __restrict__ mask, PoolSrc ps = {}) {
   const int cpr = C / 8;
   const int ch = (int)((blockIdx.x * NT + threadIdx.x) % (uint32_t)cpr) * 8;  // invariant (see bn_apply)
   float a1[8], a2[8], a3[8], sc[8], sh[8];
@@ -373,7 +412,10 @@ __global__ void __launch_bounds__(NT) bn_bwd_apply_kernel(const u16* __restrict_
   }
   for (uint32_t i = blockIdx.x * NT + threadIdx.x; i < (uint32_t)n8; i += gridDim.x * NT) {
     float g[8], yv[8];
-    unpack8(reinterpret_cast<const u32x4*>(dA)[i], g);
+    if (POOL)
+      pool_grad8(ps, i / (uint32_t)cpr, ch / 8, cpr, g);
+    else
+      unpack8(reinterpret_cast<const u32x4*>(dA)[i], g);
     unpack8(reinterpret_cast<const u32x4*>(y)[i], yv);
     if (RELU) {
       if (USE_MASK) {
@@ -551,5 +593,30 @@ PDT_API int pdt_bn_bwd_apply(const void* dA, const void* y, const void* act, con
   }
 #undef BWD_APPLY
 #undef BWD_APPLY_M
+  PDT_RETURN_LAUNCH();
+}
+
+// Stem BN(+ReLU) backward with dA gathered from the max-pool gradient (PoolSrc):
+// reduce + apply over y [N][H][W][C] (ReLU mask recomputed from y*scale+shift).
+PDT_API int pdt_bn_bwd_reduce_pool(const void* dout, const void* idx, const void* y, const float* mean,
+                                   const float* scale, const float* shift, float* part, int N, int H, int W, int C,
+                                   int Ho, int Wo, int k, int s, int p, int blocks, hipStream_t st) {
+  const long M = (long)N * H * W;
+  if (C % 8 || C / 8 > NT || M * (C / 8) >= (1L << 31) || (long)N * Ho * Wo * (C / 8) >= (1L << 31)) return -1;
+  PoolSrc ps{(const u16*)dout, (const uint8_t*)idx, H, W, Ho, Wo, k, s, p};
+  hipLaunchKernelGGL((bn_bwd_reduce_kernel<true, false, false, true>), dim3(blocks), dim3(NT), 0, st, nullptr,
+                     (const u16*)y, nullptr, mean, scale, shift, part, M, C, nullptr, ps);
+  PDT_RETURN_LAUNCH();
+}
+
+PDT_API int pdt_bn_bwd_apply_pool(const void* dout, const void* idx, const void* y, const float* scale,
+                                  const float* shift, const float* k1, const float* k2, const float* k3, void* dy,
+                                  int N, int H, int W, int C, int Ho, int Wo, int k, int s, int p, hipStream_t st) {
+  const long n8 = (long)N * H * W * (C / 8);
+  if (C % 8 || n8 >= (1L << 31) || (long)N * Ho * Wo * (C / 8) >= (1L << 31)) return -1;
+  PoolSrc ps{(const u16*)dout, (const uint8_t*)idx, H, W, Ho, Wo, k, s, p};
+  hipLaunchKernelGGL((bn_bwd_apply_kernel<true, false, false, false, true>), dim3(grid_for(n8, C)), dim3(NT), 0, st,
+                     nullptr, (const u16*)y, nullptr, scale, shift, k1, k2, k3, (u16*)dy, nullptr, n8, C, nullptr,
+                     ps);
   PDT_RETURN_LAUNCH();
 }

@@ -303,8 +303,9 @@ static int conv_nt_impl(const void* src, const void* b, void* out, float* stats,
                         int Hs, int Ws, int Cs, int Nimg, int Hm, int Wm, int Ncol, int K, int ldb,
                         int sh, int sw, int oh0, int ow0, int dh, int dw, int nth, int ntw,
                         int Ho, int Wo, int osh, int osw, int oph, int opw, int ldo, int act,
-                        void* aux, int variant, const BnbArgs& bnb, hipStream_t stream) {
+                        void* aux, int variant, const BnbArgs& bnb, int pix, hipStream_t stream) {
   if (Cs % 8 != 0 || K % 8 != 0 || Ncol % 8 != 0 || ldo % 8 != 0 || ldb % 8 != 0) return -1;
+  if (pix != 0 && (pix % 4 != 0 || pix > Cs)) return -10;
   if (K != nth * ntw * Cs) return -2;
   NTParams p;
   p.src = (const u16*)src;
@@ -322,6 +323,7 @@ static int conv_nt_impl(const void* src, const void* b, void* out, float* stats,
   p.sh = sh; p.sw = sw; p.oh0 = oh0; p.ow0 = ow0; p.dh = dh; p.dw = dw; p.nth = nth; p.ntw = ntw;
   p.Ho = Ho; p.Wo = Wo; p.osh = osh; p.osw = osw; p.oph = oph; p.opw = opw; p.ldo = ldo;
   p.act = act;
+  p.pix = pix > 0 ? pix : Cs;
   p.aux = (u16*)aux;
   p.dq_a = p.dq_b = nullptr;
   p.bnb = bnb;
@@ -353,10 +355,11 @@ PDT_API int pdt_conv_nt(const void* src, const void* b, void* out, float* stats,
                         int Hs, int Ws, int Cs, int Nimg, int Hm, int Wm, int Ncol, int K, int ldb,
                         int sh, int sw, int oh0, int ow0, int dh, int dw, int nth, int ntw,
                         int Ho, int Wo, int osh, int osw, int oph, int opw, int ldo, int act,
-                        void* aux, int variant, hipStream_t stream) {
+                        void* aux, int variant, int pix, hipStream_t stream) {
   BnbArgs none{};
   return conv_nt_impl(src, b, out, stats, bias, addend, addend_mask, Hs, Ws, Cs, Nimg, Hm, Wm, Ncol, K, ldb, sh, sw,
-                      oh0, ow0, dh, dw, nth, ntw, Ho, Wo, osh, osw, oph, opw, ldo, act, aux, variant, none, stream);
+                      oh0, ow0, dh, dw, nth, ntw, Ho, Wo, osh, osw, oph, opw, ldo, act, aux, variant, none, pix,
+                      stream);
 }
 
 // Data gradient with the BatchNorm-backward reduction of the unit it feeds fused
@@ -373,7 +376,7 @@ PDT_API int pdt_conv_nt_bnb(const void* src, const void* b, void* out, const voi
   if (relu && bn_mask == nullptr && (bn_scale == nullptr || bn_shift == nullptr)) return -8;
   BnbArgs bnb{(const u16*)bn_y, bn_mean, bn_scale, bn_shift, (const uint8_t*)bn_mask, part, relu, row0, R};
   return conv_nt_impl(src, b, out, nullptr, nullptr, addend, addend_mask, Hs, Ws, Cs, Nimg, Hm, Wm, Ncol, K, ldb, sh,
-                      sw, oh0, ow0, dh, dw, nth, ntw, Ho, Wo, osh, osw, oph, opw, ldo, 0, nullptr, variant, bnb,
+                      sw, oh0, ow0, dh, dw, nth, ntw, Ho, Wo, osh, osw, oph, opw, ldo, 0, nullptr, variant, bnb, 0,
                       stream);
 }
 
@@ -427,6 +430,7 @@ PDT_API int pdt_gemm_f8(const void* a, const void* b, void* out, const float* bi
   p.sh = 1; p.sw = 1; p.oh0 = 0; p.ow0 = 0; p.dh = 1; p.dw = 1; p.nth = 1; p.ntw = 1;
   p.Ho = 1; p.Wo = 1; p.osh = 1; p.osw = 1; p.oph = 0; p.opw = 0; p.ldo = ldo;
   p.act = act;
+  p.pix = p.Cs;
   p.aux = (u16*)aux;
   p.nstat_rows = 0;
   p.nt_store = 0;

@@ -38,6 +38,8 @@ struct NTParams {
   int sh, sw, oh0, ow0, dh, dw, nth, ntw;
   int Ho, Wo, osh, osw, oph, opw, ldo;
   int act;             // 0 none, 1 relu, 2 gelu(tanh)
+  int pix;             // elements per source pixel in memory (= Cs, or Cs/2 for the space-to-depth stem
+                       // whose 16-B chunk spans two adjacent 4-channel pixels)
   u16* aux;            // optional: pre-activation copy of the output (same layout)
   int nstat_rows;
   int nt_store;        // 1: non-temporal (streaming) output stores
@@ -141,7 +143,7 @@ __global__ void __launch_bounds__(NTH, PIPE ? 1 : 2) conv_nt_kernel(NTParams p) 
         int ih = a_ih[i] + dho, iw = a_iw[i] + dwo;
         bool ok = a_ok[i] && (unsigned)ih < (unsigned)p.Hs && (unsigned)iw < (unsigned)p.Ws;
         if (ok) {
-          ra[i] = *reinterpret_cast<const u32x4*>(p.src + (size_t)(a_base[i] + ih * p.Ws + iw) * p.Cs + c0);
+          ra[i] = *reinterpret_cast<const u32x4*>(p.src + (size_t)(a_base[i] + ih * p.Ws + iw) * p.pix + c0);
         } else {
           ra[i] = u32x4{0, 0, 0, 0};
         }
@@ -159,7 +161,7 @@ __global__ void __launch_bounds__(NTH, PIPE ? 1 : 2) conv_nt_kernel(NTParams p) 
         int ih = a_ih[i] + dho, iw = a_iw[i] + dwo;
         bool ok = kin && a_ok[i] && (unsigned)ih < (unsigned)p.Hs && (unsigned)iw < (unsigned)p.Ws;
         if (ok) {
-          ra[i] = *reinterpret_cast<const u32x4*>(p.src + (size_t)(a_base[i] + ih * p.Ws + iw) * p.Cs + c0);
+          ra[i] = *reinterpret_cast<const u32x4*>(p.src + (size_t)(a_base[i] + ih * p.Ws + iw) * p.pix + c0);
         } else {
           ra[i] = u32x4{0, 0, 0, 0};
         }
@@ -211,7 +213,7 @@ __global__ void __launch_bounds__(NTH, PIPE ? 1 : 2) conv_nt_kernel(NTParams p) 
         const int tw = tap - th * p.ntw;
         const int ih = a_ih[i] + p.dh * th, iw = a_iw[i] + p.dw * tw;
         if (a_ok[i] && (unsigned)ih < (unsigned)p.Hs && (unsigned)iw < (unsigned)p.Ws)
-          g = p.src + (size_t)(a_base[i] + ih * p.Ws + iw) * p.Cs + c0;
+          g = p.src + (size_t)(a_base[i] + ih * p.Ws + iw) * p.pix + c0;
       } else {
         const int kc = k0 / 8 + c;
         const int tap = fdiv(kc, p.div_Cs8);
@@ -220,7 +222,7 @@ __global__ void __launch_bounds__(NTH, PIPE ? 1 : 2) conv_nt_kernel(NTParams p) 
         const int tw = tap - th * p.ntw;
         const int ih = a_ih[i] + p.dh * th, iw = a_iw[i] + p.dw * tw;
         if (kc * 8 < p.K && a_ok[i] && (unsigned)ih < (unsigned)p.Hs && (unsigned)iw < (unsigned)p.Ws)
-          g = p.src + (size_t)(a_base[i] + ih * p.Ws + iw) * p.Cs + c0;
+          g = p.src + (size_t)(a_base[i] + ih * p.Ws + iw) * p.pix + c0;
       }
       __builtin_amdgcn_global_load_lds(
           g, (__attribute__((address_space(3))) void*)(sa + (8 * wave + RS * i) * 128), 16, 0, 0);

@@ -36,6 +36,7 @@ struct WGParams {
   int Mo, No;        // Mo = Cout, No = ntaps*C
   int ldy;
   int Hs, Ws, C;
+  int pix;           // elements per source pixel in memory (= C; C/2 for the space-to-depth stem)
   int Hm, Wm;        // output grid of the forward conv
   int sh, sw, oh0, ow0, dh, dw, ntw;
   int ktiles_per_split, splits;
@@ -160,7 +161,7 @@ __global__ void __launch_bounds__(NTH, NTH == NT ? 2 : 1) wgrad_kernel(WGParams 
       int ih = (int)(oh * p.sh) + offh, iw = (int)(ow * p.sw) + offw;
       ok = ok && (unsigned)ih < (unsigned)p.Hs && (unsigned)iw < (unsigned)p.Ws;
       if (ok)
-        rb[i] = *reinterpret_cast<const u32x4*>(p.x + ((size_t)(img * p.Hs + ih) * p.Ws + iw) * p.C + cB_ch);
+        rb[i] = *reinterpret_cast<const u32x4*>(p.x + ((size_t)(img * p.Hs + ih) * p.Ws + iw) * p.pix + cB_ch);
       else
         rb[i] = u32x4{0, 0, 0, 0};
     }
@@ -366,14 +367,16 @@ PDT_API long pdt_wgrad_workspace(int splits, int Mo, int No) {
 PDT_API int pdt_conv_wgrad(const void* dy, const void* x, float* slab, float* out, int M, int Mo, int No,
                            int ldy, int Hs, int Ws, int C, int Hm, int Wm, int sh, int sw, int oh0, int ow0,
                            int dh, int dw, int ntw, int splits, int ktiles_per_split, float scale,
-                           int accumulate, int variant, hipStream_t stream) {
+                           int accumulate, int variant, int pix, hipStream_t stream) {
   if (C % 8 != 0 || Mo % 8 != 0 || No % 8 != 0 || ldy % 8 != 0) return -1;
+  if (pix != 0 && (pix % 4 != 0 || pix > C)) return -10;
   WGParams p;
   p.dy = (const u16*)dy;
   p.x = (const u16*)x;
   p.slab = slab;
   p.M = M; p.Mo = Mo; p.No = No; p.ldy = ldy;
   p.Hs = Hs; p.Ws = Ws; p.C = C; p.Hm = Hm; p.Wm = Wm;
+  p.pix = pix > 0 ? pix : C;
   p.sh = sh; p.sw = sw; p.oh0 = oh0; p.ow0 = ow0; p.dh = dh; p.dw = dw; p.ntw = ntw;
   p.ktiles_per_split = ktiles_per_split; p.splits = splits;
   {

@@ -19,19 +19,19 @@ __device__ __forceinline__ u32x4 pack8(const float* f) {
 // conv output and every window element is first mapped through the BN affine
 // + ReLU (relu(x * scale[c] + shift[c]), fp32) -- the ResNet stem's BN-apply
 // pass and its full-resolution activation are never materialised.
-template <bool AFF>
+template <bool AFF, typename IdxT>
 __global__ void maxpool_fwd_kernel(const u16* __restrict__ x, u16* __restrict__ y, uint8_t* __restrict__ idx,
                                    int N, int H, int W, int C, int Ho, int Wo, int k, int s, int p,
                                    const float* __restrict__ scale, const float* __restrict__ shift) {
-  const int cpr = C / 8;
-  long total = (long)N * Ho * Wo * cpr;
-  for (long t = (long)blockIdx.x * NT + threadIdx.x; t < total; t += (long)gridDim.x * NT) {
+  const IdxT cpr = C / 8;
+  const IdxT total = (IdxT)N * Ho * Wo * cpr;
+  for (IdxT t = (IdxT)blockIdx.x * NT + threadIdx.x; t < total; t += (IdxT)gridDim.x * NT) {
     int cc = t % cpr;
-    long pix = t / cpr;
-    int ow = pix % Wo;
-    long r = pix / Wo;
-    int oh = r % Ho;
-    int n = r / Ho;
+    IdxT pix = t / cpr;
+    int ow = pix % (IdxT)Wo;
+    IdxT r = pix / (IdxT)Wo;
+    int oh = r % (IdxT)Ho;
+    int n = r / (IdxT)Ho;
     float best[8], sc[8], sh[8];
     uint8_t bi[8];
 #pragma unroll
@@ -47,7 +47,7 @@ __global__ void maxpool_fwd_kernel(const u16* __restrict__ x, u16* __restrict__ 
         int iw = ow * s - p + kw;
         if ((unsigned)iw >= (unsigned)W) continue;
         float f[8];
-        unpack8(*reinterpret_cast<const u32x4*>(x + (((long)n * H + ih) * W + iw) * C + cc * 8), f);
+        unpack8(*reinterpret_cast<const u32x4*>(x + (((IdxT)n * H + ih) * W + iw) * C + cc * 8), f);
         if (AFF) {
 #pragma unroll
           for (int j = 0; j < 8; ++j) f[j] = fmaxf(f[j] * sc[j] + sh[j], 0.f);
@@ -65,18 +65,21 @@ __global__ void maxpool_fwd_kernel(const u16* __restrict__ x, u16* __restrict__ 
   }
 }
 
-// gather: each input pixel sums the gradients of the windows whose argmax it is
+// gather: each input pixel sums the gradients of the windows whose argmax it is.
+// Index math in IdxT: 32-bit when the tensor has < 2^31 chunks (the ResNet stem at
+// batch 512 has 51M), since 64-bit division is a long software sequence per thread.
+template <typename IdxT>
 __global__ void maxpool_bwd_kernel(const u16* __restrict__ dy, const uint8_t* __restrict__ idx, u16* __restrict__ dx,
                                    int N, int H, int W, int C, int Ho, int Wo, int k, int s, int p) {
-  const int cpr = C / 8;
-  long total = (long)N * H * W * cpr;
-  for (long t = (long)blockIdx.x * NT + threadIdx.x; t < total; t += (long)gridDim.x * NT) {
+  const IdxT cpr = C / 8;
+  const IdxT total = (IdxT)N * H * W * cpr;
+  for (IdxT t = (IdxT)blockIdx.x * NT + threadIdx.x; t < total; t += (IdxT)gridDim.x * NT) {
     int cc = t % cpr;
-    long pix = t / cpr;
-    int w = pix % W;
-    long r = pix / W;
-    int h = r % H;
-    int n = r / H;
+    IdxT pix = t / cpr;
+    int w = pix % (IdxT)W;
+    IdxT r = pix / (IdxT)W;
+    int h = r % (IdxT)H;
+    int n = r / (IdxT)H;
     float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     int oh_lo = (h + p - k + s) / s; if (h + p - k + 1 < 0) oh_lo = 0;
     int oh_hi = (h + p) / s;
@@ -88,7 +91,7 @@ __global__ void maxpool_bwd_kernel(const u16* __restrict__ dy, const uint8_t* __
       for (int ow = max(ow_lo, 0); ow <= min(ow_hi, Wo - 1); ++ow) {
         int kw = w + p - ow * s;
         if (kw < 0 || kw >= k) continue;
-        long o = ((((long)n * Ho + oh) * Wo + ow) * cpr + cc);
+        IdxT o = ((((IdxT)n * Ho + oh) * Wo + ow) * cpr + cc);
         uint2 bi = reinterpret_cast<const uint2*>(idx)[o];
         float g[8];
         unpack8(reinterpret_cast<const u32x4*>(dy)[o], g);
@@ -149,8 +152,12 @@ PDT_API int pdt_maxpool_fwd(const void* x, void* y, void* idx, int N, int H, int
                             int s, int p, hipStream_t st) {
   if (C % 8 || k * k > 255) return -1;
   long total = (long)N * Ho * Wo * (C / 8);
-  hipLaunchKernelGGL(maxpool_fwd_kernel<false>, dim3(grid_for(total)), dim3(NT), 0, st, (const u16*)x, (u16*)y,
-                     (uint8_t*)idx, N, H, W, C, Ho, Wo, k, s, p, nullptr, nullptr);
+  if ((long)N * H * W * C < (1L << 31))  // 32-bit index math (element offsets of the input fit)
+    hipLaunchKernelGGL((maxpool_fwd_kernel<false, uint32_t>), dim3(grid_for(total)), dim3(NT), 0, st, (const u16*)x,
+                       (u16*)y, (uint8_t*)idx, N, H, W, C, Ho, Wo, k, s, p, nullptr, nullptr);
+  else
+    hipLaunchKernelGGL((maxpool_fwd_kernel<false, long>), dim3(grid_for(total)), dim3(NT), 0, st, (const u16*)x,
+                       (u16*)y, (uint8_t*)idx, N, H, W, C, Ho, Wo, k, s, p, nullptr, nullptr);
   PDT_RETURN_LAUNCH();
 }
 
@@ -159,8 +166,12 @@ PDT_API int pdt_maxpool_fwd_affine(const void* x, void* y, void* idx, const floa
                                    int H, int W, int C, int Ho, int Wo, int k, int s, int p, hipStream_t st) {
   if (C % 8 || k * k > 255 || !scale || !shift) return -1;
   long total = (long)N * Ho * Wo * (C / 8);
-  hipLaunchKernelGGL(maxpool_fwd_kernel<true>, dim3(grid_for(total)), dim3(NT), 0, st, (const u16*)x, (u16*)y,
-                     (uint8_t*)idx, N, H, W, C, Ho, Wo, k, s, p, scale, shift);
+  if ((long)N * H * W * C < (1L << 31))  // 32-bit index math (element offsets of the input fit)
+    hipLaunchKernelGGL((maxpool_fwd_kernel<true, uint32_t>), dim3(grid_for(total)), dim3(NT), 0, st, (const u16*)x,
+                       (u16*)y, (uint8_t*)idx, N, H, W, C, Ho, Wo, k, s, p, scale, shift);
+  else
+    hipLaunchKernelGGL((maxpool_fwd_kernel<true, long>), dim3(grid_for(total)), dim3(NT), 0, st, (const u16*)x,
+                       (u16*)y, (uint8_t*)idx, N, H, W, C, Ho, Wo, k, s, p, scale, shift);
   PDT_RETURN_LAUNCH();
 }
 
@@ -168,8 +179,12 @@ PDT_API int pdt_maxpool_bwd(const void* dy, const void* idx, void* dx, int N, in
                             int k, int s, int p, hipStream_t st) {
   if (C % 8) return -1;
   long total = (long)N * H * W * (C / 8);
-  hipLaunchKernelGGL(maxpool_bwd_kernel, dim3(grid_for(total)), dim3(NT), 0, st, (const u16*)dy,
-                     (const uint8_t*)idx, (u16*)dx, N, H, W, C, Ho, Wo, k, s, p);
+  if (total < (1L << 31))
+    hipLaunchKernelGGL(maxpool_bwd_kernel<uint32_t>, dim3(grid_for(total)), dim3(NT), 0, st, (const u16*)dy,
+                       (const uint8_t*)idx, (u16*)dx, N, H, W, C, Ho, Wo, k, s, p);
+  else
+    hipLaunchKernelGGL(maxpool_bwd_kernel<long>, dim3(grid_for(total)), dim3(NT), 0, st, (const u16*)dy,
+                       (const uint8_t*)idx, (u16*)dx, N, H, W, C, Ho, Wo, k, s, p);
   PDT_RETURN_LAUNCH();
 }
 

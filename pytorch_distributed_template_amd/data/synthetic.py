@@ -84,11 +84,11 @@ class SyntheticImageLoader:
             from ..ops import native_ops
             if native_ops.available():
                 B, C, H, W = shape
-                if channels_last and self.dtype == torch.bfloat16 and C % 8:
-                    # NHWC with the channel dim zero-padded to 8 in storage: the images are the
-                    # [B, C, H, W] view, and the stem's implicit GEMM reads the padded 16-B pixel
-                    # rows in place (no per-step pad copy; ops.native_ops.nhwc_padded_view)
-                    cp = (C + 7) // 8 * 8
+                if channels_last and self.dtype == torch.bfloat16 and C % 4:
+                    # NHWC with the channel dim zero-padded to 4 in storage: the images are the
+                    # [B, C, H, W] view, and the space-to-depth stem GEMM reads 16-B chunks of two
+                    # padded pixels in place (no per-step pad copy; ops.native_ops.nhwc_padded_view)
+                    cp = (C + 3) // 4 * 4
                     buf = torch.empty((B, H, W, cp), dtype=torch.bfloat16, device=self.device)
                     native_ops.fill_uniform_(buf, seed)
                     buf[..., C:] = 0

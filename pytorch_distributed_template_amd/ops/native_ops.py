@@ -33,7 +33,7 @@ _SIGS = {
     "pdt_conv_nt_bnb_rows": (c_int, [c_int, c_int, c_int, c_int]),
     "pdt_conv_nt_num_variants": (c_int, []),
     "pdt_conv_nt_resolve_variant": (c_int, [c_int, c_int, c_int, c_int]),
-    "pdt_conv_nt": (c_int, [P, P, P, P, P, P, P] + [c_int] * 25 + [P, c_int, P]),
+    "pdt_conv_nt": (c_int, [P, P, P, P, P, P, P] + [c_int] * 25 + [P, c_int, c_int, P]),
     "pdt_conv_nt_bnb": (c_int, [P] * 5 + [c_int] * 25 + [P] * 6 + [c_int] * 3 + [P]),
     "pdt_ln_fwd": (c_int, [P, P, P, P, P, P, c_int, c_int, c_float, P]),
     "pdt_ln_bwd_blocks": (c_int, [c_int]),
@@ -42,8 +42,10 @@ _SIGS = {
     "pdt_wgrad_plan": (c_int, [c_int, c_int, c_int, c_int, ctypes.POINTER(c_int)]),
     "pdt_wgrad_num_variants": (c_int, []),
     "pdt_wgrad_workspace": (c_long, [c_int, c_int, c_int]),
-    "pdt_conv_wgrad": (c_int, [P, P, P, P] + [c_int] * 16 + [c_int, c_int, c_float, c_int, c_int, P]),
+    "pdt_conv_wgrad": (c_int, [P, P, P, P] + [c_int] * 16 + [c_int, c_int, c_float, c_int, c_int, c_int, P]),
     "pdt_bn_stats_blocks": (c_int, [c_long, c_int]),
+    "pdt_bn_bwd_reduce_pool": (c_int, [P] * 7 + [c_int] * 10 + [P]),
+    "pdt_bn_bwd_apply_pool": (c_int, [P] * 9 + [c_int] * 9 + [P]),
     "pdt_rows_reduce_workspace": (c_long, [c_int, c_int]),
     "pdt_bn_stats": (c_int, [P, P, c_long, c_int, c_int, P]),
     "pdt_bn_finalize": (c_int, [P, c_int, c_int, c_double, c_float, c_float] + [P] * 9 + [P]),
@@ -283,7 +285,8 @@ def _variant_filter():
 def _nt_args(src, b, out, stats, bias, a, act, variant, addend=None, aux=None, addend_mask=None):
     return (_p(src), _p(b), _p(out), _p(stats), _p(bias), _p(addend), _p(addend_mask), a["Hs"], a["Ws"], a["Cs"], a["Nimg"], a["Hm"], a["Wm"],
             a["Ncol"], a["K"], a["ldb"], a["sh"], a["sw"], a["oh0"], a["ow0"], a["dh"], a["dw"], a["nth"], a["ntw"],
-            a["Ho"], a["Wo"], a["osh"], a["osw"], a["oph"], a["opw"], a["ldo"], int(act), _p(aux), int(variant), _s())
+            a["Ho"], a["Wo"], a["osh"], a["osw"], a["oph"], a["opw"], a["ldo"], int(act), _p(aux), int(variant),
+            int(a.get("pix", 0)), _s())
 
 
 def _check_nt(src, b, out, a):
@@ -292,7 +295,9 @@ def _check_nt(src, b, out, a):
     assert Cs % 8 == 0 and K % 8 == 0 and Ncol % 8 == 0 and ldo % 8 == 0, (Cs, K, Ncol, ldo)
     assert K == a["nth"] * a["ntw"] * Cs
     # bounds: the kernel reads src[0 : Nimg*Hs*Ws*Cs], b[0 : Ncol*ldb], writes out rows < Nimg*Ho*Wo
-    assert src.numel() >= a["Nimg"] * a["Hs"] * a["Ws"] * Cs, "src too small"
+    pix = a.get("pix", 0) or Cs  # elements per source pixel in memory
+    assert pix % 4 == 0 and pix <= Cs
+    assert src.numel() >= a["Nimg"] * a["Hs"] * a["Ws"] * pix, "src too small"
     assert b.numel() >= Ncol * ldb or K == 0, "B too small"
     assert out.numel() >= a["Nimg"] * a["Ho"] * a["Wo"] * ldo, "out too small"
     assert a["Hm"] * a["osh"] <= a["Ho"] and a["Wm"] * a["osw"] <= a["Wo"]
@@ -304,6 +309,8 @@ def select_nt_variant(src, b, out, *, with_stats=False, bias=None, act=0, **a):
     M = a["Nimg"] * a["Hm"] * a["Wm"]
     key = "nt5:" + ",".join(str(a[k]) for k in ("Hs", "Ws", "Cs", "Nimg", "Hm", "Wm", "Ncol", "K", "sh", "sw",
                                                  "nth", "ntw", "osh")) + f",{int(with_stats)},{int(bias is not None)}"
+    if a.get("pix"):
+        key += f",p{a['pix']}"
     table = _tuned()
     if key in table:
         return int(table[key])
@@ -361,7 +368,8 @@ def _wgrad_launch(lib, dy, x, out, v, scale, accumulate, a):
     slab = torch.empty(lib.pdt_wgrad_workspace(splits, a["Mo"], a["No"]), dtype=torch.float32, device=dy.device)
     rc = lib.pdt_conv_wgrad(_p(dy), _p(x), _p(slab), _p(out), a["M"], a["Mo"], a["No"], a["ldy"], a["Hs"], a["Ws"],
                             a["C"], a["Hm"], a["Wm"], a["sh"], a["sw"], a["oh0"], a["ow0"], a["dh"], a["dw"],
-                            a["ntw"], splits, kps.value, float(scale), int(accumulate), int(v), _s())
+                            a["ntw"], splits, kps.value, float(scale), int(accumulate), int(v), int(a.get("pix", 0)),
+                            _s())
     _chk(rc, "conv_wgrad")
 
 
@@ -371,11 +379,15 @@ def conv_wgrad(dy, x, out, *, scale=1.0, accumulate=False, variant=None, **a):
     assert dy.dtype == torch.bfloat16 and x.dtype == torch.bfloat16 and out.dtype == torch.float32
     assert C % 8 == 0 and Mo % 8 == 0 and No % 8 == 0 and ldy % 8 == 0
     assert out.numel() >= Mo * No and dy.numel() >= M * ldy
-    assert M % (Hm * Wm) == 0 and x.numel() >= (M // (Hm * Wm)) * a["Hs"] * a["Ws"] * C, "wgrad source too small"
+    pix = a.get("pix", 0) or C  # elements per source pixel in memory
+    assert pix % 4 == 0 and pix <= C
+    assert M % (Hm * Wm) == 0 and x.numel() >= (M // (Hm * Wm)) * a["Hs"] * a["Ws"] * pix, "wgrad source too small"
     assert a["ntw"] >= 1 and No % C == 0
     lib = _load()
     if variant is None:
         key = "wg2:" + ",".join(str(a[k]) for k in ("M", "Mo", "No", "Hs", "Ws", "C", "Hm", "Wm", "sh", "ntw"))
+        if a.get("pix"):
+            key += f",p{a['pix']}"
         table = _tuned()
         if key in table:
             variant = int(table[key])
@@ -782,6 +794,36 @@ def _bn_bwd(dA, u: _Unit, want_dres: bool, mask=None, pre: _BnbPartials | None =
     return dy, dres, dgamma, dbeta
 
 
+def _bn_bwd_pool(dout, idx, u: _Unit, k, s, p):
+    """Stem BN+ReLU backward reading dA straight from the max-pool output gradient
+    and argmax (csrc/bn_act.hip ``pdt_bn_bwd_*_pool``): the full-resolution dA of
+    the ``maxpool_bwd`` + ``_bn_bwd`` composition is never materialised."""
+    lib = _load()
+    st = _s()
+    N, C, H, W = u.N, u.Cout, u.g["Ho"], u.g["Wo"]
+    Ho, Wo = dout.shape[2], dout.shape[3]
+    assert dout.is_contiguous(memory_format=torch.channels_last) and dout.dtype == torch.bfloat16
+    assert idx.numel() == N * Ho * Wo * C and u.y.shape == (N, C, H, W)
+    assert u.relu and u.act is None and u.mask is None
+    M = N * H * W
+    f32 = dict(dtype=torch.float32, device=dout.device)
+    # the gathered reduce is latency-bound (argmax byte -> gradient load chains): far
+    # more blocks in flight than the streaming reduce's 512
+    rp = 256 // (C // 8)
+    blocks = max(1, min(int(os.environ.get("PDT_POOL_BN_BLOCKS", "4096")), (M + rp - 1) // rp))
+    part = torch.empty(2 * blocks * C + lib.pdt_rows_reduce_workspace(blocks, C), **f32)
+    _chk(lib.pdt_bn_bwd_reduce_pool(_p(dout), _p(idx), _p(u.y), _p(u.mean), _p(u.scale), _p(u.shift), _p(part),
+                                    N, H, W, C, Ho, Wo, k, s, p, blocks, st), "bn_bwd_reduce_pool")
+    vec = torch.empty((5, C), **f32)
+    dgamma, dbeta, k1, k2, k3 = vec[0], vec[1], vec[2], vec[3], vec[4]
+    _chk(lib.pdt_bn_bwd_finalize(_p(part), blocks, C, float(M), _p(u.gamma), _p(u.mean), _p(u.invstd),
+                                 _p(dgamma), _p(dbeta), _p(k1), _p(k2), _p(k3), 0, st), "bn_bwd_finalize")
+    dy = torch.empty_like(u.y, memory_format=torch.channels_last)
+    _chk(lib.pdt_bn_bwd_apply_pool(_p(dout), _p(idx), _p(u.y), _p(u.scale), _p(u.shift), _p(k1), _p(k2), _p(k3),
+                                   _p(dy), N, H, W, C, Ho, Wo, k, s, p, st), "bn_bwd_apply_pool")
+    return dy, dgamma, dbeta
+
+
 def _unit_dx(dy, u: _Unit, addend=None, addend_mask=None, bnb_unit=None, bnb_mask=None):
     """Data gradient of unit ``u``'s conv. With ``bnb_unit`` (the unit whose output
     this gradient flows into) returns ``(dx, _BnbPartials)``."""
@@ -1031,15 +1073,115 @@ class _MaxPool(torch.autograd.Function):
         return dx, None, None, None
 
 
+# -----------------------------------------------------------------------------
+# Space-to-depth stem. The 7x7 stride-2 conv over 3 channels, run directly, pads
+# every pixel to 8 channels (5/8 of the GEMM K is zeros) and gathers 49 taps of
+# 16 B. Over NHWC storage padded to 4 channels, one 16-B chunk is instead TWO
+# horizontally adjacent pixels: the conv becomes 8 (kh) x 4 (kw pairs) taps of
+# 8 "channels" (b, c), K = 256 instead of 392, with the stride-2 column walk
+# folded into the tap offset (ow0 = -4, dw = 2: every pair starts on an even
+# pixel, so it is 16-B aligned and either wholly inside or wholly outside the
+# image). The kernels take the pixel stride separately (pix = 4, Cs = 8).
+#   W'[co, (kh*4 + t)*8 + b*4 + c] = W[co, c, kh, 2t + b - 1]  (0 outside 7x7 / c >= C)
+# -----------------------------------------------------------------------------
+_S2D_W: dict = {}
+
+
+def _s2d_ok(x, conv: nn.Conv2d) -> bool:
+    return (tuple(conv.kernel_size) == (7, 7) and tuple(conv.stride) == (2, 2) and tuple(conv.padding) == (3, 3)
+            and conv.in_channels <= 4 and x.shape[1] == conv.in_channels and x.shape[2] % 2 == 0
+            and x.shape[3] % 2 == 0 and os.environ.get("PDT_STEM_S2D", "1") != "0")
+
+
+def _s2d_weight(w: torch.Tensor) -> torch.Tensor:
+    """[Cout, 256] bf16 space-to-depth stem weight (cached per parameter version)."""
+    ent = _S2D_W.get(id(w))
+    if ent is not None and ent[1] == w._version and ent[2] == w.data_ptr() and _same_tensor(ent[3], w):
+        return ent[0]
+    Cout, C = w.shape[0], w.shape[1]
+    wp = torch.nn.functional.pad(w.detach().float(), (1, 0, 0, 1, 0, 4 - C))  # [Cout, 4, 8(kh), 8(kw+1)]
+    out = wp.view(Cout, 4, 8, 4, 2).permute(0, 2, 3, 4, 1).reshape(Cout, 256).to(torch.bfloat16).contiguous()
+    _S2D_W[id(w)] = (out, w._version, w.data_ptr(), _weak(w))
+    return out
+
+
+def _s2d_unfold_grad(dw256: torch.Tensor, C: int) -> torch.Tensor:
+    """[Cout, 256] fp32 space-to-depth weight gradient -> [Cout, C, 7, 7]."""
+    Cout = dw256.shape[0]
+    g = dw256.view(Cout, 8, 4, 2, 4).permute(0, 4, 1, 2, 3).reshape(Cout, 4, 8, 8)
+    return g[:, :C, :7, 1:8]
+
+
+def _s2d_geom(N, H, W, Cout):
+    Ho, Wo = H // 2, W // 2
+    return dict(Hs=H, Ws=W, Cs=8, Nimg=N, Hm=Ho, Wm=Wo, Ncol=Cout, K=256, ldb=256, sh=2, sw=2, oh0=-3, ow0=-4,
+                dh=1, dw=2, nth=8, ntw=4, Ho=Ho, Wo=Wo, osh=1, osw=1, oph=0, opw=0, ldo=Cout, pix=4)
+
+
+def _unit_fwd_s2d(x, w, gamma, beta, bna: _BNArgs):
+    """Stem conv (space-to-depth GEMM) + BN statistics/finalize; no apply."""
+    lib = _load()
+    st = _s()
+    N, C, H, W = x.shape
+    x4 = nhwc_padded_view(x, 4)
+    if x4 is None:
+        x4 = _cl(torch.nn.functional.pad(_cl(x.to(torch.bfloat16)).permute(0, 2, 3, 1), (0, 4 - C))
+                 .permute(0, 3, 1, 2))
+    Cout = w.shape[0]
+    a = _s2d_geom(N, H, W, Cout)
+    Ho, Wo = a["Ho"], a["Wo"]
+    M = N * Ho * Wo
+    wb = _s2d_weight(w)
+    y = _empty_cl(N, Cout, Ho, Wo, torch.bfloat16, x.device)
+    f32 = dict(dtype=torch.float32, device=x.device)
+    v = select_nt_variant(x4, wb, y, with_stats=bna.training, **a)
+    if bna.training:
+        R = conv_stat_rows(M, Cout, a["K"], v)
+        part = torch.empty(2 * R * Cout + lib.pdt_rows_reduce_workspace(R, Cout), **f32)
+        conv_nt(x4, wb, y, stats=part, variant=v, **a)
+        vec = torch.empty((4, Cout), **f32)
+        mean, invstd, scale, shift = vec[0], vec[1], vec[2], vec[3]
+        _chk(lib.pdt_bn_finalize(_p(part), R, Cout, float(M), float(bna.eps), float(bna.momentum), _p(gamma),
+                                 _p(beta), _p(mean), _p(invstd), _p(scale), _p(shift), _p(bna.rm), _p(bna.rv),
+                                 _p(bna.nbt), st), "bn_finalize")
+    else:
+        conv_nt(x4, wb, y, variant=v, **a)
+        invstd = torch.rsqrt(bna.rv.float() + bna.eps)
+        mean = bna.rm.float().clone()
+        scale = (gamma.float() * invstd).contiguous()
+        shift = (beta.float() - mean * scale).contiguous()
+    u = _Unit()
+    u.x, u.w, u.gamma, u.y = x4, w, gamma, y
+    u.act, u.mask, u.bnb_pre = None, None, None
+    u.mean, u.invstd, u.scale, u.shift = mean, invstd, scale, shift
+    g = dict(KH=7, KW=7, sh=2, sw=2, ph=3, pw=3, Ho=Ho, Wo=Wo, s2d=True)
+    u.N, u.C, u.Cs, u.H, u.W, u.Cout, u.g, u.relu, u.has_res = N, C, 8, H, W, Cout, g, True, False
+    return u
+
+
+def _unit_dw_s2d(dy, u: _Unit):
+    a = _s2d_geom(u.N, u.H, u.W, u.Cout)
+    dw256 = torch.empty((u.Cout, 256), dtype=torch.float32, device=dy.device)
+    conv_wgrad(dy, u.x, dw256, M=u.N * a["Ho"] * a["Wo"], Mo=u.Cout, No=256, ldy=u.Cout, Hs=u.H, Ws=u.W, C=8,
+               Hm=a["Ho"], Wm=a["Wo"], sh=2, sw=2, oh0=-3, ow0=-4, dh=1, dw=2, ntw=4, pix=4)
+    dw = _s2d_unfold_grad(dw256, u.C).contiguous(memory_format=torch.channels_last)
+    return dw.to(u.w.dtype) if dw.dtype != u.w.dtype else dw
+
+
 class _StemPool(torch.autograd.Function):
     """conv -> BN -> ReLU -> max-pool (the ResNet stem) with the BN apply folded into
     the max-pool: the full-resolution post-ReLU activation is never written or read.
-    Backward: max-pool gradient (full resolution) -> BN backward (ReLU gate recomputed
-    from y) -> weight gradient (and data gradient if the input needs one)."""
+    Backward: BN backward with its input gradient gathered from the pool gradient and
+    argmax (ReLU gate recomputed from y; no full-resolution dA) -> weight gradient (and
+    data gradient if the input needs one). PDT_STEM_POOL_BWD_FUSED=0 selects the
+    two-step maxpool_bwd + BN backward composition."""
 
     @staticmethod
     def forward(ctx, x, w, gamma, beta, conv, bna, k, s, p):
-        _, u = _unit_fwd(x, w, gamma, beta, None, conv, True, bna, apply=False)
+        if _s2d_ok(x, conv) and not ctx.needs_input_grad[0]:
+            u = _unit_fwd_s2d(x, w, gamma, beta, bna)
+        else:
+            _, u = _unit_fwd(x, w, gamma, beta, None, conv, True, bna, apply=False)
         N, C, H, W = u.N, u.Cout, u.g["Ho"], u.g["Wo"]
         Ho = (H + 2 * p - k) // s + 1
         Wo = (W + 2 * p - k) // s + 1
@@ -1059,11 +1201,18 @@ class _StemPool(torch.autograd.Function):
         _, _, idx = ctx.saved_tensors
         N, C, H, W, Ho, Wo, k, s, p = ctx.meta
         dout = _cl(dout.to(torch.bfloat16))
-        dA = _empty_cl(N, C, H, W, torch.bfloat16, dout.device)
-        _chk(_load().pdt_maxpool_bwd(_p(dout), _p(idx), _p(dA), N, H, W, C, Ho, Wo, k, s, p, _s()), "maxpool_bwd")
-        dy, _, dgamma, dbeta = _bn_bwd(dA, u, False)
-        dx = _unit_dx(dy, u) if ctx.needs_input_grad[0] else None
-        dw = _unit_dw(dy, u) if ctx.needs_input_grad[1] else None
+        if os.environ.get("PDT_STEM_POOL_BWD_FUSED", "1") != "0" and N * H * W * C < (1 << 34):
+            dy, dgamma, dbeta = _bn_bwd_pool(dout, idx, u, k, s, p)
+        else:
+            dA = _empty_cl(N, C, H, W, torch.bfloat16, dout.device)
+            _chk(_load().pdt_maxpool_bwd(_p(dout), _p(idx), _p(dA), N, H, W, C, Ho, Wo, k, s, p, _s()),
+                 "maxpool_bwd")
+            dy, _, dgamma, dbeta = _bn_bwd(dA, u, False)
+        s2d = u.g.get("s2d", False)
+        dx = _unit_dx(dy, u) if ctx.needs_input_grad[0] and not s2d else None
+        dw = None
+        if ctx.needs_input_grad[1]:
+            dw = _unit_dw_s2d(dy, u) if s2d else _unit_dw(dy, u)
         del ctx.u
         return dx, dw, dgamma, dbeta, None, None, None, None, None
 

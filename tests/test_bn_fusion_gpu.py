@@ -156,3 +156,80 @@ def test_stem_bn_relu_folded_into_maxpool():
         ef, eu = nrmerr(fused[k], ref[k]), nrmerr(unfused[k], ref[k])
         print(f"stem output/grad {k}: fused {ef:.4g} unfused {eu:.4g}")
         assert ef < 1.25 * eu + 5e-3, (k, ef, eu)
+
+
+@pytest.mark.parametrize("loader_padded", [False, True])
+def test_stem_space_to_depth_vs_direct(monkeypatch, loader_padded):
+    """Space-to-depth stem GEMM (K = 8x4 taps of 2 pixels x 4 channels = 256, read
+    from NHWC storage padded to 4 channels) vs the direct 7x7 implicit GEMM (49 taps
+    of 8 padded channels) and an fp32 PyTorch reference: forward output, conv
+    weight gradient and BN gradients. ``loader_padded`` feeds the loader's padded
+    NHWC view (read in place) instead of a plain channels_last tensor."""
+    torch.manual_seed(5)
+    conv = nn.Conv2d(3, 64, 7, 2, 3, bias=False).cuda().to(memory_format=torch.channels_last)
+    bn = nn.BatchNorm2d(64).cuda()
+    with torch.no_grad():
+        bn.weight.uniform_(0.5, 1.5)
+        bn.bias.uniform_(-0.3, 0.3)
+        conv.weight.copy_(conv.weight.to(torch.bfloat16).float())
+    if loader_padded:
+        from pytorch_distributed_template_amd.data.synthetic import SyntheticImageLoader
+        dl = SyntheticImageLoader(batch_size=4, num_samples=4, pool=1, image_size=96, training=False,
+                                     device=torch.device("cuda"), dtype=torch.bfloat16)
+        x = next(iter(dl))[0]
+        assert no.nhwc_padded_view(x, 4) is not None
+    else:
+        x = _cl(torch.randn(4, 3, 96, 96, device="cuda").to(torch.bfloat16))
+    g = _cl(torch.randn(4, 64, 24, 24, device="cuda", generator=torch.Generator("cuda").manual_seed(2))
+            .to(torch.bfloat16))
+    res = []
+    for path in ("s2d", "direct", "fp32"):
+        monkeypatch.setenv("PDT_STEM_S2D", "0" if path == "direct" else "1")
+        for p_ in (conv.weight, bn.weight, bn.bias):
+            p_.grad = None
+        if path == "fp32":
+            t = F.conv2d(x.float(), conv.weight, None, 2, 3)
+            t = F.relu(F.batch_norm(t, None, None, bn.weight, bn.bias, True, 0.0, bn.eps))
+            y = F.max_pool2d(t, 3, 2, 1)
+        else:
+            no._S2D_W.clear()
+            y = no.stem_pool(x, conv, bn)
+            assert (id(conv.weight) in no._S2D_W) == (path == "s2d")  # the path under test ran
+        y.backward(g.to(y.dtype))
+        torch.cuda.synchronize()
+        res.append((y.float(), conv.weight.grad.clone(), bn.weight.grad.clone(), bn.bias.grad.clone()))
+    s2d, direct, ref = res
+    assert s2d[0].shape == (4, 64, 24, 24)
+    for k in range(4):
+        es, ed = nrmerr(s2d[k], ref[k]), nrmerr(direct[k], ref[k])
+        print(f"stem s2d vs direct {k}: s2d {es:.4g} direct {ed:.4g}")
+        assert es < 1.25 * ed + 5e-3, (k, es, ed)
+
+
+def test_stem_bn_backward_gathers_pool_gradient(monkeypatch):
+    """Stem backward with the BN-backward passes gathering dA from the max-pool
+    gradient + argmax (no full-resolution dA) vs the maxpool_bwd + BN-backward
+    composition (PDT_STEM_POOL_BWD_FUSED=0): the same math except that the
+    composition rounds dA to bf16, so the two agree to bf16 rounding."""
+    torch.manual_seed(11)
+    conv = nn.Conv2d(3, 64, 7, 2, 3, bias=False).cuda().to(memory_format=torch.channels_last)
+    bn = nn.BatchNorm2d(64).cuda()
+    with torch.no_grad():
+        bn.weight.uniform_(-1.0, 1.5)
+        bn.bias.uniform_(-0.3, 0.3)
+    x = _cl(torch.randn(6, 3, 80, 80, device="cuda").to(torch.bfloat16))
+    g = _cl(torch.randn(6, 64, 20, 20, device="cuda", generator=torch.Generator("cuda").manual_seed(4))
+            .to(torch.bfloat16))
+    res = []
+    for fused in ("1", "0"):
+        monkeypatch.setenv("PDT_STEM_POOL_BWD_FUSED", fused)
+        for p_ in (conv.weight, bn.weight, bn.bias):
+            p_.grad = None
+        y = no.stem_pool(x, conv, bn)
+        y.backward(g)
+        torch.cuda.synchronize()
+        res.append((conv.weight.grad.clone(), bn.weight.grad.clone(), bn.bias.grad.clone()))
+    for a, b in zip(*res):
+        e = nrmerr(a, b)
+        print(f"pool-gather vs composed {tuple(a.shape)}: {e:.3g}")
+        assert torch.isfinite(a).all() and e < 1e-2, (a.shape, e)

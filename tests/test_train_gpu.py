@@ -21,10 +21,10 @@ def test_synthetic_loader_native_fill():
     assert [x.shape[0] for x in xs] == [8, 8, 4]
     x = xs[0]
     assert x.is_cuda and x.dtype == torch.bfloat16
-    # 3-channel images live in NHWC storage zero-padded to 8 channels (16-B pixel rows
-    # the stem GEMM reads in place); the [B, 3, H, W] tensor is a view into it
+    # 3-channel images live in NHWC storage zero-padded to 4 channels (the space-to-depth
+    # stem GEMM reads 16-B pairs of pixels in place); the [B, 3, H, W] tensor is a view into it
     from pytorch_distributed_template_amd.ops import native_ops
-    xp = native_ops.nhwc_padded_view(x, 8)
+    xp = native_ops.nhwc_padded_view(x, 4)
     assert xp is not None and xp.is_contiguous(memory_format=torch.channels_last)
     assert torch.equal(xp[:, :3], x) and not xp[:, 3:].any()
     assert -1.0 <= float(x.min()) and float(x.max()) <= 1.0 and float(x.float().std()) > 0.5
