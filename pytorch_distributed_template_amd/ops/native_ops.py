@@ -1171,10 +1171,10 @@ def _unit_dw_s2d(dy, u: _Unit):
 class _StemPool(torch.autograd.Function):
     """conv -> BN -> ReLU -> max-pool (the ResNet stem) with the BN apply folded into
     the max-pool: the full-resolution post-ReLU activation is never written or read.
-    Backward: BN backward with its input gradient gathered from the pool gradient and
-    argmax (ReLU gate recomputed from y; no full-resolution dA) -> weight gradient (and
-    data gradient if the input needs one). PDT_STEM_POOL_BWD_FUSED=0 selects the
-    two-step maxpool_bwd + BN backward composition."""
+    Backward: max-pool gradient -> BN backward (ReLU gate recomputed from y) -> weight
+    gradient (and data gradient if the input needs one). PDT_STEM_POOL_BWD_FUSED=1 has
+    the BN passes gather dA from the pool gradient and argmax instead (no
+    full-resolution dA; measured no faster, so off by default)."""
 
     @staticmethod
     def forward(ctx, x, w, gamma, beta, conv, bna, k, s, p):
@@ -1201,7 +1201,9 @@ class _StemPool(torch.autograd.Function):
         _, _, idx = ctx.saved_tensors
         N, C, H, W, Ho, Wo, k, s, p = ctx.meta
         dout = _cl(dout.to(torch.bfloat16))
-        if os.environ.get("PDT_STEM_POOL_BWD_FUSED", "1") != "0" and N * H * W * C < (1 << 34):
+        # off by default: measured equal to the composition (gathered reduce + apply 0.54 +
+        # 0.66 ms vs maxpool_bwd + reduce + apply 0.44 + 0.31 + 0.46 ms at bs512, r59)
+        if os.environ.get("PDT_STEM_POOL_BWD_FUSED", "0") == "1" and N * H * W * C < (1 << 34):
             dy, dgamma, dbeta = _bn_bwd_pool(dout, idx, u, k, s, p)
         else:
             dA = _empty_cl(N, C, H, W, torch.bfloat16, dout.device)

@@ -209,7 +209,7 @@ def test_stem_space_to_depth_vs_direct(monkeypatch, loader_padded):
 def test_stem_bn_backward_gathers_pool_gradient(monkeypatch):
     """Stem backward with the BN-backward passes gathering dA from the max-pool
     gradient + argmax (no full-resolution dA) vs the maxpool_bwd + BN-backward
-    composition (PDT_STEM_POOL_BWD_FUSED=0): the same math except that the
+    composition (PDT_STEM_POOL_BWD_FUSED=0, the default): the same math except that the
     composition rounds dA to bf16, so the two agree to bf16 rounding."""
     torch.manual_seed(11)
     conv = nn.Conv2d(3, 64, 7, 2, 3, bias=False).cuda().to(memory_format=torch.channels_last)
