@@ -12,14 +12,20 @@ step (SGD momentum + weight decay). Nothing is skipped or cached.
     python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B]
                     [--model resnet50|resnet152|vit_b_16] [--backend native|torch]
 
-For N > 1 launch with torch.distributed.run (one rank per GPU); rank 0 prints
-one JSON line.
+N > 1: either launch it under ``torch.distributed.run`` (one rank per GPU,
+``--gpus`` must equal WORLD_SIZE), or run ``python bench.py --gpus N`` directly:
+the parent (which never touches the GPU) checks that N GPUs are visible, starts
+the N ranks through ``torch.distributed.run`` on 127.0.0.1 and exits with their
+status; rank 0 prints the one JSON line. ``--device cpu`` rehearses the same
+path on CPU ranks over gloo (plumbing tests; not a performance number).
 """
 from __future__ import annotations
 
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -53,10 +59,69 @@ def parse():
     ap.add_argument("--json-out", default=None)
     ap.add_argument("--dist-backend", default=None, choices=[None, "nccl", "gloo"],
                     help="gloo: rehearse N ranks sharing GPU 0 (gradient all-reduce on the host); default RCCL")
+    ap.add_argument("--device", default="cuda", choices=["cuda", "cpu"],
+                    help="cpu: gloo ranks on the host with stock torch ops (launcher/plumbing rehearsal)")
+    ap.add_argument("--image-size", type=int, default=224, help="only for --device cpu rehearsals")
     a = ap.parse_args()
     if a.batch is None:
         a.batch = DEFAULT_BATCH.get(a.model, 256)
+    if a.device == "cpu":
+        a.backend, a.dist_backend = "torch", "gloo"
+    elif a.image_size != 224:
+        ap.error("--image-size is a CPU-rehearsal knob; GPU runs measure 224x224")
     return a
+
+
+def _free_port() -> int:
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_ranks(args) -> int | None:
+    """Self-launch for ``--gpus N`` without a launcher; None = run in-process.
+
+    Runs before anything touches the GPU (``torch.cuda.device_count`` does not
+    initialise HIP on this image): the ranks are children, never an exec."""
+    if "WORLD_SIZE" in os.environ:
+        world = int(os.environ["WORLD_SIZE"])
+        if world != args.gpus:
+            print(f"bench.py: --gpus {args.gpus} but the launcher started WORLD_SIZE={world} ranks", file=sys.stderr)
+            return 2
+        return None
+    if args.gpus <= 1:
+        return None
+    if args.device == "cuda" and args.dist_backend != "gloo":
+        n = torch.cuda.device_count()
+        if n < args.gpus:
+            print(f"bench.py: --gpus {args.gpus} requested but only {n} GPU(s) are visible; refusing to report "
+                  f"a {n}-GPU number as {args.gpus}", file=sys.stderr)
+            return 2
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr=127.0.0.1", f"--master-port={_free_port()}", os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    env.setdefault("OMP_NUM_THREADS", "4")
+    return subprocess.call(cmd, env=env)
+
+
+def _rccl_version():
+    try:
+        v = torch.cuda.nccl.version()
+        return ".".join(str(x) for x in v) if isinstance(v, tuple) else str(v)
+    except Exception:
+        return None
+
+
+def _dtype_label(args) -> str:
+    if args.backend == "torch":
+        return "bf16 (autocast)" if args.device == "cuda" else "fp32 (cpu rehearsal)"
+    if not args.fp8:
+        return "bf16"
+    from pytorch_distributed_template_amd.ops.native_ops import fp8_settings
+    c = fp8_settings()
+    return (f"fp8(e4m3 fwd GEMMs, {c['scaling']} scaling; {'e5m2' if c['dgrad'] else 'bf16'} dgrad GEMMs; "
+            f"{'fp8' if c['attn'] else 'bf16'} attention; bf16 wgrad)+bf16")
 
 
 def heartbeat(rank, state, every_s=30.0):
@@ -79,18 +144,25 @@ def heartbeat(rank, state, every_s=30.0):
 
 def main():
     args = parse()
+    rc = launch_ranks(args)
+    if rc is not None:
+        sys.exit(rc)
     from pytorch_distributed_template_amd.utils import dist as pdist
     from pytorch_distributed_template_amd.ops import fused
     from pytorch_distributed_template_amd import models
-    from pytorch_distributed_template_amd.parallel import wrap_ddp
+    from pytorch_distributed_template_amd.parallel import pretune_for_ddp, wrap_ddp
     from pytorch_distributed_template_amd.data.synthetic import SyntheticImageLoader
 
-    shared = args.dist_backend == "gloo"
-    device = pdist.init_distributed(backend=args.dist_backend, device_index=0 if shared else None)
+    cpu = args.device == "cpu"
+    shared = args.dist_backend == "gloo" and not cpu
+    device = pdist.init_distributed(backend=args.dist_backend, device_index=0 if shared else None) if not cpu \
+        else pdist.init_distributed(backend="gloo")
     world = pdist.get_world_size()
     rank = pdist.get_rank()
-    if device.type != "cuda":
-        raise SystemExit("bench.py needs a GPU")
+    if cpu:
+        device = torch.device("cpu")
+    elif device.type != "cuda":
+        raise SystemExit("bench.py needs a GPU (use --device cpu for a plumbing rehearsal)")
     state = {"phase": "setup", "step": 0}
     hb = heartbeat(rank, state)
     fused.set_backend(args.backend)
@@ -109,18 +181,26 @@ def main():
         opt_name = "SGD(momentum=0.9, wd=5e-5)"
         opt = (FusedSGD if args.backend == "native" else torch.optim.SGD)(model.parameters(), lr=0.1, momentum=0.9,
                                                                           weight_decay=5e-5)
+    loader = SyntheticImageLoader(args.batch, num_samples=args.batch * (args.steps + args.warmup + 2) * world,
+                                  dtype="float32" if cpu else "bfloat16", pool=2, device=device,
+                                  image_size=args.image_size)
+    batches = list(iter(loader))[:2]
+    autocast = args.backend == "torch" and not cpu
+    dev_type = device.type
+
+    def _pretune_step():
+        x, y = batches[0]
+        fused.softmax_cross_entropy(model(x), y).backward()
+
+    # N ranks: rank 0 tunes the kernel variants once and broadcasts them (no per-rank timing)
+    pretune_for_ddp(model, _pretune_step)
     model = wrap_ddp(model, device, bucket_cap_mb=args.bucket_mb, broadcast_buffers=False,
                      gradient_as_bucket_view=True, comm_hook=args.comm_hook)
-
-    loader = SyntheticImageLoader(args.batch, num_samples=args.batch * (args.steps + args.warmup + 2) * world,
-                                  dtype="bfloat16", pool=2, device=device)
-    batches = list(iter(loader))[:2]
-    autocast = args.backend == "torch"
 
     def step(i):
         x, y = batches[i % 2]
         opt.zero_grad(set_to_none=True)
-        with torch.autocast("cuda", dtype=torch.bfloat16, enabled=autocast):
+        with torch.autocast(dev_type, dtype=torch.bfloat16, enabled=autocast):
             out = model(x)
             loss = fused.softmax_cross_entropy(out, y)
         loss.backward()
@@ -134,7 +214,7 @@ def main():
 
         def gstep():
             opt.zero_grad(set_to_none=False)
-            with torch.autocast("cuda", dtype=torch.bfloat16, enabled=autocast):
+            with torch.autocast(dev_type, dtype=torch.bfloat16, enabled=autocast):
                 out = model(sx)
                 loss = fused.softmax_cross_entropy(out, sy)
             loss.backward()
@@ -163,8 +243,9 @@ def main():
     for i in range(args.warmup):
         state["step"] = i
         loss = step(i)
+    sync = torch.cuda.synchronize if not cpu else (lambda: None)
     pdist.synchronize()
-    torch.cuda.synchronize()
+    sync()
     state["phase"] = "timed"
     t0 = time.perf_counter()
     cpu_issue = 0.0
@@ -174,7 +255,7 @@ def main():
         loss = step(i)
         cpu_issue += time.perf_counter() - c0
     pdist.synchronize()
-    torch.cuda.synchronize()
+    sync()
     elapsed = time.perf_counter() - t0
     hb.set()
     t = torch.tensor([elapsed], dtype=torch.float64, device=device)
@@ -197,14 +278,16 @@ def main():
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": round(value / (stock * world), 4) if stock else None,
-        "dtype": "fp8(e4m3 fwd, e5m2 dgrad)+bf16" if args.fp8 else "bf16",
-        "data": "synthetic (device-resident random 3x224x224, random-init weights)",
+        "dtype": _dtype_label(args),
+        "data": f"synthetic (device-resident random 3x{args.image_size}x{args.image_size}, random-init weights)",
         "config": {"model": args.model, "global_batch": args.batch * world, "per_gpu_batch": args.batch,
-                   "seq_len": None, "image_size": 224, "parallelism": f"dp{world}",
+                   "seq_len": None, "image_size": args.image_size, "parallelism": f"dp{world}",
                    "backend": args.backend, "optimizer": opt_name,
-                   "bucket_cap_mb": args.bucket_mb, "dist_backend": args.dist_backend or "nccl (RCCL)","final_loss": round(final_loss, 4), "hip_graph": args.graph,
+                   "bucket_cap_mb": args.bucket_mb, "dist_backend": (torch.distributed.get_backend() if world > 1 else "none (1 rank)"),
+                   "rccl_version": _rccl_version(), "device": args.device,
+                   "final_loss": round(final_loss, 4), "hip_graph": args.graph,
                    "cpu_issue_ms_per_step": round(cpu_issue / args.steps * 1e3, 3),
-                   "max_mem_gib": round(torch.cuda.max_memory_allocated() / 2 ** 30, 2)},
+                   "max_mem_gib": round(torch.cuda.max_memory_allocated() / 2 ** 30, 2) if not cpu else None},
     }
     if rank == 0:
         line = json.dumps(rec)

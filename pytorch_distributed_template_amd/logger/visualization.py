@@ -42,17 +42,15 @@ class TensorboardWriter:
 
         if enabled:
             log_dir = str(log_dir)
-            succeeded = False
-            for module in ["torch.utils.tensorboard", "tensorboardX"]:
+            for module in ("torch.utils.tensorboard", "tensorboardX"):
                 try:
                     self.writer = importlib.import_module(module).SummaryWriter(log_dir)
-                    succeeded = True
-                    break
                 except ImportError:
-                    succeeded = False
-                self.selected_module = module
+                    continue
+                self.selected_module = module  # the backend actually in use
+                break
 
-            if not succeeded:
+            if self.writer is None:
                 logger.warning("Warning: visualization (Tensorboard) is configured to use, but neither "
                                "torch.utils.tensorboard nor tensorboardX is installed; scalars go to "
                                "scalars.jsonl in the run directory instead.")

@@ -194,32 +194,50 @@ def _weak(t):
 # raw kernel wrappers
 # =============================================================================
 # -----------------------------------------------------------------------------
-# conv_nt tile-variant autotuner: the first eager call of every distinct
-# geometry times each tile variant (csrc/conv_igemm.hip) with HIP events and
-# keeps the fastest; choices persist in a JSON table (shipped tuned table:
-# _lib/autotune_gfx950.json; PDT_AUTOTUNE=0 disables tuning -> heuristic).
+# Tile-variant autotuner: the first eager call of every distinct geometry times
+# each tile variant (csrc/conv_igemm.hip, conv_wgrad.hip) with HIP events and
+# keeps the fastest.
+#   * The shipped table (_lib/autotune_gfx950.json, tracked) is READ-ONLY at run
+#     time; new entries go to a per-user cache (PDT_AUTOTUNE_CACHE, default
+#     ~/.cache/pytorch_distributed_template_amd/autotune_gfx950.json) overlaid
+#     on it at load.
+#   * PDT_AUTOTUNE=0 or --deterministic (PDT_DETERMINISTIC=1): no timing at all --
+#     shipped/cached choices, else the fixed heuristic, so every run and every
+#     rank picks the same variant (and the same split-K summation order).
+#   * World size > 1: ranks must not time variants independently (different
+#     choices per rank, stragglers inside the first backward). Tuning is off
+#     unless :func:`pretune_distributed` runs: rank 0 tunes on one step and
+#     broadcasts its table, then every rank freezes it.
 # -----------------------------------------------------------------------------
-_TUNE_PATH = Path(os.environ.get("PDT_AUTOTUNE_CACHE", str(_LIB_PATH.parent / "autotune_gfx950.json")))
+_SHIPPED_TUNE_PATH = _LIB_PATH.parent / "autotune_gfx950.json"
+_TUNE_PATH = Path(os.environ.get("PDT_AUTOTUNE_CACHE", str(Path.home() / ".cache" / "pytorch_distributed_template_amd"
+                                                          / "autotune_gfx950.json")))
 _TUNED: dict | None = None
+_TUNE_FORCE = False   # pretune_distributed: rank 0 tunes although WORLD_SIZE > 1
+_TUNE_FROZEN = False  # after the broadcast: no rank tunes any more
 
 
 def _tuned() -> dict:
     global _TUNED
     if _TUNED is None:
-        _TUNED = {}
-        try:
-            import json
-            _TUNED = json.loads(_TUNE_PATH.read_text())
-        except Exception:
-            _TUNED = {}
+        import json
+        table = {}
+        for path in (_SHIPPED_TUNE_PATH, _TUNE_PATH):
+            try:
+                table.update(json.loads(Path(path).read_text()))
+            except Exception:
+                pass
+        _TUNED = table
     return _TUNED
 
 
 def _save_tuned():
-    if os.environ.get("RANK", "0") != "0":
+    """Persist the table to the user cache (never the installed package)."""
+    if os.environ.get("RANK", "0") != "0" or _TUNE_PATH.resolve() == _SHIPPED_TUNE_PATH.resolve():
         return
     try:
         import json
+        _TUNE_PATH.parent.mkdir(parents=True, exist_ok=True)
         tmp = str(_TUNE_PATH) + f".tmp{os.getpid()}"
         with open(tmp, "w") as f:
             json.dump(_TUNED, f, indent=0, sort_keys=True)
@@ -228,8 +246,45 @@ def _save_tuned():
         pass
 
 
+def _capturing() -> bool:
+    return torch.cuda.is_available() and torch.cuda.is_current_stream_capturing()
+
+
 def _tune_allowed() -> bool:
-    return os.environ.get("PDT_AUTOTUNE", "1") != "0" and not torch.cuda.is_current_stream_capturing()
+    if _TUNE_FROZEN or _capturing():
+        return False
+    if os.environ.get("PDT_AUTOTUNE", "1") == "0" or os.environ.get("PDT_DETERMINISTIC", "0") == "1":
+        return False
+    return _TUNE_FORCE or int(os.environ.get("WORLD_SIZE", "1")) <= 1
+
+
+def pretune_distributed(run_step) -> None:
+    """Agree on kernel variants across ranks before DDP training starts.
+
+    ``run_step()`` runs one forward+backward on this rank's model (not yet
+    DDP-wrapped). Rank 0 runs it with tuning enabled, then broadcasts its table;
+    every rank adopts it and tuning is frozen (untuned shapes later fall back to
+    the deterministic heuristic on every rank alike)."""
+    global _TUNE_FORCE, _TUNE_FROZEN
+    import torch.distributed as dist
+    if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
+        return
+    obj = [None]
+    if dist.get_rank() == 0:
+        tune_on = os.environ.get("PDT_AUTOTUNE", "1") != "0" and os.environ.get("PDT_DETERMINISTIC", "0") != "1"
+        if tune_on:
+            _TUNE_FORCE = True
+            try:
+                run_step()
+                if torch.cuda.is_available():
+                    torch.cuda.synchronize()
+            finally:
+                _TUNE_FORCE = False
+        obj = [dict(_tuned())]
+    dist.broadcast_object_list(obj, src=0)
+    _tuned().clear()
+    _tuned().update(obj[0])
+    _TUNE_FROZEN = True
 
 
 NOT_APPLICABLE = -5  # kernel return code: this variant cannot run this geometry
@@ -304,7 +359,7 @@ def _check_nt(src, b, out, a):
     assert a["Nimg"] * a["Hs"] * a["Ws"] * Cs < 2 ** 31 and a["Nimg"] * a["Ho"] * a["Wo"] < 2 ** 31
 
 
-def select_nt_variant(src, b, out, *, with_stats=False, bias=None, act=0, **a):
+def select_nt_variant(src, b, out, *, with_stats=False, bias=None, act=0, aux=None, **a):
     """Variant id for this geometry (tuning it on first use when allowed)."""
     M = a["Nimg"] * a["Hm"] * a["Wm"]
     key = "nt5:" + ",".join(str(a[k]) for k in ("Hs", "Ws", "Cs", "Nimg", "Hm", "Wm", "Ncol", "K", "sh", "sw",
@@ -315,14 +370,14 @@ def select_nt_variant(src, b, out, *, with_stats=False, bias=None, act=0, **a):
     if key in table:
         return int(table[key])
     lib = _load()
-    if (os.environ.get("PDT_AUTOTUNE", "1") == "0" or torch.cuda.is_current_stream_capturing()):
+    if not _tune_allowed():
         return lib.pdt_conv_nt_resolve_variant(-1, M, a["Ncol"], a["K"])
     _check_nt(src, b, out, a)
     nvar = lib.pdt_conv_nt_num_variants()
     # partial-stat rows depend on the variant's BM and waves-along-M: size for the largest
     rows = max(lib.pdt_conv_nt_stat_rows(M, a["Ncol"], a["K"], v) for v in range(nvar))
     stats = torch.empty(2 * rows * a["Ncol"], dtype=torch.float32, device=src.device) if with_stats else None
-    best = _time_variants(nvar, lambda v: lib.pdt_conv_nt(*_nt_args(src, b, out, stats, bias, a, act, v)),
+    best = _time_variants(nvar, lambda v: lib.pdt_conv_nt(*_nt_args(src, b, out, stats, bias, a, act, v, aux=aux)),
                           _variant_filter())
     table[key] = best
     _save_tuned()
@@ -343,12 +398,17 @@ def conv_nt(src, b, out, *, stats=None, bias=None, relu=False, act=None, variant
     if aux is not None:
         assert aux.dtype == torch.bfloat16 and aux.numel() == out.numel()
     if variant is None:
-        variant = select_nt_variant(src, b, out, with_stats=stats is not None, bias=bias, act=act_id, **a)
+        variant = select_nt_variant(src, b, out, with_stats=stats is not None, bias=bias, act=act_id, aux=aux, **a)
     if addend_mask is not None:
         assert addend is not None and addend_mask.dtype == torch.uint8 and addend_mask.numel() * 8 == addend.numel()
         assert a["ldo"] == a["Ncol"]
-    _chk(_load().pdt_conv_nt(*_nt_args(src, b, out, stats, bias, a, act_id, variant, addend, aux, addend_mask)),
-         "conv_nt")
+    lib = _load()
+    rc = lib.pdt_conv_nt(*_nt_args(src, b, out, stats, bias, a, act_id, variant, addend, aux, addend_mask))
+    if rc == NOT_APPLICABLE:  # a cached variant tuned for another epilogue (e.g. the streaming 1x1 kernel)
+        M = a["Nimg"] * a["Hm"] * a["Wm"]
+        variant = lib.pdt_conv_nt_resolve_variant(-1, M, a["Ncol"], a["K"])
+        rc = lib.pdt_conv_nt(*_nt_args(src, b, out, stats, bias, a, act_id, variant, addend, aux, addend_mask))
+    _chk(rc, "conv_nt")
 
 
 def _check_addend(addend, out, addend_mask, Ncol):
@@ -391,7 +451,7 @@ def conv_wgrad(dy, x, out, *, scale=1.0, accumulate=False, variant=None, **a):
         table = _tuned()
         if key in table:
             variant = int(table[key])
-        elif os.environ.get("PDT_AUTOTUNE", "1") == "0" or torch.cuda.is_current_stream_capturing():
+        elif not _tune_allowed():
             variant = -1
         else:
             ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -1391,6 +1451,14 @@ class _Linear(torch.autograd.Function):
 E4M3, E5M2 = 0, 1
 
 
+def fp8_settings() -> dict:
+    """The fp8 recipe actually in effect (read by the layers AND by bench.py's
+    dtype label, so the label cannot drift from the code's defaults)."""
+    return {"scaling": os.environ.get("PDT_FP8_SCALING", "delayed"),
+            "dgrad": os.environ.get("PDT_FP8_DGRAD", "0") == "1",
+            "attn": os.environ.get("PDT_FP8_ATTN", "0") == "1"}
+
+
 def quantize_fp8(x: torch.Tensor, fmt: int = E4M3):
     """(q uint8 same shape, dq fp32[1]) with x ~= q.float() * dq (per-tensor scale)."""
     lib = _load()
@@ -1473,7 +1541,8 @@ class _LinearF8(torch.autograd.Function):
         x2 = x.reshape(-1, shp[-1]).to(torch.bfloat16).contiguous()
         Mrows, K = x2.shape
         Nout = w.shape[0]
-        if os.environ.get("PDT_FP8_SCALING", "delayed") == "current":
+        cfg = fp8_settings()
+        if cfg["scaling"] == "current":
             xq, dqx = quantize_fp8(x2, E4M3)
         else:  # delayed scaling: one pass, amax history kept on the module
             xq, dqx, meta = quantize_fp8_delayed(x2, getattr(fc, "_pdt_fp8_meta", None), E4M3)
@@ -1487,7 +1556,7 @@ class _LinearF8(torch.autograd.Function):
         ctx.meta = (shp, act, b is not None)
         # e5m2 data-gradient GEMM only on request: its dY quantisation pass costs
         # about what the fp8 GEMM saves over the bf16 one (PDT_FP8_DGRAD=1)
-        ctx.fp8_dgrad = os.environ.get("PDT_FP8_DGRAD", "0") == "1"
+        ctx.fp8_dgrad = cfg["dgrad"]
         return y.reshape(*shp[:-1], Nout)
 
     @staticmethod

@@ -8,8 +8,9 @@ it); the state_dict format is torch's (``momentum_buffer`` / ``exp_avg`` /
 with the torch optimizers of the same name.
 
 On GPU one HIP kernel (``csrc/optim.hip``) updates every parameter tensor:
-the host builds a chunk table once (re-built only if the set of tensors or
-their storage changes) and each step is a single launch that also writes the
+the host builds a chunk table once per parameter set, re-uploads pointer
+tables only when a tensor moved (asynchronously, from pinned memory: nothing in
+``step()`` blocks the host) and each step is a single launch that also writes the
 bf16 shadow copy of each parameter that the conv/GEMM kernels consume. On CPU
 (gloo plumbing) the step falls back to torch's reference implementation.
 """
@@ -32,35 +33,54 @@ def _bump_versions(params):
         increment_version(p)
 
 
-class _Plan:
-    """Device-side pointer/chunk tables for one param group."""
+def _to_device_async(host: torch.Tensor, device) -> torch.Tensor:
+    """H2D copy that never blocks the host: stage through pinned memory (the
+    caching host allocator keeps the pinned block alive until the copy has run)
+    -- a pageable ``.to(device)`` waits for the whole queued step to drain."""
+    if device.type != "cuda":
+        return host.to(device)
+    return host.pin_memory().to(device, non_blocking=True)
 
-    def __init__(self, params, tensors_by_role, device):
+
+class _Plan:
+    """Device-side pointer/chunk tables for one param group.
+
+    The chunk table depends only on the parameter sizes and is built once; the
+    pointer tables are re-uploaded (asynchronously) only when a tensor moved,
+    e.g. after ``zero_grad(set_to_none=True)`` handed autograd fresh gradient
+    buffers at new addresses."""
+
+    def __init__(self, params, device):
         from ..ops import native_ops
         lib = native_ops._load()
         sz = lib.pdt_chunk_struct_size()
         assert sz == 24, sz
-        chunks = []
-        for ti, p in enumerate(params):
-            n = p.numel()
-            for off in range(0, n, CHUNK):
-                chunks.append((ti, 0, off, min(CHUNK, n - off)))
         import numpy as np
-        arr = np.zeros(len(chunks), dtype=[("t", "<i4"), ("pad", "<i4"), ("off", "<i8"), ("len", "<i8")])
-        for i, c in enumerate(chunks):
-            arr[i] = c
-        self.chunks = torch.from_numpy(arr.view(np.uint8).copy()).to(device)
-        self.nchunks = len(chunks)
+        sizes = [p.numel() for p in params]
+        nch = sum((n + CHUNK - 1) // CHUNK for n in sizes)
+        arr = np.zeros(nch, dtype=[("t", "<i4"), ("pad", "<i4"), ("off", "<i8"), ("len", "<i8")])
+        i = 0
+        for ti, n in enumerate(sizes):
+            for off in range(0, n, CHUNK):
+                arr[i] = (ti, 0, off, min(CHUNK, n - off))
+                i += 1
+        self.device = device
+        self.chunks = _to_device_async(torch.from_numpy(arr.view(np.uint8).copy()), device)
+        self.nchunks = nch
+        self.shape_key = self._shape_key(params)
         self.tables = {}
-        for role, ts in tensors_by_role.items():
-            ptrs = [0 if t is None else t.data_ptr() for t in ts]
-            self.tables[role] = torch.tensor(ptrs, dtype=torch.int64).to(device)
-        self.key = self._key(params, tensors_by_role)
+        self.ptr_keys = {}
 
     @staticmethod
-    def _key(params, tensors_by_role):
-        return tuple((role, tuple(0 if t is None else t.data_ptr() for t in ts)) for role, ts in
-                     sorted(tensors_by_role.items())) + tuple(p.data_ptr() for p in params)
+    def _shape_key(params):
+        return tuple((id(p), p.numel()) for p in params)
+
+    def update(self, tensors_by_role):
+        for role, ts in tensors_by_role.items():
+            ptrs = tuple(0 if t is None else t.data_ptr() for t in ts)
+            if self.ptr_keys.get(role) != ptrs:
+                self.tables[role] = _to_device_async(torch.tensor(ptrs, dtype=torch.int64), self.device)
+                self.ptr_keys[role] = ptrs
 
     def ptr(self, role):
         t = self.tables.get(role)
@@ -95,11 +115,11 @@ class _FusedBase(Optimizer):
         return s
 
     def _plan(self, gi, params, roles, device):
-        key = _Plan._key(params, roles)
         plan = self._plans.get(gi)
-        if plan is None or plan.key != key:
-            plan = _Plan(params, roles, device)
+        if plan is None or plan.shape_key != _Plan._shape_key(params):
+            plan = _Plan(params, device)
             self._plans[gi] = plan
+        plan.update(roles)
         return plan
 
     @staticmethod

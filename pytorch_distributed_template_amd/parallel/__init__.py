@@ -1,1 +1,1 @@
-from .ddp import wrap_ddp, bucket_plan  # noqa: F401
+from .ddp import wrap_ddp, bucket_plan, pretune_for_ddp  # noqa: F401

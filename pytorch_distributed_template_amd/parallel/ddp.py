@@ -51,6 +51,30 @@ def wrap_ddp(model: torch.nn.Module, device: torch.device, bucket_cap_mb: float 
     return ddp
 
 
+def pretune_for_ddp(model: torch.nn.Module, step_fn) -> None:
+    """Make every rank run the same kernel variants before DDP training starts.
+
+    ``step_fn()`` runs one forward+backward of the (unwrapped) model. Rank 0
+    runs it with the tile autotuner on and broadcasts the resulting table; all
+    ranks then freeze it (``ops.native_ops.pretune_distributed``). The step's
+    side effects are undone: gradients are dropped and BatchNorm running stats
+    restored (DDP's constructor then broadcasts rank 0's parameters/buffers).
+    No-op for one rank, on CPU, or without the native library."""
+    if get_world_size() <= 1:
+        return
+    from ..ops import fused, native_ops
+    if fused.get_backend() == "torch" or not native_ops.available():
+        return
+    saved = [b.detach().clone() for b in model.buffers()]
+    try:
+        native_ops.pretune_distributed(step_fn)
+    finally:
+        model.zero_grad(set_to_none=True)
+        with torch.no_grad():
+            for b, s in zip(model.buffers(), saved):
+                b.copy_(s)
+
+
 def bucket_plan(model: torch.nn.Module, bucket_cap_mb: float = DEFAULT_BUCKET_MB):
     """Return the bucket sizes (bytes) DDP will build, for docs/tests."""
     import torch.distributed as dist

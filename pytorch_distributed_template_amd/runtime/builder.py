@@ -25,7 +25,7 @@ from .. import optim as module_optim
 from ..models import loss as module_loss
 from ..models import metric as module_metric
 from ..ops import fused
-from ..parallel import wrap_ddp
+from ..parallel import pretune_for_ddp, wrap_ddp
 
 
 def build_model(config, device):
@@ -62,6 +62,28 @@ def wrap_model(config, model, device):
                     gradient_as_bucket_view=ddp_cfg.get("gradient_as_bucket_view", True),
                     comm_hook=ddp_cfg.get("comm_hook"),
                     find_unused_parameters=ddp_cfg.get("find_unused_parameters", False))
+
+
+def pretune_model(config, model, data_loader, criterion, device):
+    """World size > 1 on the native backend: one forward+backward on rank 0 tunes
+    the kernel variants, which are broadcast to every rank before DDP wraps the
+    model (``parallel.pretune_for_ddp``). Other cases: no-op."""
+    from ..utils.dist import get_world_size
+    if get_world_size() <= 1 or device.type != "cuda":
+        return
+
+    def step():
+        data, target = next(iter(data_loader))
+        data, target = data.to(device, non_blocking=True), target.to(device, non_blocking=True)
+        if config["trainer"].get("channels_last", False) and data.dim() == 4 \
+                and getattr(data, "pdt_nhwc_pad", None) is None:
+            data = data.contiguous(memory_format=torch.channels_last)
+        with torch.autocast(device_type=device.type, dtype=autocast_dtype(config, device) or torch.bfloat16,
+                            enabled=autocast_dtype(config, device) is not None):
+            loss = criterion(model(data), target)
+        loss.backward()
+
+    pretune_for_ddp(model, step)
 
 
 def autocast_dtype(config, device):

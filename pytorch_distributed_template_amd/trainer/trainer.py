@@ -70,7 +70,9 @@ class Trainer(BaseTrainer):
 
     def _to_device(self, data, target):
         data = data.to(self.device, non_blocking=True)
-        if self.channels_last and data.dim() == 4:
+        # a loader's NHWC-padded batch (``pdt_nhwc_pad``) is already in the layout the
+        # native stem reads in place: re-laying it out would copy it and drop the tag
+        if self.channels_last and data.dim() == 4 and getattr(data, "pdt_nhwc_pad", None) is None:
             data = data.contiguous(memory_format=torch.channels_last)
         return data, target.to(self.device, non_blocking=True)
 

@@ -43,21 +43,6 @@ def inf_loop(data_loader):
         yield from loader
 
 
-def prepare_device(n_gpu_use):
-    """Return (device, device_ids) for ``n_gpu_use`` local GPUs (legacy helper,
-    kept for API parity; one-process-per-GPU DDP does not use it)."""
-    n_gpu = torch.cuda.device_count()
-    if n_gpu_use > 0 and n_gpu == 0:
-        print("Warning: There's no GPU available on this machine, training will be performed on CPU.")
-        n_gpu_use = 0
-    if n_gpu_use > n_gpu:
-        print(f"Warning: The number of GPU's configured to use is {n_gpu_use}, but only {n_gpu} are "
-              "available on this machine.")
-        n_gpu_use = n_gpu
-    device = torch.device("cuda:0" if n_gpu_use > 0 else "cpu")
-    return device, list(range(n_gpu_use))
-
-
 class MetricTracker:
     """Running weighted averages per key.
 

@@ -1,0 +1,51 @@
+#!/bin/bash
+# One parameterised runner for gpurun calls (replaces the old one-off scripts).
+#
+#   gpurun --timeout 900 -- bash scripts/gpu_job.sh TAG job [job ...]
+#
+# Every job runs under its own time limit; the call stops at the first crash,
+# timeout or GPU-fault message. Logs land in gpurun_out/TAG_<job>.txt.
+#
+# jobs:
+#   tests            pytest -m gpu (whole GPU suite)
+#   tests:EXPR       pytest -m gpu -k EXPR
+#   smoke            __graft_entry__.smoke()
+#   bench[:ARGS]     python bench.py ARGS   (ARGS: commas become spaces)
+#   ktrace[:ARGS]    rocprofv3 kernel trace of bench.py --steps 3 --warmup 3 ARGS,
+#                    per-step summary via scripts/step_profile.py
+#   hiptrace[:ARGS]  rocprofv3 HIP-API + kernel trace (host-sync hunting)
+#   pmc:CTRS:ARGS    one counter pass (CTRS: commas -> spaces) over bench.py ARGS
+#   py:SCRIPT[:ARGS] python SCRIPT ARGS
+source "$(dirname "$0")/gpurun_lib.sh"
+TAG=$1; shift
+for job in "$@"; do
+  name=${job%%:*}; rest=""; [[ "$job" == *:* ]] && rest=${job#*:}
+  args=${rest//,/ }
+  case $name in
+    tests)
+      if [ -n "$rest" ]; then
+        run ${TAG}_tests.txt 1100 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread -k "$rest"
+      else
+        run ${TAG}_tests.txt 1100 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread
+      fi ;;
+    smoke) run ${TAG}_smoke.txt 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
+    bench) run ${TAG}_bench_$(echo "$args" | tr -c 'a-zA-Z0-9_\n' '_').txt 400 python bench.py $args ;;
+    ktrace)
+      d=gpurun_out/${TAG}_ktrace
+      run ${TAG}_ktrace.txt 400 rocprofv3 --kernel-trace --output-format csv -d $d -o run -- python3 bench.py --steps 3 --warmup 3 $args
+      f=$(find $d -name '*kernel_trace.csv' | head -n 1)
+      python scripts/step_profile.py "$f" --top 60 > gpurun_out/${TAG}_ktrace_step.txt 2>&1 || true ;;
+    hiptrace)
+      d=gpurun_out/${TAG}_hiptrace
+      run ${TAG}_hiptrace.txt 400 rocprofv3 --hip-trace --kernel-trace --output-format csv -d $d -o run -- python3 bench.py --steps 3 --warmup 3 $args ;;
+    pmc)
+      ctrs=${rest%%:*}; bargs=""; [[ "$rest" == *:* ]] && bargs=${rest#*:}
+      d=gpurun_out/${TAG}_pmc_$(echo "$ctrs" | tr -c 'a-zA-Z0-9_\n' '_' | cut -c1-40)
+      run ${TAG}_pmc.txt 240 timeout -s KILL 200 rocprofv3 --pmc ${ctrs//,/ } --output-format csv -d $d -o run -- python3 bench.py --steps 2 --warmup 2 ${bargs//,/ } ;;
+    py)
+      scr=${rest%%:*}; sargs=""; [[ "$rest" == *:* ]] && sargs=${rest#*:}
+      run ${TAG}_py_$(basename $scr .py).txt 600 python -u $scr ${sargs//,/ } ;;
+    *) echo "unknown job $job"; exit 2 ;;
+  esac
+done
+exit 0

@@ -1,0 +1,63 @@
+"""bench.py launcher contract (CPU): ``--gpus N`` must run N ranks or fail loudly.
+
+The driver runs ``python bench.py --gpus N`` (and the torch.distributed.run
+form); a silent 1-rank run reported as the N-GPU point would corrupt the
+scaling curve (missing #1).
+"""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+BENCH = os.path.join(ROOT, "bench.py")
+
+
+def _env():
+    env = dict(os.environ)
+    env["MASTER_ADDR"] = "127.0.0.1"
+    env.pop("WORLD_SIZE", None)
+    env.pop("RANK", None)
+    env.pop("LOCAL_RANK", None)
+    env["OMP_NUM_THREADS"] = "2"
+    return env
+
+
+def _json_line(out: str) -> dict:
+    lines = [ln for ln in out.splitlines() if ln.startswith("{") and '"metric"' in ln]
+    assert len(lines) == 1, out
+    return json.loads(lines[0])
+
+
+def test_bench_self_launches_two_cpu_ranks():
+    r = subprocess.run([sys.executable, BENCH, "--gpus", "2", "--device", "cpu", "--batch", "2", "--image-size", "32",
+                        "--steps", "1", "--warmup", "1"], cwd=ROOT, env=_env(), capture_output=True, text=True,
+                       timeout=600)
+    assert r.returncode == 0, r.stderr[-3000:]
+    rec = _json_line(r.stdout)
+    assert rec["n_gpus"] == 2
+    assert rec["config"]["parallelism"] == "dp2"
+    assert rec["config"]["global_batch"] == 4
+    assert rec["config"]["dist_backend"] == "gloo"
+    assert rec["steps"] == 1 and rec["warmup"] == 1
+    assert rec["value"] > 0
+
+
+@pytest.mark.skipif(__import__("torch").cuda.device_count() >= 2, reason="host has >= 2 GPUs")
+def test_bench_refuses_more_gpus_than_visible():
+    r = subprocess.run([sys.executable, BENCH, "--gpus", "2", "--steps", "1", "--warmup", "0"], cwd=ROOT, env=_env(),
+                       capture_output=True, text=True, timeout=300)
+    assert r.returncode == 2
+    assert "GPU(s) are visible" in r.stderr
+    assert '"metric"' not in r.stdout
+
+
+def test_bench_rejects_world_size_mismatch():
+    env = _env()
+    env["WORLD_SIZE"] = "2"
+    r = subprocess.run([sys.executable, BENCH, "--gpus", "1", "--steps", "1", "--warmup", "0"], cwd=ROOT, env=env,
+                       capture_output=True, text=True, timeout=300)
+    assert r.returncode == 2
+    assert "WORLD_SIZE=2" in r.stderr

@@ -141,3 +141,29 @@ def test_single_run_dir_across_ranks(tmp_path):
     assert res[0]["dir"] == res[1]["dir"]
     runs = list((tmp_path / "D" / "train").iterdir())
     assert len(runs) == 1 and (runs[0] / "config.json").exists()
+
+
+def _w_pretune(rank, world, port, q):
+    try:
+        _init(rank, world, port)
+        from pytorch_distributed_template_amd.ops import native_ops as no
+        calls = []
+
+        def step():  # stands in for the tuning forward+backward: only rank 0 may run it
+            calls.append(rank)
+            assert no._tune_allowed()
+            no._tuned()["nt5:test"] = 7
+
+        no._tuned().pop("nt5:test", None)
+        assert not no._tune_allowed()  # WORLD_SIZE > 1: ranks never time variants on their own
+        no.pretune_distributed(step)
+        q.put((rank, {"calls": calls, "entry": no._tuned().get("nt5:test"), "allowed": no._tune_allowed()}))
+    except Exception as e:  # pragma: no cover
+        q.put((rank, repr(e)))
+
+
+def test_pretune_broadcasts_rank0_table():
+    res = _run(_w_pretune)
+    assert res[0]["calls"] == [0] and res[1]["calls"] == []
+    assert res[0]["entry"] == 7 and res[1]["entry"] == 7
+    assert not res[0]["allowed"] and not res[1]["allowed"]

@@ -20,7 +20,8 @@ import torch
 
 from pytorch_distributed_template_amd.config import ConfigParser
 from pytorch_distributed_template_amd.runtime import (autocast_dtype, build_criterion_metrics, build_loader,
-                                                      build_model, build_optimizer, wrap_model)
+                                                      build_model, build_optimizer, pretune_model,
+                                                      wrap_model)
 from pytorch_distributed_template_amd.trainer import Trainer
 from pytorch_distributed_template_amd.utils import dist as pdist
 
@@ -31,7 +32,17 @@ def seed_everything(seed, deterministic=False):
     random.seed(seed)
     torch.backends.cudnn.deterministic = deterministic
     torch.backends.cudnn.benchmark = False
-    os.environ["PDT_DETERMINISTIC"] = "1" if deterministic else "0"
+    set_deterministic(deterministic)
+
+
+def set_deterministic(on: bool):
+    """``--deterministic``: MIOpen/torch deterministic algorithms AND fixed native
+    kernel variants (no autotune timing: the shipped table or the heuristic, the
+    same on every run and rank; every reduction in csrc/ is atomic-free)."""
+    if on:
+        torch.backends.cudnn.deterministic = True
+        torch.backends.cudnn.benchmark = False
+        os.environ["PDT_DETERMINISTIC"] = "1"
 
 
 def main(args, config, device):
@@ -40,15 +51,16 @@ def main(args, config, device):
     model = build_model(config, device)
     criterion, metrics = build_criterion_metrics(config)
     optimizer, lr_scheduler = build_optimizer(config, model)
-    model = wrap_model(config, model, device)
 
     data_loader = build_loader(config, "train_loader")
     valid_data_loader = None if args.no_validate else build_loader(config, "valid_loader")
+    tcfg = config["trainer"]
+    pretune_model(config, model, data_loader, criterion, device)  # N ranks agree on kernel variants
+    model = wrap_model(config, model, device)
 
     if pdist.is_main_process():
         logger.info(model)
 
-    tcfg = config["trainer"]
     trainer = Trainer(model, criterion, metrics, optimizer, config=config, device=device,
                       data_loader=data_loader, valid_data_loader=valid_data_loader, lr_scheduler=lr_scheduler,
                       len_epoch=tcfg.get("len_epoch"), autocast_dtype=autocast_dtype(config, device),
@@ -93,6 +105,8 @@ def cli(argv=None):
         config["trainer"]["backend"] = ns.backend
     if ns.seed is not None:
         seed_everything(ns.seed, ns.deterministic)
+    else:
+        set_deterministic(ns.deterministic)
     try:
         return main(ns, config, device)
     finally:
