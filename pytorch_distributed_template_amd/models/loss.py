@@ -1,15 +1,19 @@
 """Loss registry (``"loss"`` key in config). Reference: ``/root/reference/model/loss.py:4-5``.
 
 ``cross_entropy`` routes to the fused softmax-cross-entropy HIP kernel
-(``csrc/softmax_xent.hip``) for GPU tensors; ``nll_loss`` matches the
-reference (model emits log-probabilities).
+(``csrc/xent.hip``) for GPU tensors; ``nll_loss`` matches the reference (model
+emits log-probabilities) and runs the ``csrc/lenet.hip`` NLL kernels on GPU.
 """
+import torch
 import torch.nn.functional as F
 
 from ..ops import fused
 
 
 def nll_loss(output, target):
+    if fused.use_native(output) and output.dim() == 2 and output.dtype == torch.float32:
+        from ..ops import native_ops
+        return native_ops.nll_loss(output, target)
     return F.nll_loss(output, target)
 
 

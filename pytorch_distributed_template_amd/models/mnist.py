@@ -3,6 +3,10 @@
 Same layers and parameter names (conv1 1->10 k5, conv2 10->20 k5, channel
 dropout, fc1 320->50, fc2 50->classes, log-softmax output; 21,840 params),
 so state_dicts line up with the reference's ``MnistModel``.
+
+On an MI355X the whole network runs as two hand-written kernels (forward, and a
+backward that recomputes the forward in LDS: ``csrc/lenet.hip``) instead of
+~45 stock-op launches; on CPU (gloo plumbing) it is plain torch ops.
 """
 import torch
 import torch.nn as nn
@@ -21,6 +25,11 @@ class MnistModel(BaseModel):
         self.fc2 = nn.Linear(50, num_classes)
 
     def forward(self, x):
+        from ..ops import fused
+        if fused.use_native(x):
+            from ..ops import native_ops
+            if native_ops.lenet_supported(self, x) and not x.requires_grad:
+                return native_ops.lenet_forward(self, x)
         h = F.max_pool2d(self.conv1(x), 2).relu()
         h = F.max_pool2d(self.conv2_drop(self.conv2(h)), 2).relu()
         h = torch.flatten(h, 1)

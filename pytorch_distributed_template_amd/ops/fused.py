@@ -33,6 +33,12 @@ def get_backend() -> str:
     return _BACKEND
 
 
+def use_native(x: torch.Tensor) -> bool:
+    """True when ``x``'s op should run on the native HIP kernels (GPU tensor,
+    backend not ``torch``, library present -- ``native`` raises if it is missing)."""
+    return _use_native(x)
+
+
 def _use_native(x: torch.Tensor) -> bool:
     if _BACKEND == "torch" or not x.is_cuda:
         return False

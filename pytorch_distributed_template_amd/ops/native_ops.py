@@ -83,6 +83,11 @@ _SIGS = {
     "pdt_cast_fp8_delayed": (c_int, [P, c_int, c_long, P, c_int, P, P]),
     "pdt_fp8_meta_seed": (c_int, [P, c_long, c_int, P, P]),
     "pdt_attn_bwd": (c_int, [P, P, P, P, P, P, c_int, c_int, c_int, c_float, P]),
+    "pdt_lenet_grad_row": (c_int, [c_int]),
+    "pdt_lenet_fwd": (c_int, [P] * 9 + [c_int, c_int, c_int, c_float, c_float, c_uint, P, P, P, P]),
+    "pdt_lenet_bwd": (c_int, [P] * 9 + [c_int, c_int, c_int, c_float, c_float, c_uint, P, P, P, P]),
+    "pdt_nll_fwd": (c_int, [P, P, c_int, c_int, c_int, P, P, P]),
+    "pdt_nll_bwd": (c_int, [P, P, P, c_int, c_int, c_int, P, P]),
 }
 
 
@@ -1321,83 +1326,45 @@ def global_avg_pool(x):
 # linear (bf16 MFMA GEMM with bias / relu epilogue)
 # =============================================================================
 # -----------------------------------------------------------------------------
-# Plain-GEMM backward of nn.Linear: dX = dY W (NN) and dW = dY^T X (TN). These
-# carry no fused epilogue, so per shape the first call times the native kernels
-# (conv_nt on a transposed bf16 W; the split-K wgrad kernel) against the
-# library GEMM (hipBLASLt through torch.mm, fp32-output for dW) and keeps the
-# faster one ("lg:" keys in the tuned table; PDT_LIB_GEMM=0 forces native).
+# Plain-GEMM backward of nn.Linear (reference op: /root/reference/model/model.py:19,21):
+#   dX = dY W     -> the conv_nt NT kernel on the transposed bf16 weight W^T [K][Nout]
+#                    (cast+transposed once per optimizer version, cached like the bf16 shadow)
+#   dW = dY^T X   -> the split-K weight-gradient kernel (both operands K-outer, read
+#                    through ds_read_b64_tr_b16), fp32 output for the optimizer
+# Both are hand-written kernels with their own tile-variant tuning; there is no
+# library-GEMM branch.
 # -----------------------------------------------------------------------------
-def _lib_gemm_allowed() -> bool:
-    return os.environ.get("PDT_LIB_GEMM", "1") != "0"
+_WT: dict = {}
 
 
-def _linear_dgrad_native(dy2, w):
+def bf16_weight_t(w: torch.Tensor) -> torch.Tensor:
+    """bf16 W^T [K][Nout] of an fp32 [Nout][K] weight, cached per parameter version."""
+    ent = _WT.get(id(w))
+    if ent is not None and ent[0] == w._version and ent[1] == w.data_ptr() and _same_tensor(ent[3], w):
+        return ent[2]
+    Nout, K = w.shape
+    wt = torch.empty((K, Nout), dtype=torch.bfloat16, device=w.device)
+    _chk(_load().pdt_transpose_cast(_p(w.detach().float().contiguous()), _p(wt), Nout, K, _s()), "transpose")
+    _WT[id(w)] = (w._version, w.data_ptr(), wt, _weak(w))
+    return wt
+
+
+def _linear_dgrad(dy2, w):
     Nout, K = w.shape
     Mrows = dy2.shape[0]
-    wt = torch.empty((K, Nout), dtype=torch.bfloat16, device=dy2.device)
-    _chk(_load().pdt_transpose_cast(_p(w.detach().float().contiguous()), _p(wt), Nout, K, _s()), "transpose")
+    wt = bf16_weight_t(w)
     dx = torch.empty((Mrows, K), dtype=torch.bfloat16, device=dy2.device)
     conv_nt(dy2, wt, dx, Hs=1, Ws=1, Cs=Nout, Nimg=Mrows, Hm=1, Wm=1, Ncol=K, K=Nout, ldb=Nout, sh=1, sw=1,
             oh0=0, ow0=0, dh=1, dw=1, nth=1, ntw=1, Ho=1, Wo=1, osh=1, osw=1, oph=0, opw=0, ldo=K)
     return dx
 
 
-def _linear_dgrad_lib(dy2, w):
-    return torch.mm(dy2, bf16_weight(w))
-
-
-def _linear_wgrad_native(dy2, x2, w):
+def _linear_wgrad(dy2, x2, w):
     Nout, K = w.shape
     dw = torch.empty((Nout, K), dtype=torch.float32, device=dy2.device)
     conv_wgrad(dy2, x2, dw, M=dy2.shape[0], Mo=Nout, No=K, ldy=Nout, Hs=1, Ws=1, C=K, Hm=1, Wm=1, sh=1, sw=1,
                oh0=0, ow0=0, dh=1, dw=1, ntw=1)
     return dw
-
-
-def _linear_wgrad_lib(dy2, x2, w):
-    return torch.mm(dy2.t(), x2, out_dtype=torch.float32)
-
-
-def _pick_impl(key, native, library):
-    """'native' or 'lib' for this GEMM shape, timed once (both produce the same result)."""
-    table = _tuned()
-    if key in table:
-        return table[key]
-    if not (_lib_gemm_allowed() and _tune_allowed()):
-        return "native"
-    native()  # warm: also runs the native kernels' own variant tuning
-    library()
-    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    times = {}
-    for name, fn in (("native", native), ("lib", library)):
-        t = float("inf")
-        for _ in range(2):
-            ev0.record()
-            for _ in range(3):
-                fn()
-            ev1.record()
-            ev1.synchronize()
-            t = min(t, ev0.elapsed_time(ev1))
-        times[name] = t
-    table[key] = min(times, key=times.get)
-    _save_tuned()
-    return table[key]
-
-
-def _linear_dgrad(dy2, w):
-    Nout, K = w.shape
-    key = f"lgd:{dy2.shape[0]},{Nout},{K}"
-    impl = _pick_impl(key, lambda: _linear_dgrad_native(dy2, w), lambda: _linear_dgrad_lib(dy2, w)) \
-        if _lib_gemm_allowed() else "native"
-    return _linear_dgrad_lib(dy2, w) if impl == "lib" else _linear_dgrad_native(dy2, w)
-
-
-def _linear_wgrad(dy2, x2, w):
-    Nout, K = w.shape
-    key = f"lgw2:{dy2.shape[0]},{Nout},{K}"
-    impl = _pick_impl(key, lambda: _linear_wgrad_native(dy2, x2, w), lambda: _linear_wgrad_lib(dy2, x2, w)) \
-        if _lib_gemm_allowed() else "native"
-    return _linear_wgrad_lib(dy2, x2, w) if impl == "lib" else _linear_wgrad_native(dy2, x2, w)
 
 
 class _Linear(torch.autograd.Function):
@@ -1776,3 +1743,97 @@ def patch_embed(x, conv):
         y = conv(x)
         return y.flatten(2).transpose(1, 2)
     return _PatchEmbed.apply(x, conv.weight, conv.bias, conv)
+
+
+# =============================================================================
+# MnistModel (the reference's LeNet, /root/reference/model/model.py:6-22) as two
+# whole-network kernels (csrc/lenet.hip: one workgroup per image, all layers in
+# LDS, fp32 like the reference), and the NLL loss (/root/reference/model/loss.py:5).
+# =============================================================================
+def lenet_supported(model, x) -> bool:
+    c1, c2, f1, f2 = model.conv1, model.conv2, model.fc1, model.fc2
+    return (x.is_cuda and x.dim() == 4 and tuple(x.shape[1:]) == (1, 28, 28)
+            and (c1.in_channels, c1.out_channels, c1.kernel_size, c1.stride, c1.padding) == (1, 10, (5, 5), (1, 1), (0, 0))
+            and (c2.in_channels, c2.out_channels, c2.kernel_size, c2.stride, c2.padding) == (10, 20, (5, 5), (1, 1), (0, 0))
+            and (f1.in_features, f1.out_features) == (320, 50) and f2.in_features == 50 and f2.out_features <= 64
+            and all(t is not None for t in (c1.bias, c2.bias, f1.bias, f2.bias)))
+
+
+def _lenet_params(model):
+    return [t.detach().float().contiguous() for t in (model.conv1.weight, model.conv1.bias, model.conv2.weight,
+                                                      model.conv2.bias, model.fc1.weight, model.fc1.bias,
+                                                      model.fc2.weight, model.fc2.bias)]
+
+
+class _LeNet(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, w1, b1, w2, b2, wf1, bf1, wf2, bf2, training, p2, p1, seed, masks):
+        x = x.float().contiguous()
+        ps = [t.float().contiguous() for t in (w1, b1, w2, b2, wf1, bf1, wf2, bf2)]
+        B, NC = x.shape[0], wf2.shape[0]
+        logp = torch.empty((B, NC), dtype=torch.float32, device=x.device)
+        m2, m1 = (masks if masks is not None else (None, None))
+        _chk(_load().pdt_lenet_fwd(*[_p(t) for t in [x] + ps], B, NC, int(training), float(p2), float(p1),
+                                   seed & 0xFFFFFFFF, _p(logp), _p(m2), _p(m1), _s()), "lenet_fwd")
+        ctx.save_for_backward(x, *ps)
+        ctx.meta = (B, NC, int(training), float(p2), float(p1), seed & 0xFFFFFFFF)
+        return logp
+
+    @staticmethod
+    def backward(ctx, g):
+        x, *ps = ctx.saved_tensors
+        B, NC, training, p2, p1, seed = ctx.meta
+        lib = _load()
+        row = lib.pdt_lenet_grad_row(NC)
+        part = torch.empty(B * row, dtype=torch.float32, device=x.device)
+        flat = torch.empty(row, dtype=torch.float32, device=x.device)
+        g = g.float().contiguous()
+        _chk(lib.pdt_lenet_bwd(*[_p(t) for t in [x] + ps], B, NC, training, p2, p1, seed, _p(g), _p(part), _p(flat),
+                               _s()), "lenet_bwd")
+        grads, off = [], 0
+        for t in ps:  # flat layout = parameter order (csrc/lenet.hip O_*)
+            grads.append(flat[off:off + t.numel()].view(t.shape))
+            off += t.numel()
+        assert off == row
+        if ctx.needs_input_grad[0]:
+            raise NotImplementedError("native LeNet does not produce an input gradient")
+        return (None, *grads, None, None, None, None, None)
+
+
+def lenet_forward(model, x, masks=None, seed=None):
+    """log-probabilities of MnistModel on x [B, 1, 28, 28] (Dropout2d / dropout active in training)."""
+    p2 = model.conv2_drop.p if model.training else 0.0
+    p1 = 0.5 if model.training else 0.0
+    if seed is None:
+        seed = int(torch.randint(0, 2 ** 31 - 1, (1,)).item()) if model.training else 0  # host RNG: no device sync
+    return _LeNet.apply(x, model.conv1.weight, model.conv1.bias, model.conv2.weight, model.conv2.bias,
+                        model.fc1.weight, model.fc1.bias, model.fc2.weight, model.fc2.bias, model.training, p2, p1,
+                        seed, masks)
+
+
+class _NLL(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, logp, target, ignore_index):
+        logp = logp.float().contiguous()
+        target = target.to(torch.long).contiguous()
+        B, C = logp.shape
+        assert target.numel() == B
+        out = torch.empty(2, dtype=torch.float32, device=logp.device)  # loss, count
+        _chk(_load().pdt_nll_fwd(_p(logp), _p(target), B, C, int(ignore_index), _p(out[0]), _p(out[1]), _s()),
+             "nll_fwd")
+        ctx.save_for_backward(target, out)
+        ctx.meta = (B, C, int(ignore_index))
+        return out[0].clone()
+
+    @staticmethod
+    def backward(ctx, g):
+        target, out = ctx.saved_tensors
+        B, C, ignore = ctx.meta
+        d = torch.empty((B, C), dtype=torch.float32, device=target.device)
+        _chk(_load().pdt_nll_bwd(_p(target), _p(g.float().reshape(1).contiguous()), _p(out[1]), B, C, ignore, _p(d),
+                                 _s()), "nll_bwd")
+        return d, None, None
+
+
+def nll_loss(logp, target, ignore_index=-100):
+    return _NLL.apply(logp, target, ignore_index)
