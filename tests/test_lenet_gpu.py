@@ -119,10 +119,15 @@ def test_mnist_config_step_uses_native_path():
     from pytorch_distributed_template_amd.models import loss as L
     m = _model(3).train()
     opt = torch.optim.Adam(m.parameters(), lr=1e-3, amsgrad=True)
-    x = torch.randn(128, 1, 28, 28, device="cuda")
-    y = torch.randint(0, 10, (128,), device="cuda")
+    # a learnable task (noisy class prototypes): random labels on random images with
+    # dropout 0.5 barely move in a few dozen steps (stock torch drops to ~0.42x in 40)
+    g = torch.Generator().manual_seed(5)
+    proto = torch.randn(10, 1, 28, 28, generator=g)
+    y = torch.randint(0, 10, (128,), generator=g)
+    x = (proto[y] + 0.5 * torch.randn(128, 1, 28, 28, generator=g)).cuda()
+    y = y.cuda()
     losses = []
-    for _ in range(30):
+    for _ in range(40):
         opt.zero_grad()
         out = m(x)
         assert out.grad_fn is not None and "LeNet" in type(out.grad_fn).__name__
@@ -130,4 +135,4 @@ def test_mnist_config_step_uses_native_path():
         loss.backward()
         opt.step()
         losses.append(loss.item())
-    assert losses[-1] < losses[0] * 0.8, losses
+    assert losses[-1] < losses[0] * 0.7, losses
