@@ -39,9 +39,13 @@ BASELINE_METRIC = "images/sec (whole node) ResNet-50 synthetic 3x224x224 at 1/2/
 # (`bench.py --backend torch --batch B`), keyed by (model, per-GPU batch), see
 # BASELINE.md. Scaled by N for N GPUs (weak scaling).
 STOCK_1GPU_IMG_S = {("resnet50", 256): 6605.4, ("resnet50", 512): 6863.8}
-# Per-GPU batch: 512 images (21 GiB of the 288 GiB HBM3E) -- the stage-3/4 GEMMs
-# (M = N*14*14, N*7*7) fill all 256 CUs only from ~512 images up.
-DEFAULT_BATCH = {"resnet50": 512}
+# At a batch the stock stack was not measured at (its MIOpen find at bs 1024 ran
+# past 390 s on one box), compare against its BEST measured per-GPU throughput.
+STOCK_BEST_1GPU_IMG_S = {"resnet50": (6863.8, 512)}
+# Per-GPU batch: 1024 images (41 GiB of the 288 GiB HBM3E). The stage-3/4 GEMMs
+# (M = N*14*14, N*7*7) fill all 256 CUs only from ~512 images up; measured on one
+# MI355X: 11.96k img/s at 512, 12.45k at 768, 12.66k at 1024 (profiles/bench_runs_round2.jsonl).
+DEFAULT_BATCH = {"resnet50": 1024}
 
 
 def parse():
@@ -267,6 +271,10 @@ def main():
     ms = elapsed / args.steps * 1e3
     value = world * args.batch * args.steps / elapsed
     stock = STOCK_1GPU_IMG_S.get((args.model, args.batch))
+    stock_ref = f"stock PyTorch-ROCm at per-GPU batch {args.batch}" if stock else None
+    if stock is None and args.model in STOCK_BEST_1GPU_IMG_S:
+        stock, sb = STOCK_BEST_1GPU_IMG_S[args.model]
+        stock_ref = f"stock PyTorch-ROCm best measured (per-GPU batch {sb})"
     rec = {
         "metric": BASELINE_METRIC if args.model == "resnet50" else f"images/sec (whole node) {args.model} synthetic",
         "value": round(value, 2),
@@ -287,6 +295,7 @@ def main():
                    "rccl_version": _rccl_version(), "device": args.device,
                    "final_loss": round(final_loss, 4), "hip_graph": args.graph,
                    "cpu_issue_ms_per_step": round(cpu_issue / args.steps * 1e3, 3),
+                   "baseline": stock_ref,
                    "max_mem_gib": round(torch.cuda.max_memory_allocated() / 2 ** 30, 2) if not cpu else None},
     }
     if rank == 0:

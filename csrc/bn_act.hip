@@ -235,7 +235,7 @@ __global__ void __launch_bounds__(256) bn_bwd_finalize_kernel(const float* __res
 // -------------------------------------------------------------------- apply
 // MASK: also write the ReLU mask as one bit per element (byte i = chunk i's 8
 // channels): the backward then reads 1/16 of the bytes instead of `out`.
-template <bool RES, bool RELU, bool MASK = false>
+template <bool RES, bool RELU, bool MASK = false, int U = 1>
 __global__ void __launch_bounds__(NT) bn_apply_kernel(const u16* __restrict__ y, const u16* __restrict__ res,
                                                       u16* __restrict__ out, const float* __restrict__ scale,
                                                       const float* __restrict__ shift, long n8, int C,
@@ -247,14 +247,15 @@ __global__ void __launch_bounds__(NT) bn_apply_kernel(const u16* __restrict__ y,
   float sc[8], sh[8];
   load8f(scale + ch, sc);
   load8f(shift + ch, sh);
-  for (uint32_t i = blockIdx.x * NT + threadIdx.x; i < (uint32_t)n8; i += gridDim.x * NT) {
+  const uint32_t S = gridDim.x * NT;
+  auto body = [&](uint32_t i, const u32x4& yv, const u32x4& rv) {
     float f[8];
-    unpack8(reinterpret_cast<const u32x4*>(y)[i], f);
+    unpack8(yv, f);
 #pragma unroll
     for (int k = 0; k < 8; ++k) f[k] = f[k] * sc[k] + sh[k];
     if (RES) {
       float r[8];
-      unpack8(reinterpret_cast<const u32x4*>(res)[i], r);
+      unpack8(rv, r);
 #pragma unroll
       for (int k = 0; k < 8; ++k) f[k] += r[k];
     }
@@ -273,6 +274,24 @@ __global__ void __launch_bounds__(NT) bn_apply_kernel(const u16* __restrict__ y,
       }
       mask[i] = (uint8_t)m;
     }
+  };
+  uint32_t i = blockIdx.x * NT + threadIdx.x;
+  // U chunks per trip, every load issued before any is consumed (memory-level
+  // parallelism); the tail runs one chunk per trip (no per-load predicates)
+  for (; U > 1 && i + (U - 1) * S < (uint32_t)n8; i += U * S) {
+    u32x4 yv[U], rv[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      yv[u] = reinterpret_cast<const u32x4*>(y)[i + u * S];
+      if (RES) rv[u] = reinterpret_cast<const u32x4*>(res)[i + u * S];
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) body(i + u * S, yv[u], RES ? rv[u] : yv[u]);
+  }
+  for (; i < (uint32_t)n8; i += S) {
+    const u32x4 yv = reinterpret_cast<const u32x4*>(y)[i];
+    const u32x4 rv = RES ? reinterpret_cast<const u32x4*>(res)[i] : yv;
+    body(i, yv, rv);
   }
 }
 
@@ -391,7 +410,7 @@ __global__ void __launch_bounds__(NT) bn_bwd_reduce_kernel(const u16* __restrict
   }
 }
 
-template <bool RELU, bool USE_ACT, bool DRES, bool USE_MASK = false, bool POOL = false>
+template <bool RELU, bool USE_ACT, bool DRES, bool USE_MASK = false, bool POOL = false, int U = 1>
 __global__ void __launch_bounds__(NT) bn_bwd_apply_kernel(const u16* __restrict__ dA, const u16* __restrict__ y,
                                                           const u16* __restrict__ act,
                                                           const float* __restrict__ scale,
@@ -410,21 +429,18 @@ __global__ void __launch_bounds__(NT) bn_bwd_apply_kernel(const u16* __restrict_
     load8f(scale + ch, sc);
     load8f(shift + ch, sh);
   }
-  for (uint32_t i = blockIdx.x * NT + threadIdx.x; i < (uint32_t)n8; i += gridDim.x * NT) {
-    float g[8], yv[8];
-    if (POOL)
-      pool_grad8(ps, i / (uint32_t)cpr, ch / 8, cpr, g);
-    else
-      unpack8(reinterpret_cast<const u32x4*>(dA)[i], g);
-    unpack8(reinterpret_cast<const u32x4*>(y)[i], yv);
+  const uint32_t S = gridDim.x * NT;
+  // g: dA chunk (already gathered for POOL), yq: y chunk, gate: act chunk or mask byte
+  auto body = [&](uint32_t i, float (&g)[8], const u32x4& yq, const u32x4& aq, uint32_t m) {
+    float yv[8];
+    unpack8(yq, yv);
     if (RELU) {
       if (USE_MASK) {
-        const uint32_t m = mask[i];
 #pragma unroll
         for (int k = 0; k < 8; ++k) g[k] = (m >> k) & 1u ? g[k] : 0.f;
       } else if (USE_ACT) {
         float a[8];
-        unpack8(reinterpret_cast<const u32x4*>(act)[i], a);
+        unpack8(aq, a);
 #pragma unroll
         for (int k = 0; k < 8; ++k) g[k] = a[k] > 0.f ? g[k] : 0.f;
       } else {
@@ -436,7 +452,53 @@ __global__ void __launch_bounds__(NT) bn_bwd_apply_kernel(const u16* __restrict_
 #pragma unroll
     for (int k = 0; k < 8; ++k) g[k] = a1[k] * g[k] + a2[k] * yv[k] + a3[k];
     reinterpret_cast<u32x4*>(dy)[i] = pack8(g);
+  };
+  uint32_t i = blockIdx.x * NT + threadIdx.x;
+  if constexpr (!POOL && U > 1) {
+    // U chunks per trip, all loads first (see bn_apply_kernel)
+    for (; i + (U - 1) * S < (uint32_t)n8; i += U * S) {
+      u32x4 gq[U], yq[U], aq[U];
+      uint32_t mb[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        gq[u] = reinterpret_cast<const u32x4*>(dA)[i + u * S];
+        yq[u] = reinterpret_cast<const u32x4*>(y)[i + u * S];
+        if (RELU && USE_MASK) mb[u] = mask[i + u * S];
+        else mb[u] = 0;
+        if (RELU && !USE_MASK && USE_ACT) aq[u] = reinterpret_cast<const u32x4*>(act)[i + u * S];
+        else aq[u] = yq[u];
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        float g[8];
+        unpack8(gq[u], g);
+        body(i + u * S, g, yq[u], aq[u], mb[u]);
+      }
+    }
   }
+  for (; i < (uint32_t)n8; i += S) {
+    float g[8];
+    if (POOL)
+      pool_grad8(ps, i / (uint32_t)cpr, ch / 8, cpr, g);
+    else
+      unpack8(reinterpret_cast<const u32x4*>(dA)[i], g);
+    const u32x4 yq = reinterpret_cast<const u32x4*>(y)[i];
+    const u32x4 aq = (RELU && !USE_MASK && USE_ACT) ? reinterpret_cast<const u32x4*>(act)[i] : yq;
+    const uint32_t m = (RELU && USE_MASK) ? (uint32_t)mask[i] : 0u;
+    body(i, g, yq, aq, m);
+  }
+}
+
+// elementwise trip unroll of bn_apply / bn_bwd_apply (PDT_BN_UNROLL=1|2|4, default 2;
+// pdt_bn_set_unroll for in-process A/B runs)
+int g_bn_unroll = -1;
+int bn_unroll() {
+  if (g_bn_unroll < 0) {
+    const char* e = getenv("PDT_BN_UNROLL");
+    int u = e ? atoi(e) : 2;
+    g_bn_unroll = (u == 1 || u == 2 || u == 4) ? u : 2;
+  }
+  return g_bn_unroll;
 }
 
 int gcd_i(int a, int b) { return b ? gcd_i(b, a % b) : a; }
@@ -454,6 +516,12 @@ int grid_for(long n8, int C) {
 }
 
 }  // namespace
+
+PDT_API int pdt_bn_set_unroll(int u) {
+  if (u != 1 && u != 2 && u != 4) return -1;
+  g_bn_unroll = u;
+  return 0;
+}
 
 PDT_API int pdt_bn_stats_blocks(long M, int C) {
   int cpr = C / 8;
@@ -527,8 +595,13 @@ PDT_API int pdt_bn_apply(const void* y, const void* res, void* out, const float*
   const u16* R = (const u16*)res;
   u16* O = (u16*)out;
   uint8_t* MK = (uint8_t*)mask;
-#define APPLY(R_, U_, M_) \
-  hipLaunchKernelGGL((bn_apply_kernel<R_, U_, M_>), g, b, 0, st, Y, R, O, scale, shift, n8, C, MK)
+  const int un = bn_unroll();
+#define APPLY(R_, U_, M_)                                                                                   \
+  do {                                                                                                      \
+    if (un == 4) hipLaunchKernelGGL((bn_apply_kernel<R_, U_, M_, 4>), g, b, 0, st, Y, R, O, scale, shift, n8, C, MK); \
+    else if (un == 2) hipLaunchKernelGGL((bn_apply_kernel<R_, U_, M_, 2>), g, b, 0, st, Y, R, O, scale, shift, n8, C, MK); \
+    else hipLaunchKernelGGL((bn_apply_kernel<R_, U_, M_, 1>), g, b, 0, st, Y, R, O, scale, shift, n8, C, MK); \
+  } while (0)
   if (res) {
     if (relu) { if (mask) APPLY(true, true, true); else APPLY(true, true, false); }
     else APPLY(true, false, false);
@@ -576,12 +649,21 @@ PDT_API int pdt_bn_bwd_apply(const void* dA, const void* y, const void* act, con
   const u16 *G = (const u16*)dA, *Y = (const u16*)y, *A = (const u16*)act;
   u16 *DY = (u16*)dy, *DR = (u16*)dres;
   const uint8_t* MK = (const uint8_t*)mask;
-#define BWD_APPLY(R_, U_, D_) \
-  hipLaunchKernelGGL((bn_bwd_apply_kernel<R_, U_, D_>), g, b, 0, st, G, Y, A, scale, shift, k1, k2, k3, DY, DR, n8, C, \
-                     MK)
-#define BWD_APPLY_M(D_) \
-  hipLaunchKernelGGL((bn_bwd_apply_kernel<true, false, D_, true>), g, b, 0, st, G, Y, A, scale, shift, k1, k2, k3, DY, \
-                     DR, n8, C, MK)
+  const int un = bn_unroll();
+#define BWD_LAUNCH(R_, U_, D_, M_)                                                                                   \
+  do {                                                                                                               \
+    if (un == 4)                                                                                                     \
+      hipLaunchKernelGGL((bn_bwd_apply_kernel<R_, U_, D_, M_, false, 4>), g, b, 0, st, G, Y, A, scale, shift, k1, k2, \
+                         k3, DY, DR, n8, C, MK, PoolSrc{});                                                          \
+    else if (un == 2)                                                                                                \
+      hipLaunchKernelGGL((bn_bwd_apply_kernel<R_, U_, D_, M_, false, 2>), g, b, 0, st, G, Y, A, scale, shift, k1, k2, \
+                         k3, DY, DR, n8, C, MK, PoolSrc{});                                                          \
+    else                                                                                                             \
+      hipLaunchKernelGGL((bn_bwd_apply_kernel<R_, U_, D_, M_, false, 1>), g, b, 0, st, G, Y, A, scale, shift, k1, k2, \
+                         k3, DY, DR, n8, C, MK, PoolSrc{});                                                          \
+  } while (0)
+#define BWD_APPLY(R_, U_, D_) BWD_LAUNCH(R_, U_, D_, false)
+#define BWD_APPLY_M(D_) BWD_LAUNCH(true, false, D_, true)
   if (!relu) {
     if (dres) BWD_APPLY(false, false, true); else BWD_APPLY(false, false, false);
   } else if (mask) {
@@ -593,6 +675,7 @@ PDT_API int pdt_bn_bwd_apply(const void* dA, const void* y, const void* act, con
   }
 #undef BWD_APPLY
 #undef BWD_APPLY_M
+#undef BWD_LAUNCH
   PDT_RETURN_LAUNCH();
 }
 

@@ -307,6 +307,7 @@ static int conv_nt_impl(const void* src, const void* b, void* out, float* stats,
   if (Cs % 8 != 0 || K % 8 != 0 || Ncol % 8 != 0 || ldo % 8 != 0 || ldb % 8 != 0) return -1;
   if (pix != 0 && (pix % 4 != 0 || pix > Cs)) return -10;
   if (K != nth * ntw * Cs) return -2;
+  if (act == 3 && (addend == nullptr || addend_mask != nullptr || aux != nullptr || bias != nullptr)) return -4;
   NTParams p;
   p.src = (const u16*)src;
   p.b = (const u16*)b;
@@ -382,7 +383,8 @@ PDT_API int pdt_conv_nt_bnb(const void* src, const void* b, void* out, const voi
 
 // ---------------------------------------------------------------------------
 // fp8 GEMM  out[m, n] = dq_a * dq_b * sum_k A[m, k] B[n, k] (+ bias, act, aux)
-// A: [M][lda] fp8 (e4m3 if fmt_a == 0, e5m2 if 1), B: [N][ldb] e4m3, out bf16 [M][ldo].
+// A: [M][lda] fp8 (e4m3 if fmt_a == 0, e5m2 if 1), B: [N][ldb] e4m3, out bf16 [M][ldo],
+// optional bf16 addend [M][ldo] (residual add, or the GELU-backward operand with act 3).
 // K, lda, ldb in BYTES (= elements), multiples of 128 / 16 / 16.
 namespace {
 constexpr int NVAR_F8 = 11;
@@ -412,7 +414,7 @@ PDT_API int pdt_gemm_f8_num_variants() { return NVAR_F8; }
 
 PDT_API int pdt_gemm_f8(const void* a, const void* b, void* out, const float* bias, const float* dq_a,
                         const float* dq_b, int M, int N, int K, int lda, int ldb, int ldo, int fmt_a, int act,
-                        void* aux, int variant, hipStream_t stream) {
+                        void* aux, const void* addend, int variant, hipStream_t stream) {
   if (K % 128 != 0 || lda % 16 != 0 || ldb % 16 != 0 || N % 8 != 0 || ldo % 8 != 0) return -1;
   if (lda != K) return -2;  // rows of A are dense (the gather's source row stride is Cs)
   NTParams p;
@@ -421,8 +423,9 @@ PDT_API int pdt_gemm_f8(const void* a, const void* b, void* out, const float* bi
   p.out = (u16*)out;
   p.stats = nullptr;
   p.bias = bias;
-  p.addend = nullptr;
+  p.addend = (const u16*)addend;  // [M][ldo] bf16: out += addend (act 3: out *= gelu'(addend))
   p.addend_mask = nullptr;
+  if (act == 3 && (addend == nullptr || aux != nullptr || bias != nullptr)) return -4;
   p.Hs = 1; p.Ws = 1; p.Cs = K / 2;
   p.Hm = 1; p.Wm = 1;
   p.M = M;

@@ -37,7 +37,9 @@ struct NTParams {
   int M, Ncol, K, ldb;
   int sh, sw, oh0, ow0, dh, dw, nth, ntw;
   int Ho, Wo, osh, osw, oph, opw, ldo;
-  int act;             // 0 none, 1 relu, 2 gelu(tanh)
+  int act;             // 0 none, 1 relu, 2 gelu(tanh), 3 GELU backward: out = C * gelu'(addend)
+                       //   (addend = the saved pre-activation z; fuses the activation backward
+                       //   into the data-gradient GEMM that produces dL/dgelu(z))
   int pix;             // elements per source pixel in memory (= Cs, or Cs/2 for the space-to-depth stem
                        // whose 16-B chunk spans two adjacent 4-channel pixels)
   u16* aux;            // optional: pre-activation copy of the output (same layout)
@@ -53,6 +55,14 @@ struct NTParams {
 
 constexpr int BK = 64;
 constexpr int NT = 256;
+
+// d gelu_tanh(z) / dz
+__device__ __forceinline__ float gelu_grad(float z) {
+  const float u = 0.7978845608f * (z + 0.044715f * z * z * z);
+  const float t = tanhf(u);
+  const float du = 0.7978845608f * (1.f + 3.f * 0.044715f * z * z);
+  return 0.5f * (1.f + t) + 0.5f * z * (1.f - t * t) * du;
+}
 
 __device__ __forceinline__ int swz(int row, int chunk) { return chunk ^ ((row >> 1) & 7); }
 
@@ -589,7 +599,12 @@ __global__ void __launch_bounds__(NTH, PIPE ? 1 : 2) conv_nt_kernel(NTParams p) 
             a.x &= ((mb & 1u) ? 0xffffu : 0u) | ((mb & 2u) ? 0xffff0000u : 0u);
             a.y &= ((mb & 4u) ? 0xffffu : 0u) | ((mb & 8u) ? 0xffff0000u : 0u);
           }
-          v0 += lo_bf(a.x); v1 += hi_bf(a.x); v2 += lo_bf(a.y); v3 += hi_bf(a.y);
+          if (p.act == 3) {
+            v0 *= gelu_grad(lo_bf(a.x)); v1 *= gelu_grad(hi_bf(a.x));
+            v2 *= gelu_grad(lo_bf(a.y)); v3 *= gelu_grad(hi_bf(a.y));
+          } else {
+            v0 += lo_bf(a.x); v1 += hi_bf(a.x); v2 += lo_bf(a.y); v3 += hi_bf(a.y);
+          }
         }
         uint2 w;
         w.x = pack2bf(v0, v1);
@@ -645,8 +660,14 @@ __global__ void __launch_bounds__(NTH, PIPE ? 1 : 2) conv_nt_kernel(NTParams p) 
             for (int e = 0; e < 4; ++e)
               a[e] &= ((mb >> (2 * e)) & 1u ? 0xffffu : 0u) | ((mb >> (2 * e + 1)) & 1u ? 0xffff0000u : 0u);
           }
+          if (p.act == 3) {
 #pragma unroll
-          for (int e = 0; e < 4; ++e) v[e] = pack2bf(lo_bf(v[e]) + lo_bf(a[e]), hi_bf(v[e]) + hi_bf(a[e]));
+            for (int e = 0; e < 4; ++e)
+              v[e] = pack2bf(lo_bf(v[e]) * gelu_grad(lo_bf(a[e])), hi_bf(v[e]) * gelu_grad(hi_bf(a[e])));
+          } else {
+#pragma unroll
+            for (int e = 0; e < 4; ++e) v[e] = pack2bf(lo_bf(v[e]) + lo_bf(a[e]), hi_bf(v[e]) + hi_bf(a[e]));
+          }
         }
         u32x4* dp = reinterpret_cast<u32x4*>(dst + orow * p.ldo + col);
         if (p.nt_store) __builtin_nontemporal_store(v, dp);
@@ -659,7 +680,7 @@ __global__ void __launch_bounds__(NTH, PIPE ? 1 : 2) conv_nt_kernel(NTParams p) 
     stage_store(p.aux, nullptr);
     if (!DIRECT) __syncthreads();
   }
-  if (p.act != 0) {
+  if (p.act == 1 || p.act == 2) {
 #pragma unroll
     for (int i = 0; i < MI; ++i)
 #pragma unroll

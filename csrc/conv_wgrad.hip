@@ -41,6 +41,8 @@ struct WGParams {
   int sh, sw, oh0, ow0, dh, dw, ntw;
   int ktiles_per_split, splits;
   int xcd;           // 1: XCD-aware block mapping (PDT_WGRAD_XCD=0 disables, for A/B runs)
+  float* bslab;      // optional [splits][Mo]: per-split column sums of dY (nn.Linear bias gradient),
+                     // accumulated by the tn == 0 blocks from the dY tiles they stage anyway
   FastDiv div_Wm, div_HWm, div_C, div_ntw;
 };
 
@@ -138,6 +140,11 @@ __global__ void __launch_bounds__(NTH, NTH == NT ? 2 : 1) wgrad_kernel(WGParams 
   const int offh = p.oh0 + p.dh * th, offw = p.ow0 + p.dw * tw;
 
   u32x4 ra[NA], rb[NB];
+  // bias-gradient partials: summed from the registers at LDS-store time (the
+  // loads have landed by then -- consuming them at load time would wait out the
+  // prefetch); block-uniform predicate
+  const bool dobias = p.bslab != nullptr && tn == 0;
+  float bsum[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
 
   auto load_into = [&](int kt, u32x4 (&ra)[NA], u32x4 (&rb)[NB]) {
     const int k0 = kt * BK;
@@ -170,6 +177,15 @@ __global__ void __launch_bounds__(NTH, NTH == NT ? 2 : 1) wgrad_kernel(WGParams 
   auto store_from = [&](int buf, const u32x4 (&ra)[NA], const u32x4 (&rb)[NB]) {
     char* sa = smem + buf * STAGE;
     char* sb = sa + A_BYTES;
+    if (dobias) {
+#pragma unroll
+      for (int i = 0; i < NA; ++i)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          bsum[2 * e] += lo_bf(ra[i][e]);
+          bsum[2 * e + 1] += hi_bf(ra[i][e]);
+        }
+    }
 #pragma unroll
     for (int i = 0; i < NA; ++i)
       *reinterpret_cast<u32x4*>(sa + lds_off<RBA>(rA0 + AROWS * i, cA * 16)) = ra[i];
@@ -265,6 +281,24 @@ __global__ void __launch_bounds__(NTH, NTH == NT ? 2 : 1) wgrad_kernel(WGParams 
   }
   }
 
+  if (dobias) {
+    // lanes sharing a column chunk (tid % ACH) combine through LDS
+    __syncthreads();  // every wave is done reading the operand stages
+    float* red = reinterpret_cast<float*>(smem);  // [NTH][8]
+#pragma unroll
+    for (int k = 0; k < 8; ++k) red[tid * 8 + k] = bsum[k];
+    __syncthreads();
+    if (tid < ACH && co0 + tid * 8 < p.Mo) {
+      float t8[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+      for (int j = 0; j < AROWS; ++j)
+#pragma unroll
+        for (int k = 0; k < 8; ++k) t8[k] += red[(j * ACH + tid) * 8 + k];
+      float* bo = p.bslab + (size_t)split * p.Mo + co0 + tid * 8;
+      *reinterpret_cast<f32x4*>(bo) = f32x4{t8[0], t8[1], t8[2], t8[3]};
+      *reinterpret_cast<f32x4*>(bo + 4) = f32x4{t8[4], t8[5], t8[6], t8[7]};
+    }
+  }
+
   float* out = p.slab + (size_t)split * p.Mo * p.No;
 #pragma unroll
   for (int i = 0; i < MI; ++i) {
@@ -354,20 +388,27 @@ PDT_API int pdt_wgrad_plan(int M, int Mo, int No, int variant, int* ktiles_per_s
   return splits;
 }
 
-// floats of workspace pdt_conv_wgrad needs for `splits` slabs (slabs + stage-1 partials)
-PDT_API long pdt_wgrad_workspace(int splits, int Mo, int No) {
+// stage-1 slab groups of the reduction: enough (column-block x group) blocks to stream the slabs
+static int reduce_groups(int splits, int Mo, int No) {
   long n4 = (long)Mo * No / 4;
   int xb = (int)((n4 + 255) / 256);
-  long G = splits < 2 ? 1 : 1024 / xb;
+  int G = splits < 2 ? 1 : (int)(1024 / xb);
   if (G > splits / 4) G = splits / 4;
   if (G < 1) G = 1;
-  return (long)splits * Mo * No + (G > 1 ? G * Mo * No : 0);
+  return G;
+}
+
+// floats of workspace pdt_conv_wgrad needs for `splits` slabs: slabs + stage-1
+// partials + the [splits][Mo] bias-gradient slab
+PDT_API long pdt_wgrad_workspace(int splits, int Mo, int No) {
+  const long G = reduce_groups(splits, Mo, No);
+  return (long)splits * Mo * No + (G > 1 ? G * Mo * No : 0) + (long)splits * Mo;
 }
 
 PDT_API int pdt_conv_wgrad(const void* dy, const void* x, float* slab, float* out, int M, int Mo, int No,
                            int ldy, int Hs, int Ws, int C, int Hm, int Wm, int sh, int sw, int oh0, int ow0,
                            int dh, int dw, int ntw, int splits, int ktiles_per_split, float scale,
-                           int accumulate, int variant, int pix, hipStream_t stream) {
+                           int accumulate, int variant, int pix, float* bias_out, hipStream_t stream) {
   if (C % 8 != 0 || Mo % 8 != 0 || No % 8 != 0 || ldy % 8 != 0) return -1;
   if (pix != 0 && (pix % 4 != 0 || pix > C)) return -10;
   WGParams p;
@@ -379,6 +420,9 @@ PDT_API int pdt_conv_wgrad(const void* dy, const void* x, float* slab, float* ou
   p.pix = pix > 0 ? pix : C;
   p.sh = sh; p.sw = sw; p.oh0 = oh0; p.ow0 = ow0; p.dh = dh; p.dw = dw; p.ntw = ntw;
   p.ktiles_per_split = ktiles_per_split; p.splits = splits;
+  const int G = reduce_groups(splits, Mo, No);
+  // bias_out (optional, fp32 [Mo]): also the column sums of dY, from the same pass
+  p.bslab = bias_out ? slab + (long)splits * Mo * No + (G > 1 ? (long)G * Mo * No : 0) : nullptr;
   {
     static int xcd_env = -1;
     if (xcd_env < 0) {
@@ -431,10 +475,10 @@ PDT_API int pdt_conv_wgrad(const void* dy, const void* x, float* slab, float* ou
   if (e) return e;
   long n4 = (long)Mo * No / 4;
   int xb = (int)((n4 + 255) / 256);
-  // enough (column-block x slab-group) blocks to stream the slabs at full rate
-  int G = splits < 2 ? 1 : (int)(1024 / xb);
-  if (G > splits / 4) G = splits / 4;
-  if (G < 1) G = 1;
+  if (bias_out) {
+    hipLaunchKernelGGL(wgrad_reduce1_kernel, dim3((Mo / 4 + 255) / 256, 1), dim3(256), 0, stream, p.bslab, bias_out,
+                       (long)(Mo / 4), splits, 1, scale, accumulate, 1);
+  }
   if (G == 1) {
     hipLaunchKernelGGL(wgrad_reduce1_kernel, dim3(xb, 1), dim3(256), 0, stream, slab, out, n4, splits, 1, scale,
                        accumulate, 1);

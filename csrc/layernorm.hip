@@ -72,7 +72,8 @@ __global__ void __launch_bounds__(64 * WPB) ln_bwd_kernel(const u16* __restrict_
                                                           const float* __restrict__ g,
                                                           const float* __restrict__ mean_in,
                                                           const float* __restrict__ rstd_in, u16* __restrict__ dx,
-                                                          float* __restrict__ part, int rows, int rows_per_block) {
+                                                          float* __restrict__ part, int rows, int rows_per_block,
+                                                          const u16* __restrict__ addend) {
   constexpr int D = 256 * CH;
   __shared__ float red[2][WPB][D];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -110,6 +111,12 @@ __global__ void __launch_bounds__(64 * WPB) ln_bwd_kernel(const u16* __restrict_
       float o[4];
 #pragma unroll
       for (int e = 0; e < 4; ++e) o[e] = rstd * (gy[c][e] - m1 - xh[c][e] * m2);
+      if (addend != nullptr) {  // residual-branch gradient of the same tensor: dx += addend
+        float r[4];
+        ld4(addend + (long)row * D + (c * 64 + lane) * 4, r);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) o[e] += r[e];
+      }
       st4(dx + (long)row * D + (c * 64 + lane) * 4, o);
     }
   }
@@ -208,18 +215,22 @@ PDT_API int pdt_ln_bwd_blocks(int rows) {
   return b < 1 ? 1 : b;
 }
 
+// addend (optional, bf16 [rows][D]): dx = LN backward + addend (a residual branch's
+// gradient of the same input, summed in the same pass)
 PDT_API int pdt_ln_bwd(const void* dy, const void* x, const float* g, const float* mean, const float* rstd, void* dx,
-                       float* dg, float* db, float* part, int rows, int D, int accumulate, hipStream_t st) {
+                       float* dg, float* db, float* part, int rows, int D, int accumulate, const void* addend,
+                       hipStream_t st) {
   const int blocks = pdt_ln_bwd_blocks(rows);
   const int rpb = ln_rows_per_block(rows);
   dim3 grid(blocks), blk(64 * WPB);
   const u16 *DY = (const u16*)dy, *X = (const u16*)x;
   u16* DX = (u16*)dx;
+  const u16* AD = (const u16*)addend;
   switch (D) {
-    case 256: hipLaunchKernelGGL(ln_bwd_kernel<1>, grid, blk, 0, st, DY, X, g, mean, rstd, DX, part, rows, rpb); break;
-    case 512: hipLaunchKernelGGL(ln_bwd_kernel<2>, grid, blk, 0, st, DY, X, g, mean, rstd, DX, part, rows, rpb); break;
-    case 768: hipLaunchKernelGGL(ln_bwd_kernel<3>, grid, blk, 0, st, DY, X, g, mean, rstd, DX, part, rows, rpb); break;
-    case 1024: hipLaunchKernelGGL(ln_bwd_kernel<4>, grid, blk, 0, st, DY, X, g, mean, rstd, DX, part, rows, rpb); break;
+    case 256: hipLaunchKernelGGL(ln_bwd_kernel<1>, grid, blk, 0, st, DY, X, g, mean, rstd, DX, part, rows, rpb, AD); break;
+    case 512: hipLaunchKernelGGL(ln_bwd_kernel<2>, grid, blk, 0, st, DY, X, g, mean, rstd, DX, part, rows, rpb, AD); break;
+    case 768: hipLaunchKernelGGL(ln_bwd_kernel<3>, grid, blk, 0, st, DY, X, g, mean, rstd, DX, part, rows, rpb, AD); break;
+    case 1024: hipLaunchKernelGGL(ln_bwd_kernel<4>, grid, blk, 0, st, DY, X, g, mean, rstd, DX, part, rows, rpb, AD); break;
     default: return -1;
   }
   int e = (int)hipGetLastError();

@@ -29,11 +29,10 @@ class Attention(nn.Module):
         self.qkv = nn.Linear(dim, dim * 3)
         self.proj = nn.Linear(dim, dim)
 
-    def forward(self, x, fp8=False):
-        B, T, D = x.shape
+    def forward(self, x, fp8=False, residual=None):
         qkv = fused.linear(x, self.qkv, fp8=fp8)                          # [B,T,3D]
         o = fused.qkv_attention(qkv, self.num_heads)                       # [B,T,D]
-        return fused.linear(o, self.proj, fp8=fp8)
+        return fused.linear(o, self.proj, fp8=fp8, residual=residual)     # (+ residual in the epilogue)
 
 
 class Mlp(nn.Module):
@@ -42,8 +41,8 @@ class Mlp(nn.Module):
         self.fc1 = nn.Linear(dim, hidden)
         self.fc2 = nn.Linear(hidden, dim)
 
-    def forward(self, x, fp8=False):
-        return fused.linear(fused.linear(x, self.fc1, act="gelu", fp8=fp8), self.fc2, fp8=fp8)
+    def forward(self, x, fp8=False, residual=None):
+        return fused.mlp(x, self, fp8=fp8, residual=residual)
 
 
 class Block(nn.Module):
@@ -55,9 +54,12 @@ class Block(nn.Module):
         self.mlp = Mlp(dim, int(dim * mlp_ratio))
 
     def forward(self, x, fp8=False):
-        x = x + self.attn(fused.layer_norm(x, self.norm1), fp8=fp8)
-        x = x + self.mlp(fused.layer_norm(x, self.norm2), fp8=fp8)
-        return x
+        # pre-norm residual block; the residual adds ride the proj / fc2 GEMM epilogues and
+        # their gradients are summed inside the LayerNorm backward (fused.ln_fork)
+        x, h = fused.ln_fork(x, self.norm1)
+        x = self.attn(h, fp8=fp8, residual=x)
+        x, h = fused.ln_fork(x, self.norm2)
+        return self.mlp(h, fp8=fp8, residual=x)
 
 
 class VisionTransformer(BaseModel):

@@ -124,13 +124,26 @@ def _torch_linear(x, fc: nn.Linear, act=None):
     return y
 
 
-def linear(x, fc: nn.Linear, act: str | None = None, fp8: bool = False):
-    """y = act(x @ W^T + b). ``act`` in {None, "gelu", "relu"}; ``fp8`` selects the
-    e4m3 GEMM with per-tensor scaling on the native path (ignored on torch path)."""
+def linear(x, fc: nn.Linear, act: str | None = None, fp8: bool = False, residual=None):
+    """y = act(x @ W^T + b) (+ residual). ``act`` in {None, "gelu", "relu"}; ``fp8`` selects
+    the e4m3 GEMM with per-tensor scaling on the native path (ignored on torch path).
+    Native: the residual add runs in the GEMM epilogue."""
     if _use_native(x):
         from . import native_ops
-        return native_ops.linear(x, fc, act=act, fp8=fp8)
-    return _torch_linear(x, fc, act)
+        return native_ops.linear(x, fc, act=act, fp8=fp8, residual=residual)
+    y = _torch_linear(x, fc, act)
+    return y if residual is None else y + residual
+
+
+def mlp(x, m: nn.Module, fp8: bool = False, residual=None):
+    """fc2(gelu_tanh(fc1(x))) (+ residual) of a transformer MLP with ``fc1`` / ``fc2``.
+    Native: one autograd node (GELU backward fused into fc2's data-gradient GEMM,
+    bias gradients from the weight-gradient kernels, residual in fc2's epilogue)."""
+    if _use_native(x):
+        from . import native_ops
+        return native_ops.mlp(x, m, fp8=fp8, residual=residual)
+    y = _torch_linear(_torch_linear(x, m.fc1, "gelu"), m.fc2)
+    return y if residual is None else y + residual
 
 
 def layer_norm(x, ln: nn.LayerNorm):
@@ -138,6 +151,15 @@ def layer_norm(x, ln: nn.LayerNorm):
         from . import native_ops
         return native_ops.layer_norm(x, ln)
     return ln(x)
+
+
+def ln_fork(x, ln: nn.LayerNorm):
+    """(x, ln(x)) for a pre-norm residual block. Native: the residual gradient of x
+    and the normalised branch's gradient are summed inside LayerNorm's backward."""
+    if _use_native(x):
+        from . import native_ops
+        return native_ops.ln_fork(x, ln)
+    return x, ln(x)
 
 
 def attention(q, k, v):

@@ -37,12 +37,12 @@ _SIGS = {
     "pdt_conv_nt_bnb": (c_int, [P] * 5 + [c_int] * 25 + [P] * 6 + [c_int] * 3 + [P]),
     "pdt_ln_fwd": (c_int, [P, P, P, P, P, P, c_int, c_int, c_float, P]),
     "pdt_ln_bwd_blocks": (c_int, [c_int]),
-    "pdt_ln_bwd": (c_int, [P] * 9 + [c_int, c_int, c_int, P]),
+    "pdt_ln_bwd": (c_int, [P] * 9 + [c_int, c_int, c_int, P, P]),
     "pdt_gelu_bwd": (c_int, [P, P, P, c_long, P]),
     "pdt_wgrad_plan": (c_int, [c_int, c_int, c_int, c_int, ctypes.POINTER(c_int)]),
     "pdt_wgrad_num_variants": (c_int, []),
     "pdt_wgrad_workspace": (c_long, [c_int, c_int, c_int]),
-    "pdt_conv_wgrad": (c_int, [P, P, P, P] + [c_int] * 16 + [c_int, c_int, c_float, c_int, c_int, c_int, P]),
+    "pdt_conv_wgrad": (c_int, [P, P, P, P] + [c_int] * 16 + [c_int, c_int, c_float, c_int, c_int, c_int, P, P]),
     "pdt_bn_stats_blocks": (c_int, [c_long, c_int]),
     "pdt_bn_bwd_reduce_pool": (c_int, [P] * 7 + [c_int] * 10 + [P]),
     "pdt_bn_bwd_apply_pool": (c_int, [P] * 9 + [c_int] * 9 + [P]),
@@ -74,7 +74,8 @@ _SIGS = {
     "pdt_add_bf16": (c_int, [P, P, P, c_long, P]),
     "pdt_attn_fwd": (c_int, [P, P, P, c_int, c_int, c_int, c_float, P]),
     "pdt_gemm_f8_num_variants": (c_int, []),
-    "pdt_gemm_f8": (c_int, [P, P, P, P, P, P] + [c_int] * 8 + [P, c_int, P]),
+    "pdt_gemm_f8": (c_int, [P, P, P, P, P, P] + [c_int] * 8 + [P, P, c_int, P]),
+    "pdt_bn_set_unroll": (c_int, [c_int]),
     "pdt_amax_blocks": (c_int, [c_long]),
     "pdt_amax_partial": (c_int, [P, c_int, c_long, P, P]),
     "pdt_cast_fp8": (c_int, [P, c_int, c_long, P, c_int, P, P, P]),
@@ -427,19 +428,21 @@ def conv_stat_rows(M, Ncol, K, variant):
     return _load().pdt_conv_nt_stat_rows(M, Ncol, K, variant)
 
 
-def _wgrad_launch(lib, dy, x, out, v, scale, accumulate, a):
+def _wgrad_launch(lib, dy, x, out, v, scale, accumulate, a, bias_out=None):
     kps = c_int(0)
     splits = lib.pdt_wgrad_plan(a["M"], a["Mo"], a["No"], v, ctypes.byref(kps))
     slab = torch.empty(lib.pdt_wgrad_workspace(splits, a["Mo"], a["No"]), dtype=torch.float32, device=dy.device)
     rc = lib.pdt_conv_wgrad(_p(dy), _p(x), _p(slab), _p(out), a["M"], a["Mo"], a["No"], a["ldy"], a["Hs"], a["Ws"],
                             a["C"], a["Hm"], a["Wm"], a["sh"], a["sw"], a["oh0"], a["ow0"], a["dh"], a["dw"],
                             a["ntw"], splits, kps.value, float(scale), int(accumulate), int(v), int(a.get("pix", 0)),
-                            _s())
+                            _p(bias_out), _s())
     _chk(rc, "conv_wgrad")
 
 
-def conv_wgrad(dy, x, out, *, scale=1.0, accumulate=False, variant=None, **a):
-    """dW[co, tap*C + c] = sum_m dY[m, co] X_gather[m, (tap, c)] (see csrc/conv_wgrad.hip)."""
+def conv_wgrad(dy, x, out, *, scale=1.0, accumulate=False, variant=None, bias_out=None, **a):
+    """dW[co, tap*C + c] = sum_m dY[m, co] X_gather[m, (tap, c)] (see csrc/conv_wgrad.hip).
+    ``bias_out`` (fp32 [Mo]): also sum_m dY[m, co] -- the nn.Linear bias gradient -- from the
+    dY tiles the kernel stages anyway (no separate column-sum pass)."""
     M, Mo, No, ldy, C, Hm, Wm = a["M"], a["Mo"], a["No"], a["ldy"], a["C"], a["Hm"], a["Wm"]
     assert dy.dtype == torch.bfloat16 and x.dtype == torch.bfloat16 and out.dtype == torch.float32
     assert C % 8 == 0 and Mo % 8 == 0 and No % 8 == 0 and ldy % 8 == 0
@@ -448,6 +451,8 @@ def conv_wgrad(dy, x, out, *, scale=1.0, accumulate=False, variant=None, **a):
     assert pix % 4 == 0 and pix <= C
     assert M % (Hm * Wm) == 0 and x.numel() >= (M // (Hm * Wm)) * a["Hs"] * a["Ws"] * pix, "wgrad source too small"
     assert a["ntw"] >= 1 and No % C == 0
+    if bias_out is not None:
+        assert bias_out.dtype == torch.float32 and bias_out.numel() >= Mo and bias_out.is_contiguous()
     lib = _load()
     if variant is None:
         key = "wg2:" + ",".join(str(a[k]) for k in ("M", "Mo", "No", "Hs", "Ws", "C", "Hm", "Wm", "sh", "ntw"))
@@ -474,7 +479,7 @@ def conv_wgrad(dy, x, out, *, scale=1.0, accumulate=False, variant=None, **a):
             table[key] = best
             _save_tuned()
             variant = best
-    _wgrad_launch(lib, dy, x, out, variant, scale, accumulate, a)
+    _wgrad_launch(lib, dy, x, out, variant, scale, accumulate, a, bias_out)
 
 
 def colsum(x, R, C):
@@ -1359,17 +1364,47 @@ def _linear_dgrad(dy2, w):
     return dx
 
 
-def _linear_wgrad(dy2, x2, w):
+def _linear_wgrad(dy2, x2, w, with_bias=False):
+    """(dW fp32 [Nout][K], db fp32 [Nout] or None): db comes out of the same kernel."""
     Nout, K = w.shape
     dw = torch.empty((Nout, K), dtype=torch.float32, device=dy2.device)
+    db = torch.empty(Nout, dtype=torch.float32, device=dy2.device) if with_bias else None
     conv_wgrad(dy2, x2, dw, M=dy2.shape[0], Mo=Nout, No=K, ldy=Nout, Hs=1, Ws=1, C=K, Hm=1, Wm=1, sh=1, sw=1,
-               oh0=0, ow0=0, dh=1, dw=1, ntw=1)
-    return dw
+               oh0=0, ow0=0, dh=1, dw=1, ntw=1, bias_out=db)
+    return dw, db
+
+
+def _linear_grads(dy2, x2, w, want_db, want_dw):
+    if want_dw:
+        dw, db = _linear_wgrad(dy2, x2, w, with_bias=want_db)
+        return dw, db
+    return None, (colsum(dy2, dy2.shape[0], w.shape[0]) if want_db else None)
+
+
+def _residual2d(residual, Mrows, Nout):
+    if residual is None:
+        return None
+    r = residual.reshape(Mrows, Nout)
+    assert r.dtype == torch.bfloat16, "residual stream must be bf16"
+    return r.contiguous()
+
+
+def _gemm_bf16(x2, wb, y, *, bias=None, act=None, aux=None, addend=None):
+    """y[M, N] = x2[M, K] @ wb[N, K]^T (+bias, act) (+addend) on the conv_nt kernel."""
+    Mrows, K = x2.shape
+    Nout = wb.shape[0]
+    conv_nt(x2, wb, y, Hs=1, Ws=1, Cs=K, Nimg=Mrows, Hm=1, Wm=1, Ncol=Nout, K=K, ldb=K, sh=1, sw=1, oh0=0,
+            ow0=0, dh=1, dw=1, nth=1, ntw=1, Ho=1, Wo=1, osh=1, osw=1, oph=0, opw=0, ldo=Nout, bias=bias,
+            act=act, aux=aux, addend=addend)
+    return y
 
 
 class _Linear(torch.autograd.Function):
+    """y = act(x W^T + b) (+ residual): the residual add rides the GEMM epilogue and
+    its gradient is dy itself (no add kernels either way)."""
+
     @staticmethod
-    def forward(ctx, x, w, b, act):
+    def forward(ctx, x, w, b, act, residual):
         shp = x.shape
         x2 = x.reshape(-1, shp[-1]).to(torch.bfloat16).contiguous()
         Mrows, K = x2.shape
@@ -1378,9 +1413,7 @@ class _Linear(torch.autograd.Function):
         y = torch.empty((Mrows, Nout), dtype=torch.bfloat16, device=x.device)
         z = torch.empty_like(y) if act == "gelu" else None  # pre-activation for GELU backward
         bias = b.float().contiguous() if b is not None else None
-        conv_nt(x2, wb, y, Hs=1, Ws=1, Cs=K, Nimg=Mrows, Hm=1, Wm=1, Ncol=Nout, K=K, ldb=K, sh=1, sw=1, oh0=0,
-                ow0=0, dh=1, dw=1, nth=1, ntw=1, Ho=1, Wo=1, osh=1, osw=1, oph=0, opw=0, ldo=Nout, bias=bias,
-                act=act, aux=z)
+        _gemm_bf16(x2, wb, y, bias=bias, act=act, aux=z, addend=_residual2d(residual, Mrows, Nout))
         ctx.save_for_backward(x2, w, y if act == "relu" else z)
         ctx.meta = (shp, act, b is not None)
         return y.reshape(*shp[:-1], Nout)
@@ -1401,11 +1434,8 @@ class _Linear(torch.autograd.Function):
             dy2 = dz
         Mrows = dy2.shape[0]
         dx = _linear_dgrad(dy2, w).reshape(*shp[:-1], K) if ctx.needs_input_grad[0] else None
-        dw = _linear_wgrad(dy2, x2, w) if ctx.needs_input_grad[1] else None
-        db = None
-        if has_b and ctx.needs_input_grad[2]:
-            db = colsum(dy2, Mrows, Nout)
-        return dx, dw, db, None
+        dw, db = _linear_grads(dy2, x2, w, has_b and ctx.needs_input_grad[2], ctx.needs_input_grad[1])
+        return dx, dw, db, None, (dy if ctx.needs_input_grad[4] else None)
 
 
 # =============================================================================
@@ -1485,15 +1515,18 @@ def fp8_weight(w: torch.Tensor):
     return val
 
 
-def gemm_f8(a, b, out, dq_a, dq_b, *, fmt_a=E4M3, bias=None, act=0, aux=None, variant=None):
-    """out[M, N] (bf16) = dq_a*dq_b * a[M, K] @ b[N, K]^T (+bias, act); a, b uint8 fp8 codes."""
+def gemm_f8(a, b, out, dq_a, dq_b, *, fmt_a=E4M3, bias=None, act=0, aux=None, addend=None, variant=None):
+    """out[M, N] (bf16) = dq_a*dq_b * a[M, K] @ b[N, K]^T (+bias, act) (+ addend); a, b uint8 fp8
+    codes. ``act=3``: GELU backward, out = (a @ b^T) * gelu'(addend)."""
     M, K = a.shape
     N = b.shape[0]
     assert a.dtype == torch.uint8 and b.dtype == torch.uint8 and b.shape[1] == K and K % 128 == 0
     assert out.dtype == torch.bfloat16 and out.numel() == M * N and a.is_contiguous() and b.is_contiguous()
     lib = _load()
+    if addend is not None:
+        assert addend.dtype == torch.bfloat16 and addend.numel() == M * N and addend.is_contiguous()
     args = lambda v: (_p(a), _p(b), _p(out), _p(bias), _p(dq_a), _p(dq_b), M, N, K, K, K, N, fmt_a, act,  # noqa
-                      _p(aux), v, _s())
+                      _p(aux), _p(addend), v, _s())
     if variant is None:
         key = f"f8b:{M},{N},{K},{fmt_a},{act},{int(bias is not None)}"
         variant = _autotune(key, lib.pdt_gemm_f8_num_variants(), lambda v: lib.pdt_gemm_f8(*args(v)))
@@ -1501,24 +1534,30 @@ def gemm_f8(a, b, out, dq_a, dq_b, *, fmt_a=E4M3, bias=None, act=0, aux=None, va
     return out
 
 
+def _quant_act(x2, owner, attr="_pdt_fp8_meta"):
+    """e4m3 codes + dequant scale of a bf16 activation under the configured scaling
+    (delayed: amax history kept on ``owner``)."""
+    if fp8_settings()["scaling"] == "current":
+        return quantize_fp8(x2, E4M3)
+    q, dq, meta = quantize_fp8_delayed(x2, getattr(owner, attr, None), E4M3)
+    setattr(owner, attr, meta)
+    return q, dq
+
+
 class _LinearF8(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, w, b, act, fc):
+    def forward(ctx, x, w, b, act, fc, residual):
         shp = x.shape
         x2 = x.reshape(-1, shp[-1]).to(torch.bfloat16).contiguous()
         Mrows, K = x2.shape
         Nout = w.shape[0]
         cfg = fp8_settings()
-        if cfg["scaling"] == "current":
-            xq, dqx = quantize_fp8(x2, E4M3)
-        else:  # delayed scaling: one pass, amax history kept on the module
-            xq, dqx, meta = quantize_fp8_delayed(x2, getattr(fc, "_pdt_fp8_meta", None), E4M3)
-            fc._pdt_fp8_meta = meta
+        xq, dqx = _quant_act(x2, fc)
         wq, _, dqw = fp8_weight(w)
         y = torch.empty((Mrows, Nout), dtype=torch.bfloat16, device=x.device)
         z = torch.empty_like(y) if act == "gelu" else None
         bias = b.float().contiguous() if b is not None else None
-        gemm_f8(xq, wq, y, dqx, dqw, bias=bias, act=ACT[act], aux=z)
+        gemm_f8(xq, wq, y, dqx, dqw, bias=bias, act=ACT[act], aux=z, addend=_residual2d(residual, Mrows, Nout))
         ctx.save_for_backward(x2, w, y if act == "relu" else z)
         ctx.meta = (shp, act, b is not None)
         # e5m2 data-gradient GEMM only on request: its dY quantisation pass costs
@@ -1550,22 +1589,102 @@ class _LinearF8(torch.autograd.Function):
             else:
                 dx = _linear_dgrad(dy2, w)
             dx = dx.reshape(*shp[:-1], K)
-        dw = _linear_wgrad(dy2, x2, w) if ctx.needs_input_grad[1] else None
-        db = None
-        if has_b and ctx.needs_input_grad[2]:
-            db = colsum(dy2, Mrows, Nout)
-        return dx, dw, db, None, None
+        dw, db = _linear_grads(dy2, x2, w, has_b and ctx.needs_input_grad[2], ctx.needs_input_grad[1])
+        return dx, dw, db, None, None, (dy if ctx.needs_input_grad[5] else None)
 
 
-def linear(x, fc: nn.Linear, act=None, fp8=False):
+def linear(x, fc: nn.Linear, act=None, fp8=False, residual=None):
+    """act(x W^T + b) (+ residual, added in the GEMM epilogue)."""
     K = fc.in_features
     N = fc.out_features
-    if K % 8 or N % 8 or act not in (None, "relu", "gelu"):
+    if K % 8 or N % 8 or act not in (None, "relu", "gelu") or (residual is not None and (
+            residual.dtype != torch.bfloat16 or residual.shape[:-1] != x.shape[:-1] or residual.shape[-1] != N)):
         from .fused import _torch_linear
-        return _torch_linear(x, fc, act)
+        y = _torch_linear(x, fc, act)
+        return y if residual is None else y + residual
     if fp8 and K % 128 == 0 and N % 128 == 0:
-        return _LinearF8.apply(x, fc.weight, fc.bias, act, fc)
-    return _Linear.apply(x, fc.weight, fc.bias, act)
+        return _LinearF8.apply(x, fc.weight, fc.bias, act, fc, residual)
+    return _Linear.apply(x, fc.weight, fc.bias, act, residual)
+
+
+# -----------------------------------------------------------------------------
+# Transformer MLP as one autograd node: fc1 (+bias, GELU in the epilogue, the
+# pre-activation z kept as the aux output) -> fc2 (+bias, + residual in the
+# epilogue). Backward: the fc2 data gradient's epilogue applies GELU'(z) (conv_nt
+# act 3), so dL/dz comes out of that GEMM -- no gelu_bwd pass -- and both bias
+# gradients come out of the weight-gradient kernels. fp8 (e4m3 forward operands,
+# e5m2 output gradients when PDT_FP8_DGRAD=1) or bf16 GEMMs.
+# -----------------------------------------------------------------------------
+class _Mlp(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, w1, b1, w2, b2, residual, mlp, fp8):
+        shp = x.shape
+        x2 = x.reshape(-1, shp[-1]).to(torch.bfloat16).contiguous()
+        Mrows, K = x2.shape
+        Hd, Nout = w1.shape[0], w2.shape[0]
+        dev = x.device
+        z = torch.empty((Mrows, Hd), dtype=torch.bfloat16, device=dev)
+        a = torch.empty_like(z)
+        out = torch.empty((Mrows, Nout), dtype=torch.bfloat16, device=dev)
+        res = _residual2d(residual, Mrows, Nout)
+        bias1, bias2 = b1.float().contiguous(), b2.float().contiguous()
+        if fp8:
+            xq, dqx = _quant_act(x2, mlp.fc1)
+            w1q, _, dqw1 = fp8_weight(w1)
+            gemm_f8(xq, w1q, a, dqx, dqw1, bias=bias1, act=ACT["gelu"], aux=z)
+            aq, dqa = _quant_act(a, mlp.fc2)
+            w2q, _, dqw2 = fp8_weight(w2)
+            gemm_f8(aq, w2q, out, dqa, dqw2, bias=bias2, addend=res)
+        else:
+            _gemm_bf16(x2, bf16_weight(w1), a, bias=bias1, act="gelu", aux=z)
+            _gemm_bf16(a, bf16_weight(w2), out, bias=bias2, addend=res)
+        ctx.save_for_backward(x2, a, z, w1, w2)
+        ctx.shp, ctx.fp8 = shp, fp8
+        ctx.fp8_dgrad = fp8 and fp8_settings()["dgrad"]
+        return out.reshape(*shp[:-1], Nout)
+
+    @staticmethod
+    def backward(ctx, g):
+        x2, a, z, w1, w2 = ctx.saved_tensors
+        need = ctx.needs_input_grad
+        Mrows, K = x2.shape
+        Hd, Nout = w1.shape[0], w2.shape[0]
+        g2 = g.reshape(Mrows, Nout).to(torch.bfloat16).contiguous()
+        dz = torch.empty((Mrows, Hd), dtype=torch.bfloat16, device=g.device)
+        if ctx.fp8_dgrad:
+            gq, dqg = quantize_fp8(g2, E5M2)
+            _, w2qt, dqw2 = fp8_weight(w2)
+            gemm_f8(gq, w2qt, dz, dqg, dqw2, fmt_a=E5M2, act=3, addend=z)
+        else:
+            _gemm_bf16(g2, bf16_weight_t(w2), dz, act=3, addend=z)  # dz = (g W2) * gelu'(z)
+        dw2, db2 = _linear_grads(g2, a, w2, need[4], need[3])
+        dx = None
+        if need[0]:
+            dx = torch.empty((Mrows, K), dtype=torch.bfloat16, device=g.device)
+            if ctx.fp8_dgrad:
+                dzq, dqdz = quantize_fp8(dz, E5M2)
+                _, w1qt, dqw1 = fp8_weight(w1)
+                gemm_f8(dzq, w1qt, dx, dqdz, dqw1, fmt_a=E5M2)
+            else:
+                _gemm_bf16(dz, bf16_weight_t(w1), dx)
+            dx = dx.reshape(ctx.shp)
+        dw1, db1 = _linear_grads(dz, x2, w1, need[2], need[1])
+        return dx, dw1, db1, dw2, db2, (g if need[5] else None), None, None
+
+
+def mlp(x, m, fp8=False, residual=None):
+    """fc2(gelu(fc1(x))) (+ residual) for an Mlp module with fc1 / fc2 (ViT)."""
+    fc1, fc2 = m.fc1, m.fc2
+    K, Hd, N = fc1.in_features, fc1.out_features, fc2.out_features
+    ok = (K % 8 == 0 and Hd % 8 == 0 and N % 8 == 0 and fc2.in_features == Hd and fc1.bias is not None
+          and fc2.bias is not None and (residual is None or (residual.dtype == torch.bfloat16
+                                                            and residual.shape[:-1] == x.shape[:-1]
+                                                            and residual.shape[-1] == N)))
+    use8 = fp8 and K % 128 == 0 and Hd % 128 == 0 and N % 128 == 0
+    if not ok:
+        y = linear(linear(x, fc1, act="gelu", fp8=fp8), fc2, fp8=fp8)
+        return y if residual is None else y + residual
+    return _Mlp.apply(x, fc1.weight, fc1.bias, fc2.weight, fc2.bias, residual, m, use8)
 
 
 # =============================================================================
@@ -1600,7 +1719,7 @@ class _LayerNorm(torch.autograd.Function):
         dg = torch.empty(D, dtype=torch.float32, device=dy.device)
         db = torch.empty(D, dtype=torch.float32, device=dy.device)
         _chk(lib.pdt_ln_bwd(_p(dy2), _p(x2), _p(gf), _p(stats[0]), _p(stats[1]), _p(dx), _p(dg), _p(db), _p(part),
-                            rows, D, 0, _s()), "ln_bwd")
+                            rows, D, 0, None, _s()), "ln_bwd")
         return dx.reshape(ctx.shp), dg, db, None
 
 
@@ -1609,6 +1728,56 @@ def layer_norm(x, ln):
     if len(ln.normalized_shape) != 1 or D not in (256, 512, 768, 1024) or not ln.elementwise_affine:
         return ln(x)
     return _LayerNorm.apply(x, ln.weight, ln.bias, ln.eps)
+
+
+class _LNFork(torch.autograd.Function):
+    """(x, LayerNorm(x)) for a pre-norm residual block: the pass-through output feeds
+    the block's residual add (a GEMM epilogue), so backward receives the residual
+    gradient and the normalised branch's gradient together and sums them inside
+    the LayerNorm backward kernel (no add pass)."""
+
+    @staticmethod
+    def forward(ctx, x, g, b, eps):
+        shp = x.shape
+        D = shp[-1]
+        x2 = x.reshape(-1, D).contiguous()
+        rows = x2.shape[0]
+        y = torch.empty_like(x2)
+        stats = torch.empty((2, rows), dtype=torch.float32, device=x.device)
+        gf = g.float().contiguous()
+        _chk(_load().pdt_ln_fwd(_p(x2), _p(gf), _p(b.float().contiguous()), _p(y), _p(stats[0]), _p(stats[1]), rows,
+                                D, float(eps), _s()), "ln_fwd")
+        ctx.save_for_backward(x2, gf, stats)
+        ctx.shp = shp
+        return x.view_as(x), y.reshape(shp)
+
+    @staticmethod
+    def backward(ctx, g_res, dy):
+        x2, gf, stats = ctx.saved_tensors
+        rows, D = x2.shape
+        lib = _load()
+        dev = x2.device
+        if dy is None:
+            return g_res, None, None, None
+        dy2 = dy.reshape(rows, D).to(torch.bfloat16).contiguous()
+        add = g_res.reshape(rows, D).to(torch.bfloat16).contiguous() if g_res is not None else None
+        dx = torch.empty_like(x2)
+        blocks = lib.pdt_ln_bwd_blocks(rows)
+        part = torch.empty(2 * blocks * D, dtype=torch.float32, device=dev)
+        dg = torch.empty(D, dtype=torch.float32, device=dev)
+        db = torch.empty(D, dtype=torch.float32, device=dev)
+        _chk(lib.pdt_ln_bwd(_p(dy2), _p(x2), _p(gf), _p(stats[0]), _p(stats[1]), _p(dx), _p(dg), _p(db), _p(part),
+                            rows, D, 0, _p(add), _s()), "ln_bwd")
+        return dx.reshape(ctx.shp), dg, db, None
+
+
+def ln_fork(x, ln):
+    """(x, ln(x)) with the residual gradient summed in LayerNorm's backward (see _LNFork)."""
+    D = ln.normalized_shape[-1]
+    if (len(ln.normalized_shape) != 1 or D not in (256, 512, 768, 1024) or not ln.elementwise_affine
+            or x.dtype != torch.bfloat16):
+        return x, layer_norm(x, ln)
+    return _LNFork.apply(x, ln.weight, ln.bias, ln.eps)
 
 
 # =============================================================================

@@ -31,10 +31,11 @@ for job in "$@"; do
     smoke) run ${TAG}_smoke.txt 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) run ${TAG}_bench_$(echo "$args" | tr -c 'a-zA-Z0-9_\n' '_').txt 400 python bench.py $args ;;
     ktrace)
-      d=gpurun_out/${TAG}_ktrace
-      run ${TAG}_ktrace.txt 400 rocprofv3 --kernel-trace --output-format csv -d $d -o run -- python3 bench.py --steps 3 --warmup 3 $args
+      sfx=$(echo "$args" | tr -c 'a-zA-Z0-9_\n' '_')
+      d=gpurun_out/${TAG}_ktrace$sfx
+      run ${TAG}_ktrace$sfx.txt 400 rocprofv3 --kernel-trace --output-format csv -d $d -o run -- python3 bench.py --steps 3 --warmup 3 $args
       f=$(find $d -name '*kernel_trace.csv' | head -n 1)
-      python scripts/step_profile.py "$f" --top 60 > gpurun_out/${TAG}_ktrace_step.txt 2>&1 || true ;;
+      python scripts/step_profile.py "$f" --top 60 > gpurun_out/${TAG}_ktrace${sfx}_step.txt 2>&1 || true ;;
     hiptrace)
       d=gpurun_out/${TAG}_hiptrace
       run ${TAG}_hiptrace.txt 400 rocprofv3 --hip-trace --kernel-trace --output-format csv -d $d -o run -- python3 bench.py --steps 3 --warmup 3 $args ;;

@@ -1,0 +1,160 @@
+"""Fusions of the native ViT path against plain PyTorch fp32 references:
+
+* nn.Linear bias gradient computed inside the weight-gradient kernel (every tile variant)
+* GELU backward in the data-gradient GEMM epilogue (conv_nt act 3, bf16 and fp8)
+* residual add in the linear GEMM epilogue (bf16 and fp8) and its gradient
+* LayerNorm fork: residual gradient summed inside the LayerNorm backward
+* the fused transformer MLP node, and a 2-block ViT vs the torch path in fp32
+"""
+import pytest
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+from pytorch_distributed_template_amd.ops import fused  # noqa: E402
+from pytorch_distributed_template_amd.ops import native_ops as no  # noqa: E402
+
+
+def nrmerr(a, b):
+    a, b = a.float(), b.float()
+    return ((a - b).norm() / b.norm().clamp_min(1e-6)).item()
+
+
+def setup_module(module):
+    assert no.available(), "native library must be built and loaded on GPU runs"
+    no.require()
+
+
+def _gelu_grad(z):
+    u = 0.7978845608 * (z + 0.044715 * z ** 3)
+    t = torch.tanh(u)
+    return 0.5 * (1 + t) + 0.5 * z * (1 - t * t) * 0.7978845608 * (1 + 3 * 0.044715 * z * z)
+
+
+@pytest.mark.parametrize("M,Nout,K", [(1576, 768, 2304), (600, 256, 128), (4096, 3072, 768)])
+def test_wgrad_fused_bias_all_variants(M, Nout, K):
+    torch.manual_seed(M + Nout)
+    dy = torch.randn(M, Nout, device="cuda").to(torch.bfloat16)
+    x = torch.randn(M, K, device="cuda").to(torch.bfloat16)
+    ref_w = dy.float().t() @ x.float()
+    ref_b = dy.float().sum(0)
+    lib = no._load()
+    for v in range(lib.pdt_wgrad_num_variants()):
+        dw = torch.empty(Nout, K, device="cuda")
+        db = torch.full((Nout,), float("nan"), device="cuda")
+        no.conv_wgrad(dy, x, dw, M=M, Mo=Nout, No=K, ldy=Nout, Hs=1, Ws=1, C=K, Hm=1, Wm=1, sh=1, sw=1, oh0=0, ow0=0,
+                      dh=1, dw=1, ntw=1, variant=v, bias_out=db)
+        torch.cuda.synchronize()
+        assert nrmerr(dw, ref_w) < 1e-2, (v, nrmerr(dw, ref_w))
+        assert nrmerr(db, ref_b) < 1e-5, (v, nrmerr(db, ref_b))
+
+
+def test_gelu_backward_epilogue_bf16_and_fp8():
+    torch.manual_seed(21)
+    M, N, K = 1000, 3072, 768          # dz[M, N] = (g[M, K] @ W[K, N]) * gelu'(z)
+    g = torch.randn(M, K, device="cuda").to(torch.bfloat16)
+    w = torch.randn(K, N, device="cuda") * 0.05          # fc2 weight [Nout=K][K=N]
+    z = (torch.randn(M, N, device="cuda") * 2).to(torch.bfloat16)
+    ref = (g.float() @ w.to(torch.bfloat16).float()) * _gelu_grad(z.float())
+    out = torch.empty(M, N, dtype=torch.bfloat16, device="cuda")
+    no._gemm_bf16(g, no.bf16_weight_t(w), out, act=3, addend=z)
+    torch.cuda.synchronize()
+    assert nrmerr(out, ref) < 1e-2, nrmerr(out, ref)
+    gq, dqg = no.quantize_fp8(g, no.E5M2)
+    _, wqt, dqw = no.fp8_weight(w)
+    ref8 = ((gq.view(torch.float8_e5m2).float() * dqg) @ (wqt.view(torch.float8_e4m3fn).float() * dqw).t()) \
+        * _gelu_grad(z.float())
+    out8 = torch.empty_like(out)
+    no.gemm_f8(gq, wqt, out8, dqg, dqw, fmt_a=no.E5M2, act=3, addend=z)
+    torch.cuda.synchronize()
+    assert nrmerr(out8, ref8) < 1e-2, nrmerr(out8, ref8)
+
+
+@pytest.mark.parametrize("fp8", [False, True])
+def test_linear_residual_epilogue(fp8):
+    torch.manual_seed(22)
+    fc = nn.Linear(768, 768).cuda()
+    x = torch.randn(3, 197, 768, device="cuda").to(torch.bfloat16).requires_grad_(True)
+    r = torch.randn(3, 197, 768, device="cuda").to(torch.bfloat16).requires_grad_(True)
+    y = no.linear(x, fc, fp8=fp8, residual=r)
+    xr = x.detach().float().requires_grad_(True)
+    rr = r.detach().float().requires_grad_(True)
+    wr = fc.weight.detach().to(torch.bfloat16).float().requires_grad_(True)
+    yr = F.linear(xr, wr, fc.bias.detach()) + rr
+    assert nrmerr(y, yr) < (4e-2 if fp8 else 1e-2), nrmerr(y, yr)
+    g = torch.randn_like(yr).to(torch.bfloat16)
+    y.backward(g)
+    yr.backward(g.float())
+    assert torch.equal(r.grad, g)  # the residual gradient is dy itself
+    assert nrmerr(x.grad, xr.grad) < 2e-2
+    assert nrmerr(fc.weight.grad, wr.grad) < 2e-2
+    assert nrmerr(fc.bias.grad, g.float().sum((0, 1))) < 1e-4
+
+
+def test_ln_fork_sums_residual_gradient():
+    torch.manual_seed(23)
+    ln = nn.LayerNorm(768, eps=1e-6).cuda()
+    with torch.no_grad():
+        ln.weight.uniform_(0.5, 1.5)
+        ln.bias.uniform_(-0.2, 0.2)
+    x = torch.randn(2, 197, 768, device="cuda").to(torch.bfloat16).requires_grad_(True)
+    xid, h = no.ln_fork(x, ln)
+    xr = x.detach().float().requires_grad_(True)
+    hr = F.layer_norm(xr, (768,), ln.weight, ln.bias, 1e-6)
+    assert nrmerr(h, hr) < 1e-2
+    gh = torch.randn_like(hr).to(torch.bfloat16)
+    gres = torch.randn_like(hr).to(torch.bfloat16)
+    ((xid.float() * gres.float()).sum() + (h.float() * gh.float()).sum()).backward()
+    ((xr * gres.float()).sum() + (hr * gh.float()).sum()).backward()
+    assert nrmerr(x.grad, xr.grad) < 2e-2, nrmerr(x.grad, xr.grad)
+
+
+@pytest.mark.parametrize("fp8", [False, True])
+def test_fused_mlp_node(fp8):
+    from pytorch_distributed_template_amd.models.vit import Mlp
+    torch.manual_seed(24)
+    m = Mlp(768, 3072).cuda()
+    x = torch.randn(4, 197, 768, device="cuda").to(torch.bfloat16).requires_grad_(True)
+    r = torch.randn(4, 197, 768, device="cuda").to(torch.bfloat16).requires_grad_(True)
+    y = no.mlp(x, m, fp8=fp8, residual=r)
+    assert "Mlp" in type(y.grad_fn).__name__
+    xr = x.detach().float().requires_grad_(True)
+    w1 = m.fc1.weight.detach().to(torch.bfloat16).float().requires_grad_(True)
+    w2 = m.fc2.weight.detach().to(torch.bfloat16).float().requires_grad_(True)
+    b1 = m.fc1.bias.detach().clone().requires_grad_(True)
+    b2 = m.fc2.bias.detach().clone().requires_grad_(True)
+    yr = F.linear(F.gelu(F.linear(xr, w1, b1), approximate="tanh"), w2, b2) + r.detach().float()
+    tol = 6e-2 if fp8 else 1.5e-2
+    assert nrmerr(y, yr) < tol, nrmerr(y, yr)
+    g = torch.randn_like(yr).to(torch.bfloat16)
+    y.backward(g)
+    yr.backward(g.float())
+    assert torch.equal(r.grad, g)
+    for got, ref, name in ((x.grad, xr.grad, "dx"), (m.fc1.weight.grad, w1.grad, "dw1"),
+                           (m.fc2.weight.grad, w2.grad, "dw2"), (m.fc1.bias.grad, b1.grad, "db1"),
+                           (m.fc2.bias.grad, b2.grad, "db2")):
+        e = nrmerr(got, ref)
+        assert e < (1e-1 if fp8 else 3e-2), (name, e)
+
+
+def test_vit_native_matches_torch_fp32():
+    """2-block ViT-B/16: native bf16 forward/backward vs the torch path in fp32 (same weights)."""
+    from pytorch_distributed_template_amd.models.vit import VisionTransformer
+    torch.manual_seed(25)
+    m = VisionTransformer(depth=2, num_classes=32).cuda()
+    x = torch.randn(4, 3, 224, 224, device="cuda").to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    t = torch.randint(0, 32, (4,), device="cuda")
+    out = {}
+    for backend in ("native", "torch"):
+        fused.set_backend(backend)
+        m.zero_grad(set_to_none=True)
+        logits = m(x if backend == "native" else x.float())
+        loss = fused.softmax_cross_entropy(logits, t)
+        loss.backward()
+        out[backend] = (logits.detach().float(), {n: p.grad.detach().float().clone() for n, p in m.named_parameters()})
+    fused.set_backend("auto")
+    assert nrmerr(out["native"][0], out["torch"][0]) < 3e-2
+    worst = max((nrmerr(out["native"][1][n], out["torch"][1][n]), n) for n in out["torch"][1])
+    assert worst[0] < 8e-2, worst
