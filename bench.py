@@ -128,6 +128,29 @@ def _dtype_label(args) -> str:
             f"{'fp8' if c['attn'] else 'bf16'} attention; bf16 wgrad)+bf16")
 
 
+def allreduce_probe(model, device, world, iters=10):
+    """Time an all-reduce of one gradient-sized fp32 buffer on the job's process group
+    (outside the timed region): the xGMI/RCCL evidence of a multi-GPU run, recorded in
+    the JSON next to the throughput. busbw = 2(n-1)/n * bytes / time (ring-equivalent)."""
+    if world <= 1 or device.type != "cuda":
+        return None
+    n = sum(p.numel() for p in model.parameters() if p.requires_grad)
+    buf = torch.ones(n, dtype=torch.float32, device=device)
+    for _ in range(3):
+        torch.distributed.all_reduce(buf)
+    torch.cuda.synchronize()
+    t = torch.empty(iters, dtype=torch.float64)
+    for i in range(iters):
+        t0 = time.perf_counter()
+        torch.distributed.all_reduce(buf)
+        torch.cuda.synchronize()
+        t[i] = time.perf_counter() - t0
+    ms = float(t.median()) * 1e3
+    nbytes = n * 4
+    return {"bytes": nbytes, "median_ms": round(ms, 3),
+            "busbw_GBps": round(2 * (world - 1) / world * nbytes / (ms / 1e3) / 1e9, 1)}
+
+
 def heartbeat(rank, state, every_s=30.0):
     """Rank 0 prints a progress line to stderr every ``every_s`` seconds (first-step
     autotuning / MIOpen searches can run for minutes without other output)."""
@@ -198,6 +221,7 @@ def main():
 
     # N ranks: rank 0 tunes the kernel variants once and broadcasts them (no per-rank timing)
     pretune_for_ddp(model, _pretune_step)
+    ar = allreduce_probe(model, device, world)
     model = wrap_ddp(model, device, bucket_cap_mb=args.bucket_mb, broadcast_buffers=False,
                      gradient_as_bucket_view=True, comm_hook=args.comm_hook)
 
@@ -296,6 +320,7 @@ def main():
                    "final_loss": round(final_loss, 4), "hip_graph": args.graph,
                    "cpu_issue_ms_per_step": round(cpu_issue / args.steps * 1e3, 3),
                    "baseline": stock_ref,
+                   "grad_allreduce_probe": ar,
                    "max_mem_gib": round(torch.cuda.max_memory_allocated() / 2 ** 30, 2) if not cpu else None},
     }
     if rank == 0:

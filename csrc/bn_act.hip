@@ -489,14 +489,17 @@ __global__ void __launch_bounds__(NT) bn_bwd_apply_kernel(const u16* __restrict_
   }
 }
 
-// elementwise trip unroll of bn_apply / bn_bwd_apply (PDT_BN_UNROLL=1|2|4, default 2;
-// pdt_bn_set_unroll for in-process A/B runs)
+// elementwise trip unroll of bn_apply / bn_bwd_apply (PDT_BN_UNROLL=1|2|4, default 1;
+// pdt_bn_set_unroll for in-process A/B runs). Measured at ResNet-50 stage 1, bs 1024
+// (scripts/bench_bn.py, one MI355X): apply 4.49 / 4.38 / 4.45 TB/s and backward apply
+// 4.91 / 4.47 / 4.44 TB/s for U = 1 / 2 / 4 -- the grid-stride loop already keeps
+// enough bytes in flight; deeper trips only cost occupancy.
 int g_bn_unroll = -1;
 int bn_unroll() {
   if (g_bn_unroll < 0) {
     const char* e = getenv("PDT_BN_UNROLL");
-    int u = e ? atoi(e) : 2;
-    g_bn_unroll = (u == 1 || u == 2 || u == 4) ? u : 2;
+    int u = e ? atoi(e) : 1;
+    g_bn_unroll = (u == 1 || u == 2 || u == 4) ? u : 1;
   }
   return g_bn_unroll;
 }

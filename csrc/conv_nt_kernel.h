@@ -59,7 +59,7 @@ constexpr int NT = 256;
 // d gelu_tanh(z) / dz
 __device__ __forceinline__ float gelu_grad(float z) {
   const float u = 0.7978845608f * (z + 0.044715f * z * z * z);
-  const float t = tanhf(u);
+  const float t = pdt_tanh(u);
   const float du = 0.7978845608f * (1.f + 3.f * 0.044715f * z * z);
   return 0.5f * (1.f + t) + 0.5f * z * (1.f - t * t) * du;
 }
@@ -692,7 +692,7 @@ __global__ void __launch_bounds__(NTH, PIPE ? 1 : 2) conv_nt_kernel(NTParams p) 
             x = fmaxf(x, 0.f);
           } else {
             float u = 0.7978845608f * (x + 0.044715f * x * x * x);
-            x = 0.5f * x * (1.f + tanhf(u));
+            x = 0.5f * x * (1.f + pdt_tanh(u));
           }
           acc[i][j][r] = x;
         }

@@ -25,6 +25,7 @@
 // to 4608) are otherwise bound by the staging traffic, not the matrix cores.
 #include "pdt_common.h"
 #include <stdlib.h>
+#include <type_traits>
 
 namespace {
 
@@ -89,7 +90,7 @@ __device__ __forceinline__ bf16x8 tr_frag(const char* base, int krow0, int col0,
 // of tile k+3 are issued right after tile k's barrier and land in LDS two
 // compute phases later (PF = 1: one), so a workgroup keeps ~2x the bytes in
 // flight -- the large weight gradients are load-latency bound otherwise.
-template <int BM, int BN, int NSTAGE, int NTH = NT, int WM = 2, int PF = 1>
+template <int BM, int BN, int NSTAGE, int NTH = NT, int WM = 2, int PF = 1, bool BIAS = false>
 __global__ void __launch_bounds__(NTH, NTH == NT ? 2 : 1) wgrad_kernel(WGParams p) {
   constexpr int WN = NTH / 64 / WM;    // waves along the (tap, c) columns
   constexpr int RBA = BM * 2;   // bytes per A row (co)
@@ -142,8 +143,10 @@ __global__ void __launch_bounds__(NTH, NTH == NT ? 2 : 1) wgrad_kernel(WGParams 
   u32x4 ra[NA], rb[NB];
   // bias-gradient partials: summed from the registers at LDS-store time (the
   // loads have landed by then -- consuming them at load time would wait out the
-  // prefetch); block-uniform predicate
-  const bool dobias = p.bslab != nullptr && tn == 0;
+  // prefetch). Only the tn == 0 blocks sum, and they run their OWN copy of the
+  // k-loop (compile-time DB below): a runtime branch inside the shared loop made
+  // every block 20-30 % slower (measured, ViT-B/16 weight gradients).
+  const bool dobias = BIAS && tn == 0;
   float bsum[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
 
   auto load_into = [&](int kt, u32x4 (&ra)[NA], u32x4 (&rb)[NB]) {
@@ -174,10 +177,10 @@ __global__ void __launch_bounds__(NTH, NTH == NT ? 2 : 1) wgrad_kernel(WGParams 
     }
   };
   auto load_tile = [&](int kt) { load_into(kt, ra, rb); };
-  auto store_from = [&](int buf, const u32x4 (&ra)[NA], const u32x4 (&rb)[NB]) {
+  auto store_from_db = [&](auto db, int buf, const u32x4 (&ra)[NA], const u32x4 (&rb)[NB]) {
     char* sa = smem + buf * STAGE;
     char* sb = sa + A_BYTES;
-    if (dobias) {
+    if constexpr (decltype(db)::value) {
 #pragma unroll
       for (int i = 0; i < NA; ++i)
 #pragma unroll
@@ -193,7 +196,6 @@ __global__ void __launch_bounds__(NTH, NTH == NT ? 2 : 1) wgrad_kernel(WGParams 
     for (int i = 0; i < NB; ++i)
       *reinterpret_cast<u32x4*>(sb + lds_off<RBB>(rB0 + BROWS * i, cB * 16)) = rb[i];
   };
-  auto store_tile = [&](int buf) { store_from(buf, ra, rb); };
 
   f32x4 acc[MI][NI];
 #pragma unroll
@@ -218,6 +220,9 @@ __global__ void __launch_bounds__(NTH, NTH == NT ? 2 : 1) wgrad_kernel(WGParams 
     }
   };
 
+  auto kloop = [&](auto db) {
+  auto store_from = [&](int buf, const u32x4 (&ra)[NA], const u32x4 (&rb)[NB]) { store_from_db(db, buf, ra, rb); };
+  auto store_tile = [&](int buf) { store_from(buf, ra, rb); };
   if constexpr (PF == 2) {
     static_assert(NSTAGE == 2, "deep prefetch uses the 2-stage LDS ring");
     // slot A = (ra, rb), slot B = (rb2 pair); loop unrolled by 2 so slots stay compile-time
@@ -280,8 +285,15 @@ __global__ void __launch_bounds__(NTH, NTH == NT ? 2 : 1) wgrad_kernel(WGParams 
     }
   }
   }
+  };
+  if constexpr (BIAS) {
+    if (dobias) kloop(std::integral_constant<bool, true>{});
+    else kloop(std::integral_constant<bool, false>{});
+  } else {
+    kloop(std::integral_constant<bool, false>{});
+  }
 
-  if (dobias) {
+  if (BIAS && dobias) {
     // lanes sharing a column chunk (tid % ACH) combine through LDS
     __syncthreads();  // every wave is done reading the operand stages
     float* red = reinterpret_cast<float*>(smem);  // [NTH][8]
@@ -370,6 +382,43 @@ static WGVar wg_variant(int v, int Mo, int No) {
 
 PDT_API int pdt_wgrad_num_variants() { return WG_NVAR; }
 
+template <bool BIAS>
+static void launch_wg(const WGVar& w, dim3 grid, const WGParams& p, hipStream_t stream) {
+  const int BM = w.BM, BN = w.BN, NS = w.NS;
+#define WG_LAUNCH(a, b, c) hipLaunchKernelGGL((wgrad_kernel<a, b, c, NT, 2, 1, BIAS>), grid, dim3(NT), 0, stream, p)
+#define WG_LAUNCH8(a, b, wm) hipLaunchKernelGGL((wgrad_kernel<a, b, 2, 512, wm, 1, BIAS>), grid, dim3(512), 0, stream, p)
+#define WG_LAUNCH_PF(a, b, t, wm) hipLaunchKernelGGL((wgrad_kernel<a, b, 2, t, wm, 2, BIAS>), grid, dim3(t), 0, stream, p)
+  if (NS == 3) {
+    if (w.NTH == 512) {
+      if (BM == 256 && BN == 256) WG_LAUNCH_PF(256, 256, 512, 2);
+      else if (BM == 256) WG_LAUNCH_PF(256, 128, 512, 4);
+      else WG_LAUNCH_PF(128, 256, 512, 2);
+    } else {
+      if (BM == 64 && BN == 64) WG_LAUNCH_PF(64, 64, 256, 2);
+      else if (BM == 64) WG_LAUNCH_PF(64, 128, 256, 2);
+      else if (BN == 64) WG_LAUNCH_PF(128, 64, 256, 2);
+      else WG_LAUNCH_PF(128, 128, 256, 2);
+    }
+  } else if (w.NTH == 512) {
+    if (BM == 256 && BN == 256) WG_LAUNCH8(256, 256, 2);
+    else if (BM == 256) WG_LAUNCH8(256, 128, 4);
+    else WG_LAUNCH8(128, 256, 2);
+  } else if (NS == 2) {
+    if (BM == 64 && BN == 64) WG_LAUNCH(64, 64, 2);
+    else if (BM == 64) WG_LAUNCH(64, 128, 2);
+    else if (BN == 64) WG_LAUNCH(128, 64, 2);
+    else WG_LAUNCH(128, 128, 2);
+  } else {
+    if (BM == 64 && BN == 64) WG_LAUNCH(64, 64, 1);
+    else if (BM == 64) WG_LAUNCH(64, 128, 1);
+    else if (BN == 64) WG_LAUNCH(128, 64, 1);
+    else WG_LAUNCH(128, 128, 1);
+  }
+#undef WG_LAUNCH
+#undef WG_LAUNCH8
+#undef WG_LAUNCH_PF
+}
+
 // Plan: number of splits so the grid covers the chip; returns splits and
 // writes ktiles_per_split.
 PDT_API int pdt_wgrad_plan(int M, int Mo, int No, int variant, int* ktiles_per_split) {
@@ -436,41 +485,10 @@ PDT_API int pdt_conv_wgrad(const void* dy, const void* x, float* slab, float* ou
   p.div_C = make_fastdiv(C);
   p.div_ntw = make_fastdiv(ntw);
   const WGVar w = wg_variant(variant, Mo, No);
-  const int BM = w.BM, BN = w.BN, NS = w.NS;
-  int tiles = ((Mo + BM - 1) / BM) * ((No + BN - 1) / BN);
+  int tiles = ((Mo + w.BM - 1) / w.BM) * ((No + w.BN - 1) / w.BN);
   dim3 grid(tiles * splits);
-#define WG_LAUNCH(a, b, c) hipLaunchKernelGGL((wgrad_kernel<a, b, c>), grid, dim3(NT), 0, stream, p)
-#define WG_LAUNCH8(a, b, wm) hipLaunchKernelGGL((wgrad_kernel<a, b, 2, 512, wm>), grid, dim3(512), 0, stream, p)
-#define WG_LAUNCH_PF(a, b, t, wm) hipLaunchKernelGGL((wgrad_kernel<a, b, 2, t, wm, 2>), grid, dim3(t), 0, stream, p)
-  if (NS == 3) {
-    if (w.NTH == 512) {
-      if (BM == 256 && BN == 256) WG_LAUNCH_PF(256, 256, 512, 2);
-      else if (BM == 256) WG_LAUNCH_PF(256, 128, 512, 4);
-      else WG_LAUNCH_PF(128, 256, 512, 2);
-    } else {
-      if (BM == 64 && BN == 64) WG_LAUNCH_PF(64, 64, 256, 2);
-      else if (BM == 64) WG_LAUNCH_PF(64, 128, 256, 2);
-      else if (BN == 64) WG_LAUNCH_PF(128, 64, 256, 2);
-      else WG_LAUNCH_PF(128, 128, 256, 2);
-    }
-  } else if (w.NTH == 512) {
-    if (BM == 256 && BN == 256) WG_LAUNCH8(256, 256, 2);
-    else if (BM == 256) WG_LAUNCH8(256, 128, 4);
-    else WG_LAUNCH8(128, 256, 2);
-  } else if (NS == 2) {
-    if (BM == 64 && BN == 64) WG_LAUNCH(64, 64, 2);
-    else if (BM == 64) WG_LAUNCH(64, 128, 2);
-    else if (BN == 64) WG_LAUNCH(128, 64, 2);
-    else WG_LAUNCH(128, 128, 2);
-  } else {
-    if (BM == 64 && BN == 64) WG_LAUNCH(64, 64, 1);
-    else if (BM == 64) WG_LAUNCH(64, 128, 1);
-    else if (BN == 64) WG_LAUNCH(128, 64, 1);
-    else WG_LAUNCH(128, 128, 1);
-  }
-#undef WG_LAUNCH
-#undef WG_LAUNCH8
-#undef WG_LAUNCH_PF
+  if (bias_out) launch_wg<true>(w, grid, p, stream);
+  else launch_wg<false>(w, grid, p, stream);
   int e = (int)hipGetLastError();
   if (e) return e;
   long n4 = (long)Mo * No / 4;

@@ -86,8 +86,12 @@ __global__ void __launch_bounds__(64 * WPB) ln_bwd_kernel(const u16* __restrict_
   const int r1 = min(rows, r0 + rows_per_block);
   for (int row = r0 + w; row < r1; row += WPB) {
     const float mean = mean_in[row], rstd = rstd_in[row];
-    float xh[CH][4], gy[CH][4];
+    float xh[CH][4], gy[CH][4], ad[CH][4];
     float s1 = 0.f, s2 = 0.f;
+    if (addend != nullptr) {  // issued with the row's other loads (latency overlapped)
+#pragma unroll
+      for (int c = 0; c < CH; ++c) ld4(addend + (long)row * D + (c * 64 + lane) * 4, ad[c]);
+    }
 #pragma unroll
     for (int c = 0; c < CH; ++c) {
       const int col = (c * 64 + lane) * 4;
@@ -112,10 +116,8 @@ __global__ void __launch_bounds__(64 * WPB) ln_bwd_kernel(const u16* __restrict_
 #pragma unroll
       for (int e = 0; e < 4; ++e) o[e] = rstd * (gy[c][e] - m1 - xh[c][e] * m2);
       if (addend != nullptr) {  // residual-branch gradient of the same tensor: dx += addend
-        float r[4];
-        ld4(addend + (long)row * D + (c * 64 + lane) * 4, r);
 #pragma unroll
-        for (int e = 0; e < 4; ++e) o[e] += r[e];
+        for (int e = 0; e < 4; ++e) o[e] += ad[c][e];
       }
       st4(dx + (long)row * D + (c * 64 + lane) * 4, o);
     }
@@ -178,7 +180,7 @@ __global__ void gelu_bwd_kernel(const u16* __restrict__ dy, const u16* __restric
       for (int e = 0; e < 2; ++e) {
         const float x = zv[e];
         const float u = 0.7978845608f * (x + 0.044715f * x * x * x);
-        const float t = tanhf(u);
+        const float t = pdt_tanh(u);
         const float du = 0.7978845608f * (1.f + 3.f * 0.044715f * x * x);
         r[e] = gv[e] * (0.5f * (1.f + t) + 0.5f * x * (1.f - t * t) * du);
       }

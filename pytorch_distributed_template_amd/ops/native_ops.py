@@ -365,13 +365,15 @@ def _check_nt(src, b, out, a):
     assert a["Nimg"] * a["Hs"] * a["Ws"] * Cs < 2 ** 31 and a["Nimg"] * a["Ho"] * a["Wo"] < 2 ** 31
 
 
-def select_nt_variant(src, b, out, *, with_stats=False, bias=None, act=0, aux=None, **a):
-    """Variant id for this geometry (tuning it on first use when allowed)."""
+def select_nt_variant(src, b, out, *, with_stats=False, bias=None, act=0, aux=None, addend=None, **a):
+    """Variant id for this geometry and epilogue (tuning it on first use when allowed)."""
     M = a["Nimg"] * a["Hm"] * a["Wm"]
     key = "nt5:" + ",".join(str(a[k]) for k in ("Hs", "Ws", "Cs", "Nimg", "Hm", "Wm", "Ncol", "K", "sh", "sw",
                                                  "nth", "ntw", "osh")) + f",{int(with_stats)},{int(bias is not None)}"
     if a.get("pix"):
         key += f",p{a['pix']}"
+    if act:  # epilogue work changes the best tile (and the streaming 1x1 kernels take no activation)
+        key += f",a{int(act)}"
     table = _tuned()
     if key in table:
         return int(table[key])
@@ -383,7 +385,9 @@ def select_nt_variant(src, b, out, *, with_stats=False, bias=None, act=0, aux=No
     # partial-stat rows depend on the variant's BM and waves-along-M: size for the largest
     rows = max(lib.pdt_conv_nt_stat_rows(M, a["Ncol"], a["K"], v) for v in range(nvar))
     stats = torch.empty(2 * rows * a["Ncol"], dtype=torch.float32, device=src.device) if with_stats else None
-    best = _time_variants(nvar, lambda v: lib.pdt_conv_nt(*_nt_args(src, b, out, stats, bias, a, act, v, aux=aux)),
+    tune_add = addend if act == 3 else None  # act 3 reads its operand through the addend pointer
+    best = _time_variants(nvar, lambda v: lib.pdt_conv_nt(*_nt_args(src, b, out, stats, bias, a, act, v, aux=aux,
+                                                                    addend=tune_add)),
                           _variant_filter())
     table[key] = best
     _save_tuned()
@@ -400,11 +404,12 @@ def conv_nt(src, b, out, *, stats=None, bias=None, relu=False, act=None, variant
     if addend is not None:
         assert addend.dtype == torch.bfloat16 and addend.numel() == out.numel() and addend.is_contiguous(
             memory_format=torch.channels_last if addend.dim() == 4 else torch.contiguous_format)
-    act_id = ACT[act] if act is not None else (1 if relu else 0)
+    act_id = (act if isinstance(act, int) else ACT[act]) if act is not None else (1 if relu else 0)
     if aux is not None:
         assert aux.dtype == torch.bfloat16 and aux.numel() == out.numel()
     if variant is None:
-        variant = select_nt_variant(src, b, out, with_stats=stats is not None, bias=bias, act=act_id, aux=aux, **a)
+        variant = select_nt_variant(src, b, out, with_stats=stats is not None, bias=bias, act=act_id, aux=aux,
+                                    addend=addend, **a)
     if addend_mask is not None:
         assert addend is not None and addend_mask.dtype == torch.uint8 and addend_mask.numel() * 8 == addend.numel()
         assert a["ldo"] == a["Ncol"]

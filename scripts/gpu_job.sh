@@ -8,7 +8,7 @@
 #
 # jobs:
 #   tests            pytest -m gpu (whole GPU suite)
-#   tests:EXPR       pytest -m gpu -k EXPR
+#   tests:EXPR       pytest -m gpu -k EXPR   (commas become spaces: tests:a,or,b)
 #   smoke            __graft_entry__.smoke()
 #   bench[:ARGS]     python bench.py ARGS   (ARGS: commas become spaces)
 #   ktrace[:ARGS]    rocprofv3 kernel trace of bench.py --steps 3 --warmup 3 ARGS,
@@ -24,7 +24,7 @@ for job in "$@"; do
   case $name in
     tests)
       if [ -n "$rest" ]; then
-        run ${TAG}_tests.txt 1100 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread -k "$rest"
+        run ${TAG}_tests_$(echo "$args" | tr -c 'a-zA-Z0-9_\n' '_' | cut -c1-40).txt 1100 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread -k "$args"
       else
         run ${TAG}_tests.txt 1100 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread
       fi ;;
