@@ -1,0 +1,265 @@
+// FP8 attention forward for ViT (head dim 64, T <= 256), the "CDNA4 fp8 MFMA
+// attention path" of BASELINE config #5.
+//
+//   S^T = K Q^T   on mfma_scale_f32_32x32x64_f8f6f4 (OCP e4m3 operands, K = 64 =
+//                 the head dim: ONE instruction per 32 keys x 32 queries, 2x the
+//                 bf16 MFMA rate); fp32 accumulate, unit block scales.
+//   softmax       fp32, online over 32-key tiles (running max / sum per query,
+//                 O rescaled when the max moves), exp2 with the scale folded in.
+//   O^T = V^T P^T on mfma_f32_32x32x16_bf16: P^T comes straight from the S^T
+//                 accumulator registers (query on the lane, keys in registers),
+//                 V^T through the hardware-transposing LDS read ds_read_b64_tr_b16.
+//
+// Quantization (no extra pass over HBM, no host sync): each workgroup owns one
+// (batch, head); it stages the head's K from the bf16 qkv buffer, reduces |K|max
+// over the head and quantizes K with a power-of-two scale into an fp8 LDS image
+// (16 KB instead of 32 KB of bf16). Each wave quantizes its 32-query Q tile the
+// same way (wave-wide |Q|max). Power-of-two scales make the dequantisation an
+// exact exponent shift, applied once to the fp32 scores.
+//
+// Output layout and the saved log-sum-exp follow csrc/attention.hip exactly, so
+// the bf16 recomputing backward consumes them unchanged (it recomputes P from the
+// bf16 Q and K: the fp8 forward's probabilities differ from it by the fp8 score
+// error only).
+#include "pdt_common.h"
+
+namespace {
+
+constexpr int D = 64;
+
+typedef int i32x8 __attribute__((ext_vector_type(8)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef __attribute__((address_space(3))) bf16x4 lds_bf16x4;
+
+// fp8 K image: [rows][64 B], 16-B chunk c of row r at chunk c ^ ((r >> 2) & 3):
+// a 16-lane ds_read_b128 group (16 consecutive rows, one chunk) hits 16 distinct slots
+__device__ __forceinline__ int k8_off(int row, int chunk) { return row * 64 + ((chunk ^ ((row >> 2) & 3)) << 4); }
+
+// bf16 V image for transposed reads (same swizzle as csrc/attention.hip): [rows][128 B]
+__device__ __forceinline__ int vt_off(int row, int byte_in_row) {
+  const int seg = byte_in_row >> 5;
+  const int sw = ((row >> 1) & 1) | ((row >> 2) & 2);
+  return row * 128 + ((seg ^ sw) << 5) + (byte_in_row & 31);
+}
+
+__device__ __forceinline__ uint32_t cvt4_e4m3(float a, float b, float c, float d) {
+  a = fminf(fmaxf(a, -448.f), 448.f);
+  b = fminf(fmaxf(b, -448.f), 448.f);
+  c = fminf(fmaxf(c, -448.f), 448.f);
+  d = fminf(fmaxf(d, -448.f), 448.f);
+  int r = __builtin_amdgcn_cvt_pk_fp8_f32(a, b, 0, false);
+  r = __builtin_amdgcn_cvt_pk_fp8_f32(c, d, r, true);
+  return (uint32_t)r;
+}
+
+// power-of-two quantization scale for |x|max = amax: largest 2^e with amax * 2^e <= 448
+__device__ __forceinline__ float pow2_scale(float amax) {
+  if (!(amax > 0.f)) return 1.f;
+  const int e = (int)floorf(__log2f(448.f / amax));
+  return ldexpf(1.f, max(min(e, 100), -100));
+}
+
+struct AttnF8Params {
+  const u16* qkv;   // [B, T, 3, H, 64] bf16
+  u16* out;         // [B, T, H*64]
+  float* lse;       // [B*H, T]
+  int B, T, H;
+  long ld, ldo;
+  float c;          // softmax scale * log2(e)
+};
+
+// NKT = number of 32-key tiles (ceil(T/32) <= 8)
+template <int NKT>
+__global__ void __launch_bounds__(256) attn_fwd_f8_kernel(AttnF8Params p) {
+  constexpr int ROWS = NKT * 32;
+  __shared__ __attribute__((aligned(16))) char Ks[ROWS * 64];     // fp8 K
+  __shared__ __attribute__((aligned(16))) char Vs[ROWS * 128];    // bf16 V (tr image)
+  __shared__ float red[4];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int bh = blockIdx.x, b = bh / p.H, h = bh % p.H;
+  const u16* base = p.qkv + (long)b * p.T * p.ld + h * D;
+  const u16* Kg = base + p.H * D;
+  const u16* Vg = base + 2 * p.H * D;
+
+  // ---- stage V (bf16, transposed-read image) and K (registers first: |K|max)
+  constexpr int CH = ROWS * 8;  // 16-B chunks of one [ROWS][64] bf16 matrix
+  constexpr int NIT = (CH + 255) / 256;
+  u32x4 kv[NIT];
+  float kmax = 0.f;
+#pragma unroll
+  for (int it = 0; it < NIT; ++it) {
+    const int q = tid + it * 256;
+    const int row = q >> 3, ch = q & 7;
+    u32x4 v = {0, 0, 0, 0}, k = {0, 0, 0, 0};
+    if (q < CH && row < p.T) {
+      v = *reinterpret_cast<const u32x4*>(Vg + (long)row * p.ld + ch * 8);
+      k = *reinterpret_cast<const u32x4*>(Kg + (long)row * p.ld + ch * 8);
+    }
+    if (q < CH) *reinterpret_cast<u32x4*>(Vs + vt_off(row, ch * 16)) = v;
+    kv[it] = k;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) kmax = fmaxf(kmax, fmaxf(fabsf(lo_bf(k[e])), fabsf(hi_bf(k[e]))));
+  }
+  kmax = warp_max(kmax);
+  if (lane == 0) red[wave] = kmax;
+  __syncthreads();
+  kmax = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
+  const float sk = pow2_scale(kmax);
+#pragma unroll
+  for (int it = 0; it < NIT; ++it) {
+    const int q = tid + it * 256;
+    if (q < CH) {
+      const int row = q >> 3, ch = q & 7;  // 8 bf16 -> 8 fp8 bytes: half of a 16-B fp8 chunk
+      const u32x4 k = kv[it];
+      uint2 w;
+      w.x = cvt4_e4m3(lo_bf(k[0]) * sk, hi_bf(k[0]) * sk, lo_bf(k[1]) * sk, hi_bf(k[1]) * sk);
+      w.y = cvt4_e4m3(lo_bf(k[2]) * sk, hi_bf(k[2]) * sk, lo_bf(k[3]) * sk, hi_bf(k[3]) * sk);
+      *reinterpret_cast<uint2*>(Ks + k8_off(row, ch >> 1) + (ch & 1) * 8) = w;
+    }
+  }
+  __syncthreads();
+
+  // lane roles in the 32x32 tiles: query / d column = lane & 31, half hh = lane >> 5
+  const int col = lane & 31, hh = lane >> 5;
+  const int grp = lane >> 4, i16 = lane & 15;  // 16-lane group of the transposed V reads
+  const int nqt = (p.T + 31) / 32;
+  for (int qt = wave; qt < nqt; qt += 4) {
+    // ---- Q tile -> e4m3 B fragment: lane (q = col, hh) holds Q[q][32 hh .. 32 hh + 31]
+    const int q = qt * 32 + col;
+    u32x4 qv[4];
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      qv[c] = u32x4{0, 0, 0, 0};
+      if (q < p.T) qv[c] = *reinterpret_cast<const u32x4*>(base + (long)q * p.ld + 32 * hh + 8 * c);
+    }
+    float qm = 0.f;
+#pragma unroll
+    for (int c = 0; c < 4; ++c)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) qm = fmaxf(qm, fmaxf(fabsf(lo_bf(qv[c][e])), fabsf(hi_bf(qv[c][e]))));
+    qm = warp_max(qm);
+    const float sq = pow2_scale(qm);
+    i32x8 qf;
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      qf[2 * c] = (int)cvt4_e4m3(lo_bf(qv[c][0]) * sq, hi_bf(qv[c][0]) * sq, lo_bf(qv[c][1]) * sq,
+                                 hi_bf(qv[c][1]) * sq);
+      qf[2 * c + 1] = (int)cvt4_e4m3(lo_bf(qv[c][2]) * sq, hi_bf(qv[c][2]) * sq, lo_bf(qv[c][3]) * sq,
+                                     hi_bf(qv[c][3]) * sq);
+    }
+    // scores in the log2 domain: c * S = (c / (sk sq)) * S_fp8
+    const float cs = p.c / (sk * sq);
+
+    float m = -INFINITY, l = 0.f;
+    f32x16 o[2];
+#pragma unroll
+    for (int dt = 0; dt < 2; ++dt)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) o[dt][r] = 0.f;
+
+    // not unrolled: a fully unrolled key loop hoists every tile's K fragment (214 VGPRs
+    // at 7 tiles, 2 waves/SIMD); rolled it stays near 100 (more workgroups per CU)
+#pragma unroll 1
+    for (int t = 0; t < NKT; ++t) {
+      // A fragment: K[key = 32t + col][d = 32 hh .. +31] (two swizzled 16-B chunks)
+      const int krow = 32 * t + col;
+      const u32x4 a0 = *reinterpret_cast<const u32x4*>(Ks + k8_off(krow, 2 * hh));
+      const u32x4 a1 = *reinterpret_cast<const u32x4*>(Ks + k8_off(krow, 2 * hh + 1));
+      const i32x8 kf = {(int)a0[0], (int)a0[1], (int)a0[2], (int)a0[3], (int)a1[0], (int)a1[1], (int)a1[2], (int)a1[3]};
+      f32x16 s = {};
+      s = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(kf, qf, s, 0, 0, 0, 127, 0, 127);
+      // s[r] = S[key = 32t + (r & 3) + 8 (r >> 2) + 4 hh][query q], raw (scaled) fp8 product
+      float mt = -INFINITY;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int key = 32 * t + (r & 3) + 8 * (r >> 2) + 4 * hh;
+        const float v = (t < NKT - 1 || key < p.T) ? s[r] * cs : -INFINITY;
+        s[r] = v;
+        mt = fmaxf(mt, v);
+      }
+      mt = fmaxf(mt, __shfl_xor(mt, 32, 64));  // the other 16 keys of this query
+      const float mn = fmaxf(m, mt);
+      const float alpha = exp2f(m - mn);  // m = -inf first: 0
+      float ls = 0.f;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const float e = __builtin_amdgcn_exp2f(s[r] - mn);
+        s[r] = e;
+        ls += e;
+      }
+      ls += __shfl_xor(ls, 32, 64);
+      l = l * alpha + ls;
+      m = mn;
+#pragma unroll
+      for (int dt = 0; dt < 2; ++dt) o[dt] *= alpha;
+      // O^T[d][q] += V^T[d][key] P^T[key][q], two 16-key steps. B = registers 8s..8s+7 of s
+      // (element j of half hh = key 16s + 8(j>>2) + 4hh + (j&3)); A = the same keys of V^T
+#pragma unroll
+      for (int st = 0; st < 2; ++st) {
+        bf16x8 pf;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) pf[j] = (__bf16)s[8 * st + j];
+        const int kb = 32 * t + 16 * st + 4 * (grp >> 1);  // this 16-lane group's 4 keys (j = 0..3)
+        const int rq = i16 >> 2, cp = i16 & 3;
+#pragma unroll
+        for (int dt = 0; dt < 2; ++dt) {
+          const int d0 = 32 * dt + 16 * (grp & 1);
+          const char* a_lo = Vs + vt_off(kb + rq, (d0 + 4 * cp) * 2);
+          const char* a_hi = Vs + vt_off(kb + 8 + rq, (d0 + 4 * cp) * 2);
+          const bf16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4bf16(
+              (lds_bf16x4*)((__attribute__((address_space(3))) char*)(uintptr_t)(uint32_t)(uintptr_t)a_lo));
+          const bf16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4bf16(
+              (lds_bf16x4*)((__attribute__((address_space(3))) char*)(uintptr_t)(uint32_t)(uintptr_t)a_hi));
+          const bf16x8 vf = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+          o[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf, pf, o[dt], 0, 0, 0);
+        }
+      }
+    }
+    // o[dt][r] = O^T[d = 32 dt + (r & 3) + 8 (r >> 2) + 4 hh][query q]
+    if (q < p.T) {
+      const float inv = 1.f / l;
+      u16* orow = p.out + ((long)b * p.T + q) * p.ldo + h * D;
+#pragma unroll
+      for (int dt = 0; dt < 2; ++dt)
+#pragma unroll
+        for (int g4 = 0; g4 < 4; ++g4) {
+          uint2 w;
+          w.x = pack2bf(o[dt][4 * g4] * inv, o[dt][4 * g4 + 1] * inv);
+          w.y = pack2bf(o[dt][4 * g4 + 2] * inv, o[dt][4 * g4 + 3] * inv);
+          *reinterpret_cast<uint2*>(orow + 32 * dt + 8 * g4 + 4 * hh) = w;
+        }
+      if (hh == 0) p.lse[(long)bh * p.T + q] = m + log2f(l);
+    }
+  }
+}
+
+}  // namespace
+
+// fp8 forward for T <= 256, head dim 64; -1 when the geometry is not covered
+PDT_API int pdt_attn_fwd_f8(const void* qkv, void* out, float* lse, int B, int T, int H, float scale,
+                            hipStream_t st) {
+  if (T < 1 || T > 256) return -1;
+  AttnF8Params p;
+  p.qkv = (const u16*)qkv;
+  p.out = (u16*)out;
+  p.lse = lse;
+  p.B = B; p.T = T; p.H = H;
+  p.ld = 3L * H * D;
+  p.ldo = (long)H * D;
+  p.c = scale * 1.4426950408889634f;
+  const int nkt = (T + 31) / 32;
+  dim3 g(B * H);
+#define F8(N) hipLaunchKernelGGL(attn_fwd_f8_kernel<N>, g, dim3(256), 0, st, p)
+  switch (nkt) {
+    case 1: F8(1); break;
+    case 2: F8(2); break;
+    case 3: F8(3); break;
+    case 4: F8(4); break;
+    case 5: F8(5); break;
+    case 6: F8(6); break;
+    case 7: F8(7); break;
+    default: F8(8); break;
+  }
+#undef F8
+  PDT_RETURN_LAUNCH();
+}

@@ -235,7 +235,14 @@ __global__ void __launch_bounds__(256) bn_bwd_finalize_kernel(const float* __res
 // -------------------------------------------------------------------- apply
 // MASK: also write the ReLU mask as one bit per element (byte i = chunk i's 8
 // channels): the backward then reads 1/16 of the bytes instead of `out`.
-template <bool RES, bool RELU, bool MASK = false, int U = 1>
+// NTS: nontemporal (streaming) stores of the element pass outputs
+template <typename T>
+__device__ __forceinline__ void st_pol(T* p, const T& v, bool nts) {
+  if (nts) __builtin_nontemporal_store(v, p);
+  else *p = v;
+}
+
+template <bool RES, bool RELU, bool MASK = false, int U = 1, bool NTS = false>
 __global__ void __launch_bounds__(NT) bn_apply_kernel(const u16* __restrict__ y, const u16* __restrict__ res,
                                                       u16* __restrict__ out, const float* __restrict__ scale,
                                                       const float* __restrict__ shift, long n8, int C,
@@ -264,7 +271,7 @@ __global__ void __launch_bounds__(NT) bn_apply_kernel(const u16* __restrict__ y,
       for (int k = 0; k < 8; ++k) f[k] = fmaxf(f[k], 0.f);
     }
     const u32x4 o = pack8(f);
-    reinterpret_cast<u32x4*>(out)[i] = o;
+    st_pol(reinterpret_cast<u32x4*>(out) + i, o, NTS);
     if (MASK) {
       uint32_t m = 0;
 #pragma unroll
@@ -410,7 +417,7 @@ __global__ void __launch_bounds__(NT) bn_bwd_reduce_kernel(const u16* __restrict
   }
 }
 
-template <bool RELU, bool USE_ACT, bool DRES, bool USE_MASK = false, bool POOL = false, int U = 1>
+template <bool RELU, bool USE_ACT, bool DRES, bool USE_MASK = false, bool POOL = false, int U = 1, bool NTS = false>
 __global__ void __launch_bounds__(NT) bn_bwd_apply_kernel(const u16* __restrict__ dA, const u16* __restrict__ y,
                                                           const u16* __restrict__ act,
                                                           const float* __restrict__ scale,
@@ -448,10 +455,10 @@ __global__ void __launch_bounds__(NT) bn_bwd_apply_kernel(const u16* __restrict_
         for (int k = 0; k < 8; ++k) g[k] = (yv[k] * sc[k] + sh[k]) > 0.f ? g[k] : 0.f;
       }
     }
-    if (DRES) reinterpret_cast<u32x4*>(dres)[i] = pack8(g);
+    if (DRES) st_pol(reinterpret_cast<u32x4*>(dres) + i, pack8(g), NTS);
 #pragma unroll
     for (int k = 0; k < 8; ++k) g[k] = a1[k] * g[k] + a2[k] * yv[k] + a3[k];
-    reinterpret_cast<u32x4*>(dy)[i] = pack8(g);
+    st_pol(reinterpret_cast<u32x4*>(dy) + i, pack8(g), NTS);
   };
   uint32_t i = blockIdx.x * NT + threadIdx.x;
   if constexpr (!POOL && U > 1) {
@@ -499,7 +506,7 @@ int bn_unroll() {
   if (g_bn_unroll < 0) {
     const char* e = getenv("PDT_BN_UNROLL");
     int u = e ? atoi(e) : 1;
-    g_bn_unroll = (u == 1 || u == 2 || u == 4) ? u : 1;
+    g_bn_unroll = (u == 1 || u == 2 || u == 4 || u == 11) ? u : 1;
   }
   return g_bn_unroll;
 }
@@ -520,8 +527,8 @@ int grid_for(long n8, int C) {
 
 }  // namespace
 
-PDT_API int pdt_bn_set_unroll(int u) {
-  if (u != 1 && u != 2 && u != 4) return -1;
+PDT_API int pdt_bn_set_unroll(int u) {  // 1 / 2 / 4: trip unroll; 11: unroll 1 + nontemporal stores
+  if (u != 1 && u != 2 && u != 4 && u != 11) return -1;
   g_bn_unroll = u;
   return 0;
 }
@@ -602,6 +609,7 @@ PDT_API int pdt_bn_apply(const void* y, const void* res, void* out, const float*
 #define APPLY(R_, U_, M_)                                                                                   \
   do {                                                                                                      \
     if (un == 4) hipLaunchKernelGGL((bn_apply_kernel<R_, U_, M_, 4>), g, b, 0, st, Y, R, O, scale, shift, n8, C, MK); \
+    else if (un == 11) hipLaunchKernelGGL((bn_apply_kernel<R_, U_, M_, 1, true>), g, b, 0, st, Y, R, O, scale, shift, n8, C, MK); \
     else if (un == 2) hipLaunchKernelGGL((bn_apply_kernel<R_, U_, M_, 2>), g, b, 0, st, Y, R, O, scale, shift, n8, C, MK); \
     else hipLaunchKernelGGL((bn_apply_kernel<R_, U_, M_, 1>), g, b, 0, st, Y, R, O, scale, shift, n8, C, MK); \
   } while (0)
@@ -658,6 +666,9 @@ PDT_API int pdt_bn_bwd_apply(const void* dA, const void* y, const void* act, con
     if (un == 4)                                                                                                     \
       hipLaunchKernelGGL((bn_bwd_apply_kernel<R_, U_, D_, M_, false, 4>), g, b, 0, st, G, Y, A, scale, shift, k1, k2, \
                          k3, DY, DR, n8, C, MK, PoolSrc{});                                                          \
+    else if (un == 11)                                                                                               \
+      hipLaunchKernelGGL((bn_bwd_apply_kernel<R_, U_, D_, M_, false, 1, true>), g, b, 0, st, G, Y, A, scale, shift, k1, \
+                         k2, k3, DY, DR, n8, C, MK, PoolSrc{});                                                      \
     else if (un == 2)                                                                                                \
       hipLaunchKernelGGL((bn_bwd_apply_kernel<R_, U_, D_, M_, false, 2>), g, b, 0, st, G, Y, A, scale, shift, k1, k2, \
                          k3, DY, DR, n8, C, MK, PoolSrc{});                                                          \

@@ -573,7 +573,7 @@ __global__ void __launch_bounds__(NTH, PIPE ? 1 : 2) conv_nt_kernel(NTParams p) 
   constexpr int CPR = BN / 8;  // 16-B chunks per row
   // DIRECT: each lane stores its 4 consecutive channels (8 B) straight to HBM
   // (no LDS round trip / barrier); L2 merges the 32-B row pieces into lines.
-  auto direct_store = [&](u16* dst, const u16* addend) {
+  auto direct_store = [&](u16* dst, const u16* addend) __attribute__((always_inline)) {
 #pragma unroll
     for (int i = 0; i < MI; ++i) {
       int m = m0 + wm * (BM / WM) + i * 16 + lrow;
@@ -618,7 +618,7 @@ __global__ void __launch_bounds__(NTH, PIPE ? 1 : 2) conv_nt_kernel(NTParams p) 
     }
   };
 
-  auto stage_store = [&](u16* dst, const u16* addend) {
+  auto stage_store = [&](u16* dst, const u16* addend) __attribute__((always_inline)) {
     if (DIRECT) {
       direct_store(dst, addend);
       return;

@@ -141,13 +141,15 @@ __global__ void __launch_bounds__(NTH, NTH == NT ? 2 : 1) wgrad_kernel(WGParams 
   const int offh = p.oh0 + p.dh * th, offw = p.ow0 + p.dw * tw;
 
   u32x4 ra[NA], rb[NB];
-  // bias-gradient partials: summed from the registers at LDS-store time (the
-  // loads have landed by then -- consuming them at load time would wait out the
-  // prefetch). Only the tn == 0 blocks sum, and they run their OWN copy of the
-  // k-loop (compile-time DB below): a runtime branch inside the shared loop made
-  // every block 20-30 % slower (measured, ViT-B/16 weight gradients).
-  const bool dobias = BIAS && tn == 0;
-  float bsum[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  // bias gradient on the matrix cores: the tn == 0 blocks also multiply their
+  // dY fragments by a fragment of ones (the wn == 0 waves' sums are written) (D[tc][co] = sum_m dY[m][co]
+  // in every tc lane), MI extra MFMAs per 16*NI; they run their OWN copy of the
+  // k-loop (compile-time DB below) so the other blocks' loop is the plain one.
+  // (Summing the staged registers on the VALU instead cost every block 20-30 %.)
+  const bool dobias = BIAS && tn == 0;  // block-uniform (the loop copies hold barriers)
+  f32x4 bacc[BIAS ? MI : 1];
+#pragma unroll
+  for (int i = 0; i < (BIAS ? MI : 1); ++i) bacc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   auto load_into = [&](int kt, u32x4 (&ra)[NA], u32x4 (&rb)[NB]) {
     const int k0 = kt * BK;
@@ -177,18 +179,9 @@ __global__ void __launch_bounds__(NTH, NTH == NT ? 2 : 1) wgrad_kernel(WGParams 
     }
   };
   auto load_tile = [&](int kt) { load_into(kt, ra, rb); };
-  auto store_from_db = [&](auto db, int buf, const u32x4 (&ra)[NA], const u32x4 (&rb)[NB]) {
+  auto store_from_db = [&](auto, int buf, const u32x4 (&ra)[NA], const u32x4 (&rb)[NB]) {
     char* sa = smem + buf * STAGE;
     char* sb = sa + A_BYTES;
-    if constexpr (decltype(db)::value) {
-#pragma unroll
-      for (int i = 0; i < NA; ++i)
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          bsum[2 * e] += lo_bf(ra[i][e]);
-          bsum[2 * e + 1] += hi_bf(ra[i][e]);
-        }
-    }
 #pragma unroll
     for (int i = 0; i < NA; ++i)
       *reinterpret_cast<u32x4*>(sa + lds_off<RBA>(rA0 + AROWS * i, cA * 16)) = ra[i];
@@ -203,7 +196,7 @@ __global__ void __launch_bounds__(NTH, NTH == NT ? 2 : 1) wgrad_kernel(WGParams 
 #pragma unroll
     for (int j = 0; j < NI; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  auto compute = [&](const char* sa) {
+  auto compute = [&](auto, const char* sa) {
     const char* sb = sa + A_BYTES;
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk) {
@@ -237,13 +230,13 @@ __global__ void __launch_bounds__(NTH, NTH == NT ? 2 : 1) wgrad_kernel(WGParams 
     __syncthreads();
     for (int i = 0; i < n; i += 2) {
       // tile i in LDS stage 0, tile i+1 in slot B, tile i+2 in flight to slot A
-      compute(smem);
+      compute(db, smem);
       if (i + 1 < n) store_from(1, ra2, rb2);
       __syncthreads();
       if (i + 3 < n) load_into(kt_begin + i + 3, ra2, rb2);
       if (i + 1 >= n) break;
       // tile i+1 in LDS stage 1, tile i+2 in slot A, tile i+3 in flight to slot B
-      compute(smem + STAGE);
+      compute(db, smem + STAGE);
       if (i + 2 < n) store_from(0, ra, rb);
       __syncthreads();
       if (i + 4 < n) load_into(kt_begin + i + 4, ra, rb);
@@ -257,24 +250,9 @@ __global__ void __launch_bounds__(NTH, NTH == NT ? 2 : 1) wgrad_kernel(WGParams 
   for (int kt = kt_begin; kt < kt_end; ++kt) {
     const int cur = NSTAGE == 2 ? ((kt - kt_begin) & 1) : 0;
     if (kt + 1 < kt_end) load_tile(kt + 1);
-    const char* sa = smem + cur * STAGE;
-    const char* sb = sa + A_BYTES;
-#pragma unroll
-    for (int kk = 0; kk < 2; ++kk) {
-      // B fragments for the whole k-step, A fragments one 16-row tile at a time
-      // (the 128x64-per-wave tile would otherwise hold 12 fragments at once)
-      bf16x8 bfr[NI];
-#pragma unroll
-      for (int j = 0; j < NI; ++j) bfr[j] = tr_frag<RBB>(sb, kk * 32, wn * (BN / WN) + j * 16, lane);
-#pragma unroll
-      for (int i = 0; i < MI; ++i) {
-        const bf16x8 af = tr_frag<RBA>(sa, kk * 32, wm * (BM / WM) + i * 16, lane);
-#pragma unroll
-        for (int j = 0; j < NI; ++j)
-          // D[tc][co]: lane holds 4 consecutive tc of one co
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[j], af, acc[i][j], 0, 0, 0);
-      }
-    }
+    // B fragments for the whole k-step, A fragments one 16-row tile at a time
+    // (the 128x64-per-wave tile would otherwise hold 12 fragments at once)
+    compute(db, smem + cur * STAGE);
     if (NSTAGE == 2) {
       if (kt + 1 < kt_end) store_tile(cur ^ 1);
       __syncthreads();
@@ -286,28 +264,53 @@ __global__ void __launch_bounds__(NTH, NTH == NT ? 2 : 1) wgrad_kernel(WGParams 
   }
   }
   };
-  if constexpr (BIAS) {
-    if (dobias) kloop(std::integral_constant<bool, true>{});
-    else kloop(std::integral_constant<bool, false>{});
-  } else {
-    kloop(std::integral_constant<bool, false>{});
-  }
+  kloop(std::integral_constant<bool, false>{});
 
-  if (BIAS && dobias) {
-    // lanes sharing a column chunk (tid % ACH) combine through LDS
-    __syncthreads();  // every wave is done reading the operand stages
-    float* red = reinterpret_cast<float*>(smem);  // [NTH][8]
+  if constexpr (BIAS) {
+    if (dobias) {
+      // column sums of dY[k-range of this split][co0, co0 + BM): thread = (16-B chunk, row phase)
+      constexpr int CPR = BM / 8, RPP = NTH / CPR;
+      const int cc = tid % CPR, rr = tid / CPR;
+      const int co = co0 + cc * 8;
+      float bs[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+      if (co < p.Mo) {
+        const int m1 = min(p.M, kt_end * BK);
+        int m = kt_begin * BK + rr;
+        for (; m + 3 * RPP < m1; m += 4 * RPP) {  // 4 rows in flight
+          u32x4 v[4];
 #pragma unroll
-    for (int k = 0; k < 8; ++k) red[tid * 8 + k] = bsum[k];
-    __syncthreads();
-    if (tid < ACH && co0 + tid * 8 < p.Mo) {
-      float t8[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-      for (int j = 0; j < AROWS; ++j)
+          for (int u = 0; u < 4; ++u) v[u] = *reinterpret_cast<const u32x4*>(p.dy + (size_t)(m + u * RPP) * p.ldy + co);
 #pragma unroll
-        for (int k = 0; k < 8; ++k) t8[k] += red[(j * ACH + tid) * 8 + k];
-      float* bo = p.bslab + (size_t)split * p.Mo + co0 + tid * 8;
-      *reinterpret_cast<f32x4*>(bo) = f32x4{t8[0], t8[1], t8[2], t8[3]};
-      *reinterpret_cast<f32x4*>(bo + 4) = f32x4{t8[4], t8[5], t8[6], t8[7]};
+          for (int u = 0; u < 4; ++u)
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              bs[2 * e] += lo_bf(v[u][e]);
+              bs[2 * e + 1] += hi_bf(v[u][e]);
+            }
+        }
+        for (; m < m1; m += RPP) {
+          const u32x4 v = *reinterpret_cast<const u32x4*>(p.dy + (size_t)m * p.ldy + co);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            bs[2 * e] += lo_bf(v[e]);
+            bs[2 * e + 1] += hi_bf(v[e]);
+          }
+        }
+      }
+      __syncthreads();  // operand stages are free
+      float* red = reinterpret_cast<float*>(smem);  // [NTH][8]
+#pragma unroll
+      for (int k = 0; k < 8; ++k) red[tid * 8 + k] = bs[k];
+      __syncthreads();
+      if (tid < CPR && co < p.Mo) {
+        float t8[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+        for (int j = 0; j < RPP; ++j)
+#pragma unroll
+          for (int k = 0; k < 8; ++k) t8[k] += red[(j * CPR + tid) * 8 + k];
+        float* bo = p.bslab + (size_t)split * p.Mo + co;
+        *reinterpret_cast<f32x4*>(bo) = f32x4{t8[0], t8[1], t8[2], t8[3]};
+        *reinterpret_cast<f32x4*>(bo + 4) = f32x4{t8[4], t8[5], t8[6], t8[7]};
+      }
     }
   }
 

@@ -21,6 +21,12 @@ from ..base.base_model import BaseModel
 from ..ops import fused
 
 
+def _fp8_attn() -> bool:
+    """fp8 score GEMM in attention for fp8 models (PDT_FP8_ATTN=0 keeps it bf16)."""
+    import os
+    return os.environ.get("PDT_FP8_ATTN", "1") == "1"
+
+
 class Attention(nn.Module):
     def __init__(self, dim, num_heads):
         super().__init__()
@@ -31,7 +37,7 @@ class Attention(nn.Module):
 
     def forward(self, x, fp8=False, residual=None):
         qkv = fused.linear(x, self.qkv, fp8=fp8)                          # [B,T,3D]
-        o = fused.qkv_attention(qkv, self.num_heads)                       # [B,T,D]
+        o = fused.qkv_attention(qkv, self.num_heads, fp8=fp8 and _fp8_attn())  # [B,T,D]
         return fused.linear(o, self.proj, fp8=fp8, residual=residual)     # (+ residual in the epilogue)
 
 

@@ -73,6 +73,7 @@ _SIGS = {
     "pdt_wt_dgrad_multi": (c_int, [P, c_int, c_long, P]),
     "pdt_add_bf16": (c_int, [P, P, P, c_long, P]),
     "pdt_attn_fwd": (c_int, [P, P, P, c_int, c_int, c_int, c_float, P]),
+    "pdt_attn_fwd_f8": (c_int, [P, P, P, c_int, c_int, c_int, c_float, P]),
     "pdt_gemm_f8_num_variants": (c_int, []),
     "pdt_gemm_f8": (c_int, [P, P, P, P, P, P] + [c_int] * 8 + [P, P, c_int, P]),
     "pdt_bn_set_unroll": (c_int, [c_int]),
@@ -1458,7 +1459,7 @@ def fp8_settings() -> dict:
     dtype label, so the label cannot drift from the code's defaults)."""
     return {"scaling": os.environ.get("PDT_FP8_SCALING", "delayed"),
             "dgrad": os.environ.get("PDT_FP8_DGRAD", "0") == "1",
-            "attn": os.environ.get("PDT_FP8_ATTN", "0") == "1"}
+            "attn": os.environ.get("PDT_FP8_ATTN", "1") == "1"}
 
 
 def quantize_fp8(x: torch.Tensor, fmt: int = E4M3):
@@ -1835,14 +1836,17 @@ class _QKVAttention(torch.autograd.Function):
     backward, which writes d(qkv) in the qkv layout (the qkv GEMM's dY)."""
 
     @staticmethod
-    def forward(ctx, qkv, H):
+    def forward(ctx, qkv, H, fp8=False):
         B, T, D3 = qkv.shape
         assert D3 == 3 * H * 64 and qkv.dtype == torch.bfloat16, "head_dim must be 64, bf16"
         qkv = qkv.contiguous()
         out = torch.empty((B, T, H * 64), dtype=torch.bfloat16, device=qkv.device)
         lse = torch.empty((B * H, T), dtype=torch.float32, device=qkv.device)
         scale = 64 ** -0.5
-        _chk(_load().pdt_attn_fwd(_p(qkv), _p(out), _p(lse), B, T, H, scale, _s()), "attn_fwd")
+        if fp8 and T <= 256:  # fp8 QK^T (csrc/attention_f8.hip), fp32 softmax, bf16 PV
+            _chk(_load().pdt_attn_fwd_f8(_p(qkv), _p(out), _p(lse), B, T, H, scale, _s()), "attn_fwd_f8")
+        else:
+            _chk(_load().pdt_attn_fwd(_p(qkv), _p(out), _p(lse), B, T, H, scale, _s()), "attn_fwd")
         ctx.save_for_backward(qkv, out, lse)
         ctx.H, ctx.scale = H, scale
         return out
@@ -1856,12 +1860,14 @@ class _QKVAttention(torch.autograd.Function):
         dqkv = torch.empty_like(qkv)
         _chk(_load().pdt_attn_bwd(_p(qkv), _p(out), _p(dout), _p(lse), _p(delta), _p(dqkv), B, T, ctx.H,
                                   ctx.scale, _s()), "attn_bwd")
-        return dqkv, None
+        return dqkv, None, None
 
 
-def qkv_attention(qkv, num_heads):
-    """softmax(q k^T / 8) v over heads of 64 for a packed [B, T, 3*H*64] qkv."""
-    return _QKVAttention.apply(qkv, num_heads)
+def qkv_attention(qkv, num_heads, fp8=False):
+    """softmax(q k^T / 8) v over heads of 64 for a packed [B, T, 3*H*64] qkv. ``fp8``: the
+    score GEMM on e4m3 MFMA (per-head / per-tile power-of-two scales, T <= 256); the
+    backward is the bf16 recomputing one either way."""
+    return _QKVAttention.apply(qkv, num_heads, bool(fp8))
 
 
 def attention(q, k, v):

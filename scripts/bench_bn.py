@@ -49,10 +49,12 @@ def bwd_apply():
 passes = {"bn_apply res+relu+mask": (apply, n * 2 * 3 + n // 8),
           "bn_bwd_apply mask": (bwd_apply, n * 2 * 3 + n // 8)}
 ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-times = {(k, u): [] for k in passes for u in (1, 2, 4)}
+MODES = (1, 11, 2)  # 1 / 2: trip unroll; 11: unroll 1 + nontemporal stores
+times = {(k, u): [] for k in passes for u in MODES}
 for r in range(a.rounds):
-    for u in (1, 2, 4):
-        lib.pdt_bn_set_unroll(u)
+    for u in MODES:
+        assert lib.pdt_bn_set_unroll(u) == 0
+
         for k, (fn, _) in passes.items():
             fn()
             ev0.record()
@@ -63,7 +65,7 @@ for r in range(a.rounds):
             times[(k, u)].append(ev0.elapsed_time(ev1) / 5)
 print(f"M={M} C={C} ({n * 2 / 2**30:.2f} GiB per bf16 tensor)")
 for k, (_, nbytes) in passes.items():
-    for u in (1, 2, 4):
+    for u in MODES:
         t = times[(k, u)]
         med = statistics.median(t)
-        print(f"{k:26s} U={u}: median {med * 1e3:8.1f} us  min {min(t) * 1e3:8.1f} us  {nbytes / med / 1e9:6.2f} TB/s")
+        print(f"{k:26s} mode={u:2d}: median {med * 1e3:8.1f} us  min {min(t) * 1e3:8.1f} us  {nbytes / med / 1e9:6.2f} TB/s")

@@ -9,6 +9,7 @@
 # jobs:
 #   tests            pytest -m gpu (whole GPU suite)
 #   tests:EXPR       pytest -m gpu -k EXPR   (commas become spaces: tests:a,or,b)
+#   testss:EXPR      the same with -s and a 600 s per-test limit (long numerics tests)
 #   smoke            __graft_entry__.smoke()
 #   bench[:ARGS]     python bench.py ARGS   (ARGS: commas become spaces)
 #   ktrace[:ARGS]    rocprofv3 kernel trace of bench.py --steps 3 --warmup 3 ARGS,
@@ -28,6 +29,8 @@ for job in "$@"; do
       else
         run ${TAG}_tests.txt 1100 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread
       fi ;;
+    testss)  # like tests:EXPR but with -s (prints stream into the log: long tests show progress)
+      PDT_SLOW_TESTS=1 run ${TAG}_testss_$(echo "$args" | tr -c 'a-zA-Z0-9_\n' '_' | cut -c1-40).txt 1100 python -u -m pytest tests -m gpu -x -v -s --timeout 600 --timeout-method thread -k "$args" ;;
     smoke) run ${TAG}_smoke.txt 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) run ${TAG}_bench_$(echo "$args" | tr -c 'a-zA-Z0-9_\n' '_').txt 400 python bench.py $args ;;
     ktrace)

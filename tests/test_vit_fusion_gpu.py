@@ -158,3 +158,32 @@ def test_vit_native_matches_torch_fp32():
     assert nrmerr(out["native"][0], out["torch"][0]) < 3e-2
     worst = max((nrmerr(out["native"][1][n], out["torch"][1][n]), n) for n in out["torch"][1])
     assert worst[0] < 8e-2, worst
+
+
+@pytest.mark.parametrize("B,T,H", [(3, 197, 4), (2, 64, 2), (1, 50, 12), (2, 256, 3), (2, 16, 3), (1, 120, 2)])
+def test_fp8_attention_forward_and_bf16_backward(B, T, H):
+    """fp8 score GEMM (csrc/attention_f8.hip) vs an fp32 softmax reference; the bf16
+    recomputing backward run on the fp8 forward's output and log-sum-exp."""
+    torch.manual_seed(B * 100 + T)
+    qkv = (torch.randn(B, T, 3 * H * 64, device="cuda") * 1.5).to(torch.bfloat16)
+    dout = torch.randn(B, T, H * 64, device="cuda").to(torch.bfloat16)
+    x = qkv.float().requires_grad_(True)
+    q, k, v = x.view(B, T, 3, H, 64).permute(2, 0, 3, 1, 4)
+    s = q @ k.transpose(-1, -2) / 8.0
+    ref = (torch.softmax(s, dim=-1) @ v).transpose(1, 2).reshape(B, T, H * 64)
+    ref.backward(dout.float())
+    lse_ref = torch.logsumexp(s.detach(), dim=-1) / 0.6931471805599453  # log2 domain
+    xn = qkv.clone().requires_grad_(True)
+    out = no.qkv_attention(xn, H, fp8=True)
+    # the saved log-sum-exp (log2 domain of the scaled scores) matches to fp8 score accuracy
+    lse = out.grad_fn.saved_tensors[2]
+    assert (lse.view(B, H, T) - lse_ref.view(B, H, T)).abs().max().item() < 0.25
+    out.backward(dout)
+    torch.cuda.synchronize()
+    assert out.shape == ref.shape and out.dtype == torch.bfloat16
+    e = nrmerr(out, ref)
+    assert e < 4e-2, e
+    g, gr = xn.grad.view(B, T, 3, H * 64), x.grad.view(B, T, 3, H * 64)
+    for i, name in enumerate("qkv"):
+        ei = nrmerr(g[:, :, i], gr[:, :, i])
+        assert ei < 8e-2, (name, ei)
