@@ -160,10 +160,30 @@ def test_vit_native_matches_torch_fp32():
     assert worst[0] < 8e-2, worst
 
 
+def _pow2_scale(amax):
+    e = torch.floor(torch.log2(448.0 / amax.clamp_min(1e-30)))
+    return torch.where(amax > 0, torch.exp2(e.clamp(-100, 100)), torch.ones_like(amax))
+
+
+def _fp8_emulated_scores(q, k):
+    """S = Q K^T with Q, K quantized exactly as csrc/attention_f8.hip does: K per (b, h)
+    and Q per (b, h, 32-query tile) with power-of-two scales, e4m3 round-to-nearest."""
+    B, H, T, _ = q.shape
+    sk = _pow2_scale(k.abs().amax(dim=(2, 3), keepdim=True))
+    kq = (k * sk).to(torch.float8_e4m3fn).float() / sk
+    nqt = (T + 31) // 32
+    qp = torch.nn.functional.pad(q, (0, 0, 0, nqt * 32 - T)).view(B, H, nqt, 32, 64)
+    sq = _pow2_scale(qp.abs().amax(dim=(3, 4), keepdim=True))
+    qq = ((qp * sq).to(torch.float8_e4m3fn).float() / sq).view(B, H, nqt * 32, 64)[:, :, :T]
+    return qq @ kq.transpose(-1, -2)
+
+
 @pytest.mark.parametrize("B,T,H", [(3, 197, 4), (2, 64, 2), (1, 50, 12), (2, 256, 3), (2, 16, 3), (1, 120, 2)])
 def test_fp8_attention_forward_and_bf16_backward(B, T, H):
-    """fp8 score GEMM (csrc/attention_f8.hip) vs an fp32 softmax reference; the bf16
-    recomputing backward run on the fp8 forward's output and log-sum-exp."""
+    """fp8 score GEMM (csrc/attention_f8.hip): (1) against a reference that applies the
+    kernel's own quantization (per-head K / per-32-query-tile Q power-of-two scales, e4m3)
+    in fp32 -- checks the kernel itself tightly; (2) against exact fp32 attention -- the
+    fp8 error budget, with the bf16 recomputing backward run on its output and LSE."""
     torch.manual_seed(B * 100 + T)
     qkv = (torch.randn(B, T, 3 * H * 64, device="cuda") * 1.5).to(torch.bfloat16)
     dout = torch.randn(B, T, H * 64, device="cuda").to(torch.bfloat16)
@@ -172,18 +192,22 @@ def test_fp8_attention_forward_and_bf16_backward(B, T, H):
     s = q @ k.transpose(-1, -2) / 8.0
     ref = (torch.softmax(s, dim=-1) @ v).transpose(1, 2).reshape(B, T, H * 64)
     ref.backward(dout.float())
-    lse_ref = torch.logsumexp(s.detach(), dim=-1) / 0.6931471805599453  # log2 domain
+    with torch.no_grad():
+        s8 = _fp8_emulated_scores(q.detach(), k.detach()) / 8.0
+        ref8 = (torch.softmax(s8, dim=-1) @ v.detach()).transpose(1, 2).reshape(B, T, H * 64)
+        lse8 = torch.logsumexp(s8, dim=-1) / 0.6931471805599453  # log2 domain
     xn = qkv.clone().requires_grad_(True)
     out = no.qkv_attention(xn, H, fp8=True)
-    # the saved log-sum-exp (log2 domain of the scaled scores) matches to fp8 score accuracy
-    lse = out.grad_fn.saved_tensors[2]
-    assert (lse.view(B, H, T) - lse_ref.view(B, H, T)).abs().max().item() < 0.25
+    lse = out.grad_fn.saved_tensors[2].view(B, H, T)
+    e8 = nrmerr(out, ref8)
+    dl = (lse - lse8).abs().max().item()
+    assert e8 < 1e-2 and dl < 5e-2, (e8, dl)  # the kernel == its quantization model
     out.backward(dout)
     torch.cuda.synchronize()
     assert out.shape == ref.shape and out.dtype == torch.bfloat16
     e = nrmerr(out, ref)
-    assert e < 4e-2, e
+    assert e < 6e-2, e  # fp8 score error budget vs exact attention
     g, gr = xn.grad.view(B, T, 3, H * 64), x.grad.view(B, T, 3, H * 64)
     for i, name in enumerate("qkv"):
         ei = nrmerr(g[:, :, i], gr[:, :, i])
-        assert ei < 8e-2, (name, ei)
+        assert ei < 1e-1, (name, ei)
