@@ -454,6 +454,16 @@ __device__ __forceinline__ int tr_lane_off(int lane, int dt) {
   const int sw = ((q >> 1) & 1) | (((g >> 1) & 1) << 1);  // seg_swz(32x + 16h + 4g + q)
   return (4 * g + q) * 128 + ((dt ^ sw) << 5) + 8 * pp;
 }
+// The same transposed-read fragment taken from a ROW image (row_off swizzle) instead of
+// a separate transposed image: the backward kernels then stage each matrix once
+// (half the LDS -> two workgroups per CU). Byte column 32dt + 8pp of row 4g + q sits in
+// 16-B chunk 2dt + (pp >> 1), swizzled by ((row >> 1) & 7) -- bits of (g, q) only, and
+// unchanged by the +16 / +32x row offsets frag_tr adds.
+__device__ __forceinline__ int tr_row_lane_off(int lane, int dt) {
+  const int g = lane >> 4, q = (lane >> 2) & 3, pp = lane & 3;
+  const int row = 4 * g + q;
+  return row * 128 + (((2 * dt + (pp >> 1)) ^ ((row >> 1) & 7)) << 4) + 8 * (pp & 1);
+}
 __device__ __forceinline__ bf16x8 frag_row(const char* img, int off, int t) {
   return *reinterpret_cast<const bf16x8*>(img + off + t * 2048);
 }
@@ -585,16 +595,19 @@ struct AttnSeqBwdParams {
 // dK, dV: one workgroup (8 waves) per (b, h); wave w owns key subtiles w, w+8.
 // Per query subtile u: S = Q K^T (q on the register axis, key on the lane),
 // P = exp2(c S - lse), dS = P (dP - delta); dV^T += dO^T P, dK^T += Q^T dS.
-template <int NT>
+// SINGLE: Q and dO staged once (row images serve the transposed reads too): 2 images
+// instead of 4 -> 2 workgroups per CU
+template <int NT, bool SINGLE>
 __global__ void __launch_bounds__(512) attn_bwd_dkdv_seq_kernel(AttnSeqBwdParams p) {
   constexpr int NE = (NT + 1) & ~1;
   constexpr int IMG = NE * 16 * 128;
-  __shared__ __attribute__((aligned(16))) char smem[4 * IMG + 2 * NE * 16 * 4];
+  constexpr int NIMG = SINGLE ? 2 : 4;
+  __shared__ __attribute__((aligned(16))) char smem[NIMG * IMG + 2 * NE * 16 * 4];
   char* Qr = smem;
-  char* Qt = smem + IMG;
-  char* dOr = smem + 2 * IMG;
-  char* dOt = smem + 3 * IMG;
-  float* lse_s = reinterpret_cast<float*>(smem + 4 * IMG);  // pre-negated: -lse
+  char* dOr = smem + IMG;
+  char* Qt = SINGLE ? Qr : smem + 2 * IMG;
+  char* dOt = SINGLE ? dOr : smem + 3 * IMG;
+  float* lse_s = reinterpret_cast<float*>(smem + NIMG * IMG);  // pre-negated: -lse
   float* dl_s = lse_s + NE * 16;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, g = lane >> 4;
   const int bh = blockIdx.x, b = bh / p.H, h = bh % p.H;
@@ -602,9 +615,11 @@ __global__ void __launch_bounds__(512) attn_bwd_dkdv_seq_kernel(AttnSeqBwdParams
   const u16* dOg = p.dout + (long)b * p.T * p.ldo + h * D;
   const u16* Og = p.out + (long)b * p.T * p.ldo + h * D;
   stage_seq<false, NE, 512>(Qr, base, p.ld, p.T, tid);
-  stage_seq<true, NE, 512>(Qt, base, p.ld, p.T, tid);
   stage_seq<false, NE, 512>(dOr, dOg, p.ldo, p.T, tid);
-  stage_seq<true, NE, 512>(dOt, dOg, p.ldo, p.T, tid);
+  if (!SINGLE) {
+    stage_seq<true, NE, 512>(Qt, base, p.ld, p.T, tid);
+    stage_seq<true, NE, 512>(dOt, dOg, p.ldo, p.T, tid);
+  }
   // per-query stats: -lse (so P = exp2(fma(S, c, -lse))) and delta (8 lanes per query);
   // rows >= T get -inf -> P = 0
   for (int i = tid; i < NE * 16 * 8; i += 512) {
@@ -627,7 +642,7 @@ __global__ void __launch_bounds__(512) attn_bwd_dkdv_seq_kernel(AttnSeqBwdParams
   const int r0 = row_lane_off(lane, 0), r1 = row_lane_off(lane, 1);
   int to[4];
 #pragma unroll
-  for (int dt = 0; dt < 4; ++dt) to[dt] = tr_lane_off(lane, dt);
+  for (int dt = 0; dt < 4; ++dt) to[dt] = SINGLE ? tr_row_lane_off(lane, dt) : tr_lane_off(lane, dt);
   __syncthreads();
   for (int kt = wave; kt < NT; kt += 8) {
     const int key = kt * 16 + (lane & 15);
@@ -697,26 +712,26 @@ __global__ void __launch_bounds__(512) attn_bwd_dkdv_seq_kernel(AttnSeqBwdParams
 }
 
 // dQ: one workgroup (8 waves) per (b, h); wave w owns query subtiles w, w+8.
-template <int NT>
+template <int NT, bool SINGLE>
 __global__ void __launch_bounds__(512) attn_bwd_dq_seq_kernel(AttnSeqBwdParams p) {
   constexpr int NE = (NT + 1) & ~1;
   constexpr int IMG = NE * 16 * 128;
-  __shared__ __attribute__((aligned(16))) char smem[3 * IMG];
+  __shared__ __attribute__((aligned(16))) char smem[(SINGLE ? 2 : 3) * IMG];
   char* Kr = smem;
-  char* Kt = smem + IMG;
-  char* Vr = smem + 2 * IMG;
+  char* Vr = smem + IMG;
+  char* Kt = SINGLE ? Kr : smem + 2 * IMG;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, g = lane >> 4;
   const int bh = blockIdx.x, b = bh / p.H, h = bh % p.H;
   const u16* base = p.qkv + (long)b * p.T * p.ld + h * D;
   const u16* dOg = p.dout + (long)b * p.T * p.ldo + h * D;
   const u16* Og = p.out + (long)b * p.T * p.ldo + h * D;
   stage_seq<false, NE, 512>(Kr, base + p.H * D, p.ld, p.T, tid);
-  stage_seq<true, NE, 512>(Kt, base + p.H * D, p.ld, p.T, tid);
   stage_seq<false, NE, 512>(Vr, base + 2 * p.H * D, p.ld, p.T, tid);
+  if (!SINGLE) stage_seq<true, NE, 512>(Kt, base + p.H * D, p.ld, p.T, tid);
   const int r0 = row_lane_off(lane, 0), r1 = row_lane_off(lane, 1);
   int to[4];
 #pragma unroll
-  for (int dt = 0; dt < 4; ++dt) to[dt] = tr_lane_off(lane, dt);
+  for (int dt = 0; dt < 4; ++dt) to[dt] = SINGLE ? tr_row_lane_off(lane, dt) : tr_lane_off(lane, dt);
   const int klast = 16 * (NT - 1) + 4 * g;
   __syncthreads();
   for (int qs = wave; qs < NT; qs += 8) {
@@ -807,6 +822,20 @@ static int seq_nkt(int T) {
     default: CALL(16); break;   \
   }
 
+// PDT_ATTN_BWD_SINGLE=0: the two-image (row + transposed) backward staging, for A/B runs
+static int g_attn_bwd_single = -1;
+static int attn_bwd_single() {
+  if (g_attn_bwd_single < 0) {
+    const char* e = getenv("PDT_ATTN_BWD_SINGLE");
+    g_attn_bwd_single = (e && e[0] == '0') ? 0 : 1;
+  }
+  return g_attn_bwd_single;
+}
+PDT_API int pdt_attn_set_bwd_single(int on) {
+  g_attn_bwd_single = on ? 1 : 0;
+  return 0;
+}
+
 static int attn_seq_disabled() {
   static int v = -1;
   if (v < 0) {
@@ -854,9 +883,14 @@ PDT_API int pdt_attn_bwd(const void* qkv, const void* out, const void* dout, con
     q.c = scale * 1.4426950408889634f;
     q.scale = scale;
     dim3 g(B * H);
-#define SEQ_BWD(N)                                                                \
-  hipLaunchKernelGGL(attn_bwd_dkdv_seq_kernel<N>, g, dim3(512), 0, st, q);        \
-  hipLaunchKernelGGL(attn_bwd_dq_seq_kernel<N>, g, dim3(512), 0, st, q)
+#define SEQ_BWD(N)                                                                     \
+  if (attn_bwd_single()) {                                                             \
+    hipLaunchKernelGGL((attn_bwd_dkdv_seq_kernel<N, true>), g, dim3(512), 0, st, q);   \
+    hipLaunchKernelGGL((attn_bwd_dq_seq_kernel<N, true>), g, dim3(512), 0, st, q);     \
+  } else {                                                                             \
+    hipLaunchKernelGGL((attn_bwd_dkdv_seq_kernel<N, false>), g, dim3(512), 0, st, q);  \
+    hipLaunchKernelGGL((attn_bwd_dq_seq_kernel<N, false>), g, dim3(512), 0, st, q);    \
+  }
     PDT_SEQ_SWITCH(nkt, SEQ_BWD)
 #undef SEQ_BWD
     PDT_RETURN_LAUNCH();

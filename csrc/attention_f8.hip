@@ -68,11 +68,17 @@ struct AttnF8Params {
   float c;          // softmax scale * log2(e)
 };
 
-// NKT = number of 32-key tiles (ceil(T/32) <= 8)
-template <int NKT>
+// bf16 K row image: [rows][128 B], chunk c of row r at c ^ ((r >> 1) & 7)
+__device__ __forceinline__ int k16_off(int row, int chunk) { return row * 128 + ((chunk ^ ((row >> 1) & 7)) << 4); }
+
+// NKT = number of 32-key tiles (ceil(T/32) <= 8). F8 = false: the same kernel with the
+// score GEMM in bf16 (4 x mfma_f32_32x32x16_bf16 per 32 x 32 tile, K kept as bf16) -- the
+// bf16 forward of ViT (126 VGPRs, 3 workgroups per CU, vs 248 VGPRs / 1 wave per SIMD
+// for the whole-sequence kernel in csrc/attention.hip)
+template <int NKT, bool F8>
 __global__ void __launch_bounds__(256) attn_fwd_f8_kernel(AttnF8Params p) {
   constexpr int ROWS = NKT * 32;
-  __shared__ __attribute__((aligned(16))) char Ks[ROWS * 64];     // fp8 K
+  __shared__ __attribute__((aligned(16))) char Ks[ROWS * (F8 ? 64 : 128)];  // fp8 or bf16 K
   __shared__ __attribute__((aligned(16))) char Vs[ROWS * 128];    // bf16 V (tr image)
   __shared__ float red[4];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -100,15 +106,21 @@ __global__ void __launch_bounds__(256) attn_fwd_f8_kernel(AttnF8Params p) {
 #pragma unroll
     for (int e = 0; e < 4; ++e) kmax = fmaxf(kmax, fmaxf(fabsf(lo_bf(k[e])), fabsf(hi_bf(k[e]))));
   }
-  kmax = warp_max(kmax);
-  if (lane == 0) red[wave] = kmax;
-  __syncthreads();
-  kmax = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
-  const float sk = pow2_scale(kmax);
+  float sk = 1.f;
+  if constexpr (F8) {
+    kmax = warp_max(kmax);
+    if (lane == 0) red[wave] = kmax;
+    __syncthreads();
+    kmax = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
+    sk = pow2_scale(kmax);
+  }
 #pragma unroll
   for (int it = 0; it < NIT; ++it) {
     const int q = tid + it * 256;
-    if (q < CH) {
+    if (!F8 && q < CH) {
+      const int row = q >> 3, ch = q & 7;
+      *reinterpret_cast<u32x4*>(Ks + k16_off(row, ch)) = kv[it];
+    } else if (q < CH) {
       const int row = q >> 3, ch = q & 7;  // 8 bf16 -> 8 fp8 bytes: half of a 16-B fp8 chunk
       const u32x4 k = kv[it];
       uint2 w;
@@ -126,22 +138,30 @@ __global__ void __launch_bounds__(256) attn_fwd_f8_kernel(AttnF8Params p) {
   for (int qt = wave; qt < nqt; qt += 4) {
     // ---- Q tile -> e4m3 B fragment: lane (q = col, hh) holds Q[q][32 hh .. 32 hh + 31]
     const int q = qt * 32 + col;
-    u32x4 qv[4];
+    // fp8: qv[c] = Q[q][32 hh + 8 c .. +7] (one 32-B fp8 fragment); bf16: qb[kk] = Q[q][16 kk + 8 hh .. +7]
+    u32x4 qv[4], qb[4];
 #pragma unroll
     for (int c = 0; c < 4; ++c) {
       qv[c] = u32x4{0, 0, 0, 0};
-      if (q < p.T) qv[c] = *reinterpret_cast<const u32x4*>(base + (long)q * p.ld + 32 * hh + 8 * c);
+      qb[c] = u32x4{0, 0, 0, 0};
+      if (q < p.T) {
+        if (F8) qv[c] = *reinterpret_cast<const u32x4*>(base + (long)q * p.ld + 32 * hh + 8 * c);
+        else qb[c] = *reinterpret_cast<const u32x4*>(base + (long)q * p.ld + 16 * c + 8 * hh);
+      }
     }
-    float qm = 0.f;
+    float sq = 1.f;
+    if constexpr (F8) {
+      float qm = 0.f;
 #pragma unroll
-    for (int c = 0; c < 4; ++c)
+      for (int c = 0; c < 4; ++c)
 #pragma unroll
-      for (int e = 0; e < 4; ++e) qm = fmaxf(qm, fmaxf(fabsf(lo_bf(qv[c][e])), fabsf(hi_bf(qv[c][e]))));
-    qm = warp_max(qm);
-    const float sq = pow2_scale(qm);
+        for (int e = 0; e < 4; ++e) qm = fmaxf(qm, fmaxf(fabsf(lo_bf(qv[c][e])), fabsf(hi_bf(qv[c][e]))));
+      qm = warp_max(qm);
+      sq = pow2_scale(qm);
+    }
     i32x8 qf;
 #pragma unroll
-    for (int c = 0; c < 4; ++c) {
+    for (int c = 0; c < (F8 ? 4 : 0); ++c) {
       qf[2 * c] = (int)cvt4_e4m3(lo_bf(qv[c][0]) * sq, hi_bf(qv[c][0]) * sq, lo_bf(qv[c][1]) * sq,
                                  hi_bf(qv[c][1]) * sq);
       qf[2 * c + 1] = (int)cvt4_e4m3(lo_bf(qv[c][2]) * sq, hi_bf(qv[c][2]) * sq, lo_bf(qv[c][3]) * sq,
@@ -161,13 +181,22 @@ __global__ void __launch_bounds__(256) attn_fwd_f8_kernel(AttnF8Params p) {
     // at 7 tiles, 2 waves/SIMD); rolled it stays near 100 (more workgroups per CU)
 #pragma unroll 1
     for (int t = 0; t < NKT; ++t) {
-      // A fragment: K[key = 32t + col][d = 32 hh .. +31] (two swizzled 16-B chunks)
       const int krow = 32 * t + col;
-      const u32x4 a0 = *reinterpret_cast<const u32x4*>(Ks + k8_off(krow, 2 * hh));
-      const u32x4 a1 = *reinterpret_cast<const u32x4*>(Ks + k8_off(krow, 2 * hh + 1));
-      const i32x8 kf = {(int)a0[0], (int)a0[1], (int)a0[2], (int)a0[3], (int)a1[0], (int)a1[1], (int)a1[2], (int)a1[3]};
       f32x16 s = {};
-      s = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(kf, qf, s, 0, 0, 0, 127, 0, 127);
+      if constexpr (F8) {
+        // A fragment: K[key = 32t + col][d = 32 hh .. +31] (two swizzled 16-B chunks)
+        const u32x4 a0 = *reinterpret_cast<const u32x4*>(Ks + k8_off(krow, 2 * hh));
+        const u32x4 a1 = *reinterpret_cast<const u32x4*>(Ks + k8_off(krow, 2 * hh + 1));
+        const i32x8 kf = {(int)a0[0], (int)a0[1], (int)a0[2], (int)a0[3], (int)a1[0], (int)a1[1], (int)a1[2], (int)a1[3]};
+        s = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(kf, qf, s, 0, 0, 0, 127, 0, 127);
+      } else {
+        // k-step kk covers d = 16 kk .. +15: lane half hh holds d = 16 kk + 8 hh .. +7
+#pragma unroll
+        for (int kk = 0; kk < 4; ++kk) {
+          const bf16x8 kf = *reinterpret_cast<const bf16x8*>(Ks + k16_off(krow, 2 * kk + hh));
+          s = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf, __builtin_bit_cast(bf16x8, qb[kk]), s, 0, 0, 0);
+        }
+      }
       // s[r] = S[key = 32t + (r & 3) + 8 (r >> 2) + 4 hh][query q], raw (scaled) fp8 product
       float mt = -INFINITY;
 #pragma unroll
@@ -249,7 +278,7 @@ PDT_API int pdt_attn_fwd_f8(const void* qkv, void* out, float* lse, int B, int T
   p.c = scale * 1.4426950408889634f;
   const int nkt = (T + 31) / 32;
   dim3 g(B * H);
-#define F8(N) hipLaunchKernelGGL(attn_fwd_f8_kernel<N>, g, dim3(256), 0, st, p)
+#define F8(N) hipLaunchKernelGGL((attn_fwd_f8_kernel<N, true>), g, dim3(256), 0, st, p)
   switch (nkt) {
     case 1: F8(1); break;
     case 2: F8(2); break;
@@ -261,5 +290,34 @@ PDT_API int pdt_attn_fwd_f8(const void* qkv, void* out, float* lse, int B, int T
     default: F8(8); break;
   }
 #undef F8
+  PDT_RETURN_LAUNCH();
+}
+
+// the same kernel with a bf16 score GEMM (ViT bf16 forward); -1 when not covered
+PDT_API int pdt_attn_fwd_tiles(const void* qkv, void* out, float* lse, int B, int T, int H, float scale,
+                               hipStream_t st) {
+  if (T < 1 || T > 256) return -1;
+  AttnF8Params p;
+  p.qkv = (const u16*)qkv;
+  p.out = (u16*)out;
+  p.lse = lse;
+  p.B = B; p.T = T; p.H = H;
+  p.ld = 3L * H * D;
+  p.ldo = (long)H * D;
+  p.c = scale * 1.4426950408889634f;
+  const int nkt = (T + 31) / 32;
+  dim3 g(B * H);
+#define BF(N) hipLaunchKernelGGL((attn_fwd_f8_kernel<N, false>), g, dim3(256), 0, st, p)
+  switch (nkt) {
+    case 1: BF(1); break;
+    case 2: BF(2); break;
+    case 3: BF(3); break;
+    case 4: BF(4); break;
+    case 5: BF(5); break;
+    case 6: BF(6); break;
+    case 7: BF(7); break;
+    default: BF(8); break;
+  }
+#undef BF
   PDT_RETURN_LAUNCH();
 }

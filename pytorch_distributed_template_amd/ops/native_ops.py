@@ -74,6 +74,8 @@ _SIGS = {
     "pdt_add_bf16": (c_int, [P, P, P, c_long, P]),
     "pdt_attn_fwd": (c_int, [P, P, P, c_int, c_int, c_int, c_float, P]),
     "pdt_attn_fwd_f8": (c_int, [P, P, P, c_int, c_int, c_int, c_float, P]),
+    "pdt_attn_fwd_tiles": (c_int, [P, P, P, c_int, c_int, c_int, c_float, P]),
+    "pdt_attn_set_bwd_single": (c_int, [c_int]),
     "pdt_gemm_f8_num_variants": (c_int, []),
     "pdt_gemm_f8": (c_int, [P, P, P, P, P, P] + [c_int] * 8 + [P, P, c_int, P]),
     "pdt_bn_set_unroll": (c_int, [c_int]),
@@ -1846,6 +1848,8 @@ class _QKVAttention(torch.autograd.Function):
         scale = 64 ** -0.5
         if fp8 and T <= 256:  # fp8 QK^T (csrc/attention_f8.hip), fp32 softmax, bf16 PV
             _chk(_load().pdt_attn_fwd_f8(_p(qkv), _p(out), _p(lse), B, T, H, scale, _s()), "attn_fwd_f8")
+        elif T <= 256 and os.environ.get("PDT_ATTN_FWD32", "1") == "1":  # 32x32-tile bf16 forward
+            _chk(_load().pdt_attn_fwd_tiles(_p(qkv), _p(out), _p(lse), B, T, H, scale, _s()), "attn_fwd_tiles")
         else:
             _chk(_load().pdt_attn_fwd(_p(qkv), _p(out), _p(lse), B, T, H, scale, _s()), "attn_fwd")
         ctx.save_for_backward(qkv, out, lse)

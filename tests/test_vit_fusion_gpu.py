@@ -88,7 +88,8 @@ def test_linear_residual_epilogue(fp8):
     y.backward(g)
     yr.backward(g.float())
     assert torch.equal(r.grad, g)  # the residual gradient is dy itself
-    assert nrmerr(x.grad, xr.grad) < 2e-2
+    # fp8: the data gradient runs on e5m2 output gradients (2 mantissa bits) by default
+    assert nrmerr(x.grad, xr.grad) < (8e-2 if fp8 else 2e-2), nrmerr(x.grad, xr.grad)
     assert nrmerr(fc.weight.grad, wr.grad) < 2e-2
     assert nrmerr(fc.bias.grad, g.float().sum((0, 1))) < 1e-4
 
