@@ -53,7 +53,7 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=30)
     ap.add_argument("--warmup", type=int, default=10)
-    ap.add_argument("--batch", type=int, default=None, help="per-GPU batch (default: 512 for resnet50, else 256)")
+    ap.add_argument("--batch", type=int, default=None, help="per-GPU batch (default: 1024 for resnet50, else 256)")
     ap.add_argument("--model", default="resnet50")
     ap.add_argument("--fp8", action="store_true", help="ViT: fp8 (e4m3/e5m2) GEMMs on the native path")
     ap.add_argument("--backend", default="native", choices=["native", "torch"])

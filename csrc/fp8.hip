@@ -58,20 +58,7 @@ __device__ __forceinline__ float block_amax(const float* __restrict__ partial, i
 
 template <int FMT>
 __device__ __forceinline__ uint32_t cvt4(float a, float b, float c, float d) {
-  constexpr float FMAX = FMT == 0 ? 448.f : 57344.f;
-  a = fminf(fmaxf(a, -FMAX), FMAX);
-  b = fminf(fmaxf(b, -FMAX), FMAX);
-  c = fminf(fmaxf(c, -FMAX), FMAX);
-  d = fminf(fmaxf(d, -FMAX), FMAX);
-  int r;
-  if (FMT == 0) {
-    r = __builtin_amdgcn_cvt_pk_fp8_f32(a, b, 0, false);
-    r = __builtin_amdgcn_cvt_pk_fp8_f32(c, d, r, true);
-  } else {
-    r = __builtin_amdgcn_cvt_pk_bf8_f32(a, b, 0, false);
-    r = __builtin_amdgcn_cvt_pk_bf8_f32(c, d, r, true);
-  }
-  return (uint32_t)r;
+  return pdt_cvt4_f8<FMT>(a, b, c, d);
 }
 
 template <int FMT>
@@ -207,6 +194,25 @@ __global__ void fp8_meta_roll_kernel(float* __restrict__ meta) {
   mu[2] = 0u;
 }
 
+// the same roll for a producer kernel that wrote per-block amax partials instead of
+// the atomicMax slot (the LayerNorm forward's fused fp8 output)
+template <int FMT>
+__global__ void __launch_bounds__(256) fp8_meta_roll_part_kernel(float* __restrict__ meta,
+                                                                const float* __restrict__ partial, int nblk) {
+  const float a = block_amax(partial, nblk);
+  if (threadIdx.x != 0) return;
+  unsigned int* mu = reinterpret_cast<unsigned int*>(meta);
+  const float cur = fmaxf(a, __uint_as_float(mu[2]));
+  const int idx = (int)mu[4];
+  meta[5 + idx % HIST] = cur;
+  mu[4] = (unsigned)(idx + 1);
+  float h = 0.f;
+  for (int i = 0; i < HIST; ++i) h = fmaxf(h, meta[5 + i]);
+  meta[1] = 1.f / meta[0];
+  meta[0] = scale_from<FMT>(h);
+  mu[2] = 0u;
+}
+
 int nblocks(long n) {
   long b = (n + 256 * 8 - 1) / (256 * 8);
   if (b > AMAX_BLOCKS) b = AMAX_BLOCKS;
@@ -261,6 +267,13 @@ PDT_API int pdt_cast_fp8_delayed(const void* x, int bf16, long n, float* meta, i
 #undef CD
   if (fmt == 0) hipLaunchKernelGGL(fp8_meta_roll_kernel<0>, dim3(1), dim3(64), 0, st, meta);
   else hipLaunchKernelGGL(fp8_meta_roll_kernel<1>, dim3(1), dim3(64), 0, st, meta);
+  PDT_RETURN_LAUNCH();
+}
+
+// roll after a fused producer (pdt_ln_fwd_f8): partial[nblk] holds its per-block amaxes
+PDT_API int pdt_fp8_meta_roll_partial(float* meta, const float* partial, int nblk, int fmt, hipStream_t st) {
+  if (fmt == 0) hipLaunchKernelGGL(fp8_meta_roll_part_kernel<0>, dim3(1), dim3(256), 0, st, meta, partial, nblk);
+  else hipLaunchKernelGGL(fp8_meta_roll_part_kernel<1>, dim3(1), dim3(256), 0, st, meta, partial, nblk);
   PDT_RETURN_LAUNCH();
 }
 

@@ -23,14 +23,25 @@ __device__ __forceinline__ void st4(u16* p, const float* f) {
   *reinterpret_cast<uint2*>(p) = v;
 }
 
-template <int CH>  // chunks of 4 per lane: D = 256*CH
+// F8: also write the e4m3 codes of the (bf16-rounded) output with the delayed scale
+// meta[0] of the consuming fp8 GEMM, and the block's |y| max to amax_part[blockIdx.x]
+// (rolled into that GEMM's amax history by pdt_fp8_meta_roll_partial) -- the
+// activation-quantisation pass of the fp8 path folded into the producer.
+template <int CH, bool F8 = false>  // chunks of 4 per lane: D = 256*CH
 __global__ void __launch_bounds__(64 * WPB) ln_fwd_kernel(const u16* __restrict__ x, const float* __restrict__ g,
                                                           const float* __restrict__ b, u16* __restrict__ y,
                                                           float* __restrict__ mean_out, float* __restrict__ rstd_out,
-                                                          int rows, float eps) {
+                                                          int rows, float eps, uint8_t* __restrict__ q8 = nullptr,
+                                                          const float* __restrict__ meta = nullptr,
+                                                          float* __restrict__ amax_part = nullptr) {
   const int lane = threadIdx.x & 63;
-  const int row = blockIdx.x * WPB + (threadIdx.x >> 6);
-  if (row >= rows) return;
+  int row = blockIdx.x * WPB + (threadIdx.x >> 6);
+  __shared__ float red[WPB];
+  if (!F8 && row >= rows) return;
+  // F8: a wave past the last row recomputes row rows-1 (same values) so every wave
+  // reaches the block's amax barrier; its stores are the same bytes as that row's
+  if (F8 && row >= rows) row = rows - 1;
+  float amax = 0.f;
   constexpr int D = 256 * CH;
   const u16* xr = x + (long)row * D;
   float v[CH][4];
@@ -60,10 +71,31 @@ __global__ void __launch_bounds__(64 * WPB) ln_fwd_kernel(const u16* __restrict_
 #pragma unroll
     for (int e = 0; e < 4; ++e) o[e] = (v[c][e] - mean) * rstd * gg[e] + bb[e];
     st4(yr + col, o);
+    if (F8) {
+      const float s = meta[0];
+      float r[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        r[e] = bf2f(f2bf(o[e]));  // quantise exactly what the bf16 output holds
+        amax = fmaxf(amax, fabsf(r[e]));
+      }
+      *reinterpret_cast<uint32_t*>(q8 + (long)row * D + col) = pdt_cvt4_f8<0>(r[0] * s, r[1] * s, r[2] * s, r[3] * s);
+    }
   }
   if (lane == 0) {
     mean_out[row] = mean;
     rstd_out[row] = rstd;
+  }
+  if (F8) {
+    amax = warp_max(amax);
+    if (lane == 0) red[threadIdx.x >> 6] = amax;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      float m = red[0];
+#pragma unroll
+      for (int w = 1; w < WPB; ++w) m = fmaxf(m, red[w]);
+      amax_part[blockIdx.x] = m;
+    }
   }
 }
 
@@ -203,6 +235,32 @@ PDT_API int pdt_ln_fwd(const void* x, const float* g, const float* b, void* y, f
     default: return -1;
   }
   PDT_RETURN_LAUNCH();
+}
+
+PDT_API int pdt_fp8_meta_roll_partial(float* meta, const float* partial, int nblk, int fmt, hipStream_t st);
+
+PDT_API int pdt_ln_fwd_f8_blocks(int rows) { return (rows + WPB - 1) / WPB; }
+
+// LayerNorm forward that also emits the e4m3 codes of its output for the next fp8 GEMM
+// (delayed scale meta[0]) and rolls that GEMM's amax history; amax_part holds
+// pdt_ln_fwd_f8_blocks(rows) floats.
+PDT_API int pdt_ln_fwd_f8(const void* x, const float* g, const float* b, void* y, float* mean, float* rstd, int rows,
+                          int D, float eps, void* q, float* meta, float* amax_part, hipStream_t st) {
+  const int nb = (rows + WPB - 1) / WPB;
+  dim3 grid(nb), blk(64 * WPB);
+#define LF(CH_) hipLaunchKernelGGL((ln_fwd_kernel<CH_, true>), grid, blk, 0, st, (const u16*)x, g, b, (u16*)y, mean, \
+                                   rstd, rows, eps, (uint8_t*)q, (const float*)meta, amax_part)
+  switch (D) {
+    case 256: LF(1); break;
+    case 512: LF(2); break;
+    case 768: LF(3); break;
+    case 1024: LF(4); break;
+    default: return -1;
+  }
+#undef LF
+  int e = (int)hipGetLastError();
+  if (e) return e;
+  return pdt_fp8_meta_roll_partial(meta, amax_part, nb, 0, st);
 }
 
 static int ln_rows_per_block(int rows) {

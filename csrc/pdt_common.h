@@ -21,6 +21,26 @@ __device__ __forceinline__ float pdt_tanh(float x) {
   return 1.f - 2.f * __builtin_amdgcn_rcpf(1.f + __expf(2.f * x));
 }
 
+// four floats -> four packed OCP fp8 codes (FMT 0 = e4m3fn, 1 = e5m2) with the gfx950
+// packed converts (round to nearest even); clamped to the finite range first
+template <int FMT>
+__device__ __forceinline__ uint32_t pdt_cvt4_f8(float a, float b, float c, float d) {
+  constexpr float FMAX = FMT == 0 ? 448.f : 57344.f;
+  a = fminf(fmaxf(a, -FMAX), FMAX);
+  b = fminf(fmaxf(b, -FMAX), FMAX);
+  c = fminf(fmaxf(c, -FMAX), FMAX);
+  d = fminf(fmaxf(d, -FMAX), FMAX);
+  int r;
+  if (FMT == 0) {
+    r = __builtin_amdgcn_cvt_pk_fp8_f32(a, b, 0, false);
+    r = __builtin_amdgcn_cvt_pk_fp8_f32(c, d, r, true);
+  } else {
+    r = __builtin_amdgcn_cvt_pk_bf8_f32(a, b, 0, false);
+    r = __builtin_amdgcn_cvt_pk_bf8_f32(c, d, r, true);
+  }
+  return (uint32_t)r;
+}
+
 #define PDT_API extern "C" __attribute__((visibility("default")))
 #define LDS_PTR(T) T __attribute__((address_space(3)))*
 

@@ -62,9 +62,10 @@ class Block(nn.Module):
     def forward(self, x, fp8=False):
         # pre-norm residual block; the residual adds ride the proj / fc2 GEMM epilogues and
         # their gradients are summed inside the LayerNorm backward (fused.ln_fork)
-        x, h = fused.ln_fork(x, self.norm1)
+        # (fp8: the LayerNorm kernels also write the e4m3 inputs of qkv / fc1)
+        x, h = fused.ln_fork(x, self.norm1, self.attn.qkv if fp8 else None)
         x = self.attn(h, fp8=fp8, residual=x)
-        x, h = fused.ln_fork(x, self.norm2)
+        x, h = fused.ln_fork(x, self.norm2, self.mlp.fc1 if fp8 else None)
         return self.mlp(h, fp8=fp8, residual=x)
 
 

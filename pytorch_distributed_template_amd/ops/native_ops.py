@@ -36,6 +36,9 @@ _SIGS = {
     "pdt_conv_nt": (c_int, [P, P, P, P, P, P, P] + [c_int] * 25 + [P, c_int, c_int, P]),
     "pdt_conv_nt_bnb": (c_int, [P] * 5 + [c_int] * 25 + [P] * 6 + [c_int] * 3 + [P]),
     "pdt_ln_fwd": (c_int, [P, P, P, P, P, P, c_int, c_int, c_float, P]),
+    "pdt_ln_fwd_f8": (c_int, [P, P, P, P, P, P, c_int, c_int, c_float, P, P, P, P]),
+    "pdt_ln_fwd_f8_blocks": (c_int, [c_int]),
+    "pdt_fp8_meta_roll_partial": (c_int, [P, P, c_int, c_int, P]),
     "pdt_ln_bwd_blocks": (c_int, [c_int]),
     "pdt_ln_bwd": (c_int, [P] * 9 + [c_int, c_int, c_int, P, P]),
     "pdt_gelu_bwd": (c_int, [P, P, P, c_long, P]),
@@ -1552,6 +1555,17 @@ def _quant_act(x2, owner, attr="_pdt_fp8_meta"):
     return q, dq
 
 
+def _quant_grad(g2, owner, attr):
+    """e5m2 codes + dequant scale of an output gradient for the fp8 data-gradient GEMM.
+    Delayed scaling (the default) is one fused cast+amax pass with the history kept on
+    ``owner``; current scaling needs a separate amax pass over the gradient first."""
+    if fp8_settings()["scaling"] == "current":
+        return quantize_fp8(g2, E5M2)
+    q, dq, meta = quantize_fp8_delayed(g2, getattr(owner, attr, None), E5M2)
+    setattr(owner, attr, meta)
+    return q, dq
+
+
 class _LinearF8(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, w, b, act, fc, residual):
@@ -1560,7 +1574,8 @@ class _LinearF8(torch.autograd.Function):
         Mrows, K = x2.shape
         Nout = w.shape[0]
         cfg = fp8_settings()
-        xq, dqx = _quant_act(x2, fc)
+        pre = _prequant(x, fc)
+        xq, dqx = pre if pre is not None else _quant_act(x2, fc)
         wq, _, dqw = fp8_weight(w)
         y = torch.empty((Mrows, Nout), dtype=torch.bfloat16, device=x.device)
         z = torch.empty_like(y) if act == "gelu" else None
@@ -1568,9 +1583,8 @@ class _LinearF8(torch.autograd.Function):
         gemm_f8(xq, wq, y, dqx, dqw, bias=bias, act=ACT[act], aux=z, addend=_residual2d(residual, Mrows, Nout))
         ctx.save_for_backward(x2, w, y if act == "relu" else z)
         ctx.meta = (shp, act, b is not None)
-        # e5m2 data-gradient GEMM (default on; PDT_FP8_DGRAD=0 keeps it bf16): measured
-        # +0.8 % end to end on ViT-B/16 -- its dY quantisation pass costs most of what
-        # the fp8 GEMM saves over the bf16 one
+        ctx.fc = fc
+        # e5m2 data-gradient GEMM (default on; PDT_FP8_DGRAD=0 keeps it bf16)
         ctx.fp8_dgrad = cfg["dgrad"]
         return y.reshape(*shp[:-1], Nout)
 
@@ -1591,7 +1605,7 @@ class _LinearF8(torch.autograd.Function):
         dx = None
         if ctx.needs_input_grad[0]:
             if ctx.fp8_dgrad:
-                dyq, dqdy = quantize_fp8(dy2, E5M2)
+                dyq, dqdy = _quant_grad(dy2, ctx.fc, "_pdt_fp8_gmeta")
                 _, wqt, dqw = fp8_weight(w)
                 dx = torch.empty((Mrows, K), dtype=torch.bfloat16, device=dy.device)
                 gemm_f8(dyq, wqt, dx, dqdy, dqw, fmt_a=E5M2)
@@ -1638,7 +1652,8 @@ class _Mlp(torch.autograd.Function):
         res = _residual2d(residual, Mrows, Nout)
         bias1, bias2 = b1.float().contiguous(), b2.float().contiguous()
         if fp8:
-            xq, dqx = _quant_act(x2, mlp.fc1)
+            pre = _prequant(x, mlp.fc1)
+            xq, dqx = pre if pre is not None else _quant_act(x2, mlp.fc1)
             w1q, _, dqw1 = fp8_weight(w1)
             gemm_f8(xq, w1q, a, dqx, dqw1, bias=bias1, act=ACT["gelu"], aux=z)
             aq, dqa = _quant_act(a, mlp.fc2)
@@ -1648,7 +1663,7 @@ class _Mlp(torch.autograd.Function):
             _gemm_bf16(x2, bf16_weight(w1), a, bias=bias1, act="gelu", aux=z)
             _gemm_bf16(a, bf16_weight(w2), out, bias=bias2, addend=res)
         ctx.save_for_backward(x2, a, z, w1, w2)
-        ctx.shp, ctx.fp8 = shp, fp8
+        ctx.shp, ctx.fp8, ctx.mlp = shp, fp8, mlp
         ctx.fp8_dgrad = fp8 and fp8_settings()["dgrad"]
         return out.reshape(*shp[:-1], Nout)
 
@@ -1661,7 +1676,7 @@ class _Mlp(torch.autograd.Function):
         g2 = g.reshape(Mrows, Nout).to(torch.bfloat16).contiguous()
         dz = torch.empty((Mrows, Hd), dtype=torch.bfloat16, device=g.device)
         if ctx.fp8_dgrad:
-            gq, dqg = quantize_fp8(g2, E5M2)
+            gq, dqg = _quant_grad(g2, ctx.mlp.fc2, "_pdt_fp8_gmeta")
             _, w2qt, dqw2 = fp8_weight(w2)
             gemm_f8(gq, w2qt, dz, dqg, dqw2, fmt_a=E5M2, act=3, addend=z)
         else:
@@ -1671,7 +1686,7 @@ class _Mlp(torch.autograd.Function):
         if need[0]:
             dx = torch.empty((Mrows, K), dtype=torch.bfloat16, device=g.device)
             if ctx.fp8_dgrad:
-                dzq, dqdz = quantize_fp8(dz, E5M2)
+                dzq, dqdz = _quant_grad(dz, ctx.mlp.fc1, "_pdt_fp8_gmeta")
                 _, w1qt, dqw1 = fp8_weight(w1)
                 gemm_f8(dzq, w1qt, dx, dqdz, dqw1, fmt_a=E5M2)
             else:
@@ -1746,7 +1761,7 @@ class _LNFork(torch.autograd.Function):
     the LayerNorm backward kernel (no add pass)."""
 
     @staticmethod
-    def forward(ctx, x, g, b, eps):
+    def forward(ctx, x, g, b, eps, f8meta, f8box):
         shp = x.shape
         D = shp[-1]
         x2 = x.reshape(-1, D).contiguous()
@@ -1754,8 +1769,17 @@ class _LNFork(torch.autograd.Function):
         y = torch.empty_like(x2)
         stats = torch.empty((2, rows), dtype=torch.float32, device=x.device)
         gf = g.float().contiguous()
-        _chk(_load().pdt_ln_fwd(_p(x2), _p(gf), _p(b.float().contiguous()), _p(y), _p(stats[0]), _p(stats[1]), rows,
-                                D, float(eps), _s()), "ln_fwd")
+        lib = _load()
+        bf = b.float().contiguous()
+        if f8meta is not None:  # also emit the next fp8 GEMM's e4m3 input (delayed scale f8meta)
+            q = torch.empty((rows, D), dtype=torch.uint8, device=x.device)
+            part = torch.empty(lib.pdt_ln_fwd_f8_blocks(rows), dtype=torch.float32, device=x.device)
+            _chk(lib.pdt_ln_fwd_f8(_p(x2), _p(gf), _p(bf), _p(y), _p(stats[0]), _p(stats[1]), rows, D, float(eps),
+                                   _p(q), _p(f8meta), _p(part), _s()), "ln_fwd_f8")
+            f8box.append((q, f8meta[1:2]))
+        else:
+            _chk(lib.pdt_ln_fwd(_p(x2), _p(gf), _p(bf), _p(y), _p(stats[0]), _p(stats[1]), rows, D, float(eps),
+                                _s()), "ln_fwd")
         ctx.save_for_backward(x2, gf, stats)
         ctx.shp = shp
         return x.view_as(x), y.reshape(shp)
@@ -1777,16 +1801,37 @@ class _LNFork(torch.autograd.Function):
         db = torch.empty(D, dtype=torch.float32, device=dev)
         _chk(lib.pdt_ln_bwd(_p(dy2), _p(x2), _p(gf), _p(stats[0]), _p(stats[1]), _p(dx), _p(dg), _p(db), _p(part),
                             rows, D, 0, _p(add), _s()), "ln_bwd")
-        return dx.reshape(ctx.shp), dg, db, None
+        return dx.reshape(ctx.shp), dg, db, None, None, None
 
 
-def ln_fork(x, ln):
-    """(x, ln(x)) with the residual gradient summed in LayerNorm's backward (see _LNFork)."""
+def ln_fork(x, ln, fp8_for=None):
+    """(x, ln(x)) with the residual gradient summed in LayerNorm's backward (see _LNFork).
+
+    ``fp8_for``: the nn.Linear that consumes ln(x) in fp8. Under delayed scaling (once
+    that layer's amax history exists) the LayerNorm kernel also writes the e4m3 codes
+    of its output with the layer's scale and rolls its history, and the codes ride on
+    the returned tensor (``_pdt_f8``) for the fp8 GEMM to pick up -- no separate
+    quantisation pass over the activation."""
     D = ln.normalized_shape[-1]
     if (len(ln.normalized_shape) != 1 or D not in (256, 512, 768, 1024) or not ln.elementwise_affine
             or x.dtype != torch.bfloat16):
         return x, layer_norm(x, ln)
-    return _LNFork.apply(x, ln.weight, ln.bias, ln.eps)
+    meta = None
+    if fp8_for is not None and fp8_settings()["scaling"] == "delayed" and D % 128 == 0:
+        meta = getattr(fp8_for, "_pdt_fp8_meta", None)
+    box: list = []
+    xo, h = _LNFork.apply(x, ln.weight, ln.bias, ln.eps, meta, box)
+    if box:
+        h._pdt_f8 = (box[0][0], box[0][1], fp8_for)
+    return xo, h
+
+
+def _prequant(x, owner):
+    """(codes [rows, K], dq) if ``x`` carries fp8 codes made for ``owner`` (ln_fork), else None."""
+    pre = getattr(x, "_pdt_f8", None)
+    if pre is None or pre[2] is not owner:
+        return None
+    return pre[0], pre[1]
 
 
 # =============================================================================

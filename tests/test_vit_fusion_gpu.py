@@ -5,6 +5,9 @@
 * residual add in the linear GEMM epilogue (bf16 and fp8) and its gradient
 * LayerNorm fork: residual gradient summed inside the LayerNorm backward
 * the fused transformer MLP node, and a 2-block ViT vs the torch path in fp32
+* fp8: LayerNorm forward emitting the next GEMM's e4m3 input (bit-exact vs the separate
+  delayed-scaling cast), and a 2-block fp8 ViT over several steps (delayed scaling for
+  activations and e5m2 output gradients) vs the torch path in fp32
 """
 import pytest
 import torch
@@ -110,6 +113,61 @@ def test_ln_fork_sums_residual_gradient():
     ((xid.float() * gres.float()).sum() + (h.float() * gh.float()).sum()).backward()
     ((xr * gres.float()).sum() + (hr * gh.float()).sum()).backward()
     assert nrmerr(x.grad, xr.grad) < 2e-2, nrmerr(x.grad, xr.grad)
+
+
+def test_ln_fork_fp8_codes_match_separate_cast():
+    """pdt_ln_fwd_f8: same e4m3 codes, dq and amax-history roll as LayerNorm followed by
+    the delayed-scaling cast (rows % 4 != 0 exercises the idle-wave path)."""
+    torch.manual_seed(26)
+    ln = nn.LayerNorm(768, eps=1e-6).cuda()
+    with torch.no_grad():
+        ln.weight.uniform_(0.5, 1.5)
+        ln.bias.uniform_(-0.2, 0.2)
+    fc = nn.Linear(768, 256).cuda()
+    x = (torch.randn(2, 197, 768, device="cuda") * 2).to(torch.bfloat16)
+    no._quant_act(torch.randn(394, 768, device="cuda").to(torch.bfloat16), fc)  # seed fc's history
+    meta0 = fc._pdt_fp8_meta.clone()
+    _, h = no.ln_fork(x, ln, fc)
+    assert hasattr(h, "_pdt_f8") and h._pdt_f8[2] is fc
+    q, dq = h._pdt_f8[0].clone(), h._pdt_f8[1].clone()
+    meta1 = fc._pdt_fp8_meta.clone()
+    _, h_ref = no.ln_fork(x, ln)
+    assert torch.equal(h, h_ref)
+    q_ref, dq_ref, meta_ref = no.quantize_fp8_delayed(h_ref.reshape(-1, 768), meta0.clone(), no.E4M3)
+    torch.cuda.synchronize()
+    assert torch.equal(q.view(-1, 768), q_ref), (q.view(-1, 768) != q_ref).sum().item()
+    assert torch.equal(dq, dq_ref)
+    assert torch.equal(meta1, meta_ref), (meta1, meta_ref)
+
+
+def test_vit_fp8_steps_track_torch_fp32():
+    """2-block fp8 ViT, three forward/backward passes (the first seeds the delayed-scaling
+    histories; the later ones take the LayerNorm-fused e4m3 inputs and delayed e5m2
+    gradient scales) vs the torch path in fp32 on the same weights."""
+    from pytorch_distributed_template_amd.models.vit import VisionTransformer
+    torch.manual_seed(27)
+    m = VisionTransformer(depth=2, num_classes=32, fp8=True).cuda()
+    x = torch.randn(4, 3, 224, 224, device="cuda").to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    t = torch.randint(0, 32, (4,), device="cuda")
+    errs = []
+    for it in range(3):
+        out = {}
+        for backend in ("native", "torch"):
+            fused.set_backend(backend)
+            m.zero_grad(set_to_none=True)
+            logits = m(x if backend == "native" else x.float())
+            fused.softmax_cross_entropy(logits, t).backward()
+            out[backend] = (logits.detach().float(), {n: p.grad.detach().float().clone()
+                                                      for n, p in m.named_parameters()})
+        fused.set_backend("auto")
+        el = nrmerr(out["native"][0], out["torch"][0])
+        worst = max((nrmerr(out["native"][1][n], out["torch"][1][n]), n) for n in out["torch"][1])
+        errs.append((it, el, worst))
+    print(errs)
+    for it, el, worst in errs:
+        assert el < 8e-2, errs
+        assert worst[0] < 0.25, errs
+    assert m.blocks[0].attn.qkv._pdt_fp8_meta is not None and m.blocks[0].mlp.fc2._pdt_fp8_gmeta is not None
 
 
 @pytest.mark.parametrize("fp8", [False, True])
