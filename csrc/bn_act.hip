@@ -242,18 +242,27 @@ __device__ __forceinline__ void st_pol(T* p, const T& v, bool nts) {
   else *p = v;
 }
 
-template <bool RES, bool RELU, bool MASK = false, int U = 1, bool NTS = false>
+// RAFF: the residual is itself a raw conv output whose BatchNorm affine is applied
+// here (r*rscale + rshift) -- the ResNet downsample branch's BN apply folded into
+// the block's bn3 apply (its output is never written or re-read).
+template <bool RES, bool RELU, bool MASK = false, int U = 1, bool NTS = false, bool RAFF = false>
 __global__ void __launch_bounds__(NT) bn_apply_kernel(const u16* __restrict__ y, const u16* __restrict__ res,
                                                       u16* __restrict__ out, const float* __restrict__ scale,
                                                       const float* __restrict__ shift, long n8, int C,
-                                                      uint8_t* __restrict__ mask) {
+                                                      uint8_t* __restrict__ mask,
+                                                      const float* __restrict__ rscale = nullptr,
+                                                      const float* __restrict__ rshift = nullptr) {
   // the host sizes the grid so the stride is a multiple of C/8: a thread's 8
   // channels never change, so the per-channel coefficients are loaded once
   const int cpr = C / 8;
   const int ch = (int)((blockIdx.x * NT + threadIdx.x) % (uint32_t)cpr) * 8;
-  float sc[8], sh[8];
+  float sc[8], sh[8], rsc[8], rsh[8];
   load8f(scale + ch, sc);
   load8f(shift + ch, sh);
+  if (RAFF) {
+    load8f(rscale + ch, rsc);
+    load8f(rshift + ch, rsh);
+  }
   const uint32_t S = gridDim.x * NT;
   auto body = [&](uint32_t i, const u32x4& yv, const u32x4& rv) {
     float f[8];
@@ -263,8 +272,13 @@ __global__ void __launch_bounds__(NT) bn_apply_kernel(const u16* __restrict__ y,
     if (RES) {
       float r[8];
       unpack8(rv, r);
+      if (RAFF) {
 #pragma unroll
-      for (int k = 0; k < 8; ++k) f[k] += r[k];
+        for (int k = 0; k < 8; ++k) f[k] += r[k] * rsc[k] + rsh[k];
+      } else {
+#pragma unroll
+        for (int k = 0; k < 8; ++k) f[k] += r[k];
+      }
     }
     if (RELU) {
 #pragma unroll
@@ -621,6 +635,31 @@ PDT_API int pdt_bn_apply(const void* y, const void* res, void* out, const float*
     else APPLY(false, false, false);
   }
 #undef APPLY
+  PDT_RETURN_LAUNCH();
+}
+
+// out = relu?(y*scale + shift + (r*rscale + rshift)): a residual that is the raw output
+// of another conv whose BN affine (rscale, rshift) is applied here
+PDT_API int pdt_bn_apply_res_affine(const void* y, const void* r, void* out, const float* scale, const float* shift,
+                                    const float* rscale, const float* rshift, long M, int C, int relu, void* mask,
+                                    hipStream_t st) {
+  if (C % 8 || !r || !rscale || !rshift) return -1;
+  if (mask && !relu) return -2;
+  long n8 = M * C / 8;
+  dim3 g(grid_for(n8, C)), b(NT);
+  const u16* Y = (const u16*)y;
+  const u16* R = (const u16*)r;
+  u16* O = (u16*)out;
+  uint8_t* MK = (uint8_t*)mask;
+  if (relu && mask)
+    hipLaunchKernelGGL((bn_apply_kernel<true, true, true, 1, false, true>), g, b, 0, st, Y, R, O, scale, shift, n8, C,
+                       MK, rscale, rshift);
+  else if (relu)
+    hipLaunchKernelGGL((bn_apply_kernel<true, true, false, 1, false, true>), g, b, 0, st, Y, R, O, scale, shift, n8, C,
+                       MK, rscale, rshift);
+  else
+    hipLaunchKernelGGL((bn_apply_kernel<true, false, false, 1, false, true>), g, b, 0, st, Y, R, O, scale, shift, n8,
+                       C, MK, rscale, rshift);
   PDT_RETURN_LAUNCH();
 }
 

@@ -36,6 +36,7 @@ _SIGS = {
     "pdt_conv_nt": (c_int, [P, P, P, P, P, P, P] + [c_int] * 25 + [P, c_int, c_int, P]),
     "pdt_conv_nt_bnb": (c_int, [P] * 5 + [c_int] * 25 + [P] * 6 + [c_int] * 3 + [P]),
     "pdt_ln_fwd": (c_int, [P, P, P, P, P, P, c_int, c_int, c_float, P]),
+    "pdt_bn_apply_res_affine": (c_int, [P] * 7 + [c_long, c_int, c_int, P, P]),
     "pdt_ln_fwd_f8": (c_int, [P, P, P, P, P, P, c_int, c_int, c_float, P, P, P, P]),
     "pdt_ln_fwd_f8_blocks": (c_int, [c_int]),
     "pdt_fp8_meta_roll_partial": (c_int, [P, P, c_int, c_int, P]),
@@ -783,7 +784,10 @@ def nhwc_padded_view(x, cp):
     return torch.as_strided(x, (N, cp, H, W), (H * W * cp, 1, W * cp, cp))
 
 
-def _unit_fwd(x, w, gamma, beta, residual, conv, relu, bna: _BNArgs, apply: bool = True):
+def _unit_fwd(x, w, gamma, beta, residual, conv, relu, bna: _BNArgs, apply: bool = True, res_unit=None):
+    """conv -> BN (batch statistics from the conv epilogue) -> (+ residual) -> (ReLU).
+    ``res_unit``: the residual is that unit's RAW conv output and its BN affine is applied
+    inside this unit's BN apply (``residual`` must be ``res_unit.y``)."""
     lib = _load()
     st = _s()
     N, C, H, W = x.shape
@@ -830,8 +834,13 @@ def _unit_fwd(x, w, gamma, beta, residual, conv, relu, bna: _BNArgs, apply: bool
     # as one bit per element instead of re-reading the bf16 output (1/16 of the bytes)
     mask = torch.empty(M * Cout // 8, dtype=torch.uint8, device=x.device) if (relu and residual is not None) \
         else None
-    _chk(lib.pdt_bn_apply(_p(y), _p(res), _p(out), _p(scale), _p(shift), M, Cout, int(relu), _p(mask), st),
-         "bn_apply")
+    if res_unit is not None:
+        assert residual is res_unit.y and res_unit.Cout == Cout
+        _chk(lib.pdt_bn_apply_res_affine(_p(y), _p(res), _p(out), _p(scale), _p(shift), _p(res_unit.scale),
+                                         _p(res_unit.shift), M, Cout, int(relu), _p(mask), st), "bn_apply_res_affine")
+    else:
+        _chk(lib.pdt_bn_apply(_p(y), _p(res), _p(out), _p(scale), _p(shift), M, Cout, int(relu), _p(mask), st),
+             "bn_apply")
     u = _Unit()
     u.x, u.w, u.gamma, u.y = x, w, gamma, y
     u.act = None
@@ -1049,9 +1058,10 @@ class _SideWgrad:
 class _Bottleneck(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, blk, has_ds, *params):
-        if has_ds:
-            idn, ud = _unit_fwd(x, blk.downsample[0].weight, blk.downsample[1].weight, blk.downsample[1].bias, None,
-                                blk.downsample[0], False, _BNArgs(blk.downsample[1]))
+        if has_ds:  # raw downsample conv output; its BN affine is applied inside bn3's apply
+            _, ud = _unit_fwd(x, blk.downsample[0].weight, blk.downsample[1].weight, blk.downsample[1].bias, None,
+                              blk.downsample[0], False, _BNArgs(blk.downsample[1]), apply=False)
+            idn = ud.y
         else:
             idn, ud = _cl(x.to(torch.bfloat16)), None
         a1, u1 = _unit_fwd(x, blk.conv1.weight, blk.bn1.weight, blk.bn1.bias, None, blk.conv1, True,
@@ -1059,7 +1069,7 @@ class _Bottleneck(torch.autograd.Function):
         a2, u2 = _unit_fwd(a1, blk.conv2.weight, blk.bn2.weight, blk.bn2.bias, None, blk.conv2, True,
                            _BNArgs(blk.bn2))
         out, u3 = _unit_fwd(a2, blk.conv3.weight, blk.bn3.weight, blk.bn3.bias, idn, blk.conv3, True,
-                            _BNArgs(blk.bn3))
+                            _BNArgs(blk.bn3), res_unit=ud)
         ctx.units = (u1, u2, u3, ud)
         ctx.has_ds = has_ds
         prev = _producer_of(x) if _bnb_enabled() else None

@@ -384,21 +384,38 @@ def test_fused_bottleneck_matches_unit_composition(stride, ds):
         o = no.conv_bn_act(o, blk.conv2, blk.bn2, relu=True)
         return no.conv_bn_act(o, blk.conv3, blk.bn3, residual=idn, relu=True)
 
+    from pytorch_distributed_template_amd.ops import fused
+
+    def torch_fp32(xx):
+        fused.set_backend("torch")
+        try:
+            return blk(xx.float())
+        finally:
+            fused.set_backend("auto")
+
     outs = []
-    for fn in (lambda xx: no.bottleneck(xx, blk), unfused):
+    for fn in (lambda xx: no.bottleneck(xx, blk), unfused, torch_fp32):
         for p in blk.parameters():
             p.grad = None
         xi = x.detach().clone().requires_grad_(True)
         y = fn(xi)
         g = torch.ones_like(y) * 0.01 + _cl(torch.randn(y.shape, device="cuda", generator=torch.Generator(
             "cuda").manual_seed(3)).to(torch.bfloat16))
-        y.backward(g)
+        y.backward(g.to(y.dtype))
         outs.append((y.float(), xi.grad.float(), [p.grad.float().clone() for p in blk.parameters()]))
-    (y1, dx1, g1), (y2, dx2, g2) = outs
-    assert nrmerr(y1, y2) < 1e-3
-    assert nrmerr(dx1, dx2) < 1e-2
-    for a, b in zip(g1, g2):
-        assert nrmerr(a, b) < 1e-2
+    (y1, dx1, g1), (y2, dx2, g2), (yr, dxr, gr) = outs
+    if not ds:
+        assert nrmerr(y1, y2) < 1e-3
+        assert nrmerr(dx1, dx2) < 1e-2
+        for a, b in zip(g1, g2):
+            assert nrmerr(a, b) < 1e-2
+    else:
+        # the fused node applies the shortcut's BN affine inside bn3's apply in fp32; the
+        # composition rounds that BN output to bf16 first -- so they are not bitwise
+        # comparable (ReLU-boundary flips move dx by ~2 %): both against fp32 instead
+        assert nrmerr(y1, y2) < 4e-3, nrmerr(y1, y2)
+        for a, b, r in [(y1, y2, yr), (dx1, dx2, dxr)] + list(zip(g1, g2, gr)):
+            assert nrmerr(a, r) <= 1.5 * nrmerr(b, r) + 2e-3, (nrmerr(a, r), nrmerr(b, r))
 
 
 def test_layernorm_gelu_linear_patch_embed():
