@@ -42,10 +42,12 @@ STOCK_1GPU_IMG_S = {("resnet50", 256): 6605.4, ("resnet50", 512): 6863.8}
 # At a batch the stock stack was not measured at (its MIOpen find at bs 1024 ran
 # past 390 s on one box), compare against its BEST measured per-GPU throughput.
 STOCK_BEST_1GPU_IMG_S = {"resnet50": (6863.8, 512)}
-# Per-GPU batch: 1024 images (41 GiB of the 288 GiB HBM3E). The stage-3/4 GEMMs
-# (M = N*14*14, N*7*7) fill all 256 CUs only from ~512 images up; measured on one
-# MI355X: 11.96k img/s at 512, 12.45k at 768, 12.66k at 1024 (profiles/bench_runs_round2.jsonl).
-DEFAULT_BATCH = {"resnet50": 1024}
+# Per-GPU batch: 2048 images (82 GiB of the 288 GiB HBM3E; weak scaling, so the
+# 8-GPU job holds 16384 images). The stage-3/4 GEMMs (M = N*14*14, N*7*7) fill all
+# 256 CUs only from ~512 images up and every per-launch cost amortises over more
+# images; measured on one MI355X: 11.96k img/s at 512, 12.45k at 768, 12.66k at
+# 1024, 13.01k at 1536, 13.09-13.11k at 2048 (profiles/bench_runs_round2.jsonl).
+DEFAULT_BATCH = {"resnet50": 2048}
 
 
 def parse():
@@ -53,7 +55,7 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=30)
     ap.add_argument("--warmup", type=int, default=10)
-    ap.add_argument("--batch", type=int, default=None, help="per-GPU batch (default: 1024 for resnet50, else 256)")
+    ap.add_argument("--batch", type=int, default=None, help="per-GPU batch (default: 2048 for resnet50, else 256)")
     ap.add_argument("--model", default="resnet50")
     ap.add_argument("--fp8", action="store_true", help="ViT: fp8 (e4m3/e5m2) GEMMs on the native path")
     ap.add_argument("--backend", default="native", choices=["native", "torch"])
