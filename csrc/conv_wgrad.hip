@@ -457,6 +457,9 @@ PDT_API long pdt_wgrad_workspace(int splits, int Mo, int No) {
   return (long)splits * Mo * No + (G > 1 ? G * Mo * No : 0) + (long)splits * Mo;
 }
 
+PDT_API int pdt_wgrad_reduce(float* slab, float* out, const float* bslab, float* bias_out, int splits, int Mo, int No,
+                             float scale, int accumulate, hipStream_t stream);
+
 PDT_API int pdt_conv_wgrad(const void* dy, const void* x, float* slab, float* out, int M, int Mo, int No,
                            int ldy, int Hs, int Ws, int C, int Hm, int Wm, int sh, int sw, int oh0, int ow0,
                            int dh, int dw, int ntw, int splits, int ktiles_per_split, float scale,
@@ -494,18 +497,25 @@ PDT_API int pdt_conv_wgrad(const void* dy, const void* x, float* slab, float* ou
   else launch_wg<false>(w, grid, p, stream);
   int e = (int)hipGetLastError();
   if (e) return e;
+  return pdt_wgrad_reduce(slab, out, p.bslab, bias_out, splits, Mo, No, scale, accumulate, stream);
+}
+
+// Deterministic reduction of the split-K slabs [splits][Mo][No] (+ the optional bias slab
+// [splits][Mo]) into out (= or += scale * sum); shared by the bf16 and fp8 weight gradients.
+PDT_API int pdt_wgrad_reduce(float* slab, float* out, const float* bslab, float* bias_out, int splits, int Mo, int No,
+                             float scale, int accumulate, hipStream_t stream) {
+  const int G = reduce_groups(splits, Mo, No);
   long n4 = (long)Mo * No / 4;
   int xb = (int)((n4 + 255) / 256);
   if (bias_out) {
-    hipLaunchKernelGGL(wgrad_reduce1_kernel, dim3((Mo / 4 + 255) / 256, 1), dim3(256), 0, stream, p.bslab, bias_out,
+    hipLaunchKernelGGL(wgrad_reduce1_kernel, dim3((Mo / 4 + 255) / 256, 1), dim3(256), 0, stream, bslab, bias_out,
                        (long)(Mo / 4), splits, 1, scale, accumulate, 1);
   }
   if (G == 1) {
     hipLaunchKernelGGL(wgrad_reduce1_kernel, dim3(xb, 1), dim3(256), 0, stream, slab, out, n4, splits, 1, scale,
                        accumulate, 1);
   } else {
-    // stage-1 partials reuse the head of the slab buffer region past the live slabs? no: use slab[0..G) rows
-    // in place is unsafe (read while written), so partials go to the tail workspace provided by the caller.
+    // stage-1 partials go to the workspace tail (pdt_wgrad_workspace), never into live slabs
     float* part = slab + (long)splits * Mo * No;
     hipLaunchKernelGGL(wgrad_reduce1_kernel, dim3(xb, G), dim3(256), 0, stream, slab, part, n4, splits, G, 1.f, 0,
                        0);

@@ -47,8 +47,17 @@ __global__ void __launch_bounds__(256) amax_partial_kernel(const void* __restric
 // amax from the partials; every thread of the block gets it
 __device__ __forceinline__ float block_amax(const float* __restrict__ partial, int nblk) {
   __shared__ float red[4];
-  float m = 0.f;
-  for (int i = threadIdx.x; i < nblk; i += blockDim.x) m = fmaxf(m, partial[i]);
+  float m = 0.f, m1 = 0.f, m2 = 0.f, m3 = 0.f;
+  const int B = blockDim.x;
+  int i = threadIdx.x;
+  for (; i + 3 * B < nblk; i += 4 * B) {  // four independent loads in flight
+    m = fmaxf(m, partial[i]);
+    m1 = fmaxf(m1, partial[i + B]);
+    m2 = fmaxf(m2, partial[i + 2 * B]);
+    m3 = fmaxf(m3, partial[i + 3 * B]);
+  }
+  for (; i < nblk; i += B) m = fmaxf(m, partial[i]);
+  m = fmaxf(fmaxf(m, m1), fmaxf(m2, m3));
   m = warp_max(m);
   __syncthreads();
   if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = m;

@@ -36,6 +36,10 @@ _SIGS = {
     "pdt_conv_nt": (c_int, [P, P, P, P, P, P, P] + [c_int] * 25 + [P, c_int, c_int, P]),
     "pdt_conv_nt_bnb": (c_int, [P] * 5 + [c_int] * 25 + [P] * 6 + [c_int] * 3 + [P]),
     "pdt_ln_fwd": (c_int, [P, P, P, P, P, P, c_int, c_int, c_float, P]),
+    "pdt_wgrad_f8_num_variants": (c_int, []),
+    "pdt_wgrad_f8_plan": (c_int, [c_int, c_int, c_int, c_int, ctypes.POINTER(c_int)]),
+    "pdt_wgrad_f8_workspace": (c_long, [c_int, c_int, c_int]),
+    "pdt_linear_wgrad_f8": (c_int, [P] * 8 + [c_int] * 9 + [P]),
     "pdt_bn_apply_res_affine": (c_int, [P] * 7 + [c_long, c_int, c_int, P, P]),
     "pdt_ln_fwd_f8": (c_int, [P, P, P, P, P, P, c_int, c_int, c_float, P, P, P, P]),
     "pdt_ln_fwd_f8_blocks": (c_int, [c_int]),
@@ -1474,7 +1478,8 @@ def fp8_settings() -> dict:
     dtype label, so the label cannot drift from the code's defaults)."""
     return {"scaling": os.environ.get("PDT_FP8_SCALING", "delayed"),
             "dgrad": os.environ.get("PDT_FP8_DGRAD", "1") == "1",
-            "attn": os.environ.get("PDT_FP8_ATTN", "1") == "1"}
+            "attn": os.environ.get("PDT_FP8_ATTN", "1") == "1",
+            "wgrad": os.environ.get("PDT_FP8_WGRAD", "1") == "1"}
 
 
 def quantize_fp8(x: torch.Tensor, fmt: int = E4M3):
@@ -1555,6 +1560,60 @@ def gemm_f8(a, b, out, dq_a, dq_b, *, fmt_a=E4M3, bias=None, act=0, aux=None, ad
     return out
 
 
+def _wgrad_f8_launch(lib, dyq, xq, dq_dy, dq_x, dy16, dw, db, v):
+    M, Mo = dyq.shape
+    No = xq.shape[1]
+    kps = c_int(0)
+    splits = lib.pdt_wgrad_f8_plan(M, Mo, No, v, ctypes.byref(kps))
+    slab = torch.empty(lib.pdt_wgrad_f8_workspace(splits, Mo, No), dtype=torch.float32, device=dyq.device)
+    _chk(lib.pdt_linear_wgrad_f8(_p(dyq), _p(xq), _p(dq_dy), _p(dq_x), _p(dy16), _p(slab), _p(dw), _p(db), M, Mo, No,
+                                 Mo, No, splits, kps.value, 0, int(v), _s()), "linear_wgrad_f8")
+
+
+def linear_wgrad_f8(dyq, xq, dq_dy, dq_x, dy16=None, with_bias=False, variant=None):
+    """(dW fp32 [Nout][K], db fp32 [Nout] or None) of nn.Linear from the fp8 codes the
+    data-gradient and forward GEMMs consumed: dyq [M][Nout] e5m2, xq [M][K] e4m3, device
+    dequant scales. db = column sums of the bf16 ``dy16`` (csrc/wgrad_f8.hip)."""
+    M, Nout = dyq.shape
+    K = xq.shape[1]
+    assert dyq.dtype == torch.uint8 and xq.dtype == torch.uint8 and xq.shape[0] == M
+    assert dyq.is_contiguous() and xq.is_contiguous() and Nout % 16 == 0 and K % 16 == 0
+    if with_bias:
+        assert dy16 is not None and dy16.dtype == torch.bfloat16 and dy16.shape == (M, Nout) and dy16.is_contiguous()
+    lib = _load()
+    dw = torch.empty((Nout, K), dtype=torch.float32, device=dyq.device)
+    db = torch.empty(Nout, dtype=torch.float32, device=dyq.device) if with_bias else None
+    if variant is None:
+        key = f"wg8:{M},{Nout},{K}"
+        table = _tuned()
+        if key in table:
+            variant = int(table[key])
+        elif not _tune_allowed():
+            variant = 0
+        else:
+            ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            best, best_t = 0, float("inf")
+            for v in range(lib.pdt_wgrad_f8_num_variants()):
+                _wgrad_f8_launch(lib, dyq, xq, dq_dy, dq_x, None, dw, None, v)
+                ev0.record()
+                for _ in range(3):
+                    _wgrad_f8_launch(lib, dyq, xq, dq_dy, dq_x, None, dw, None, v)
+                ev1.record()
+                ev1.synchronize()
+                t = ev0.elapsed_time(ev1)
+                if t < best_t:
+                    best, best_t = v, t
+            table[key] = best
+            _save_tuned()
+            variant = best
+    _wgrad_f8_launch(lib, dyq, xq, dq_dy, dq_x, dy16 if with_bias else None, dw, db, variant)
+    return dw, db
+
+
+def _fp8_wgrad_on() -> bool:
+    return fp8_settings()["wgrad"]
+
+
 def _quant_act(x2, owner, attr="_pdt_fp8_meta"):
     """e4m3 codes + dequant scale of a bf16 activation under the configured scaling
     (delayed: amax history kept on ``owner``)."""
@@ -1591,7 +1650,14 @@ class _LinearF8(torch.autograd.Function):
         z = torch.empty_like(y) if act == "gelu" else None
         bias = b.float().contiguous() if b is not None else None
         gemm_f8(xq, wq, y, dqx, dqw, bias=bias, act=ACT[act], aux=z, addend=_residual2d(residual, Mrows, Nout))
-        ctx.save_for_backward(x2, w, y if act == "relu" else z)
+        # fp8 weight gradient (needs the e5m2 dY codes of the fp8 data gradient): keep the
+        # e4m3 input codes + their dequant scale instead of the bf16 input
+        ctx.f8w = cfg["dgrad"] and cfg["wgrad"] and K % 16 == 0 and Nout % 16 == 0
+        if ctx.f8w:
+            ctx.xq, ctx.dqx = xq, dqx.clone()  # (the scale slot is rewritten at this layer's next cast)
+            ctx.save_for_backward(None, w, y if act == "relu" else z)
+        else:
+            ctx.save_for_backward(x2, w, y if act == "relu" else z)
         ctx.meta = (shp, act, b is not None)
         ctx.fc = fc
         # e5m2 data-gradient GEMM (default on; PDT_FP8_DGRAD=0 keeps it bf16)
@@ -1612,18 +1678,28 @@ class _LinearF8(torch.autograd.Function):
             _chk(lib.pdt_gelu_bwd(_p(dy2), _p(saved), _p(dz), dz.numel(), _s()), "gelu_bwd")
             dy2 = dz
         Mrows = dy2.shape[0]
+        need = ctx.needs_input_grad
         dx = None
-        if ctx.needs_input_grad[0]:
+        dyq = dqdy = None
+        if ctx.fp8_dgrad and (need[0] or (ctx.f8w and need[1])):
+            dyq, dqdy = _quant_grad(dy2, ctx.fc, "_pdt_fp8_gmeta")
+        if need[0]:
             if ctx.fp8_dgrad:
-                dyq, dqdy = _quant_grad(dy2, ctx.fc, "_pdt_fp8_gmeta")
                 _, wqt, dqw = fp8_weight(w)
                 dx = torch.empty((Mrows, K), dtype=torch.bfloat16, device=dy.device)
                 gemm_f8(dyq, wqt, dx, dqdy, dqw, fmt_a=E5M2)
             else:
                 dx = _linear_dgrad(dy2, w)
             dx = dx.reshape(*shp[:-1], K)
-        dw, db = _linear_grads(dy2, x2, w, has_b and ctx.needs_input_grad[2], ctx.needs_input_grad[1])
-        return dx, dw, db, None, None, (dy if ctx.needs_input_grad[5] else None)
+        want_db = has_b and need[2]
+        if ctx.f8w and need[1]:
+            dw, db = linear_wgrad_f8(dyq, ctx.xq, dqdy, ctx.dqx, dy16=dy2, with_bias=want_db)
+        elif ctx.f8w:
+            dw, db = None, (colsum(dy2, Mrows, Nout) if want_db else None)
+        else:
+            dw, db = _linear_grads(dy2, x2, w, want_db, need[1])
+        ctx.xq = ctx.dqx = None
+        return dx, dw, db, None, None, (dy if need[5] else None)
 
 
 def linear(x, fc: nn.Linear, act=None, fp8=False, residual=None):
@@ -1661,6 +1737,8 @@ class _Mlp(torch.autograd.Function):
         out = torch.empty((Mrows, Nout), dtype=torch.bfloat16, device=dev)
         res = _residual2d(residual, Mrows, Nout)
         bias1, bias2 = b1.float().contiguous(), b2.float().contiguous()
+        cfg = fp8_settings()
+        f8w = fp8 and cfg["dgrad"] and cfg["wgrad"]
         if fp8:
             pre = _prequant(x, mlp.fc1)
             xq, dqx = pre if pre is not None else _quant_act(x2, mlp.fc1)
@@ -1672,37 +1750,55 @@ class _Mlp(torch.autograd.Function):
         else:
             _gemm_bf16(x2, bf16_weight(w1), a, bias=bias1, act="gelu", aux=z)
             _gemm_bf16(a, bf16_weight(w2), out, bias=bias2, addend=res)
-        ctx.save_for_backward(x2, a, z, w1, w2)
+        if f8w:  # fp8 weight gradients: the e4m3 GEMM inputs replace the bf16 ones in the saved state
+            ctx.f8 = (xq, dqx.clone(), aq, dqa.clone())
+            ctx.save_for_backward(None, None, z, w1, w2)
+        else:
+            ctx.f8 = None
+            ctx.save_for_backward(x2, a, z, w1, w2)
         ctx.shp, ctx.fp8, ctx.mlp = shp, fp8, mlp
-        ctx.fp8_dgrad = fp8 and fp8_settings()["dgrad"]
+        ctx.fp8_dgrad = fp8 and cfg["dgrad"]
         return out.reshape(*shp[:-1], Nout)
 
     @staticmethod
     def backward(ctx, g):
         x2, a, z, w1, w2 = ctx.saved_tensors
         need = ctx.needs_input_grad
-        Mrows, K = x2.shape
+        Mrows = z.shape[0]
         Hd, Nout = w1.shape[0], w2.shape[0]
+        K = w1.shape[1]
         g2 = g.reshape(Mrows, Nout).to(torch.bfloat16).contiguous()
         dz = torch.empty((Mrows, Hd), dtype=torch.bfloat16, device=g.device)
+        f8 = ctx.f8
         if ctx.fp8_dgrad:
             gq, dqg = _quant_grad(g2, ctx.mlp.fc2, "_pdt_fp8_gmeta")
             _, w2qt, dqw2 = fp8_weight(w2)
             gemm_f8(gq, w2qt, dz, dqg, dqw2, fmt_a=E5M2, act=3, addend=z)
         else:
             _gemm_bf16(g2, bf16_weight_t(w2), dz, act=3, addend=z)  # dz = (g W2) * gelu'(z)
-        dw2, db2 = _linear_grads(g2, a, w2, need[4], need[3])
+        if f8 is not None:
+            dw2, db2 = linear_wgrad_f8(gq, f8[2], dqg, f8[3], dy16=g2, with_bias=need[4]) if need[3] \
+                else (None, colsum(g2, Mrows, Nout) if need[4] else None)
+        else:
+            dw2, db2 = _linear_grads(g2, a, w2, need[4], need[3])
         dx = None
+        dzq = dqdz = None
+        if ctx.fp8_dgrad and (need[0] or (f8 is not None and need[1])):
+            dzq, dqdz = _quant_grad(dz, ctx.mlp.fc1, "_pdt_fp8_gmeta")
         if need[0]:
             dx = torch.empty((Mrows, K), dtype=torch.bfloat16, device=g.device)
             if ctx.fp8_dgrad:
-                dzq, dqdz = _quant_grad(dz, ctx.mlp.fc1, "_pdt_fp8_gmeta")
                 _, w1qt, dqw1 = fp8_weight(w1)
                 gemm_f8(dzq, w1qt, dx, dqdz, dqw1, fmt_a=E5M2)
             else:
                 _gemm_bf16(dz, bf16_weight_t(w1), dx)
             dx = dx.reshape(ctx.shp)
-        dw1, db1 = _linear_grads(dz, x2, w1, need[2], need[1])
+        if f8 is not None:
+            dw1, db1 = linear_wgrad_f8(dzq, f8[0], dqdz, f8[1], dy16=dz, with_bias=need[2]) if need[1] \
+                else (None, colsum(dz, Mrows, Hd) if need[2] else None)
+        else:
+            dw1, db1 = _linear_grads(dz, x2, w1, need[2], need[1])
+        ctx.f8 = None
         return dx, dw1, db1, dw2, db2, (g if need[5] else None), None, None
 
 

@@ -556,7 +556,10 @@ def test_linear_fp8_autograd():
     y.backward(g)
     yr.backward(g.float())
     assert nrmerr(x.grad, xr.grad) < 1e-1, nrmerr(x.grad, xr.grad)
-    assert nrmerr(fc.weight.grad, fcr.weight.grad) < 3e-2
+    # the weight gradient is fp8 too (e5m2 dY x e4m3 X, csrc/wgrad_f8.hip): e5m2 keeps 2
+    # mantissa bits, so it carries the same ~6 % quantisation error as the data gradient;
+    # the bias gradient sums the bf16 dY
+    assert nrmerr(fc.weight.grad, fcr.weight.grad) < 1e-1, nrmerr(fc.weight.grad, fcr.weight.grad)
     assert nrmerr(fc.bias.grad, fcr.bias.grad) < 3e-2
 
 

@@ -91,9 +91,9 @@ def test_linear_residual_epilogue(fp8):
     y.backward(g)
     yr.backward(g.float())
     assert torch.equal(r.grad, g)  # the residual gradient is dy itself
-    # fp8: the data gradient runs on e5m2 output gradients (2 mantissa bits) by default
+    # fp8: the data and weight gradients run on e5m2 output gradients (2 mantissa bits)
     assert nrmerr(x.grad, xr.grad) < (8e-2 if fp8 else 2e-2), nrmerr(x.grad, xr.grad)
-    assert nrmerr(fc.weight.grad, wr.grad) < 2e-2
+    assert nrmerr(fc.weight.grad, wr.grad) < (8e-2 if fp8 else 2e-2), nrmerr(fc.weight.grad, wr.grad)
     assert nrmerr(fc.bias.grad, g.float().sum((0, 1))) < 1e-4
 
 
@@ -113,6 +113,28 @@ def test_ln_fork_sums_residual_gradient():
     ((xid.float() * gres.float()).sum() + (h.float() * gh.float()).sum()).backward()
     ((xr * gres.float()).sum() + (hr * gh.float()).sum()).backward()
     assert nrmerr(x.grad, xr.grad) < 2e-2, nrmerr(x.grad, xr.grad)
+
+
+@pytest.mark.parametrize("M,Nout,K", [(600, 256, 128), (1576, 2304, 768), (4096, 768, 3072)])
+def test_linear_wgrad_f8_all_variants(M, Nout, K):
+    """fp8 weight gradient (csrc/wgrad_f8.hip, ds_read_b64_tr_b8 + 16x16x128 f8f6f4 MFMA) ==
+    the fp32 product of the dequantised e5m2 dY / e4m3 X codes, every tile variant; bias
+    gradient == column sums of the bf16 dY. M % 128 != 0 exercises the zero-filled tail."""
+    torch.manual_seed(M + K)
+    dy = torch.randn(M, Nout, device="cuda").to(torch.bfloat16)
+    x = torch.randn(M, K, device="cuda").to(torch.bfloat16)
+    dyq, dqdy = no.quantize_fp8(dy, no.E5M2)
+    xq, dqx = no.quantize_fp8(x, no.E4M3)
+    ref = (dyq.view(torch.float8_e5m2).float() * dqdy).t() @ (xq.view(torch.float8_e4m3fn).float() * dqx)
+    lib = no._load()
+    for v in range(lib.pdt_wgrad_f8_num_variants()):
+        dw, db = no.linear_wgrad_f8(dyq, xq, dqdy, dqx, dy16=dy, with_bias=True, variant=v)
+        e = nrmerr(dw, ref)
+        assert e < 1e-4, (v, e)  # fp32 summation order / dequant placement only
+        assert nrmerr(db, dy.float().sum(0)) < 1e-5, v
+    # and the quantisation budget vs the exact bf16 operands (e5m2 keeps 2 mantissa bits)
+    exact = dy.float().t() @ x.float()
+    assert nrmerr(dw, exact) < 0.1, nrmerr(dw, exact)
 
 
 def test_ln_fork_fp8_codes_match_separate_cast():
