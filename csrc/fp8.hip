@@ -188,9 +188,12 @@ __global__ void __launch_bounds__(256) cast_fp8_delayed_kernel(const void* __res
 // history roll, one tiny launch after the cast (a last-block roll inside the
 // cast would need a device-scope release fence per block: an L2 write-back on
 // the multi-XCD part)
+// dq_out (optional): this cast's dequant factor 1/scale in a caller-owned slot that later
+// casts do not overwrite (meta[1] is rewritten by the tensor's next cast)
 template <int FMT>
-__global__ void fp8_meta_roll_kernel(float* __restrict__ meta) {
+__global__ void fp8_meta_roll_kernel(float* __restrict__ meta, float* __restrict__ dq_out) {
   if (threadIdx.x != 0) return;
+  if (dq_out) dq_out[0] = 1.f / meta[0];
   unsigned int* mu = reinterpret_cast<unsigned int*>(meta);
   const float cur = __uint_as_float(mu[2]);
   const int idx = (int)mu[4];
@@ -207,9 +210,11 @@ __global__ void fp8_meta_roll_kernel(float* __restrict__ meta) {
 // the atomicMax slot (the LayerNorm forward's fused fp8 output)
 template <int FMT>
 __global__ void __launch_bounds__(256) fp8_meta_roll_part_kernel(float* __restrict__ meta,
-                                                                const float* __restrict__ partial, int nblk) {
+                                                                const float* __restrict__ partial, int nblk,
+                                                                float* __restrict__ dq_out) {
   const float a = block_amax(partial, nblk);
   if (threadIdx.x != 0) return;
+  if (dq_out) dq_out[0] = 1.f / meta[0];
   unsigned int* mu = reinterpret_cast<unsigned int*>(meta);
   const float cur = fmaxf(a, __uint_as_float(mu[2]));
   const int idx = (int)mu[4];
@@ -267,22 +272,26 @@ PDT_API int pdt_cast_fp8_t(const float* x, int R, int C, const float* partial, v
 PDT_API int pdt_fp8_meta_words() { return 5 + HIST; }
 
 // one-pass delayed-scaling cast; meta must be initialised by pdt_fp8_meta_seed
-PDT_API int pdt_cast_fp8_delayed(const void* x, int bf16, long n, float* meta, int fmt, void* q, hipStream_t st) {
+PDT_API int pdt_cast_fp8_delayed(const void* x, int bf16, long n, float* meta, int fmt, void* q, float* dq_out,
+                                 hipStream_t st) {
   const int nb = nblocks(n);
   uint8_t* qo = (uint8_t*)q;
 #define CD(B_, F_) hipLaunchKernelGGL((cast_fp8_delayed_kernel<B_, F_>), dim3(nb), dim3(256), 0, st, x, n, meta, qo)
   if (bf16) { if (fmt == 0) CD(true, 0); else CD(true, 1); }
   else { if (fmt == 0) CD(false, 0); else CD(false, 1); }
 #undef CD
-  if (fmt == 0) hipLaunchKernelGGL(fp8_meta_roll_kernel<0>, dim3(1), dim3(64), 0, st, meta);
-  else hipLaunchKernelGGL(fp8_meta_roll_kernel<1>, dim3(1), dim3(64), 0, st, meta);
+  if (fmt == 0) hipLaunchKernelGGL(fp8_meta_roll_kernel<0>, dim3(1), dim3(64), 0, st, meta, dq_out);
+  else hipLaunchKernelGGL(fp8_meta_roll_kernel<1>, dim3(1), dim3(64), 0, st, meta, dq_out);
   PDT_RETURN_LAUNCH();
 }
 
 // roll after a fused producer (pdt_ln_fwd_f8): partial[nblk] holds its per-block amaxes
-PDT_API int pdt_fp8_meta_roll_partial(float* meta, const float* partial, int nblk, int fmt, hipStream_t st) {
-  if (fmt == 0) hipLaunchKernelGGL(fp8_meta_roll_part_kernel<0>, dim3(1), dim3(256), 0, st, meta, partial, nblk);
-  else hipLaunchKernelGGL(fp8_meta_roll_part_kernel<1>, dim3(1), dim3(256), 0, st, meta, partial, nblk);
+PDT_API int pdt_fp8_meta_roll_partial(float* meta, const float* partial, int nblk, int fmt, float* dq_out,
+                                      hipStream_t st) {
+  if (fmt == 0)
+    hipLaunchKernelGGL(fp8_meta_roll_part_kernel<0>, dim3(1), dim3(256), 0, st, meta, partial, nblk, dq_out);
+  else
+    hipLaunchKernelGGL(fp8_meta_roll_part_kernel<1>, dim3(1), dim3(256), 0, st, meta, partial, nblk, dq_out);
   PDT_RETURN_LAUNCH();
 }
 

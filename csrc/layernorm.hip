@@ -237,15 +237,16 @@ PDT_API int pdt_ln_fwd(const void* x, const float* g, const float* b, void* y, f
   PDT_RETURN_LAUNCH();
 }
 
-PDT_API int pdt_fp8_meta_roll_partial(float* meta, const float* partial, int nblk, int fmt, hipStream_t st);
+PDT_API int pdt_fp8_meta_roll_partial(float* meta, const float* partial, int nblk, int fmt, float* dq_out,
+                                      hipStream_t st);
 
 PDT_API int pdt_ln_fwd_f8_blocks(int rows) { return (rows + WPB - 1) / WPB; }
 
 // LayerNorm forward that also emits the e4m3 codes of its output for the next fp8 GEMM
 // (delayed scale meta[0]) and rolls that GEMM's amax history; amax_part holds
-// pdt_ln_fwd_f8_blocks(rows) floats.
+// pdt_ln_fwd_f8_blocks(rows) floats; dq_out receives the codes' dequant factor.
 PDT_API int pdt_ln_fwd_f8(const void* x, const float* g, const float* b, void* y, float* mean, float* rstd, int rows,
-                          int D, float eps, void* q, float* meta, float* amax_part, hipStream_t st) {
+                          int D, float eps, void* q, float* meta, float* amax_part, float* dq_out, hipStream_t st) {
   const int nb = (rows + WPB - 1) / WPB;
   dim3 grid(nb), blk(64 * WPB);
 #define LF(CH_) hipLaunchKernelGGL((ln_fwd_kernel<CH_, true>), grid, blk, 0, st, (const u16*)x, g, b, (u16*)y, mean, \
@@ -260,7 +261,7 @@ PDT_API int pdt_ln_fwd_f8(const void* x, const float* g, const float* b, void* y
 #undef LF
   int e = (int)hipGetLastError();
   if (e) return e;
-  return pdt_fp8_meta_roll_partial(meta, amax_part, nb, 0, st);
+  return pdt_fp8_meta_roll_partial(meta, amax_part, nb, 0, dq_out, st);
 }
 
 static int ln_rows_per_block(int rows) {

@@ -30,7 +30,7 @@ namespace {
 typedef int i32x2 __attribute__((ext_vector_type(2)));
 typedef int i32x8 __attribute__((ext_vector_type(8)));
 
-constexpr int BK = 128;  // token rows per k-tile = one MFMA k-step
+constexpr int BK1 = 128;  // token rows per MFMA k-step (a k-tile holds KS of them)
 
 struct WG8Params {
   const uint8_t* dy;    // [M][ldy] e5m2 codes (co contiguous)
@@ -55,14 +55,14 @@ __device__ __forceinline__ int chunk_swz(int r, int c) {
 }
 
 template <int RB>
-__device__ __forceinline__ i32x8 frag8(const char* base, int col0, int lane) {
-  // lane group g = lane/16 -> k rows 32g .. 32g+31; lane j -> row j/2, bytes 8*(j%2) of column block col0
+__device__ __forceinline__ i32x8 frag8(const char* base, int col0, int lane, int krow0) {
+  // lane group g = lane/16 -> k rows krow0 + 32g .. +31; lane j -> row j/2, bytes 8*(j%2) of column block col0
   const int g = lane >> 4, j = lane & 15;
   const int c = col0 >> 4;
   i32x8 out;
 #pragma unroll
   for (int r = 0; r < 4; ++r) {
-    const int row = 32 * g + 8 * r + (j >> 1);
+    const int row = krow0 + 32 * g + 8 * r + (j >> 1);
     const char* a = base + row * RB + (chunk_swz<RB>(row, c) << 4) + 8 * (j & 1);
     i32x2 v = __builtin_amdgcn_ds_read_tr8_b64_v2i32(
         (i32x2 __attribute__((address_space(3)))*)((__attribute__((address_space(3))) char*)(uintptr_t)(uint32_t)(
@@ -73,8 +73,9 @@ __device__ __forceinline__ i32x8 frag8(const char* base, int col0, int lane) {
   return out;
 }
 
-template <int BM, int BN, int NSTAGE, int NTH, int WM, bool BIAS>
+template <int BM, int BN, int NSTAGE, int NTH, int WM, bool BIAS, int KS = 1>
 __global__ void __launch_bounds__(NTH, NTH == 256 ? 2 : 1) wgrad_f8_kernel(WG8Params p) {
+  constexpr int BK = BK1 * KS;
   constexpr int WN = NTH / 64 / WM;
   constexpr int RBA = BM, RBB = BN;  // bytes per LDS row
   constexpr int A_BYTES = BK * RBA, B_BYTES = BK * RBB, STAGE = A_BYTES + B_BYTES;
@@ -141,15 +142,18 @@ __global__ void __launch_bounds__(NTH, NTH == 256 ? 2 : 1) wgrad_f8_kernel(WG8Pa
 
   auto compute = [&](const char* sa) {
     const char* sb = sa + A_BYTES;
-    i32x8 bfr[NI];
 #pragma unroll
-    for (int j = 0; j < NI; ++j) bfr[j] = frag8<RBB>(sb, wn * (BN / WN) + j * 16, lane);
+    for (int ks = 0; ks < KS; ++ks) {
+      i32x8 bfr[NI];
 #pragma unroll
-    for (int i = 0; i < MI; ++i) {
-      const i32x8 af = frag8<RBA>(sa, wm * (BM / WM) + i * 16, lane);
+      for (int j = 0; j < NI; ++j) bfr[j] = frag8<RBB>(sb, wn * (BN / WN) + j * 16, lane, ks * BK1);
 #pragma unroll
-      for (int j = 0; j < NI; ++j)  // X (e4m3) x dY (e5m2): lane holds 4 consecutive c of one co
-        acc[i][j] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(bfr[j], af, acc[i][j], 0, 1, 0, 127, 0, 127);
+      for (int i = 0; i < MI; ++i) {
+        const i32x8 af = frag8<RBA>(sa, wm * (BM / WM) + i * 16, lane, ks * BK1);
+#pragma unroll
+        for (int j = 0; j < NI; ++j)  // X (e4m3) x dY (e5m2): lane holds 4 consecutive c of one co
+          acc[i][j] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(bfr[j], af, acc[i][j], 0, 1, 0, 127, 0, 127);
+      }
     }
   };
 
@@ -233,13 +237,16 @@ __global__ void __launch_bounds__(NTH, NTH == 256 ? 2 : 1) wgrad_f8_kernel(WG8Pa
 }
 
 struct WG8Var {
-  int BM, BN, NS, NTH, target;
+  int BM, BN, NS, NTH, target, KS;
 };
-// 4-wave tiles (2x2 waves, two workgroups per CU) and 8-wave tiles; target = workgroups
-constexpr int WG8_NVAR = 8;
+// 4-wave tiles (2x2 waves, two workgroups per CU) and 8-wave tiles; target = workgroups,
+// KS = MFMA k-steps (128 token rows each) per k-tile / barrier
+constexpr int WG8_NVAR = 13;
 constexpr WG8Var WG8_VARS[WG8_NVAR] = {
-    {128, 128, 2, 256, 1024}, {128, 128, 1, 256, 1024}, {128, 128, 2, 256, 512}, {128, 128, 1, 256, 2048},
-    {256, 128, 2, 512, 512},  {128, 256, 2, 512, 512},  {256, 128, 2, 512, 1024}, {64, 128, 2, 256, 1024},
+    {128, 128, 2, 256, 1024, 1}, {128, 128, 1, 256, 1024, 1}, {128, 128, 2, 256, 512, 1}, {128, 128, 1, 256, 2048, 1},
+    {256, 128, 2, 512, 512, 1},  {128, 256, 2, 512, 512, 1},  {256, 128, 2, 512, 1024, 1}, {64, 128, 2, 256, 1024, 1},
+    {128, 128, 1, 256, 1024, 2}, {128, 128, 1, 256, 512, 2},  {256, 256, 1, 512, 256, 1}, {256, 256, 2, 512, 256, 1},
+    {256, 256, 1, 512, 512, 1},
 };
 
 WG8Var wg8_variant(int v) { return (v < 0 || v >= WG8_NVAR) ? WG8_VARS[0] : WG8_VARS[v]; }
@@ -247,7 +254,12 @@ WG8Var wg8_variant(int v) { return (v < 0 || v >= WG8_NVAR) ? WG8_VARS[0] : WG8_
 template <bool BIAS>
 void launch8(const WG8Var& w, dim3 grid, const WG8Params& p, hipStream_t st) {
 #define L8(a, b, ns, t, wm) hipLaunchKernelGGL((wgrad_f8_kernel<a, b, ns, t, wm, BIAS>), grid, dim3(t), 0, st, p)
-  if (w.NTH == 512) {
+  if (w.KS == 2) {
+    hipLaunchKernelGGL((wgrad_f8_kernel<128, 128, 1, 256, 2, BIAS, 2>), grid, dim3(256), 0, st, p);
+  } else if (w.BM == 256 && w.BN == 256) {
+    if (w.NS == 2) L8(256, 256, 2, 512, 2);
+    else L8(256, 256, 1, 512, 2);
+  } else if (w.NTH == 512) {
     if (w.BM == 256) L8(256, 128, 2, 512, 4);
     else L8(128, 256, 2, 512, 2);
   } else if (w.BM == 64) {
@@ -276,11 +288,12 @@ PDT_API int pdt_wgrad_f8_num_variants() { return WG8_NVAR; }
 PDT_API int pdt_wgrad_f8_plan(int M, int Mo, int No, int variant, int* ktiles_per_split) {
   const WG8Var w = wg8_variant(variant);
   const int tiles = ((Mo + w.BM - 1) / w.BM) * ((No + w.BN - 1) / w.BN);
+  const int BK = BK1 * w.KS;
   const int nk = (M + BK - 1) / BK;
   int splits = (w.target + tiles - 1) / tiles;
   if (splits > nk) splits = nk;
   if (splits < 1) splits = 1;
-  while (splits > 1 && (nk + splits - 1) / splits < 4) --splits;  // >= 4 k-tiles (512 rows) per split
+  while (splits > 1 && (nk + splits - 1) / splits * BK < 512) --splits;  // >= 512 token rows per split
   const int kps = (nk + splits - 1) / splits;
   *ktiles_per_split = kps;
   return (nk + kps - 1) / kps;

@@ -41,9 +41,9 @@ _SIGS = {
     "pdt_wgrad_f8_workspace": (c_long, [c_int, c_int, c_int]),
     "pdt_linear_wgrad_f8": (c_int, [P] * 8 + [c_int] * 9 + [P]),
     "pdt_bn_apply_res_affine": (c_int, [P] * 7 + [c_long, c_int, c_int, P, P]),
-    "pdt_ln_fwd_f8": (c_int, [P, P, P, P, P, P, c_int, c_int, c_float, P, P, P, P]),
+    "pdt_ln_fwd_f8": (c_int, [P, P, P, P, P, P, c_int, c_int, c_float, P, P, P, P, P]),
     "pdt_ln_fwd_f8_blocks": (c_int, [c_int]),
-    "pdt_fp8_meta_roll_partial": (c_int, [P, P, c_int, c_int, P]),
+    "pdt_fp8_meta_roll_partial": (c_int, [P, P, c_int, c_int, P, P]),
     "pdt_ln_bwd_blocks": (c_int, [c_int]),
     "pdt_ln_bwd": (c_int, [P] * 9 + [c_int, c_int, c_int, P, P]),
     "pdt_gelu_bwd": (c_int, [P, P, P, c_long, P]),
@@ -92,7 +92,7 @@ _SIGS = {
     "pdt_cast_fp8": (c_int, [P, c_int, c_long, P, c_int, P, P, P]),
     "pdt_cast_fp8_t": (c_int, [P, c_int, c_int, P, P, P]),
     "pdt_fp8_meta_words": (c_int, []),
-    "pdt_cast_fp8_delayed": (c_int, [P, c_int, c_long, P, c_int, P, P]),
+    "pdt_cast_fp8_delayed": (c_int, [P, c_int, c_long, P, c_int, P, P, P]),
     "pdt_fp8_meta_seed": (c_int, [P, c_long, c_int, P, P]),
     "pdt_attn_bwd": (c_int, [P, P, P, P, P, P, c_int, c_int, c_int, c_float, P]),
     "pdt_lenet_grad_row": (c_int, [c_int]),
@@ -1513,8 +1513,9 @@ def quantize_fp8_delayed(x: torch.Tensor, meta: torch.Tensor | None, fmt: int = 
         _chk(lib.pdt_amax_partial(_p(x), bf, n, _p(part), _s()), "amax")
         _chk(lib.pdt_fp8_meta_seed(_p(part), n, fmt, _p(meta), _s()), "fp8_meta_seed")
     q = torch.empty(x.shape, dtype=torch.uint8, device=x.device)
-    _chk(lib.pdt_cast_fp8_delayed(_p(x), bf, n, _p(meta), fmt, _p(q), _s()), "cast_fp8_delayed")
-    return q, meta[1:2], meta
+    dq = torch.empty(1, dtype=torch.float32, device=x.device)  # this cast's dequant factor (stable)
+    _chk(lib.pdt_cast_fp8_delayed(_p(x), bf, n, _p(meta), fmt, _p(q), _p(dq), _s()), "cast_fp8_delayed")
+    return q, dq, meta
 
 
 _F8W: dict = {}
@@ -1654,7 +1655,7 @@ class _LinearF8(torch.autograd.Function):
         # e4m3 input codes + their dequant scale instead of the bf16 input
         ctx.f8w = cfg["dgrad"] and cfg["wgrad"] and K % 16 == 0 and Nout % 16 == 0
         if ctx.f8w:
-            ctx.xq, ctx.dqx = xq, dqx.clone()  # (the scale slot is rewritten at this layer's next cast)
+            ctx.xq, ctx.dqx = xq, dqx
             ctx.save_for_backward(None, w, y if act == "relu" else z)
         else:
             ctx.save_for_backward(x2, w, y if act == "relu" else z)
@@ -1751,7 +1752,7 @@ class _Mlp(torch.autograd.Function):
             _gemm_bf16(x2, bf16_weight(w1), a, bias=bias1, act="gelu", aux=z)
             _gemm_bf16(a, bf16_weight(w2), out, bias=bias2, addend=res)
         if f8w:  # fp8 weight gradients: the e4m3 GEMM inputs replace the bf16 ones in the saved state
-            ctx.f8 = (xq, dqx.clone(), aq, dqa.clone())
+            ctx.f8 = (xq, dqx, aq, dqa)
             ctx.save_for_backward(None, None, z, w1, w2)
         else:
             ctx.f8 = None
@@ -1879,10 +1880,11 @@ class _LNFork(torch.autograd.Function):
         bf = b.float().contiguous()
         if f8meta is not None:  # also emit the next fp8 GEMM's e4m3 input (delayed scale f8meta)
             q = torch.empty((rows, D), dtype=torch.uint8, device=x.device)
-            part = torch.empty(lib.pdt_ln_fwd_f8_blocks(rows), dtype=torch.float32, device=x.device)
+            part = torch.empty(lib.pdt_ln_fwd_f8_blocks(rows) + 1, dtype=torch.float32, device=x.device)
+            dq = part[-1:]  # the codes' dequant factor (written by the history roll)
             _chk(lib.pdt_ln_fwd_f8(_p(x2), _p(gf), _p(bf), _p(y), _p(stats[0]), _p(stats[1]), rows, D, float(eps),
-                                   _p(q), _p(f8meta), _p(part), _s()), "ln_fwd_f8")
-            f8box.append((q, f8meta[1:2]))
+                                   _p(q), _p(f8meta), _p(part), _p(dq), _s()), "ln_fwd_f8")
+            f8box.append((q, dq))
         else:
             _chk(lib.pdt_ln_fwd(_p(x2), _p(gf), _p(bf), _p(y), _p(stats[0]), _p(stats[1]), rows, D, float(eps),
                                 _s()), "ln_fwd")
