@@ -175,15 +175,32 @@ __global__ void __launch_bounds__(64 * WPB) ln_bwd_kernel(const u16* __restrict_
 }
 
 // out[c] (+)= sum_r part[r][c]  for the two halves (dgamma, dbeta);
-// 256 threads = 64 columns x 4 row groups, combined through LDS.
-__global__ void __launch_bounds__(256) colsum_f32_kernel(const float* __restrict__ part, float* __restrict__ dg,
-                                                         float* __restrict__ db, int R, int D, int accumulate) {
-  __shared__ float sa[4][64], sb[4][64];
+// 1024 threads = 64 columns x 16 row groups, 8 rows per trip with every load issued
+// before the adds (12 workgroups for D = 768: latency, not bandwidth, bounds this),
+// combined through LDS in a fixed order.
+constexpr int CS_RG = 16;
+__global__ void __launch_bounds__(64 * CS_RG) colsum_f32_kernel(const float* __restrict__ part, float* __restrict__ dg,
+                                                                float* __restrict__ db, int R, int D, int accumulate) {
+  __shared__ float sa[CS_RG][64], sb[CS_RG][64];
   const int cl = threadIdx.x & 63, rg = threadIdx.x >> 6;
   const int c = blockIdx.x * 64 + cl;
   float a = 0.f, b = 0.f;
   if (c < D) {
-    for (int r = rg; r < R; r += 4) {
+    int r = rg;
+    for (; r + 7 * CS_RG < R; r += 8 * CS_RG) {
+      float x[8], y[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        x[u] = part[(long)(r + u * CS_RG) * D + c];
+        y[u] = part[(long)(R + r + u * CS_RG) * D + c];
+      }
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        a += x[u];
+        b += y[u];
+      }
+    }
+    for (; r < R; r += CS_RG) {
       a += part[(long)r * D + c];
       b += part[(long)(R + r) * D + c];
     }
@@ -192,8 +209,13 @@ __global__ void __launch_bounds__(256) colsum_f32_kernel(const float* __restrict
   sb[rg][cl] = b;
   __syncthreads();
   if (rg == 0 && c < D) {
-    a = sa[0][cl] + sa[1][cl] + sa[2][cl] + sa[3][cl];
-    b = sb[0][cl] + sb[1][cl] + sb[2][cl] + sb[3][cl];
+    a = 0.f;
+    b = 0.f;
+#pragma unroll
+    for (int g = 0; g < CS_RG; ++g) {
+      a += sa[g][cl];
+      b += sb[g][cl];
+    }
     dg[c] = accumulate ? dg[c] + a : a;
     db[c] = accumulate ? db[c] + b : b;
   }
@@ -296,7 +318,7 @@ PDT_API int pdt_ln_bwd(const void* dy, const void* x, const float* g, const floa
   }
   int e = (int)hipGetLastError();
   if (e) return e;
-  hipLaunchKernelGGL(colsum_f32_kernel, dim3((D + 63) / 64), dim3(256), 0, st, part, dg, db, blocks, D,
+  hipLaunchKernelGGL(colsum_f32_kernel, dim3((D + 63) / 64), dim3(64 * CS_RG), 0, st, part, dg, db, blocks, D,
                      accumulate);
   PDT_RETURN_LAUNCH();
 }

@@ -73,8 +73,20 @@ __device__ __forceinline__ i32x8 frag8(const char* base, int col0, int lane, int
   return out;
 }
 
-template <int BM, int BN, int NSTAGE, int NTH, int WM, bool BIAS, int KS = 1>
-__global__ void __launch_bounds__(NTH, NTH == 256 ? 2 : 1) wgrad_f8_kernel(WG8Params p) {
+// rows one pass of all waves covers when every lane moves 16 B of RB-byte rows
+constexpr int NW_ROWS(int nth, int rb) { return nth * 16 / rb; }
+
+// zero bytes: the LDS-DMA source for rows past M / columns past Mo, No
+static __device__ __attribute__((aligned(64))) u32x4 wg8_zero_chunk[4];
+
+// GL: tiles go global -> LDS by global_load_lds_dwordx4 (no VGPR staging) on an
+// NSTAGE-deep ring with ONE barrier per k-tile: tile t+NSTAGE-1 is issued right after
+// the barrier that proves every wave finished reading its buffer (tile t-1's), and the
+// counted vmcnt before the barrier retires only tile t's DMA (later tiles stay in
+// flight across it). A wave instruction writes 1 KB of LDS lane-linearly, so the chunk
+// swizzle moves to the source address (the XOR is an involution).
+template <int BM, int BN, int NSTAGE, int NTH, int WM, bool BIAS, int KS = 1, bool GL = false>
+__global__ void __launch_bounds__(NTH, NTH == 256 && !GL ? 2 : 1) wgrad_f8_kernel(WG8Params p) {
   constexpr int BK = BK1 * KS;
   constexpr int WN = NTH / 64 / WM;
   constexpr int RBA = BM, RBB = BN;  // bytes per LDS row
@@ -134,6 +146,31 @@ __global__ void __launch_bounds__(NTH, NTH == 256 ? 2 : 1) wgrad_f8_kernel(WG8Pa
     }
   };
 
+  // GL source mapping: pass i of a wave instruction covers rows i*AROWS + wave*(1024/RB) + lane/(RB/16)
+  auto gl_tile = [&](int kt, int buf) {
+    char* sa = smem + buf * STAGE;
+    char* sb = sa + A_BYTES;
+    const int k0 = kt * BK;
+#pragma unroll
+    for (int i = 0; i < NA; ++i) {
+      const int r = i * AROWS + wave * (1024 / RBA) + lane / ACH;
+      const int c = chunk_swz<RBA>(r, lane % ACH);  // logical chunk stored at this physical slot
+      const int m = k0 + r, co = co0 + c * 16;
+      const void* g = (co < p.Mo && m < p.M) ? (const void*)(p.dy + (size_t)m * p.ldy + co) : (const void*)wg8_zero_chunk;
+      __builtin_amdgcn_global_load_lds(
+          g, (__attribute__((address_space(3))) void*)(sa + (i * AROWS + wave * (1024 / RBA)) * RBA), 16, 0, 0);
+    }
+#pragma unroll
+    for (int i = 0; i < NB; ++i) {
+      const int r = i * BROWS + wave * (1024 / RBB) + lane / BCH;
+      const int c = chunk_swz<RBB>(r, lane % BCH);
+      const int m = k0 + r, tc = tc0 + c * 16;
+      const void* g = (tc < p.No && m < p.M) ? (const void*)(p.x + (size_t)m * p.ldx + tc) : (const void*)wg8_zero_chunk;
+      __builtin_amdgcn_global_load_lds(
+          g, (__attribute__((address_space(3))) void*)(sb + (i * BROWS + wave * (1024 / RBB)) * RBB), 16, 0, 0);
+    }
+  };
+
   f32x4 acc[MI][NI];
 #pragma unroll
   for (int i = 0; i < MI; ++i)
@@ -157,6 +194,25 @@ __global__ void __launch_bounds__(NTH, NTH == 256 ? 2 : 1) wgrad_f8_kernel(WG8Pa
     }
   };
 
+  if constexpr (GL) {
+    static_assert(NSTAGE >= 2 && NSTAGE <= 4 && AROWS == NW_ROWS(NTH, RBA) && BROWS == NW_ROWS(NTH, RBB),
+                  "GL ring shape");
+    const int n = kt_end - kt_begin;
+    for (int t = 0; t < NSTAGE - 1; ++t)
+      if (t < n) gl_tile(kt_begin + t, t);
+    for (int t = 0; t < n; ++t) {
+      if (t + NSTAGE - 2 < n) {  // tiles t+1 .. t+NSTAGE-2 were issued after tile t: leave them in flight
+        asm volatile("s_waitcnt vmcnt(%0)" ::"n"((NSTAGE - 2) * (NA + NB)) : "memory");
+      } else {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+      if (t + NSTAGE - 1 < n) gl_tile(kt_begin + t + NSTAGE - 1, (t + NSTAGE - 1) % NSTAGE);
+      compute(smem + (t % NSTAGE) * STAGE);
+    }
+    __syncthreads();  // before the bias tail reuses LDS
+  } else {
   if (kt_begin < kt_end) {
     load_tile(kt_begin);
     store_tile(0);
@@ -174,6 +230,7 @@ __global__ void __launch_bounds__(NTH, NTH == 256 ? 2 : 1) wgrad_f8_kernel(WG8Pa
       store_tile(0);
       __syncthreads();
     }
+  }
   }
 
   if constexpr (BIAS) {
@@ -237,16 +294,20 @@ __global__ void __launch_bounds__(NTH, NTH == 256 ? 2 : 1) wgrad_f8_kernel(WG8Pa
 }
 
 struct WG8Var {
-  int BM, BN, NS, NTH, target, KS;
+  int BM, BN, NS, NTH, target, KS, GL;
 };
 // 4-wave tiles (2x2 waves, two workgroups per CU) and 8-wave tiles; target = workgroups,
 // KS = MFMA k-steps (128 token rows each) per k-tile / barrier
-constexpr int WG8_NVAR = 13;
+// GL = LDS-DMA ring (NS stages, one workgroup per CU)
+constexpr int WG8_NVAR = 19;
 constexpr WG8Var WG8_VARS[WG8_NVAR] = {
-    {128, 128, 2, 256, 1024, 1}, {128, 128, 1, 256, 1024, 1}, {128, 128, 2, 256, 512, 1}, {128, 128, 1, 256, 2048, 1},
-    {256, 128, 2, 512, 512, 1},  {128, 256, 2, 512, 512, 1},  {256, 128, 2, 512, 1024, 1}, {64, 128, 2, 256, 1024, 1},
-    {128, 128, 1, 256, 1024, 2}, {128, 128, 1, 256, 512, 2},  {256, 256, 1, 512, 256, 1}, {256, 256, 2, 512, 256, 1},
-    {256, 256, 1, 512, 512, 1},
+    {128, 128, 2, 256, 1024, 1, 0}, {128, 128, 1, 256, 1024, 1, 0}, {128, 128, 2, 256, 512, 1, 0},
+    {128, 128, 1, 256, 2048, 1, 0}, {256, 128, 2, 512, 512, 1, 0},  {128, 256, 2, 512, 512, 1, 0},
+    {256, 128, 2, 512, 1024, 1, 0}, {64, 128, 2, 256, 1024, 1, 0},  {128, 128, 1, 256, 1024, 2, 0},
+    {128, 128, 1, 256, 512, 2, 0},  {256, 256, 1, 512, 256, 1, 0},  {256, 256, 2, 512, 256, 1, 0},
+    {256, 256, 1, 512, 512, 1, 0},  {128, 128, 3, 256, 1024, 1, 1}, {128, 128, 4, 256, 1024, 1, 1},
+    {256, 128, 3, 512, 512, 1, 1},  {128, 256, 3, 512, 512, 1, 1},  {256, 128, 3, 512, 1024, 1, 1},
+    {128, 128, 2, 256, 1024, 1, 1},
 };
 
 WG8Var wg8_variant(int v) { return (v < 0 || v >= WG8_NVAR) ? WG8_VARS[0] : WG8_VARS[v]; }
@@ -254,7 +315,19 @@ WG8Var wg8_variant(int v) { return (v < 0 || v >= WG8_NVAR) ? WG8_VARS[0] : WG8_
 template <bool BIAS>
 void launch8(const WG8Var& w, dim3 grid, const WG8Params& p, hipStream_t st) {
 #define L8(a, b, ns, t, wm) hipLaunchKernelGGL((wgrad_f8_kernel<a, b, ns, t, wm, BIAS>), grid, dim3(t), 0, st, p)
-  if (w.KS == 2) {
+#define G8(a, b, ns, t, wm) hipLaunchKernelGGL((wgrad_f8_kernel<a, b, ns, t, wm, BIAS, 1, true>), grid, dim3(t), 0, st, p)
+  if (w.GL) {
+    if (w.NTH == 512) {
+      if (w.BM == 256) G8(256, 128, 3, 512, 4);
+      else G8(128, 256, 3, 512, 2);
+    } else if (w.NS == 4) {
+      G8(128, 128, 4, 256, 2);
+    } else if (w.NS == 3) {
+      G8(128, 128, 3, 256, 2);
+    } else {
+      G8(128, 128, 2, 256, 2);
+    }
+  } else if (w.KS == 2) {
     hipLaunchKernelGGL((wgrad_f8_kernel<128, 128, 1, 256, 2, BIAS, 2>), grid, dim3(256), 0, st, p);
   } else if (w.BM == 256 && w.BN == 256) {
     if (w.NS == 2) L8(256, 256, 2, 512, 2);
@@ -270,6 +343,7 @@ void launch8(const WG8Var& w, dim3 grid, const WG8Params& p, hipStream_t st) {
     L8(128, 128, 1, 256, 2);
   }
 #undef L8
+#undef G8
 }
 
 int reduce_groups8(int splits, int Mo, int No) {
