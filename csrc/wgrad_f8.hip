@@ -299,7 +299,7 @@ struct WG8Var {
 // 4-wave tiles (2x2 waves, two workgroups per CU) and 8-wave tiles; target = workgroups,
 // KS = MFMA k-steps (128 token rows each) per k-tile / barrier
 // GL = LDS-DMA ring (NS stages, one workgroup per CU)
-constexpr int WG8_NVAR = 19;
+constexpr int WG8_NVAR = 21;
 constexpr WG8Var WG8_VARS[WG8_NVAR] = {
     {128, 128, 2, 256, 1024, 1, 0}, {128, 128, 1, 256, 1024, 1, 0}, {128, 128, 2, 256, 512, 1, 0},
     {128, 128, 1, 256, 2048, 1, 0}, {256, 128, 2, 512, 512, 1, 0},  {128, 256, 2, 512, 512, 1, 0},
@@ -307,7 +307,7 @@ constexpr WG8Var WG8_VARS[WG8_NVAR] = {
     {128, 128, 1, 256, 512, 2, 0},  {256, 256, 1, 512, 256, 1, 0},  {256, 256, 2, 512, 256, 1, 0},
     {256, 256, 1, 512, 512, 1, 0},  {128, 128, 3, 256, 1024, 1, 1}, {128, 128, 4, 256, 1024, 1, 1},
     {256, 128, 3, 512, 512, 1, 1},  {128, 256, 3, 512, 512, 1, 1},  {256, 128, 3, 512, 1024, 1, 1},
-    {128, 128, 2, 256, 1024, 1, 1},
+    {128, 128, 2, 256, 1024, 1, 1}, {256, 256, 2, 512, 256, 1, 1},  {256, 256, 2, 512, 512, 1, 1},
 };
 
 WG8Var wg8_variant(int v) { return (v < 0 || v >= WG8_NVAR) ? WG8_VARS[0] : WG8_VARS[v]; }
@@ -317,7 +317,9 @@ void launch8(const WG8Var& w, dim3 grid, const WG8Params& p, hipStream_t st) {
 #define L8(a, b, ns, t, wm) hipLaunchKernelGGL((wgrad_f8_kernel<a, b, ns, t, wm, BIAS>), grid, dim3(t), 0, st, p)
 #define G8(a, b, ns, t, wm) hipLaunchKernelGGL((wgrad_f8_kernel<a, b, ns, t, wm, BIAS, 1, true>), grid, dim3(t), 0, st, p)
   if (w.GL) {
-    if (w.NTH == 512) {
+    if (w.BM == 256 && w.BN == 256) {
+      G8(256, 256, 2, 512, 2);
+    } else if (w.NTH == 512) {
       if (w.BM == 256) G8(256, 128, 3, 512, 4);
       else G8(128, 256, 3, 512, 2);
     } else if (w.NS == 4) {

@@ -1593,17 +1593,18 @@ def linear_wgrad_f8(dyq, xq, dq_dy, dq_x, dy16=None, with_bias=False, variant=No
             variant = 0
         else:
             ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            best, best_t = 0, float("inf")
-            for v in range(lib.pdt_wgrad_f8_num_variants()):
-                _wgrad_f8_launch(lib, dyq, xq, dq_dy, dq_x, None, dw, None, v)
-                ev0.record()
-                for _ in range(3):
+            nv = lib.pdt_wgrad_f8_num_variants()
+            times = [float("inf")] * nv
+            for _ in range(2):  # two interleaved rounds, best of each: the variants are within ~10 %
+                for v in range(nv):
                     _wgrad_f8_launch(lib, dyq, xq, dq_dy, dq_x, None, dw, None, v)
-                ev1.record()
-                ev1.synchronize()
-                t = ev0.elapsed_time(ev1)
-                if t < best_t:
-                    best, best_t = v, t
+                    ev0.record()
+                    for _ in range(3):
+                        _wgrad_f8_launch(lib, dyq, xq, dq_dy, dq_x, None, dw, None, v)
+                    ev1.record()
+                    ev1.synchronize()
+                    times[v] = min(times[v], ev0.elapsed_time(ev1))
+            best = min(range(nv), key=lambda v: times[v])
             table[key] = best
             _save_tuned()
             variant = best
