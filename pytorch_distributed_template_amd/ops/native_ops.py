@@ -239,7 +239,10 @@ def _tuned() -> dict:
     if _TUNED is None:
         import json
         table = {}
-        for path in (_SHIPPED_TUNE_PATH, _TUNE_PATH):
+        # PDT_AUTOTUNE_SHIPPED=0: ignore the shipped table (re-tuning experiments)
+        paths = (_SHIPPED_TUNE_PATH, _TUNE_PATH) if os.environ.get("PDT_AUTOTUNE_SHIPPED", "1") != "0" \
+            else (_TUNE_PATH,)
+        for path in paths:
             try:
                 table.update(json.loads(Path(path).read_text()))
             except Exception:
@@ -308,9 +311,11 @@ NOT_APPLICABLE = -5  # kernel return code: this variant cannot run this geometry
 
 
 def _time_variants(nvar, launch, allowed=None):
-    """Fastest variant id: one warm launch, then the best of two 3-launch HIP-event trials."""
-    best, best_t = -1, float("inf")
+    """Fastest variant id: one warm launch each, then two interleaved rounds over all
+    variants of a 3-launch HIP-event trial, best trial per variant (interleaving keeps a
+    clock / cache transient from favouring whichever variants happen to run first)."""
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    cand = []
     for v in range(nvar):
         if allowed is not None and v not in allowed:
             continue
@@ -318,17 +323,19 @@ def _time_variants(nvar, launch, allowed=None):
         if rc == NOT_APPLICABLE:  # e.g. the streaming 1x1 kernel on a 3x3 geometry
             continue
         _chk(rc, f"tune variant {v}")
-        t = float("inf")
-        for _ in range(2):
+        cand.append(v)
+    if not cand:
+        return -1
+    best_t = {v: float("inf") for v in cand}
+    for _ in range(2):
+        for v in cand:
             ev0.record()
             for _ in range(3):
                 launch(v)
             ev1.record()
             ev1.synchronize()
-            t = min(t, ev0.elapsed_time(ev1))
-        if t < best_t:
-            best, best_t = v, t
-    return best
+            best_t[v] = min(best_t[v], ev0.elapsed_time(ev1))
+    return min(cand, key=lambda v: best_t[v])
 
 
 def _autotune(key, nvar, launch, default=0):
@@ -480,18 +487,8 @@ def conv_wgrad(dy, x, out, *, scale=1.0, accumulate=False, variant=None, bias_ou
         elif not _tune_allowed():
             variant = -1
         else:
-            ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            best, best_t = -1, float("inf")
-            for v in range(lib.pdt_wgrad_num_variants()):
-                _wgrad_launch(lib, dy, x, out, v, scale, False, a)
-                ev0.record()
-                for _ in range(3):
-                    _wgrad_launch(lib, dy, x, out, v, scale, False, a)
-                ev1.record()
-                ev1.synchronize()
-                t = ev0.elapsed_time(ev1)
-                if t < best_t:
-                    best, best_t = v, t
+            best = _time_variants(lib.pdt_wgrad_num_variants(),
+                                  lambda v: _wgrad_launch(lib, dy, x, out, v, scale, False, a) or 0)
             table[key] = best
             _save_tuned()
             variant = best
@@ -1592,19 +1589,8 @@ def linear_wgrad_f8(dyq, xq, dq_dy, dq_x, dy16=None, with_bias=False, variant=No
         elif not _tune_allowed():
             variant = 0
         else:
-            ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            nv = lib.pdt_wgrad_f8_num_variants()
-            times = [float("inf")] * nv
-            for _ in range(2):  # two interleaved rounds, best of each: the variants are within ~10 %
-                for v in range(nv):
-                    _wgrad_f8_launch(lib, dyq, xq, dq_dy, dq_x, None, dw, None, v)
-                    ev0.record()
-                    for _ in range(3):
-                        _wgrad_f8_launch(lib, dyq, xq, dq_dy, dq_x, None, dw, None, v)
-                    ev1.record()
-                    ev1.synchronize()
-                    times[v] = min(times[v], ev0.elapsed_time(ev1))
-            best = min(range(nv), key=lambda v: times[v])
+            best = _time_variants(lib.pdt_wgrad_f8_num_variants(),
+                                  lambda v: _wgrad_f8_launch(lib, dyq, xq, dq_dy, dq_x, None, dw, None, v) or 0)
             table[key] = best
             _save_tuned()
             variant = best
