@@ -127,7 +127,8 @@ def _dtype_label(args) -> str:
     from pytorch_distributed_template_amd.ops.native_ops import fp8_settings
     c = fp8_settings()
     return (f"fp8(e4m3 fwd GEMMs, {c['scaling']} scaling; {'e5m2' if c['dgrad'] else 'bf16'} dgrad GEMMs; "
-            f"{'fp8' if c['attn'] else 'bf16'} attention; bf16 wgrad)+bf16")
+            f"{'fp8' if c['attn'] else 'bf16'} attention; {'e5m2 x e4m3' if c['dgrad'] and c['wgrad'] else 'bf16'} "
+            f"wgrad GEMMs)+bf16")
 
 
 def allreduce_probe(model, device, world, iters=10):
