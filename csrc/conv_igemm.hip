@@ -327,6 +327,7 @@ static int conv_nt_impl(const void* src, const void* b, void* out, float* stats,
   p.pix = pix > 0 ? pix : Cs;
   p.aux = (u16*)aux;
   p.dq_a = p.dq_b = nullptr;
+  p.q8 = nullptr; p.q8_meta = nullptr; p.q8_part = nullptr; p.q8_fmt = 0; p.q8_only = 0;
   p.bnb = bnb;
   if (bnb.part != nullptr && (stats != nullptr || bias != nullptr || act != 0 || aux != nullptr || ldo != Ncol))
     return -7;  // the fused BN-backward epilogue is for plain (dense-output) data gradients
@@ -386,6 +387,9 @@ PDT_API int pdt_conv_nt_bnb(const void* src, const void* b, void* out, const voi
 // A: [M][lda] fp8 (e4m3 if fmt_a == 0, e5m2 if 1), B: [N][ldb] e4m3, out bf16 [M][ldo],
 // optional bf16 addend [M][ldo] (residual add, or the GELU-backward operand with act 3).
 // K, lda, ldb in BYTES (= elements), multiples of 128 / 16 / 16.
+PDT_API int pdt_fp8_meta_roll_partial(float* meta, const float* partial, int nblk, int fmt, float* dq_out,
+                                      hipStream_t st);
+
 namespace {
 constexpr int NVAR_F8 = 11;
 constexpr int VAR_F8_BM[NVAR_F8] = {128, 128, 256, 128, 64, 128, 256, 128, 256, 128, 256};
@@ -412,9 +416,10 @@ int launch_f8(int v, const NTParams& p, hipStream_t st) {
 
 PDT_API int pdt_gemm_f8_num_variants() { return NVAR_F8; }
 
-PDT_API int pdt_gemm_f8(const void* a, const void* b, void* out, const float* bias, const float* dq_a,
+static int gemm_f8_impl(const void* a, const void* b, void* out, const float* bias, const float* dq_a,
                         const float* dq_b, int M, int N, int K, int lda, int ldb, int ldo, int fmt_a, int act,
-                        void* aux, const void* addend, int variant, hipStream_t stream) {
+                        void* aux, const void* addend, int variant, void* q8, float* q8_meta, float* q8_part,
+                        int q8_fmt, int q8_only, float* q8_dq, hipStream_t stream) {
   if (K % 128 != 0 || lda % 16 != 0 || ldb % 16 != 0 || N % 8 != 0 || ldo % 8 != 0) return -1;
   if (lda != K) return -2;  // rows of A are dense (the gather's source row stride is Cs)
   NTParams p;
@@ -446,5 +451,36 @@ PDT_API int pdt_gemm_f8(const void* a, const void* b, void* out, const float* bi
   p.div_Cs8 = make_fastdiv(K / 16);
   p.div_ntw = make_fastdiv(1);
   const int v = (variant >= 0 && variant < NVAR_F8) ? variant : 1;
-  return fmt_a == 1 ? launch_f8<2>(v, p, stream) : launch_f8<1>(v, p, stream);
+  p.q8 = (uint8_t*)q8;
+  p.q8_meta = q8_meta;
+  p.q8_part = q8_part;
+  p.q8_fmt = q8_fmt;
+  p.q8_only = q8_only;
+  if (q8 != nullptr && v == 7) return -5;  // the direct-store epilogue has no fp8 output (NOT_APPLICABLE)
+  const int rc = fmt_a == 1 ? launch_f8<2>(v, p, stream) : launch_f8<1>(v, p, stream);
+  if (rc || q8 == nullptr) return rc;
+  const int nblk = ((M + VAR_F8_BM[v] - 1) / VAR_F8_BM[v]) * ((N + VAR_F8_BN[v] - 1) / VAR_F8_BN[v]);
+  return pdt_fp8_meta_roll_partial(q8_meta, q8_part, nblk, q8_fmt, q8_dq, stream);
+}
+
+PDT_API int pdt_gemm_f8(const void* a, const void* b, void* out, const float* bias, const float* dq_a,
+                        const float* dq_b, int M, int N, int K, int lda, int ldb, int ldo, int fmt_a, int act,
+                        void* aux, const void* addend, int variant, hipStream_t stream) {
+  return gemm_f8_impl(a, b, out, bias, dq_a, dq_b, M, N, K, lda, ldb, ldo, fmt_a, act, aux, addend, variant, nullptr,
+                      nullptr, nullptr, 0, 0, nullptr, stream);
+}
+
+// floats of amax workspace pdt_gemm_f8_q8 needs (any variant)
+PDT_API long pdt_gemm_f8_q8_part(int M, int N) { return (long)((M + 63) / 64) * ((N + 63) / 64); }
+
+// pdt_gemm_f8 that also emits the fp8 codes (format q8_fmt) of its bf16 output for the next
+// fp8 GEMM with that GEMM's delayed scale (q8_meta[0]), rolls q8_meta's amax history and
+// writes the codes' dequant factor to q8_dq; q8_only = 1 skips the bf16 output.
+PDT_API int pdt_gemm_f8_q8(const void* a, const void* b, void* out, const float* bias, const float* dq_a,
+                           const float* dq_b, int M, int N, int K, int lda, int ldb, int ldo, int fmt_a, int act,
+                           void* aux, const void* addend, int variant, void* q8, float* q8_meta, float* q8_part,
+                           int q8_fmt, int q8_only, float* q8_dq, hipStream_t stream) {
+  if (!q8 || !q8_meta || !q8_part || ldo != N) return -1;
+  return gemm_f8_impl(a, b, out, bias, dq_a, dq_b, M, N, K, lda, ldb, ldo, fmt_a, act, aux, addend, variant, q8,
+                      q8_meta, q8_part, q8_fmt, q8_only, q8_dq, stream);
 }

@@ -51,6 +51,15 @@ struct NTParams {
   const float* dq_b;   // fp8 only: dequant scale of the B operand
   BnbArgs bnb;         // optional: BatchNorm-backward partial sums of the unit this output feeds
   FastDiv div_Wm, div_HWm, div_Cs8, div_ntw;
+  // optional fp8 copy of the final output for the NEXT fp8 GEMM (staged epilogue only):
+  // codes of the bf16-rounded values times q8_meta[0] (its delayed scale), same layout
+  // as out (1 byte / element), and each workgroup's max |value| in q8_part[blockIdx.x]
+  // (pdt_fp8_meta_roll_partial folds those into the amax history afterwards)
+  uint8_t* q8;
+  const float* q8_meta;
+  float* q8_part;
+  int q8_fmt;          // 0 e4m3, 1 e5m2
+  int q8_only;         // 1: the bf16 output itself is not written
 };
 
 constexpr int BK = 64;
@@ -618,11 +627,13 @@ __global__ void __launch_bounds__(NTH, PIPE ? 1 : 2) conv_nt_kernel(NTParams p) 
     }
   };
 
-  auto stage_store = [&](u16* dst, const u16* addend) __attribute__((always_inline)) {
+  auto stage_store = [&](u16* dst, const u16* addend, bool q8) __attribute__((always_inline)) {
     if (DIRECT) {
       direct_store(dst, addend);
       return;
     }
+    const float q8s = q8 ? p.q8_meta[0] : 0.f;
+    float q8max = 0.f;
 #pragma unroll
     for (int i = 0; i < MI; ++i) {
 #pragma unroll
@@ -669,15 +680,47 @@ __global__ void __launch_bounds__(NTH, PIPE ? 1 : 2) conv_nt_kernel(NTParams p) 
             for (int e = 0; e < 4; ++e) v[e] = pack2bf(lo_bf(v[e]) + lo_bf(a[e]), hi_bf(v[e]) + hi_bf(a[e]));
           }
         }
+        if (q8) {
+          float f[8];
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            f[2 * e] = lo_bf(v[e]);
+            f[2 * e + 1] = hi_bf(v[e]);
+          }
+#pragma unroll
+          for (int e = 0; e < 8; ++e) q8max = fmaxf(q8max, fabsf(f[e]));
+          uint2 c8;
+          if (p.q8_fmt == 0) {
+            c8.x = pdt_cvt4_f8<0>(f[0] * q8s, f[1] * q8s, f[2] * q8s, f[3] * q8s);
+            c8.y = pdt_cvt4_f8<0>(f[4] * q8s, f[5] * q8s, f[6] * q8s, f[7] * q8s);
+          } else {
+            c8.x = pdt_cvt4_f8<1>(f[0] * q8s, f[1] * q8s, f[2] * q8s, f[3] * q8s);
+            c8.y = pdt_cvt4_f8<1>(f[4] * q8s, f[5] * q8s, f[6] * q8s, f[7] * q8s);
+          }
+          *reinterpret_cast<uint2*>(p.q8 + orow * p.ldo + col) = c8;
+          if (p.q8_only) continue;
+        }
         u32x4* dp = reinterpret_cast<u32x4*>(dst + orow * p.ldo + col);
         if (p.nt_store) __builtin_nontemporal_store(v, dp);
         else *dp = v;
       }
     }
+    if (q8) {  // workgroup max |value| -> q8_part[blockIdx.x]
+      __shared__ float q8red[NTH / 64];
+      q8max = warp_max(q8max);
+      if ((tid & 63) == 0) q8red[tid >> 6] = q8max;
+      __syncthreads();
+      if (tid == 0) {
+        float m = q8red[0];
+#pragma unroll
+        for (int w = 1; w < NTH / 64; ++w) m = fmaxf(m, q8red[w]);
+        p.q8_part[blockIdx.x] = m;
+      }
+    }
   };
 
   if (p.aux != nullptr) {
-    stage_store(p.aux, nullptr);
+    stage_store(p.aux, nullptr, false);
     if (!DIRECT) __syncthreads();
   }
   if (p.act == 1 || p.act == 2) {
@@ -697,7 +740,7 @@ __global__ void __launch_bounds__(NTH, PIPE ? 1 : 2) conv_nt_kernel(NTParams p) 
           acc[i][j][r] = x;
         }
   }
-  stage_store(p.out, p.addend);
+  stage_store(p.out, p.addend, !DIRECT && p.q8 != nullptr);
 }
 
 template <int BM, int BN, int NS, bool CS64, bool DIRECT, bool GLDS = false, int NTH = 256, int WM = 2, int F8 = 0,

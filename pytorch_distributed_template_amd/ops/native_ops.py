@@ -36,6 +36,8 @@ _SIGS = {
     "pdt_conv_nt": (c_int, [P, P, P, P, P, P, P] + [c_int] * 25 + [P, c_int, c_int, P]),
     "pdt_conv_nt_bnb": (c_int, [P] * 5 + [c_int] * 25 + [P] * 6 + [c_int] * 3 + [P]),
     "pdt_ln_fwd": (c_int, [P, P, P, P, P, P, c_int, c_int, c_float, P]),
+    "pdt_gemm_f8_q8": (c_int, [P] * 6 + [c_int] * 8 + [P, P, c_int, P, P, P, c_int, c_int, P, P]),
+    "pdt_gemm_f8_q8_part": (c_long, [c_int, c_int]),
     "pdt_wgrad_f8_num_variants": (c_int, []),
     "pdt_wgrad_f8_plan": (c_int, [c_int, c_int, c_int, c_int, ctypes.POINTER(c_int)]),
     "pdt_wgrad_f8_workspace": (c_long, [c_int, c_int, c_int]),
@@ -1539,9 +1541,15 @@ def fp8_weight(w: torch.Tensor):
     return val
 
 
-def gemm_f8(a, b, out, dq_a, dq_b, *, fmt_a=E4M3, bias=None, act=0, aux=None, addend=None, variant=None):
+def gemm_f8(a, b, out, dq_a, dq_b, *, fmt_a=E4M3, bias=None, act=0, aux=None, addend=None, variant=None,
+            q8=None):
     """out[M, N] (bf16) = dq_a*dq_b * a[M, K] @ b[N, K]^T (+bias, act) (+ addend); a, b uint8 fp8
-    codes. ``act=3``: GELU backward, out = (a @ b^T) * gelu'(addend)."""
+    codes. ``act=3``: GELU backward, out = (a @ b^T) * gelu'(addend).
+
+    ``q8 = (codes, meta, fmt, only)``: the epilogue also writes the fp8 codes (format fmt) of
+    the output for the NEXT fp8 GEMM with that GEMM's delayed scale ``meta`` and rolls its
+    amax history (no separate quantisation pass); ``only`` skips the bf16 output. Returns
+    the codes' dequant factor (device [1]) in that case, else ``out``."""
     M, K = a.shape
     N = b.shape[0]
     assert a.dtype == torch.uint8 and b.dtype == torch.uint8 and b.shape[1] == K and K % 128 == 0
@@ -1549,13 +1557,28 @@ def gemm_f8(a, b, out, dq_a, dq_b, *, fmt_a=E4M3, bias=None, act=0, aux=None, ad
     lib = _load()
     if addend is not None:
         assert addend.dtype == torch.bfloat16 and addend.numel() == M * N and addend.is_contiguous()
+    if q8 is None:
+        args = lambda v: (_p(a), _p(b), _p(out), _p(bias), _p(dq_a), _p(dq_b), M, N, K, K, K, N, fmt_a, act,  # noqa
+                          _p(aux), _p(addend), v, _s())
+        if variant is None:
+            key = f"f8b:{M},{N},{K},{fmt_a},{act},{int(bias is not None)}"
+            variant = _autotune(key, lib.pdt_gemm_f8_num_variants(), lambda v: lib.pdt_gemm_f8(*args(v)))
+        _chk(lib.pdt_gemm_f8(*args(variant)), "gemm_f8")
+        return out
+    codes, meta, qfmt, only = q8
+    assert codes.dtype == torch.uint8 and codes.numel() == M * N and codes.is_contiguous()
+    part = torch.empty(lib.pdt_gemm_f8_q8_part(M, N) + 1, dtype=torch.float32, device=a.device)
+    dq = part[-1:]
     args = lambda v: (_p(a), _p(b), _p(out), _p(bias), _p(dq_a), _p(dq_b), M, N, K, K, K, N, fmt_a, act,  # noqa
-                      _p(aux), _p(addend), v, _s())
+                      _p(aux), _p(addend), v, _p(codes), _p(meta), _p(part), int(qfmt), int(only), _p(dq), _s())
     if variant is None:
-        key = f"f8b:{M},{N},{K},{fmt_a},{act},{int(bias is not None)}"
-        variant = _autotune(key, lib.pdt_gemm_f8_num_variants(), lambda v: lib.pdt_gemm_f8(*args(v)))
-    _chk(lib.pdt_gemm_f8(*args(variant)), "gemm_f8")
-    return out
+        key = f"f8b:{M},{N},{K},{fmt_a},{act},{int(bias is not None)},q{qfmt}{int(only)}"
+        # (tuning launches roll the history too: tune on a scratch copy of the state)
+        scratch = meta.clone()
+        targs = lambda v: args(v)[:17] + (_p(codes), _p(scratch)) + args(v)[19:]  # noqa: E731
+        variant = _autotune(key, lib.pdt_gemm_f8_num_variants(), lambda v: lib.pdt_gemm_f8_q8(*targs(v)))
+    _chk(lib.pdt_gemm_f8_q8(*args(variant)), "gemm_f8_q8")
+    return dq
 
 
 def _wgrad_f8_launch(lib, dyq, xq, dq_dy, dq_x, dy16, dw, db, v):
@@ -1731,8 +1754,14 @@ class _Mlp(torch.autograd.Function):
             pre = _prequant(x, mlp.fc1)
             xq, dqx = pre if pre is not None else _quant_act(x2, mlp.fc1)
             w1q, _, dqw1 = fp8_weight(w1)
-            gemm_f8(xq, w1q, a, dqx, dqw1, bias=bias1, act=ACT["gelu"], aux=z)
-            aq, dqa = _quant_act(a, mlp.fc2)
+            meta2 = getattr(mlp.fc2, "_pdt_fp8_meta", None) if cfg["scaling"] == "delayed" else None
+            if meta2 is not None:  # fc1's epilogue writes fc2's e4m3 input (bf16 a only if a bf16 wgrad needs it)
+                aq = torch.empty((Mrows, Hd), dtype=torch.uint8, device=dev)
+                dqa = gemm_f8(xq, w1q, a, dqx, dqw1, bias=bias1, act=ACT["gelu"], aux=z,
+                              q8=(aq, meta2, E4M3, f8w))
+            else:
+                gemm_f8(xq, w1q, a, dqx, dqw1, bias=bias1, act=ACT["gelu"], aux=z)
+                aq, dqa = _quant_act(a, mlp.fc2)
             w2q, _, dqw2 = fp8_weight(w2)
             gemm_f8(aq, w2q, out, dqa, dqw2, bias=bias2, addend=res)
         else:
@@ -1758,10 +1787,17 @@ class _Mlp(torch.autograd.Function):
         g2 = g.reshape(Mrows, Nout).to(torch.bfloat16).contiguous()
         dz = torch.empty((Mrows, Hd), dtype=torch.bfloat16, device=g.device)
         f8 = ctx.f8
+        dzq = dqdz = None
         if ctx.fp8_dgrad:
             gq, dqg = _quant_grad(g2, ctx.mlp.fc2, "_pdt_fp8_gmeta")
             _, w2qt, dqw2 = fp8_weight(w2)
-            gemm_f8(gq, w2qt, dz, dqg, dqw2, fmt_a=E5M2, act=3, addend=z)
+            gmeta1 = getattr(ctx.mlp.fc1, "_pdt_fp8_gmeta", None) if fp8_settings()["scaling"] == "delayed" \
+                else None
+            if gmeta1 is not None:  # the epilogue also writes fc1's e5m2 output gradient (bf16 dz: bias grad)
+                dzq = torch.empty((Mrows, Hd), dtype=torch.uint8, device=g.device)
+                dqdz = gemm_f8(gq, w2qt, dz, dqg, dqw2, fmt_a=E5M2, act=3, addend=z, q8=(dzq, gmeta1, E5M2, False))
+            else:
+                gemm_f8(gq, w2qt, dz, dqg, dqw2, fmt_a=E5M2, act=3, addend=z)
         else:
             _gemm_bf16(g2, bf16_weight_t(w2), dz, act=3, addend=z)  # dz = (g W2) * gelu'(z)
         if f8 is not None:
@@ -1770,8 +1806,7 @@ class _Mlp(torch.autograd.Function):
         else:
             dw2, db2 = _linear_grads(g2, a, w2, need[4], need[3])
         dx = None
-        dzq = dqdz = None
-        if ctx.fp8_dgrad and (need[0] or (f8 is not None and need[1])):
+        if dzq is None and ctx.fp8_dgrad and (need[0] or (f8 is not None and need[1])):
             dzq, dqdz = _quant_grad(dz, ctx.mlp.fc1, "_pdt_fp8_gmeta")
         if need[0]:
             dx = torch.empty((Mrows, K), dtype=torch.bfloat16, device=g.device)

@@ -137,6 +137,44 @@ def test_linear_wgrad_f8_all_variants(M, Nout, K):
     assert nrmerr(dw, exact) < 0.1, nrmerr(dw, exact)
 
 
+@pytest.mark.parametrize("act,qfmt", [(2, 0), (3, 1), (0, 0)])
+def test_gemm_f8_fp8_output_epilogue(act, qfmt):
+    """gemm_f8(q8=...): the epilogue's fp8 codes, dequant factor and amax-history roll equal
+    the bf16 output followed by the separate delayed-scaling cast, for every variant that
+    supports it (GELU forward -> e4m3, GELU backward -> e5m2, plain)."""
+    torch.manual_seed(40 + act)
+    M, N, K = 1000, 384, 256
+    a8, dqa = no.quantize_fp8(torch.randn(M, K, device="cuda").to(torch.bfloat16), no.E4M3 if act != 3 else no.E5M2)
+    b8, dqb = no.quantize_fp8(torch.randn(N, K, device="cuda").to(torch.bfloat16) * 0.1, no.E4M3)
+    fmt_a = no.E5M2 if act == 3 else no.E4M3
+    z = torch.randn(M, N, device="cuda").to(torch.bfloat16)
+    bias = torch.randn(N, device="cuda") if act == 2 else None
+    kw = dict(fmt_a=fmt_a, bias=bias, act=act, addend=z if act == 3 else None,
+              aux=torch.empty(M, N, dtype=torch.bfloat16, device="cuda") if act == 2 else None)
+    _, _, meta0 = no.quantize_fp8_delayed(torch.randn(M, N, device="cuda").to(torch.bfloat16), None, qfmt)
+    lib = no._load()
+    for v in range(lib.pdt_gemm_f8_num_variants()):
+        out = torch.empty(M, N, dtype=torch.bfloat16, device="cuda")
+        no.gemm_f8(a8, b8, out, dqa, dqb, variant=v, **kw)
+        q_ref, dq_ref, meta_ref = no.quantize_fp8_delayed(out, meta0.clone(), qfmt)
+        out2 = torch.empty_like(out)
+        codes = torch.empty(M, N, dtype=torch.uint8, device="cuda")
+        meta = meta0.clone()
+        part = torch.empty(lib.pdt_gemm_f8_q8_part(M, N) + 1, device="cuda")
+        args = (no._p(a8), no._p(b8), no._p(out2), no._p(bias), no._p(dqa), no._p(dqb), M, N, K, K, K, N, fmt_a, act,
+                no._p(kw["aux"]), no._p(kw["addend"]), v, no._p(codes), no._p(meta), no._p(part), qfmt, 0,
+                no._p(part[-1:]), no._s())
+        rc = lib.pdt_gemm_f8_q8(*args)
+        if rc == no.NOT_APPLICABLE:
+            continue
+        assert rc == 0, (v, rc)
+        torch.cuda.synchronize()
+        assert torch.equal(out2, out), v
+        assert torch.equal(codes, q_ref), (v, (codes != q_ref).sum().item())
+        assert torch.equal(part[-1:], dq_ref), v
+        assert torch.equal(meta, meta_ref), v
+
+
 def test_ln_fork_fp8_codes_match_separate_cast():
     """pdt_ln_fwd_f8: same e4m3 codes, dq and amax-history roll as LayerNorm followed by
     the delayed-scaling cast (rows % 4 != 0 exercises the idle-wave path)."""
