@@ -99,15 +99,24 @@ __global__ void __launch_bounds__(64 * WPB) ln_fwd_kernel(const u16* __restrict_
   }
 }
 
-template <int CH>
+// F8: also write the e5m2 codes of dx (bf16-rounded) with the delayed scale q8_meta[0]
+// of the fp8 GEMM that consumes this gradient, and the block's max |dx| to
+// q8_part[blockIdx.x] (the e5m2 quantisation pass of that GEMM folded in here).
+template <int CH, bool F8 = false>
 __global__ void __launch_bounds__(64 * WPB) ln_bwd_kernel(const u16* __restrict__ dy, const u16* __restrict__ x,
                                                           const float* __restrict__ g,
                                                           const float* __restrict__ mean_in,
                                                           const float* __restrict__ rstd_in, u16* __restrict__ dx,
                                                           float* __restrict__ part, int rows, int rows_per_block,
-                                                          const u16* __restrict__ addend) {
+                                                          const u16* __restrict__ addend,
+                                                          uint8_t* __restrict__ q8 = nullptr,
+                                                          const float* __restrict__ q8_meta = nullptr,
+                                                          float* __restrict__ q8_part = nullptr) {
   constexpr int D = 256 * CH;
   __shared__ float red[2][WPB][D];
+  __shared__ float q8red[WPB];
+  float q8max = 0.f;
+  const float q8s = F8 ? q8_meta[0] : 0.f;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   float dg[CH][4], db[CH][4];
 #pragma unroll
@@ -152,7 +161,21 @@ __global__ void __launch_bounds__(64 * WPB) ln_bwd_kernel(const u16* __restrict_
         for (int e = 0; e < 4; ++e) o[e] += ad[c][e];
       }
       st4(dx + (long)row * D + (c * 64 + lane) * 4, o);
+      if (F8) {
+        float r[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          r[e] = bf2f(f2bf(o[e]));  // quantise exactly what the bf16 gradient holds
+          q8max = fmaxf(q8max, fabsf(r[e]));
+        }
+        *reinterpret_cast<uint32_t*>(q8 + (long)row * D + (c * 64 + lane) * 4) =
+            pdt_cvt4_f8<1>(r[0] * q8s, r[1] * q8s, r[2] * q8s, r[3] * q8s);
+      }
     }
+  }
+  if (F8) {
+    q8max = warp_max(q8max);
+    if (lane == 0) q8red[w] = q8max;
   }
 #pragma unroll
   for (int c = 0; c < CH; ++c)
@@ -171,6 +194,12 @@ __global__ void __launch_bounds__(64 * WPB) ln_bwd_kernel(const u16* __restrict_
     }
     part[(long)blockIdx.x * D + col] = a;
     part[(long)(gridDim.x + blockIdx.x) * D + col] = bsum;
+  }
+  if (F8 && threadIdx.x == 0) {  // q8red was written before the barrier above
+    float m = q8red[0];
+#pragma unroll
+    for (int k = 1; k < WPB; ++k) m = fmaxf(m, q8red[k]);
+    q8_part[blockIdx.x] = m;
   }
 }
 
@@ -321,6 +350,36 @@ PDT_API int pdt_ln_bwd(const void* dy, const void* x, const float* g, const floa
   hipLaunchKernelGGL(colsum_f32_kernel, dim3((D + 63) / 64), dim3(64 * CS_RG), 0, st, part, dg, db, blocks, D,
                      accumulate);
   PDT_RETURN_LAUNCH();
+}
+
+// LayerNorm backward that also emits the e5m2 codes of dx for the fp8 GEMM consuming that
+// gradient (delayed scale q8_meta[0]), rolls its amax history and writes the codes'
+// dequant factor to q8_dq; q8_part holds pdt_ln_bwd_blocks(rows) floats.
+PDT_API int pdt_ln_bwd_f8(const void* dy, const void* x, const float* g, const float* mean, const float* rstd,
+                          void* dx, float* dg, float* db, float* part, int rows, int D, int accumulate,
+                          const void* addend, void* q8, float* q8_meta, float* q8_part, float* q8_dq, hipStream_t st) {
+  const int blocks = pdt_ln_bwd_blocks(rows);
+  const int rpb = ln_rows_per_block(rows);
+  dim3 grid(blocks), blk(64 * WPB);
+  const u16 *DY = (const u16*)dy, *X = (const u16*)x;
+  u16* DX = (u16*)dx;
+  const u16* AD = (const u16*)addend;
+  uint8_t* Q = (uint8_t*)q8;
+#define LB8(CH_) hipLaunchKernelGGL((ln_bwd_kernel<CH_, true>), grid, blk, 0, st, DY, X, g, mean, rstd, DX, part, rows, \
+                                    rpb, AD, Q, (const float*)q8_meta, q8_part)
+  switch (D) {
+    case 256: LB8(1); break;
+    case 512: LB8(2); break;
+    case 768: LB8(3); break;
+    case 1024: LB8(4); break;
+    default: return -1;
+  }
+#undef LB8
+  int e = (int)hipGetLastError();
+  if (e) return e;
+  hipLaunchKernelGGL(colsum_f32_kernel, dim3((D + 63) / 64), dim3(64 * CS_RG), 0, st, part, dg, db, blocks, D,
+                     accumulate);
+  return pdt_fp8_meta_roll_partial(q8_meta, q8_part, blocks, 1, q8_dq, st);
 }
 
 PDT_API int pdt_gelu_bwd(const void* dy, const void* z, void* dz, long n, hipStream_t st) {

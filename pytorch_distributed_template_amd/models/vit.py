@@ -59,13 +59,15 @@ class Block(nn.Module):
         self.norm2 = nn.LayerNorm(dim, eps=1e-6)
         self.mlp = Mlp(dim, int(dim * mlp_ratio))
 
-    def forward(self, x, fp8=False):
+    def forward(self, x, fp8=False, prev_fc2=None):
         # pre-norm residual block; the residual adds ride the proj / fc2 GEMM epilogues and
         # their gradients are summed inside the LayerNorm backward (fused.ln_fork)
-        # (fp8: the LayerNorm kernels also write the e4m3 inputs of qkv / fc1)
-        x, h = fused.ln_fork(x, self.norm1, self.attn.qkv if fp8 else None)
+        # (fp8: the LayerNorm forward kernels also write the e4m3 inputs of qkv / fc1, and
+        # the LayerNorm backward kernels the e5m2 output gradients of the previous block's
+        # fc2 / this block's proj -- the layers that produced their inputs)
+        x, h = fused.ln_fork(x, self.norm1, self.attn.qkv if fp8 else None, prev_fc2 if fp8 else None)
         x = self.attn(h, fp8=fp8, residual=x)
-        x, h = fused.ln_fork(x, self.norm2, self.mlp.fc1 if fp8 else None)
+        x, h = fused.ln_fork(x, self.norm2, self.mlp.fc1 if fp8 else None, self.attn.proj if fp8 else None)
         return self.mlp(h, fp8=fp8, residual=x)
 
 
@@ -96,8 +98,10 @@ class VisionTransformer(BaseModel):
         B = x.shape[0]
         cls = self.cls_token.to(x.dtype).expand(B, -1, -1)
         x = torch.cat([cls, x], dim=1) + self.pos_embed.to(x.dtype)
+        prev = None
         for blk in self.blocks:
-            x = blk(x, fp8=self.fp8)
+            x = blk(x, fp8=self.fp8, prev_fc2=prev)
+            prev = blk.mlp.fc2
         x = fused.layer_norm(x[:, 0], self.norm)
         return fused.linear(x, self.head)
 

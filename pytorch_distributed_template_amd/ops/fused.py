@@ -153,14 +153,15 @@ def layer_norm(x, ln: nn.LayerNorm):
     return ln(x)
 
 
-def ln_fork(x, ln: nn.LayerNorm, fp8_for: nn.Linear | None = None):
+def ln_fork(x, ln: nn.LayerNorm, fp8_for: nn.Linear | None = None, grad_fp8_for: nn.Linear | None = None):
     """(x, ln(x)) for a pre-norm residual block. Native: the residual gradient of x
     and the normalised branch's gradient are summed inside LayerNorm's backward;
     ``fp8_for`` (the fp8 layer consuming ln(x)) lets the LayerNorm kernel emit that
-    layer's e4m3 input directly."""
+    layer's e4m3 input directly, and ``grad_fp8_for`` (the fp8 layer that produced x) its
+    e5m2 output gradient in the backward."""
     if _use_native(x):
         from . import native_ops
-        return native_ops.ln_fork(x, ln, fp8_for)
+        return native_ops.ln_fork(x, ln, fp8_for, grad_fp8_for)
     return x, ln(x)
 
 

@@ -38,6 +38,7 @@ _SIGS = {
     "pdt_ln_fwd": (c_int, [P, P, P, P, P, P, c_int, c_int, c_float, P]),
     "pdt_gemm_f8_q8": (c_int, [P] * 6 + [c_int] * 8 + [P, P, c_int, P, P, P, c_int, c_int, P, P]),
     "pdt_gemm_f8_q8_part": (c_long, [c_int, c_int]),
+    "pdt_ln_bwd_f8": (c_int, [P] * 9 + [c_int, c_int, c_int] + [P] * 6),
     "pdt_wgrad_f8_num_variants": (c_int, []),
     "pdt_wgrad_f8_plan": (c_int, [c_int, c_int, c_int, c_int, ctypes.POINTER(c_int)]),
     "pdt_wgrad_f8_workspace": (c_long, [c_int, c_int, c_int]),
@@ -1635,10 +1636,15 @@ def _quant_act(x2, owner, attr="_pdt_fp8_meta"):
     return q, dq
 
 
-def _quant_grad(g2, owner, attr):
+def _quant_grad(g2, owner, attr, src=None):
     """e5m2 codes + dequant scale of an output gradient for the fp8 data-gradient GEMM.
     Delayed scaling (the default) is one fused cast+amax pass with the history kept on
-    ``owner``; current scaling needs a separate amax pass over the gradient first."""
+    ``owner``; current scaling needs a separate amax pass over the gradient first.
+    ``src``: the gradient tensor as received -- if its producer (the LayerNorm backward,
+    ``ln_fork(grad_fp8_for=owner)``) already wrote the codes, they are used as they are."""
+    pre = getattr(src, "_pdt_f8g", None) if src is not None else None
+    if pre is not None and pre[2] is owner:
+        return pre[0].view(g2.shape), pre[1]
     if fp8_settings()["scaling"] == "current":
         return quantize_fp8(g2, E5M2)
     q, dq, meta = quantize_fp8_delayed(g2, getattr(owner, attr, None), E5M2)
@@ -1693,7 +1699,7 @@ class _LinearF8(torch.autograd.Function):
         dx = None
         dyq = dqdy = None
         if ctx.fp8_dgrad and (need[0] or (ctx.f8w and need[1])):
-            dyq, dqdy = _quant_grad(dy2, ctx.fc, "_pdt_fp8_gmeta")
+            dyq, dqdy = _quant_grad(dy2, ctx.fc, "_pdt_fp8_gmeta", src=dy if act is None else None)
         if need[0]:
             if ctx.fp8_dgrad:
                 _, wqt, dqw = fp8_weight(w)
@@ -1789,7 +1795,7 @@ class _Mlp(torch.autograd.Function):
         f8 = ctx.f8
         dzq = dqdz = None
         if ctx.fp8_dgrad:
-            gq, dqg = _quant_grad(g2, ctx.mlp.fc2, "_pdt_fp8_gmeta")
+            gq, dqg = _quant_grad(g2, ctx.mlp.fc2, "_pdt_fp8_gmeta", src=g)
             _, w2qt, dqw2 = fp8_weight(w2)
             gmeta1 = getattr(ctx.mlp.fc1, "_pdt_fp8_gmeta", None) if fp8_settings()["scaling"] == "delayed" \
                 else None
@@ -1890,7 +1896,7 @@ class _LNFork(torch.autograd.Function):
     the LayerNorm backward kernel (no add pass)."""
 
     @staticmethod
-    def forward(ctx, x, g, b, eps, f8meta, f8box):
+    def forward(ctx, x, g, b, eps, f8meta, f8box, grad_owner):
         shp = x.shape
         D = shp[-1]
         x2 = x.reshape(-1, D).contiguous()
@@ -1912,6 +1918,7 @@ class _LNFork(torch.autograd.Function):
                                 _s()), "ln_fwd")
         ctx.save_for_backward(x2, gf, stats)
         ctx.shp = shp
+        ctx.grad_owner = grad_owner
         return x.view_as(x), y.reshape(shp)
 
     @staticmethod
@@ -1929,19 +1936,34 @@ class _LNFork(torch.autograd.Function):
         part = torch.empty(2 * blocks * D, dtype=torch.float32, device=dev)
         dg = torch.empty(D, dtype=torch.float32, device=dev)
         db = torch.empty(D, dtype=torch.float32, device=dev)
+        owner = ctx.grad_owner
+        gmeta = getattr(owner, "_pdt_fp8_gmeta", None) if owner is not None else None
+        if gmeta is not None and fp8_settings()["scaling"] == "delayed":
+            # also the e5m2 codes of dx for the fp8 GEMM that consumes this gradient
+            codes = torch.empty((rows, D), dtype=torch.uint8, device=dev)
+            qpart = torch.empty(blocks + 1, dtype=torch.float32, device=dev)
+            dq = qpart[-1:]
+            _chk(lib.pdt_ln_bwd_f8(_p(dy2), _p(x2), _p(gf), _p(stats[0]), _p(stats[1]), _p(dx), _p(dg), _p(db),
+                                   _p(part), rows, D, 0, _p(add), _p(codes), _p(gmeta), _p(qpart), _p(dq), _s()),
+                 "ln_bwd_f8")
+            out = dx.reshape(ctx.shp)
+            out._pdt_f8g = (codes, dq, owner)
+            return out, dg, db, None, None, None, None
         _chk(lib.pdt_ln_bwd(_p(dy2), _p(x2), _p(gf), _p(stats[0]), _p(stats[1]), _p(dx), _p(dg), _p(db), _p(part),
                             rows, D, 0, _p(add), _s()), "ln_bwd")
-        return dx.reshape(ctx.shp), dg, db, None, None, None
+        return dx.reshape(ctx.shp), dg, db, None, None, None, None
 
 
-def ln_fork(x, ln, fp8_for=None):
+def ln_fork(x, ln, fp8_for=None, grad_fp8_for=None):
     """(x, ln(x)) with the residual gradient summed in LayerNorm's backward (see _LNFork).
 
     ``fp8_for``: the nn.Linear that consumes ln(x) in fp8. Under delayed scaling (once
     that layer's amax history exists) the LayerNorm kernel also writes the e4m3 codes
     of its output with the layer's scale and rolls its history, and the codes ride on
     the returned tensor (``_pdt_f8``) for the fp8 GEMM to pick up -- no separate
-    quantisation pass over the activation."""
+    quantisation pass over the activation. ``grad_fp8_for``: the fp8 layer whose OUTPUT
+    gradient is this fork's input gradient (the residual-stream producer): the LayerNorm
+    backward then also writes that layer's e5m2 gradient codes (``_pdt_f8g``)."""
     D = ln.normalized_shape[-1]
     if (len(ln.normalized_shape) != 1 or D not in (256, 512, 768, 1024) or not ln.elementwise_affine
             or x.dtype != torch.bfloat16):
@@ -1950,7 +1972,9 @@ def ln_fork(x, ln, fp8_for=None):
     if fp8_for is not None and fp8_settings()["scaling"] == "delayed" and D % 128 == 0:
         meta = getattr(fp8_for, "_pdt_fp8_meta", None)
     box: list = []
-    xo, h = _LNFork.apply(x, ln.weight, ln.bias, ln.eps, meta, box)
+    if os.environ.get("PDT_FP8_LN_GRAD", "1") == "0":
+        grad_fp8_for = None
+    xo, h = _LNFork.apply(x, ln.weight, ln.bias, ln.eps, meta, box, grad_fp8_for)
     if box:
         h._pdt_f8 = (box[0][0], box[0][1], fp8_for)
     return xo, h

@@ -200,6 +200,45 @@ def test_ln_fork_fp8_codes_match_separate_cast():
     assert torch.equal(meta1, meta_ref), (meta1, meta_ref)
 
 
+def test_ln_fork_backward_e5m2_codes_match_separate_cast():
+    """pdt_ln_bwd_f8: the e5m2 codes of dx riding on the gradient (for the fp8 layer that
+    produced the fork's input) equal the delayed-scaling cast of that gradient."""
+    torch.manual_seed(28)
+    ln = nn.LayerNorm(768, eps=1e-6).cuda()
+    owner = nn.Linear(768, 768).cuda()
+    no._quant_grad(torch.randn(394, 768, device="cuda").to(torch.bfloat16), owner, "_pdt_fp8_gmeta")  # seed
+    meta0 = owner._pdt_fp8_gmeta.clone()
+    captured = []
+
+    class Cap(torch.autograd.Function):
+        @staticmethod
+        def forward(ctx, t):
+            return t.view_as(t)
+
+        @staticmethod
+        def backward(ctx, g):
+            captured.append(g)
+            return g
+
+    x = torch.randn(2, 197, 768, device="cuda").to(torch.bfloat16).requires_grad_(True)
+    xid, h = no.ln_fork(Cap.apply(x), ln, grad_fp8_for=owner)
+    gh = torch.randn_like(h)
+    gres = torch.randn_like(h)
+    ((xid.float() * gres.float()).sum() + (h.float() * gh.float()).sum()).backward()
+    g = captured[0]
+    assert hasattr(g, "_pdt_f8g") and g._pdt_f8g[2] is owner
+    q_ref, dq_ref, meta_ref = no.quantize_fp8_delayed(g.reshape(-1, 768), meta0.clone(), no.E5M2)
+    torch.cuda.synchronize()
+    assert torch.equal(g._pdt_f8g[0].view(-1, 768), q_ref)
+    assert torch.equal(g._pdt_f8g[1], dq_ref)
+    assert torch.equal(owner._pdt_fp8_gmeta, meta_ref)
+    # and the gradient itself is the plain LayerNorm-fork gradient
+    x2 = x.detach().clone().requires_grad_(True)
+    xid2, h2 = no.ln_fork(x2, ln)
+    ((xid2.float() * gres.float()).sum() + (h2.float() * gh.float()).sum()).backward()
+    assert torch.equal(x.grad, x2.grad)
+
+
 def test_vit_fp8_steps_track_torch_fp32():
     """2-block fp8 ViT, three forward/backward passes (the first seeds the delayed-scaling
     histories; the later ones take the LayerNorm-fused e4m3 inputs and delayed e5m2
