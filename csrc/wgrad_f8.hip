@@ -46,12 +46,18 @@ struct WG8Params {
 };
 
 // physical 16-B chunk of logical chunk c in row r of a RB-byte LDS row
+// The 8 rows one 16-lane group reads get distinct bank groups from (r / WRAP); lane
+// groups g and g+1 (k rows 32 apart, serviced together) are moved to the other half of
+// the row's chunks by bit HB (the counter profile showed ~1.7 conflict cycles per LDS
+// instruction without it).
 template <int RB>
 __device__ __forceinline__ int chunk_swz(int r, int c) {
   constexpr int WRAP = RB >= 256 ? 1 : 256 / RB;  // rows per 256-B bank period
   constexpr int NCH = RB / 16;
   constexpr int MSK = (NCH < 8 ? NCH : 8) - 1;
-  return c ^ ((r / WRAP) & MSK);
+  constexpr int HB = 8 / WRAP;                      // first chunk bit one group's rows do not use
+  static_assert(HB < NCH, "swizzle bits");
+  return c ^ ((r / WRAP) & MSK) ^ (((r >> 5) & 1) * HB);
 }
 
 template <int RB>
