@@ -107,13 +107,17 @@ __global__ void __launch_bounds__(256) cast_fp8_kernel(const void* __restrict__ 
   }
 }
 
-// [R][C] fp32 -> fp8 [C][R] with the tensor's scale (64x64 tiles, 256 threads)
+// [R][C] fp32 -> fp8 [C][R] with the tensor's scale (64x64 tiles, 256 threads).
+// q_rows (optional): the same codes in [R][C] layout from the same tile (one read of the
+// fp32 weight for both the forward and the data-gradient operand), dq: 1 / scale.
 template <int FMT>
 __global__ void __launch_bounds__(256) cast_fp8_t_kernel(const float* __restrict__ x, int R, int C,
                                                          const float* __restrict__ partial, int nblk,
-                                                         uint8_t* __restrict__ q) {
+                                                         uint8_t* __restrict__ q, uint8_t* __restrict__ q_rows = nullptr,
+                                                         float* __restrict__ dq = nullptr) {
   __shared__ float tile[64][65];
   const float s = scale_from<FMT>(block_amax(partial, nblk));
+  if (dq != nullptr && blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) dq[0] = 1.f / s;
   const int r0 = blockIdx.y * 64, c0 = blockIdx.x * 64;
   const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
   for (int i = ty; i < 64; i += 4) {
@@ -121,6 +125,19 @@ __global__ void __launch_bounds__(256) cast_fp8_t_kernel(const float* __restrict
     tile[i][tx] = (r < R && c < C) ? x[(long)r * C + c] * s : 0.f;
   }
   __syncthreads();
+  if (q_rows != nullptr) {  // [R][C] codes: row r0 + i, 4-byte groups of columns
+    for (int i = threadIdx.x; i < 64 * 16; i += 256) {
+      const int rr = i >> 4, g = (i & 15) * 4;
+      const int r = r0 + rr, c = c0 + g;
+      if (r < R && c + 3 < C) {
+        *reinterpret_cast<uint32_t*>(q_rows + (long)r * C + c) =
+            cvt4<FMT>(tile[rr][g], tile[rr][g + 1], tile[rr][g + 2], tile[rr][g + 3]);
+      } else if (r < R) {
+        for (int e = 0; e < 4 && c + e < C; ++e)
+          q_rows[(long)r * C + c + e] = (uint8_t)(cvt4<FMT>(tile[rr][g + e], 0.f, 0.f, 0.f) & 0xff);
+      }
+    }
+  }
   // out row = c (64 of them), 64 bytes each: thread -> (row, 4-byte group)
   for (int i = threadIdx.x; i < 64 * 16; i += 256) {
     const int oc = i >> 4, g = (i & 15) * 4;
@@ -266,6 +283,17 @@ PDT_API int pdt_cast_fp8_t(const float* x, int R, int C, const float* partial, v
   const int nb = nblocks((long)R * C);
   dim3 grid((C + 63) / 64, (R + 63) / 64);
   hipLaunchKernelGGL(cast_fp8_t_kernel<0>, grid, dim3(256), 0, st, x, R, C, partial, nb, (uint8_t*)q);
+  PDT_RETURN_LAUNCH();
+}
+
+// fp32 [R][C] -> e4m3 [R][C] AND [C][R] in one pass (the weight's forward and data-gradient
+// operands), dq = 1 / scale; the partials must come from pdt_amax_partial over the same values
+PDT_API int pdt_cast_fp8_dual(const float* x, int R, int C, const float* partial, void* q, void* qt, float* dq,
+                              hipStream_t st) {
+  const int nb = nblocks((long)R * C);
+  dim3 grid((C + 63) / 64, (R + 63) / 64);
+  hipLaunchKernelGGL(cast_fp8_t_kernel<0>, grid, dim3(256), 0, st, x, R, C, partial, nb, (uint8_t*)qt, (uint8_t*)q,
+                     dq);
   PDT_RETURN_LAUNCH();
 }
 

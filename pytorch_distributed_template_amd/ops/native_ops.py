@@ -94,6 +94,7 @@ _SIGS = {
     "pdt_amax_partial": (c_int, [P, c_int, c_long, P, P]),
     "pdt_cast_fp8": (c_int, [P, c_int, c_long, P, c_int, P, P, P]),
     "pdt_cast_fp8_t": (c_int, [P, c_int, c_int, P, P, P]),
+    "pdt_cast_fp8_dual": (c_int, [P, c_int, c_int, P, P, P, P, P]),
     "pdt_fp8_meta_words": (c_int, []),
     "pdt_cast_fp8_delayed": (c_int, [P, c_int, c_long, P, c_int, P, P, P]),
     "pdt_fp8_meta_seed": (c_int, [P, c_long, c_int, P, P]),
@@ -1535,8 +1536,8 @@ def fp8_weight(w: torch.Tensor):
     dq = torch.empty(1, dtype=torch.float32, device=w.device)
     st = _s()
     _chk(lib.pdt_amax_partial(_p(src), 0, src.numel(), _p(part), st), "amax")
-    _chk(lib.pdt_cast_fp8(_p(src), 0, src.numel(), _p(part), E4M3, _p(wq), _p(dq), st), "cast_fp8")
-    _chk(lib.pdt_cast_fp8_t(_p(src), N, K, _p(part), _p(wqt), st), "cast_fp8_t")
+    # both layouts (forward [N][K], data gradient [K][N]) from one read of the fp32 weight
+    _chk(lib.pdt_cast_fp8_dual(_p(src), N, K, _p(part), _p(wq), _p(wqt), _p(dq), st), "cast_fp8_dual")
     val = (wq, wqt, dq)
     _F8W[id(w)] = (w._version, w.data_ptr(), val, _weak(w))
     return val
