@@ -66,6 +66,11 @@ struct AttnF8Params {
   int B, T, H;
   long ld, ldo;
   float c;          // softmax scale * log2(e)
+  // optional: e4m3 codes of the (bf16-rounded) output for the next fp8 GEMM (the attention
+  // projection) with its delayed scale q8_meta[0]; per-workgroup max |O| -> q8_part[bh]
+  uint8_t* q8;
+  const float* q8_meta;
+  float* q8_part;
 };
 
 // bf16 K row image: [rows][128 B], chunk c of row r at c ^ ((r >> 1) & 7)
@@ -135,6 +140,7 @@ __global__ void __launch_bounds__(256) attn_fwd_f8_kernel(AttnF8Params p) {
   const int col = lane & 31, hh = lane >> 5;
   const int grp = lane >> 4, i16 = lane & 15;  // 16-lane group of the transposed V reads
   const int nqt = (p.T + 31) / 32;
+  float q8max = 0.f;
   for (int qt = wave; qt < nqt; qt += 4) {
     // ---- Q tile -> e4m3 B fragment: lane (q = col, hh) holds Q[q][32 hh .. 32 hh + 31]
     const int q = qt * 32 + col;
@@ -247,7 +253,8 @@ __global__ void __launch_bounds__(256) attn_fwd_f8_kernel(AttnF8Params p) {
     // o[dt][r] = O^T[d = 32 dt + (r & 3) + 8 (r >> 2) + 4 hh][query q]
     if (q < p.T) {
       const float inv = 1.f / l;
-      u16* orow = p.out + ((long)b * p.T + q) * p.ldo + h * D;
+      const long orow_off = ((long)b * p.T + q) * p.ldo + h * D;
+      u16* orow = p.out + orow_off;
 #pragma unroll
       for (int dt = 0; dt < 2; ++dt)
 #pragma unroll
@@ -256,9 +263,23 @@ __global__ void __launch_bounds__(256) attn_fwd_f8_kernel(AttnF8Params p) {
           w.x = pack2bf(o[dt][4 * g4] * inv, o[dt][4 * g4 + 1] * inv);
           w.y = pack2bf(o[dt][4 * g4 + 2] * inv, o[dt][4 * g4 + 3] * inv);
           *reinterpret_cast<uint2*>(orow + 32 * dt + 8 * g4 + 4 * hh) = w;
+          if (p.q8 != nullptr) {
+            const float s8 = p.q8_meta[0];
+            const float f0 = lo_bf(w.x), f1 = hi_bf(w.x), f2 = lo_bf(w.y), f3 = hi_bf(w.y);
+            q8max = fmaxf(q8max, fmaxf(fmaxf(fabsf(f0), fabsf(f1)), fmaxf(fabsf(f2), fabsf(f3))));
+            *reinterpret_cast<uint32_t*>(p.q8 + orow_off + 32 * dt + 8 * g4 + 4 * hh) =
+                cvt4_e4m3(f0 * s8, f1 * s8, f2 * s8, f3 * s8);
+          }
         }
       if (hh == 0) p.lse[(long)bh * p.T + q] = m + log2f(l);
     }
+  }
+  if (p.q8 != nullptr) {  // workgroup max |O| (all waves reach this after their query tiles)
+    q8max = warp_max(q8max);
+    __syncthreads();
+    if (lane == 0) red[wave] = q8max;
+    __syncthreads();
+    if (tid == 0) p.q8_part[bh] = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
   }
 }
 
@@ -276,6 +297,7 @@ PDT_API int pdt_attn_fwd_f8(const void* qkv, void* out, float* lse, int B, int T
   p.ld = 3L * H * D;
   p.ldo = (long)H * D;
   p.c = scale * 1.4426950408889634f;
+  p.q8 = nullptr; p.q8_meta = nullptr; p.q8_part = nullptr;
   const int nkt = (T + 31) / 32;
   dim3 g(B * H);
 #define F8(N) hipLaunchKernelGGL((attn_fwd_f8_kernel<N, true>), g, dim3(256), 0, st, p)
@@ -293,6 +315,43 @@ PDT_API int pdt_attn_fwd_f8(const void* qkv, void* out, float* lse, int B, int T
   PDT_RETURN_LAUNCH();
 }
 
+PDT_API int pdt_fp8_meta_roll_partial(float* meta, const float* partial, int nblk, int fmt, float* dq_out,
+                                      hipStream_t st);
+
+// pdt_attn_fwd_f8 that also writes the e4m3 codes of O for the projection GEMM (delayed scale
+// q8_meta[0]), rolls that GEMM's amax history (q8_part: B*H floats) and writes the codes'
+// dequant factor to q8_dq
+PDT_API int pdt_attn_fwd_f8_q8(const void* qkv, void* out, float* lse, int B, int T, int H, float scale, void* q8,
+                               float* q8_meta, float* q8_part, float* q8_dq, hipStream_t st) {
+  if (T < 1 || T > 256 || !q8 || !q8_meta || !q8_part) return -1;
+  AttnF8Params p;
+  p.qkv = (const u16*)qkv;
+  p.out = (u16*)out;
+  p.lse = lse;
+  p.B = B; p.T = T; p.H = H;
+  p.ld = 3L * H * D;
+  p.ldo = (long)H * D;
+  p.c = scale * 1.4426950408889634f;
+  p.q8 = (uint8_t*)q8; p.q8_meta = q8_meta; p.q8_part = q8_part;
+  const int nkt = (T + 31) / 32;
+  dim3 g(B * H);
+#define F8(N) hipLaunchKernelGGL((attn_fwd_f8_kernel<N, true>), g, dim3(256), 0, st, p)
+  switch (nkt) {
+    case 1: F8(1); break;
+    case 2: F8(2); break;
+    case 3: F8(3); break;
+    case 4: F8(4); break;
+    case 5: F8(5); break;
+    case 6: F8(6); break;
+    case 7: F8(7); break;
+    default: F8(8); break;
+  }
+#undef F8
+  int e = (int)hipGetLastError();
+  if (e) return e;
+  return pdt_fp8_meta_roll_partial(q8_meta, q8_part, B * H, 0, q8_dq, st);
+}
+
 // the same kernel with a bf16 score GEMM (ViT bf16 forward); -1 when not covered
 PDT_API int pdt_attn_fwd_tiles(const void* qkv, void* out, float* lse, int B, int T, int H, float scale,
                                hipStream_t st) {
@@ -305,6 +364,7 @@ PDT_API int pdt_attn_fwd_tiles(const void* qkv, void* out, float* lse, int B, in
   p.ld = 3L * H * D;
   p.ldo = (long)H * D;
   p.c = scale * 1.4426950408889634f;
+  p.q8 = nullptr; p.q8_meta = nullptr; p.q8_part = nullptr;
   const int nkt = (T + 31) / 32;
   dim3 g(B * H);
 #define BF(N) hipLaunchKernelGGL((attn_fwd_f8_kernel<N, false>), g, dim3(256), 0, st, p)

@@ -37,7 +37,9 @@ class Attention(nn.Module):
 
     def forward(self, x, fp8=False, residual=None):
         qkv = fused.linear(x, self.qkv, fp8=fp8)                          # [B,T,3D]
-        o = fused.qkv_attention(qkv, self.num_heads, fp8=fp8 and _fp8_attn())  # [B,T,D]
+        # (fp8: the attention kernel also writes the projection GEMM's e4m3 input)
+        o = fused.qkv_attention(qkv, self.num_heads, fp8=fp8 and _fp8_attn(),
+                                fp8_for=self.proj if fp8 else None)      # [B,T,D]
         return fused.linear(o, self.proj, fp8=fp8, residual=residual)     # (+ residual in the epilogue)
 
 

@@ -94,6 +94,7 @@ _SIGS = {
     "pdt_amax_partial": (c_int, [P, c_int, c_long, P, P]),
     "pdt_cast_fp8": (c_int, [P, c_int, c_long, P, c_int, P, P, P]),
     "pdt_cast_fp8_t": (c_int, [P, c_int, c_int, P, P, P]),
+    "pdt_attn_fwd_f8_q8": (c_int, [P, P, P, c_int, c_int, c_int, c_float, P, P, P, P, P]),
     "pdt_cast_fp8_dual": (c_int, [P, c_int, c_int, P, P, P, P, P]),
     "pdt_fp8_meta_words": (c_int, []),
     "pdt_cast_fp8_delayed": (c_int, [P, c_int, c_long, P, c_int, P, P, P]),
@@ -2039,14 +2040,21 @@ class _QKVAttention(torch.autograd.Function):
     backward, which writes d(qkv) in the qkv layout (the qkv GEMM's dY)."""
 
     @staticmethod
-    def forward(ctx, qkv, H, fp8=False):
+    def forward(ctx, qkv, H, fp8=False, q8meta=None, box=None):
         B, T, D3 = qkv.shape
         assert D3 == 3 * H * 64 and qkv.dtype == torch.bfloat16, "head_dim must be 64, bf16"
         qkv = qkv.contiguous()
         out = torch.empty((B, T, H * 64), dtype=torch.bfloat16, device=qkv.device)
         lse = torch.empty((B * H, T), dtype=torch.float32, device=qkv.device)
         scale = 64 ** -0.5
-        if fp8 and T <= 256:  # fp8 QK^T (csrc/attention_f8.hip), fp32 softmax, bf16 PV
+        if fp8 and T <= 256 and q8meta is not None:  # + the projection GEMM's e4m3 input
+            codes = torch.empty((B * T, H * 64), dtype=torch.uint8, device=qkv.device)
+            part = torch.empty(B * H + 1, dtype=torch.float32, device=qkv.device)
+            dq = part[-1:]
+            _chk(_load().pdt_attn_fwd_f8_q8(_p(qkv), _p(out), _p(lse), B, T, H, scale, _p(codes), _p(q8meta),
+                                            _p(part), _p(dq), _s()), "attn_fwd_f8_q8")
+            box.append((codes, dq))
+        elif fp8 and T <= 256:  # fp8 QK^T (csrc/attention_f8.hip), fp32 softmax, bf16 PV
             _chk(_load().pdt_attn_fwd_f8(_p(qkv), _p(out), _p(lse), B, T, H, scale, _s()), "attn_fwd_f8")
         elif T <= 256 and os.environ.get("PDT_ATTN_FWD32", "1") == "1":  # 32x32-tile bf16 forward
             _chk(_load().pdt_attn_fwd_tiles(_p(qkv), _p(out), _p(lse), B, T, H, scale, _s()), "attn_fwd_tiles")
@@ -2065,14 +2073,23 @@ class _QKVAttention(torch.autograd.Function):
         dqkv = torch.empty_like(qkv)
         _chk(_load().pdt_attn_bwd(_p(qkv), _p(out), _p(dout), _p(lse), _p(delta), _p(dqkv), B, T, ctx.H,
                                   ctx.scale, _s()), "attn_bwd")
-        return dqkv, None, None
+        return dqkv, None, None, None, None
 
 
-def qkv_attention(qkv, num_heads, fp8=False):
+def qkv_attention(qkv, num_heads, fp8=False, fp8_for=None):
     """softmax(q k^T / 8) v over heads of 64 for a packed [B, T, 3*H*64] qkv. ``fp8``: the
     score GEMM on e4m3 MFMA (per-head / per-tile power-of-two scales, T <= 256); the
-    backward is the bf16 recomputing one either way."""
-    return _QKVAttention.apply(qkv, num_heads, bool(fp8))
+    backward is the bf16 recomputing one either way. ``fp8_for``: the fp8 layer consuming
+    the output (the attention projection): under delayed scaling the kernel also writes
+    its e4m3 input (``_pdt_f8`` on the result, as :func:`ln_fork` does)."""
+    meta = None
+    if fp8 and fp8_for is not None and fp8_settings()["scaling"] == "delayed":
+        meta = getattr(fp8_for, "_pdt_fp8_meta", None)
+    box: list = []
+    out = _QKVAttention.apply(qkv, num_heads, bool(fp8), meta, box)
+    if box:
+        out._pdt_f8 = (box[0][0], box[0][1], fp8_for)
+    return out
 
 
 def attention(q, k, v):

@@ -239,6 +239,28 @@ def test_ln_fork_backward_e5m2_codes_match_separate_cast():
     assert torch.equal(x.grad, x2.grad)
 
 
+def test_attention_fp8_output_codes_match_separate_cast():
+    """pdt_attn_fwd_f8_q8: O unchanged, and the projection's e4m3 input codes / dequant factor /
+    amax-history roll equal the delayed-scaling cast of O."""
+    torch.manual_seed(29)
+    B, T, H = 2, 197, 4
+    qkv = torch.randn(B, T, 3 * H * 64, device="cuda").to(torch.bfloat16)
+    proj = nn.Linear(H * 64, H * 64).cuda()
+    no._quant_act(torch.randn(B * T, H * 64, device="cuda").to(torch.bfloat16), proj)  # seed the history
+    meta0 = proj._pdt_fp8_meta.clone()
+    o = no.qkv_attention(qkv, H, fp8=True, fp8_for=proj)
+    assert hasattr(o, "_pdt_f8") and o._pdt_f8[2] is proj
+    codes, dq = o._pdt_f8[0].clone(), o._pdt_f8[1].clone()
+    meta1 = proj._pdt_fp8_meta.clone()
+    o_ref = no.qkv_attention(qkv, H, fp8=True)
+    assert torch.equal(o, o_ref)
+    q_ref, dq_ref, meta_ref = no.quantize_fp8_delayed(o_ref.reshape(-1, H * 64), meta0.clone(), no.E4M3)
+    torch.cuda.synchronize()
+    assert torch.equal(codes, q_ref)
+    assert torch.equal(dq, dq_ref)
+    assert torch.equal(meta1, meta_ref)
+
+
 def test_vit_fp8_steps_track_torch_fp32():
     """2-block fp8 ViT, three forward/backward passes (the first seeds the delayed-scaling
     histories; the later ones take the LayerNorm-fused e4m3 inputs and delayed e5m2
