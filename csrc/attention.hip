@@ -590,7 +590,34 @@ struct AttnSeqBwdParams {
   int B, T, H;
   long ld, ldo;
   float c, scale;
+  // optional: e5m2 codes of d(qkv) (bf16-rounded, same layout) for the qkv projection's fp8
+  // data / weight gradients, delayed scale q8_meta[0]; per-workgroup max |d(qkv)| ->
+  // q8_part[bh] (dK/dV kernel) and q8_part[B*H + bh] (dQ kernel)
+  uint8_t* q8;
+  const float* q8_meta;
+  float* q8_part;
 };
+
+// 4 bf16 (packed) -> 4 e5m2 codes with scale s (saturating), updating |max|
+__device__ __forceinline__ uint32_t q8_e5m2(uint2 w, float s, float& mx) {
+  const float f0 = lo_bf(w.x), f1 = hi_bf(w.x), f2 = lo_bf(w.y), f3 = hi_bf(w.y);
+  mx = fmaxf(mx, fmaxf(fmaxf(fabsf(f0), fabsf(f1)), fmaxf(fabsf(f2), fabsf(f3))));
+  return pdt_cvt4_f8<1>(f0 * s, f1 * s, f2 * s, f3 * s);
+}
+
+// block max of a per-thread value -> part[slot] (all threads of the block call this)
+__device__ __forceinline__ void q8_block_max(float mx, float* part, long slot, float* red) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  mx = warp_max(mx);
+  __syncthreads();
+  if (lane == 0) red[wave] = mx;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float m = red[0];
+    for (int w = 1; w < nw; ++w) m = fmaxf(m, red[w]);
+    part[slot] = m;
+  }
+}
 
 // dK, dV: one workgroup (8 waves) per (b, h); wave w owns key subtiles w, w+8.
 // Per query subtile u: S = Q K^T (q on the register axis, key on the lane),
@@ -643,6 +670,8 @@ __global__ void __launch_bounds__(512) attn_bwd_dkdv_seq_kernel(AttnSeqBwdParams
   int to[4];
 #pragma unroll
   for (int dt = 0; dt < 4; ++dt) to[dt] = SINGLE ? tr_row_lane_off(lane, dt) : tr_lane_off(lane, dt);
+  __shared__ float q8red[8];
+  float q8max = 0.f;
   __syncthreads();
   for (int kt = wave; kt < NT; kt += 8) {
     const int key = kt * 16 + (lane & 15);
@@ -696,7 +725,8 @@ __global__ void __launch_bounds__(512) attn_bwd_dkdv_seq_kernel(AttnSeqBwdParams
       }
     }
     if (kok) {
-      u16* drow = p.dqkv + ((long)b * p.T + key) * p.ld + h * D;
+      const long roff = ((long)b * p.T + key) * p.ld + h * D;
+      u16* drow = p.dqkv + roff;
 #pragma unroll
       for (int dt = 0; dt < 4; ++dt) {
         uint2 wk, wv;
@@ -706,9 +736,15 @@ __global__ void __launch_bounds__(512) attn_bwd_dkdv_seq_kernel(AttnSeqBwdParams
         wv.y = pack2bf(dv[dt][2], dv[dt][3]);
         *reinterpret_cast<uint2*>(drow + p.H * D + 16 * dt + 4 * g) = wk;
         *reinterpret_cast<uint2*>(drow + 2 * p.H * D + 16 * dt + 4 * g) = wv;
+        if (p.q8 != nullptr) {
+          const float s8 = p.q8_meta[0];
+          *reinterpret_cast<uint32_t*>(p.q8 + roff + p.H * D + 16 * dt + 4 * g) = q8_e5m2(wk, s8, q8max);
+          *reinterpret_cast<uint32_t*>(p.q8 + roff + 2 * p.H * D + 16 * dt + 4 * g) = q8_e5m2(wv, s8, q8max);
+        }
       }
     }
   }
+  if (p.q8 != nullptr) q8_block_max(q8max, p.q8_part, bh, q8red);
 }
 
 // dQ: one workgroup (8 waves) per (b, h); wave w owns query subtiles w, w+8.
@@ -733,6 +769,8 @@ __global__ void __launch_bounds__(512) attn_bwd_dq_seq_kernel(AttnSeqBwdParams p
 #pragma unroll
   for (int dt = 0; dt < 4; ++dt) to[dt] = SINGLE ? tr_row_lane_off(lane, dt) : tr_lane_off(lane, dt);
   const int klast = 16 * (NT - 1) + 4 * g;
+  __shared__ float q8red[8];
+  float q8max = 0.f;
   __syncthreads();
   for (int qs = wave; qs < NT; qs += 8) {
     const int qrow = qs * 16 + (lane & 15);
@@ -782,16 +820,20 @@ __global__ void __launch_bounds__(512) attn_bwd_dq_seq_kernel(AttnSeqBwdParams p
         dq[dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(frag_tr(Kt, to[dt], kp), sf, dq[dt], 0, 0, 0);
     }
     if (qok) {
-      u16* drow = p.dqkv + ((long)b * p.T + qrow) * p.ld + h * D;
+      const long roff = ((long)b * p.T + qrow) * p.ld + h * D;
+      u16* drow = p.dqkv + roff;
 #pragma unroll
       for (int dt = 0; dt < 4; ++dt) {
         uint2 w;
         w.x = pack2bf(dq[dt][0] * p.scale, dq[dt][1] * p.scale);
         w.y = pack2bf(dq[dt][2] * p.scale, dq[dt][3] * p.scale);
         *reinterpret_cast<uint2*>(drow + 16 * dt + 4 * g) = w;
+        if (p.q8 != nullptr)
+          *reinterpret_cast<uint32_t*>(p.q8 + roff + 16 * dt + 4 * g) = q8_e5m2(w, p.q8_meta[0], q8max);
       }
     }
   }
+  if (p.q8 != nullptr) q8_block_max(q8max, p.q8_part, (long)p.B * p.H + bh, q8red);
 }
 
 }  // namespace
@@ -867,11 +909,37 @@ PDT_API int pdt_attn_fwd(const void* qkv, void* out, float* lse, int B, int T, i
   PDT_RETURN_LAUNCH();
 }
 
+PDT_API int pdt_fp8_meta_roll_partial(float* meta, const float* partial, int nblk, int fmt, float* dq_out,
+                                      hipStream_t st);
+
+static int attn_bwd_impl(const void* qkv, const void* out, const void* dout, const float* lse, float* delta,
+                         void* dqkv, int B, int T, int H, float scale, void* q8, float* q8_meta, float* q8_part,
+                         float* q8_dq, hipStream_t st);
+
 PDT_API int pdt_attn_bwd(const void* qkv, const void* out, const void* dout, const float* lse, float* delta,
                          void* dqkv, int B, int T, int H, float scale, hipStream_t st) {
+  return attn_bwd_impl(qkv, out, dout, lse, delta, dqkv, B, T, H, scale, nullptr, nullptr, nullptr, nullptr, st);
+}
+
+// pdt_attn_bwd that also writes the e5m2 codes of d(qkv) for the qkv projection's fp8
+// gradient GEMMs (delayed scale q8_meta[0]), rolls that history (q8_part: 2*B*H floats) and
+// writes the codes' dequant factor to q8_dq. Whole-sequence kernels only (T <= 256): -1 else.
+PDT_API int pdt_attn_bwd_q8(const void* qkv, const void* out, const void* dout, const float* lse, float* delta,
+                            void* dqkv, int B, int T, int H, float scale, void* q8, float* q8_meta, float* q8_part,
+                            float* q8_dq, hipStream_t st) {
+  if (!q8 || !q8_meta || !q8_part || attn_seq_disabled() || !seq_nkt(T)) return -1;
+  return attn_bwd_impl(qkv, out, dout, lse, delta, dqkv, B, T, H, scale, q8, q8_meta, q8_part, q8_dq, st);
+}
+
+static int attn_bwd_impl(const void* qkv, const void* out, const void* dout, const float* lse, float* delta,
+                         void* dqkv, int B, int T, int H, float scale, void* q8, float* q8_meta, float* q8_part,
+                         float* q8_dq, hipStream_t st) {
   const int nkt = attn_seq_disabled() ? 0 : seq_nkt(T);
   if (nkt) {
     AttnSeqBwdParams q;
+    q.q8 = (uint8_t*)q8;
+    q.q8_meta = q8_meta;
+    q.q8_part = q8_part;
     q.qkv = (const u16*)qkv;
     q.out = (const u16*)out;
     q.dout = (const u16*)dout;
@@ -893,7 +961,10 @@ PDT_API int pdt_attn_bwd(const void* qkv, const void* out, const void* dout, con
   }
     PDT_SEQ_SWITCH(nkt, SEQ_BWD)
 #undef SEQ_BWD
-    PDT_RETURN_LAUNCH();
+    if (q8 == nullptr) PDT_RETURN_LAUNCH();
+    const int e = (int)hipGetLastError();
+    if (e) return e;
+    return pdt_fp8_meta_roll_partial(q8_meta, q8_part, 2 * B * H, 1, q8_dq, st);
   }
   const long rows = (long)B * T * H;
   hipLaunchKernelGGL(attn_delta_kernel, dim3((unsigned)((rows * 8 + 255) / 256)), dim3(256), 0, st, (const u16*)dout,

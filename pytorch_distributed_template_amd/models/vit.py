@@ -37,9 +37,11 @@ class Attention(nn.Module):
 
     def forward(self, x, fp8=False, residual=None):
         qkv = fused.linear(x, self.qkv, fp8=fp8)                          # [B,T,3D]
-        # (fp8: the attention kernel also writes the projection GEMM's e4m3 input)
+        # (fp8: the attention kernels also write the projection GEMM's e4m3 input and, in
+        # backward, the qkv projection's e5m2 output gradient)
         o = fused.qkv_attention(qkv, self.num_heads, fp8=fp8 and _fp8_attn(),
-                                fp8_for=self.proj if fp8 else None)      # [B,T,D]
+                                fp8_for=self.proj if fp8 else None,
+                                grad_fp8_for=self.qkv if fp8 else None)  # [B,T,D]
         return fused.linear(o, self.proj, fp8=fp8, residual=residual)     # (+ residual in the epilogue)
 
 

@@ -173,14 +173,15 @@ def attention(q, k, v):
     return F.scaled_dot_product_attention(q, k, v)
 
 
-def qkv_attention(qkv, num_heads: int, fp8: bool = False, fp8_for: nn.Linear | None = None):
+def qkv_attention(qkv, num_heads: int, fp8: bool = False, fp8_for: nn.Linear | None = None,
+                  grad_fp8_for: nn.Linear | None = None):
     """Multi-head attention on a packed qkv projection [B, T, 3*H*hd] -> [B, T, H*hd].
     Native path: one fused MFMA kernel (hd = 64; ``fp8``: e4m3 score GEMM); torch path: SDPA."""
     B, T, D3 = qkv.shape
     hd = D3 // (3 * num_heads)
     if _use_native(qkv) and hd == 64:
         from . import native_ops
-        return native_ops.qkv_attention(qkv, num_heads, fp8=fp8, fp8_for=fp8_for)
+        return native_ops.qkv_attention(qkv, num_heads, fp8=fp8, fp8_for=fp8_for, grad_fp8_for=grad_fp8_for)
     q, k, v = qkv.view(B, T, 3, num_heads, hd).permute(2, 0, 3, 1, 4)
     o = F.scaled_dot_product_attention(q, k, v)
     return o.transpose(1, 2).reshape(B, T, num_heads * hd)

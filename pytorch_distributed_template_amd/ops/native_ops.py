@@ -94,6 +94,7 @@ _SIGS = {
     "pdt_amax_partial": (c_int, [P, c_int, c_long, P, P]),
     "pdt_cast_fp8": (c_int, [P, c_int, c_long, P, c_int, P, P, P]),
     "pdt_cast_fp8_t": (c_int, [P, c_int, c_int, P, P, P]),
+    "pdt_attn_bwd_q8": (c_int, [P] * 6 + [c_int, c_int, c_int, c_float] + [P] * 5),
     "pdt_attn_fwd_f8_q8": (c_int, [P, P, P, c_int, c_int, c_int, c_float, P, P, P, P, P]),
     "pdt_cast_fp8_dual": (c_int, [P, c_int, c_int, P, P, P, P, P]),
     "pdt_fp8_meta_words": (c_int, []),
@@ -2040,7 +2041,7 @@ class _QKVAttention(torch.autograd.Function):
     backward, which writes d(qkv) in the qkv layout (the qkv GEMM's dY)."""
 
     @staticmethod
-    def forward(ctx, qkv, H, fp8=False, q8meta=None, box=None):
+    def forward(ctx, qkv, H, fp8=False, q8meta=None, box=None, grad_owner=None):
         B, T, D3 = qkv.shape
         assert D3 == 3 * H * 64 and qkv.dtype == torch.bfloat16, "head_dim must be 64, bf16"
         qkv = qkv.contiguous()
@@ -2061,7 +2062,7 @@ class _QKVAttention(torch.autograd.Function):
         else:
             _chk(_load().pdt_attn_fwd(_p(qkv), _p(out), _p(lse), B, T, H, scale, _s()), "attn_fwd")
         ctx.save_for_backward(qkv, out, lse)
-        ctx.H, ctx.scale = H, scale
+        ctx.H, ctx.scale, ctx.grad_owner = H, scale, grad_owner
         return out
 
     @staticmethod
@@ -2071,22 +2072,36 @@ class _QKVAttention(torch.autograd.Function):
         dout = dout.to(torch.bfloat16).contiguous()
         delta = torch.empty_like(lse)
         dqkv = torch.empty_like(qkv)
+        owner = ctx.grad_owner
+        gmeta = getattr(owner, "_pdt_fp8_gmeta", None) if owner is not None else None
+        if gmeta is not None and T <= 256 and fp8_settings()["scaling"] == "delayed":
+            # also the e5m2 codes of d(qkv) for the qkv projection's fp8 gradient GEMMs
+            codes = torch.empty((B * T, qkv.shape[2]), dtype=torch.uint8, device=qkv.device)
+            part = torch.empty(2 * B * ctx.H + 1, dtype=torch.float32, device=qkv.device)
+            dq = part[-1:]
+            rc = _load().pdt_attn_bwd_q8(_p(qkv), _p(out), _p(dout), _p(lse), _p(delta), _p(dqkv), B, T, ctx.H,
+                                         ctx.scale, _p(codes), _p(gmeta), _p(part), _p(dq), _s())
+            if rc == 0:
+                dqkv._pdt_f8g = (codes, dq, owner)
+                return dqkv, None, None, None, None, None
         _chk(_load().pdt_attn_bwd(_p(qkv), _p(out), _p(dout), _p(lse), _p(delta), _p(dqkv), B, T, ctx.H,
                                   ctx.scale, _s()), "attn_bwd")
-        return dqkv, None, None, None, None
+        return dqkv, None, None, None, None, None
 
 
-def qkv_attention(qkv, num_heads, fp8=False, fp8_for=None):
+def qkv_attention(qkv, num_heads, fp8=False, fp8_for=None, grad_fp8_for=None):
     """softmax(q k^T / 8) v over heads of 64 for a packed [B, T, 3*H*64] qkv. ``fp8``: the
     score GEMM on e4m3 MFMA (per-head / per-tile power-of-two scales, T <= 256); the
     backward is the bf16 recomputing one either way. ``fp8_for``: the fp8 layer consuming
     the output (the attention projection): under delayed scaling the kernel also writes
-    its e4m3 input (``_pdt_f8`` on the result, as :func:`ln_fork` does)."""
+    its e4m3 input (``_pdt_f8`` on the result, as :func:`ln_fork` does); ``grad_fp8_for``:
+    the fp8 layer that produced qkv -- the backward then also writes its e5m2 output
+    gradient (``_pdt_f8g`` on d(qkv))."""
     meta = None
     if fp8 and fp8_for is not None and fp8_settings()["scaling"] == "delayed":
         meta = getattr(fp8_for, "_pdt_fp8_meta", None)
     box: list = []
-    out = _QKVAttention.apply(qkv, num_heads, bool(fp8), meta, box)
+    out = _QKVAttention.apply(qkv, num_heads, bool(fp8), meta, box, grad_fp8_for if fp8 else None)
     if box:
         out._pdt_f8 = (box[0][0], box[0][1], fp8_for)
     return out

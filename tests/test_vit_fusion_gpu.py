@@ -261,6 +261,42 @@ def test_attention_fp8_output_codes_match_separate_cast():
     assert torch.equal(meta1, meta_ref)
 
 
+def test_attention_backward_e5m2_codes_match_separate_cast():
+    """pdt_attn_bwd_q8: d(qkv) unchanged, and its e5m2 codes / dequant factor / history roll
+    (for the qkv projection) equal the delayed-scaling cast of d(qkv)."""
+    torch.manual_seed(30)
+    B, T, H = 2, 197, 4
+    qkv_fc = nn.Linear(H * 64, 3 * H * 64).cuda()
+    no._quant_grad(torch.randn(B * T, 3 * H * 64, device="cuda").to(torch.bfloat16), qkv_fc, "_pdt_fp8_gmeta")
+    meta0 = qkv_fc._pdt_fp8_gmeta.clone()
+    captured = []
+
+    class Cap(torch.autograd.Function):
+        @staticmethod
+        def forward(ctx, t):
+            return t.view_as(t)
+
+        @staticmethod
+        def backward(ctx, g):
+            captured.append(g)
+            return g
+
+    base = torch.randn(B, T, 3 * H * 64, device="cuda").to(torch.bfloat16)
+    gout = torch.randn(B, T, H * 64, device="cuda").to(torch.bfloat16)
+    x = base.clone().requires_grad_(True)
+    no.qkv_attention(Cap.apply(x), H, fp8=True, grad_fp8_for=qkv_fc).backward(gout)
+    g = captured[0]
+    assert hasattr(g, "_pdt_f8g") and g._pdt_f8g[2] is qkv_fc
+    x2 = base.clone().requires_grad_(True)
+    no.qkv_attention(x2, H, fp8=True).backward(gout)
+    assert torch.equal(x.grad, x2.grad)
+    q_ref, dq_ref, meta_ref = no.quantize_fp8_delayed(g.reshape(-1, 3 * H * 64), meta0.clone(), no.E5M2)
+    torch.cuda.synchronize()
+    assert torch.equal(g._pdt_f8g[0], q_ref)
+    assert torch.equal(g._pdt_f8g[1], dq_ref)
+    assert torch.equal(qkv_fc._pdt_fp8_gmeta, meta_ref)
+
+
 def test_vit_fp8_steps_track_torch_fp32():
     """2-block fp8 ViT, three forward/backward passes (the first seeds the delayed-scaling
     histories; the later ones take the LayerNorm-fused e4m3 inputs and delayed e5m2
