@@ -239,10 +239,11 @@ def test_ln_fork_backward_e5m2_codes_match_separate_cast():
     assert torch.equal(x.grad, x2.grad)
 
 
-def test_attention_fp8_output_codes_match_separate_cast():
+def test_attention_fp8_output_codes_match_separate_cast(monkeypatch):
     """pdt_attn_fwd_f8_q8: O unchanged, and the projection's e4m3 input codes / dequant factor /
     amax-history roll equal the delayed-scaling cast of O."""
     torch.manual_seed(29)
+    monkeypatch.setenv("PDT_FP8_ATTN_Q8", "1")
     B, T, H = 2, 197, 4
     qkv = torch.randn(B, T, 3 * H * 64, device="cuda").to(torch.bfloat16)
     proj = nn.Linear(H * 64, H * 64).cuda()
@@ -261,10 +262,11 @@ def test_attention_fp8_output_codes_match_separate_cast():
     assert torch.equal(meta1, meta_ref)
 
 
-def test_attention_backward_e5m2_codes_match_separate_cast():
+def test_attention_backward_e5m2_codes_match_separate_cast(monkeypatch):
     """pdt_attn_bwd_q8: d(qkv) unchanged, and its e5m2 codes / dequant factor / history roll
     (for the qkv projection) equal the delayed-scaling cast of d(qkv)."""
     torch.manual_seed(30)
+    monkeypatch.setenv("PDT_FP8_ATTN_Q8", "1")
     B, T, H = 2, 197, 4
     qkv_fc = nn.Linear(H * 64, 3 * H * 64).cuda()
     no._quant_grad(torch.randn(B * T, 3 * H * 64, device="cuda").to(torch.bfloat16), qkv_fc, "_pdt_fp8_gmeta")
