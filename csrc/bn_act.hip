@@ -690,6 +690,56 @@ PDT_API int pdt_bn_bwd_finalize(const float* part, int R, int C, double count, c
   PDT_RETURN_LAUNCH();
 }
 
+// ResNet downsample blocks: the block-output gradient dA feeds TWO BatchNorm backwards -- bn3
+// of the main branch and the shortcut's BN -- both gated by the block's ReLU bit mask. One
+// pass reads dA and the mask once and writes both input gradients:
+//   dy1 = (k1a*g + k2a*y1 + k3a),  dy2 = (k1b*g + k2b*y2 + k3b),  g = dA masked
+__global__ void __launch_bounds__(NT) bn_bwd_apply_dual_kernel(
+    const u16* __restrict__ dA, const uint8_t* __restrict__ mask, const u16* __restrict__ y1,
+    const float* __restrict__ k1a, const float* __restrict__ k2a, const float* __restrict__ k3a, u16* __restrict__ dy1,
+    const u16* __restrict__ y2, const float* __restrict__ k1b, const float* __restrict__ k2b,
+    const float* __restrict__ k3b, u16* __restrict__ dy2, long n8, int C) {
+  const int cpr = C / 8;
+  const int ch = (int)((blockIdx.x * NT + threadIdx.x) % (uint32_t)cpr) * 8;  // invariant (see bn_apply)
+  float a1[8], a2[8], a3[8], b1[8], b2[8], b3[8];
+  load8f(k1a + ch, a1);
+  load8f(k2a + ch, a2);
+  load8f(k3a + ch, a3);
+  load8f(k1b + ch, b1);
+  load8f(k2b + ch, b2);
+  load8f(k3b + ch, b3);
+  const uint32_t S = gridDim.x * NT;
+  for (uint32_t i = blockIdx.x * NT + threadIdx.x; i < (uint32_t)n8; i += S) {
+    const u32x4 gq = reinterpret_cast<const u32x4*>(dA)[i];
+    const u32x4 yq1 = reinterpret_cast<const u32x4*>(y1)[i];
+    const u32x4 yq2 = reinterpret_cast<const u32x4*>(y2)[i];
+    const uint32_t m = mask[i];
+    float g[8], v1[8], v2[8], o1[8], o2[8];
+    unpack8(gq, g);
+    unpack8(yq1, v1);
+    unpack8(yq2, v2);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const float gg = (m >> k) & 1u ? g[k] : 0.f;
+      o1[k] = a1[k] * gg + a2[k] * v1[k] + a3[k];
+      o2[k] = b1[k] * gg + b2[k] * v2[k] + b3[k];
+    }
+    reinterpret_cast<u32x4*>(dy1)[i] = pack8(o1);
+    reinterpret_cast<u32x4*>(dy2)[i] = pack8(o2);
+  }
+}
+
+PDT_API int pdt_bn_bwd_apply_dual(const void* dA, const void* mask, const void* y1, const float* k1a,
+                                  const float* k2a, const float* k3a, void* dy1, const void* y2, const float* k1b,
+                                  const float* k2b, const float* k3b, void* dy2, long M, int C, hipStream_t st) {
+  if (C % 8 || !mask) return -1;
+  const long n8 = M * C / 8;
+  hipLaunchKernelGGL(bn_bwd_apply_dual_kernel, dim3(grid_for(n8, C)), dim3(NT), 0, st, (const u16*)dA,
+                     (const uint8_t*)mask, (const u16*)y1, k1a, k2a, k3a, (u16*)dy1, (const u16*)y2, k1b, k2b, k3b,
+                     (u16*)dy2, n8, C);
+  PDT_RETURN_LAUNCH();
+}
+
 PDT_API int pdt_bn_bwd_apply(const void* dA, const void* y, const void* act, const float* scale,
                              const float* shift, const float* k1, const float* k2, const float* k3, void* dy,
                              void* dres, long M, int C, int relu, const void* mask, hipStream_t st) {

@@ -43,6 +43,7 @@ _SIGS = {
     "pdt_wgrad_f8_plan": (c_int, [c_int, c_int, c_int, c_int, ctypes.POINTER(c_int)]),
     "pdt_wgrad_f8_workspace": (c_long, [c_int, c_int, c_int]),
     "pdt_linear_wgrad_f8": (c_int, [P] * 8 + [c_int] * 9 + [P]),
+    "pdt_bn_bwd_apply_dual": (c_int, [P] * 12 + [c_long, c_int, P]),
     "pdt_bn_apply_res_affine": (c_int, [P] * 7 + [c_long, c_int, c_int, P, P]),
     "pdt_ln_fwd_f8": (c_int, [P, P, P, P, P, P, c_int, c_int, c_float, P, P, P, P, P]),
     "pdt_ln_fwd_f8_blocks": (c_int, [c_int]),
@@ -858,11 +859,12 @@ def _unit_fwd(x, w, gamma, beta, residual, conv, relu, bna: _BNArgs, apply: bool
     return out, u
 
 
-def _bn_bwd(dA, u: _Unit, want_dres: bool, mask=None, pre: _BnbPartials | None = None):
+def _bn_bwd(dA, u: _Unit, want_dres: bool, mask=None, pre: _BnbPartials | None = None, coeffs_only=False):
     """BN(+res)(+ReLU) backward: returns (dy, dres, dgamma, dbeta). ``mask`` (a ReLU bit
     mask of another unit's output) gates dA first -- the downsample branch of a bottleneck
     sees the block's ReLU exactly as the main branch does. ``pre``: the reduction was
-    already done by the epilogue of the GEMM that produced dA (no reduce pass)."""
+    already done by the epilogue of the GEMM that produced dA (no reduce pass).
+    ``coeffs_only``: stop before the apply pass, return (dgamma, dbeta, k1, k2, k3)."""
     lib = _load()
     st = _s()
     dA = _cl(dA.to(torch.bfloat16))
@@ -884,6 +886,8 @@ def _bn_bwd(dA, u: _Unit, want_dres: bool, mask=None, pre: _BnbPartials | None =
     dgamma, dbeta, k1, k2, k3 = vec[0], vec[1], vec[2], vec[3], vec[4]
     _chk(lib.pdt_bn_bwd_finalize(_p(part), blocks, Cout, float(M), _p(u.gamma), _p(u.mean), _p(u.invstd),
                                  _p(dgamma), _p(dbeta), _p(k1), _p(k2), _p(k3), 0, st), "bn_bwd_finalize")
+    if coeffs_only:
+        return dgamma, dbeta, k1, k2, k3
     dy = torch.empty_like(u.y, memory_format=torch.channels_last)
     dres = torch.empty_like(u.y, memory_format=torch.channels_last) if want_dres else None
     _chk(lib.pdt_bn_bwd_apply(_p(dA), _p(u.y), _p(u.act), _p(u.scale), _p(u.shift), _p(k1), _p(k2), _p(k3),
@@ -1090,7 +1094,20 @@ class _Bottleneck(torch.autograd.Function):
         u1, u2, u3, ud = ctx.units
         need = ctx.needs_input_grad
         dout = _cl(dout.to(torch.bfloat16))
-        dy3, _, dg3, db3 = _bn_bwd(dout, u3, False, pre=_take_bnb(u3, dout))
+        dual = ctx.has_ds and u3.mask is not None and os.environ.get("PDT_BN_DUAL_APPLY", "1") == "1"
+        if dual:
+            # both BN backwards fed by dout (bn3 and the shortcut's BN): coefficients first, then
+            # ONE apply pass that reads dout and the ReLU mask once and writes both gradients
+            dg3, db3, a1, a2, a3 = _bn_bwd(dout, u3, False, pre=_take_bnb(u3, dout), coeffs_only=True)
+            dgd, dbd, b1, b2, b3 = _bn_bwd(dout, ud, False, mask=u3.mask, coeffs_only=True)
+            dy3 = torch.empty_like(u3.y, memory_format=torch.channels_last)
+            dyd = torch.empty_like(ud.y, memory_format=torch.channels_last)
+            M3 = u3.N * u3.g["Ho"] * u3.g["Wo"]
+            _chk(_load().pdt_bn_bwd_apply_dual(_p(dout), _p(u3.mask), _p(u3.y), _p(a1), _p(a2), _p(a3), _p(dy3),
+                                               _p(ud.y), _p(b1), _p(b2), _p(b3), _p(dyd), M3, u3.Cout, _s()),
+                 "bn_bwd_apply_dual")
+        else:
+            dy3, _, dg3, db3 = _bn_bwd(dout, u3, False, pre=_take_bnb(u3, dout))
         fuse = _bnb_enabled()
         if fuse:  # bn2 / bn1 backward reductions in the epilogues of the conv3 / conv2 dgrads
             da2, pre2 = _unit_dx(dy3, u3, bnb_unit=u2)
@@ -1111,7 +1128,8 @@ class _Bottleneck(torch.autograd.Function):
         # (masked) by the epilogue of the block-input dgrad GEMM
         addend_mask = None
         if ctx.has_ds:
-            dyd, _, dgd, dbd = _bn_bwd(dout, ud, False, mask=u3.mask)
+            if not dual:
+                dyd, _, dgd, dbd = _bn_bwd(dout, ud, False, mask=u3.mask)
             addend = _unit_dx(dyd, ud) if need[0] else None
             dwd = wg.dw(dyd, ud)
             grads_ds = (dwd, dgd, dbd)
