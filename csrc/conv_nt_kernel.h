@@ -91,8 +91,13 @@ static __device__ __attribute__((aligned(64))) u32x4 pdt_zero_chunk[4];
 // consumes a whole 128-byte LDS k-row: the two bf16 k-step fragments of a lane
 // ARE its 32-byte fp8 fragment (a k permutation shared by both operands).
 // The per-tensor dequant scales multiply the accumulators in the epilogue.
+// PIPE 1: NSTAGE-deep LDS-DMA ring, one barrier per K-tile. PIPE 2 (256x256, 8 waves): a
+// 4-phase ring -- each K-tile's MFMAs run as four C-quadrant phases, and the next K-tile
+// is fetched one quarter per phase with counted vmcnt (never 0 in the loop), so three
+// quarters stay in flight across every barrier (the schedule of the guide's 256^2 8-phase
+// template, 4 phases per K-tile).
 template <int BM, int BN, int NSTAGE, bool CS64, bool DIRECT, bool GLDS, int NTH = 256, int WM = 2, int F8 = 0,
-          bool PIPE = false, bool BNB = false>
+          int PIPE = 0, bool BNB = false>
 __global__ void __launch_bounds__(NTH, PIPE ? 1 : 2) conv_nt_kernel(NTParams p) {
   constexpr int WN = NTH / 64 / WM;       // waves along N
   constexpr int MI = BM / (WM * 16);      // 16-row MFMA tiles per wave
@@ -112,6 +117,15 @@ __global__ void __launch_bounds__(NTH, PIPE ? 1 : 2) conv_nt_kernel(NTParams p) 
   const int lane = tid & 63;
   const int wave = tid >> 6;
   const int wm = wave / WN, wn = wave % WN;
+  // tile column of this wave's j-th 16-column block. PIPE 2 gives each wave one 32-column
+  // block in each HALF of the tile, so a K-tile's B operand arrives as two contiguous
+  // 128-row halves (one per phase pair).
+  auto wcol = [&](int j) -> int {
+    if constexpr (PIPE == 2)
+      return j < NI / 2 ? wn * (BN / 2 / WN) + j * 16 : BN / 2 + wn * (BN / 2 / WN) + (j - NI / 2) * 16;
+    else
+      return wn * (BN / WN) + j * 16;
+  };
 
   const int ntm = (p.M + BM - 1) / BM;
   const int ntn = (p.Ncol + BN - 1) / BN;
@@ -216,45 +230,51 @@ __global__ void __launch_bounds__(NTH, PIPE ? 1 : 2) conv_nt_kernel(NTParams p) 
   // LDS image stays lane-linear per wave instruction (8 rows x 128 B), so the
   // XOR swizzle moves to the SOURCE: lane (row r, physical chunk ca) fetches
   // logical chunk ca ^ swz(r). Padding / out-of-range rows read a zero page.
-  auto glds_tile = [&](int kt, int buf) {
+  auto glds_a = [&](int kt, int buf, int i) __attribute__((always_inline)) {
     char* sa = smem + buf * STAGE;
-    char* sb = sa + A_BYTES;
     const int k0 = kt * BK;
-#pragma unroll
-    for (int i = 0; i < LA; ++i) {
-      const int r = (tid >> 3) + RS * i;
-      const int c = swz(r, ca);  // logical chunk for this lane's LDS slot
-      const void* g = pdt_zero_chunk;
-      if (CS64) {
-        const int tap = k0 / p.Cs;
-        const int c0 = k0 - tap * p.Cs + c * 8;
-        const int th = fdiv(tap, p.div_ntw);
-        const int tw = tap - th * p.ntw;
-        const int ih = a_ih[i] + p.dh * th, iw = a_iw[i] + p.dw * tw;
-        if (a_ok[i] && (unsigned)ih < (unsigned)p.Hs && (unsigned)iw < (unsigned)p.Ws)
-          g = p.src + (size_t)(a_base[i] + ih * p.Ws + iw) * p.pix + c0;
-      } else {
-        const int kc = k0 / 8 + c;
-        const int tap = fdiv(kc, p.div_Cs8);
-        const int c0 = (kc - tap * (p.Cs / 8)) * 8;
-        const int th = fdiv(tap, p.div_ntw);
-        const int tw = tap - th * p.ntw;
-        const int ih = a_ih[i] + p.dh * th, iw = a_iw[i] + p.dw * tw;
-        if (kc * 8 < p.K && a_ok[i] && (unsigned)ih < (unsigned)p.Hs && (unsigned)iw < (unsigned)p.Ws)
-          g = p.src + (size_t)(a_base[i] + ih * p.Ws + iw) * p.pix + c0;
-      }
-      __builtin_amdgcn_global_load_lds(
-          g, (__attribute__((address_space(3))) void*)(sa + (8 * wave + RS * i) * 128), 16, 0, 0);
+    const int r = (tid >> 3) + RS * i;
+    const int c = swz(r, ca);  // logical chunk for this lane's LDS slot
+    const void* g = pdt_zero_chunk;
+    if (CS64) {
+      const int tap = k0 / p.Cs;
+      const int c0 = k0 - tap * p.Cs + c * 8;
+      const int th = fdiv(tap, p.div_ntw);
+      const int tw = tap - th * p.ntw;
+      const int ih = a_ih[i] + p.dh * th, iw = a_iw[i] + p.dw * tw;
+      if (a_ok[i] && (unsigned)ih < (unsigned)p.Hs && (unsigned)iw < (unsigned)p.Ws)
+        g = p.src + (size_t)(a_base[i] + ih * p.Ws + iw) * p.pix + c0;
+    } else {
+      const int kc = k0 / 8 + c;
+      const int tap = fdiv(kc, p.div_Cs8);
+      const int c0 = (kc - tap * (p.Cs / 8)) * 8;
+      const int th = fdiv(tap, p.div_ntw);
+      const int tw = tap - th * p.ntw;
+      const int ih = a_ih[i] + p.dh * th, iw = a_iw[i] + p.dw * tw;
+      if (kc * 8 < p.K && a_ok[i] && (unsigned)ih < (unsigned)p.Hs && (unsigned)iw < (unsigned)p.Ws)
+        g = p.src + (size_t)(a_base[i] + ih * p.Ws + iw) * p.pix + c0;
     }
+    __builtin_amdgcn_global_load_lds(g, (__attribute__((address_space(3))) void*)(sa + (8 * wave + RS * i) * 128),
+                                     16, 0, 0);
+  };
+  auto glds_b = [&](int kt, int buf, int j) __attribute__((always_inline)) {
+    char* sb = smem + buf * STAGE + A_BYTES;
+    const int r = (tid >> 3) + RS * j;
+    const int kb = kt * BK + swz(r, ca) * 8;
+    const void* g = (b_ok[j] && kb < p.K) ? (const void*)(p.b + (size_t)b_row[j] * p.ldb + kb)
+                                          : (const void*)pdt_zero_chunk;
+    __builtin_amdgcn_global_load_lds(g, (__attribute__((address_space(3))) void*)(sb + (8 * wave + RS * j) * 128),
+                                     16, 0, 0);
+  };
+  // GLDS: global_load_lds_dwordx4 straight into LDS (no VGPR staging). The
+  // LDS image stays lane-linear per wave instruction (8 rows x 128 B), so the
+  // XOR swizzle moves to the SOURCE: lane (row r, physical chunk ca) fetches
+  // logical chunk ca ^ swz(r). Padding / out-of-range rows read a zero page.
+  auto glds_tile = [&](int kt, int buf) {
 #pragma unroll
-    for (int j = 0; j < LB; ++j) {
-      const int r = (tid >> 3) + RS * j;
-      const int kb = k0 + swz(r, ca) * 8;
-      const void* g = (b_ok[j] && kb < p.K) ? (const void*)(p.b + (size_t)b_row[j] * p.ldb + kb)
-                                            : (const void*)pdt_zero_chunk;
-      __builtin_amdgcn_global_load_lds(
-          g, (__attribute__((address_space(3))) void*)(sb + (8 * wave + RS * j) * 128), 16, 0, 0);
-    }
+    for (int i = 0; i < LA; ++i) glds_a(kt, buf, i);
+#pragma unroll
+    for (int j = 0; j < LB; ++j) glds_b(kt, buf, j);
   };
 
   f32x4 acc[MI][NI];
@@ -277,7 +297,7 @@ __global__ void __launch_bounds__(NTH, PIPE ? 1 : 2) conv_nt_kernel(NTParams p) 
         }
 #pragma unroll
         for (int j = 0; j < NI; ++j) {
-          int r = wn * (BN / WN) + j * 16 + (lane & 15);
+          int r = wcol(j) + (lane & 15);
           bfr[kk][j] = *reinterpret_cast<const bf16x8*>(sb + r * 128 + swz(r, kch) * 16);
         }
       }
@@ -301,7 +321,7 @@ __global__ void __launch_bounds__(NTH, PIPE ? 1 : 2) conv_nt_kernel(NTParams p) 
         }
 #pragma unroll
         for (int j = 0; j < NI; ++j) {
-          int r = wn * (BN / WN) + j * 16 + (lane & 15);
+          int r = wcol(j) + (lane & 15);
           bfr[j] = *reinterpret_cast<const bf16x8*>(sb + r * 128 + swz(r, kch) * 16);
         }
         if (PIPE) __builtin_amdgcn_s_setprio(1);
@@ -316,7 +336,125 @@ __global__ void __launch_bounds__(NTH, PIPE ? 1 : 2) conv_nt_kernel(NTParams p) 
     }
   };
 
-  if constexpr (PIPE) {
+  if constexpr (PIPE == 2) {
+    // 4-phase ring (see the template comment). Quarter loads of a K-tile: q0 = A rows of
+    // quadrant row r = 0 (chunks i = 0, 2), q1 = B half 0 (j = 0, 1), q2 = B half 1 (j = 2, 3),
+    // q3 = A rows r = 1 (i = 1, 3); 2 LDS-DMA instructions each per thread. Phases of K-tile t
+    // (C-quadrant (r, c)): 1 = (0,0) needs q0 q1, 2 = (0,1) needs q2, 3 = (1,1) needs q3, 4 =
+    // (1,0) needs nothing new; phase p issues quarter p-1 of K-tile t+1 into the other buffer,
+    // whose last reads (K-tile t-1) all precede phase 1's barrier.
+    // RAW: each wave retires its own DMA of a quarter with a counted vmcnt, then the barrier
+    // makes every wave's copy visible; reads of a quarter never precede that barrier.
+    static_assert(GLDS && NSTAGE == 2 && LA == 4 && LB == 4 && MI % 2 == 0 && NI % 2 == 0, "4-phase ring shape");
+    auto issue = [&](int q, int kt, int buf) __attribute__((always_inline)) {
+      if (q == 0) { glds_a(kt, buf, 0); glds_a(kt, buf, 2); }
+      else if (q == 1) { glds_b(kt, buf, 0); glds_b(kt, buf, 1); }
+      else if (q == 2) { glds_b(kt, buf, 2); glds_b(kt, buf, 3); }
+      else { glds_a(kt, buf, 1); glds_a(kt, buf, 3); }
+    };
+    constexpr int HM = MI / 2, HN = NI / 2;
+    bf16x8 af[HM][2], bq[HN][2];
+    auto read_a = [&](const char* sa, int r) __attribute__((always_inline)) {
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) {
+        const int kch = kk * 4 + (lane >> 4);
+#pragma unroll
+        for (int i = 0; i < HM; ++i) {
+          const int row = wm * (BM / WM) + (r * HM + i) * 16 + (lane & 15);
+          af[i][kk] = *reinterpret_cast<const bf16x8*>(sa + row * 128 + swz(row, kch) * 16);
+        }
+      }
+    };
+    auto read_b = [&](const char* sb, int c) __attribute__((always_inline)) {
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) {
+        const int kch = kk * 4 + (lane >> 4);
+#pragma unroll
+        for (int j = 0; j < HN; ++j) {
+          const int row = wcol(c * HN + j) + (lane & 15);
+          bq[j][kk] = *reinterpret_cast<const bf16x8*>(sb + row * 128 + swz(row, kch) * 16);
+        }
+      }
+    };
+    auto mma = [&](int r, int c) __attribute__((always_inline)) {
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int i = 0; i < HM; ++i)
+#pragma unroll
+        for (int j = 0; j < HN; ++j) {
+          if constexpr (F8 != 0) {
+            acc[r * HM + i][c * HN + j] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(
+                cat8(bq[j][0], bq[j][1]), cat8(af[i][0], af[i][1]), acc[r * HM + i][c * HN + j], 0,
+                F8 == 2 ? 1 : 0, 0, 127, 0, 127);
+          } else {
+#pragma unroll
+            for (int kk = 0; kk < 2; ++kk)
+              acc[r * HM + i][c * HN + j] =
+                  __builtin_amdgcn_mfma_f32_16x16x32_bf16(bq[j][kk], af[i][kk], acc[r * HM + i][c * HN + j], 0, 0, 0);
+          }
+        }
+      __builtin_amdgcn_s_setprio(0);
+    };
+    // Two wave groups (wm = 0 / 1) run one barrier apart (ping-pong): each phase is a
+    // memory section (wait, LDS-DMA issue, fragment ds_reads, lgkmcnt(0)), a barrier, the
+    // 16-MFMA section, a barrier -- so one group's MFMAs overlap the other group's memory
+    // section. A quarter is waited (vmcnt) in the memory section BEFORE the phase that
+    // reads it: every wave has retired its copy before the barrier that ends that section,
+    // which every reader has passed. A buffer is restaged only after the barrier that
+    // follows both groups' last reads of it (their lgkmcnt(0) precedes it).
+    auto bar = [&]() __attribute__((always_inline)) {
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+    };
+    auto mma_phase = [&](int r, int c) __attribute__((always_inline)) {
+      bar();
+      mma(r, c);
+      bar();
+    };
+    if (nk > 0) {
+#pragma unroll
+      for (int q = 0; q < 4; ++q) issue(q, 0, 0);
+      asm volatile("s_waitcnt vmcnt(4)" ::: "memory");  // q0 q1 of K-tile 0
+    }
+    bar();
+    if (wm == 1) bar();  // the stagger
+    for (int kt = 0; kt < nk; ++kt) {
+      const int cur = kt & 1, nxt = cur ^ 1;
+      const bool more = kt + 1 < nk;
+      const char* sa = smem + cur * STAGE;
+      const char* sb = sa + A_BYTES;
+      // M1: retire q2 of this K-tile (read in phase 2); prefetch q0 of the next
+      asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+      if (more) issue(0, kt + 1, nxt);
+      read_a(sa, 0);
+      read_b(sb, 0);
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      mma_phase(0, 0);
+      // M2: retire q3 (read in phase 3)
+      if (more) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      if (more) issue(1, kt + 1, nxt);
+      read_b(sb, 1);
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      mma_phase(0, 1);
+      // M3
+      if (more) issue(2, kt + 1, nxt);
+      read_a(sa, 1);
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      mma_phase(1, 1);
+      // M4: retire q0 q1 of the next K-tile (read in its phase 1)
+      if (more) {
+        asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+        issue(3, kt + 1, nxt);
+      }
+      read_b(sb, 0);
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      mma_phase(1, 0);
+    }
+    if (wm == 0) bar();  // close the stagger: equal barrier counts on every wave
+    if (!DIRECT) __syncthreads();  // before the epilogue reuses LDS
+  } else if constexpr (PIPE) {
     // NSTAGE-deep LDS-DMA ring, ONE raw barrier per K-tile: tile kt+NSTAGE-1
     // is issued right after the barrier that proves every wave finished
     // reading its buffer (tile kt-1's); the counted vmcnt before the barrier
@@ -392,7 +530,7 @@ __global__ void __launch_bounds__(NTH, PIPE ? 1 : 2) conv_nt_kernel(NTParams p) 
     for (int j = 0; j < NI; ++j) {
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        int col = n0 + wn * (BN / WN) + j * 16 + lcol + r;
+        int col = n0 + wcol(j) + lcol + r;
         float bv = col < p.Ncol ? p.bias[col] : 0.f;
 #pragma unroll
         for (int i = 0; i < MI; ++i) acc[i][j][r] += bv;
@@ -420,7 +558,7 @@ __global__ void __launch_bounds__(NTH, PIPE ? 1 : 2) conv_nt_kernel(NTParams p) 
 #pragma unroll
       for (int j = 0; j < NI; ++j) {
         int r = wm * (BM / WM) + i * 16 + lrow;
-        int c = wn * (BN / WN) + j * 16 + lcol;
+        int c = wcol(j) + lcol;
         uint2 w;
         w.x = pack2bf(acc[i][j][0], acc[i][j][1]);
         w.y = pack2bf(acc[i][j][2], acc[i][j][3]);
@@ -567,7 +705,7 @@ __global__ void __launch_bounds__(NTH, PIPE ? 1 : 2) conv_nt_kernel(NTParams p) 
       if (lrow == 0) {
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          int col = n0 + wn * (BN / WN) + j * 16 + lcol + r;
+          int col = n0 + wcol(j) + lcol + r;
           if (col < p.Ncol) {
             p.stats[(size_t)srow * p.Ncol + col] = s[r];
             p.stats[(size_t)(p.nstat_rows + srow) * p.Ncol + col] = q[r];
@@ -597,7 +735,7 @@ __global__ void __launch_bounds__(NTH, PIPE ? 1 : 2) conv_nt_kernel(NTParams p) 
       }
 #pragma unroll
       for (int j = 0; j < NI; ++j) {
-        int col = n0 + wn * (BN / WN) + j * 16 + lcol;
+        int col = n0 + wcol(j) + lcol;
         if (col >= p.Ncol) continue;
         float v0 = acc[i][j][0], v1 = acc[i][j][1], v2 = acc[i][j][2], v3 = acc[i][j][3];
         if (addend != nullptr) {
@@ -639,7 +777,7 @@ __global__ void __launch_bounds__(NTH, PIPE ? 1 : 2) conv_nt_kernel(NTParams p) 
 #pragma unroll
       for (int j = 0; j < NI; ++j) {
         int r = wm * (BM / WM) + i * 16 + lrow;
-        int c = wn * (BN / WN) + j * 16 + lcol;
+        int c = wcol(j) + lcol;
         uint2 w;
         w.x = pack2bf(acc[i][j][0], acc[i][j][1]);
         w.y = pack2bf(acc[i][j][2], acc[i][j][3]);
@@ -744,7 +882,7 @@ __global__ void __launch_bounds__(NTH, PIPE ? 1 : 2) conv_nt_kernel(NTParams p) 
 }
 
 template <int BM, int BN, int NS, bool CS64, bool DIRECT, bool GLDS = false, int NTH = 256, int WM = 2, int F8 = 0,
-          bool PIPE = false, bool BNB = false>
+          int PIPE = 0, bool BNB = false>
 int launch(const NTParams& p, hipStream_t st) {
   int ntm = (p.M + BM - 1) / BM, ntn = (p.Ncol + BN - 1) / BN;
   hipLaunchKernelGGL((conv_nt_kernel<BM, BN, NS, CS64, DIRECT, GLDS, NTH, WM, F8, PIPE, BNB>), dim3(ntm * ntn),
@@ -765,17 +903,20 @@ int launch(const NTParams& p, hipStream_t st) {
 //   id 36      : 256x256 (2x4 waves of 128x64), 2-stage ring (128 KB LDS): the
 //                per-wave tile that lifts the LDS-bytes-per-MFMA ratio above the
 //                64x64 tiles' (LDS read bandwidth, not MFMA, bounds those)
-constexpr int NVAR = 37;
+//   id 37      : the same tile on the 4-phase ping-pong ring (PIPE 2): bit-identical to id 36,
+//                within +-5 % of it on the ViT / ResNet GEMM shapes (scripts/ab_variant.py;
+//                the fp8 instantiation spilled and ran 1.7x slower, so it is not built)
+constexpr int NVAR = 38;
 constexpr int VAR_BM[NVAR] = {128, 256, 64, 128, 64, 128, 256, 64, 128, 64,
                               128, 256, 64, 128, 64, 128, 256, 64, 128, 64,
                               128, 256, 64, 128, 64, 128, 256, 64, 128, 64,
-                              256, 128, 256, 128, 256, 128, 256};
+                              256, 128, 256, 128, 256, 128, 256, 256};
 constexpr int VAR_BN[NVAR] = {128, 64, 128, 64, 64, 128, 64, 128, 64, 64,
                               128, 64, 128, 64, 64, 128, 64, 128, 64, 64,
                               128, 64, 128, 64, 64, 128, 64, 128, 64, 64,
-                              128, 256, 128, 256, 128, 256, 256};
+                              128, 256, 128, 256, 128, 256, 256, 256};
 constexpr int VAR_WM[NVAR] = {2, 2, 2, 2, 2, 2, 2, 2, 2, 2, 2, 2, 2, 2, 2, 2, 2, 2, 2, 2,
-                              2, 2, 2, 2, 2, 2, 2, 2, 2, 2, 4, 2, 4, 2, 4, 2, 2};
+                              2, 2, 2, 2, 2, 2, 2, 2, 2, 2, 4, 2, 4, 2, 4, 2, 2, 2};
 
 inline int heuristic_variant(int M, int Ncol, int K) {
   (void)M;
@@ -823,6 +964,7 @@ int launch_variant(int v, const NTParams& p, hipStream_t st) {
     case 34: return launch<256, 128, 3, CS64, false, true, 512, 4, 0, true, BNB>(p, st);
     case 35: return launch<128, 256, 3, CS64, false, true, 512, 2, 0, true, BNB>(p, st);
     case 36: return launch<256, 256, 2, CS64, false, true, 512, 2, 0, true, BNB>(p, st);
+    case 37: return launch<256, 256, 2, CS64, false, true, 512, 2, 0, 2, BNB>(p, st);
   }
   return -3;
 }

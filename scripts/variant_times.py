@@ -1,4 +1,4 @@
-"""Time every conv_nt variant (LDS-tiled 0..36 and streaming 37+) on the ResNet-50
+"""Time every conv_nt variant (LDS-tiled 0..37 and streaming 38+) on the ResNet-50
 1x1 GEMM shapes at batch 256, forward (with BN statistics) and data-gradient
 (plain) epilogues; prints the fastest few per shape with achieved HBM GB/s."""
 import os
@@ -52,7 +52,7 @@ def main():
             res.sort()
             bytes_ = (n * Hi * Hi * K + M * N) * 2
             top = " ".join(f"v{v}:{t:.1f}" for t, v in res[:5])
-            stream = " ".join(f"v{v}:{t:.1f}" for t, v in res if v >= 37)
+            stream = " ".join(f"v{v}:{t:.1f}" for t, v in res if v >= 38)
             print(f"K={K:4d} N={N:4d} H={H:2d} s={s} stats={int(stats)}  best {res[0][0]:6.1f}us "
                   f"{bytes_ / res[0][0] / 1e3:6.0f} GB/s | {top} | stream {stream}", flush=True)
 
