@@ -353,26 +353,35 @@ __global__ void __launch_bounds__(NTH, PIPE ? 1 : 2) conv_nt_kernel(NTParams p) 
       else { glds_a(kt, buf, 1); glds_a(kt, buf, 3); }
     };
     constexpr int HM = MI / 2, HN = NI / 2;
-    bf16x8 af[HM][2], bq[HN][2];
+    // bf16: two k-step fragments per 16-row block; fp8: the same 32 bytes as ONE operand
+    // (the k permutation of the F8 note above), assembled at read time
+    bf16x8 af[F8 ? 1 : HM][2], bq[F8 ? 1 : HN][2];
+    i32x8 af8[F8 ? HM : 1], bq8[F8 ? HN : 1];
     auto read_a = [&](const char* sa, int r) __attribute__((always_inline)) {
 #pragma unroll
-      for (int kk = 0; kk < 2; ++kk) {
-        const int kch = kk * 4 + (lane >> 4);
-#pragma unroll
-        for (int i = 0; i < HM; ++i) {
-          const int row = wm * (BM / WM) + (r * HM + i) * 16 + (lane & 15);
-          af[i][kk] = *reinterpret_cast<const bf16x8*>(sa + row * 128 + swz(row, kch) * 16);
+      for (int i = 0; i < HM; ++i) {
+        const int row = wm * (BM / WM) + (r * HM + i) * 16 + (lane & 15);
+        const bf16x8 f0 = *reinterpret_cast<const bf16x8*>(sa + row * 128 + swz(row, lane >> 4) * 16);
+        const bf16x8 f1 = *reinterpret_cast<const bf16x8*>(sa + row * 128 + swz(row, 4 + (lane >> 4)) * 16);
+        if constexpr (F8 != 0) {
+          af8[i] = cat8(f0, f1);
+        } else {
+          af[i][0] = f0;
+          af[i][1] = f1;
         }
       }
     };
     auto read_b = [&](const char* sb, int c) __attribute__((always_inline)) {
 #pragma unroll
-      for (int kk = 0; kk < 2; ++kk) {
-        const int kch = kk * 4 + (lane >> 4);
-#pragma unroll
-        for (int j = 0; j < HN; ++j) {
-          const int row = wcol(c * HN + j) + (lane & 15);
-          bq[j][kk] = *reinterpret_cast<const bf16x8*>(sb + row * 128 + swz(row, kch) * 16);
+      for (int j = 0; j < HN; ++j) {
+        const int row = wcol(c * HN + j) + (lane & 15);
+        const bf16x8 f0 = *reinterpret_cast<const bf16x8*>(sb + row * 128 + swz(row, lane >> 4) * 16);
+        const bf16x8 f1 = *reinterpret_cast<const bf16x8*>(sb + row * 128 + swz(row, 4 + (lane >> 4)) * 16);
+        if constexpr (F8 != 0) {
+          bq8[j] = cat8(f0, f1);
+        } else {
+          bq[j][0] = f0;
+          bq[j][1] = f1;
         }
       }
     };
@@ -385,8 +394,7 @@ __global__ void __launch_bounds__(NTH, PIPE ? 1 : 2) conv_nt_kernel(NTParams p) 
         for (int j = 0; j < HN; ++j) {
           if constexpr (F8 != 0) {
             acc[r * HM + i][c * HN + j] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(
-                cat8(bq[j][0], bq[j][1]), cat8(af[i][0], af[i][1]), acc[r * HM + i][c * HN + j], 0,
-                F8 == 2 ? 1 : 0, 0, 127, 0, 127);
+                bq8[j], af8[i], acc[r * HM + i][c * HN + j], 0, F8 == 2 ? 1 : 0, 0, 127, 0, 127);
           } else {
 #pragma unroll
             for (int kk = 0; kk < 2; ++kk)
@@ -424,32 +432,33 @@ __global__ void __launch_bounds__(NTH, PIPE ? 1 : 2) conv_nt_kernel(NTParams p) 
       const bool more = kt + 1 < nk;
       const char* sa = smem + cur * STAGE;
       const char* sb = sa + A_BYTES;
-      // M1: retire q2 of this K-tile (read in phase 2); prefetch q0 of the next
-      asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
-      if (more) issue(0, kt + 1, nxt);
+      // Memory sections: fragment ds_reads first (their data was retired one section
+      // earlier), then the counted wait for the quarter the NEXT section reads, then the
+      // prefetch of the next K-tile's quarter. The reads are retired by the lgkmcnt(0) after
+      // the section's barrier (inside mma): every restage comes >= 2 phases after the last
+      // read of its region, so no wait is needed before that barrier.
+      // M1: reads (0,0); retire q2 of this K-tile (read in phase 2); prefetch q0 of the next
       read_a(sa, 0);
       read_b(sb, 0);
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+      if (more) issue(0, kt + 1, nxt);
       mma_phase(0, 0);
-      // M2: retire q3 (read in phase 3)
+      // M2: reads (0,1); retire q3 (read in phase 3)
+      read_b(sb, 1);
       if (more) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
       else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       if (more) issue(1, kt + 1, nxt);
-      read_b(sb, 1);
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       mma_phase(0, 1);
-      // M3
-      if (more) issue(2, kt + 1, nxt);
+      // M3: reads (1,1)
       read_a(sa, 1);
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      if (more) issue(2, kt + 1, nxt);
       mma_phase(1, 1);
-      // M4: retire q0 q1 of the next K-tile (read in its phase 1)
+      // M4: reads (1,0); retire q0 q1 of the next K-tile (read in its phase 1)
+      read_b(sb, 0);
       if (more) {
         asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
         issue(3, kt + 1, nxt);
       }
-      read_b(sb, 0);
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       mma_phase(1, 0);
     }
     if (wm == 0) bar();  // close the stagger: equal barrier counts on every wave
