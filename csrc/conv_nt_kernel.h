@@ -236,7 +236,9 @@ __global__ void __launch_bounds__(NTH, PIPE ? 1 : 2) conv_nt_kernel(NTParams p) 
     const int r = (tid >> 3) + RS * i;
     const int c = swz(r, ca);  // logical chunk for this lane's LDS slot
     const void* g = pdt_zero_chunk;
-    if (CS64) {
+    if constexpr (F8 != 0) {  // the fp8 GEMM's A is a dense [M][K] matrix (pdt_gemm_f8): no gather math
+      if (m0 + r < p.M) g = p.src + (size_t)(m0 + r) * p.Cs + k0 + c * 8;
+    } else if (CS64) {
       const int tap = k0 / p.Cs;
       const int c0 = k0 - tap * p.Cs + c * 8;
       const int th = fdiv(tap, p.div_ntw);
