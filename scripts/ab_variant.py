@@ -1,7 +1,7 @@
 """A/B two conv_nt (bf16) or gemm_f8 variants on the ViT-B/16 linear shapes and a few
 ResNet-50 bs2048 1x1 GEMM shapes: interleaved rounds, median time per variant.
 
-    python scripts/ab_variant.py --bf16 36,37 --f8 10
+    python scripts/ab_variant.py --bf16 36,37 --f8 10     (or 36/37: gpu_job.sh turns commas into spaces)
 """
 import argparse
 import os
@@ -23,8 +23,8 @@ def main():
     ap.add_argument("--f8", default="10")
     ap.add_argument("--rounds", type=int, default=5)
     a = ap.parse_args()
-    vb = [int(v) for v in a.bf16.split(",") if v]
-    vf = [int(v) for v in a.f8.split(",") if v]
+    vb = [int(v) for v in a.bf16.replace("/", ",").split(",") if v.isdigit()]  # "/" also separates
+    vf = [int(v) for v in a.f8.replace("/", ",").split(",") if v.isdigit()]
     lib = no._load()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     for M, N, K in SHAPES:

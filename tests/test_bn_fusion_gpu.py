@@ -233,3 +233,52 @@ def test_stem_bn_backward_gathers_pool_gradient(monkeypatch):
         e = nrmerr(a, b)
         print(f"pool-gather vs composed {tuple(a.shape)}: {e:.3g}")
         assert torch.isfinite(a).all() and e < 1e-2, (a.shape, e)
+
+
+@pytest.mark.parametrize("ncol,use_mask,use_add", [(128, False, True), (512, True, False)])
+def test_bnb_epilogue_every_variant(ncol, use_mask, use_add):
+    """Every conv_nt tile variant (and stream variant) with the fused BN-backward
+    epilogue, on a 1x1 data-gradient geometry: the output (+ ReLU-masked addend)
+    and the partial sums (sum of the gated gradient g, sum of g * (y - mean)) vs
+    an fp32 reference."""
+    torch.manual_seed(21)
+    dev = "cuda"
+    N, H, K = 4, 28, 256
+    M = N * H * H
+    lib = no._load()
+    dy = torch.randn(M, K, device=dev).to(torch.bfloat16)
+    wt = (torch.randn(ncol, K, device=dev) / K ** 0.5).to(torch.bfloat16)  # B: [Ncol][K]
+    y = torch.randn(M, ncol, device=dev).to(torch.bfloat16)
+    mean = torch.randn(ncol, device=dev) * 0.1
+    scale = torch.rand(ncol, device=dev) + 0.5
+    shift = torch.randn(ncol, device=dev) * 0.2
+    add = torch.randn(M, ncol, device=dev).to(torch.bfloat16) if use_add else None
+    amask = torch.randint(0, 256, (M * ncol // 8,), dtype=torch.uint8, device=dev) if use_add else None
+    mask = torch.randint(0, 256, (M * ncol // 8,), dtype=torch.uint8, device=dev) if use_mask else None
+
+    def bits(m):
+        return ((m.view(-1, 1).int() >> torch.arange(8, device=dev)) & 1).view(M, ncol).float()
+
+    ref = dy.float() @ wt.float().t()
+    if use_add:
+        ref = ref + add.float() * bits(amask)
+    gate = bits(mask) if use_mask else ((y.float() * scale + shift) > 0).float()
+    ran = 0
+    for v in range(lib.pdt_conv_nt_num_variants()):
+        R = lib.pdt_conv_nt_bnb_rows(M, ncol, K, v)
+        part = torch.full((2 * max(R, 1) * ncol,), float("nan"), device=dev)
+        out = torch.empty(M, ncol, device=dev, dtype=torch.bfloat16)
+        rc = lib.pdt_conv_nt_bnb(no._p(dy), no._p(wt), no._p(out), no._p(add), no._p(amask),
+                                 H, H, K, N, H, H, ncol, K, K, 1, 1, 0, 0, 1, 1, 1, 1,
+                                 H, H, 1, 1, 0, 0, ncol, v, no._p(y), no._p(mean), no._p(scale), no._p(shift),
+                                 no._p(mask), no._p(part), 1, 0, R, no._s())
+        if rc == no.NOT_APPLICABLE:
+            continue
+        assert rc == 0, (v, rc)
+        ran += 1
+        assert nrmerr(out, ref) < 1e-2, v
+        g = out.float() * gate  # the partials see the stored bf16 value
+        ps = part.view(2, R, ncol).sum(1)
+        assert nrmerr(ps[0], g.sum(0)) < 1e-3, v
+        assert nrmerr(ps[1], (g * (y.float() - mean)).sum(0)) < 1e-3, v
+    assert ran >= 30

@@ -73,12 +73,19 @@ def test_conv_fwd_dgrad_wgrad(shape):
                              f"{torch.equal(wb.float()[:, :Cin] if Cs != Cin else wb.float(), wr)}")
     # every tile variant the autotuner may pick computes the same conv
     a = no._fwd_nt_geom(N, H, W, Cs, Cout, g)
+    Mv = a["Nimg"] * a["Hm"] * a["Wm"]
     for v in range(no._load().pdt_conv_nt_num_variants()):
         yv = torch.empty_like(y)
-        rc = no._load().pdt_conv_nt(*no._nt_args(xs, wb, yv, None, None, a, 0, v))
+        rows = no._load().pdt_conv_nt_stat_rows(Mv, Cout, a["K"], v)
+        pv = torch.full((2 * max(rows, 1) * Cout,), float("nan"), device=dev)
+        rc = no._load().pdt_conv_nt(*no._nt_args(xs, wb, yv, pv, None, a, 0, v))
         if rc == no.NOT_APPLICABLE:
             continue
         assert rc == 0 and relerr(yv, ref) < 1e-2, v
+        # ... and the same BN partial statistics from its epilogue
+        psv = pv.view(2, rows, Cout).sum(1)
+        assert relerr(psv[0], ref.sum((0, 2, 3))) < 1e-3, v
+        assert relerr(psv[1], (ref * ref).sum((0, 2, 3))) < 1e-3, v
     # BN partial statistics from the epilogue
     ps = part[:2 * R * Cout].view(2, R, Cout).sum(1)
     rs = ref.sum((0, 2, 3))
