@@ -221,6 +221,28 @@ def test_maxpool_avgpool():
     assert relerr(z.grad, zr.grad) < 1e-2
 
 
+@pytest.mark.parametrize("hw", [(112, 112), (57, 31), (8, 9)])
+def test_maxpool_bwd_row_kernel_matches_generic(hw, monkeypatch):
+    """The 3x3/s2/p1 row-per-workgroup backward (C = 64) is bit-identical to the generic
+    gather kernel, odd sizes included (edge windows), and matches fp32 autograd."""
+    torch.manual_seed(4)
+    H, W = hw
+    x = _cl(torch.randn(3, 64, H, W, device="cuda").to(torch.bfloat16)).requires_grad_(True)
+    y = no.max_pool2d(x, 3, 2, 1)
+    g = _cl(torch.randn_like(y))
+    outs = {}
+    for row in ("1", "0"):
+        monkeypatch.setenv("PDT_MAXPOOL_BWD_ROW", row)
+        x.grad = None
+        no.max_pool2d(x, 3, 2, 1).backward(g)
+        torch.cuda.synchronize()
+        outs[row] = x.grad.clone()
+    assert torch.equal(outs["1"], outs["0"])
+    xr = x.detach().float().requires_grad_(True)
+    F.max_pool2d(xr, 3, 2, 1).backward(g.float())
+    assert relerr(outs["1"], xr.grad) < 1e-2
+
+
 def test_linear_and_xent():
     torch.manual_seed(3)
     fc = nn.Linear(2048, 1000).cuda()
