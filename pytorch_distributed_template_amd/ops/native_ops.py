@@ -20,7 +20,8 @@ from pathlib import Path
 import torch
 import torch.nn as nn
 
-_LIB_PATH = Path(__file__).resolve().parents[1] / "_lib" / "libpdt_hip.so"
+_LIB_PATH = Path(os.environ.get("PDT_LIB_PATH", "") or
+                 Path(__file__).resolve().parents[1] / "_lib" / "libpdt_hip.so")  # override: A/B builds
 _lib = None
 _lock = threading.Lock()
 
