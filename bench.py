@@ -38,16 +38,21 @@ BASELINE_METRIC = "images/sec (whole node) ResNet-50 synthetic 3x224x224 at 1/2/
 # MIOpen convs/BN, torch SGD) measured on one MI355X with this same harness
 # (`bench.py --backend torch --batch B`), keyed by (model, per-GPU batch), see
 # BASELINE.md. Scaled by N for N GPUs (weak scaling).
-STOCK_1GPU_IMG_S = {("resnet50", 256): 6605.4, ("resnet50", 512): 6863.8}
+STOCK_1GPU_IMG_S = {("resnet50", 256): 6605.4, ("resnet50", 512): 6863.8,
+                    ("vit_b_16", 256): 3547.25, ("vit_b_16", 1024): 4059.96}
 # At a batch the stock stack was not measured at (its MIOpen find at bs 1024 ran
 # past 390 s on one box), compare against its BEST measured per-GPU throughput.
-STOCK_BEST_1GPU_IMG_S = {"resnet50": (6863.8, 512)}
+STOCK_BEST_1GPU_IMG_S = {"resnet50": (6863.8, 512), "vit_b_16": (4059.96, 1024)}
 # Per-GPU batch: 2048 images (82 GiB of the 288 GiB HBM3E; weak scaling, so the
 # 8-GPU job holds 16384 images). The stage-3/4 GEMMs (M = N*14*14, N*7*7) fill all
 # 256 CUs only from ~512 images up and every per-launch cost amortises over more
 # images; measured on one MI355X: 11.96k img/s at 512, 12.45k at 768, 12.66k at
 # 1024, 13.01k at 1536, 13.09-13.11k at 2048 (profiles/bench_runs_round2.jsonl).
-DEFAULT_BATCH = {"resnet50": 2048}
+# ViT-B/16: 1024 images per GPU (52 GiB fp8 / 60 GiB bf16); measured on one MI355X,
+# fp8: 6.46k img/s at 256, 6.96k at 512, 7.31k at 1024, 7.49k at 2048; bf16 5.38k at
+# 1024 (stock autocast: 3.55k at 256, 4.06k at 1024). At 256 the host-side issue
+# time (~35 ms) is close to the 40 ms step: the GPU idles between kernels.
+DEFAULT_BATCH = {"resnet50": 2048, "vit_b_16": 1024}
 
 
 def parse():
@@ -55,7 +60,7 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=30)
     ap.add_argument("--warmup", type=int, default=10)
-    ap.add_argument("--batch", type=int, default=None, help="per-GPU batch (default: 2048 for resnet50, else 256)")
+    ap.add_argument("--batch", type=int, default=None, help="per-GPU batch (default: 2048 for resnet50, 1024 for vit_b_16, else 256)")
     ap.add_argument("--model", default="resnet50")
     ap.add_argument("--fp8", action="store_true", help="ViT: fp8 (e4m3/e5m2) GEMMs on the native path")
     ap.add_argument("--backend", default="native", choices=["native", "torch"])

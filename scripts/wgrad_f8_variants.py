@@ -1,7 +1,8 @@
 """Time every fp8 weight-gradient variant (csrc/wgrad_f8.hip) on the ViT-B/16 bs256 linear
-shapes (M = 50432 tokens) against the bf16 weight gradient's best variant.
+shapes (M tokens, default 50432 = bs256; 201728 = bs1024) against the bf16 weight
+gradient's best variant.
 
-    python scripts/wgrad_f8_variants.py
+    python scripts/wgrad_f8_variants.py [M]
 """
 import os
 import sys
@@ -25,7 +26,7 @@ def timed(fn, n=5):
 
 def main():
     lib = no._load()
-    M = 50432
+    M = int(sys.argv[1]) if len(sys.argv) > 1 else 50432
     tot8 = tot16 = 0.0
     for Mo, K in ((2304, 768), (768, 768), (3072, 768), (768, 3072)):
         dy = torch.randn(M, Mo, device="cuda").to(torch.bfloat16)
