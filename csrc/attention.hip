@@ -219,9 +219,7 @@ __global__ void __launch_bounds__(256) attn_delta_kernel(const u16* __restrict__
 #pragma unroll
     for (int e = 0; e < 4; ++e) v += lo_bf(a[e]) * lo_bf(b[e]) + hi_bf(a[e]) * hi_bf(b[e]);
   }
-  v += __shfl_xor(v, 1, 64);
-  v += __shfl_xor(v, 2, 64);
-  v += __shfl_xor(v, 4, 64);
+  v = row8_sum(v);  // the 8 lanes of this row (DPP)
   if (ok && part == 0) {
     const int b = bt / T, t = bt % T;
     delta[((long)b * H + h) * T + t] = v;
@@ -658,9 +656,7 @@ __global__ void __launch_bounds__(512) attn_bwd_dkdv_seq_kernel(AttnSeqBwdParams
 #pragma unroll
       for (int e = 0; e < 4; ++e) v += lo_bf(a[e]) * lo_bf(o[e]) + hi_bf(a[e]) * hi_bf(o[e]);
     }
-    v += __shfl_xor(v, 1, 64);
-    v += __shfl_xor(v, 2, 64);
-    v += __shfl_xor(v, 4, 64);
+    v = row8_sum(v);  // the 8 lanes of this query (DPP)
     if (part == 0) {
       dl_s[q] = v;
       lse_s[q] = q < p.T ? -p.lse[(long)bh * p.T + q] : -INFINITY;

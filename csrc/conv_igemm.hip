@@ -197,12 +197,9 @@ __global__ void __launch_bounds__(256) gemm_stream_kernel(SParams p) {
 #pragma unroll
     for (int j = 0; j < NJ; ++j) {
 #pragma unroll
-      for (int o = 1; o < 16; o <<= 1) {
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          s[j][r] += __shfl_xor(s[j][r], o, 64);
-          q[j][r] += __shfl_xor(q[j][r], o, 64);
-        }
+      for (int r = 0; r < 4; ++r) {  // DPP row = the 16 lanes sharing these columns
+        s[j][r] = row16_sum(s[j][r]);
+        q[j][r] = row16_sum(q[j][r]);
       }
       if (lr == 0) {
         const int col = n0 + j * 16 + (lane >> 4) * 4;

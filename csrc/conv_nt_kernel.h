@@ -705,13 +705,11 @@ __global__ void __launch_bounds__(NTH, PIPE ? 1 : 2) conv_nt_kernel(NTParams p) 
         s[r] = a;
         q[r] = b;
       }
+      // the 16 lanes of a DPP row hold the 16 rows of this column group
 #pragma unroll
-      for (int o = 1; o < 16; o <<= 1) {
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          s[r] += __shfl_xor(s[r], o, 64);
-          q[r] += __shfl_xor(q[r], o, 64);
-        }
+      for (int r = 0; r < 4; ++r) {
+        s[r] = row16_sum(s[r]);
+        q[r] = row16_sum(q[r]);
       }
       if (lrow == 0) {
 #pragma unroll

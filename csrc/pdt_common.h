@@ -71,6 +71,28 @@ __device__ __forceinline__ float warp_max(float v) {
   return v;
 }
 
+// DPP row reductions: a DPP "row" is 16 lanes; the operand permutes ride on the
+// VALU add (no LDS round trip, unlike __shfl_xor's ds_bpermute).
+//   quad_perm [1,0,3,2] (0xB1) = lane ^ 1, quad_perm [2,3,0,1] (0x4E) = lane ^ 2,
+//   row_half_mirror (0x141) = 7 - lane within 8, row_mirror (0x140) = 15 - lane.
+// bound_ctrl set (every source lane is in range anyway) lets the compiler fold the
+// move into the add: one v_add_f32_dpp per step.
+template <int CTRL>
+__device__ __forceinline__ float dpp_f(float v) {
+  return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), CTRL, 0xF, 0xF, true));
+}
+// sum over the 8 lanes (lane & ~7 group); every lane of the group gets it
+__device__ __forceinline__ float row8_sum(float v) {
+  v += dpp_f<0xB1>(v);
+  v += dpp_f<0x4E>(v);
+  return v + dpp_f<0x141>(v);
+}
+// sum over the 16 lanes of a DPP row (same set as xor 1, 2, 4, 8); every lane gets it
+__device__ __forceinline__ float row16_sum(float v) {
+  v = row8_sum(v);
+  return v + dpp_f<0x140>(v);
+}
+
 // Fast unsigned division by a runtime-constant divisor (Granlund-Montgomery).
 struct FastDiv {
   uint32_t d, m, s;

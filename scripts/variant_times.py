@@ -1,5 +1,5 @@
 """Time every conv_nt variant (LDS-tiled 0..37 and streaming 38+) on the ResNet-50
-1x1 GEMM shapes at batch 256, forward (with BN statistics) and data-gradient
+1x1 GEMM shapes at batch 256 (argv[1]: another batch), forward (with BN statistics) and data-gradient
 (plain) epilogues; prints the fastest few per shape with achieved HBM GB/s."""
 import os
 import sys
@@ -17,7 +17,7 @@ SHAPES = [  # K, N, H(out), stride  -- GEMM view: M = 256*H*H rows, K in, N out
 
 
 def main():
-    n = 256
+    n = int(sys.argv[1]) if len(sys.argv) > 1 else 256
     lib = no._load()
     nvar = lib.pdt_conv_nt_num_variants()
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -53,7 +53,7 @@ def main():
             bytes_ = (n * Hi * Hi * K + M * N) * 2
             top = " ".join(f"v{v}:{t:.1f}" for t, v in res[:5])
             stream = " ".join(f"v{v}:{t:.1f}" for t, v in res if v >= 38)
-            print(f"K={K:4d} N={N:4d} H={H:2d} s={s} stats={int(stats)}  best {res[0][0]:6.1f}us "
+            print(f"n={n} K={K:4d} N={N:4d} H={H:2d} s={s} stats={int(stats)}  best {res[0][0]:6.1f}us "
                   f"{bytes_ / res[0][0] / 1e3:6.0f} GB/s | {top} | stream {stream}", flush=True)
 
 
