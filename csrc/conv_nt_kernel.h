@@ -689,37 +689,40 @@ __global__ void __launch_bounds__(NTH, PIPE ? 1 : 2) conv_nt_kernel(NTParams p) 
 
   if (p.stats != nullptr) {
     // per-wave column partials over its BM/2 rows (invalid rows hold zeros)
+    typedef float f32x2 __attribute__((ext_vector_type(2)));
     const int srow = tm * WM + wm;
 #pragma unroll
     for (int j = 0; j < NI; ++j) {
-      float s[4], q[4];
+      // column sums over this lane's MI rows on packed fp32 (v_pk_add / v_pk_fma: 2 columns
+      // each) in the bf16 instantiations; scalar in the fp8 ones (the packed temporaries push
+      // the 256x256 fp8 ring into more scratch, and no fp8 GEMM feeds a BatchNorm)
+      f32x2 s01 = {0.f, 0.f}, s23 = s01, q01 = s01, q23 = s01;
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        float a = 0.f, b = 0.f;
-#pragma unroll
-        for (int i = 0; i < MI; ++i) {
-          float v = acc[i][j][r];
-          a += v;
-          b += v * v;
+      for (int i = 0; i < MI; ++i) {
+        if constexpr (F8 == 0) {
+          const f32x2 v01 = {acc[i][j][0], acc[i][j][1]}, v23 = {acc[i][j][2], acc[i][j][3]};
+          s01 += v01;
+          s23 += v23;
+          q01 = __builtin_elementwise_fma(v01, v01, q01);
+          q23 = __builtin_elementwise_fma(v23, v23, q23);
+        } else {
+          s01.x += acc[i][j][0]; s01.y += acc[i][j][1]; s23.x += acc[i][j][2]; s23.y += acc[i][j][3];
+          q01.x += acc[i][j][0] * acc[i][j][0]; q01.y += acc[i][j][1] * acc[i][j][1];
+          q23.x += acc[i][j][2] * acc[i][j][2]; q23.y += acc[i][j][3] * acc[i][j][3];
         }
-        s[r] = a;
-        q[r] = b;
       }
       // the 16 lanes of a DPP row hold the 16 rows of this column group
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        s[r] = row16_sum(s[r]);
-        q[r] = row16_sum(q[r]);
-      }
-      if (lrow == 0) {
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          int col = n0 + wcol(j) + lcol + r;
-          if (col < p.Ncol) {
-            p.stats[(size_t)srow * p.Ncol + col] = s[r];
-            p.stats[(size_t)(p.nstat_rows + srow) * p.Ncol + col] = q[r];
-          }
-        }
+      float s[4] = {row16_sum(s01.x), row16_sum(s01.y), row16_sum(s23.x), row16_sum(s23.y)};
+      float q[4] = {row16_sum(q01.x), row16_sum(q01.y), row16_sum(q23.x), row16_sum(q23.y)};
+      // every lane of the row now has all 8 sums: lanes 0-3 store sum[r], lanes 4-7 sumsq[r]
+      // (one store per lane instead of eight from one lane)
+      if (lrow < 8) {
+        const int r = lrow & 3;
+        const float sv = (r & 2) ? ((r & 1) ? s[3] : s[2]) : ((r & 1) ? s[1] : s[0]);
+        const float qv = (r & 2) ? ((r & 1) ? q[3] : q[2]) : ((r & 1) ? q[1] : q[0]);
+        const int col = n0 + wcol(j) + lcol + r;
+        if (col < p.Ncol)
+          p.stats[(size_t)((lrow < 4 ? 0 : p.nstat_rows) + srow) * p.Ncol + col] = lrow < 4 ? sv : qv;
       }
     }
   }
