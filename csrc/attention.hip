@@ -73,14 +73,9 @@ __device__ __forceinline__ bf16x8 tr_frag2(const char* lds, int kb0, int kb1, in
   return r;
 }
 
-__device__ __forceinline__ float xor_max4(float v) {
-  v = fmaxf(v, __shfl_xor(v, 16, 64));
-  return fmaxf(v, __shfl_xor(v, 32, 64));
-}
-__device__ __forceinline__ float xor_sum4(float v) {
-  v += __shfl_xor(v, 16, 64);
-  return v + __shfl_xor(v, 32, 64);
-}
+// reductions over lanes l, l^16, l^32, l^48 (permlane swaps, see pdt_common.h)
+__device__ __forceinline__ float xor_max4(float v) { return xor32_reduce(xor16_reduce(v, MaxOp{}), MaxOp{}); }
+__device__ __forceinline__ float xor_sum4(float v) { return xor32_reduce(xor16_reduce(v, AddOp{}), AddOp{}); }
 
 __device__ __forceinline__ bf16x8 pack_p(const f32x4& a, const f32x4& b) {
   bf16x8 r;

@@ -212,7 +212,7 @@ __global__ void __launch_bounds__(256) attn_fwd_f8_kernel(AttnF8Params p) {
         s[r] = v;
         mt = fmaxf(mt, v);
       }
-      mt = fmaxf(mt, __shfl_xor(mt, 32, 64));  // the other 16 keys of this query
+      mt = xor32_reduce(mt, MaxOp{});  // the other 16 keys of this query
       const float mn = fmaxf(m, mt);
       const float alpha = exp2f(m - mn);  // m = -inf first: 0
       float ls = 0.f;
@@ -222,7 +222,7 @@ __global__ void __launch_bounds__(256) attn_fwd_f8_kernel(AttnF8Params p) {
         s[r] = e;
         ls += e;
       }
-      ls += __shfl_xor(ls, 32, 64);
+      ls = xor32_reduce(ls, AddOp{});
       l = l * alpha + ls;
       m = mn;
 #pragma unroll

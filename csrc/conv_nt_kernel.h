@@ -656,14 +656,24 @@ __global__ void __launch_bounds__(NTH, PIPE ? 1 : 2) conv_nt_kernel(NTParams p) 
         }
       }
     }
-    // lanes sharing a chunk column: lane, lane ^ CPR, ... (CPR < 64)
+    // lanes sharing a chunk column: lane, lane ^ CPR, ... (CPR < 64); the xor-16 / xor-32
+    // steps on the permlane swaps (VALU), smaller strides on ds_bpermute
 #pragma unroll
-    for (int o = CPR; o < 64; o <<= 1)
+    for (int o = CPR; o < 16; o <<= 1)
 #pragma unroll
       for (int k = 0; k < 8; ++k) {
         s[k] += __shfl_xor(s[k], o, 64);
         q[k] += __shfl_xor(q[k], o, 64);
       }
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      if constexpr (CPR <= 16) {
+        s[k] = xor16_reduce(s[k], AddOp{});
+        q[k] = xor16_reduce(q[k], AddOp{});
+      }
+      s[k] = xor32_reduce(s[k], AddOp{});
+      q[k] = xor32_reduce(q[k], AddOp{});
+    }
     constexpr int NW = NTH / 64;
     float* red = reinterpret_cast<float*>(smem);  // [NW][CPR][16], staging reads are done after the barrier
     __syncthreads();

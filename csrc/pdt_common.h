@@ -59,18 +59,6 @@ __device__ __forceinline__ uint32_t pack2bf(float lo, float hi) {
 __device__ __forceinline__ float lo_bf(uint32_t w) { return __uint_as_float(w << 16); }
 __device__ __forceinline__ float hi_bf(uint32_t w) { return __uint_as_float(w & 0xffff0000u); }
 
-__device__ __forceinline__ float warp_sum(float v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-  return v;
-}
-
-__device__ __forceinline__ float warp_max(float v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
-  return v;
-}
-
 // DPP row reductions: a DPP "row" is 16 lanes; the operand permutes ride on the
 // VALU add (no LDS round trip, unlike __shfl_xor's ds_bpermute).
 //   quad_perm [1,0,3,2] (0xB1) = lane ^ 1, quad_perm [2,3,0,1] (0x4E) = lane ^ 2,
@@ -91,6 +79,42 @@ __device__ __forceinline__ float row8_sum(float v) {
 __device__ __forceinline__ float row16_sum(float v) {
   v = row8_sum(v);
   return v + dpp_f<0x140>(v);
+}
+
+template <typename Op>
+__device__ __forceinline__ float row16_reduce(float v, Op op) {
+  v = op(v, dpp_f<0xB1>(v));
+  v = op(v, dpp_f<0x4E>(v));
+  v = op(v, dpp_f<0x141>(v));
+  return op(v, dpp_f<0x140>(v));
+}
+
+// Cross-row lane exchanges on gfx950's v_permlane{16,32}_swap (VALU, no LDS): swapping a
+// register with itself leaves {x[l], x[l ^ 32]} (resp. x[l ^ 16]) in the two results, so
+// op(r0, r1) equals op(v, __shfl_xor(v, 32)) bit for bit (op commutative).
+template <typename Op>
+__device__ __forceinline__ float xor32_reduce(float v, Op op) {
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return op(__uint_as_float(r[0]), __uint_as_float(r[1]));
+}
+template <typename Op>
+__device__ __forceinline__ float xor16_reduce(float v, Op op) {
+  const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return op(__uint_as_float(r[0]), __uint_as_float(r[1]));
+}
+struct AddOp {
+  __device__ float operator()(float a, float b) const { return a + b; }
+};
+struct MaxOp {
+  __device__ float operator()(float a, float b) const { return fmaxf(a, b); }
+};
+
+// whole-wave reductions (every lane gets the result): 2 permlane swaps + 4 DPP steps
+__device__ __forceinline__ float warp_sum(float v) {
+  return row16_reduce(xor16_reduce(xor32_reduce(v, AddOp{}), AddOp{}), AddOp{});
+}
+__device__ __forceinline__ float warp_max(float v) {
+  return row16_reduce(xor16_reduce(xor32_reduce(v, MaxOp{}), MaxOp{}), MaxOp{});
 }
 
 // Fast unsigned division by a runtime-constant divisor (Granlund-Montgomery).
