@@ -48,7 +48,7 @@ def main():
     a = ap.parse_args()
     torch.backends.cudnn.benchmark = True
     N = a.batch
-    tot = {"nf": 0, "sf": 0, "nd": 0, "sd": 0, "nw": 0, "sw": 0}
+    tot = {"nf": 0, "nf0": 0, "sf": 0, "nd": 0, "sd": 0, "nw": 0, "sw": 0}
     print(f"{'shape':34s} {'fwd nat/stk us':>18s} {'dgrad nat/stk':>18s} {'wgrad nat/stk':>18s}  TFLOPs(fwd nat)")
     for Cin, H, Cout, k, s, cnt in SHAPES:
         p = k // 2
@@ -61,6 +61,7 @@ def main():
         wb = no.bf16_weight(conv.weight, pad_cin_to=Cs if Cs != Cin else None)
         wbt = conv.weight.detach().to(torch.bfloat16)
         nf = timeit(lambda: no._conv_forward(xs, wb, N, H, H, Cs, Cout, g, with_stats=True), a.iters)
+        nf0 = timeit(lambda: no._conv_forward(xs, wb, N, H, H, Cs, Cout, g, with_stats=False), a.iters)
         sf = timeit(lambda: F.conv2d(x, wbt, None, s, p), a.iters)
         y = F.conv2d(x, wbt, None, s, p)
         dy = torch.randn_like(y)
@@ -85,8 +86,10 @@ def main():
               f"  eff {ff / nf:4.0%}/{(f'{fd / nd:4.0%}' if nd else '   -')}/{fw / nw:4.0%}", flush=True)
         for key, v in (("ff", ff), ("fd", fd), ("fw", fw)):
             tot[key] = tot.get(key, 0.0) + v * cnt
-        for key, v in (("nf", nf), ("sf", sf), ("nd", nd), ("sd", sd), ("nw", nw), ("sw", sw)):
+        print(f"{'':34s} fwd without the BN-statistics epilogue: {nf0:8.1f} us", flush=True)
+        for key, v in (("nf", nf), ("nf0", nf0), ("sf", sf), ("nd", nd), ("sd", sd), ("nw", nw), ("sw", sw)):
             tot[key] += v * cnt
+    print("weighted fwd total without statistics (ms): native %.2f vs stock %.2f" % (tot["nf0"] / 1e3, tot["sf"] / 1e3))
     print("weighted totals (ms, per ResNet-50 step): fwd %.2f/%.2f dgrad %.2f/%.2f wgrad %.2f/%.2f" % (
         tot["nf"] / 1e3, tot["sf"] / 1e3, tot["nd"] / 1e3, tot["sd"] / 1e3, tot["nw"] / 1e3, tot["sw"] / 1e3))
     print("roofline floors (ms): fwd %.2f dgrad %.2f wgrad %.2f" % (tot["ff"] / 1e3, tot["fd"] / 1e3,
