@@ -163,3 +163,24 @@ PDT_API int pdt_add_bf16(const void* a, const void* b, void* y, long n, hipStrea
                      n / 8);
   PDT_RETURN_LAUNCH();
 }
+
+// Probe of the cross-lane reduction primitives (pdt_common.h) for the unit tests: one
+// wave per 64 inputs; out[6][n] = row16_sum, row8_sum, xor16+xor32 sum (4 lanes l^16k),
+// xor32 max, warp_sum, warp_max of each lane's value.
+__global__ void __launch_bounds__(64) lane_reduce_probe_kernel(const float* __restrict__ x, float* __restrict__ out,
+                                                               int n) {
+  const int i = blockIdx.x * 64 + threadIdx.x;  // n is a multiple of 64 (host check)
+  const float v = x[i];
+  out[i] = row16_sum(v);
+  out[n + i] = row8_sum(v);
+  out[2 * n + i] = xor32_reduce(xor16_reduce(v, AddOp{}), AddOp{});
+  out[3 * n + i] = xor32_reduce(v, MaxOp{});
+  out[4 * n + i] = warp_sum(v);
+  out[5 * n + i] = warp_max(v);
+}
+
+PDT_API int pdt_lane_reduce_probe(const float* x, float* out, int n, hipStream_t st) {
+  if (n <= 0 || n % 64) return -1;
+  hipLaunchKernelGGL(lane_reduce_probe_kernel, dim3(n / 64), dim3(64), 0, st, x, out, n);
+  PDT_RETURN_LAUNCH();
+}

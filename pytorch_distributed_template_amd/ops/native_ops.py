@@ -80,6 +80,7 @@ _SIGS = {
     "pdt_adam_step": (c_int, [P, c_int, P, P, P, P, P, P] + [c_float] * 5 + [c_int, c_float, c_float, c_float, P]),
     "pdt_fill_uniform_bf16": (c_int, [P, c_long, c_uint, P]),
     "pdt_cast_f32_bf16": (c_int, [P, P, c_long, P]),
+    "pdt_lane_reduce_probe": (c_int, [P, P, c_int, P]),
     "pdt_wt_dgrad": (c_int, [P, P] + [c_int] * 9 + [P]),
     "pdt_transpose_cast": (c_int, [P, P, c_int, c_int, P]),
     "pdt_wt_job_size": (c_int, []),

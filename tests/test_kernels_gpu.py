@@ -663,3 +663,28 @@ def test_fp8_delayed_scaling_history():
     torch.cuda.synchronize()
     assert abs(dq3.item() - 4 * amax1 / 448.0) < 1e-5 * amax1
     assert nrmerr(_f8(q3, 0) * dq3, x2) < 0.03
+
+
+def test_lane_reduction_primitives():
+    """DPP row sums and gfx950 permlane16/32-swap exchanges (csrc/pdt_common.h) against
+    the same lane groups reduced in fp64 on the host: sums to fp32 rounding, maxima exact."""
+    torch.manual_seed(0)
+    n = 64 * 37
+    x = torch.randn(n, device="cuda", dtype=torch.float32)
+    out = torch.empty(6, n, device="cuda", dtype=torch.float32)
+    assert no._load().pdt_lane_reduce_probe(no._p(x), no._p(out), n, no._s()) == 0
+    torch.cuda.synchronize()
+    w = x.double().view(-1, 64)  # [wave][lane]
+    lane = torch.arange(64)
+    row16 = w.view(-1, 4, 16).sum(-1).repeat_interleave(16, dim=1)
+    row8 = w.view(-1, 8, 8).sum(-1).repeat_interleave(8, dim=1)
+    x4 = w.view(-1, 4, 16).sum(1).repeat(1, 4)                     # lanes l, l^16, l^32, l^48
+    m32 = torch.maximum(w, w[:, lane ^ 32])
+    wsum = w.sum(1, keepdim=True).expand(-1, 64)
+    wmax = w.max(1, keepdim=True).values.expand(-1, 64)
+    o = out.double().view(6, -1, 64)
+    for k, ref in enumerate((row16, row8, x4)):
+        assert (o[k] - ref).abs().max().item() < 1e-5, k
+    assert torch.equal(o[3], m32)
+    assert (o[4] - wsum).abs().max().item() < 1e-4
+    assert torch.equal(o[5], wmax)
