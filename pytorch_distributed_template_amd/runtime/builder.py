@@ -7,13 +7,14 @@ Registries (``init_obj`` lookups, searched in order):
   loaders     -> pytorch_distributed_template_amd.data
   loss        -> pytorch_distributed_template_amd.models.loss
   metrics     -> pytorch_distributed_template_amd.models.metric
-  optimizer   -> pytorch_distributed_template_amd.optim, then torch.optim
+  optimizer   -> pytorch_distributed_template_amd.optim, then torch.optim (SGD / Adam /
+                 AdamW become the fused HIP optimizers on the native GPU path)
   lr_scheduler-> torch.optim.lr_scheduler (optional: null / missing disables it)
 
 Extra (optional) ``trainer`` keys, all defaulting to reference behaviour:
   precision "fp32"|"bf16", channels_last bool, backend "auto"|"native"|"torch",
   ddp {bucket_cap_mb, broadcast_buffers, gradient_as_bucket_view, comm_hook},
-  len_epoch int (iteration-based epochs), log_images bool.
+  len_epoch int (iteration-based epochs), log_images bool, fused_optimizer bool.
 """
 from __future__ import annotations
 
@@ -45,9 +46,30 @@ def build_criterion_metrics(config):
     return criterion, metrics
 
 
+# torch.optim names a config may use -> the multi-tensor HIP optimizer with the same
+# semantics and interchangeable state_dict (optim/fused.py), and the args it accepts
+_FUSED_FOR = {
+    "SGD": ("FusedSGD", {"lr", "momentum", "dampening", "weight_decay", "nesterov"}),
+    "Adam": ("FusedAdam", {"lr", "betas", "eps", "weight_decay", "amsgrad"}),
+    "AdamW": ("FusedAdamW", {"lr", "betas", "eps", "weight_decay", "amsgrad"}),
+}
+
+
 def build_optimizer(config, model):
+    """``optimizer.type`` is looked up in ``optim`` first, then ``torch.optim``. On the
+    native GPU path a torch.optim SGD / Adam / AdamW (e.g. the reference's ``"Adam"``)
+    becomes its fused HIP counterpart -- one launch per step instead of torch's foreach
+    kernels -- unless ``trainer.fused_optimizer`` is false."""
     params = [p for p in model.parameters() if p.requires_grad]
-    optimizer = config.init_obj("optimizer", [module_optim, torch.optim], params)
+    ocfg = config["optimizer"]
+    fused_name, allowed = _FUSED_FOR.get(ocfg["type"], (None, None))
+    if (fused_name and config["trainer"].get("fused_optimizer", True) and params
+            and set(ocfg.get("args", {})) <= allowed and fused.use_native(params[0])):
+        # fp32-only models (LeNet) read no bf16 weight shadow
+        optimizer = getattr(module_optim, fused_name)(params, **dict(ocfg.get("args", {})),
+                                                      write_bf16_shadow=config["trainer"].get("precision") == "bf16")
+    else:
+        optimizer = config.init_obj("optimizer", [module_optim, torch.optim], params)
     lr_scheduler = None
     if config.get("lr_scheduler"):
         lr_scheduler = config.init_obj("lr_scheduler", torch.optim.lr_scheduler, optimizer)

@@ -136,3 +136,27 @@ def test_mnist_config_step_uses_native_path():
         opt.step()
         losses.append(loss.item())
     assert losses[-1] < losses[0] * 0.7, losses
+
+
+def test_config_adam_becomes_fused_on_gpu_and_matches_torch():
+    """The reference config's "Adam" runs as FusedAdam on the native GPU path (one HIP
+    launch per step) and tracks torch.optim.Adam(amsgrad) on the same gradients."""
+    from pytorch_distributed_template_amd.optim import FusedAdam
+    from pytorch_distributed_template_amd.runtime.builder import build_optimizer
+    from test_optim_cpu import _mnist_opt_cfg
+    torch.manual_seed(0)
+    a = _model(3)
+    b = _model(3)
+    b.load_state_dict(a.state_dict())
+    oa, _ = build_optimizer(_mnist_opt_cfg(), a)
+    ob = torch.optim.Adam(b.parameters(), lr=1e-3, weight_decay=0, amsgrad=True)
+    assert isinstance(oa, FusedAdam) and not oa.write_bf16_shadow
+    for _ in range(5):
+        for m, o in ((a, oa), (b, ob)):
+            o.zero_grad()
+            for p in m.parameters():
+                p.grad = torch.sin(p.detach() * 3.0 + 1.0)
+            o.step()
+    for pa, pb in zip(a.parameters(), b.parameters()):
+        assert torch.allclose(pa, pb, rtol=1e-5, atol=1e-6)
+    assert set(oa.state_dict()["state"][0]) == set(ob.state_dict()["state"][0])

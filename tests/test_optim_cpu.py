@@ -31,3 +31,25 @@ def test_cpu_fallback_matches_torch(kind):
         assert torch.allclose(p, q, atol=1e-6), (p - q).abs().max()
     sd = a.state_dict()
     b.load_state_dict(sd)
+
+
+class _Cfg(dict):
+    """The two ConfigParser calls build_optimizer makes: cfg[key] and init_obj."""
+
+    def init_obj(self, name, module, *args):
+        spec = self[name]
+        for m in (module if isinstance(module, (list, tuple)) else [module]):
+            if hasattr(m, spec["type"]):
+                return getattr(m, spec["type"])(*args, **spec["args"])
+        raise AttributeError(spec["type"])
+
+
+def _mnist_opt_cfg(**trainer):
+    return _Cfg(optimizer={"type": "Adam", "args": {"lr": 1e-3, "weight_decay": 0, "amsgrad": True}},
+                trainer=dict(trainer))
+
+
+def test_build_optimizer_keeps_torch_adam_on_cpu():
+    from pytorch_distributed_template_amd.runtime.builder import build_optimizer
+    opt, sched = build_optimizer(_mnist_opt_cfg(), torch.nn.Linear(4, 3))
+    assert type(opt) is torch.optim.Adam and sched is None
