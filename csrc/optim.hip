@@ -27,22 +27,54 @@ __global__ void sgd_kernel(const Chunk* __restrict__ chunks, int nchunks, float*
                            const float* const* __restrict__ grads, float* const* __restrict__ bufs,
                            u16* const* __restrict__ shadows, float lr, float momentum, float dampening, float wd,
                            int nesterov, int first, float grad_scale) {
+  // one element: returns the new parameter, updates the momentum buffer value in place
+  auto upd = [&](float gi, float pi, float& bi, bool has_b) {
+    gi *= grad_scale;
+    if (wd != 0.f) gi += wd * pi;
+    if (momentum != 0.f && has_b) {
+      bi = first ? gi : momentum * bi + (1.f - dampening) * gi;
+      gi = nesterov ? gi + momentum * bi : bi;
+    }
+    return pi - lr * gi;
+  };
   for (int c = blockIdx.x; c < nchunks; c += gridDim.x) {
     const Chunk ch = chunks[c];
     float* p = params[ch.tensor] + ch.offset;
     const float* g = grads[ch.tensor] + ch.offset;
     float* b = bufs ? (bufs[ch.tensor] ? bufs[ch.tensor] + ch.offset : nullptr) : nullptr;
     u16* sh = shadows ? (shadows[ch.tensor] ? shadows[ch.tensor] + ch.offset : nullptr) : nullptr;
-    for (long i = threadIdx.x; i < ch.len; i += NT) {
-      float gi = g[i] * grad_scale;
-      float pi = p[i];
-      if (wd != 0.f) gi += wd * pi;
-      if (momentum != 0.f && b) {
-        float bi = first ? gi : momentum * b[i] + (1.f - dampening) * gi;
-        b[i] = bi;
-        gi = nesterov ? gi + momentum * bi : bi;
+    const bool hb = b != nullptr;
+    long i0 = 0;
+    // 16-B vector path when every stream is aligned (gradients can be unaligned views
+    // into DDP's buckets): 4 elements per lane, all loads issued before the math
+    const uintptr_t al = (uintptr_t)p | (uintptr_t)g | (hb ? (uintptr_t)b : 0);
+    if ((al & 15) == 0 && (!sh || ((uintptr_t)sh & 7) == 0)) {
+      const long n4 = ch.len >> 2;
+      for (long j = threadIdx.x; j < n4; j += NT) {
+        const f32x4 gv = reinterpret_cast<const f32x4*>(g)[j];
+        f32x4 pv = reinterpret_cast<const f32x4*>(p)[j];
+        f32x4 bv = hb ? reinterpret_cast<const f32x4*>(b)[j] : f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          float be = bv[e];
+          pv[e] = upd(gv[e], pv[e], be, hb);
+          bv[e] = be;
+        }
+        reinterpret_cast<f32x4*>(p)[j] = pv;
+        if (hb && momentum != 0.f) reinterpret_cast<f32x4*>(b)[j] = bv;
+        if (sh) {
+          uint2 w;
+          w.x = pack2bf(pv[0], pv[1]);
+          w.y = pack2bf(pv[2], pv[3]);
+          reinterpret_cast<uint2*>(sh)[j] = w;
+        }
       }
-      pi -= lr * gi;
+      i0 = n4 << 2;
+    }
+    for (long i = i0 + threadIdx.x; i < ch.len; i += NT) {
+      float bi = hb ? b[i] : 0.f;
+      const float pi = upd(g[i], p[i], bi, hb);
+      if (hb && momentum != 0.f) b[i] = bi;
       p[i] = pi;
       if (sh) sh[i] = f2bf(pi);
     }
