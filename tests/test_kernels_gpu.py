@@ -688,3 +688,31 @@ def test_lane_reduction_primitives():
     assert torch.equal(o[3], m32)
     assert (o[4] - wsum).abs().max().item() < 1e-4
     assert torch.equal(o[5], wmax)
+
+
+def test_fused_sgd_unaligned_and_aligned_chunks_match_torch():
+    """FusedSGD's 16-B vector path (aligned chunks) and scalar fallback (parameters and
+    gradients that are unaligned views, as DDP bucket views can be) against torch.optim.SGD."""
+    from pytorch_distributed_template_amd.optim import FusedSGD
+    torch.manual_seed(0)
+    sizes = (40000, 70001, 13)  # chunk tails not a multiple of 4, several chunks
+    for off in (0, 1, 3):
+        flat = torch.randn(sum(sizes) + off, device="cuda")
+        gflat = torch.randn(sum(sizes) + off, device="cuda")
+        ps, ref = [], []
+        o = off
+        for n in sizes:
+            p = flat[o:o + n]
+            p.grad = gflat[o:o + n]
+            q = p.detach().clone()
+            q.grad = p.grad.clone()
+            ps.append(p)
+            ref.append(q)
+            o += n
+        kw = dict(lr=0.1, momentum=0.9, weight_decay=1e-4, nesterov=True)
+        a, b = FusedSGD(ps, write_bf16_shadow=False, **kw), torch.optim.SGD(ref, **kw)
+        for _ in range(3):
+            a.step()
+            b.step()
+        for p, q in zip(ps, ref):
+            assert torch.allclose(p, q, rtol=1e-6, atol=1e-6), off
