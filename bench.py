@@ -7,7 +7,9 @@ RCCL (xGMI) when N > 1. Weak scaling: the per-GPU batch is fixed.
 
 Each timed step is a full training step: forward, softmax-cross-entropy,
 backward (DDP bucketed all-reduce over RCCL overlapped with it), optimizer
-step (SGD momentum + weight decay). Nothing is skipped or cached.
+step (SGD momentum + weight decay). Nothing is skipped or cached. N = 1 runs
+the same path: a 1-rank RCCL process group and the DDP reducer (``--no-ddp``
+drops both for an A/B).
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B]
                     [--model resnet50|resnet152|vit_b_16] [--backend native|torch]
@@ -40,8 +42,8 @@ BASELINE_METRIC = "images/sec (whole node) ResNet-50 synthetic 3x224x224 at 1/2/
 # BASELINE.md. Scaled by N for N GPUs (weak scaling).
 STOCK_1GPU_IMG_S = {("resnet50", 256): 6605.4, ("resnet50", 512): 6863.8,
                     ("vit_b_16", 256): 3547.25, ("vit_b_16", 1024): 4059.96}
-# At a batch the stock stack was not measured at (its MIOpen find at bs 1024 ran
-# past 390 s on one box), compare against its BEST measured per-GPU throughput.
+# The stock stack's BEST measured per-GPU throughput (and its batch): reported as
+# ``vs_best_stock``, never as ``vs_baseline``.
 STOCK_BEST_1GPU_IMG_S = {"resnet50": (6863.8, 512), "vit_b_16": (4059.96, 1024)}
 # Per-GPU batch: 2048 images (82 GiB of the 288 GiB HBM3E; weak scaling, so the
 # 8-GPU job holds 16384 images). The stage-3/4 GEMMs (M = N*14*14, N*7*7) fill all
@@ -68,8 +70,16 @@ def parse():
     ap.add_argument("--comm-hook", default=None, choices=[None, "bf16"])
     ap.add_argument("--graph", action="store_true", help="capture the whole training step in a HIP graph")
     ap.add_argument("--json-out", default=None)
+    ap.add_argument("--miopen-find", type=int, default=1, choices=[0, 1],
+                    help="torch backend: 1 = cudnn.benchmark (MIOpen find), 0 = immediate mode")
     ap.add_argument("--dist-backend", default=None, choices=[None, "nccl", "gloo"],
                     help="gloo: rehearse N ranks sharing GPU 0 (gradient all-reduce on the host); default RCCL")
+    ap.add_argument("--data", default="sampler", choices=["sampler", "pool"],
+                    help="sampler: SyntheticImageNet index batches from DistributedSampler, images made on device "
+                         "every step (the config loader); pool: two pre-made resident batches")
+    ap.add_argument("--no-ddp", action="store_true",
+                    help="N=1 only: no process group and no DDP wrapper (A/B against the default 1-rank "
+                         "RCCL group + DDP reducer that every N>1 rank also runs)")
     ap.add_argument("--device", default="cuda", choices=["cuda", "cpu"],
                     help="cpu: gloo ranks on the host with stock torch ops (launcher/plumbing rehearsal)")
     ap.add_argument("--image-size", type=int, default=224, help="only for --device cpu rehearsals")
@@ -136,11 +146,15 @@ def _dtype_label(args) -> str:
             f"wgrad GEMMs)+bf16")
 
 
+def pdist_ready() -> bool:
+    return torch.distributed.is_available() and torch.distributed.is_initialized()
+
+
 def allreduce_probe(model, device, world, iters=10):
     """Time an all-reduce of one gradient-sized fp32 buffer on the job's process group
     (outside the timed region): the xGMI/RCCL evidence of a multi-GPU run, recorded in
     the JSON next to the throughput. busbw = 2(n-1)/n * bytes / time (ring-equivalent)."""
-    if world <= 1 or device.type != "cuda":
+    if not pdist_ready() or device.type != "cuda":
         return None
     n = sum(p.numel() for p in model.parameters() if p.requires_grad)
     buf = torch.ones(n, dtype=torch.float32, device=device)
@@ -186,12 +200,16 @@ def main():
     from pytorch_distributed_template_amd.ops import fused
     from pytorch_distributed_template_amd import models
     from pytorch_distributed_template_amd.parallel import pretune_for_ddp, wrap_ddp
-    from pytorch_distributed_template_amd.data.synthetic import SyntheticImageLoader
+    from pytorch_distributed_template_amd.data.synthetic import SyntheticImageLoader, SyntheticImageNetLoader
 
     cpu = args.device == "cpu"
     shared = args.dist_backend == "gloo" and not cpu
-    device = pdist.init_distributed(backend=args.dist_backend, device_index=0 if shared else None) if not cpu \
-        else pdist.init_distributed(backend="gloo")
+    # N = 1 runs the same DDP-over-RCCL path as every rank of an N > 1 job: a 1-rank
+    # process group (RCCL on the GPU) and the DDP reducer with its bucketed all-reduce
+    one_rank_pg = args.gpus == 1 and not args.no_ddp
+    device = pdist.init_distributed(backend=args.dist_backend, device_index=0 if shared else None,
+                                    single_rank_group=one_rank_pg) if not cpu \
+        else pdist.init_distributed(backend="gloo", single_rank_group=one_rank_pg)
     world = pdist.get_world_size()
     rank = pdist.get_rank()
     if cpu:
@@ -201,7 +219,7 @@ def main():
     state = {"phase": "setup", "step": 0}
     hb = heartbeat(rank, state)
     fused.set_backend(args.backend)
-    torch.backends.cudnn.benchmark = True
+    torch.backends.cudnn.benchmark = bool(args.miopen_find)
 
     torch.manual_seed(1234)
     ctor = {"resnet50": models.resnet50, "resnet152": models.resnet152, "vit_b_16": models.vit_b_16}[args.model]
@@ -216,15 +234,38 @@ def main():
         opt_name = "SGD(momentum=0.9, wd=5e-5)"
         opt = (FusedSGD if args.backend == "native" else torch.optim.SGD)(model.parameters(), lr=0.1, momentum=0.9,
                                                                           weight_decay=5e-5)
-    loader = SyntheticImageLoader(args.batch, num_samples=args.batch * (args.steps + args.warmup + 2) * world,
-                                  dtype="float32" if cpu else "bfloat16", pool=2, device=device,
-                                  image_size=args.image_size)
-    batches = list(iter(loader))[:2]
+    dtype = "float32" if cpu else "bfloat16"
+    if args.data == "pool":
+        loader = SyntheticImageLoader(args.batch, num_samples=args.batch * (args.steps + args.warmup + 2) * world,
+                                      dtype=dtype, pool=2, device=device, image_size=args.image_size)
+        pooled = list(iter(loader))[:2]
+
+        def next_batch(i):
+            return pooled[i % 2]
+    else:
+        # the reference's data path: DistributedSampler shards the (synthetic) dataset over
+        # the ranks; each step's index batch becomes images in one device launch
+        loader = SyntheticImageNetLoader(args.batch, num_samples=args.batch * 64 * world, dtype=dtype,
+                                         device=device, image_size=args.image_size)
+
+        def _forever():
+            epoch = 0
+            while True:
+                loader.set_epoch(epoch)
+                for b in loader:
+                    if b[0].shape[0] == args.batch:
+                        yield b
+                epoch += 1
+
+        _it = _forever()
+
+        def next_batch(i):
+            return next(_it)
     autocast = args.backend == "torch" and not cpu
     dev_type = device.type
 
     def _pretune_step():
-        x, y = batches[0]
+        x, y = next_batch(0)
         fused.softmax_cross_entropy(model(x), y).backward()
 
     # N ranks: rank 0 tunes the kernel variants once and broadcasts them (no per-rank timing)
@@ -234,7 +275,7 @@ def main():
                      gradient_as_bucket_view=True, comm_hook=args.comm_hook)
 
     def step(i):
-        x, y = batches[i % 2]
+        x, y = next_batch(i)
         opt.zero_grad(set_to_none=True)
         with torch.autocast(dev_type, dtype=torch.bfloat16, enabled=autocast):
             out = model(x)
@@ -245,8 +286,14 @@ def main():
 
     if args.graph:
         # static input buffers; each replayed step first copies the next batch in
-        sx = batches[0][0].clone()
-        sy = batches[0][1].clone()
+        x0, y0 = next_batch(0)
+        sx, sy = x0.clone(), y0.clone()
+        if getattr(x0, "pdt_nhwc_pad", None):  # keep the padded-NHWC view the stem reads in place
+            from pytorch_distributed_template_amd.ops.native_ops import nhwc_padded_view
+            cp = x0.pdt_nhwc_pad
+            sbuf = nhwc_padded_view(x0, cp).clone(memory_format=torch.channels_last)
+            sx = sbuf[:, :x0.shape[1]]
+            sx.pdt_nhwc_pad = cp
 
         def gstep():
             opt.zero_grad(set_to_none=False)
@@ -261,8 +308,9 @@ def main():
         side.wait_stream(torch.cuda.current_stream())
         with torch.cuda.stream(side):
             for i in range(max(3, args.warmup)):
-                sx.copy_(batches[i % 2][0])
-                sy.copy_(batches[i % 2][1])
+                xb, yb = next_batch(i)
+                sx.copy_(xb)
+                sy.copy_(yb)
                 gstep()
         torch.cuda.current_stream().wait_stream(side)
         graph = torch.cuda.CUDAGraph()
@@ -270,8 +318,9 @@ def main():
             static_loss = gstep()
 
         def step(i):  # noqa: F811
-            sx.copy_(batches[i % 2][0])
-            sy.copy_(batches[i % 2][1])
+            xb, yb = next_batch(i)
+            sx.copy_(xb)
+            sy.copy_(yb)
             graph.replay()
             return static_loss
 
@@ -295,18 +344,18 @@ def main():
     elapsed = time.perf_counter() - t0
     hb.set()
     t = torch.tensor([elapsed], dtype=torch.float64, device=device)
-    if world > 1:
+    if pdist_ready():
         torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
     elapsed = float(t.item())
     final_loss = float(loss.item())
 
     ms = elapsed / args.steps * 1e3
     value = world * args.batch * args.steps / elapsed
+    # vs_baseline only against the stock stack measured at the SAME per-GPU batch (else
+    # null); the ratio to the stock stack's best measured batch is a separately named field
     stock = STOCK_1GPU_IMG_S.get((args.model, args.batch))
     stock_ref = f"stock PyTorch-ROCm at per-GPU batch {args.batch}" if stock else None
-    if stock is None and args.model in STOCK_BEST_1GPU_IMG_S:
-        stock, sb = STOCK_BEST_1GPU_IMG_S[args.model]
-        stock_ref = f"stock PyTorch-ROCm best measured (per-GPU batch {sb})"
+    best = STOCK_BEST_1GPU_IMG_S.get(args.model)
     rec = {
         "metric": BASELINE_METRIC if args.model == "resnet50" else f"images/sec (whole node) {args.model} synthetic",
         "value": round(value, 2),
@@ -319,15 +368,20 @@ def main():
         "scaling": "weak",
         "vs_baseline": round(value / (stock * world), 4) if stock else None,
         "dtype": _dtype_label(args),
-        "data": f"synthetic (device-resident random 3x{args.image_size}x{args.image_size}, random-init weights)",
+        "data": (f"synthetic 3x{args.image_size}x{args.image_size}, random-init weights; " +
+                 ("SyntheticImageNet index batches from DistributedSampler, images generated on device each step"
+                  if args.data == "sampler" else "two pre-made device-resident batches")),
         "config": {"model": args.model, "global_batch": args.batch * world, "per_gpu_batch": args.batch,
                    "seq_len": None, "image_size": args.image_size, "parallelism": f"dp{world}",
                    "backend": args.backend, "optimizer": opt_name,
-                   "bucket_cap_mb": args.bucket_mb, "dist_backend": (torch.distributed.get_backend() if world > 1 else "none (1 rank)"),
+                   "bucket_cap_mb": args.bucket_mb, "dist_backend": (torch.distributed.get_backend() if pdist_ready() else "none (no process group)"),
+                   "ddp": type(model).__name__ == "DistributedDataParallel",
                    "rccl_version": _rccl_version(), "device": args.device,
                    "final_loss": round(final_loss, 4), "hip_graph": args.graph,
                    "cpu_issue_ms_per_step": round(cpu_issue / args.steps * 1e3, 3),
                    "baseline": stock_ref,
+                   "vs_best_stock": ({"ratio": round(value / (best[0] * world), 4), "stock_img_s": best[0],
+                                      "stock_per_gpu_batch": best[1]} if best else None),
                    "grad_allreduce_probe": ar,
                    "max_mem_gib": round(torch.cuda.max_memory_allocated() / 2 ** 30, 2) if not cpu else None},
     }

@@ -305,28 +305,37 @@ __global__ void __launch_bounds__(NT) lenet_grad_reduce_kernel(const float* __re
   out[j] = acc;
 }
 
-// NLL loss (mean over targets != ignore_index) of log-probabilities [B][C]
+// NLL loss (mean over targets != ignore_index) of log-probabilities [B][C].
+// A target outside [0, C) that is not ignore_index is an error (torch raises): the
+// kernel counts them into bad[0] (the host checks it lazily, without a sync in the
+// step) and poisons the loss with a NaN so the error cannot train silently.
 __global__ void __launch_bounds__(NT) nll_fwd_kernel(const float* __restrict__ logp, const int64_t* __restrict__ tgt,
                                                      int B, int C, int ignore, float* __restrict__ loss,
-                                                     float* __restrict__ count) {
-  __shared__ float rs[NT / 64], rc[NT / 64];
-  float s = 0.f, n = 0.f;
+                                                     float* __restrict__ count, float* __restrict__ bad) {
+  __shared__ float rs[NT / 64], rc[NT / 64], rb[NT / 64];
+  float s = 0.f, n = 0.f, nb = 0.f;
   for (int i = threadIdx.x; i < B; i += NT) {
     const int64_t t = tgt[i];
-    if (t == ignore || t < 0 || t >= C) continue;
+    if (t == ignore) continue;
+    if (t < 0 || t >= C) {
+      nb += 1.f;
+      continue;
+    }
     s -= logp[(size_t)i * C + t];
     n += 1.f;
   }
   s = warp_sum(s);
   n = warp_sum(n);
+  nb = warp_sum(nb);
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  if (lane == 0) { rs[wave] = s; rc[wave] = n; }
+  if (lane == 0) { rs[wave] = s; rc[wave] = n; rb[wave] = nb; }
   __syncthreads();
   if (threadIdx.x == 0) {
-    float S = 0.f, Nn = 0.f;
-    for (int w = 0; w < NT / 64; ++w) { S += rs[w]; Nn += rc[w]; }
-    loss[0] = S / Nn;  // NaN when every target is ignored, as torch
+    float S = 0.f, Nn = 0.f, Nb = 0.f;
+    for (int w = 0; w < NT / 64; ++w) { S += rs[w]; Nn += rc[w]; Nb += rb[w]; }
+    loss[0] = Nb > 0.f ? __builtin_nanf("") : S / Nn;  // NaN when every target is ignored, as torch
     count[0] = Nn;
+    bad[0] = Nb;
   }
 }
 
@@ -337,7 +346,7 @@ __global__ void __launch_bounds__(NT) nll_bwd_kernel(const int64_t* __restrict__
   if (e >= B * C) return;
   const int i = e / C, c = e % C;
   const int64_t t = tgt[i];
-  dlogp[e] = (t == c && t != ignore) ? -g[0] / count[0] : 0.f;
+  dlogp[e] = (t == c && t != ignore) ? -g[0] / count[0] : 0.f;  // (out-of-range t never equals c)
 }
 
 bool bad_args(const LeNetArgs& a) { return a.B <= 0 || a.NC <= 0 || a.NC > MAXNC; }
@@ -370,9 +379,9 @@ PDT_API int pdt_lenet_bwd(const float* x, const float* w1, const float* b1, cons
 }
 
 PDT_API int pdt_nll_fwd(const float* logp, const int64_t* tgt, int B, int C, int ignore, float* loss, float* count,
-                        hipStream_t st) {
+                        float* bad, hipStream_t st) {
   if (B <= 0 || C <= 0) return -1;
-  hipLaunchKernelGGL(nll_fwd_kernel, dim3(1), dim3(NT), 0, st, logp, tgt, B, C, ignore, loss, count);
+  hipLaunchKernelGGL(nll_fwd_kernel, dim3(1), dim3(NT), 0, st, logp, tgt, B, C, ignore, loss, count, bad);
   PDT_RETURN_LAUNCH();
 }
 

@@ -26,6 +26,33 @@ __global__ void fill_uniform_kernel(u16* __restrict__ out, long n8, uint32_t see
   }
 }
 
+// Index-addressable synthetic images (data/synthetic.py SyntheticImageNet): sample i
+// of the dataset is a pure function of (seed, i), so a DistributedSampler's index
+// batch is materialised on the device in one launch. out: [B][HW][Cp] bf16 (NHWC,
+// channel dim padded to Cp in storage, pad channels 0); labels[b] in [0, classes).
+// One thread per (image, pixel, 4-channel group): one 8-byte store.
+__global__ void synth_images_kernel(u16* __restrict__ out, const int64_t* __restrict__ idx, long B, int HW, int C,
+                                    int Cp, uint32_t seed, int64_t* __restrict__ labels, int classes) {
+  const int G = Cp / 4;
+  const long total = B * HW * G;
+  for (long t = (long)blockIdx.x * NT + threadIdx.x; t < total; t += (long)gridDim.x * NT) {
+    const long pix = t / G;
+    const int g = (int)(t - pix * G);
+    const long b = pix / HW;
+    const int p = (int)(pix - b * HW);
+    const uint32_t s = hash32((uint32_t)idx[b] * 0x9E3779B9u ^ seed);
+    float f[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int c = g * 4 + j;
+      const uint32_t h = hash32((uint32_t)(p * C + c) * 0x85EBCA6Bu ^ s);
+      f[j] = c < C ? (float)(h >> 8) * (2.0f / 16777216.0f) - 1.0f : 0.f;
+    }
+    reinterpret_cast<uint2*>(out)[t] = uint2{pack2bf(f[0], f[1]), pack2bf(f[2], f[3])};
+    if (t < B) labels[t] = (int64_t)(hash32((uint32_t)idx[t] * 0xC2B2AE35u ^ seed ^ 0x5bd1e995u) % (uint32_t)classes);
+  }
+}
+
 __global__ void cast_f32_bf16_kernel(const float* __restrict__ x, u16* __restrict__ y, long n) {
   long n4 = n / 4;
   for (long i = (long)blockIdx.x * NT + threadIdx.x; i < n4; i += (long)gridDim.x * NT) {
@@ -122,6 +149,16 @@ int grid_for(long n) {
 PDT_API int pdt_fill_uniform_bf16(void* out, long n, unsigned seed, hipStream_t st) {
   if (n % 8) return -1;
   hipLaunchKernelGGL(fill_uniform_kernel, dim3(grid_for(n / 8)), dim3(NT), 0, st, (u16*)out, n / 8, seed);
+  PDT_RETURN_LAUNCH();
+}
+
+PDT_API int pdt_synth_images_bf16(void* out, const int64_t* idx, long B, int HW, int C, int Cp, unsigned seed,
+                                  int64_t* labels, int classes, hipStream_t st) {
+  if (B <= 0 || HW <= 0 || C <= 0 || Cp % 4 || C > Cp || classes <= 0 || (long)HW * Cp * B >= (1L << 40)) return -1;
+  const long n = B * HW * (Cp / 4);
+  if (n < B) return -1;  // the label writes ride on the first B threads
+  hipLaunchKernelGGL(synth_images_kernel, dim3(grid_for(n)), dim3(NT), 0, st, (u16*)out, idx, B, HW, C, Cp, seed,
+                     labels, classes);
   PDT_RETURN_LAUNCH();
 }
 

@@ -3,9 +3,13 @@
 
 Same handlers and formats (console ``%(message)s``; rotating ``info.log``,
 10 MiB x 20, ``%(asctime)s - %(name)s - %(levelname)s - %(message)s``).
-Differences: the default config path is resolved relative to this package,
-built in (``default_log_config``) or any JSON path; non-zero ranks get console-only logging at WARNING so a
-multi-rank run writes one ``info.log``.
+The reference's JSON ships as ``logger/logger_config.json`` in this package
+(same schema; edit it to change handlers/levels) and is the default config.
+Differences: the default path is resolved relative to this package instead of
+the CWD (the reference's ``logger/logger_config.json`` only worked from the repo
+root); ``default_log_config()`` is the built-in equivalent used if the file is
+missing; non-zero ranks get console-only logging at WARNING so a multi-rank run
+writes one ``info.log``.
 """
 import logging
 import logging.config
@@ -35,7 +39,10 @@ def default_log_config():
     }
 
 
-def setup_logging(save_dir, log_config=None, default_level=logging.INFO, rank: int = 0):
+DEFAULT_LOG_CONFIG = Path(__file__).resolve().parent / "logger_config.json"
+
+
+def setup_logging(save_dir, log_config=DEFAULT_LOG_CONFIG, default_level=logging.INFO, rank: int = 0):
     if rank != 0:
         logging.basicConfig(level=logging.WARNING, format="[rank%d] %%(message)s" % rank, force=True)
         return

@@ -11,9 +11,11 @@ from ..ops import fused
 
 
 def nll_loss(output, target):
-    if fused.use_native(output) and output.dim() == 2 and output.dtype == torch.float32:
+    if fused.use_native(output):
         from ..ops import native_ops
-        return native_ops.nll_loss(output, target)
+        if output.dim() == 2 and output.dtype == torch.float32:
+            return native_ops.nll_loss(output, target)
+        native_ops.fallback("nll_loss", f"{tuple(output.shape)} {output.dtype} (kernel: fp32 [B, C])")
     return F.nll_loss(output, target)
 
 

@@ -30,6 +30,8 @@ class MnistModel(BaseModel):
             from ..ops import native_ops
             if native_ops.lenet_supported(self, x) and not x.requires_grad:
                 return native_ops.lenet_forward(self, x)
+            native_ops.fallback("MnistModel", f"input {tuple(x.shape)} requires_grad={x.requires_grad} "
+                                              "(kernel: [B, 1, 28, 28], the reference layer sizes)")
         h = F.max_pool2d(self.conv1(x), 2).relu()
         h = F.max_pool2d(self.conv2_drop(self.conv2(h)), 2).relu()
         h = torch.flatten(h, 1)

@@ -179,9 +179,11 @@ def qkv_attention(qkv, num_heads: int, fp8: bool = False, fp8_for: nn.Linear | N
     Native path: one fused MFMA kernel (hd = 64; ``fp8``: e4m3 score GEMM); torch path: SDPA."""
     B, T, D3 = qkv.shape
     hd = D3 // (3 * num_heads)
-    if _use_native(qkv) and hd == 64:
+    if _use_native(qkv):
         from . import native_ops
-        return native_ops.qkv_attention(qkv, num_heads, fp8=fp8, fp8_for=fp8_for, grad_fp8_for=grad_fp8_for)
+        if hd == 64 and qkv.dtype == torch.bfloat16:
+            return native_ops.qkv_attention(qkv, num_heads, fp8=fp8, fp8_for=fp8_for, grad_fp8_for=grad_fp8_for)
+        native_ops.fallback("qkv_attention", f"head dim {hd}, {qkv.dtype} (kernel: head dim 64, bf16)")
     q, k, v = qkv.view(B, T, 3, num_heads, hd).permute(2, 0, 3, 1, 4)
     o = F.scaled_dot_product_attention(q, k, v)
     return o.transpose(1, 2).reshape(B, T, num_heads * hd)

@@ -80,6 +80,7 @@ _SIGS = {
     "pdt_adam_step": (c_int, [P, c_int, P, P, P, P, P, P] + [c_float] * 5 + [c_int, c_float, c_float, c_float, P]),
     "pdt_fill_uniform_bf16": (c_int, [P, c_long, c_uint, P]),
     "pdt_cast_f32_bf16": (c_int, [P, P, c_long, P]),
+    "pdt_synth_images_bf16": (c_int, [P, P, c_long, c_int, c_int, c_int, c_uint, P, c_int, P]),
     "pdt_lane_reduce_probe": (c_int, [P, P, c_int, P]),
     "pdt_wt_dgrad": (c_int, [P, P] + [c_int] * 9 + [P]),
     "pdt_transpose_cast": (c_int, [P, P, c_int, c_int, P]),
@@ -107,7 +108,7 @@ _SIGS = {
     "pdt_lenet_grad_row": (c_int, [c_int]),
     "pdt_lenet_fwd": (c_int, [P] * 9 + [c_int, c_int, c_int, c_float, c_float, c_uint, P, P, P, P]),
     "pdt_lenet_bwd": (c_int, [P] * 9 + [c_int, c_int, c_int, c_float, c_float, c_uint, P, P, P, P]),
-    "pdt_nll_fwd": (c_int, [P, P, c_int, c_int, c_int, P, P, P]),
+    "pdt_nll_fwd": (c_int, [P, P, c_int, c_int, c_int, P, P, P, P]),
     "pdt_nll_bwd": (c_int, [P, P, P, c_int, c_int, c_int, P, P]),
 }
 
@@ -157,6 +158,23 @@ def _p(t):
 def _chk(rc, name):
     if rc != 0:
         raise RuntimeError(f"{name} failed with code {rc}")
+
+
+_FALLBACK_WARNED: set = set()
+
+
+def fallback(what: str, reason: str) -> None:
+    """Called where a native op cannot run its input and the stock PyTorch path would.
+    Under backend ``native`` that is an error -- a run that asked for the HIP kernels
+    never silently measures MIOpen / SDPA instead; under ``auto`` it warns once per op."""
+    from . import fused
+    if fused.get_backend() == "native":
+        raise NotImplementedError(f"backend 'native': no HIP kernel path for {what} ({reason}); "
+                                  "select backend 'auto' to allow the stock PyTorch op for it")
+    if what not in _FALLBACK_WARNED:
+        _FALLBACK_WARNED.add(what)
+        import warnings
+        warnings.warn(f"[pdt] {what}: {reason} -> stock PyTorch op", stacklevel=3)
 
 
 def _cl(t: torch.Tensor) -> torch.Tensor:
@@ -301,19 +319,66 @@ def pretune_distributed(run_step) -> None:
     obj = [None]
     if dist.get_rank() == 0:
         tune_on = os.environ.get("PDT_AUTOTUNE", "1") != "0" and os.environ.get("PDT_DETERMINISTIC", "0") != "1"
+        err = None
         if tune_on:
+            # the step must leave no trace on rank 0 that the other ranks do not share:
+            # RNG streams are restored (DataLoader seeds, dropout), the fp8 scaling
+            # histories it created or rolled are dropped (``_snapshot_fp8_meta``)
+            cpu_rng = torch.get_rng_state()
+            cuda_rng = torch.cuda.get_rng_state() if torch.cuda.is_available() else None
+            fp8_before = _snapshot_fp8_meta()
             _TUNE_FORCE = True
             try:
                 run_step()
                 if torch.cuda.is_available():
                     torch.cuda.synchronize()
+            except Exception as e:  # tell the other ranks instead of leaving them in the broadcast
+                err = f"{type(e).__name__}: {e}"
             finally:
                 _TUNE_FORCE = False
-        obj = [dict(_tuned())]
+                torch.set_rng_state(cpu_rng)
+                if cuda_rng is not None:
+                    torch.cuda.set_rng_state(cuda_rng)
+                _restore_fp8_meta(fp8_before)
+        obj = [{"error": err} if err is not None else dict(_tuned())]
     dist.broadcast_object_list(obj, src=0)
+    if isinstance(obj[0], dict) and set(obj[0]) == {"error"}:
+        raise RuntimeError(f"kernel pre-tuning step failed on rank 0: {obj[0]['error']}")
     _tuned().clear()
     _tuned().update(obj[0])
     _TUNE_FROZEN = True
+
+
+_FP8_META_ATTRS = ("_pdt_fp8_meta", "_pdt_fp8_gmeta")
+
+
+def _snapshot_fp8_meta():
+    """{module: {attr: clone}} of every live fp8 delayed-scaling state (nn.Linear owners)."""
+    import gc
+    snap = {}
+    for obj in gc.get_objects():
+        if isinstance(obj, nn.Module):
+            st = {a: getattr(obj, a).clone() for a in _FP8_META_ATTRS if getattr(obj, a, None) is not None}
+            snap[id(obj)] = (weakref.ref(obj), st)
+    return snap
+
+
+def _restore_fp8_meta(snap):
+    """Undo what a step did to the fp8 scaling states: states it created are removed,
+    states it rolled get their previous values back."""
+    import gc
+    for obj in gc.get_objects():
+        if not isinstance(obj, nn.Module):
+            continue
+        ent = snap.get(id(obj))
+        before = ent[1] if ent is not None and ent[0]() is obj else {}
+        for a in _FP8_META_ATTRS:
+            if getattr(obj, a, None) is None:
+                continue
+            if a in before:
+                getattr(obj, a).copy_(before[a])
+            else:
+                delattr(obj, a)
 
 
 NOT_APPLICABLE = -5  # kernel return code: this variant cannot run this geometry
@@ -518,6 +583,17 @@ def fill_uniform_(t: torch.Tensor, seed: int):
     assert t.dtype == torch.bfloat16 and t.numel() % 8 == 0
     _chk(_load().pdt_fill_uniform_bf16(_p(t), t.numel(), seed & 0xFFFFFFFF, _s()), "fill")
     return t
+
+
+def synthetic_images_at(buf, idx, C, seed, labels, num_classes):
+    """Samples ``idx`` (int64 [B], device) of the index-addressable synthetic dataset into
+    ``buf`` (bf16 [B, H, W, Cp], channels >= C zeroed) and ``labels`` (int64 [B])."""
+    B, H, W, Cp = buf.shape
+    assert buf.dtype == torch.bfloat16 and buf.is_contiguous() and Cp % 4 == 0 and C <= Cp
+    assert idx.dtype == torch.int64 and idx.numel() == B and idx.device == buf.device
+    assert labels.dtype == torch.int64 and labels.numel() == B and labels.device == buf.device
+    _chk(_load().pdt_synth_images_bf16(_p(buf), _p(idx), B, H * W, C, Cp, seed & 0xFFFFFFFF, _p(labels),
+                                       int(num_classes), _s()), "synth_images")
 
 
 def synthetic_images(shape, dtype, device, seed=0, channels_last=True):
@@ -974,6 +1050,8 @@ class _ConvBNAct(torch.autograd.Function):
 
 def conv_bn_act(x, conv: nn.Conv2d, bn: nn.BatchNorm2d, residual=None, relu=True):
     if not supports_conv(x, conv) or (residual is not None and residual.dtype != torch.bfloat16):
+        fallback("conv_bn_act", f"conv {tuple(conv.kernel_size)}/{tuple(conv.stride)} groups={conv.groups} "
+                                f"bias={conv.bias is not None} on {tuple(x.shape)} {x.dtype}")
         from .fused import _torch_conv_bn_act
         return _torch_conv_bn_act(x, conv, bn, residual, relu)
     return _ConvBNAct.apply(x, conv.weight, bn.weight, bn.bias, residual, conv, relu, _BNArgs(bn))
@@ -1153,8 +1231,9 @@ class _Bottleneck(torch.autograd.Function):
 
 def bottleneck(x, blk):
     convs = [blk.conv1, blk.conv2, blk.conv3] + ([blk.downsample[0]] if blk.downsample is not None else [])
-    if x.dtype != torch.bfloat16 or not all(supports_conv(x if c is blk.conv1 else x, c) for c in convs) \
-            or x.shape[1] % 8:
+    if x.dtype != torch.bfloat16 or not all(supports_conv(x, c) for c in convs) or x.shape[1] % 8:
+        fallback("bottleneck", f"input {tuple(x.shape)} {x.dtype} (needs bf16, channels % 8 == 0, "
+                               "plain convs)")
         return None
     has_ds = blk.downsample is not None
     params = [blk.conv1.weight, blk.bn1.weight, blk.bn1.bias, blk.conv2.weight, blk.bn2.weight, blk.bn2.bias,
@@ -1340,12 +1419,14 @@ class _StemPool(torch.autograd.Function):
 def stem_pool(x, conv: nn.Conv2d, bn: nn.BatchNorm2d, kernel_size=3, stride=2, padding=1):
     """max_pool2d(relu(bn(conv(x)))) as one node; None if the native path cannot run it."""
     if not supports_conv(x, conv) or conv.out_channels % 8:
+        fallback("stem conv+bn+relu+maxpool", f"conv {tuple(conv.kernel_size)} on {tuple(x.shape)}")
         return None
     return _StemPool.apply(x, conv.weight, bn.weight, bn.bias, conv, _BNArgs(bn), kernel_size, stride, padding)
 
 
 def max_pool2d(x, kernel_size=3, stride=2, padding=1):
     if x.dtype != torch.bfloat16 or x.shape[1] % 8:
+        fallback("max_pool2d", f"{tuple(x.shape)} {x.dtype} (needs bf16, channels % 8 == 0)")
         return torch.nn.functional.max_pool2d(x, kernel_size, stride, padding)
     return _MaxPool.apply(x, kernel_size, stride, padding)
 
@@ -1371,6 +1452,7 @@ class _AvgPool(torch.autograd.Function):
 
 def global_avg_pool(x):
     if x.dtype != torch.bfloat16 or x.shape[1] % 8:
+        fallback("global_avg_pool", f"{tuple(x.shape)} {x.dtype} (needs bf16, channels % 8 == 0)")
         return torch.flatten(torch.nn.functional.adaptive_avg_pool2d(x, 1), 1)
     return _AvgPool.apply(x)
 
@@ -1748,6 +1830,7 @@ def linear(x, fc: nn.Linear, act=None, fp8=False, residual=None):
     N = fc.out_features
     if K % 8 or N % 8 or act not in (None, "relu", "gelu") or (residual is not None and (
             residual.dtype != torch.bfloat16 or residual.shape[:-1] != x.shape[:-1] or residual.shape[-1] != N)):
+        fallback("linear", f"{K}->{N} act={act} (needs K, N % 8 == 0, act in relu/gelu/None, bf16 residual)")
         from .fused import _torch_linear
         y = _torch_linear(x, fc, act)
         return y if residual is None else y + residual
@@ -1908,6 +1991,7 @@ class _LayerNorm(torch.autograd.Function):
 def layer_norm(x, ln):
     D = ln.normalized_shape[-1]
     if len(ln.normalized_shape) != 1 or D not in (256, 512, 768, 1024) or not ln.elementwise_affine:
+        fallback("layer_norm", f"normalized_shape {tuple(ln.normalized_shape)} (kernels: D in 256/512/768/1024, affine)")
         return ln(x)
     return _LayerNorm.apply(x, ln.weight, ln.bias, ln.eps)
 
@@ -2047,6 +2131,7 @@ class _XEnt(torch.autograd.Function):
 
 def softmax_cross_entropy(logits, target, label_smoothing=0.0):
     if logits.dim() != 2:
+        fallback("softmax_cross_entropy", f"logits of shape {tuple(logits.shape)} (kernel: [B, V])")
         return torch.nn.functional.cross_entropy(logits.float(), target, label_smoothing=label_smoothing)
     return _XEnt.apply(logits, target, float(label_smoothing))
 
@@ -2133,7 +2218,14 @@ def qkv_attention(qkv, num_heads, fp8=False, fp8_for=None, grad_fp8_for=None):
 
 
 def attention(q, k, v):
-    return torch.nn.functional.scaled_dot_product_attention(q, k, v)
+    """softmax(q k^T / sqrt(64)) v for [B, H, T, 64] q / k / v on the fused attention
+    kernel (packs them into the [B, T, 3*H*64] layout :func:`qkv_attention` reads)."""
+    B, H, T, d = q.shape
+    if d != 64 or k.shape != q.shape or v.shape != q.shape or q.dtype != torch.bfloat16:
+        fallback("attention", f"q {tuple(q.shape)} {q.dtype} (kernel: head dim 64, bf16, self-attention shapes)")
+        return torch.nn.functional.scaled_dot_product_attention(q, k, v)
+    qkv = torch.stack([q, k, v], dim=2).permute(0, 3, 2, 1, 4).reshape(B, T, 3 * H * d)
+    return qkv_attention(qkv, H).view(B, T, H, d).transpose(1, 2)
 
 
 class _PatchEmbed(torch.autograd.Function):
@@ -2182,6 +2274,8 @@ def patch_embed(x, conv):
     if (conv.stride != conv.kernel_size or conv.padding != (0, 0) or conv.out_channels % 8 or conv.groups != 1
             or conv.dilation != (1, 1) or x.dim() != 4 or x.shape[2] % KH or x.shape[3] % KW
             or (x.shape[1] % 8 and x.shape[1] > 8)):
+        fallback("patch_embed", f"conv {tuple(conv.kernel_size)}/{tuple(conv.stride)} on {tuple(x.shape)} "
+                                "(kernel: non-overlapping patches, bias-any, channels <= 8 or % 8 == 0)")
         y = conv(x)
         return y.flatten(2).transpose(1, 2)
     return _PatchEmbed.apply(x, conv.weight, conv.bias, conv)
@@ -2253,16 +2347,56 @@ def lenet_forward(model, x, masks=None, seed=None):
                         seed, masks)
 
 
+class _TargetCheck:
+    """Lazy device-side check of NLL targets: each forward's count of out-of-range
+    targets is copied (non-blocking) to pinned host memory; the NEXT call reads it once
+    its event has completed and raises -- no host sync inside the step. The loss of
+    the offending batch itself is already NaN (csrc/lenet.hip nll_fwd_kernel).
+    ``PDT_CHECK_TARGETS=sync`` checks every call synchronously instead."""
+
+    def __init__(self):
+        self.pending = []  # (event, pinned host tensor)
+
+    def record(self, bad: torch.Tensor):
+        if os.environ.get("PDT_CHECK_TARGETS", "lazy") == "sync":
+            n = float(bad.item())
+            if n:
+                raise ValueError(f"nll_loss: {int(n)} target(s) out of range [0, num_classes)")
+            return
+        host = torch.empty(1, dtype=torch.float32, pin_memory=True)
+        host.copy_(bad.reshape(1), non_blocking=True)
+        ev = torch.cuda.Event()
+        ev.record()
+        self.pending.append((ev, host))
+
+    def poll(self):
+        keep = []
+        for ev, host in self.pending:
+            if not ev.query():
+                keep.append((ev, host))
+                continue
+            if float(host[0]):
+                self.pending = []
+                raise ValueError(f"nll_loss: {int(host[0])} target(s) out of range [0, num_classes) "
+                                 "in an earlier batch (its loss was NaN)")
+        self.pending = keep[-8:]
+
+
+_TARGETS = _TargetCheck()
+
+
 class _NLL(torch.autograd.Function):
     @staticmethod
     def forward(ctx, logp, target, ignore_index):
+        _TARGETS.poll()
         logp = logp.float().contiguous()
         target = target.to(torch.long).contiguous()
         B, C = logp.shape
         assert target.numel() == B
-        out = torch.empty(2, dtype=torch.float32, device=logp.device)  # loss, count
-        _chk(_load().pdt_nll_fwd(_p(logp), _p(target), B, C, int(ignore_index), _p(out[0]), _p(out[1]), _s()),
-             "nll_fwd")
+        out = torch.empty(3, dtype=torch.float32, device=logp.device)  # loss, count, #out-of-range targets
+        _chk(_load().pdt_nll_fwd(_p(logp), _p(target), B, C, int(ignore_index), _p(out[0]), _p(out[1]),
+                                 _p(out[2]), _s()), "nll_fwd")
+        _TARGETS.record(out[2])
         ctx.save_for_backward(target, out)
         ctx.meta = (B, C, int(ignore_index))
         return out[0].clone()

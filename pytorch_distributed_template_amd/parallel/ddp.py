@@ -26,7 +26,7 @@ from __future__ import annotations
 import torch
 from torch.nn.parallel import DistributedDataParallel
 
-from ..utils.dist import get_world_size
+from ..utils.dist import get_world_size, is_dist_ready
 
 DEFAULT_BUCKET_MB = 64
 
@@ -35,8 +35,11 @@ def wrap_ddp(model: torch.nn.Module, device: torch.device, bucket_cap_mb: float 
              broadcast_buffers: bool = True, gradient_as_bucket_view: bool = True,
              comm_hook: str | None = None, static_graph: bool = False,
              find_unused_parameters: bool = False):
-    """Wrap in DDP when world_size > 1, else return the model unchanged."""
-    if get_world_size() <= 1:
+    """Wrap in DDP whenever a process group exists -- a 1-rank RCCL group too
+    (``torchrun --nproc-per-node 1``, ``bench.py --gpus 1``): the reducer, its
+    bucket views and the RCCL all-reduce on its own stream then run at N = 1
+    exactly as at N > 1. Without a process group the model is returned unchanged."""
+    if not is_dist_ready():
         return model
     kwargs = dict(bucket_cap_mb=bucket_cap_mb, broadcast_buffers=broadcast_buffers,
                   gradient_as_bucket_view=gradient_as_bucket_view, static_graph=static_graph,

@@ -66,15 +66,33 @@ def env_world_size() -> int:
     return int(os.environ.get("WORLD_SIZE", "1"))
 
 
+def launched() -> bool:
+    """True when a launcher (torchrun / torch.distributed.launch) started this process."""
+    return "WORLD_SIZE" in os.environ and "MASTER_ADDR" in os.environ
+
+
+def _free_port() -> int:
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
 def init_distributed(local_rank: Optional[int] = None, backend: Optional[str] = None,
-                     timeout_s: float = 1800.0, device_index: Optional[int] = None) -> torch.device:
+                     timeout_s: float = 1800.0, device_index: Optional[int] = None,
+                     single_rank_group: bool = False) -> torch.device:
     """Initialise the default process group from the ``env://`` rendezvous.
 
-    Returns the device this rank should use. Safe to call with WORLD_SIZE=1
-    (returns the device, no process group). ``device_index`` pins the GPU
-    (e.g. several gloo ranks sharing one GPU to rehearse a multi-rank job on a
-    one-GPU box); by default a rank uses GPU ``LOCAL_RANK`` and a ``gloo``
-    backend means a CPU run.
+    Returns the device this rank should use. A process group is created when a
+    launcher started the process -- including ``torchrun --nproc-per-node 1``:
+    a 1-rank RCCL group, so the DDP reducer and its RCCL all-reduces run exactly
+    as they do at N > 1 -- or when ``single_rank_group`` asks for one in a plain
+    ``python`` process (the rendezvous env is then filled in for a 1-rank job on
+    127.0.0.1). Plain ``python train.py`` without a launcher keeps the
+    reference's behaviour (``distributed = WORLD_SIZE > 1``, /root/reference/train.py:20-21):
+    no group. ``device_index`` pins the GPU (e.g. several gloo ranks sharing one
+    GPU to rehearse a multi-rank job on a one-GPU box); by default a rank uses
+    GPU ``LOCAL_RANK`` and a ``gloo`` backend means a CPU run.
     """
     local_rank = get_local_rank(local_rank)
     use_cuda = torch.cuda.is_available() and (backend != "gloo" or device_index is not None)
@@ -82,7 +100,13 @@ def init_distributed(local_rank: Optional[int] = None, backend: Optional[str] = 
     device = torch.device("cuda", index) if use_cuda else torch.device("cpu")
     if use_cuda:
         torch.cuda.set_device(device)
-    if env_world_size() > 1 and not is_dist_ready():
+    if single_rank_group and not launched():
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", str(_free_port()))
+        os.environ.setdefault("RANK", "0")
+        os.environ.setdefault("LOCAL_RANK", "0")
+        os.environ["WORLD_SIZE"] = "1"
+    if (env_world_size() > 1 or launched()) and not is_dist_ready():
         backend = backend or ("nccl" if use_cuda else "gloo")
         kwargs = dict(backend=backend, init_method="env://",
                       timeout=datetime.timedelta(seconds=timeout_s))

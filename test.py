@@ -43,7 +43,9 @@ def main(args, config, device):
     outputs, targets = [], []
     for data, target in data_loader:
         data, target = data.to(device, non_blocking=True), target.to(device, non_blocking=True)
-        if channels_last and data.dim() == 4:
+        # a loader's NHWC-padded batch (``pdt_nhwc_pad``) is already in the layout the native
+        # stem reads in place: re-laying it out would copy it and drop the tag (as in Trainer)
+        if channels_last and data.dim() == 4 and getattr(data, "pdt_nhwc_pad", None) is None:
             data = data.contiguous(memory_format=torch.channels_last)
         with torch.autocast(device_type=device.type, dtype=ac or torch.float32, enabled=ac is not None):
             output = model(data)

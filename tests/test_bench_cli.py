@@ -61,3 +61,18 @@ def test_bench_rejects_world_size_mismatch():
                        capture_output=True, text=True, timeout=300)
     assert r.returncode == 2
     assert "WORLD_SIZE=2" in r.stderr
+
+
+def test_bench_one_rank_runs_ddp_over_a_process_group():
+    """N = 1 measures the same DDP path as N > 1: a 1-rank process group (gloo on
+    the CPU rehearsal, RCCL on a GPU) and the DDP reducer; --no-ddp drops both."""
+    base = [sys.executable, BENCH, "--gpus", "1", "--device", "cpu", "--batch", "2", "--image-size", "32",
+            "--steps", "1", "--warmup", "1"]
+    r = subprocess.run(base, cwd=ROOT, env=_env(), capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stderr[-3000:]
+    rec = _json_line(r.stdout)
+    assert rec["n_gpus"] == 1 and rec["config"]["dist_backend"] == "gloo" and rec["config"]["ddp"] is True
+    r = subprocess.run(base + ["--no-ddp"], cwd=ROOT, env=_env(), capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stderr[-3000:]
+    rec = _json_line(r.stdout)
+    assert rec["config"]["ddp"] is False and rec["config"]["dist_backend"].startswith("none")

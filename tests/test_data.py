@@ -59,6 +59,32 @@ def test_synthetic_imagenet_loader_cpu():
     assert x.dtype == torch.float32 and -1 <= float(x.min()) and float(x.max()) < 1
     assert y.dtype == torch.int64 and int(y.max()) < 5
     assert len(dl.dataset) == 10
-    tl = SyntheticImageNetLoader(batch_size=4, num_samples=10, pool=2, image_size=8)
+    tl = SyntheticImageNetLoader(batch_size=4, num_samples=10, pool=2, image_size=8, mode="pool")
     tl.set_epoch(1)
     assert torch.equal(next(iter(tl))[0], tl._pool[1][0])
+
+
+def test_synthetic_imagenet_is_index_addressable_and_sampler_sharded():
+    """The config loader is SyntheticImageNet -> DistributedSampler -> BaseDataLoader
+    (/root/reference/data_loader/data_loaders.py:23-26): every index batch is
+    materialised per sample index, ranks get disjoint shards, set_epoch reshuffles."""
+    from torch.utils.data import DistributedSampler
+    from pytorch_distributed_template_amd.base import BaseDataLoader
+    dl = SyntheticImageNetLoader(batch_size=4, num_samples=10, image_size=8, num_classes=7)
+    assert isinstance(dl, BaseDataLoader) and isinstance(dl.sampler, DistributedSampler)
+    ds = dl.dataset
+    order0 = list(iter(dl.sampler))
+    x, y = next(iter(dl))
+    for b, i in enumerate(order0[:4]):  # batch row b is sample order0[b]
+        xi, yi = ds[i]
+        assert torch.equal(x[b], xi) and int(y[b]) == int(yi)
+    assert -1 <= float(x.min()) and float(x.max()) < 1 and 0 <= int(y.min()) and int(y.max()) < 7
+    dl.set_epoch(1)
+    assert list(iter(dl.sampler)) != order0 and sorted(iter(dl.sampler)) == sorted(order0)
+    # two ranks: disjoint shards covering the (padded) dataset, equal step counts
+    from pytorch_distributed_template_amd.data.synthetic import SyntheticImageNet
+    shards = [list(DistributedSampler(ds, num_replicas=2, rank=r, shuffle=True, seed=0)) for r in range(2)]
+    assert len(shards[0]) == len(shards[1]) == 5 and set(shards[0]) | set(shards[1]) == set(range(10))
+    # same (seed, index) -> same sample, another seed -> another sample
+    a, b = SyntheticImageNet(10, image_size=8, seed=3), SyntheticImageNet(10, image_size=8, seed=4)
+    assert torch.equal(a[5][0], SyntheticImageNet(10, image_size=8, seed=3)[5][0]) and not torch.equal(a[5][0], b[5][0])

@@ -115,6 +115,26 @@ def test_nll_loss_kernels_match_torch():
     torch.testing.assert_close(g, logp.grad, rtol=1e-6, atol=1e-7)
 
 
+def test_nll_loss_out_of_range_target_fails_loudly(monkeypatch):
+    """torch's F.nll_loss raises on a target outside [0, C); the native kernel cannot
+    raise from the device: the batch's loss is NaN, and the next call (lazy check, no
+    sync in the step) or this call (PDT_CHECK_TARGETS=sync) raises."""
+    B, C = 64, 10
+    logp = torch.log_softmax(torch.randn(B, C, device="cuda"), 1)
+    y = torch.randint(0, C, (B,), device="cuda")
+    y[5] = C  # == num_classes: out of range
+    loss = no.nll_loss(logp, y)
+    assert torch.isnan(loss).item()
+    torch.cuda.synchronize()
+    with pytest.raises(ValueError, match="out of range"):
+        no.nll_loss(logp, torch.randint(0, C, (B,), device="cuda"))
+    monkeypatch.setenv("PDT_CHECK_TARGETS", "sync")
+    with pytest.raises(ValueError, match="out of range"):
+        no.nll_loss(logp, y)
+    ok = no.nll_loss(logp, torch.randint(0, C, (B,), device="cuda"))
+    assert torch.isfinite(ok).item()
+
+
 def test_mnist_config_step_uses_native_path():
     from pytorch_distributed_template_amd.models import loss as L
     m = _model(3).train()

@@ -32,6 +32,18 @@ def test_synthetic_loader_native_fill():
     assert torch.equal(next(iter(dl2))[0], x)  # counter-based: same seed -> same data
 
 
+def test_synthetic_imagenet_kernel_matches_host_hash():
+    """pdt_synth_images_bf16 == the torch-integer-op host path, bit for bit (images and labels)."""
+    from pytorch_distributed_template_amd.data.synthetic import SyntheticImageNet
+    g = SyntheticImageNet(1000, image_size=16, num_classes=11, seed=9, device="cuda")
+    c = SyntheticImageNet(1000, image_size=16, num_classes=11, seed=9, device="cpu", dtype="bfloat16")
+    idx = [3, 999, 0, 512, 77]
+    xg, yg = g.collate(idx)
+    xc, yc = c.collate(idx)
+    assert getattr(xg, "pdt_nhwc_pad", None) == 4
+    assert torch.equal(xg.cpu(), xc) and torch.equal(yg.cpu(), yc)
+
+
 def test_resnet50_config_train_resume_test(tmp_path):
     cfg = json.loads((ROOT / "config" / "resnet50_bf16.json").read_text())
     cfg["trainer"].update(save_dir=str(tmp_path), len_epoch=3, epochs=1, monitor="max val_accuracy")

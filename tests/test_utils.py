@@ -49,3 +49,20 @@ def test_tensorboard_writer_fallback_jsonl(tmp_path):
         assert "loss/train" in tags and "acc/valid" in tags and "steps_per_sec/valid" in tags
     off = TensorboardWriter(tmp_path, logging.getLogger("t"), False)
     off.add_scalar("x", 1.0)  # no-op
+
+
+def test_shipped_logger_config_json_is_the_default(tmp_path):
+    """logger/logger_config.json ships with the reference schema (/root/reference/logger/logger.py:7)
+    and setup_logging reads it by default: console + rotating info.log in the run dir."""
+    import json
+    import logging
+    from pytorch_distributed_template_amd.logger.logger import (DEFAULT_LOG_CONFIG, default_log_config,
+                                                                setup_logging)
+    cfg = json.loads(DEFAULT_LOG_CONFIG.read_text())
+    assert cfg == default_log_config()
+    assert cfg["handlers"]["info_file_handler"]["class"] == "logging.handlers.RotatingFileHandler"
+    setup_logging(tmp_path)
+    logging.getLogger("t").info("hello-from-test")
+    for h in logging.getLogger().handlers:
+        h.flush()
+    assert "hello-from-test" in (tmp_path / "info.log").read_text()

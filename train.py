@@ -59,6 +59,9 @@ def main(args, config, device):
     model = wrap_model(config, model, device)
 
     if pdist.is_main_process():
+        if pdist.is_dist_ready():
+            logger.info("process group: {}, world size {}".format(torch.distributed.get_backend(),
+                                                                   pdist.get_world_size()))
         logger.info(model)
 
     trainer = Trainer(model, criterion, metrics, optimizer, config=config, device=device,
