@@ -272,10 +272,20 @@ int run_stream(int s, const NTParams& p, hipStream_t st) {
 
 }  // namespace
 
-PDT_API int pdt_conv_nt_num_variants() { return NVAR + NVAR_STREAM; }
+// variant ids: [0, NVAR) the LDS-tiled kernels, then NVAR_STREAM streaming 1x1 kernels,
+// then NVAR_HALO 3x3 halo-patch kernels (conv3x3_halo.hip)
+constexpr int HALO0 = NVAR + NVAR_STREAM;
+
+PDT_API int pdt_conv_nt_num_variants() { return NVAR + NVAR_STREAM + NVAR_HALO; }
+
+// 0: LDS-tiled, 1: streaming 1x1, 2: 3x3 halo-patch (conv3x3_halo.hip); -1: no such variant
+PDT_API int pdt_conv_nt_variant_kind(int v) {
+  if (v < 0 || v >= HALO0 + NVAR_HALO) return -1;
+  return v >= HALO0 ? 2 : (v >= NVAR ? 1 : 0);
+}
 
 PDT_API int pdt_conv_nt_resolve_variant(int variant, int M, int Ncol, int K) {
-  return (variant >= 0 && variant < NVAR + NVAR_STREAM) ? variant : heuristic_variant(M, Ncol, K);
+  return (variant >= 0 && variant < HALO0 + NVAR_HALO) ? variant : heuristic_variant(M, Ncol, K);
 }
 
 // Number of BN-statistics partial rows a launch of `variant` writes (sizes the stats buffer).
@@ -283,12 +293,14 @@ PDT_API int pdt_conv_nt_resolve_variant(int variant, int M, int Ncol, int K) {
 // one per M-tile (lanes and waves reduced in-block), or the stream kernel's row groups.
 PDT_API int pdt_conv_nt_bnb_rows(int M, int Ncol, int K, int variant) {
   int v = pdt_conv_nt_resolve_variant(variant, M, Ncol, K);
+  if (v >= HALO0) return halo_rows(M);
   if (v >= NVAR) return stream_rows(v - NVAR, M, Ncol);
   return (M + VAR_BM[v] - 1) / VAR_BM[v];
 }
 
 PDT_API int pdt_conv_nt_stat_rows(int M, int Ncol, int K, int variant) {
   int v = pdt_conv_nt_resolve_variant(variant, M, Ncol, K);
+  if (v >= HALO0) return halo_rows(M);
   if (v >= NVAR) return stream_rows(v - NVAR, M, Ncol);
   int BM = VAR_BM[v];
   return ((M + BM - 1) / BM) * VAR_WM[v];
@@ -343,6 +355,7 @@ static int conv_nt_impl(const void* src, const void* b, void* out, float* stats,
   }
   const int v = pdt_conv_nt_resolve_variant(variant, p.M, Ncol, K);
   p.nstat_rows = pdt_conv_nt_stat_rows(p.M, Ncol, K, v);
+  if (v >= HALO0) return run_halo(v - HALO0, p, stream);
   if (v >= NVAR) return run_stream(v - NVAR, p, stream);
   const bool cs64 = (Cs % 64) == 0;
   if (bnb.part != nullptr) return launch_variant_bnb(v, cs64, p, stream);

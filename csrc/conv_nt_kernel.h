@@ -995,4 +995,14 @@ int launch_variant(int v, const NTParams& p, hipStream_t st) {
 // the fused BatchNorm-backward instantiations (defined in conv_igemm_bnb.hip)
 int launch_variant_bnb(int v, bool cs64, const NTParams& p, hipStream_t st);
 
+// stride-1 pad-1 3x3 halo-patch kernels (conv3x3_halo.hip): variant hv in [0, NVAR_HALO)
+//   0: BN 64, 4 waves; 1: BN 128, 8 waves; 2: BN 128, 4 waves (112 x 64 per wave)
+constexpr int NVAR_HALO = 3;
+int run_halo(int hv, const NTParams& p, hipStream_t st);  // -5: geometry not supported
+int halo_rows(int M);                                     // stats / BN-backward partial rows
+// the halo weight gradient (conv3x3_halo.hip): plan (0 = applicable) and launch of the slab kernel
+int halo_wgrad_plan(int M, int Mo, int C, int Hs, int Ws, int* splits, int* tps);
+int run_halo_wgrad(const void* dy, const void* x, float* slab, int M, int Mo, int C, int Hs, int Ws, int splits,
+                   int tps, hipStream_t st);
+
 }  // namespace pdt_nt

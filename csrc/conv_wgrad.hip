@@ -27,6 +27,12 @@
 #include <stdlib.h>
 #include <type_traits>
 
+namespace pdt_nt {  // the 3x3 halo-patch weight gradient (conv3x3_halo.hip), variant id WG_NVAR
+int halo_wgrad_plan(int M, int Mo, int C, int Hs, int Ws, int* splits, int* tps);
+int run_halo_wgrad(const void* dy, const void* x, float* slab, int M, int Mo, int C, int Hs, int Ws, int splits,
+                   int tps, hipStream_t st);
+}  // namespace pdt_nt
+
 namespace {
 
 struct WGParams {
@@ -383,7 +389,8 @@ static WGVar wg_variant(int v, int Mo, int No) {
   return WG_VARS[v];
 }
 
-PDT_API int pdt_wgrad_num_variants() { return WG_NVAR; }
+// + 1: the 3x3 halo-patch kernel (id WG_NVAR; NOT_APPLICABLE (-5) outside stride-1 3x3 geometry)
+PDT_API int pdt_wgrad_num_variants() { return WG_NVAR + 1; }
 
 template <bool BIAS>
 static void launch_wg(const WGVar& w, dim3 grid, const WGParams& p, hipStream_t stream) {
@@ -440,6 +447,17 @@ PDT_API int pdt_wgrad_plan(int M, int Mo, int No, int variant, int* ktiles_per_s
   return splits;
 }
 
+// Plan with the conv geometry (the halo variant's split depends on it): splits, and the
+// per-split k-tiles (generic) or 224-pixel tiles (halo). -5: variant not applicable.
+PDT_API int pdt_wgrad_plan2(int M, int Mo, int No, int Hs, int Ws, int C, int variant, int* per_split) {
+  if (variant == WG_NVAR) {
+    int splits = 0;
+    const int rc = pdt_nt::halo_wgrad_plan(M, Mo, C, Hs, Ws, &splits, per_split);
+    return rc ? rc : splits;
+  }
+  return pdt_wgrad_plan(M, Mo, No, variant, per_split);
+}
+
 // stage-1 slab groups of the reduction: enough (column-block x group) blocks to stream the slabs
 static int reduce_groups(int splits, int Mo, int No) {
   long n4 = (long)Mo * No / 4;
@@ -466,6 +484,14 @@ PDT_API int pdt_conv_wgrad(const void* dy, const void* x, float* slab, float* ou
                            int accumulate, int variant, int pix, float* bias_out, hipStream_t stream) {
   if (C % 8 != 0 || Mo % 8 != 0 || No % 8 != 0 || ldy % 8 != 0) return -1;
   if (pix != 0 && (pix % 4 != 0 || pix > C)) return -10;
+  if (variant == WG_NVAR) {  // 3x3 / stride 1 / pad 1 halo-patch kernel
+    if (ntw != 3 || No != 9 * C || sh != 1 || sw != 1 || oh0 != -1 || ow0 != -1 || dh != 1 || dw != 1 ||
+        Hm != Hs || Wm != Ws || (pix != 0 && pix != C) || ldy != Mo || bias_out != nullptr || M % Wm != 0)
+      return -5;
+    const int rc = pdt_nt::run_halo_wgrad(dy, x, slab, M, Mo, C, Hs, Ws, splits, ktiles_per_split, stream);
+    if (rc) return rc;
+    return pdt_wgrad_reduce(slab, out, nullptr, nullptr, splits, Mo, No, scale, accumulate, stream);
+  }
   WGParams p;
   p.dy = (const u16*)dy;
   p.x = (const u16*)x;

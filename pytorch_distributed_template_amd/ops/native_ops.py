@@ -33,6 +33,7 @@ _SIGS = {
     "pdt_conv_nt_stat_rows": (c_int, [c_int, c_int, c_int, c_int]),
     "pdt_conv_nt_bnb_rows": (c_int, [c_int, c_int, c_int, c_int]),
     "pdt_conv_nt_num_variants": (c_int, []),
+    "pdt_conv_nt_variant_kind": (c_int, [c_int]),
     "pdt_conv_nt_resolve_variant": (c_int, [c_int, c_int, c_int, c_int]),
     "pdt_conv_nt": (c_int, [P, P, P, P, P, P, P] + [c_int] * 25 + [P, c_int, c_int, P]),
     "pdt_conv_nt_bnb": (c_int, [P] * 5 + [c_int] * 25 + [P] * 6 + [c_int] * 3 + [P]),
@@ -53,6 +54,7 @@ _SIGS = {
     "pdt_ln_bwd": (c_int, [P] * 9 + [c_int, c_int, c_int, P, P]),
     "pdt_gelu_bwd": (c_int, [P, P, P, c_long, P]),
     "pdt_wgrad_plan": (c_int, [c_int, c_int, c_int, c_int, ctypes.POINTER(c_int)]),
+    "pdt_wgrad_plan2": (c_int, [c_int] * 7 + [ctypes.POINTER(c_int)]),
     "pdt_wgrad_num_variants": (c_int, []),
     "pdt_wgrad_workspace": (c_long, [c_int, c_int, c_int]),
     "pdt_conv_wgrad": (c_int, [P, P, P, P] + [c_int] * 16 + [c_int, c_int, c_float, c_int, c_int, c_int, P, P]),
@@ -526,14 +528,17 @@ def conv_stat_rows(M, Ncol, K, variant):
 
 
 def _wgrad_launch(lib, dy, x, out, v, scale, accumulate, a, bias_out=None):
+    """One weight-gradient launch (+ slab reduction); returns the kernel's return code
+    (NOT_APPLICABLE: variant ``v`` cannot run this geometry)."""
     kps = c_int(0)
-    splits = lib.pdt_wgrad_plan(a["M"], a["Mo"], a["No"], v, ctypes.byref(kps))
+    splits = lib.pdt_wgrad_plan2(a["M"], a["Mo"], a["No"], a["Hs"], a["Ws"], a["C"], v, ctypes.byref(kps))
+    if splits < 0:
+        return splits
     slab = torch.empty(lib.pdt_wgrad_workspace(splits, a["Mo"], a["No"]), dtype=torch.float32, device=dy.device)
-    rc = lib.pdt_conv_wgrad(_p(dy), _p(x), _p(slab), _p(out), a["M"], a["Mo"], a["No"], a["ldy"], a["Hs"], a["Ws"],
-                            a["C"], a["Hm"], a["Wm"], a["sh"], a["sw"], a["oh0"], a["ow0"], a["dh"], a["dw"],
-                            a["ntw"], splits, kps.value, float(scale), int(accumulate), int(v), int(a.get("pix", 0)),
-                            _p(bias_out), _s())
-    _chk(rc, "conv_wgrad")
+    return lib.pdt_conv_wgrad(_p(dy), _p(x), _p(slab), _p(out), a["M"], a["Mo"], a["No"], a["ldy"], a["Hs"], a["Ws"],
+                              a["C"], a["Hm"], a["Wm"], a["sh"], a["sw"], a["oh0"], a["ow0"], a["dh"], a["dw"],
+                              a["ntw"], splits, kps.value, float(scale), int(accumulate), int(v),
+                              int(a.get("pix", 0)), _p(bias_out), _s())
 
 
 def conv_wgrad(dy, x, out, *, scale=1.0, accumulate=False, variant=None, bias_out=None, **a):
@@ -562,11 +567,14 @@ def conv_wgrad(dy, x, out, *, scale=1.0, accumulate=False, variant=None, bias_ou
             variant = -1
         else:
             best = _time_variants(lib.pdt_wgrad_num_variants(),
-                                  lambda v: _wgrad_launch(lib, dy, x, out, v, scale, False, a) or 0)
+                                  lambda v: _wgrad_launch(lib, dy, x, out, v, scale, False, a))
             table[key] = best
             _save_tuned()
             variant = best
-    _wgrad_launch(lib, dy, x, out, variant, scale, accumulate, a, bias_out)
+    rc = _wgrad_launch(lib, dy, x, out, variant, scale, accumulate, a, bias_out)
+    if rc == NOT_APPLICABLE:  # e.g. a tuned halo id for a geometry it does not cover: the heuristic tile
+        rc = _wgrad_launch(lib, dy, x, out, -1, scale, accumulate, a, bias_out)
+    _chk(rc, "conv_wgrad")
 
 
 def colsum(x, R, C):
