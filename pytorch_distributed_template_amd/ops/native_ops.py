@@ -119,6 +119,49 @@ def lib_path() -> Path:
     return _LIB_PATH
 
 
+class OpTimer:
+    """``PDT_OP_TIMING=1``: every launching entry point of the kernel library is bracketed
+    by HIP events, and its device time attributed to (entry point, integer arguments) --
+    the per-op, per-shape breakdown of a training step (scripts/op_profile.py). Query
+    entry points (plans, row counts, workspace sizes) pass through untimed."""
+    _QUERY = ("_rows", "_variants", "_plan", "_plan2", "_workspace", "_size", "_blocks", "_kind", "_resolve_variant",
+              "_part", "_words", "_grad_row", "_set_unroll", "_set_bwd_single")
+
+    def __init__(self, lib):
+        self._lib = lib
+        self.records = []
+        self.enabled = False
+
+    def __getattr__(self, name):
+        fn = getattr(self._lib, name)
+        if not name.startswith("pdt_") or name.endswith(self._QUERY):
+            return fn
+        ints = [i for i, t in enumerate(_SIGS.get(name, (None, []))[1]) if t in (c_int, c_long, c_uint)]
+
+        def call(*args):
+            if not self.enabled or _capturing():
+                return fn(*args)
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            rc = fn(*args)
+            e1.record()
+            self.records.append((name, tuple(args[i] for i in ints if i < len(args)), e0, e1))
+            return rc
+        return call
+
+    def summary(self, top=60):
+        """[(ms, calls, name, int-args)] sorted by total time (synchronises)."""
+        torch.cuda.synchronize()
+        agg = {}
+        for name, key, e0, e1 in self.records:
+            ms = e0.elapsed_time(e1)
+            ent = agg.setdefault((name, key), [0.0, 0])
+            ent[0] += ms
+            ent[1] += 1
+        rows = sorted(((v[0], v[1], k[0], k[1]) for k, v in agg.items()), key=lambda r: -r[0])
+        return rows[:top]
+
+
 def _load():
     global _lib
     if _lib is not None:
@@ -133,7 +176,7 @@ def _load():
                 fn = getattr(lib, name)
                 fn.restype = res
                 fn.argtypes = args
-            _lib = lib
+            _lib = OpTimer(lib) if os.environ.get("PDT_OP_TIMING", "0") == "1" else lib
     return _lib
 
 

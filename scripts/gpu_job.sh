@@ -33,8 +33,10 @@ for job in "$@"; do
       PDT_SLOW_TESTS=1 run ${TAG}_testss_$(echo "$args" | tr -c 'a-zA-Z0-9_\n' '_' | cut -c1-40).txt 1100 python -u -m pytest tests -m gpu -x -v -s --timeout 600 --timeout-method thread -k "$args" ;;
     smoke) run ${TAG}_smoke.txt 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) run ${TAG}_bench_$(echo "$args" | tr -c 'a-zA-Z0-9_\n' '_').txt 400 python bench.py $args ;;
-    benchlong)  # stock-stack runs whose MIOpen find takes minutes; find results kept in gpurun_out/miopen_db
+    benchlong)  # stock-stack runs whose MIOpen find takes minutes; find results kept in gpurun_out/miopen_db,
+                # seeded from the find db of earlier runs (profiles/miopen_db_bs2048: MIOpen's own text db)
       mkdir -p gpurun_out/miopen_db
+      cp -n profiles/miopen_db_bs2048/*.txt gpurun_out/miopen_db/ 2>/dev/null || true
       export MIOPEN_USER_DB_PATH=$PWD/gpurun_out/miopen_db
       run ${TAG}_benchlong_$(echo "$args" | tr -c 'a-zA-Z0-9_\n' '_').txt 1000 python bench.py $args ;;
     ktrace)

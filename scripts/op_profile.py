@@ -1,0 +1,96 @@
+"""Per-op, per-shape device-time breakdown of the bench training step.
+
+    python scripts/op_profile.py [--model resnet50] [--batch 2048] [--steps 2]
+
+Runs bench.py's model/optimizer/data path (no DDP, one GPU) for a few warm-up steps,
+then times every kernel-library launch of ``--steps`` steps with HIP events
+(ops.native_ops.OpTimer) and prints the top entries: total ms per step, calls per
+step, the entry point and its integer arguments (geometry, variant)."""
+import argparse
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from pytorch_distributed_template_amd import models  # noqa: E402
+from pytorch_distributed_template_amd.data.synthetic import SyntheticImageLoader  # noqa: E402
+from pytorch_distributed_template_amd.ops import fused, native_ops  # noqa: E402
+from pytorch_distributed_template_amd.optim import FusedAdamW, FusedSGD  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--model", default="resnet50")
+    ap.add_argument("--batch", type=int, default=2048)
+    ap.add_argument("--steps", type=int, default=2)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--fp8", action="store_true")
+    ap.add_argument("--top", type=int, default=70)
+    ap.add_argument("--cprofile", action="store_true",
+                    help="instead: host-side cProfile of --steps steps (where the Python issue time goes)")
+    a = ap.parse_args()
+    os.environ["PDT_OP_TIMING"] = "0" if a.cprofile else "1"  # read at the library's first load
+    fused.set_backend("native")
+    dev = torch.device("cuda", 0)
+    torch.manual_seed(0)
+    ctor = {"resnet50": models.resnet50, "resnet152": models.resnet152, "vit_b_16": models.vit_b_16}[a.model]
+    model = ctor(num_classes=1000, **({"fp8": True} if a.fp8 else {})).to(dev).to(memory_format=torch.channels_last)
+    if a.model.startswith("vit"):
+        opt = FusedAdamW(model.parameters(), lr=1e-3, weight_decay=0.05)
+    else:
+        opt = FusedSGD(model.parameters(), lr=0.1, momentum=0.9, weight_decay=5e-5)
+    batches = list(iter(SyntheticImageLoader(a.batch, num_samples=2 * a.batch, pool=2, device=dev)))
+
+    def step(i):
+        x, y = batches[i % 2]
+        opt.zero_grad(set_to_none=True)
+        fused.softmax_cross_entropy(model(x), y).backward()
+        opt.step()
+
+    lib = native_ops._load()
+    for i in range(a.warmup):
+        step(i)
+    torch.cuda.synchronize()
+    if a.cprofile:
+        import cProfile
+        import pstats
+        import time
+        pr = cProfile.Profile()
+        t0 = time.perf_counter()
+        pr.enable()
+        for i in range(a.steps):
+            step(i)
+        pr.disable()
+        t1 = time.perf_counter()
+        torch.cuda.synchronize()
+        t2 = time.perf_counter()
+        print(f"host issue {1e3 * (t1 - t0) / a.steps:.1f} ms/step (under cProfile), drain {1e3 * (t2 - t1):.1f} ms")
+        pstats.Stats(pr).sort_stats("tottime").print_stats(45)
+        return
+    lib.records.clear()
+    lib.enabled = True
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    ev0.record()
+    for i in range(a.steps):
+        step(i)
+    ev1.record()
+    lib.enabled = False
+    rows = lib.summary(top=10 ** 6)
+    wall = ev0.elapsed_time(ev1) / a.steps
+    total = sum(r[0] for r in rows) / a.steps
+    print(f"{a.model} bs {a.batch}: {wall:.2f} ms/step wall, {total:.2f} ms/step inside library calls, "
+          f"{sum(r[1] for r in rows) / a.steps:.0f} calls/step")
+    by_name = {}
+    for ms, n, name, key in rows:
+        by_name[name] = by_name.get(name, 0.0) + ms / a.steps
+    print("by entry point:")
+    for name, ms in sorted(by_name.items(), key=lambda x: -x[1]):
+        print(f"  {ms:8.3f} ms {100 * ms / total:5.1f}%  {name}")
+    print("top (entry point, integer args):")
+    for ms, n, name, key in rows[:a.top]:
+        print(f"  {ms / a.steps:8.3f} ms {n // a.steps:3d}x  {name} {key}")
+
+
+if __name__ == "__main__":
+    main()
