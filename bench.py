@@ -351,6 +351,13 @@ def main():
         torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
     elapsed = float(t.item())
     final_loss = float(loss.item())
+    # host enqueue cost of one step with an idle GPU (cpu_issue above includes the time the
+    # host waits on a full submission queue while the GPU is busy)
+    sync()
+    h0 = time.perf_counter()
+    step(args.steps)
+    host_enqueue_ms = (time.perf_counter() - h0) * 1e3
+    sync()
 
     ms = elapsed / args.steps * 1e3
     value = world * args.batch * args.steps / elapsed
@@ -382,6 +389,7 @@ def main():
                    "rccl_version": _rccl_version(), "device": args.device,
                    "final_loss": round(final_loss, 4), "hip_graph": args.graph,
                    "cpu_issue_ms_per_step": round(cpu_issue / args.steps * 1e3, 3),
+                   "host_enqueue_ms_idle_gpu": round(host_enqueue_ms, 3),
                    "baseline": stock_ref,
                    "vs_best_stock": ({"ratio": round(value / (best[0] * world), 4), "stock_img_s": best[0],
                                       "stock_per_gpu_batch": best[1]} if best else None),

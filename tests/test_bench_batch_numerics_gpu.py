@@ -8,8 +8,9 @@ along the batch (per-image ops, so chunking is exact) and BatchNorm over the FUL
 batch, which keeps MIOpen on small, fast problems.
 
 * the stem node (conv 7x7/2 + BN + ReLU + max-pool) and layer1.0 (bottleneck with
-  downsample), forward and backward, vs fp32: relative Frobenius error < 0.03
-  (the yardstick floor of tests/test_bench_geometry_gpu.py);
+  downsample), forward and backward, vs fp32: relative Frobenius error no worse than
+  max(3 x the stock bf16 autocast error, 0.03) (the yardstick of
+  tests/test_bench_geometry_gpu.py);
 * 3 SGD steps of the whole ResNet-50 at bs 2048 on the native kernels vs the same
   steps in fp32 on the stock ops: the loss trajectory agrees to 1 %.
 """
@@ -77,21 +78,32 @@ def _compare(name, fn, x, params, tol=0.03, need_dx=True):
     out_n, gp_n = yn.detach().float(), _grads(params)
     dx_n = xn.grad.float() if need_dx else None
     del yn, xn
-    # fp32 reference (stock ops, chunked convs)
-    for p in params:
-        p.grad = None
-    fused.set_backend("torch")
-    xr = x.detach().float().requires_grad_(need_dx)
-    with chunked_fp32_convs():
-        yr = fn(xr)
-    yr.backward(gy.float())
-    fused.set_backend("auto")
-    errs = [nrmerr(out_n, yr.detach())] + ([nrmerr(dx_n, xr.grad)] if need_dx else []) + \
-        [nrmerr(a, b) for a, b in zip(gp_n, _grads(params))]
-    del yr, xr
+    def stock(autocast):
+        for p in params:
+            p.grad = None
+        fused.set_backend("torch")
+        xr = x.detach().float().requires_grad_(need_dx)
+        with chunked_fp32_convs(), torch.autocast("cuda", dtype=torch.bfloat16, enabled=autocast):
+            yr = fn(xr)
+        yr.float().backward(gy.float() if not autocast else gy.to(yr.dtype))
+        fused.set_backend("auto")
+        res = (yr.detach().float(), xr.grad.float() if need_dx else None, _grads(params))
+        del yr, xr
+        return res
+
+    # fp32 reference (stock ops, chunked convs), then the stock bf16 autocast yardstick: the
+    # gradient of a conv feeding a BatchNorm cancels strongly (BN's dy has zero mean and is
+    # orthogonal to y per channel), so bf16 rounding alone costs it ~7-14 % (round 2 logs)
+    yr, dxr, pr = stock(False)
+    ya, dxa, pa = stock(True)
+    pairs = [(out_n, yr, ya)] + ([(dx_n, dxr, dxa)] if need_dx else []) + list(zip(gp_n, pr, pa))
+    en = [nrmerr(n_, r_) for n_, r_, _ in pairs]
+    ea = [nrmerr(a_, r_) for _, r_, a_ in pairs]
+    del yr, dxr, pr, ya, dxa, pa, pairs
     torch.cuda.empty_cache()
-    print(f"{name}: {['%.4f' % e for e in errs]}")
-    assert max(errs) < tol, (name, errs)
+    msg = f"{name}: native {['%.4f' % e for e in en]} autocast {['%.4f' % e for e in ea]}"
+    print(msg)
+    assert all(e <= max(3 * a, tol) for e, a in zip(en, ea)), msg
     return out_n
 
 
