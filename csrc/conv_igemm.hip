@@ -312,7 +312,8 @@ static int conv_nt_impl(const void* src, const void* b, void* out, float* stats,
                         int Hs, int Ws, int Cs, int Nimg, int Hm, int Wm, int Ncol, int K, int ldb,
                         int sh, int sw, int oh0, int ow0, int dh, int dw, int nth, int ntw,
                         int Ho, int Wo, int osh, int osw, int oph, int opw, int ldo, int act,
-                        void* aux, int variant, const BnbArgs& bnb, int pix, hipStream_t stream) {
+                        void* aux, int variant, const BnbArgs& bnb, int pix, hipStream_t stream,
+                        const AXArgs& ax = AXArgs{}) {
   if (Cs % 8 != 0 || K % 8 != 0 || Ncol % 8 != 0 || ldo % 8 != 0 || ldb % 8 != 0) return -1;
   if (pix != 0 && (pix % 4 != 0 || pix > Cs)) return -10;
   if (K != nth * ntw * Cs) return -2;
@@ -338,6 +339,7 @@ static int conv_nt_impl(const void* src, const void* b, void* out, float* stats,
   p.dq_a = p.dq_b = nullptr;
   p.q8 = nullptr; p.q8_meta = nullptr; p.q8_part = nullptr; p.q8_fmt = 0; p.q8_only = 0;
   p.bnb = bnb;
+  p.ax = ax;
   if (bnb.part != nullptr && (stats != nullptr || bias != nullptr || act != 0 || aux != nullptr || ldo != Ncol))
     return -7;  // the fused BN-backward epilogue is for plain (dense-output) data gradients
   p.div_Wm = make_fastdiv(Wm);
@@ -355,6 +357,15 @@ static int conv_nt_impl(const void* src, const void* b, void* out, float* stats,
   }
   const int v = pdt_conv_nt_resolve_variant(variant, p.M, Ncol, K);
   p.nstat_rows = pdt_conv_nt_stat_rows(p.M, Ncol, K, v);
+  if (ax.mode != 0) {
+    // the A-staging BN apply: 1x1, stride 1, unpadded, dense rows, 32-bit element offsets
+    if (nth != 1 || ntw != 1 || sh != 1 || sw != 1 || oh0 != 0 || ow0 != 0 || p.pix != Cs || Cs % 64 != 0 ||
+        bias != nullptr || aux != nullptr || act != 0 || addend != nullptr || ax.y2 == nullptr || ax.c1 == nullptr ||
+        ax.c2 == nullptr || (ax.mode == 2 && (ax.c3 == nullptr || ax.mask_in == nullptr)) ||
+        (long long)p.M * Cs >= (1LL << 31) || v >= NVAR)
+      return -5;
+    return launch_variant_ax(v, p, stream);
+  }
   if (v >= HALO0) return run_halo(v - HALO0, p, stream);
   if (v >= NVAR) return run_stream(v - NVAR, p, stream);
   const bool cs64 = (Cs % 64) == 0;
@@ -390,6 +401,29 @@ PDT_API int pdt_conv_nt_bnb(const void* src, const void* b, void* out, const voi
   return conv_nt_impl(src, b, out, nullptr, nullptr, addend, addend_mask, Hs, Ws, Cs, Nimg, Hm, Wm, Ncol, K, ldb, sh,
                       sw, oh0, ow0, dh, dw, nth, ntw, Ho, Wo, osh, osw, oph, opw, ldo, 0, nullptr, variant, bnb, 0,
                       stream);
+}
+
+// 1x1 GEMM with the BatchNorm apply folded into its A staging (AXArgs in conv_nt_kernel.h):
+// ax_mode 1 = forward (optional BN statistics of the output: stats), ax_mode 2 = the
+// BN-backward apply (with the fused bn partials of the unit the output feeds: part != 0).
+// NOT_APPLICABLE (-5) for variants without an AX instantiation.
+PDT_API int pdt_conv_nt_ax(const void* src, const void* b, void* out, float* stats,
+                           int Hs, int Ws, int Cs, int Nimg, int Hm, int Wm, int Ncol, int K, int ldb,
+                           int ldo, int variant,
+                           const void* bn_y, const float* bn_mean, const float* bn_scale, const float* bn_shift,
+                           const void* bn_mask, float* part, int relu, int row0, int R,
+                           int ax_mode, const void* ax_y2, const float* ax_c1, const float* ax_c2,
+                           const float* ax_c3, const float* ax_rsc, const float* ax_rsh, const void* ax_mask_in,
+                           void* ax_mask_out, void* ax_dst, hipStream_t stream) {
+  if (ax_mode != 1 && ax_mode != 2) return -8;
+  if (part != nullptr && (bn_y == nullptr || bn_mean == nullptr)) return -8;
+  if (part != nullptr && relu && bn_mask == nullptr && (bn_scale == nullptr || bn_shift == nullptr)) return -8;
+  if ((long long)Nimg * Hm * Wm * ldo >= (1LL << 31)) return -9;
+  BnbArgs bnb{(const u16*)bn_y, bn_mean, bn_scale, bn_shift, (const uint8_t*)bn_mask, part, relu, row0, R};
+  AXArgs ax{ax_mode, (const u16*)ax_y2, ax_c1, ax_c2, ax_c3, ax_rsc, ax_rsh, (const uint8_t*)ax_mask_in,
+            (uint8_t*)ax_mask_out, (u16*)ax_dst};
+  return conv_nt_impl(src, b, out, stats, nullptr, nullptr, nullptr, Hs, Ws, Cs, Nimg, Hm, Wm, Ncol, K, ldb, 1, 1,
+                      0, 0, 1, 1, 1, 1, Hm, Wm, 1, 1, 0, 0, ldo, 0, nullptr, variant, bnb, 0, stream, ax);
 }
 
 // ---------------------------------------------------------------------------
@@ -456,6 +490,7 @@ static int gemm_f8_impl(const void* a, const void* b, void* out, const float* bi
   p.dq_a = dq_a;
   p.dq_b = dq_b;
   p.bnb = BnbArgs{};
+  p.ax = AXArgs{};
   p.div_Wm = make_fastdiv(1);
   p.div_HWm = make_fastdiv(1);
   p.div_Cs8 = make_fastdiv(K / 16);

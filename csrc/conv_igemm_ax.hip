@@ -1,0 +1,35 @@
+// Instantiations of the implicit-GEMM kernel (conv_nt_kernel.h) with the BatchNorm apply
+// folded into the A-operand staging (AXArgs): mode 1 = the forward bn3(+residual)+ReLU
+// of the previous ResNet block applied by the next block's conv1 (plain epilogue, BN
+// statistics of conv1's output); mode 2 = the bn3 backward apply applied by conv3's
+// data-gradient GEMM (with the fused bn2 BatchNorm-backward epilogue). Register-staged
+// tiles only; a separate translation unit like conv_igemm_bnb.hip.
+#include "conv_nt_kernel.h"
+
+namespace pdt_nt {
+
+template <int AX, bool BNB>
+static int launch_ax(int v, const NTParams& p, hipStream_t st) {
+  switch (v) {
+    case 0: return launch<128, 128, 2, true, false, false, 256, 2, 0, 0, BNB, AX>(p, st);
+    case 1: return launch<256, 64, 2, true, false, false, 256, 2, 0, 0, BNB, AX>(p, st);
+    case 3: return launch<128, 64, 2, true, false, false, 256, 2, 0, 0, BNB, AX>(p, st);
+    case 5: return launch<128, 128, 1, true, false, false, 256, 2, 0, 0, BNB, AX>(p, st);
+    case 6: return launch<256, 64, 1, true, false, false, 256, 2, 0, 0, BNB, AX>(p, st);
+    case 8: return launch<128, 64, 1, true, false, false, 256, 2, 0, 0, BNB, AX>(p, st);
+    case 10: return launch<128, 128, 2, true, true, false, 256, 2, 0, 0, BNB, AX>(p, st);
+    case 13: return launch<128, 64, 2, true, true, false, 256, 2, 0, 0, BNB, AX>(p, st);
+    case 15: return launch<128, 128, 1, true, true, false, 256, 2, 0, 0, BNB, AX>(p, st);
+    case 16: return launch<256, 64, 1, true, true, false, 256, 2, 0, 0, BNB, AX>(p, st);
+    case 18: return launch<128, 64, 1, true, true, false, 256, 2, 0, 0, BNB, AX>(p, st);
+  }
+  return -5;  // NOT_APPLICABLE: no AX instantiation of this tile
+}
+
+int launch_variant_ax(int v, const NTParams& p, hipStream_t st) {
+  if (p.ax.mode == 1 && p.bnb.part == nullptr) return launch_ax<1, false>(v, p, st);
+  if (p.ax.mode == 2 && p.bnb.part != nullptr) return launch_ax<2, true>(v, p, st);
+  return -5;
+}
+
+}  // namespace pdt_nt

@@ -25,6 +25,30 @@ struct BnbArgs {
   int relu, row0, R;
 };
 
+// BatchNorm apply folded into the A-operand staging of a 1x1 GEMM (register-staged
+// variants only), so the BN'd tensor is produced by its consumer instead of by a
+// separate element pass that writes it and a GEMM that re-reads it. The A loads read
+// `src` (and `y2`), the staging pass applies the BN, feeds the MFMAs and -- in the
+// tn == 0 workgroups, which stage every A row exactly once -- writes the result to
+// `dst` (and the ReLU bit mask), bit-identical to the element pass (csrc/bn_act.hip).
+//   mode 1 (forward, the next conv1):  A = relu(src*c1 + c2 + y2)       (src = y3, y2 = residual)
+//                                      y2 term = y2*rsc + rsh when rsc (raw downsample output)
+//                                      dst = the block output, mask_out = its ReLU bit mask
+//   mode 2 (backward, conv3's dgrad):  A = c1*gate(src) + c2*y2 + c3   (src = dout, y2 = y3,
+//                                      gate = mask_in bit), dst = dy3 (the wgrad operand)
+struct AXArgs {
+  int mode;
+  const u16* y2;
+  const float* c1;
+  const float* c2;
+  const float* c3;
+  const float* rsc;
+  const float* rsh;
+  const uint8_t* mask_in;
+  uint8_t* mask_out;
+  u16* dst;
+};
+
 struct NTParams {
   const u16* src;
   const u16* b;
@@ -50,6 +74,7 @@ struct NTParams {
   const float* dq_a;   // fp8 only: dequant scale of the A (src) operand (device scalar)
   const float* dq_b;   // fp8 only: dequant scale of the B operand
   BnbArgs bnb;         // optional: BatchNorm-backward partial sums of the unit this output feeds
+  AXArgs ax;           // optional (AX instantiations): BN apply in the A staging
   FastDiv div_Wm, div_HWm, div_Cs8, div_ntw;
   // optional fp8 copy of the final output for the NEXT fp8 GEMM (staged epilogue only):
   // codes of the bf16-rounded values times q8_meta[0] (its delayed scale), same layout
@@ -97,8 +122,9 @@ static __device__ __attribute__((aligned(64))) u32x4 pdt_zero_chunk[4];
 // quarters stay in flight across every barrier (the schedule of the guide's 256^2 8-phase
 // template, 4 phases per K-tile).
 template <int BM, int BN, int NSTAGE, bool CS64, bool DIRECT, bool GLDS, int NTH = 256, int WM = 2, int F8 = 0,
-          int PIPE = 0, bool BNB = false>
+          int PIPE = 0, bool BNB = false, int AX = 0>
 __global__ void __launch_bounds__(NTH, PIPE ? 1 : 2) conv_nt_kernel(NTParams p) {
+  static_assert(AX == 0 || (!GLDS && !PIPE && F8 == 0 && CS64), "the A-staging BN apply needs register staging");
   constexpr int WN = NTH / 64 / WM;       // waves along N
   constexpr int MI = BM / (WM * 16);      // 16-row MFMA tiles per wave
   constexpr int NI = BN / (WN * 16);
@@ -162,6 +188,13 @@ __global__ void __launch_bounds__(NTH, PIPE ? 1 : 2) conv_nt_kernel(NTParams p) 
 
   u32x4 ra[LA], rb[LB];
   const int nk = (p.K + BK - 1) / BK;
+  // AX: the second A operand, the mask bytes, the element offset of each staged chunk
+  // (-1: padding / out of range) and this thread's 8 channels' coefficients for the k-tile
+  u32x4 ry[AX ? LA : 1];
+  uint32_t rmk[AX ? LA : 1];
+  int roff[AX ? LA : 1];
+  float cf1[AX ? 8 : 1], cf2[AX ? 8 : 1], cf3[AX == 2 ? 8 : 1], cfs[AX == 1 ? 8 : 1], cfh[AX == 1 ? 8 : 1];
+  const bool ax_write = AX != 0 && p.ax.dst != nullptr && tn == 0;
 
   auto load_tile = [&](int kt) {
     const int k0 = kt * BK;
@@ -175,10 +208,37 @@ __global__ void __launch_bounds__(NTH, PIPE ? 1 : 2) conv_nt_kernel(NTParams p) 
       for (int i = 0; i < LA; ++i) {
         int ih = a_ih[i] + dho, iw = a_iw[i] + dwo;
         bool ok = a_ok[i] && (unsigned)ih < (unsigned)p.Hs && (unsigned)iw < (unsigned)p.Ws;
+        const size_t off = (size_t)(a_base[i] + ih * p.Ws + iw) * p.pix + c0;
         if (ok) {
-          ra[i] = *reinterpret_cast<const u32x4*>(p.src + (size_t)(a_base[i] + ih * p.Ws + iw) * p.pix + c0);
+          ra[i] = *reinterpret_cast<const u32x4*>(p.src + off);
         } else {
           ra[i] = u32x4{0, 0, 0, 0};
+        }
+        if constexpr (AX != 0) {
+          roff[i] = ok ? (int)off : -1;  // host guarantees 32-bit element offsets
+          ry[i] = ok ? *reinterpret_cast<const u32x4*>(p.ax.y2 + off) : u32x4{0, 0, 0, 0};
+          rmk[i] = (AX == 2 && ok) ? (uint32_t)p.ax.mask_in[off >> 3] : 0u;
+        }
+      }
+      if constexpr (AX != 0) {
+#pragma unroll
+        for (int e = 0; e < 8; e += 4) {
+          const f32x4 a = *reinterpret_cast<const f32x4*>(p.ax.c1 + c0 + e);
+          const f32x4 b = *reinterpret_cast<const f32x4*>(p.ax.c2 + c0 + e);
+#pragma unroll
+          for (int q = 0; q < 4; ++q) { cf1[e + q] = a[q]; cf2[e + q] = b[q]; }
+          if constexpr (AX == 2) {
+            const f32x4 c = *reinterpret_cast<const f32x4*>(p.ax.c3 + c0 + e);
+#pragma unroll
+            for (int q = 0; q < 4; ++q) cf3[e + q] = c[q];
+          }
+          if constexpr (AX == 1) {
+            const bool raff = p.ax.rsc != nullptr;
+            const f32x4 c = raff ? *reinterpret_cast<const f32x4*>(p.ax.rsc + c0 + e) : f32x4{1.f, 1.f, 1.f, 1.f};
+            const f32x4 d = raff ? *reinterpret_cast<const f32x4*>(p.ax.rsh + c0 + e) : f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int q = 0; q < 4; ++q) { cfs[e + q] = c[q]; cfh[e + q] = d[q]; }
+          }
         }
       }
     } else {
@@ -211,11 +271,57 @@ __global__ void __launch_bounds__(NTH, PIPE ? 1 : 2) conv_nt_kernel(NTParams p) 
     }
   };
 
+  // AX: apply the BN to the staged A chunk (same arithmetic as csrc/bn_act.hip's element
+  // passes), write it (+ mask) once from the tn == 0 workgroups
+  auto ax_apply = [&](int i) __attribute__((always_inline)) {
+    if constexpr (AX != 0) {
+      if (roff[i] < 0) return;  // padding / out-of-range rows stay zero (never written)
+      float f[8], r[8];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        f[2 * e] = lo_bf(ra[i][e]); f[2 * e + 1] = hi_bf(ra[i][e]);
+        r[2 * e] = lo_bf(ry[i][e]); r[2 * e + 1] = hi_bf(ry[i][e]);
+      }
+      u32x4 o;
+      if constexpr (AX == 1) {
+        const bool raff = p.ax.rsc != nullptr;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          f[k] = f[k] * cf1[k] + cf2[k];
+          f[k] += raff ? r[k] * cfs[k] + cfh[k] : r[k];
+          f[k] = fmaxf(f[k], 0.f);
+        }
+#pragma unroll
+        for (int e = 0; e < 4; ++e) o[e] = pack2bf(f[2 * e], f[2 * e + 1]);
+        if (ax_write && p.ax.mask_out != nullptr) {
+          uint32_t m = 0;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {  // mask of the ROUNDED output, as bn_apply_kernel
+            m |= ((o[e] & 0x7fffu) != 0 && !(o[e] & 0x8000u)) ? (1u << (2 * e)) : 0u;
+            m |= ((o[e] & 0x7fff0000u) != 0 && !(o[e] & 0x80000000u)) ? (1u << (2 * e + 1)) : 0u;
+          }
+          p.ax.mask_out[roff[i] >> 3] = (uint8_t)m;
+        }
+      } else {
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          const float g = (rmk[i] >> k) & 1u ? f[k] : 0.f;
+          f[k] = cf1[k] * g + cf2[k] * r[k] + cf3[k];
+        }
+#pragma unroll
+        for (int e = 0; e < 4; ++e) o[e] = pack2bf(f[2 * e], f[2 * e + 1]);
+      }
+      if (ax_write) *reinterpret_cast<u32x4*>(p.ax.dst + roff[i]) = o;
+      ra[i] = o;
+    }
+  };
+
   auto store_tile = [&](int buf) {
     char* sa = smem + buf * STAGE;
     char* sb = sa + A_BYTES;
 #pragma unroll
     for (int i = 0; i < LA; ++i) {
+      ax_apply(i);
       int r = (tid >> 3) + RS * i;
       *reinterpret_cast<u32x4*>(sa + r * 128 + swz(r, ca) * 16) = ra[i];
     }
@@ -904,11 +1010,11 @@ __global__ void __launch_bounds__(NTH, PIPE ? 1 : 2) conv_nt_kernel(NTParams p) 
 }
 
 template <int BM, int BN, int NS, bool CS64, bool DIRECT, bool GLDS = false, int NTH = 256, int WM = 2, int F8 = 0,
-          int PIPE = 0, bool BNB = false>
+          int PIPE = 0, bool BNB = false, int AX = 0>
 int launch(const NTParams& p, hipStream_t st) {
   int ntm = (p.M + BM - 1) / BM, ntn = (p.Ncol + BN - 1) / BN;
-  hipLaunchKernelGGL((conv_nt_kernel<BM, BN, NS, CS64, DIRECT, GLDS, NTH, WM, F8, PIPE, BNB>), dim3(ntm * ntn),
-                     dim3(NTH), 0, st, p);
+  hipLaunchKernelGGL((conv_nt_kernel<BM, BN, NS, CS64, DIRECT, GLDS, NTH, WM, F8, PIPE, BNB, AX>),
+                     dim3(ntm * ntn), dim3(NTH), 0, st, p);
   PDT_RETURN_LAUNCH();
 }
 
@@ -994,6 +1100,11 @@ int launch_variant(int v, const NTParams& p, hipStream_t st) {
 
 // the fused BatchNorm-backward instantiations (defined in conv_igemm_bnb.hip)
 int launch_variant_bnb(int v, bool cs64, const NTParams& p, hipStream_t st);
+
+// The A-staging BN apply (AXArgs) is instantiated for some register-staged tiles
+// (conv_igemm_ax.hip: mode 1 plain epilogue, mode 2 with the BN-backward epilogue);
+// other variant ids return NOT_APPLICABLE (-5).
+int launch_variant_ax(int v, const NTParams& p, hipStream_t st);
 
 // stride-1 pad-1 3x3 halo-patch kernels (conv3x3_halo.hip): variant hv in [0, NVAR_HALO)
 //   0: BN 64, 4 waves; 1: BN 128, 8 waves; 2: BN 128, 4 waves (112 x 64 per wave)

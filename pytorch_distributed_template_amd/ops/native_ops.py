@@ -30,6 +30,7 @@ c_int, c_long, c_float, c_double, c_void_p, c_uint = (ctypes.c_int, ctypes.c_lon
 P = c_void_p
 
 _SIGS = {
+    "pdt_conv_nt_ax": (c_int, [P] * 4 + [c_int] * 11 + [P] * 6 + [c_int] * 3 + [c_int] + [P] * 9 + [P]),
     "pdt_conv_nt_stat_rows": (c_int, [c_int, c_int, c_int, c_int]),
     "pdt_conv_nt_bnb_rows": (c_int, [c_int, c_int, c_int, c_int]),
     "pdt_conv_nt_num_variants": (c_int, []),
@@ -1066,6 +1067,82 @@ def _unit_dx(dy, u: _Unit, addend=None, addend_mask=None, bnb_unit=None, bnb_mas
     return dx[:, :u.C] if u.Cs != u.C else dx
 
 
+# -----------------------------------------------------------------------------
+# BatchNorm apply folded into a 1x1 GEMM's A staging (csrc/conv_nt_kernel.h AXArgs):
+# the BN'd tensor is produced by the GEMM that consumes it (and written once for its
+# other consumers) instead of by an element pass + a re-read. PDT_FUSE_BN_AX=0 disables.
+# -----------------------------------------------------------------------------
+AX_VARIANTS = (0, 1, 3, 5, 6, 8, 10, 13, 15, 16, 18)  # csrc/conv_igemm_ax.hip
+
+
+def _ax_enabled() -> bool:
+    return os.environ.get("PDT_FUSE_BN_AX", "1") != "0"
+
+
+def _ax_launch(lib, src, b, out, v, a, stats=None, bnb=None, ax=None):
+    """One pdt_conv_nt_ax launch. ``bnb`` = (y, mean, scale, shift, mask, part, relu, row0, R) or None;
+    ``ax`` = (mode, y2, c1, c2, c3, rsc, rsh, mask_in, mask_out, dst)."""
+    bn = bnb if bnb is not None else (None, None, None, None, None, None, 0, 0, 0)
+    mode, y2, c1, c2, c3, rsc, rsh, mki, mko, dst = ax
+    return lib.pdt_conv_nt_ax(_p(src), _p(b), _p(out), _p(stats), a["Hs"], a["Ws"], a["Cs"], a["Nimg"], a["Hm"],
+                              a["Wm"], a["Ncol"], a["K"], a["ldb"], a["ldo"], int(v), _p(bn[0]), _p(bn[1]),
+                              _p(bn[2]), _p(bn[3]), _p(bn[4]), _p(bn[5]), int(bn[6]), int(bn[7]), int(bn[8]),
+                              int(mode), _p(y2), _p(c1), _p(c2), _p(c3), _p(rsc), _p(rsh), _p(mki), _p(mko), _p(dst),
+                              _s())
+
+
+def _ax_select(key, run):
+    """Tile for an AX launch (tuned over the AX instantiations on first use when allowed);
+    ``run(v)`` launches variant v (with the caller's scratch outputs) and returns its code."""
+    table = _tuned()
+    if key in table:
+        return int(table[key])
+    if not _tune_allowed():
+        return AX_VARIANTS[3]  # 128x128, one LDS stage
+    best = _time_variants(max(AX_VARIANTS) + 1, run, set(AX_VARIANTS))
+    table[key] = best
+    _save_tuned()
+    return best
+
+
+def _conv3_dgrad_bn_bwd(dout, u3, k1, k2, k3, dy3, u2):
+    """Data gradient of a bottleneck's conv3 (1x1) with bn3's backward apply folded into its A
+    staging: A = dy3 = k1*gate(dout) + k2*y3 + k3 (gate: u3's ReLU bit mask), written to ``dy3``
+    for the weight gradient; bn2's backward partials in the epilogue (as ``_unit_dx(...,
+    bnb_unit=u2)``). Returns (da2, _BnbPartials) or None when the geometry is not covered."""
+    N, Cout, H, W = u3.y.shape
+    Cin = u3.C
+    if u3.g["KH"] != 1 or u3.g["sh"] != 1 or u3.Cs != Cin or Cout % 64 or u2.Cout != Cin or u3.mask is None:
+        return None
+    lib = _load()
+    wt = _DGRAD_W.get(u3.w, Cout, 1, 1, Cin, 0, 0, 1, 1, 1)
+    da2 = _empty_cl(N, Cin, H, W, torch.bfloat16, dout.device)
+    a = dict(Hs=H, Ws=W, Cs=Cout, Nimg=N, Hm=H, Wm=W, Ncol=Cin, K=Cout, ldb=Cout, ldo=Cin)
+    M = N * H * W
+    assert u2.y.shape == da2.shape and u2.y.is_contiguous(memory_format=torch.channels_last)
+    ax = (2, u3.y, k1, k2, k3, None, None, u3.mask, None, dy3)
+
+    def bnb(part, R):
+        return (u2.y, u2.mean, u2.scale, u2.shift, None, part, 1, 0, R)
+
+    def run(v):
+        R = lib.pdt_conv_nt_bnb_rows(M, Cin, Cout, v)
+        part = torch.empty(2 * R * Cin, dtype=torch.float32, device=dout.device)
+        return _ax_launch(lib, dout, wt, da2, v, a, bnb=bnb(part, R), ax=ax)
+
+    key = "axb:" + ",".join(str(x) for x in (H, W, Cout, N, Cin))
+    v = _ax_select(key, run)
+    if v < 0:
+        return None
+    R = lib.pdt_conv_nt_bnb_rows(M, Cin, Cout, v)
+    part = torch.empty(2 * R * Cin + lib.pdt_rows_reduce_workspace(R, Cin), dtype=torch.float32, device=dout.device)
+    rc = _ax_launch(lib, dout, wt, da2, v, a, bnb=bnb(part, R), ax=ax)
+    if rc == NOT_APPLICABLE:
+        return None
+    _chk(rc, "conv_nt_ax (bn3 backward apply + conv3 dgrad)")
+    return da2, _BnbPartials(part, R, u2)
+
+
 def _unit_dw(dy, u: _Unit):
     w = u.w
     KH, KW = u.g["KH"], u.g["KW"]
@@ -1237,10 +1314,23 @@ class _Bottleneck(torch.autograd.Function):
             _chk(_load().pdt_bn_bwd_apply_dual(_p(dout), _p(u3.mask), _p(u3.y), _p(a1), _p(a2), _p(a3), _p(dy3),
                                                _p(ud.y), _p(b1), _p(b2), _p(b3), _p(dyd), M3, u3.Cout, _s()),
                  "bn_bwd_apply_dual")
-        else:
-            dy3, _, dg3, db3 = _bn_bwd(dout, u3, False, pre=_take_bnb(u3, dout))
         fuse = _bnb_enabled()
-        if fuse:  # bn2 / bn1 backward reductions in the epilogues of the conv3 / conv2 dgrads
+        fused3 = None
+        if not dual and fuse and _ax_enabled() and u3.mask is not None:
+            # bn3's backward apply inside conv3's data-gradient A staging (dy3 written once, for
+            # the weight gradient): no separate element pass, no re-read of dy3 by the dgrad
+            dg3, db3, k1, k2, k3 = _bn_bwd(dout, u3, False, pre=_take_bnb(u3, dout), coeffs_only=True)
+            dy3 = torch.empty_like(u3.y, memory_format=torch.channels_last)
+            fused3 = _conv3_dgrad_bn_bwd(dout, u3, k1, k2, k3, dy3, u2)
+            if fused3 is None:  # not covered: the element pass
+                _chk(_load().pdt_bn_bwd_apply(_p(dout), _p(u3.y), None, _p(u3.scale), _p(u3.shift), _p(k1), _p(k2),
+                                              _p(k3), _p(dy3), None, u3.y.numel() // u3.Cout, u3.Cout, 1,
+                                              _p(u3.mask), _s()), "bn_bwd_apply")
+        elif not dual:
+            dy3, _, dg3, db3 = _bn_bwd(dout, u3, False, pre=_take_bnb(u3, dout))
+        if fused3 is not None:
+            da2, pre2 = fused3
+        elif fuse:  # bn2 / bn1 backward reductions in the epilogues of the conv3 / conv2 dgrads
             da2, pre2 = _unit_dx(dy3, u3, bnb_unit=u2)
         else:
             da2, pre2 = _unit_dx(dy3, u3), None

@@ -1,0 +1,133 @@
+"""BatchNorm applies folded into the A staging of the consuming 1x1 GEMM
+(csrc/conv_nt_kernel.h AXArgs, csrc/conv_igemm_ax.hip):
+
+* the tensor the fold writes for its other consumers (the block output + ReLU bit mask
+  in the forward; dy3 in the backward) equals the element pass (csrc/bn_act.hip) it
+  replaces to within one bf16 rounding (the two kernels may contract the same fp32
+  expression into FMAs differently), for every AX tile;
+* the GEMM output equals the unfused GEMM on the element pass's output;
+* a whole identity bottleneck's backward with the fold on matches the fold off.
+"""
+import os
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+from pytorch_distributed_template_amd.ops import native_ops as no  # noqa: E402
+
+
+def _cl(t):
+    return t.contiguous(memory_format=torch.channels_last)
+
+
+def assert_one_rounding(a, b, what):
+    """a, b: bf16 results of the same fp32 expression: equal up to one bf16 ulp of the result."""
+    a, b = a.float(), b.float()
+    bad = ((a - b).abs() > b.abs() * 2.0 ** -7 + 1e-5).sum().item()
+    assert bad == 0, (what, bad)
+
+
+def nrmerr(a, b):
+    a, b = a.float(), b.float()
+    return ((a - b).norm() / b.norm().clamp_min(1e-6)).item()
+
+
+@pytest.mark.parametrize("C,Cm,H", [(256, 64, 14), (512, 128, 7)])
+def test_ax_mode2_dy3_and_dgrad(C, Cm, H):
+    """mode 2: dy3 = k1*gate(dout) + k2*y3 + k3 staged and written by conv3's dgrad."""
+    torch.manual_seed(0)
+    lib = no._load()
+    N = 6
+    dout = _cl(torch.randn(N, C, H, H, device="cuda").to(torch.bfloat16))
+    y3 = _cl(torch.randn(N, C, H, H, device="cuda").to(torch.bfloat16))
+    mask = torch.randint(0, 256, (dout.numel() // 8,), dtype=torch.uint8, device="cuda")
+    k1, k2, k3 = (torch.randn(C, device="cuda") for _ in range(3))
+    # reference: the element pass, then the plain data gradient
+    dy_ref = torch.empty_like(y3)
+    no._chk(lib.pdt_bn_bwd_apply(no._p(dout), no._p(y3), None, None, None, no._p(k1), no._p(k2), no._p(k3),
+                                 no._p(dy_ref), None, y3.numel() // C, C, 1, no._p(mask), no._s()), "apply")
+    w = _cl(torch.randn(C, Cm, 1, 1, device="cuda") * 0.05)
+    wt = torch.empty(Cm * C, dtype=torch.bfloat16, device="cuda")
+    no._chk(lib.pdt_wt_dgrad(no._p(w), no._p(wt), C, 1, 1, Cm, 0, 0, 1, 1, 1, no._s()), "wt")
+    ref = torch.nn.functional.conv2d(dy_ref.float(), w.detach().to(torch.bfloat16).float().transpose(0, 1))
+    a = dict(Hs=H, Ws=H, Cs=C, Nimg=N, Hm=H, Wm=H, Ncol=Cm, K=C, ldb=C, ldo=Cm)
+    yb = _cl(torch.randn(N, Cm, H, H, device="cuda").to(torch.bfloat16))
+    mean, sc, sh = torch.zeros(Cm, device="cuda"), torch.ones(Cm, device="cuda"), torch.zeros(Cm, device="cuda")
+    M = N * H * H
+    ran = 0
+    for v in no.AX_VARIANTS:
+        R = lib.pdt_conv_nt_bnb_rows(M, Cm, C, v)
+        part = torch.empty(2 * R * Cm, device="cuda")
+        dy = torch.full_like(y3, float("nan"))
+        out = torch.full_like(yb, float("nan"))
+        rc = no._ax_launch(lib, dout, wt, out, v, a, bnb=(yb, mean, sc, sh, None, part, 1, 0, R),
+                           ax=(2, y3, k1, k2, k3, None, None, mask, None, dy))
+        assert rc == 0, (v, rc)
+        ran += 1
+        assert_one_rounding(dy, dy_ref, v)
+        assert nrmerr(out, ref) < 1e-2, v
+    assert ran == len(no.AX_VARIANTS)
+
+
+@pytest.mark.parametrize("affine_res", [False, True])
+def test_ax_mode1_out_mask_and_fwd(affine_res):
+    """mode 1: out = relu(y3*s + b + res) (+ the downsample BN affine on res) staged and
+    written by the next conv1, with its ReLU bit mask."""
+    torch.manual_seed(1)
+    lib = no._load()
+    N, C, Cm, H = 6, 256, 64, 14
+    y3 = _cl(torch.randn(N, C, H, H, device="cuda").to(torch.bfloat16))
+    res = _cl(torch.randn(N, C, H, H, device="cuda").to(torch.bfloat16))
+    s, b = torch.rand(C, device="cuda") + 0.5, torch.randn(C, device="cuda") * 0.1
+    rs, rb = (torch.rand(C, device="cuda") + 0.5, torch.randn(C, device="cuda") * 0.1) if affine_res else (None, None)
+    out_ref = torch.empty_like(y3)
+    mask_ref = torch.empty(y3.numel() // 8, dtype=torch.uint8, device="cuda")
+    M = N * H * H
+    if affine_res:
+        no._chk(lib.pdt_bn_apply_res_affine(no._p(y3), no._p(res), no._p(out_ref), no._p(s), no._p(b), no._p(rs),
+                                            no._p(rb), M, C, 1, no._p(mask_ref), no._s()), "apply")
+    else:
+        no._chk(lib.pdt_bn_apply(no._p(y3), no._p(res), no._p(out_ref), no._p(s), no._p(b), M, C, 1,
+                                 no._p(mask_ref), no._s()), "apply")
+    w = _cl(torch.randn(Cm, C, 1, 1, device="cuda") * 0.05)
+    wb = no.bf16_weight(w)
+    ref = torch.nn.functional.conv2d(out_ref.float(), w.to(torch.bfloat16).float())
+    a = dict(Hs=H, Ws=H, Cs=C, Nimg=N, Hm=H, Wm=H, Ncol=Cm, K=C, ldb=C, ldo=Cm)
+    for v in no.AX_VARIANTS:
+        rows = lib.pdt_conv_nt_stat_rows(M, Cm, C, v)
+        st = torch.empty(2 * rows * Cm, device="cuda")
+        out = torch.full_like(y3, float("nan"))
+        mk = torch.zeros_like(mask_ref)
+        y1 = _cl(torch.empty(N, Cm, H, H, device="cuda", dtype=torch.bfloat16))
+        rc = no._ax_launch(lib, y3, wb, y1, v, a, stats=st, ax=(1, res, s, b, None, rs, rb, None, mk, out))
+        assert rc == 0, (v, rc)
+        assert_one_rounding(out, out_ref, v)
+        flips = (mk ^ mask_ref).to(torch.int32)
+        assert int(sum(((flips >> k) & 1).sum().item() for k in range(8))) <= 4, v  # only at a rounding tie with 0
+        assert nrmerr(y1, ref) < 1e-2, v
+        ps = st.view(2, rows, Cm).sum(1)
+        assert nrmerr(ps[0], ref.sum((0, 2, 3))) < 2e-3, v
+
+
+def test_identity_bottleneck_backward_with_and_without_fold(monkeypatch):
+    from pytorch_distributed_template_amd.models.resnet import Bottleneck
+    torch.manual_seed(7)
+    blk = Bottleneck(256, 64).cuda().to(memory_format=torch.channels_last)
+    x = _cl(torch.randn(8, 256, 14, 14, device="cuda").to(torch.bfloat16))
+    g = _cl(torch.randn(8, 256, 14, 14, device="cuda").to(torch.bfloat16))
+    res = []
+    for on in ("1", "0"):
+        monkeypatch.setenv("PDT_FUSE_BN_AX", on)
+        for p in blk.parameters():
+            p.grad = None
+        xi = x.detach().clone().requires_grad_(True)
+        y = no.bottleneck(xi, blk)
+        y.backward(g)
+        res.append((y.detach().float(), xi.grad.float(), [p.grad.float().clone() for p in blk.parameters()]))
+    (y1, dx1, g1), (y0, dx0, g0) = res
+    assert torch.equal(y1, y0)
+    assert nrmerr(dx1, dx0) < 2e-3
+    for a, b in zip(g1, g0):
+        assert nrmerr(a, b) < 2e-3
