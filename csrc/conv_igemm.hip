@@ -360,8 +360,9 @@ static int conv_nt_impl(const void* src, const void* b, void* out, float* stats,
   if (ax.mode != 0) {
     // the A-staging BN apply: 1x1, stride 1, unpadded, dense rows, 32-bit element offsets
     if (nth != 1 || ntw != 1 || sh != 1 || sw != 1 || oh0 != 0 || ow0 != 0 || p.pix != Cs || Cs % 64 != 0 ||
-        bias != nullptr || aux != nullptr || act != 0 || addend != nullptr || ax.y2 == nullptr || ax.c1 == nullptr ||
-        ax.c2 == nullptr || (ax.mode == 2 && (ax.c3 == nullptr || ax.mask_in == nullptr)) ||
+        bias != nullptr || aux != nullptr || act != 0 || addend != nullptr || ax.c1 == nullptr ||
+        ax.c2 == nullptr || (ax.mode == 2 && (ax.y2 == nullptr || ax.c3 == nullptr || ax.mask_in == nullptr)) ||
+        (ax.y2 == nullptr && ax.rsc != nullptr) ||
         (long long)p.M * Cs >= (1LL << 31) || v >= NVAR)
       return -5;
     return launch_variant_ax(v, p, stream);

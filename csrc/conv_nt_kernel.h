@@ -30,10 +30,13 @@ struct BnbArgs {
 // separate element pass that writes it and a GEMM that re-reads it. The A loads read
 // `src` (and `y2`), the staging pass applies the BN, feeds the MFMAs and -- in the
 // tn == 0 workgroups, which stage every A row exactly once -- writes the result to
-// `dst` (and the ReLU bit mask), bit-identical to the element pass (csrc/bn_act.hip).
+// `dst` (and the ReLU bit mask), equal to the element pass (csrc/bn_act.hip) up to FMA
+// contraction (one bf16 rounding).
 //   mode 1 (forward, the next conv1):  A = relu(src*c1 + c2 + y2)       (src = y3, y2 = residual)
 //                                      y2 term = y2*rsc + rsh when rsc (raw downsample output)
 //                                      dst = the block output, mask_out = its ReLU bit mask
+//          (forward, conv3):           y2 = nullptr: A = relu(src*c1 + c2) (src = y2 of bn2),
+//                                      dst = the conv3 input the weight gradient reads
 //   mode 2 (backward, conv3's dgrad):  A = c1*gate(src) + c2*y2 + c3   (src = dout, y2 = y3,
 //                                      gate = mask_in bit), dst = dy3 (the wgrad operand)
 struct AXArgs {
@@ -216,7 +219,8 @@ __global__ void __launch_bounds__(NTH, PIPE ? 1 : 2) conv_nt_kernel(NTParams p) 
         }
         if constexpr (AX != 0) {
           roff[i] = ok ? (int)off : -1;  // host guarantees 32-bit element offsets
-          ry[i] = ok ? *reinterpret_cast<const u32x4*>(p.ax.y2 + off) : u32x4{0, 0, 0, 0};
+          // mode 1 without a residual (y2 == nullptr): r = 0, f + 0 == f exactly
+          ry[i] = (ok && p.ax.y2 != nullptr) ? *reinterpret_cast<const u32x4*>(p.ax.y2 + off) : u32x4{0, 0, 0, 0};
           rmk[i] = (AX == 2 && ok) ? (uint32_t)p.ax.mask_in[off >> 3] : 0u;
         }
       }

@@ -82,10 +82,10 @@ class ResNet(BaseModel):
 
     def forward(self, x):
         x = fused.conv_bn_relu_maxpool(x, self.conv1, self.bn1, 3, 2, 1)
-        x = self.layer1(x)
-        x = self.layer2(x)
-        x = self.layer3(x)
-        x = self.layer4(x)
+        # all 16 (50) bottlenecks as one chain: on the native path each block's output BN
+        # pass runs inside the next block's conv1 (ops.native_ops.bottleneck_chain); the
+        # layerN containers keep the usual state_dict names
+        x = fused.bottleneck_chain(x, [*self.layer1, *self.layer2, *self.layer3, *self.layer4])
         x = fused.global_avg_pool(x)
         return fused.linear(x, self.fc)
 

@@ -87,6 +87,19 @@ def bottleneck(x, blk):
     return conv_bn_act(out, blk.conv3, blk.bn3, residual=identity, relu=True)
 
 
+def bottleneck_chain(x, blocks):
+    """A sequence of bottleneck blocks. Native: each block's final BN(+res)+ReLU pass is
+    folded into the next block's first 1x1 GEMM (``native_ops.bottleneck_chain``)."""
+    blocks = list(blocks)
+    if _use_native(x):
+        from . import native_ops
+        x, n = native_ops.bottleneck_chain(x, blocks)
+        blocks = blocks[n:]
+    for blk in blocks:
+        x = bottleneck(x, blk)
+    return x
+
+
 def conv_bn_relu_maxpool(x, conv: nn.Conv2d, bn: nn.BatchNorm2d, kernel_size=3, stride=2, padding=1):
     """max_pool2d(relu(BN(conv(x)))) -- the ResNet stem. Native: one node whose
     max-pool applies the BN affine + ReLU on the fly (no full-resolution activation)."""

@@ -905,7 +905,7 @@ class _BNArgs:
 class _Unit:
     """Saved state of one conv->BN->act unit between forward and backward."""
     __slots__ = ("x", "w", "gamma", "y", "act", "mask", "mean", "invstd", "scale", "shift", "N", "C", "Cs", "H",
-                 "W", "Cout", "g", "relu", "has_res", "bnb_pre", "__weakref__")
+                 "W", "Cout", "g", "relu", "has_res", "bnb_pre", "pend", "__weakref__")
 
 
 def nhwc_padded_view(x, cp):
@@ -922,10 +922,15 @@ def nhwc_padded_view(x, cp):
     return torch.as_strided(x, (N, cp, H, W), (H * W * cp, 1, W * cp, cp))
 
 
-def _unit_fwd(x, w, gamma, beta, residual, conv, relu, bna: _BNArgs, apply: bool = True, res_unit=None):
+def _unit_fwd(x, w, gamma, beta, residual, conv, relu, bna: _BNArgs, apply: bool = True, res_unit=None,
+              src_pend=None, defer: bool = False):
     """conv -> BN (batch statistics from the conv epilogue) -> (+ residual) -> (ReLU).
     ``res_unit``: the residual is that unit's RAW conv output and its BN affine is applied
-    inside this unit's BN apply (``residual`` must be ``res_unit.y``)."""
+    inside this unit's BN apply (``residual`` must be ``res_unit.y``).
+    ``defer``: skip the BN(+res)+ReLU element pass; the returned output buffer is still
+    unwritten (``u.pend`` set) and the NEXT unit that reads it must be called with
+    ``src_pend=u`` -- its 1x1 GEMM computes the apply in its A staging and writes the
+    buffer (+ ReLU mask) once (``_conv1x1_fwd_ax``), or the element pass runs first."""
     lib = _load()
     st = _s()
     N, C, H, W = x.shape
@@ -942,15 +947,23 @@ def _unit_fwd(x, w, gamma, beta, residual, conv, relu, bna: _BNArgs, apply: bool
     wb = bf16_weight(w, pad_cin_to=Cs if Cs != C else None)
     f32 = dict(dtype=torch.float32, device=x.device)
     M = N * g["Ho"] * g["Wo"]
+    r = None
+    if src_pend is not None and getattr(src_pend, "pend", None) is not None:
+        assert src_pend.y.shape == x.shape and x.data_ptr() == src_pend.pend[2].data_ptr()
+        r = _conv1x1_fwd_ax(src_pend, x, wb, N, H, W, Cs, Cout, g, bna.training)
+        if r is None:  # not covered by the AX tiles: the deferred element pass, then the plain GEMM
+            _materialize(src_pend)
+        src_pend.pend = None
+    if r is None:
+        r = _conv_forward(x, wb, N, H, W, Cs, Cout, g, with_stats=bna.training)
+    y, _, part, R = r
     if bna.training:
-        y, _, part, R = _conv_forward(x, wb, N, H, W, Cs, Cout, g, with_stats=True)
         vec = torch.empty((4, Cout), **f32)
         mean, invstd, scale, shift = vec[0], vec[1], vec[2], vec[3]
         _chk(lib.pdt_bn_finalize(_p(part), R, Cout, float(M), float(bna.eps), float(bna.momentum), _p(gamma),
                                  _p(beta), _p(mean), _p(invstd), _p(scale), _p(shift), _p(bna.rm), _p(bna.rv),
                                  _p(bna.nbt), st), "bn_finalize")
     else:
-        y, _, _, _ = _conv_forward(x, wb, N, H, W, Cs, Cout, g, with_stats=False)
         invstd = torch.rsqrt(bna.rv.float() + bna.eps)
         mean = bna.rm.float().clone()
         scale = (gamma.float() * invstd).contiguous()
@@ -959,7 +972,7 @@ def _unit_fwd(x, w, gamma, beta, residual, conv, relu, bna: _BNArgs, apply: bool
     if not apply:  # the consumer applies the BN affine (+ReLU) itself (stem max-pool)
         u = _Unit()
         u.x, u.w, u.gamma, u.y = x, w, gamma, y
-        u.act, u.mask, u.bnb_pre = None, None, None
+        u.act, u.mask, u.bnb_pre, u.pend = None, None, None, None
         u.mean, u.invstd, u.scale, u.shift = mean, invstd, scale, shift
         u.N, u.C, u.Cs, u.H, u.W, u.Cout, u.g, u.relu, u.has_res = N, C, Cs, H, W, Cout, g, relu, False
         return None, u
@@ -974,12 +987,16 @@ def _unit_fwd(x, w, gamma, beta, residual, conv, relu, bna: _BNArgs, apply: bool
         else None
     if res_unit is not None:
         assert residual is res_unit.y and res_unit.Cout == Cout
+    u = _Unit()
+    u.pend = None
+    if defer and relu:
+        u.pend = (res, res_unit, out)
+    elif res_unit is not None:
         _chk(lib.pdt_bn_apply_res_affine(_p(y), _p(res), _p(out), _p(scale), _p(shift), _p(res_unit.scale),
                                          _p(res_unit.shift), M, Cout, int(relu), _p(mask), st), "bn_apply_res_affine")
     else:
         _chk(lib.pdt_bn_apply(_p(y), _p(res), _p(out), _p(scale), _p(shift), M, Cout, int(relu), _p(mask), st),
              "bn_apply")
-    u = _Unit()
     u.x, u.w, u.gamma, u.y = x, w, gamma, y
     u.act = None
     u.mask = mask
@@ -1091,15 +1108,38 @@ def _ax_launch(lib, src, b, out, v, a, stats=None, bnb=None, ax=None):
                               _s())
 
 
-def _ax_select(key, run):
+def _time_fn(fn):
+    """Best of two 3-launch HIP-event trials after one warm call (``_time_variants``' protocol), ms."""
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    fn()
+    best = float("inf")
+    for _ in range(2):
+        ev0.record()
+        for _ in range(3):
+            fn()
+        ev1.record()
+        ev1.synchronize()
+        best = min(best, ev0.elapsed_time(ev1))
+    return best
+
+
+AX_UNFUSED = -2  # tuned-table value: the element pass + the plain GEMM beat every AX tile here
+
+
+def _ax_select(key, run, run_ref=None):
     """Tile for an AX launch (tuned over the AX instantiations on first use when allowed);
-    ``run(v)`` launches variant v (with the caller's scratch outputs) and returns its code."""
+    ``run(v)`` launches variant v (with the caller's scratch outputs) and returns its code.
+    ``run_ref()``: the unfused alternative (element pass + the plain GEMM's tuned tile);
+    when it is faster the key records ``AX_UNFUSED`` and the caller takes that path (the
+    fold is a per-geometry tuning decision, not a blanket switch)."""
     table = _tuned()
     if key in table:
         return int(table[key])
     if not _tune_allowed():
         return AX_VARIANTS[3]  # 128x128, one LDS stage
     best = _time_variants(max(AX_VARIANTS) + 1, run, set(AX_VARIANTS))
+    if best >= 0 and run_ref is not None and _time_fn(run_ref) < _time_fn(lambda: run(best)):
+        best = AX_UNFUSED
     table[key] = best
     _save_tuned()
     return best
@@ -1130,8 +1170,13 @@ def _conv3_dgrad_bn_bwd(dout, u3, k1, k2, k3, dy3, u2):
         part = torch.empty(2 * R * Cin, dtype=torch.float32, device=dout.device)
         return _ax_launch(lib, dout, wt, da2, v, a, bnb=bnb(part, R), ax=ax)
 
+    def run_ref():
+        _chk(lib.pdt_bn_bwd_apply(_p(dout), _p(u3.y), None, None, None, _p(k1), _p(k2), _p(k3), _p(dy3), None, M,
+                                  Cout, 1, _p(u3.mask), _s()), "bn_bwd_apply")
+        _unit_dx(dy3, u3, bnb_unit=u2)
+
     key = "axb:" + ",".join(str(x) for x in (H, W, Cout, N, Cin))
-    v = _ax_select(key, run)
+    v = _ax_select(key, run, run_ref)
     if v < 0:
         return None
     R = lib.pdt_conv_nt_bnb_rows(M, Cin, Cout, v)
@@ -1141,6 +1186,66 @@ def _conv3_dgrad_bn_bwd(dout, u3, k1, k2, k3, dy3, u2):
         return None
     _chk(rc, "conv_nt_ax (bn3 backward apply + conv3 dgrad)")
     return da2, _BnbPartials(part, R, u2)
+
+
+def _materialize(u: _Unit):
+    """The deferred BN(+res)+ReLU element pass of unit ``u`` (see ``_unit_fwd(defer=True)``)."""
+    _apply_pending(u)
+    u.pend = None
+
+
+def _apply_pending(u: _Unit):
+    res, ru, out = u.pend
+    lib = _load()
+    M = u.y.numel() // u.Cout
+    if ru is not None:
+        _chk(lib.pdt_bn_apply_res_affine(_p(u.y), _p(res), _p(out), _p(u.scale), _p(u.shift), _p(ru.scale),
+                                         _p(ru.shift), M, u.Cout, 1, _p(u.mask), _s()), "bn_apply_res_affine")
+    else:
+        _chk(lib.pdt_bn_apply(_p(u.y), _p(res), _p(out), _p(u.scale), _p(u.shift), M, u.Cout, 1, _p(u.mask), _s()),
+             "bn_apply")
+
+
+def _conv1x1_fwd_ax(pu: _Unit, xbuf, wb, N, H, W, Cs, Cout, g, with_stats):
+    """Forward 1x1 conv whose A operand is unit ``pu``'s deferred output relu(bn(pu.y) [+ res]),
+    computed in the A staging (AX mode 1) and written to ``xbuf`` (+ pu.mask) on the way.
+    Returns ``_conv_forward``'s (y, M, part, R), or None when the geometry is not covered."""
+    res, ru, _ = pu.pend
+    M = N * H * W
+    if g["KH"] != 1 or g["KW"] != 1 or g["sh"] != 1 or g["sw"] != 1 or g["ph"] or g["pw"] or Cs != pu.Cout or \
+            Cs % 64 or Cout % 8 or M * Cs >= 2 ** 31 or not pu.relu:
+        return None
+    lib = _load()
+    y = _empty_cl(N, Cout, H, W, torch.bfloat16, xbuf.device)
+    a = dict(Hs=H, Ws=W, Cs=Cs, Nimg=N, Hm=H, Wm=W, Ncol=Cout, K=Cs, ldb=Cs, ldo=Cout)
+    ax = (1, res, pu.scale, pu.shift, None, ru.scale if ru is not None else None,
+          ru.shift if ru is not None else None, None, pu.mask, xbuf)
+
+    def stats(v, tail):
+        if not with_stats:
+            return None, 0
+        R = lib.pdt_conv_nt_stat_rows(M, Cout, Cs, v)
+        ws = lib.pdt_rows_reduce_workspace(R, Cout) if tail else 0
+        return torch.empty(2 * R * Cout + ws, dtype=torch.float32, device=xbuf.device), R
+
+    def run(v):
+        return _ax_launch(lib, pu.y, wb, y, v, a, stats=stats(v, False)[0], ax=ax)
+
+    def run_ref():
+        _apply_pending(pu)
+        _conv_forward(xbuf, wb, N, H, W, Cs, Cout, g, with_stats=with_stats)
+
+    key = "axf:" + ",".join(str(x) for x in (H, W, Cs, N, Cout, int(res is not None), int(ru is not None),
+                                              int(with_stats)))
+    v = _ax_select(key, run, run_ref)
+    if v < 0:
+        return None
+    part, R = stats(v, True)
+    rc = _ax_launch(lib, pu.y, wb, y, v, a, stats=part, ax=ax)
+    if rc == NOT_APPLICABLE:
+        return None
+    _chk(rc, "conv_nt_ax (deferred BN apply + 1x1 conv)")
+    return y, M, part, R
 
 
 def _unit_dw(dy, u: _Unit):
@@ -1276,19 +1381,25 @@ class _SideWgrad:
 
 class _Bottleneck(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, blk, has_ds, *params):
+    def forward(ctx, x, blk, has_ds, xpend, defer, holder, *params):
+        # xpend: the previous block's unit whose output x is still unwritten (its bn3 apply is
+        # computed in conv1's A staging, which writes x); conv1 therefore runs first
+        a1, u1 = _unit_fwd(x, blk.conv1.weight, blk.bn1.weight, blk.bn1.bias, None, blk.conv1, True,
+                           _BNArgs(blk.bn1), src_pend=xpend)
         if has_ds:  # raw downsample conv output; its BN affine is applied inside bn3's apply
             _, ud = _unit_fwd(x, blk.downsample[0].weight, blk.downsample[1].weight, blk.downsample[1].bias, None,
                               blk.downsample[0], False, _BNArgs(blk.downsample[1]), apply=False)
             idn = ud.y
         else:
             idn, ud = _cl(x.to(torch.bfloat16)), None
-        a1, u1 = _unit_fwd(x, blk.conv1.weight, blk.bn1.weight, blk.bn1.bias, None, blk.conv1, True,
-                           _BNArgs(blk.bn1))
+        fold = _ax_enabled()
+        # bn2's apply+ReLU inside conv3's A staging (a2 written once, for conv3's weight gradient)
         a2, u2 = _unit_fwd(a1, blk.conv2.weight, blk.bn2.weight, blk.bn2.bias, None, blk.conv2, True,
-                           _BNArgs(blk.bn2))
+                           _BNArgs(blk.bn2), defer=fold)
         out, u3 = _unit_fwd(a2, blk.conv3.weight, blk.bn3.weight, blk.bn3.bias, idn, blk.conv3, True,
-                            _BNArgs(blk.bn3), res_unit=ud)
+                            _BNArgs(blk.bn3), res_unit=ud, src_pend=u2, defer=defer and fold)
+        if holder is not None:
+            holder[0] = u3 if u3.pend is not None else None
         ctx.units = (u1, u2, u3, ud)
         ctx.has_ds = has_ds
         prev = _producer_of(x) if _bnb_enabled() else None
@@ -1367,21 +1478,54 @@ class _Bottleneck(torch.autograd.Function):
         dw1 = wg.dw(dy1, u1)
         wg.join()
         del ctx.units
-        return (dx, None, None, dw1, dg1, db1, dw2, dg2, db2, dw3, dg3, db3) + grads_ds
+        return (dx, None, None, None, None, None, dw1, dg1, db1, dw2, dg2, db2, dw3, dg3, db3) + grads_ds
+
+
+def _bottleneck_params(blk):
+    params = [blk.conv1.weight, blk.bn1.weight, blk.bn1.bias, blk.conv2.weight, blk.bn2.weight, blk.bn2.bias,
+              blk.conv3.weight, blk.bn3.weight, blk.bn3.bias]
+    if blk.downsample is not None:
+        params += [blk.downsample[0].weight, blk.downsample[1].weight, blk.downsample[1].bias]
+    return params
+
+
+def _bottleneck_ok(x, blk):
+    convs = [blk.conv1, blk.conv2, blk.conv3] + ([blk.downsample[0]] if blk.downsample is not None else [])
+    return x.dtype == torch.bfloat16 and all(supports_conv(x, c) for c in convs) and x.shape[1] % 8 == 0
 
 
 def bottleneck(x, blk):
-    convs = [blk.conv1, blk.conv2, blk.conv3] + ([blk.downsample[0]] if blk.downsample is not None else [])
-    if x.dtype != torch.bfloat16 or not all(supports_conv(x, c) for c in convs) or x.shape[1] % 8:
+    if not _bottleneck_ok(x, blk):
         fallback("bottleneck", f"input {tuple(x.shape)} {x.dtype} (needs bf16, channels % 8 == 0, "
                                "plain convs)")
         return None
-    has_ds = blk.downsample is not None
-    params = [blk.conv1.weight, blk.bn1.weight, blk.bn1.bias, blk.conv2.weight, blk.bn2.weight, blk.bn2.bias,
-              blk.conv3.weight, blk.bn3.weight, blk.bn3.bias]
-    if has_ds:
-        params += [blk.downsample[0].weight, blk.downsample[1].weight, blk.downsample[1].bias]
-    return _Bottleneck.apply(x, blk, has_ds, *params)
+    return _Bottleneck.apply(x, blk, blk.downsample is not None, None, False, None, *_bottleneck_params(blk))
+
+
+def bottleneck_chain(x, blocks):
+    """A sequence of bottleneck blocks, one autograd node per block (DDP's per-parameter
+    gradient hooks keep firing block by block), with each block's final BN(+residual)+ReLU
+    element pass deferred into the NEXT block's conv1: that 1x1 GEMM computes the block
+    output in its A staging and writes it (+ ReLU bit mask) once for the shortcut and the
+    backward -- one full read of every block output per step saved. The deferred output is
+    only ever read by the next block of this chain, which runs immediately after; the last
+    block's output is materialised normally. Returns ``(y, n)``: ``blocks[:n]`` ran here
+    (n < len(blocks) when block n is not covered -- the caller runs the rest)."""
+    blocks = list(blocks)
+    pend = None
+    for i, blk in enumerate(blocks):
+        if not _bottleneck_ok(x, blk):
+            assert pend is None
+            return x, i
+        holder = [None]
+        defer = i + 1 < len(blocks)
+        x = _Bottleneck.apply(x, blk, blk.downsample is not None, pend, defer, holder, *_bottleneck_params(blk))
+        pend = holder[0]
+        if pend is not None and not _bottleneck_ok(x, blocks[i + 1]):
+            _materialize(pend)
+            pend = None
+    assert pend is None
+    return x, len(blocks)
 
 
 # =============================================================================

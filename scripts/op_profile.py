@@ -29,7 +29,12 @@ def main():
     ap.add_argument("--top", type=int, default=70)
     ap.add_argument("--cprofile", action="store_true",
                     help="instead: host-side cProfile of --steps steps (where the Python issue time goes)")
+    ap.add_argument("--set", action="append", default=[], metavar="K=V",
+                    help="environment switch for this run (e.g. PDT_FUSE_BN_AX=0), read at call time")
     a = ap.parse_args()
+    for kv in a.set:
+        k, v = kv.split("=", 1)
+        os.environ[k] = v
     os.environ["PDT_OP_TIMING"] = "0" if a.cprofile else "1"  # read at the library's first load
     fused.set_backend("native")
     dev = torch.device("cuda", 0)
