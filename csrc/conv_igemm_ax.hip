@@ -3,7 +3,9 @@
 // of the previous ResNet block applied by the next block's conv1 (plain epilogue, BN
 // statistics of conv1's output); mode 2 = the bn3 backward apply applied by conv3's
 // data-gradient GEMM (with the fused bn2 BatchNorm-backward epilogue). Register-staged
-// tiles only; a separate translation unit like conv_igemm_bnb.hip.
+// tiles apply it while staging; LDS-DMA tiles (20..28; not 21, whose BN-backward
+// instantiation spills) rewrite the landed A tile in LDS.
+// A separate translation unit like conv_igemm_bnb.hip.
 #include "conv_nt_kernel.h"
 
 namespace pdt_nt {
@@ -22,6 +24,11 @@ static int launch_ax(int v, const NTParams& p, hipStream_t st) {
     case 15: return launch<128, 128, 1, true, true, false, 256, 2, 0, 0, BNB, AX>(p, st);
     case 16: return launch<256, 64, 1, true, true, false, 256, 2, 0, 0, BNB, AX>(p, st);
     case 18: return launch<128, 64, 1, true, true, false, 256, 2, 0, 0, BNB, AX>(p, st);
+    case 20: return launch<128, 128, 2, true, false, true, 256, 2, 0, 0, BNB, AX>(p, st);
+    case 23: return launch<128, 64, 2, true, false, true, 256, 2, 0, 0, BNB, AX>(p, st);
+    case 25: return launch<128, 128, 1, true, false, true, 256, 2, 0, 0, BNB, AX>(p, st);
+    case 26: return launch<256, 64, 1, true, false, true, 256, 2, 0, 0, BNB, AX>(p, st);
+    case 28: return launch<128, 64, 1, true, false, true, 256, 2, 0, 0, BNB, AX>(p, st);
   }
   return -5;  // NOT_APPLICABLE: no AX instantiation of this tile
 }

@@ -127,7 +127,7 @@ static __device__ __attribute__((aligned(64))) u32x4 pdt_zero_chunk[4];
 template <int BM, int BN, int NSTAGE, bool CS64, bool DIRECT, bool GLDS, int NTH = 256, int WM = 2, int F8 = 0,
           int PIPE = 0, bool BNB = false, int AX = 0>
 __global__ void __launch_bounds__(NTH, PIPE ? 1 : 2) conv_nt_kernel(NTParams p) {
-  static_assert(AX == 0 || (!GLDS && !PIPE && F8 == 0 && CS64), "the A-staging BN apply needs register staging");
+  static_assert(AX == 0 || (!PIPE && F8 == 0 && CS64), "the A-staging BN apply: bf16, 64-channel chunks, no ring");
   constexpr int WN = NTH / 64 / WM;       // waves along N
   constexpr int MI = BM / (WM * 16);      // 16-row MFMA tiles per wave
   constexpr int NI = BN / (WN * 16);
@@ -199,6 +199,31 @@ __global__ void __launch_bounds__(NTH, PIPE ? 1 : 2) conv_nt_kernel(NTParams p) 
   float cf1[AX ? 8 : 1], cf2[AX ? 8 : 1], cf3[AX == 2 ? 8 : 1], cfs[AX == 1 ? 8 : 1], cfh[AX == 1 ? 8 : 1];
   const bool ax_write = AX != 0 && p.ax.dst != nullptr && tn == 0;
 
+  // AX: this thread's 8 channels' BN coefficients (channel c0..c0+7 of the k-tile)
+  auto ax_coef = [&](int c0) __attribute__((always_inline)) {
+    if constexpr (AX != 0) {
+#pragma unroll
+      for (int e = 0; e < 8; e += 4) {
+        const f32x4 a = *reinterpret_cast<const f32x4*>(p.ax.c1 + c0 + e);
+        const f32x4 b = *reinterpret_cast<const f32x4*>(p.ax.c2 + c0 + e);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) { cf1[e + q] = a[q]; cf2[e + q] = b[q]; }
+        if constexpr (AX == 2) {
+          const f32x4 c = *reinterpret_cast<const f32x4*>(p.ax.c3 + c0 + e);
+#pragma unroll
+          for (int q = 0; q < 4; ++q) cf3[e + q] = c[q];
+        }
+        if constexpr (AX == 1) {
+          const bool raff = p.ax.rsc != nullptr;
+          const f32x4 c = raff ? *reinterpret_cast<const f32x4*>(p.ax.rsc + c0 + e) : f32x4{1.f, 1.f, 1.f, 1.f};
+          const f32x4 d = raff ? *reinterpret_cast<const f32x4*>(p.ax.rsh + c0 + e) : f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+          for (int q = 0; q < 4; ++q) { cfs[e + q] = c[q]; cfh[e + q] = d[q]; }
+        }
+      }
+    }
+  };
+
   auto load_tile = [&](int kt) {
     const int k0 = kt * BK;
     if (CS64) {
@@ -224,27 +249,7 @@ __global__ void __launch_bounds__(NTH, PIPE ? 1 : 2) conv_nt_kernel(NTParams p) 
           rmk[i] = (AX == 2 && ok) ? (uint32_t)p.ax.mask_in[off >> 3] : 0u;
         }
       }
-      if constexpr (AX != 0) {
-#pragma unroll
-        for (int e = 0; e < 8; e += 4) {
-          const f32x4 a = *reinterpret_cast<const f32x4*>(p.ax.c1 + c0 + e);
-          const f32x4 b = *reinterpret_cast<const f32x4*>(p.ax.c2 + c0 + e);
-#pragma unroll
-          for (int q = 0; q < 4; ++q) { cf1[e + q] = a[q]; cf2[e + q] = b[q]; }
-          if constexpr (AX == 2) {
-            const f32x4 c = *reinterpret_cast<const f32x4*>(p.ax.c3 + c0 + e);
-#pragma unroll
-            for (int q = 0; q < 4; ++q) cf3[e + q] = c[q];
-          }
-          if constexpr (AX == 1) {
-            const bool raff = p.ax.rsc != nullptr;
-            const f32x4 c = raff ? *reinterpret_cast<const f32x4*>(p.ax.rsc + c0 + e) : f32x4{1.f, 1.f, 1.f, 1.f};
-            const f32x4 d = raff ? *reinterpret_cast<const f32x4*>(p.ax.rsh + c0 + e) : f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-            for (int q = 0; q < 4; ++q) { cfs[e + q] = c[q]; cfh[e + q] = d[q]; }
-          }
-        }
-      }
+      if constexpr (AX != 0) ax_coef(c0);
     } else {
       const int kc = k0 / 8 + ca;  // global 8-channel chunk index
       const bool kin = kc * 8 < p.K;
@@ -333,6 +338,40 @@ __global__ void __launch_bounds__(NTH, PIPE ? 1 : 2) conv_nt_kernel(NTParams p) 
     for (int j = 0; j < LB; ++j) {
       int r = (tid >> 3) + RS * j;
       *reinterpret_cast<u32x4*>(sb + r * 128 + swz(r, ca) * 16) = rb[j];
+    }
+  };
+
+  // GLDS + AX: the A tile lands in LDS untouched; the thread that DMA'd a chunk (row r,
+  // physical chunk ca = logical chunk swz(r, ca) -- the same logical chunk for all its
+  // rows, RS being a multiple of 16) fetches that chunk's second operand / mask /
+  // coefficients into registers alongside the DMA (ax_fetch), then, once the tile is in
+  // LDS, rewrites the chunk in place with the applied values (ax_lds) before the MFMAs
+  // read it. 1x1 stride-1 unpadded geometry (host-checked): the k-tile's tap is 0.
+  auto ax_fetch = [&](int kt) __attribute__((always_inline)) {
+    if constexpr (AX != 0 && GLDS) {
+      static_assert(RS % 16 == 0, "one logical chunk per thread");
+      const int c0 = kt * BK + swz(tid >> 3, ca) * 8;
+#pragma unroll
+      for (int i = 0; i < LA; ++i) {
+        const bool ok = a_ok[i];
+        const size_t off = (size_t)(a_base[i] + a_ih[i] * p.Ws + a_iw[i]) * p.pix + c0;
+        roff[i] = ok ? (int)off : -1;
+        ry[i] = (ok && p.ax.y2 != nullptr) ? *reinterpret_cast<const u32x4*>(p.ax.y2 + off) : u32x4{0, 0, 0, 0};
+        rmk[i] = (AX == 2 && ok) ? (uint32_t)p.ax.mask_in[off >> 3] : 0u;
+      }
+      ax_coef(c0);
+    }
+  };
+  auto ax_lds = [&](int buf) __attribute__((always_inline)) {
+    if constexpr (AX != 0 && GLDS) {
+      char* sa = smem + buf * STAGE;
+#pragma unroll
+      for (int i = 0; i < LA; ++i) {
+        u32x4* q = reinterpret_cast<u32x4*>(sa + ((tid >> 3) + RS * i) * 128 + ca * 16);
+        ra[i] = *q;
+        ax_apply(i);
+        *q = ra[i];
+      }
     }
   };
 
@@ -596,8 +635,12 @@ __global__ void __launch_bounds__(NTH, PIPE ? 1 : 2) conv_nt_kernel(NTParams p) 
     if (!DIRECT) __syncthreads();  // before the epilogue reuses LDS
   } else {
   if (GLDS) {
-    if (nk > 0) glds_tile(0, 0);
+    if (nk > 0) {
+      glds_tile(0, 0);
+      ax_fetch(0);
+    }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (nk > 0) ax_lds(0);  // a lane's DMA fills its own LDS slot: no barrier before the rewrite
   } else if (nk > 0) {
     load_tile(0);
     store_tile(0);
@@ -607,7 +650,10 @@ __global__ void __launch_bounds__(NTH, PIPE ? 1 : 2) conv_nt_kernel(NTParams p) 
   for (int kt = 0; kt < nk; ++kt) {
     const int cur = NSTAGE == 2 ? (kt & 1) : 0;
     if (GLDS) {
-      if (NSTAGE == 2 && kt + 1 < nk) glds_tile(kt + 1, cur ^ 1);
+      if (NSTAGE == 2 && kt + 1 < nk) {
+        glds_tile(kt + 1, cur ^ 1);
+        ax_fetch(kt + 1);
+      }
     } else if (kt + 1 < nk) {
       load_tile(kt + 1);
     }
@@ -616,11 +662,14 @@ __global__ void __launch_bounds__(NTH, PIPE ? 1 : 2) conv_nt_kernel(NTParams p) 
     if (GLDS) {
       if (NSTAGE == 2) {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // my DMA into the other buffer landed
+        if (kt + 1 < nk) ax_lds(cur ^ 1);                  // (AX) rewrite my chunks of it in place
         __syncthreads();                                   // ... and everyone's; buffer cur is free
       } else if (kt + 1 < nk) {
         __syncthreads();
         glds_tile(kt + 1, 0);
+        ax_fetch(kt + 1);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        ax_lds(0);
         __syncthreads();
       }
     } else if (NSTAGE == 2) {

@@ -1089,7 +1089,7 @@ def _unit_dx(dy, u: _Unit, addend=None, addend_mask=None, bnb_unit=None, bnb_mas
 # the BN'd tensor is produced by the GEMM that consumes it (and written once for its
 # other consumers) instead of by an element pass + a re-read. PDT_FUSE_BN_AX=0 disables.
 # -----------------------------------------------------------------------------
-AX_VARIANTS = (0, 1, 3, 5, 6, 8, 10, 13, 15, 16, 18)  # csrc/conv_igemm_ax.hip
+AX_VARIANTS = (0, 1, 3, 5, 6, 8, 10, 13, 15, 16, 18, 20, 23, 25, 26, 28)  # csrc/conv_igemm_ax.hip
 
 
 def _ax_enabled() -> bool:
