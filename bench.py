@@ -196,6 +196,10 @@ def heartbeat(rank, state, every_s=30.0):
 
 def main():
     args = parse()
+    if args.graph:
+        # DDP inside a captured graph: the RCCL watchdog must not query the captured work
+        # (PyTorch's whole-network-capture recipe), set before the process group exists
+        os.environ.setdefault("TORCH_NCCL_ASYNC_ERROR_HANDLING", "0")
     rc = launch_ranks(args)
     if rc is not None:
         sys.exit(rc)
@@ -274,8 +278,15 @@ def main():
     # N ranks: rank 0 tunes the kernel variants once and broadcasts them (no per-rank timing)
     pretune_for_ddp(model, _pretune_step)
     ar = allreduce_probe(model, device, world)
-    model = wrap_ddp(model, device, bucket_cap_mb=args.bucket_mb, broadcast_buffers=False,
-                     gradient_as_bucket_view=True, comm_hook=args.comm_hook)
+    side = torch.cuda.Stream() if args.graph else None
+    if side is not None:  # graph capture of DDP: the reducer is built on the capture side stream
+        side.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(side):
+            model = wrap_ddp(model, device, bucket_cap_mb=args.bucket_mb, broadcast_buffers=False,
+                             gradient_as_bucket_view=True, comm_hook=args.comm_hook)
+    else:
+        model = wrap_ddp(model, device, bucket_cap_mb=args.bucket_mb, broadcast_buffers=False,
+                         gradient_as_bucket_view=True, comm_hook=args.comm_hook)
 
     def step(i):
         x, y = next_batch(i)
@@ -307,10 +318,11 @@ def main():
             opt.step()
             return loss
 
-        side = torch.cuda.Stream()
         side.wait_stream(torch.cuda.current_stream())
         with torch.cuda.stream(side):
-            for i in range(max(3, args.warmup)):
+            # >= 11 eager iterations: DDP samples runtime stats (host-synchronising) on
+            # iterations 1..10, which must all precede the capture
+            for i in range(max(11, args.warmup)):
                 xb, yb = next_batch(i)
                 sx.copy_(xb)
                 sy.copy_(yb)

@@ -193,8 +193,14 @@ def require():
     _load()
 
 
+_raw_stream = torch._C._cuda_getCurrentRawStream
+_cur_device = torch._C._cuda_getDevice
+
+
 def _s():
-    return torch.cuda.current_stream().cuda_stream
+    """The current HIP stream handle (the raw accessor: ~20x cheaper than
+    ``torch.cuda.current_stream().cuda_stream``, which builds a Stream object per call)."""
+    return _raw_stream(_cur_device())
 
 
 def _p(t):
@@ -503,15 +509,22 @@ def _check_nt(src, b, out, a):
     assert a["Nimg"] * a["Hs"] * a["Ws"] * Cs < 2 ** 31 and a["Nimg"] * a["Ho"] * a["Wo"] < 2 ** 31
 
 
+_NT_KEYS: dict = {}  # geometry tuple -> tuned-table key string (built once per geometry)
+
+
 def select_nt_variant(src, b, out, *, with_stats=False, bias=None, act=0, aux=None, addend=None, **a):
     """Variant id for this geometry and epilogue (tuning it on first use when allowed)."""
     M = a["Nimg"] * a["Hm"] * a["Wm"]
-    key = "nt5:" + ",".join(str(a[k]) for k in ("Hs", "Ws", "Cs", "Nimg", "Hm", "Wm", "Ncol", "K", "sh", "sw",
-                                                 "nth", "ntw", "osh")) + f",{int(with_stats)},{int(bias is not None)}"
-    if a.get("pix"):
-        key += f",p{a['pix']}"
-    if act:  # epilogue work changes the best tile (and the streaming 1x1 kernels take no activation)
-        key += f",a{int(act)}"
+    geom = (a["Hs"], a["Ws"], a["Cs"], a["Nimg"], a["Hm"], a["Wm"], a["Ncol"], a["K"], a["sh"], a["sw"], a["nth"],
+            a["ntw"], a["osh"], int(with_stats), int(bias is not None), a.get("pix", 0), int(act))
+    key = _NT_KEYS.get(geom)
+    if key is None:
+        key = "nt5:" + ",".join(str(x) for x in geom[:15])
+        if a.get("pix"):
+            key += f",p{a['pix']}"
+        if act:  # epilogue work changes the best tile (and the streaming 1x1 kernels take no activation)
+            key += f",a{int(act)}"
+        _NT_KEYS[geom] = key
     table = _tuned()
     if key in table:
         return int(table[key])
@@ -585,6 +598,9 @@ def _wgrad_launch(lib, dy, x, out, v, scale, accumulate, a, bias_out=None):
                               int(a.get("pix", 0)), _p(bias_out), _s())
 
 
+_WG_KEYS: dict = {}
+
+
 def conv_wgrad(dy, x, out, *, scale=1.0, accumulate=False, variant=None, bias_out=None, **a):
     """dW[co, tap*C + c] = sum_m dY[m, co] X_gather[m, (tap, c)] (see csrc/conv_wgrad.hip).
     ``bias_out`` (fp32 [Mo]): also sum_m dY[m, co] -- the nn.Linear bias gradient -- from the
@@ -601,9 +617,13 @@ def conv_wgrad(dy, x, out, *, scale=1.0, accumulate=False, variant=None, bias_ou
         assert bias_out.dtype == torch.float32 and bias_out.numel() >= Mo and bias_out.is_contiguous()
     lib = _load()
     if variant is None:
-        key = "wg2:" + ",".join(str(a[k]) for k in ("M", "Mo", "No", "Hs", "Ws", "C", "Hm", "Wm", "sh", "ntw"))
-        if a.get("pix"):
-            key += f",p{a['pix']}"
+        gt = (a["M"], a["Mo"], a["No"], a["Hs"], a["Ws"], a["C"], a["Hm"], a["Wm"], a["sh"], a["ntw"], a.get("pix", 0))
+        key = _WG_KEYS.get(gt)
+        if key is None:
+            key = "wg2:" + ",".join(str(x) for x in gt[:10])
+            if a.get("pix"):
+                key += f",p{a['pix']}"
+            _WG_KEYS[gt] = key
         table = _tuned()
         if key in table:
             variant = int(table[key])
@@ -848,12 +868,18 @@ def _conv_dgrad(dy, w32, N, H, W, Cin, Cout, g, addend=None, addend_mask=None, b
     return dx, _BnbPartials(part, R, u)
 
 
+_NTB_KEYS: dict = {}
+
+
 def _select_bnb_variant(launch, a, has_addend, has_mask, device):
     """Variant for a data gradient with the fused BN-backward epilogue: its own
     tuned-table key (the epilogue's extra loads / registers shift the best tile)."""
-    geom = ",".join(str(a[k]) for k in ("Hs", "Ws", "Cs", "Nimg", "Hm", "Wm", "Ncol", "K", "sh", "sw", "nth", "ntw",
-                                        "osh"))
-    key = f"ntb2:{geom},{int(has_addend)},{int(has_mask)}"
+    gt = (a["Hs"], a["Ws"], a["Cs"], a["Nimg"], a["Hm"], a["Wm"], a["Ncol"], a["K"], a["sh"], a["sw"], a["nth"],
+          a["ntw"], a["osh"], int(has_addend), int(has_mask))
+    key = _NTB_KEYS.get(gt)
+    if key is None:
+        key = _NTB_KEYS[gt] = "ntb2:" + ",".join(str(x) for x in gt)
+    geom = key[5:].rsplit(",", 2)[0]
     table = _tuned()
     if key in table:
         return int(table[key])

@@ -62,6 +62,19 @@ def main():
         import pstats
         import time
         pr = cProfile.Profile()
+        # the autograd engine runs CUDA backward functions on its own device thread, which the
+        # main thread's profiler does not see: every native backward enables a second
+        # profiler on that thread for its own duration
+        pb = cProfile.Profile()
+        for cls in vars(native_ops).values():
+            if isinstance(cls, type) and issubclass(cls, torch.autograd.Function) and "backward" in cls.__dict__:
+                def wrapped(ctx, *g, _orig=cls.__dict__["backward"].__func__):
+                    pb.enable()
+                    try:
+                        return _orig(ctx, *g)
+                    finally:
+                        pb.disable()
+                cls.backward = staticmethod(wrapped)
         t0 = time.perf_counter()
         pr.enable()
         for i in range(a.steps):
@@ -71,7 +84,10 @@ def main():
         torch.cuda.synchronize()
         t2 = time.perf_counter()
         print(f"host issue {1e3 * (t1 - t0) / a.steps:.1f} ms/step (under cProfile), drain {1e3 * (t2 - t1):.1f} ms")
-        pstats.Stats(pr).sort_stats("tottime").print_stats(45)
+        print("==== main thread (forward, optimizer)")
+        pstats.Stats(pr).sort_stats("tottime").print_stats(40)
+        print("==== autograd device thread (native backward functions)")
+        pstats.Stats(pb).sort_stats("tottime").print_stats(40)
         return
     lib.records.clear()
     lib.enabled = True
