@@ -1,0 +1,374 @@
+// Fused fp8 attention backward for ViT (head dim 64, T <= 256): ONE kernel computes dQ,
+// dK and dV of a (batch, head) -- the bf16 path (csrc/attention.hip) runs two kernels that
+// each re-stage the head and recompute S / dP. Every GEMM runs on
+// mfma_scale_f32_32x32x64_f8f6f4 (OCP e4m3 operands, K = 64 per instruction, 2x the bf16
+// MFMA rate) with per-lane E8M0 block scales:
+//
+//   S    = Q K^T    A = Q rows, B = K rows          (per-head pow2 scales, K = head dim)
+//   dP   = dO V^T   A = dO rows, B = V rows
+//   P    = exp2(c S - lse),  dS = P (dP - delta)    fp32, in the S accumulator registers
+//   dV^T = dO^T P   A = dO^T (ds_read_b64_tr_b8 from the dO rows), B = P (registers)
+//   dK^T = Q^T dS   A = Q^T  (tr8 from the Q rows),                 B = dS (registers)
+//   dQ^T = K^T dS^T A = K^T  (tr8 from the K rows),                 B = dS^T (LDS image)
+//
+// Operand K layout of the 32x32x64 f8 MFMA (probe: scripts/probes/mfma_scale_probe.hip):
+// byte b of lane (row, half hh) is k = 16 hh + b for b < 16 and k = 32 + 16 hh + (b - 16)
+// otherwise, and lane (row, hh)'s E8M0 scale covers the k block [32 hh, 32 hh + 32) -- i.e.
+// the first 16 bytes of BOTH halves form scale block 0.
+// Phase 1: wave w owns key tile w (32 keys) and walks the query tiles in pairs. An S / dP
+// accumulator holds 16 queries x 1 key per lane; packed to fp8 as they are (tile 2qp in
+// bytes 0..15, tile 2qp + 1 in bytes 16..31) they ARE the dV / dK B operand with scale
+// block hh = query tile 2qp + hh, in the query order k -> 64 qp + 32 (k >> 5) + pi(k & 31),
+// pi(p) = 8 ((p & 15) >> 2) + 4 (p >> 4) + (p & 3). The A operands (dO^T, Q^T) are read in
+// that order: each tr8 read addresses its 8 rows through it.
+// dS is also written, fp8 with one power-of-two scale per 32 x 32 tile, to a [key][query]
+// LDS image. Phase 2: dQ^T = K^T dS^T from that image (tr8 reads, natural key order), the
+// tile scales as the per-lane B block scales.
+//
+// Scales: Q, K, V, dO get per-head power-of-two scales at staging (exact dequantisation
+// through the E8M0 operands); P uses the fixed 2^8 (P <= 1); dS a per-tile 2^e. All
+// accumulation is fp32; dQ / dK / dV are written bf16 into the qkv-layout gradient as the
+// bf16 kernels do. lse is the forward's (log2 domain), delta = rowsum(dO * O) is computed
+// here from the bf16 O and dO.
+#include "pdt_common.h"
+
+namespace {
+
+constexpr int D = 64;
+
+typedef int i32x8 __attribute__((ext_vector_type(8)));
+typedef int i32x2 __attribute__((ext_vector_type(2)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+// fp8 row image [rows][64 B]: 16-B chunk c of row r at chunk c ^ ((r >> 2) & 3)
+__device__ __forceinline__ int k8_off(int row, int chunk) { return row * 64 + ((chunk ^ ((row >> 2) & 3)) << 4); }
+
+// largest e with amax * 2^e <= 448 (0 for an all-zero block)
+__device__ __forceinline__ int pow2_exp(float amax) {
+  if (!(amax > 0.f)) return 0;
+  const int e = (int)floorf(__log2f(448.f / amax));
+  return max(min(e, 100), -100);
+}
+
+__device__ __forceinline__ uint32_t e4m3x4(float a, float b, float c, float d) { return pdt_cvt4_f8<0>(a, b, c, d); }
+
+// the 32-byte A / B fragment of a row image: row `row`, bytes 32 hh .. 32 hh + 31
+__device__ __forceinline__ i32x8 row_frag(const char* img, int row, int hh) {
+  const u32x4 a = *reinterpret_cast<const u32x4*>(img + k8_off(row, 2 * hh));
+  const u32x4 b = *reinterpret_cast<const u32x4*>(img + k8_off(row, 2 * hh + 1));
+  return i32x8{(int)a[0], (int)a[1], (int)a[2], (int)a[3], (int)b[0], (int)b[1], (int)b[2], (int)b[3]};
+}
+
+__device__ __forceinline__ i32x2 tr8(const char* a) {
+  return __builtin_amdgcn_ds_read_tr8_b64_v2i32(
+      (i32x2 __attribute__((address_space(3)))*)((__attribute__((address_space(3))) char*)(uintptr_t)(uint32_t)(
+          uintptr_t)a));
+}
+
+// the query order of a packed P / dS accumulator within one 32-query tile (see the header)
+__device__ __forceinline__ int pi_q(int p) { return 8 * ((p & 15) >> 2) + 4 * (p >> 4) + (p & 3); }
+
+// the image row holding MFMA k of lane half hh's 4 tr8 reads: read r, row jj of the read
+// (bytes 8 r + jj): k block r >> 1, position 16 hh + 8 (r & 1) + jj within it
+template <bool PI>
+__device__ __forceinline__ int kb_row(int r, int jj, int hh) {
+  const int pos = 16 * hh + 8 * (r & 1) + jj;
+  return 32 * (r >> 1) + (PI ? pi_q(pos) : pos);
+}
+
+// Transposed 32x32x64 operand from a row image: lane (16-lane group g, j) gets column
+// 16 (g & 1) + j of the 16-byte column block `chunk`, for the 64 k rows row0 + kb_row(..)
+// (4 tr8 reads of 8 rows; lane pair j >> 1 addresses one row, byte half j & 1).
+template <bool PI>
+__device__ __forceinline__ i32x8 tr_frag(const char* img, int row0, int chunk, int j, int hh) {
+  i32x8 out;
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int row = row0 + kb_row<PI>(r, j >> 1, hh);
+    const i32x2 v = tr8(img + k8_off(row, chunk) + 8 * (j & 1));
+    out[2 * r] = v[0];
+    out[2 * r + 1] = v[1];
+  }
+  return out;
+}
+
+__device__ __forceinline__ f32x16 mfma8(const i32x8& a, const i32x8& b, const f32x16& c, int sa, int sb) {
+  return __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(a, b, c, 0, 0, 0, sa, 0, sb);
+}
+
+struct AttnBwdF8Params {
+  const u16* qkv;    // [B, T, 3, H, 64] bf16
+  const u16* out;    // forward output O [B, T, H*64]
+  const u16* dout;   // [B, T, H*64]
+  const float* lse;  // [B*H, T] (log2 domain)
+  u16* dqkv;         // [B, T, 3, H, 64]
+  int B, T, H;
+  long ld, ldo;
+  float c, scale;
+  float* dbg;  // optional (tests): dS [B*H][ROWS][ROWS] fp32 as phase 1 computes it
+};
+
+// NQP query-tile pairs: images of ROWS = 64 NQP rows (zero beyond T); 8 waves
+template <int NQP>
+__global__ void __launch_bounds__(512) attn_bwd_f8_kernel(AttnBwdF8Params p) {
+  constexpr int NT2 = 2 * NQP;  // 32-row tiles (queries and keys)
+  constexpr int ROWS = 32 * NT2;
+  constexpr int IMG = ROWS * 64;
+  constexpr int DSR = ROWS + 16;  // dS^T image row stride (bytes): 4 banks apart per row
+  __shared__ __attribute__((aligned(16))) char smem[4 * IMG + ROWS * DSR];
+  __shared__ float nlse_s[ROWS], dl_s[ROWS];
+  __shared__ int tsc[NT2 * NT2];  // E8M0 dequant of each dS tile [q tile][key tile]
+  __shared__ float red[8][4];
+  char* Qi = smem;
+  char* Ki = smem + IMG;
+  char* Vi = smem + 2 * IMG;
+  char* Oi = smem + 3 * IMG;  // dO
+  char* dSt = smem + 4 * IMG;
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int col = lane & 31, hh = lane >> 5, g = lane >> 4, j = lane & 15;
+  const int bh = blockIdx.x, b = bh / p.H, h = bh % p.H;
+  const u16* Qg = p.qkv + (long)b * p.T * p.ld + h * D;
+  const u16* Kg = Qg + p.H * D;
+  const u16* Vg = Qg + 2 * p.H * D;
+  const u16* dOg = p.dout + (long)b * p.T * p.ldo + h * D;
+  const u16* Og = p.out + (long)b * p.T * p.ldo + h * D;
+
+  // ---------------------------------------------------------------- staging
+  // chunk q = tid + 512 it: row q >> 3, 16-B column ch = q & 7 (the 8 lanes of a row adjacent)
+  u32x4 rq[NQP], rk[NQP], rv[NQP], rd[NQP];
+  float mx[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int it = 0; it < NQP; ++it) {
+    const int q = tid + 512 * it, row = q >> 3, ch = q & 7;
+    u32x4 a = {0, 0, 0, 0}, k = a, v = a, d = a, o = a;
+    if (row < p.T) {
+      a = *reinterpret_cast<const u32x4*>(Qg + (long)row * p.ld + ch * 8);
+      k = *reinterpret_cast<const u32x4*>(Kg + (long)row * p.ld + ch * 8);
+      v = *reinterpret_cast<const u32x4*>(Vg + (long)row * p.ld + ch * 8);
+      d = *reinterpret_cast<const u32x4*>(dOg + (long)row * p.ldo + ch * 8);
+      o = *reinterpret_cast<const u32x4*>(Og + (long)row * p.ldo + ch * 8);
+    }
+    rq[it] = a; rk[it] = k; rv[it] = v; rd[it] = d;
+    float dl = 0.f;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      mx[0] = fmaxf(mx[0], fmaxf(fabsf(lo_bf(a[e])), fabsf(hi_bf(a[e]))));
+      mx[1] = fmaxf(mx[1], fmaxf(fabsf(lo_bf(k[e])), fabsf(hi_bf(k[e]))));
+      mx[2] = fmaxf(mx[2], fmaxf(fabsf(lo_bf(v[e])), fabsf(hi_bf(v[e]))));
+      mx[3] = fmaxf(mx[3], fmaxf(fabsf(lo_bf(d[e])), fabsf(hi_bf(d[e]))));
+      dl += lo_bf(d[e]) * lo_bf(o[e]) + hi_bf(d[e]) * hi_bf(o[e]);
+    }
+    dl = row8_sum(dl);  // delta of this row: the 8 lanes of the row (DPP)
+    if (ch == 0) {
+      dl_s[row] = dl;
+      nlse_s[row] = row < p.T ? -p.lse[(long)bh * p.T + row] : -INFINITY;  // rows >= T: P = 0
+    }
+  }
+#pragma unroll
+  for (int m = 0; m < 4; ++m) {
+    const float w = warp_max(mx[m]);
+    if (lane == 0) red[wave][m] = w;
+  }
+  __syncthreads();
+  int ex[4];
+#pragma unroll
+  for (int m = 0; m < 4; ++m) {
+    float a = red[0][m];
+#pragma unroll
+    for (int w = 1; w < 8; ++w) a = fmaxf(a, red[w][m]);
+    ex[m] = pow2_exp(a);
+  }
+  const float sq = ldexpf(1.f, ex[0]), sk = ldexpf(1.f, ex[1]), sv = ldexpf(1.f, ex[2]), sd = ldexpf(1.f, ex[3]);
+#pragma unroll
+  for (int it = 0; it < NQP; ++it) {
+    const int q = tid + 512 * it, row = q >> 3, ch = q & 7;
+    const int off = k8_off(row, ch >> 1) + (ch & 1) * 8;
+    auto put = [&](char* img, const u32x4& x, float s) __attribute__((always_inline)) {
+      uint2 w;
+      w.x = e4m3x4(lo_bf(x[0]) * s, hi_bf(x[0]) * s, lo_bf(x[1]) * s, hi_bf(x[1]) * s);
+      w.y = e4m3x4(lo_bf(x[2]) * s, hi_bf(x[2]) * s, lo_bf(x[3]) * s, hi_bf(x[3]) * s);
+      *reinterpret_cast<uint2*>(img + off) = w;
+    };
+    put(Qi, rq[it], sq);
+    put(Ki, rk[it], sk);
+    put(Vi, rv[it], sv);
+    put(Oi, rd[it], sd);
+  }
+  __syncthreads();
+  // E8M0 dequantisation operands of the staged tensors
+  const int dq_q = 127 - ex[0], dq_k = 127 - ex[1], dq_v = 127 - ex[2], dq_d = 127 - ex[3];
+  constexpr int P_EXP = 8;  // P in [0, 1] -> codes of 256 P
+
+  // ---------------------------------------------------------------- phase 1: dK, dV
+  if (wave < NT2) {
+    const int kt = wave, k0 = 32 * kt;
+    const int key = k0 + col;
+    const bool kok = key < p.T;
+    const i32x8 kf = row_frag(Ki, key, hh);
+    const i32x8 vf = row_frag(Vi, key, hh);
+    f32x16 dvT[2], dkT[2];
+#pragma unroll
+    for (int dn = 0; dn < 2; ++dn)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) dvT[dn][r] = dkT[dn][r] = 0.f;
+#pragma unroll 1
+    for (int qp = 0; qp < NQP; ++qp) {
+      uint32_t pc[2][4], dc[2][4];
+      int de[2];
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        const int qt = 2 * qp + u;
+        const f32x16 z = {};
+        // S[q = 32 qt + 8 (r >> 2) + 4 hh + (r & 3)][key]
+        const f32x16 s = mfma8(row_frag(Qi, 32 * qt + col, hh), kf, z, dq_q, dq_k);
+        const f32x16 dp = mfma8(row_frag(Oi, 32 * qt + col, hh), vf, z, dq_d, dq_v);
+        float pv[16], ds[16], am = 0.f;
+#pragma unroll
+        for (int jj = 0; jj < 4; ++jj) {
+          const int q4 = 32 * qt + 8 * jj + 4 * hh;
+          const f32x4 nl = *reinterpret_cast<const f32x4*>(nlse_s + q4);
+          const f32x4 dl = *reinterpret_cast<const f32x4*>(dl_s + q4);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const int r = 4 * jj + e;
+            const float pr = kok ? __builtin_amdgcn_exp2f(fmaf(s[r], p.c, nl[e])) : 0.f;
+            pv[r] = pr;
+            ds[r] = pr * (dp[r] - dl[e]);
+            am = fmaxf(am, fabsf(ds[r]));
+          }
+        }
+        if (p.dbg != nullptr) {
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            const int q = 32 * qt + 8 * (r >> 2) + 4 * hh + (r & 3);
+            p.dbg[((long)bh * ROWS + q) * ROWS + key] = ds[r];
+          }
+        }
+        const int e = pow2_exp(warp_max(am));  // one scale per 32 x 32 dS tile
+        de[u] = e;
+        const float sds = ldexpf(1.f, e);
+#pragma unroll
+        for (int w = 0; w < 4; ++w) {
+          pc[u][w] = e4m3x4(pv[4 * w] * 256.f, pv[4 * w + 1] * 256.f, pv[4 * w + 2] * 256.f, pv[4 * w + 3] * 256.f);
+          dc[u][w] = e4m3x4(ds[4 * w] * sds, ds[4 * w + 1] * sds, ds[4 * w + 2] * sds, ds[4 * w + 3] * sds);
+          // dS^T image [key][q]: 4 consecutive queries 32 qt + 8 w + 4 hh of this key
+          *reinterpret_cast<uint32_t*>(dSt + key * DSR + 32 * qt + 8 * w + 4 * hh) = dc[u][w];
+        }
+        if (lane == 0) tsc[qt * NT2 + kt] = 127 - e;
+      }
+      // B operands as packed: tile 2 qp in bytes 0..15, tile 2 qp + 1 in bytes 16..31, so
+      // lane half hh's block scale is query tile 2 qp + hh's
+      const i32x8 pf = {(int)pc[0][0], (int)pc[0][1], (int)pc[0][2], (int)pc[0][3],
+                        (int)pc[1][0], (int)pc[1][1], (int)pc[1][2], (int)pc[1][3]};
+      const i32x8 sf = {(int)dc[0][0], (int)dc[0][1], (int)dc[0][2], (int)dc[0][3],
+                        (int)dc[1][0], (int)dc[1][1], (int)dc[1][2], (int)dc[1][3]};
+      const int sb_ds = 127 - (hh ? de[1] : de[0]);
+#pragma unroll
+      for (int dn = 0; dn < 2; ++dn) {
+        // A: rows d = 32 dn + 16 (g & 1) + j of dO^T / Q^T, k = the pair's queries (same order)
+        const i32x8 oa = tr_frag<true>(Oi, 64 * qp, 2 * dn + (g & 1), j, hh);
+        dvT[dn] = mfma8(oa, pf, dvT[dn], dq_d, 127 - P_EXP);
+        const i32x8 qa = tr_frag<true>(Qi, 64 * qp, 2 * dn + (g & 1), j, hh);
+        dkT[dn] = mfma8(qa, sf, dkT[dn], dq_q, sb_ds);
+      }
+    }
+    // dK^T / dV^T[d = 32 dn + 8 jj + 4 hh + e][key]: 4 consecutive d per store
+    if (kok) {
+      u16* drow = p.dqkv + ((long)b * p.T + key) * p.ld + h * D;
+#pragma unroll
+      for (int dn = 0; dn < 2; ++dn)
+#pragma unroll
+        for (int jj = 0; jj < 4; ++jj) {
+          const int d0 = 32 * dn + 8 * jj + 4 * hh;
+          uint2 wk, wv;
+          wk.x = pack2bf(dkT[dn][4 * jj] * p.scale, dkT[dn][4 * jj + 1] * p.scale);
+          wk.y = pack2bf(dkT[dn][4 * jj + 2] * p.scale, dkT[dn][4 * jj + 3] * p.scale);
+          wv.x = pack2bf(dvT[dn][4 * jj], dvT[dn][4 * jj + 1]);
+          wv.y = pack2bf(dvT[dn][4 * jj + 2], dvT[dn][4 * jj + 3]);
+          *reinterpret_cast<uint2*>(drow + p.H * D + d0) = wk;
+          *reinterpret_cast<uint2*>(drow + 2 * p.H * D + d0) = wv;
+        }
+    }
+  }
+  __syncthreads();
+
+  // ---------------------------------------------------------------- phase 2: dQ
+  const int nqt = (p.T + 31) / 32;
+  for (int unit = wave; unit < 2 * nqt; unit += 8) {
+    const int qt = unit >> 1, dn = unit & 1;
+    f32x16 acc = {};
+#pragma unroll
+    for (int kp = 0; kp < NQP; ++kp) {
+      const int kt = 2 * kp + hh;  // this lane half's scale block = key tile kt
+      // A: K^T rows d = 32 dn + 16 (g & 1) + j, k = keys 64 kp .. 64 kp + 63 (natural order)
+      const i32x8 ka = tr_frag<false>(Ki, 64 * kp, 2 * dn + (g & 1), j, hh);
+      // B: dS^T[key][q]: column q = 32 qt + 16 (g & 1) + j, the same keys
+      i32x8 sb;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int krow = 64 * kp + kb_row<false>(r, j >> 1, hh);
+        const i32x2 v = tr8(dSt + krow * DSR + 32 * qt + 16 * (g & 1) + 8 * (j & 1));
+        sb[2 * r] = v[0];
+        sb[2 * r + 1] = v[1];
+      }
+      acc = mfma8(ka, sb, acc, dq_k, tsc[qt * NT2 + kt]);
+    }
+    const int q = 32 * qt + col;
+    if (q < p.T) {
+      u16* drow = p.dqkv + ((long)b * p.T + q) * p.ld + h * D;
+#pragma unroll
+      for (int jj = 0; jj < 4; ++jj) {
+        uint2 w;
+        w.x = pack2bf(acc[4 * jj] * p.scale, acc[4 * jj + 1] * p.scale);
+        w.y = pack2bf(acc[4 * jj + 2] * p.scale, acc[4 * jj + 3] * p.scale);
+        *reinterpret_cast<uint2*>(drow + 32 * dn + 8 * jj + 4 * hh) = w;
+      }
+    }
+  }
+}
+
+}  // namespace
+
+// fused fp8 backward for T <= 256, head dim 64 (d(qkv) bf16); -1 when not covered
+static int attn_bwd_f8(const void* qkv, const void* out, const void* dout, const float* lse, void* dqkv, int B,
+                       int T, int H, float scale, float* dbg, hipStream_t st);
+
+PDT_API int pdt_attn_bwd_f8(const void* qkv, const void* out, const void* dout, const float* lse, void* dqkv,
+                            int B, int T, int H, float scale, hipStream_t st) {
+  return attn_bwd_f8(qkv, out, dout, lse, dqkv, B, T, H, scale, nullptr, st);
+}
+
+// the same, also writing phase 1's fp32 dS to dbg ([B*H][R][R], R = 64 ceil(T / 64)) for tests
+PDT_API int pdt_attn_bwd_f8_debug(const void* qkv, const void* out, const void* dout, const float* lse, void* dqkv,
+                                  int B, int T, int H, float scale, float* dbg, hipStream_t st) {
+  return attn_bwd_f8(qkv, out, dout, lse, dqkv, B, T, H, scale, dbg, st);
+}
+
+static int attn_bwd_f8(const void* qkv, const void* out, const void* dout, const float* lse, void* dqkv, int B,
+                       int T, int H, float scale, float* dbg, hipStream_t st) {
+  if (T < 1 || T > 256) return -1;
+  AttnBwdF8Params p;
+  p.qkv = (const u16*)qkv;
+  p.out = (const u16*)out;
+  p.dout = (const u16*)dout;
+  p.lse = lse;
+  p.dqkv = (u16*)dqkv;
+  p.B = B; p.T = T; p.H = H;
+  p.ld = 3L * H * D;
+  p.ldo = (long)H * D;
+  p.c = scale * 1.4426950408889634f;
+  p.scale = scale;
+  p.dbg = dbg;
+  const int nqp = (T + 63) / 64;
+  dim3 g(B * H);
+#define BWD(N) hipLaunchKernelGGL((attn_bwd_f8_kernel<N>), g, dim3(512), 0, st, p)
+  switch (nqp) {
+    case 1: BWD(1); break;
+    case 2: BWD(2); break;
+    case 3: BWD(3); break;
+    default: BWD(4); break;
+  }
+#undef BWD
+  PDT_RETURN_LAUNCH();
+}

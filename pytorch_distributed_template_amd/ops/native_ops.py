@@ -108,6 +108,8 @@ _SIGS = {
     "pdt_cast_fp8_delayed": (c_int, [P, c_int, c_long, P, c_int, P, P, P]),
     "pdt_fp8_meta_seed": (c_int, [P, c_long, c_int, P, P]),
     "pdt_attn_bwd": (c_int, [P, P, P, P, P, P, c_int, c_int, c_int, c_float, P]),
+    "pdt_attn_bwd_f8": (c_int, [P, P, P, P, P, c_int, c_int, c_int, c_float, P]),
+    "pdt_attn_bwd_f8_debug": (c_int, [P, P, P, P, P, c_int, c_int, c_int, c_float, P, P]),
     "pdt_lenet_grad_row": (c_int, [c_int]),
     "pdt_lenet_fwd": (c_int, [P] * 9 + [c_int, c_int, c_int, c_float, c_float, c_uint, P, P, P, P]),
     "pdt_lenet_bwd": (c_int, [P] * 9 + [c_int, c_int, c_int, c_float, c_float, c_uint, P, P, P, P]),
@@ -2478,7 +2480,7 @@ class _QKVAttention(torch.autograd.Function):
         else:
             _chk(_load().pdt_attn_fwd(_p(qkv), _p(out), _p(lse), B, T, H, scale, _s()), "attn_fwd")
         ctx.save_for_backward(qkv, out, lse)
-        ctx.H, ctx.scale, ctx.grad_owner = H, scale, grad_owner
+        ctx.H, ctx.scale, ctx.grad_owner, ctx.fp8 = H, scale, grad_owner, bool(fp8)
         return out
 
     @staticmethod
@@ -2500,6 +2502,11 @@ class _QKVAttention(torch.autograd.Function):
             if rc == 0:
                 dqkv._pdt_f8g = (codes, dq, owner)
                 return dqkv, None, None, None, None, None
+        if ctx.fp8 and T <= 256 and os.environ.get("PDT_FP8_ATTN_BWD", "1") == "1":
+            # fused fp8 backward (csrc/attention_bwd_f8.hip): dQ, dK, dV in one kernel on e4m3 MFMA
+            _chk(_load().pdt_attn_bwd_f8(_p(qkv), _p(out), _p(dout), _p(lse), _p(dqkv), B, T, ctx.H, ctx.scale,
+                                         _s()), "attn_bwd_f8")
+            return dqkv, None, None, None, None, None
         _chk(_load().pdt_attn_bwd(_p(qkv), _p(out), _p(dout), _p(lse), _p(delta), _p(dqkv), B, T, ctx.H,
                                   ctx.scale, _s()), "attn_bwd")
         return dqkv, None, None, None, None, None
@@ -2507,8 +2514,8 @@ class _QKVAttention(torch.autograd.Function):
 
 def qkv_attention(qkv, num_heads, fp8=False, fp8_for=None, grad_fp8_for=None):
     """softmax(q k^T / 8) v over heads of 64 for a packed [B, T, 3*H*64] qkv. ``fp8``: the
-    score GEMM on e4m3 MFMA (per-head / per-tile power-of-two scales, T <= 256); the
-    backward is the bf16 recomputing one either way. ``fp8_for``: the fp8 layer consuming
+    score GEMM on e4m3 MFMA (per-head / per-tile power-of-two scales, T <= 256) and the
+    fused fp8 backward (csrc/attention_bwd_f8.hip; PDT_FP8_ATTN_BWD=0: the bf16 one). ``fp8_for``: the fp8 layer consuming
     the output (the attention projection): under delayed scaling the kernel also writes
     its e4m3 input (``_pdt_f8`` on the result, as :func:`ln_fork` does); ``grad_fp8_for``:
     the fp8 layer that produced qkv -- the backward then also writes its e5m2 output

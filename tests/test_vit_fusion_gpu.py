@@ -396,12 +396,15 @@ def _fp8_emulated_scores(q, k):
     return qq @ kq.transpose(-1, -2)
 
 
+@pytest.mark.parametrize("bwd", ["f8", "bf16"])
 @pytest.mark.parametrize("B,T,H", [(3, 197, 4), (2, 64, 2), (1, 50, 12), (2, 256, 3), (2, 16, 3), (1, 120, 2)])
-def test_fp8_attention_forward_and_bf16_backward(B, T, H):
+def test_fp8_attention_forward_and_backward(B, T, H, bwd, monkeypatch):
     """fp8 score GEMM (csrc/attention_f8.hip): (1) against a reference that applies the
     kernel's own quantization (per-head K / per-32-query-tile Q power-of-two scales, e4m3)
     in fp32 -- checks the kernel itself tightly; (2) against exact fp32 attention -- the
-    fp8 error budget, with the bf16 recomputing backward run on its output and LSE."""
+    fp8 error budget, with the fused fp8 backward (csrc/attention_bwd_f8.hip, the default
+    for fp8 attention) or the bf16 recomputing one run on its output and LSE."""
+    monkeypatch.setenv("PDT_FP8_ATTN_BWD", "1" if bwd == "f8" else "0")
     torch.manual_seed(B * 100 + T)
     qkv = (torch.randn(B, T, 3 * H * 64, device="cuda") * 1.5).to(torch.bfloat16)
     dout = torch.randn(B, T, H * 64, device="cuda").to(torch.bfloat16)
@@ -428,4 +431,5 @@ def test_fp8_attention_forward_and_bf16_backward(B, T, H):
     g, gr = xn.grad.view(B, T, 3, H * 64), x.grad.view(B, T, 3, H * 64)
     for i, name in enumerate("qkv"):
         ei = nrmerr(g[:, :, i], gr[:, :, i])
-        assert ei < 1e-1, (name, ei)
+        # fp8 backward: its own e4m3 score recompute adds ~0.1 (tests/test_attention_bwd_f8_gpu.py)
+        assert ei < (1.6e-1 if bwd == "f8" else 1e-1), (name, ei)
