@@ -212,7 +212,7 @@ __global__ void __launch_bounds__(512) attn_bwd_f8_kernel(AttnBwdF8Params p) {
     for (int dn = 0; dn < 2; ++dn)
 #pragma unroll
       for (int r = 0; r < 16; ++r) dvT[dn][r] = dkT[dn][r] = 0.f;
-#pragma unroll 1
+#pragma unroll 1  // (unrolled by 2 it spills at NQP 3 / 4)
     for (int qp = 0; qp < NQP; ++qp) {
       uint32_t pc[2][4], dc[2][4];
       int de[2];

@@ -267,6 +267,7 @@ def test_attention_backward_e5m2_codes_match_separate_cast(monkeypatch):
     (for the qkv projection) equal the delayed-scaling cast of d(qkv)."""
     torch.manual_seed(30)
     monkeypatch.setenv("PDT_FP8_ATTN_Q8", "1")
+    monkeypatch.setenv("PDT_FP8_ATTN_BWD", "0")  # the codes ride on the bf16 backward kernels
     B, T, H = 2, 197, 4
     qkv_fc = nn.Linear(H * 64, 3 * H * 64).cuda()
     no._quant_grad(torch.randn(B * T, 3 * H * 64, device="cuda").to(torch.bfloat16), qkv_fc, "_pdt_fp8_gmeta")
