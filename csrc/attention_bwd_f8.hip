@@ -11,10 +11,8 @@
 //   dK^T = Q^T dS   A = Q^T  (tr8 from the Q rows),                 B = dS (registers)
 //   dQ^T = K^T dS^T A = K^T  (tr8 from the K rows),                 B = dS^T (LDS image)
 //
-// Operand K layout of the 32x32x64 f8 MFMA (probe: scripts/probes/mfma_scale_probe.hip):
-// byte b of lane (row, half hh) is k = 16 hh + b for b < 16 and k = 32 + 16 hh + (b - 16)
-// otherwise, and lane (row, hh)'s E8M0 scale covers the k block [32 hh, 32 hh + 32) -- i.e.
-// the first 16 bytes of BOTH halves form scale block 0.
+// Operand k layout and its consequences: csrc/fp8_mfma.h (the first 16 bytes of BOTH lane
+// halves form E8M0 scale block 0).
 // Phase 1: wave w owns key tile w (32 keys) and walks the query tiles in pairs. An S / dP
 // accumulator holds 16 queries x 1 key per lane; packed to fp8 as they are (tile 2qp in
 // bytes 0..15, tile 2qp + 1 in bytes 16..31) they ARE the dV / dK B operand with scale
@@ -30,71 +28,12 @@
 // accumulation is fp32; dQ / dK / dV are written bf16 into the qkv-layout gradient as the
 // bf16 kernels do. lse is the forward's (log2 domain), delta = rowsum(dO * O) is computed
 // here from the bf16 O and dO.
-#include "pdt_common.h"
+#include "fp8_mfma.h"
 
 namespace {
 
 constexpr int D = 64;
-
-typedef int i32x8 __attribute__((ext_vector_type(8)));
-typedef int i32x2 __attribute__((ext_vector_type(2)));
-typedef float f32x16 __attribute__((ext_vector_type(16)));
-
-// fp8 row image [rows][64 B]: 16-B chunk c of row r at chunk c ^ ((r >> 2) & 3)
-__device__ __forceinline__ int k8_off(int row, int chunk) { return row * 64 + ((chunk ^ ((row >> 2) & 3)) << 4); }
-
-// largest e with amax * 2^e <= 448 (0 for an all-zero block)
-__device__ __forceinline__ int pow2_exp(float amax) {
-  if (!(amax > 0.f)) return 0;
-  const int e = (int)floorf(__log2f(448.f / amax));
-  return max(min(e, 100), -100);
-}
-
-__device__ __forceinline__ uint32_t e4m3x4(float a, float b, float c, float d) { return pdt_cvt4_f8<0>(a, b, c, d); }
-
-// the 32-byte A / B fragment of a row image: row `row`, bytes 32 hh .. 32 hh + 31
-__device__ __forceinline__ i32x8 row_frag(const char* img, int row, int hh) {
-  const u32x4 a = *reinterpret_cast<const u32x4*>(img + k8_off(row, 2 * hh));
-  const u32x4 b = *reinterpret_cast<const u32x4*>(img + k8_off(row, 2 * hh + 1));
-  return i32x8{(int)a[0], (int)a[1], (int)a[2], (int)a[3], (int)b[0], (int)b[1], (int)b[2], (int)b[3]};
-}
-
-__device__ __forceinline__ i32x2 tr8(const char* a) {
-  return __builtin_amdgcn_ds_read_tr8_b64_v2i32(
-      (i32x2 __attribute__((address_space(3)))*)((__attribute__((address_space(3))) char*)(uintptr_t)(uint32_t)(
-          uintptr_t)a));
-}
-
-// the query order of a packed P / dS accumulator within one 32-query tile (see the header)
-__device__ __forceinline__ int pi_q(int p) { return 8 * ((p & 15) >> 2) + 4 * (p >> 4) + (p & 3); }
-
-// the image row holding MFMA k of lane half hh's 4 tr8 reads: read r, row jj of the read
-// (bytes 8 r + jj): k block r >> 1, position 16 hh + 8 (r & 1) + jj within it
-template <bool PI>
-__device__ __forceinline__ int kb_row(int r, int jj, int hh) {
-  const int pos = 16 * hh + 8 * (r & 1) + jj;
-  return 32 * (r >> 1) + (PI ? pi_q(pos) : pos);
-}
-
-// Transposed 32x32x64 operand from a row image: lane (16-lane group g, j) gets column
-// 16 (g & 1) + j of the 16-byte column block `chunk`, for the 64 k rows row0 + kb_row(..)
-// (4 tr8 reads of 8 rows; lane pair j >> 1 addresses one row, byte half j & 1).
-template <bool PI>
-__device__ __forceinline__ i32x8 tr_frag(const char* img, int row0, int chunk, int j, int hh) {
-  i32x8 out;
-#pragma unroll
-  for (int r = 0; r < 4; ++r) {
-    const int row = row0 + kb_row<PI>(r, j >> 1, hh);
-    const i32x2 v = tr8(img + k8_off(row, chunk) + 8 * (j & 1));
-    out[2 * r] = v[0];
-    out[2 * r + 1] = v[1];
-  }
-  return out;
-}
-
-__device__ __forceinline__ f32x16 mfma8(const i32x8& a, const i32x8& b, const f32x16& c, int sa, int sb) {
-  return __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(a, b, c, 0, 0, 0, sa, 0, sb);
-}
+using namespace pdt_f8;
 
 struct AttnBwdF8Params {
   const u16* qkv;    // [B, T, 3, H, 64] bf16

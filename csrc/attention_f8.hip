@@ -6,9 +6,14 @@
 //                 bf16 MFMA rate); fp32 accumulate, unit block scales.
 //   softmax       fp32, online over 32-key tiles (running max / sum per query,
 //                 O rescaled when the max moves), exp2 with the scale folded in.
-//   O^T = V^T P^T on mfma_f32_32x32x16_bf16: P^T comes straight from the S^T
-//                 accumulator registers (query on the lane, keys in registers),
-//                 V^T through the hardware-transposing LDS read ds_read_b64_tr_b16.
+//   O^T = V^T P^T on mfma_scale_f32_32x32x64_f8f6f4 as well (64 keys = two key tiles per
+//                 instruction, softmax max / rescale per tile pair): P^T comes straight from
+//                 the S^T accumulator registers as e4m3 codes of 256 P (P <= 1), packed
+//                 tile 2tp in bytes 0..15 / 2tp + 1 in 16..31 -- the operand k layout of
+//                 csrc/fp8_mfma.h -- and V^T from an e4m3 row image of V (per-head power-of-
+//                 two scale) through ds_read_b64_tr_b8 in that same key order. The row sums
+//                 l are of the fp32 P. The bf16 instantiation (F8 = false) keeps the bf16
+//                 PV on mfma_f32_32x32x16_bf16 with V^T via ds_read_b64_tr_b16.
 //
 // Quantization (no extra pass over HBM, no host sync): each workgroup owns one
 // (batch, head); it stages the head's K from the bf16 qkv buffer, reduces |K|max
@@ -21,7 +26,7 @@
 // the bf16 recomputing backward consumes them unchanged (it recomputes P from the
 // bf16 Q and K: the fp8 forward's probabilities differ from it by the fp8 score
 // error only).
-#include "pdt_common.h"
+#include "fp8_mfma.h"
 
 namespace {
 
@@ -31,9 +36,10 @@ typedef int i32x8 __attribute__((ext_vector_type(8)));
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 typedef __attribute__((address_space(3))) bf16x4 lds_bf16x4;
 
-// fp8 K image: [rows][64 B], 16-B chunk c of row r at chunk c ^ ((r >> 2) & 3):
-// a 16-lane ds_read_b128 group (16 consecutive rows, one chunk) hits 16 distinct slots
-__device__ __forceinline__ int k8_off(int row, int chunk) { return row * 64 + ((chunk ^ ((row >> 2) & 3)) << 4); }
+// fp8 K / V images: [rows][64 B], 16-B chunk c of row r at chunk c ^ ((r >> 2) & 3)
+// (pdt_f8::k8_off): a 16-lane ds_read_b128 group (16 consecutive rows, one chunk) hits 16
+// distinct slots
+using pdt_f8::k8_off;
 
 // bf16 V image for transposed reads (same swizzle as csrc/attention.hip): [rows][128 B]
 __device__ __forceinline__ int vt_off(int row, int byte_in_row) {
@@ -80,44 +86,74 @@ __device__ __forceinline__ int k16_off(int row, int chunk) { return row * 128 + 
 // score GEMM in bf16 (4 x mfma_f32_32x32x16_bf16 per 32 x 32 tile, K kept as bf16) -- the
 // bf16 forward of ViT (126 VGPRs, 3 workgroups per CU, vs 248 VGPRs / 1 wave per SIMD
 // for the whole-sequence kernel in csrc/attention.hip)
-template <int NKT, bool F8>
+template <int NKT, bool F8, bool PV8 = false>
 __global__ void __launch_bounds__(256) attn_fwd_f8_kernel(AttnF8Params p) {
+  static_assert(F8 || !PV8, "the fp8 PV rides on the fp8 score kernel");
   constexpr int ROWS = NKT * 32;
+  constexpr int VROWS = PV8 ? 64 * ((NKT + 1) / 2) : ROWS;         // fp8 V: whole key-tile pairs
   __shared__ __attribute__((aligned(16))) char Ks[ROWS * (F8 ? 64 : 128)];  // fp8 or bf16 K
-  __shared__ __attribute__((aligned(16))) char Vs[ROWS * 128];    // bf16 V (tr image)
-  __shared__ float red[4];
+  __shared__ __attribute__((aligned(16))) char Vs[VROWS * (PV8 ? 64 : 128)];  // fp8 rows / bf16 tr image
+  __shared__ float red[4], vred[4];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int bh = blockIdx.x, b = bh / p.H, h = bh % p.H;
   const u16* base = p.qkv + (long)b * p.T * p.ld + h * D;
   const u16* Kg = base + p.H * D;
   const u16* Vg = base + 2 * p.H * D;
 
-  // ---- stage V (bf16, transposed-read image) and K (registers first: |K|max)
+  // ---- stage V (bf16 transposed-read image, or e4m3 rows) and K (registers first: |K|max)
   constexpr int CH = ROWS * 8;  // 16-B chunks of one [ROWS][64] bf16 matrix
-  constexpr int NIT = (CH + 255) / 256;
-  u32x4 kv[NIT];
-  float kmax = 0.f;
+  constexpr int VCH = VROWS * 8;
+  constexpr int NIT = (VCH + 255) / 256;
+  u32x4 kv[NIT], vv[PV8 ? NIT : 1];
+  float kmax = 0.f, vmax = 0.f;
 #pragma unroll
   for (int it = 0; it < NIT; ++it) {
     const int q = tid + it * 256;
     const int row = q >> 3, ch = q & 7;
     u32x4 v = {0, 0, 0, 0}, k = {0, 0, 0, 0};
-    if (q < CH && row < p.T) {
+    if (q < VCH && row < p.T) {
       v = *reinterpret_cast<const u32x4*>(Vg + (long)row * p.ld + ch * 8);
       k = *reinterpret_cast<const u32x4*>(Kg + (long)row * p.ld + ch * 8);
     }
-    if (q < CH) *reinterpret_cast<u32x4*>(Vs + vt_off(row, ch * 16)) = v;
+    if constexpr (PV8) {
+      vv[it] = v;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) vmax = fmaxf(vmax, fmaxf(fabsf(lo_bf(v[e])), fabsf(hi_bf(v[e]))));
+    } else if (q < CH) {
+      *reinterpret_cast<u32x4*>(Vs + vt_off(row, ch * 16)) = v;
+    }
     kv[it] = k;
 #pragma unroll
     for (int e = 0; e < 4; ++e) kmax = fmaxf(kmax, fmaxf(fabsf(lo_bf(k[e])), fabsf(hi_bf(k[e]))));
   }
-  float sk = 1.f;
+  float sk = 1.f, sv = 1.f;
+  int ev = 0;
   if constexpr (F8) {
     kmax = warp_max(kmax);
-    if (lane == 0) red[wave] = kmax;
+    vmax = warp_max(vmax);
+    if (lane == 0) {
+      red[wave] = kmax;
+      vred[wave] = vmax;
+    }
     __syncthreads();
     kmax = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
     sk = pow2_scale(kmax);
+  }
+  if constexpr (PV8) {
+    ev = pdt_f8::pow2_exp(fmaxf(fmaxf(vred[0], vred[1]), fmaxf(vred[2], vred[3])));
+    sv = ldexpf(1.f, ev);
+#pragma unroll
+    for (int it = 0; it < NIT; ++it) {  // e4m3 V rows (zero rows up to the tile pair)
+      const int q = tid + it * 256;
+      if (q < VCH) {
+        const int row = q >> 3, ch = q & 7;
+        const u32x4 v = vv[it];
+        uint2 w;
+        w.x = cvt4_e4m3(lo_bf(v[0]) * sv, hi_bf(v[0]) * sv, lo_bf(v[1]) * sv, hi_bf(v[1]) * sv);
+        w.y = cvt4_e4m3(lo_bf(v[2]) * sv, hi_bf(v[2]) * sv, lo_bf(v[3]) * sv, hi_bf(v[3]) * sv);
+        *reinterpret_cast<uint2*>(Vs + k8_off(row, ch >> 1) + (ch & 1) * 8) = w;
+      }
+    }
   }
 #pragma unroll
   for (int it = 0; it < NIT; ++it) {
@@ -183,10 +219,70 @@ __global__ void __launch_bounds__(256) attn_fwd_f8_kernel(AttnF8Params p) {
 #pragma unroll
       for (int r = 0; r < 16; ++r) o[dt][r] = 0.f;
 
+    if constexpr (PV8) {
+      // key tiles in pairs: S^T of tiles 2tp, 2tp + 1 (e4m3), one softmax update, then
+      // O^T += V^T P^T on ONE 64-key fp8 MFMA per 32-d half
+#pragma unroll 1
+      for (int tp = 0; tp < (NKT + 1) / 2; ++tp) {
+        f32x16 s2[2];
+        float mt = -INFINITY;
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+          const int t = 2 * tp + u;
+          f32x16 s = {};
+          if (t < NKT) {
+            const int krow = 32 * t + col;
+            const u32x4 a0 = *reinterpret_cast<const u32x4*>(Ks + k8_off(krow, 2 * hh));
+            const u32x4 a1 = *reinterpret_cast<const u32x4*>(Ks + k8_off(krow, 2 * hh + 1));
+            const i32x8 kf = {(int)a0[0], (int)a0[1], (int)a0[2], (int)a0[3],
+                              (int)a1[0], (int)a1[1], (int)a1[2], (int)a1[3]};
+            s = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(kf, qf, s, 0, 0, 0, 127, 0, 127);
+          }
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            const int key = 32 * t + (r & 3) + 8 * (r >> 2) + 4 * hh;
+            const float v = (t < NKT && (t < NKT - 1 || key < p.T)) ? s[r] * cs : -INFINITY;
+            s[r] = v;
+            mt = fmaxf(mt, v);
+          }
+          s2[u] = s;
+        }
+        mt = xor32_reduce(mt, MaxOp{});
+        const float mn = fmaxf(m, mt);
+        const float alpha = exp2f(m - mn);
+        float ls = 0.f;
+        uint32_t pc[2][4];
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            const float e = __builtin_amdgcn_exp2f(s2[u][r] - mn);
+            s2[u][r] = e;
+            ls += e;
+          }
+#pragma unroll
+          for (int w = 0; w < 4; ++w)
+            pc[u][w] = cvt4_e4m3(s2[u][4 * w] * 256.f, s2[u][4 * w + 1] * 256.f, s2[u][4 * w + 2] * 256.f,
+                                 s2[u][4 * w + 3] * 256.f);
+        }
+        ls = xor32_reduce(ls, AddOp{});
+        l = l * alpha + ls;
+        m = mn;
+        const i32x8 pf = {(int)pc[0][0], (int)pc[0][1], (int)pc[0][2], (int)pc[0][3],
+                          (int)pc[1][0], (int)pc[1][1], (int)pc[1][2], (int)pc[1][3]};
+#pragma unroll
+        for (int dt = 0; dt < 2; ++dt) {
+          o[dt] *= alpha;
+          // A: V^T rows d = 32 dt + 16 (grp & 1) + i16, k = keys of the pair (P's order)
+          const i32x8 va = pdt_f8::tr_frag<true>(Vs, 64 * tp, 2 * dt + (grp & 1), i16, hh);
+          o[dt] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(va, pf, o[dt], 0, 0, 0, 127 - ev, 0, 127 - 8);
+        }
+      }
+    }
     // not unrolled: a fully unrolled key loop hoists every tile's K fragment (214 VGPRs
     // at 7 tiles, 2 waves/SIMD); rolled it stays near 100 (more workgroups per CU)
 #pragma unroll 1
-    for (int t = 0; t < NKT; ++t) {
+    for (int t = 0; t < (PV8 ? 0 : NKT); ++t) {
       const int krow = 32 * t + col;
       f32x16 s = {};
       if constexpr (F8) {
@@ -285,6 +381,23 @@ __global__ void __launch_bounds__(256) attn_fwd_f8_kernel(AttnF8Params p) {
 
 }  // namespace
 
+// PDT_FP8_ATTN_PV=1 (or pdt_attn_set_pv8(1)): the PV GEMM on e4m3 as well. Off by default:
+// measured slower at ViT-B/16 bs 1024 (6.66 vs 5.27 ms per step over 12 layers: the
+// per-pair softmax and the tr8 V reads lengthen the serial chain more than the 2x MFMA
+// rate saves) and it adds ~1.5 % logits error (profiles/vit_b16_fp8_bs1024_step_round3_*).
+static int g_attn_pv8 = -1;
+static int attn_pv8() {
+  if (g_attn_pv8 < 0) {
+    const char* e = getenv("PDT_FP8_ATTN_PV");
+    g_attn_pv8 = (e && e[0] == '1') ? 1 : 0;
+  }
+  return g_attn_pv8;
+}
+PDT_API int pdt_attn_set_pv8(int on) {
+  g_attn_pv8 = on ? 1 : 0;
+  return 0;
+}
+
 // fp8 forward for T <= 256, head dim 64; -1 when the geometry is not covered
 PDT_API int pdt_attn_fwd_f8(const void* qkv, void* out, float* lse, int B, int T, int H, float scale,
                             hipStream_t st) {
@@ -300,7 +413,9 @@ PDT_API int pdt_attn_fwd_f8(const void* qkv, void* out, float* lse, int B, int T
   p.q8 = nullptr; p.q8_meta = nullptr; p.q8_part = nullptr;
   const int nkt = (T + 31) / 32;
   dim3 g(B * H);
-#define F8(N) hipLaunchKernelGGL((attn_fwd_f8_kernel<N, true>), g, dim3(256), 0, st, p)
+#define F8(N)                                                                         \
+  if (attn_pv8()) hipLaunchKernelGGL((attn_fwd_f8_kernel<N, true, true>), g, dim3(256), 0, st, p); \
+  else hipLaunchKernelGGL((attn_fwd_f8_kernel<N, true, false>), g, dim3(256), 0, st, p)
   switch (nkt) {
     case 1: F8(1); break;
     case 2: F8(2); break;
@@ -335,7 +450,9 @@ PDT_API int pdt_attn_fwd_f8_q8(const void* qkv, void* out, float* lse, int B, in
   p.q8 = (uint8_t*)q8; p.q8_meta = q8_meta; p.q8_part = q8_part;
   const int nkt = (T + 31) / 32;
   dim3 g(B * H);
-#define F8(N) hipLaunchKernelGGL((attn_fwd_f8_kernel<N, true>), g, dim3(256), 0, st, p)
+#define F8(N)                                                                         \
+  if (attn_pv8()) hipLaunchKernelGGL((attn_fwd_f8_kernel<N, true, true>), g, dim3(256), 0, st, p); \
+  else hipLaunchKernelGGL((attn_fwd_f8_kernel<N, true, false>), g, dim3(256), 0, st, p)
   switch (nkt) {
     case 1: F8(1); break;
     case 2: F8(2); break;

@@ -109,6 +109,7 @@ _SIGS = {
     "pdt_fp8_meta_seed": (c_int, [P, c_long, c_int, P, P]),
     "pdt_attn_bwd": (c_int, [P, P, P, P, P, P, c_int, c_int, c_int, c_float, P]),
     "pdt_attn_bwd_f8": (c_int, [P, P, P, P, P, c_int, c_int, c_int, c_float, P]),
+    "pdt_attn_set_pv8": (c_int, [c_int]),
     "pdt_attn_bwd_f8_debug": (c_int, [P, P, P, P, P, c_int, c_int, c_int, c_float, P, P]),
     "pdt_lenet_grad_row": (c_int, [c_int]),
     "pdt_lenet_fwd": (c_int, [P] * 9 + [c_int, c_int, c_int, c_float, c_float, c_uint, P, P, P, P]),

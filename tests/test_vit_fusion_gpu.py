@@ -397,15 +397,41 @@ def _fp8_emulated_scores(q, k):
     return qq @ kq.transpose(-1, -2)
 
 
-@pytest.mark.parametrize("bwd", ["f8", "bf16"])
+def _fp8_emulated_pv(s8, v):
+    """O = softmax(S) V as csrc/attention_f8.hip computes it on fp8: keys in pairs of 32-key
+    tiles, running max / rescale per pair, P coded as e4m3(256 exp2(S log2e - m_running)),
+    V per (b, h) power-of-two e4m3, row sums of the fp32 P."""
+    B, H, T, _ = s8.shape
+    sv = _pow2_scale(v.abs().amax(dim=(2, 3), keepdim=True))
+    vq = (v * sv).to(torch.float8_e4m3fn).float() / sv
+    z = s8 / 0.6931471805599453  # log2 domain
+    m = torch.full((B, H, T, 1), -float("inf"), device=s8.device)
+    l = torch.zeros((B, H, T, 1), device=s8.device)
+    o = torch.zeros((B, H, T, 64), device=s8.device)
+    for k0 in range(0, T, 64):
+        zs = z[..., k0:k0 + 64]
+        mn = torch.maximum(m, zs.amax(-1, keepdim=True))
+        alpha = torch.exp2(m - mn)
+        p = torch.exp2(zs - mn)
+        p8 = (p * 256).to(torch.float8_e4m3fn).float() / 256
+        o = o * alpha + p8 @ vq[:, :, k0:k0 + 64]
+        l = l * alpha + p.sum(-1, keepdim=True)
+        m = mn
+    return o / l
+
+
+@pytest.mark.parametrize("bwd,pv8", [("f8", False), ("bf16", False), ("f8", True)])
 @pytest.mark.parametrize("B,T,H", [(3, 197, 4), (2, 64, 2), (1, 50, 12), (2, 256, 3), (2, 16, 3), (1, 120, 2)])
-def test_fp8_attention_forward_and_backward(B, T, H, bwd, monkeypatch):
-    """fp8 score GEMM (csrc/attention_f8.hip): (1) against a reference that applies the
-    kernel's own quantization (per-head K / per-32-query-tile Q power-of-two scales, e4m3)
-    in fp32 -- checks the kernel itself tightly; (2) against exact fp32 attention -- the
+def test_fp8_attention_forward_and_backward(B, T, H, bwd, pv8, monkeypatch):
+    """fp8 attention forward (csrc/attention_f8.hip: e4m3 S = Q K^T and O = P V): (1) against
+    a reference that applies the kernel's own quantization (per-head K / V and per-32-query-
+    tile Q power-of-two scales, P coded per key-tile pair, e4m3) in fp32 -- checks the kernel
+    itself tightly; (2) against exact fp32 attention -- the
     fp8 error budget, with the fused fp8 backward (csrc/attention_bwd_f8.hip, the default
-    for fp8 attention) or the bf16 recomputing one run on its output and LSE."""
+    for fp8 attention) or the bf16 recomputing one run on its output and LSE. ``pv8``: the
+    PV GEMM on e4m3 too (PDT_FP8_ATTN_PV=1; default bf16 PV)."""
     monkeypatch.setenv("PDT_FP8_ATTN_BWD", "1" if bwd == "f8" else "0")
+    no._load().pdt_attn_set_pv8(int(pv8))
     torch.manual_seed(B * 100 + T)
     qkv = (torch.randn(B, T, 3 * H * 64, device="cuda") * 1.5).to(torch.bfloat16)
     dout = torch.randn(B, T, H * 64, device="cuda").to(torch.bfloat16)
@@ -416,10 +442,16 @@ def test_fp8_attention_forward_and_backward(B, T, H, bwd, monkeypatch):
     ref.backward(dout.float())
     with torch.no_grad():
         s8 = _fp8_emulated_scores(q.detach(), k.detach()) / 8.0
-        ref8 = (torch.softmax(s8, dim=-1) @ v.detach()).transpose(1, 2).reshape(B, T, H * 64)
+        if pv8:
+            ref8 = _fp8_emulated_pv(s8, v.detach()).transpose(1, 2).reshape(B, T, H * 64)
+        else:
+            ref8 = (torch.softmax(s8, dim=-1) @ v.detach()).transpose(1, 2).reshape(B, T, H * 64)
         lse8 = torch.logsumexp(s8, dim=-1) / 0.6931471805599453  # log2 domain
     xn = qkv.clone().requires_grad_(True)
-    out = no.qkv_attention(xn, H, fp8=True)
+    try:
+        out = no.qkv_attention(xn, H, fp8=True)
+    finally:
+        no._load().pdt_attn_set_pv8(0)
     lse = out.grad_fn.saved_tensors[2].view(B, H, T)
     e8 = nrmerr(out, ref8)
     dl = (lse - lse8).abs().max().item()
@@ -428,7 +460,9 @@ def test_fp8_attention_forward_and_backward(B, T, H, bwd, monkeypatch):
     torch.cuda.synchronize()
     assert out.shape == ref.shape and out.dtype == torch.bfloat16
     e = nrmerr(out, ref)
-    assert e < 8e-2, e  # fp8 score error budget vs exact attention (measured 0.065 at T=197, x1.5 inputs)
+    # fp8 error budget vs exact attention (x1.5 inputs; the score GEMM's e4m3 error dominates:
+    # 0.065 at T=197 with bf16 PV, round 2)
+    assert e < 9e-2, e
     g, gr = xn.grad.view(B, T, 3, H * 64), x.grad.view(B, T, 3, H * 64)
     for i, name in enumerate("qkv"):
         ei = nrmerr(g[:, :, i], gr[:, :, i])
