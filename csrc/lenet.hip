@@ -72,18 +72,19 @@ struct FwdSmem {
   float z2[MAXNC], lp[MAXNC];  // logits, log-probabilities
 };
 
-// Forward of image b into LDS (all threads participate; ends with a barrier).
-__device__ void lenet_forward(const LeNetArgs& a, int b, FwdSmem& s) {
+// Forward of image b into LDS (all threads participate; ends with a barrier). The conv
+// weights are staged only when `weights` (a workgroup looping over images keeps them).
+__device__ void lenet_forward(const LeNetArgs& a, int b, FwdSmem& s, bool weights = true) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const float* xb = a.x + (size_t)b * IH * IH;
   for (int i = tid; i < IH * IH; i += NT) s.x[i] = xb[i];
-  for (int i = tid; i < C1 * K5 * K5; i += NT) s.w1[i] = a.w1[i];
-  for (int i = tid; i < C2 * C1 * K5 * K5; i += NT) s.w2[i] = a.w2[i];
-  if (tid < C1) s.b1[tid] = a.b1[tid];
-  if (tid < C2) {
-    s.b2[tid] = a.b2[tid];
-    s.keep2[tid] = a.training ? keep_mult(a.seed, b, tid, a.p2) : 1.f;
+  if (weights) {
+    for (int i = tid; i < C1 * K5 * K5; i += NT) s.w1[i] = a.w1[i];
+    for (int i = tid; i < C2 * C1 * K5 * K5; i += NT) s.w2[i] = a.w2[i];
+    if (tid < C1) s.b1[tid] = a.b1[tid];
+    if (tid < C2) s.b2[tid] = a.b2[tid];
   }
+  if (tid < C2) s.keep2[tid] = a.training ? keep_mult(a.seed, b, tid, a.p2) : 1.f;
   if (tid < F1) s.keep1[tid] = a.training ? keep_mult(a.seed, b, 64 + tid, a.p1) : 1.f;
   __syncthreads();
 
@@ -191,14 +192,21 @@ struct BwdSmem {
   float dp1[C1 * P1 * P1];  // pooled-cell gradient of conv1's output (at the argmax position)
 };
 
+// One workgroup per `per` consecutive images: each image's parameter gradient is added into
+// an LDS row (24.6 K floats), written once per workgroup -- at batch 1024 the per-image rows
+// were 89 MB of partials (the fc1 outer products) and the kernel fell behind the stock ops.
 __global__ void __launch_bounds__(NT) lenet_bwd_kernel(LeNetArgs a, const float* __restrict__ dlogp,
-                                                       float* __restrict__ part) {
+                                                       float* __restrict__ part, int per) {
   __shared__ FwdSmem s;
   __shared__ BwdSmem t;
-  const int b = blockIdx.x;
+  __shared__ float pr[grad_row(MAXNC)];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  lenet_forward(a, b, s);
-  float* pr = part + (size_t)b * grad_row(a.NC);
+  const int row = grad_row(a.NC);
+  for (int i = tid; i < row; i += NT) pr[i] = 0.f;
+  for (int img = 0; img < per; ++img) {
+  const int b = blockIdx.x * per + img;
+  if (b >= a.B) break;  // uniform over the workgroup
+  lenet_forward(a, b, s, img == 0);
 
   // log_softmax backward: dz = g - softmax * sum(g)
   if (wave == 0) {
@@ -209,8 +217,8 @@ __global__ void __launch_bounds__(NT) lenet_bwd_kernel(LeNetArgs a, const float*
   __syncthreads();
 
   // fc2: dW = dz2 (x) f1, db = dz2, df1 = W^T dz2 -> through dropout + relu -> dz1
-  for (int e = tid; e < a.NC * F1; e += NT) pr[O_WF2 + e] = t.dz2[e / F1] * s.f1[e % F1];
-  if (tid < a.NC) pr[O_WF2 + a.NC * F1 + tid] = t.dz2[tid];
+  for (int e = tid; e < a.NC * F1; e += NT) pr[O_WF2 + e] += t.dz2[e / F1] * s.f1[e % F1];
+  if (tid < a.NC) pr[O_WF2 + a.NC * F1 + tid] += t.dz2[tid];
   if (tid < F1) {
     float d = 0.f;
     for (int c = 0; c < a.NC; ++c) d = fmaf(a.wf2[(size_t)c * F1 + tid], t.dz2[c], d);
@@ -219,8 +227,8 @@ __global__ void __launch_bounds__(NT) lenet_bwd_kernel(LeNetArgs a, const float*
   __syncthreads();
 
   // fc1: dW = dz1 (x) h2, db = dz1, dh2 = W^T dz1 (coalesced over k for each row j)
-  for (int e = tid; e < F1 * F0; e += NT) pr[O_WF1 + e] = t.dz1[e / F0] * s.h2[e % F0];
-  if (tid < F1) pr[O_BF1 + tid] = t.dz1[tid];
+  for (int e = tid; e < F1 * F0; e += NT) pr[O_WF1 + e] += t.dz1[e / F0] * s.h2[e % F0];
+  if (tid < F1) pr[O_BF1 + tid] += t.dz1[tid];
   for (int k = tid; k < F0; k += NT) {
     float d = 0.f;
     for (int j = 0; j < F1; ++j) d = fmaf(a.wf1[(size_t)j * F0 + k], t.dz1[j], d);
@@ -247,12 +255,12 @@ __global__ void __launch_bounds__(NT) lenet_bwd_kernel(LeNetArgs a, const float*
     for (int oy = 0; oy < H2; ++oy)
 #pragma unroll
       for (int ox = 0; ox < H2; ++ox) acc = fmaf(dc[oy * H2 + ox], h[oy * P1 + ox], acc);
-    pr[O_W2 + e] = acc;
+    pr[O_W2 + e] += acc;
   }
   if (tid < C2) {
     float acc = 0.f;
     for (int q = 0; q < H2 * H2; ++q) acc += t.dc2[tid * H2 * H2 + q];
-    pr[O_B2 + tid] = acc;
+    pr[O_B2 + tid] += acc;
   }
   // conv2 data gradient (full correlation with the flipped kernel), then relu -> pool1
   for (int i = tid; i < C1 * P1 * P1; i += NT) {
@@ -286,13 +294,17 @@ __global__ void __launch_bounds__(NT) lenet_bwd_kernel(LeNetArgs a, const float*
       const int oy = 2 * (q / P1) + (d >> 1), ox = 2 * (q % P1) + (d & 1);
       acc = fmaf(t.dp1[i], s.x[(oy + kh) * IH + ox + kw], acc);
     }
-    pr[O_W1 + e] = acc;
+    pr[O_W1 + e] += acc;
   }
   if (tid < C1) {
     float acc = 0.f;
     for (int q = 0; q < P1 * P1; ++q) acc += t.dp1[tid * P1 * P1 + q];
-    pr[O_B1 + tid] = acc;
+    pr[O_B1 + tid] += acc;
   }
+  __syncthreads();  // the next image overwrites the forward / backward scratch
+  }
+  float* out = part + (size_t)blockIdx.x * row;
+  for (int i = tid; i < row; i += NT) out[i] = pr[i];
 }
 
 // out[j] = sum_b part[b][j] (fixed order: deterministic)
@@ -365,16 +377,19 @@ PDT_API int pdt_lenet_fwd(const float* x, const float* w1, const float* b1, cons
   PDT_RETURN_LAUNCH();
 }
 
-// part: [B][grad_row(NC)] scratch; grads: [grad_row(NC)] flat output (see O_* layout)
+// part: [B][grad_row(NC)] scratch (the first ceil(B / ceil(B / 256)) rows are used); grads:
+// [grad_row(NC)] flat output (see O_* layout)
 PDT_API int pdt_lenet_bwd(const float* x, const float* w1, const float* b1, const float* w2, const float* b2,
                           const float* wf1, const float* bf1, const float* wf2, const float* bf2, int B, int NC,
                           int training, float p2, float p1, unsigned seed, const float* dlogp, float* part,
                           float* grads, hipStream_t st) {
   LeNetArgs a{x, w1, b1, w2, b2, wf1, bf1, wf2, bf2, B, NC, training, p2, p1, seed};
   if (bad_args(a)) return -1;
-  hipLaunchKernelGGL(lenet_bwd_kernel, dim3(B), dim3(NT), 0, st, a, dlogp, part);
+  // one workgroup per CU at most (the LDS gradient row), each looping over `per` images
+  const int per = (B + 255) / 256, nwg = (B + per - 1) / per;
+  hipLaunchKernelGGL(lenet_bwd_kernel, dim3(nwg), dim3(NT), 0, st, a, dlogp, part, per);
   const int row = grad_row(NC);
-  hipLaunchKernelGGL(lenet_grad_reduce_kernel, dim3((row + NT - 1) / NT), dim3(NT), 0, st, part, B, row, grads);
+  hipLaunchKernelGGL(lenet_grad_reduce_kernel, dim3((row + NT - 1) / NT), dim3(NT), 0, st, part, nwg, row, grads);
   PDT_RETURN_LAUNCH();
 }
 

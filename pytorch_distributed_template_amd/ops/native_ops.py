@@ -1174,11 +1174,14 @@ def _ax_select(key, run, run_ref=None):
     return best
 
 
-def _conv3_dgrad_bn_bwd(dout, u3, k1, k2, k3, dy3, u2):
+def _conv3_dgrad_bn_bwd(dout, u3, k1, k2, k3, dy3, u2, side=None):
     """Data gradient of a bottleneck's conv3 (1x1) with bn3's backward apply folded into its A
     staging: A = dy3 = k1*gate(dout) + k2*y3 + k3 (gate: u3's ReLU bit mask), written to ``dy3``
     for the weight gradient; bn2's backward partials in the epilogue (as ``_unit_dx(...,
-    bnb_unit=u2)``). Returns (da2, _BnbPartials) or None when the geometry is not covered."""
+    bnb_unit=u2)``). Returns (da2, _BnbPartials) or None when the geometry is not covered.
+    ``side`` = (ud, b1, b2, b3, dyd): a downsample block's shortcut BN backward, otherwise
+    applied together with bn3's by ``pdt_bn_bwd_apply_dual``; here it runs as its own pass and
+    the tuner compares (fold + that pass) against (dual pass + plain data gradient)."""
     N, Cout, H, W = u3.y.shape
     Cin = u3.C
     if u3.g["KH"] != 1 or u3.g["sh"] != 1 or u3.Cs != Cin or Cout % 64 or u2.Cout != Cin or u3.mask is None:
@@ -1199,13 +1202,30 @@ def _conv3_dgrad_bn_bwd(dout, u3, k1, k2, k3, dy3, u2):
         part = torch.empty(2 * R * Cin, dtype=torch.float32, device=dout.device)
         return _ax_launch(lib, dout, wt, da2, v, a, bnb=bnb(part, R), ax=ax)
 
+    def side_apply():
+        ud, b1, b2, b3, dyd = side
+        _chk(lib.pdt_bn_bwd_apply(_p(dout), _p(ud.y), None, None, None, _p(b1), _p(b2), _p(b3), _p(dyd), None, M,
+                                  Cout, 1, _p(u3.mask), _s()), "bn_bwd_apply (shortcut)")
+
     def run_ref():
-        _chk(lib.pdt_bn_bwd_apply(_p(dout), _p(u3.y), None, None, None, _p(k1), _p(k2), _p(k3), _p(dy3), None, M,
-                                  Cout, 1, _p(u3.mask), _s()), "bn_bwd_apply")
+        if side is None:
+            _chk(lib.pdt_bn_bwd_apply(_p(dout), _p(u3.y), None, None, None, _p(k1), _p(k2), _p(k3), _p(dy3), None,
+                                      M, Cout, 1, _p(u3.mask), _s()), "bn_bwd_apply")
+        else:
+            ud, b1, b2, b3, dyd = side
+            _chk(lib.pdt_bn_bwd_apply_dual(_p(dout), _p(u3.mask), _p(u3.y), _p(k1), _p(k2), _p(k3), _p(dy3),
+                                           _p(ud.y), _p(b1), _p(b2), _p(b3), _p(dyd), M, Cout, _s()),
+                 "bn_bwd_apply_dual")
         _unit_dx(dy3, u3, bnb_unit=u2)
 
-    key = "axb:" + ",".join(str(x) for x in (H, W, Cout, N, Cin))
-    v = _ax_select(key, run, run_ref)
+    def run_tuned(v):
+        rc = run(v)
+        if rc == 0 and side is not None:
+            side_apply()
+        return rc
+
+    key = ("axd:" if side is not None else "axb:") + ",".join(str(x) for x in (H, W, Cout, N, Cin))
+    v = _ax_select(key, run_tuned, run_ref)
     if v < 0:
         return None
     R = lib.pdt_conv_nt_bnb_rows(M, Cin, Cout, v)
@@ -1214,6 +1234,8 @@ def _conv3_dgrad_bn_bwd(dout, u3, k1, k2, k3, dy3, u2):
     if rc == NOT_APPLICABLE:
         return None
     _chk(rc, "conv_nt_ax (bn3 backward apply + conv3 dgrad)")
+    if side is not None:
+        side_apply()
     return da2, _BnbPartials(part, R, u2)
 
 
@@ -1450,12 +1472,17 @@ class _Bottleneck(torch.autograd.Function):
             dgd, dbd, b1, b2, b3 = _bn_bwd(dout, ud, False, mask=u3.mask, coeffs_only=True)
             dy3 = torch.empty_like(u3.y, memory_format=torch.channels_last)
             dyd = torch.empty_like(ud.y, memory_format=torch.channels_last)
-            M3 = u3.N * u3.g["Ho"] * u3.g["Wo"]
-            _chk(_load().pdt_bn_bwd_apply_dual(_p(dout), _p(u3.mask), _p(u3.y), _p(a1), _p(a2), _p(a3), _p(dy3),
-                                               _p(ud.y), _p(b1), _p(b2), _p(b3), _p(dyd), M3, u3.Cout, _s()),
-                 "bn_bwd_apply_dual")
+            fused3 = None
+            if _bnb_enabled() and _ax_enabled():  # bn3's half in conv3's A staging (when it wins)
+                fused3 = _conv3_dgrad_bn_bwd(dout, u3, a1, a2, a3, dy3, u2, side=(ud, b1, b2, b3, dyd))
+            if fused3 is None:
+                M3 = u3.N * u3.g["Ho"] * u3.g["Wo"]
+                _chk(_load().pdt_bn_bwd_apply_dual(_p(dout), _p(u3.mask), _p(u3.y), _p(a1), _p(a2), _p(a3),
+                                                   _p(dy3), _p(ud.y), _p(b1), _p(b2), _p(b3), _p(dyd), M3, u3.Cout,
+                                                   _s()), "bn_bwd_apply_dual")
+        else:
+            fused3 = None
         fuse = _bnb_enabled()
-        fused3 = None
         if not dual and fuse and _ax_enabled() and u3.mask is not None:
             # bn3's backward apply inside conv3's data-gradient A staging (dy3 written once, for
             # the weight gradient): no separate element pass, no re-read of dy3 by the dgrad
