@@ -35,12 +35,17 @@ struct BnbArgs {
 //   mode 1 (forward, the next conv1):  A = relu(src*c1 + c2 + y2)       (src = y3, y2 = residual)
 //                                      y2 term = y2*rsc + rsh when rsc (raw downsample output)
 //                                      dst = the block output, mask_out = its ReLU bit mask
-//          (forward, conv3):           y2 = nullptr: A = relu(src*c1 + c2) (src = y2 of bn2),
-//                                      dst = the conv3 input the weight gradient reads
+//          (forward, conv2 / conv3):   y2 = nullptr: A = relu(src*c1 + c2) (src = the raw conv
+//                                      output of bn1 / bn2), dst = the input the weight gradient reads
+//   mode 3 (backward, conv2's dgrad):  A = c1*gate + c2*y2 + c3, gate = src where y2*rsc + rsh > 0
+//                                      (the ReLU recomputed from the BN input), dst = dy2
+// Any stride-1 geometry with 64-channel k-tiles (3x3 included): dst / mask_out are written
+// from the k-tiles of tap `ctr`, the one that maps every output row onto its own source pixel.
 //   mode 2 (backward, conv3's dgrad):  A = c1*gate(src) + c2*y2 + c3   (src = dout, y2 = y3,
 //                                      gate = mask_in bit), dst = dy3 (the wgrad operand)
 struct AXArgs {
   int mode;
+  int ctr;  // the tap whose A chunks are the source pixels themselves (dst / mask_out written there)
   const u16* y2;
   const float* c1;
   const float* c2;
@@ -196,8 +201,10 @@ __global__ void __launch_bounds__(NTH, PIPE ? 1 : 2) conv_nt_kernel(NTParams p) 
   u32x4 ry[AX ? LA : 1];
   uint32_t rmk[AX ? LA : 1];
   int roff[AX ? LA : 1];
-  float cf1[AX ? 8 : 1], cf2[AX ? 8 : 1], cf3[AX == 2 ? 8 : 1], cfs[AX == 1 ? 8 : 1], cfh[AX == 1 ? 8 : 1];
+  constexpr bool AXC3 = AX == 2 || AX == 3, AXRS = AX == 1 || AX == 3;
+  float cf1[AX ? 8 : 1], cf2[AX ? 8 : 1], cf3[AXC3 ? 8 : 1], cfs[AXRS ? 8 : 1], cfh[AXRS ? 8 : 1];
   const bool ax_write = AX != 0 && p.ax.dst != nullptr && tn == 0;
+  bool ax_wr = false;  // ax_write AND the staged k-tile is the centre tap (set with its fetch)
 
   // AX: this thread's 8 channels' BN coefficients (channel c0..c0+7 of the k-tile)
   auto ax_coef = [&](int c0) __attribute__((always_inline)) {
@@ -208,12 +215,12 @@ __global__ void __launch_bounds__(NTH, PIPE ? 1 : 2) conv_nt_kernel(NTParams p) 
         const f32x4 b = *reinterpret_cast<const f32x4*>(p.ax.c2 + c0 + e);
 #pragma unroll
         for (int q = 0; q < 4; ++q) { cf1[e + q] = a[q]; cf2[e + q] = b[q]; }
-        if constexpr (AX == 2) {
+        if constexpr (AXC3) {
           const f32x4 c = *reinterpret_cast<const f32x4*>(p.ax.c3 + c0 + e);
 #pragma unroll
           for (int q = 0; q < 4; ++q) cf3[e + q] = c[q];
         }
-        if constexpr (AX == 1) {
+        if constexpr (AXRS) {
           const bool raff = p.ax.rsc != nullptr;
           const f32x4 c = raff ? *reinterpret_cast<const f32x4*>(p.ax.rsc + c0 + e) : f32x4{1.f, 1.f, 1.f, 1.f};
           const f32x4 d = raff ? *reinterpret_cast<const f32x4*>(p.ax.rsh + c0 + e) : f32x4{0.f, 0.f, 0.f, 0.f};
@@ -249,7 +256,10 @@ __global__ void __launch_bounds__(NTH, PIPE ? 1 : 2) conv_nt_kernel(NTParams p) 
           rmk[i] = (AX == 2 && ok) ? (uint32_t)p.ax.mask_in[off >> 3] : 0u;
         }
       }
-      if constexpr (AX != 0) ax_coef(c0);
+      if constexpr (AX != 0) {
+        ax_coef(c0);
+        ax_wr = ax_write && tap == p.ax.ctr;
+      }
     } else {
       const int kc = k0 / 8 + ca;  // global 8-channel chunk index
       const bool kin = kc * 8 < p.K;
@@ -302,7 +312,7 @@ __global__ void __launch_bounds__(NTH, PIPE ? 1 : 2) conv_nt_kernel(NTParams p) 
         }
 #pragma unroll
         for (int e = 0; e < 4; ++e) o[e] = pack2bf(f[2 * e], f[2 * e + 1]);
-        if (ax_write && p.ax.mask_out != nullptr) {
+        if (ax_wr && p.ax.mask_out != nullptr) {
           uint32_t m = 0;
 #pragma unroll
           for (int e = 0; e < 4; ++e) {  // mask of the ROUNDED output, as bn_apply_kernel
@@ -314,13 +324,15 @@ __global__ void __launch_bounds__(NTH, PIPE ? 1 : 2) conv_nt_kernel(NTParams p) 
       } else {
 #pragma unroll
         for (int k = 0; k < 8; ++k) {
-          const float g = (rmk[i] >> k) & 1u ? f[k] : 0.f;
+          // mode 2: ReLU gate from the bit mask; mode 3: recomputed as bn_bwd_apply does (y s + b > 0)
+          const bool on = AX == 2 ? ((rmk[i] >> k) & 1u) != 0 : r[k] * cfs[k] + cfh[k] > 0.f;
+          const float g = on ? f[k] : 0.f;
           f[k] = cf1[k] * g + cf2[k] * r[k] + cf3[k];
         }
 #pragma unroll
         for (int e = 0; e < 4; ++e) o[e] = pack2bf(f[2 * e], f[2 * e + 1]);
       }
-      if (ax_write) *reinterpret_cast<u32x4*>(p.ax.dst + roff[i]) = o;
+      if (ax_wr) *reinterpret_cast<u32x4*>(p.ax.dst + roff[i]) = o;
       ra[i] = o;
     }
   };
@@ -346,15 +358,22 @@ __global__ void __launch_bounds__(NTH, PIPE ? 1 : 2) conv_nt_kernel(NTParams p) 
   // rows, RS being a multiple of 16) fetches that chunk's second operand / mask /
   // coefficients into registers alongside the DMA (ax_fetch), then, once the tile is in
   // LDS, rewrites the chunk in place with the applied values (ax_lds) before the MFMAs
-  // read it. 1x1 stride-1 unpadded geometry (host-checked): the k-tile's tap is 0.
+  // read it. 64-channel k-tiles (CS64): each k-tile lies within one tap.
   auto ax_fetch = [&](int kt) __attribute__((always_inline)) {
     if constexpr (AX != 0 && GLDS) {
       static_assert(RS % 16 == 0, "one logical chunk per thread");
-      const int c0 = kt * BK + swz(tid >> 3, ca) * 8;
+      const int k0 = kt * BK;
+      const int tap = k0 / p.Cs;
+      const int c0 = k0 - tap * p.Cs + swz(tid >> 3, ca) * 8;
+      const int th = fdiv(tap, p.div_ntw);
+      const int tw = tap - th * p.ntw;
+      const int dho = p.dh * th, dwo = p.dw * tw;
+      ax_wr = ax_write && tap == p.ax.ctr;
 #pragma unroll
       for (int i = 0; i < LA; ++i) {
-        const bool ok = a_ok[i];
-        const size_t off = (size_t)(a_base[i] + a_ih[i] * p.Ws + a_iw[i]) * p.pix + c0;
+        const int ih = a_ih[i] + dho, iw = a_iw[i] + dwo;
+        const bool ok = a_ok[i] && (unsigned)ih < (unsigned)p.Hs && (unsigned)iw < (unsigned)p.Ws;
+        const size_t off = (size_t)(a_base[i] + ih * p.Ws + iw) * p.pix + c0;
         roff[i] = ok ? (int)off : -1;
         ry[i] = (ok && p.ax.y2 != nullptr) ? *reinterpret_cast<const u32x4*>(p.ax.y2 + off) : u32x4{0, 0, 0, 0};
         rmk[i] = (AX == 2 && ok) ? (uint32_t)p.ax.mask_in[off >> 3] : 0u;

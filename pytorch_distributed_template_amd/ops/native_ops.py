@@ -31,6 +31,7 @@ P = c_void_p
 
 _SIGS = {
     "pdt_conv_nt_ax": (c_int, [P] * 4 + [c_int] * 11 + [P] * 6 + [c_int] * 3 + [c_int] + [P] * 9 + [P]),
+    "pdt_conv_nt_ax2": (c_int, [P] * 4 + [c_int] * 25 + [P] * 6 + [c_int] * 3 + [c_int] + [P] * 9 + [P]),
     "pdt_conv_nt_stat_rows": (c_int, [c_int, c_int, c_int, c_int]),
     "pdt_conv_nt_bnb_rows": (c_int, [c_int, c_int, c_int, c_int]),
     "pdt_conv_nt_num_variants": (c_int, []),
@@ -959,7 +960,7 @@ def _unit_fwd(x, w, gamma, beta, residual, conv, relu, bna: _BNArgs, apply: bool
     ``defer``: skip the BN(+res)+ReLU element pass; the returned output buffer is still
     unwritten (``u.pend`` set) and the NEXT unit that reads it must be called with
     ``src_pend=u`` -- its 1x1 GEMM computes the apply in its A staging and writes the
-    buffer (+ ReLU mask) once (``_conv1x1_fwd_ax``), or the element pass runs first."""
+    buffer (+ ReLU mask) once (``_conv_fwd_ax``), or the element pass runs first."""
     lib = _load()
     st = _s()
     N, C, H, W = x.shape
@@ -979,7 +980,7 @@ def _unit_fwd(x, w, gamma, beta, residual, conv, relu, bna: _BNArgs, apply: bool
     r = None
     if src_pend is not None and getattr(src_pend, "pend", None) is not None:
         assert src_pend.y.shape == x.shape and x.data_ptr() == src_pend.pend[2].data_ptr()
-        r = _conv1x1_fwd_ax(src_pend, x, wb, N, H, W, Cs, Cout, g, bna.training)
+        r = _conv_fwd_ax(src_pend, x, wb, N, H, W, Cs, Cout, g, bna.training)
         if r is None:  # not covered by the AX tiles: the deferred element pass, then the plain GEMM
             _materialize(src_pend)
         src_pend.pend = None
@@ -1155,6 +1156,18 @@ def _time_fn(fn):
 AX_UNFUSED = -2  # tuned-table value: the element pass + the plain GEMM beat every AX tile here
 
 
+def _ax2_launch(lib, src, b, out, v, a, stats=None, bnb=None, ax=None):
+    """``_ax_launch`` for any stride-1 geometry (``a`` as ``_fwd_nt_geom`` / ``_conv_dgrad`` build it)."""
+    bn = bnb if bnb is not None else (None, None, None, None, None, None, 0, 0, 0)
+    mode, y2, c1, c2, c3, rsc, rsh, mki, mko, dst = ax
+    return lib.pdt_conv_nt_ax2(
+        _p(src), _p(b), _p(out), _p(stats), a["Hs"], a["Ws"], a["Cs"], a["Nimg"], a["Hm"], a["Wm"], a["Ncol"], a["K"],
+        a["ldb"], a["sh"], a["sw"], a["oh0"], a["ow0"], a["dh"], a["dw"], a["nth"], a["ntw"], a["Ho"], a["Wo"],
+        a["osh"], a["osw"], a["oph"], a["opw"], a["ldo"], int(v), _p(bn[0]), _p(bn[1]), _p(bn[2]), _p(bn[3]),
+        _p(bn[4]), _p(bn[5]), int(bn[6]), int(bn[7]), int(bn[8]), int(mode), _p(y2), _p(c1), _p(c2), _p(c3), _p(rsc),
+        _p(rsh), _p(mki), _p(mko), _p(dst), _s())
+
+
 def _ax_select(key, run, run_ref=None):
     """Tile for an AX launch (tuned over the AX instantiations on first use when allowed);
     ``run(v)`` launches variant v (with the caller's scratch outputs) and returns its code.
@@ -1257,30 +1270,33 @@ def _apply_pending(u: _Unit):
              "bn_apply")
 
 
-def _conv1x1_fwd_ax(pu: _Unit, xbuf, wb, N, H, W, Cs, Cout, g, with_stats):
-    """Forward 1x1 conv whose A operand is unit ``pu``'s deferred output relu(bn(pu.y) [+ res]),
-    computed in the A staging (AX mode 1) and written to ``xbuf`` (+ pu.mask) on the way.
-    Returns ``_conv_forward``'s (y, M, part, R), or None when the geometry is not covered."""
+def _conv_fwd_ax(pu: _Unit, xbuf, wb, N, H, W, Cs, Cout, g, with_stats):
+    """Forward stride-1 conv (1x1, or 3x3 'same') whose A operand is unit ``pu``'s deferred output
+    relu(bn(pu.y) [+ res]), computed in the A staging (AX mode 1) and written to ``xbuf``
+    (+ pu.mask) on the way. Returns ``_conv_forward``'s (y, M, part, R), or None when the
+    geometry is not covered."""
     res, ru, _ = pu.pend
-    M = N * H * W
-    if g["KH"] != 1 or g["KW"] != 1 or g["sh"] != 1 or g["sw"] != 1 or g["ph"] or g["pw"] or Cs != pu.Cout or \
-            Cs % 64 or Cout % 8 or M * Cs >= 2 ** 31 or not pu.relu:
+    Ho, Wo = g["Ho"], g["Wo"]
+    M = N * Ho * Wo
+    if g["sh"] != 1 or g["sw"] != 1 or Ho != H or Wo != W or Cs != pu.Cout or Cs % 64 or Cout % 8 or \
+            N * H * W * Cs >= 2 ** 31 or not pu.relu:
         return None
     lib = _load()
-    y = _empty_cl(N, Cout, H, W, torch.bfloat16, xbuf.device)
-    a = dict(Hs=H, Ws=W, Cs=Cs, Nimg=N, Hm=H, Wm=W, Ncol=Cout, K=Cs, ldb=Cs, ldo=Cout)
+    y = _empty_cl(N, Cout, Ho, Wo, torch.bfloat16, xbuf.device)
+    a = _fwd_nt_geom(N, H, W, Cs, Cout, g)
+    K = a["K"]
     ax = (1, res, pu.scale, pu.shift, None, ru.scale if ru is not None else None,
           ru.shift if ru is not None else None, None, pu.mask, xbuf)
 
     def stats(v, tail):
         if not with_stats:
             return None, 0
-        R = lib.pdt_conv_nt_stat_rows(M, Cout, Cs, v)
+        R = lib.pdt_conv_nt_stat_rows(M, Cout, K, v)
         ws = lib.pdt_rows_reduce_workspace(R, Cout) if tail else 0
         return torch.empty(2 * R * Cout + ws, dtype=torch.float32, device=xbuf.device), R
 
     def run(v):
-        return _ax_launch(lib, pu.y, wb, y, v, a, stats=stats(v, False)[0], ax=ax)
+        return _ax2_launch(lib, pu.y, wb, y, v, a, stats=stats(v, False)[0], ax=ax)
 
     def run_ref():
         _apply_pending(pu)
@@ -1288,15 +1304,65 @@ def _conv1x1_fwd_ax(pu: _Unit, xbuf, wb, N, H, W, Cs, Cout, g, with_stats):
 
     key = "axf:" + ",".join(str(x) for x in (H, W, Cs, N, Cout, int(res is not None), int(ru is not None),
                                               int(with_stats)))
+    if g["KH"] != 1 or g["KW"] != 1:
+        key += f",k{g['KH']}x{g['KW']}p{g['ph']}"
     v = _ax_select(key, run, run_ref)
     if v < 0:
         return None
     part, R = stats(v, True)
-    rc = _ax_launch(lib, pu.y, wb, y, v, a, stats=part, ax=ax)
+    rc = _ax2_launch(lib, pu.y, wb, y, v, a, stats=part, ax=ax)
     if rc == NOT_APPLICABLE:
         return None
-    _chk(rc, "conv_nt_ax (deferred BN apply + 1x1 conv)")
+    _chk(rc, "conv_nt_ax (deferred BN apply + conv)")
     return y, M, part, R
+
+
+def _conv2_dgrad_bn_bwd(da2, u2, k1, k2, k3, dy2, u1):
+    """Data gradient of a bottleneck's stride-1 conv2 (3x3) with bn2's backward apply folded into
+    its A staging (AX mode 3: dy2 = k1*gate(da2) + k2*y2 + k3, the ReLU gate recomputed from y2
+    as ``pdt_bn_bwd_apply`` does), dy2 written once (centre tap) for the weight gradient; bn1's
+    backward partials in the epilogue. Returns (da1, _BnbPartials) or None (not covered / the
+    element pass + plain data gradient tuned faster)."""
+    g = u2.g
+    N, Cout, Ho, Wo = u2.y.shape
+    Cin = u2.C
+    if g["sh"] != 1 or g["sw"] != 1 or Ho != u2.H or Wo != u2.W or u2.Cs != Cin or Cout % 64 or u1.Cout != Cin or \
+            u2.mask is not None or not u2.relu or N * Ho * Wo * Cout >= 2 ** 31:
+        return None
+    KH, KW, ph, pw = g["KH"], g["KW"], g["ph"], g["pw"]
+    lib = _load()
+    wt = _DGRAD_W.get(u2.w, Cout, KH, KW, Cin, 0, 0, 1, KH, KW)
+    da1 = _empty_cl(N, Cin, u2.H, u2.W, torch.bfloat16, da2.device)
+    a = dict(Hs=Ho, Ws=Wo, Cs=Cout, Nimg=N, Hm=u2.H, Wm=u2.W, Ncol=Cin, K=KH * KW * Cout, ldb=KH * KW * Cout, sh=1,
+             sw=1, oh0=ph, ow0=pw, dh=-1, dw=-1, nth=KH, ntw=KW, Ho=u2.H, Wo=u2.W, osh=1, osw=1, oph=0, opw=0,
+             ldo=Cin)
+    M = N * u2.H * u2.W
+    ax = (3, u2.y, k1, k2, k3, u2.scale, u2.shift, None, None, dy2)
+
+    def bnb(part, R):
+        return (u1.y, u1.mean, u1.scale, u1.shift, None, part, 1, 0, R)
+
+    def run(v):
+        R = lib.pdt_conv_nt_bnb_rows(M, Cin, a["K"], v)
+        part = torch.empty(2 * R * Cin, dtype=torch.float32, device=da2.device)
+        return _ax2_launch(lib, da2, wt, da1, v, a, bnb=bnb(part, R), ax=ax)
+
+    def run_ref():
+        _chk(lib.pdt_bn_bwd_apply(_p(da2), _p(u2.y), None, _p(u2.scale), _p(u2.shift), _p(k1), _p(k2), _p(k3),
+                                  _p(dy2), None, N * Ho * Wo, Cout, 1, None, _s()), "bn_bwd_apply")
+        _unit_dx(dy2, u2, bnb_unit=u1)
+
+    key = "ax3:" + ",".join(str(x) for x in (Ho, Wo, Cout, N, Cin, KH, KW, ph))
+    v = _ax_select(key, run, run_ref)
+    if v < 0:
+        return None
+    R = lib.pdt_conv_nt_bnb_rows(M, Cin, a["K"], v)
+    part = torch.empty(2 * R * Cin + lib.pdt_rows_reduce_workspace(R, Cin), dtype=torch.float32, device=da2.device)
+    rc = _ax2_launch(lib, da2, wt, da1, v, a, bnb=bnb(part, R), ax=ax)
+    if rc == NOT_APPLICABLE:
+        return None
+    _chk(rc, "conv_nt_ax (bn2 backward apply + conv2 dgrad)")
+    return da1, _BnbPartials(part, R, u1)
 
 
 def _unit_dw(dy, u: _Unit):
@@ -1435,18 +1501,20 @@ class _Bottleneck(torch.autograd.Function):
     def forward(ctx, x, blk, has_ds, xpend, defer, holder, *params):
         # xpend: the previous block's unit whose output x is still unwritten (its bn3 apply is
         # computed in conv1's A staging, which writes x); conv1 therefore runs first
+        fold = _ax_enabled()
+        # bn1's apply+ReLU inside conv2's A staging when conv2 is stride 1 (a1 written once, at
+        # the centre tap, for conv2's weight gradient); otherwise materialised before conv2
         a1, u1 = _unit_fwd(x, blk.conv1.weight, blk.bn1.weight, blk.bn1.bias, None, blk.conv1, True,
-                           _BNArgs(blk.bn1), src_pend=xpend)
+                           _BNArgs(blk.bn1), src_pend=xpend, defer=fold)
         if has_ds:  # raw downsample conv output; its BN affine is applied inside bn3's apply
             _, ud = _unit_fwd(x, blk.downsample[0].weight, blk.downsample[1].weight, blk.downsample[1].bias, None,
                               blk.downsample[0], False, _BNArgs(blk.downsample[1]), apply=False)
             idn = ud.y
         else:
             idn, ud = _cl(x.to(torch.bfloat16)), None
-        fold = _ax_enabled()
         # bn2's apply+ReLU inside conv3's A staging (a2 written once, for conv3's weight gradient)
         a2, u2 = _unit_fwd(a1, blk.conv2.weight, blk.bn2.weight, blk.bn2.bias, None, blk.conv2, True,
-                           _BNArgs(blk.bn2), defer=fold)
+                           _BNArgs(blk.bn2), src_pend=u1, defer=fold)
         out, u3 = _unit_fwd(a2, blk.conv3.weight, blk.bn3.weight, blk.bn3.bias, idn, blk.conv3, True,
                             _BNArgs(blk.bn3), res_unit=ud, src_pend=u2, defer=defer and fold)
         if holder is not None:
@@ -1503,8 +1571,21 @@ class _Bottleneck(torch.autograd.Function):
             da2, pre2 = _unit_dx(dy3, u3), None
         wg = _SideWgrad()
         dw3 = wg.dw(dy3, u3)
-        dy2, _, dg2, db2 = _bn_bwd(da2, u2, False, pre=pre2)
-        if fuse:
+        fused2 = None
+        if fuse and _ax_enabled():
+            # bn2's backward apply inside conv2's data gradient (stride-1 conv2; tuned per shape)
+            dg2, db2, c1, c2, c3 = _bn_bwd(da2, u2, False, pre=pre2, coeffs_only=True)
+            dy2 = torch.empty_like(u2.y, memory_format=torch.channels_last)
+            fused2 = _conv2_dgrad_bn_bwd(da2, u2, c1, c2, c3, dy2, u1)
+            if fused2 is None:
+                _chk(_load().pdt_bn_bwd_apply(_p(da2), _p(u2.y), None, _p(u2.scale), _p(u2.shift), _p(c1), _p(c2),
+                                              _p(c3), _p(dy2), None, u2.y.numel() // u2.Cout, u2.Cout, 1, None,
+                                              _s()), "bn_bwd_apply")
+        else:
+            dy2, _, dg2, db2 = _bn_bwd(da2, u2, False, pre=pre2)
+        if fused2 is not None:
+            da1, pre1 = fused2
+        elif fuse:
             da1, pre1 = _unit_dx(dy2, u2, bnb_unit=u1)
         else:
             da1, pre1 = _unit_dx(dy2, u2), None

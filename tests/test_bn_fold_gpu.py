@@ -143,11 +143,17 @@ def _chain():
         memory_format=torch.channels_last)
 
 
+@pytest.mark.parametrize("force", [None, 5, 25])
 @pytest.mark.parametrize("train", [True, False])
-def test_bottleneck_chain_fold_matches_unfolded(monkeypatch, train):
+def test_bottleneck_chain_fold_matches_unfolded(monkeypatch, train, force):
     """Fold on vs off, both against the fp32 stock-op reference of the same chain: the fold
     may flip bf16 roundings (which small-batch BatchNorms re-normalise and the backward
-    amplifies), so the check is that it is no less accurate than the unfolded blocks."""
+    amplifies), so the check is that it is no less accurate than the unfolded blocks.
+    ``force``: every fold site takes AX tile ``force`` (5: register-staged 128x128, 25: the
+    LDS-DMA 128x128) instead of the tuner's choice, so the 1x1 and 3x3 folds (forward modes
+    with and without residual, backward modes 2 and 3) all run whatever the timings say."""
+    if force is not None:
+        monkeypatch.setattr(no, "_ax_select", lambda key, run, run_ref=None: force)
     from pytorch_distributed_template_amd.ops import fused
     torch.manual_seed(11)
     net = _chain()
