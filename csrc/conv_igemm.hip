@@ -361,7 +361,7 @@ static int conv_nt_impl(const void* src, const void* b, void* out, float* stats,
     // the A-staging BN apply: stride-1 source walk, 64-channel k-tiles, dense pixels, 32-bit
     // element offsets into the source
     if (sh != 1 || sw != 1 || p.pix != Cs || Cs % 64 != 0 || bias != nullptr || aux != nullptr || act != 0 ||
-        addend != nullptr || ax.c1 == nullptr || ax.c2 == nullptr ||
+        (addend != nullptr && bnb.part == nullptr) || ax.c1 == nullptr || ax.c2 == nullptr ||
         (ax.mode == 2 && (ax.y2 == nullptr || ax.c3 == nullptr || ax.mask_in == nullptr)) ||
         (ax.mode == 3 && (ax.y2 == nullptr || ax.c3 == nullptr || ax.rsc == nullptr || ax.rsh == nullptr)) ||
         (ax.mode == 1 && ax.y2 == nullptr && ax.rsc != nullptr) ||
@@ -420,7 +420,11 @@ PDT_API int pdt_conv_nt_bnb(const void* src, const void* b, void* out, const voi
 // BN statistics of the output: stats), 2 / 3 = a BN-backward apply (with the fused bn
 // partials of the unit the output feeds: part != 0). NOT_APPLICABLE (-5) for variants
 // without an AX instantiation or geometries it does not cover.
-PDT_API int pdt_conv_nt_ax2(const void* src, const void* b, void* out, float* stats,
+// pdt_conv_nt_ax3: the same with an addend (+ its ReLU bit mask) added in the fused
+// BN-backward epilogue (modes 2 / 3 only): a bottleneck's conv1 data gradient, whose
+// output also carries the shortcut gradient, with bn1's backward apply in its A staging.
+PDT_API int pdt_conv_nt_ax3(const void* src, const void* b, void* out, float* stats, const void* addend,
+                            const void* addend_mask,
                             int Hs, int Ws, int Cs, int Nimg, int Hm, int Wm, int Ncol, int K, int ldb,
                             int sh, int sw, int oh0, int ow0, int dh, int dw, int nth, int ntw,
                             int Ho, int Wo, int osh, int osw, int oph, int opw, int ldo, int variant,
@@ -430,15 +434,31 @@ PDT_API int pdt_conv_nt_ax2(const void* src, const void* b, void* out, float* st
                             const float* ax_c3, const float* ax_rsc, const float* ax_rsh, const void* ax_mask_in,
                             void* ax_mask_out, void* ax_dst, hipStream_t stream) {
   if (ax_mode < 1 || ax_mode > 3) return -8;
+  if (addend != nullptr && (ax_mode == 1 || part == nullptr)) return -8;
   if (part != nullptr && (bn_y == nullptr || bn_mean == nullptr)) return -8;
   if (part != nullptr && relu && bn_mask == nullptr && (bn_scale == nullptr || bn_shift == nullptr)) return -8;
   if ((long long)Nimg * Ho * Wo * ldo >= (1LL << 31)) return -9;
   BnbArgs bnb{(const u16*)bn_y, bn_mean, bn_scale, bn_shift, (const uint8_t*)bn_mask, part, relu, row0, R};
   AXArgs ax{ax_mode, -1, (const u16*)ax_y2, ax_c1, ax_c2, ax_c3, ax_rsc, ax_rsh, (const uint8_t*)ax_mask_in,
             (uint8_t*)ax_mask_out, (u16*)ax_dst};
-  return conv_nt_impl(src, b, out, stats, nullptr, nullptr, nullptr, Hs, Ws, Cs, Nimg, Hm, Wm, Ncol, K, ldb, sh, sw,
-                      oh0, ow0, dh, dw, nth, ntw, Ho, Wo, osh, osw, oph, opw, ldo, 0, nullptr, variant, bnb, 0, stream,
-                      ax);
+  return conv_nt_impl(src, b, out, stats, nullptr, addend, addend_mask, Hs, Ws, Cs, Nimg, Hm, Wm, Ncol, K, ldb, sh,
+                      sw, oh0, ow0, dh, dw, nth, ntw, Ho, Wo, osh, osw, oph, opw, ldo, 0, nullptr, variant, bnb, 0,
+                      stream, ax);
+}
+
+PDT_API int pdt_conv_nt_ax2(const void* src, const void* b, void* out, float* stats,
+                            int Hs, int Ws, int Cs, int Nimg, int Hm, int Wm, int Ncol, int K, int ldb,
+                            int sh, int sw, int oh0, int ow0, int dh, int dw, int nth, int ntw,
+                            int Ho, int Wo, int osh, int osw, int oph, int opw, int ldo, int variant,
+                            const void* bn_y, const float* bn_mean, const float* bn_scale, const float* bn_shift,
+                            const void* bn_mask, float* part, int relu, int row0, int R,
+                            int ax_mode, const void* ax_y2, const float* ax_c1, const float* ax_c2,
+                            const float* ax_c3, const float* ax_rsc, const float* ax_rsh, const void* ax_mask_in,
+                            void* ax_mask_out, void* ax_dst, hipStream_t stream) {
+  return pdt_conv_nt_ax3(src, b, out, stats, nullptr, nullptr, Hs, Ws, Cs, Nimg, Hm, Wm, Ncol, K, ldb, sh, sw, oh0,
+                         ow0, dh, dw, nth, ntw, Ho, Wo, osh, osw, oph, opw, ldo, variant, bn_y, bn_mean, bn_scale,
+                         bn_shift, bn_mask, part, relu, row0, R, ax_mode, ax_y2, ax_c1, ax_c2, ax_c3, ax_rsc, ax_rsh,
+                         ax_mask_in, ax_mask_out, ax_dst, stream);
 }
 
 // the 1x1 form (stride 1, unpadded)

@@ -32,6 +32,7 @@ P = c_void_p
 _SIGS = {
     "pdt_conv_nt_ax": (c_int, [P] * 4 + [c_int] * 11 + [P] * 6 + [c_int] * 3 + [c_int] + [P] * 9 + [P]),
     "pdt_conv_nt_ax2": (c_int, [P] * 4 + [c_int] * 25 + [P] * 6 + [c_int] * 3 + [c_int] + [P] * 9 + [P]),
+    "pdt_conv_nt_ax3": (c_int, [P] * 6 + [c_int] * 25 + [P] * 6 + [c_int] * 3 + [c_int] + [P] * 9 + [P]),
     "pdt_conv_nt_stat_rows": (c_int, [c_int, c_int, c_int, c_int]),
     "pdt_conv_nt_bnb_rows": (c_int, [c_int, c_int, c_int, c_int]),
     "pdt_conv_nt_num_variants": (c_int, []),
@@ -1126,6 +1127,11 @@ def _ax_enabled() -> bool:
     return os.environ.get("PDT_FUSE_BN_AX", "1") != "0"
 
 
+def _conv1_fold_enabled() -> bool:
+    """bn1's backward apply in conv1's data gradient (PDT_FUSE_BN_AX1=0 disables)."""
+    return os.environ.get("PDT_FUSE_BN_AX1", "1") != "0"
+
+
 def _ax_launch(lib, src, b, out, v, a, stats=None, bnb=None, ax=None):
     """One pdt_conv_nt_ax launch. ``bnb`` = (y, mean, scale, shift, mask, part, relu, row0, R) or None;
     ``ax`` = (mode, y2, c1, c2, c3, rsc, rsh, mask_in, mask_out, dst)."""
@@ -1156,12 +1162,13 @@ def _time_fn(fn):
 AX_UNFUSED = -2  # tuned-table value: the element pass + the plain GEMM beat every AX tile here
 
 
-def _ax2_launch(lib, src, b, out, v, a, stats=None, bnb=None, ax=None):
-    """``_ax_launch`` for any stride-1 geometry (``a`` as ``_fwd_nt_geom`` / ``_conv_dgrad`` build it)."""
+def _ax2_launch(lib, src, b, out, v, a, stats=None, bnb=None, ax=None, addend=None, addend_mask=None):
+    """``_ax_launch`` for any stride-1 geometry (``a`` as ``_fwd_nt_geom`` / ``_conv_dgrad`` build it);
+    ``addend`` (+ ``addend_mask``): added in the fused BN-backward epilogue (modes 2 / 3)."""
     bn = bnb if bnb is not None else (None, None, None, None, None, None, 0, 0, 0)
     mode, y2, c1, c2, c3, rsc, rsh, mki, mko, dst = ax
-    return lib.pdt_conv_nt_ax2(
-        _p(src), _p(b), _p(out), _p(stats), a["Hs"], a["Ws"], a["Cs"], a["Nimg"], a["Hm"], a["Wm"], a["Ncol"], a["K"],
+    return lib.pdt_conv_nt_ax3(
+        _p(src), _p(b), _p(out), _p(stats), _p(addend), _p(addend_mask), a["Hs"], a["Ws"], a["Cs"], a["Nimg"], a["Hm"], a["Wm"], a["Ncol"], a["K"],
         a["ldb"], a["sh"], a["sw"], a["oh0"], a["ow0"], a["dh"], a["dw"], a["nth"], a["ntw"], a["Ho"], a["Wo"],
         a["osh"], a["osw"], a["oph"], a["opw"], a["ldo"], int(v), _p(bn[0]), _p(bn[1]), _p(bn[2]), _p(bn[3]),
         _p(bn[4]), _p(bn[5]), int(bn[6]), int(bn[7]), int(bn[8]), int(mode), _p(y2), _p(c1), _p(c2), _p(c3), _p(rsc),
@@ -1317,12 +1324,15 @@ def _conv_fwd_ax(pu: _Unit, xbuf, wb, N, H, W, Cs, Cout, g, with_stats):
     return y, M, part, R
 
 
-def _conv2_dgrad_bn_bwd(da2, u2, k1, k2, k3, dy2, u1):
+def _conv2_dgrad_bn_bwd(da2, u2, k1, k2, k3, dy2, u1, bnb_mask=None, addend=None, addend_mask=None):
     """Data gradient of a bottleneck's stride-1 conv2 (3x3) with bn2's backward apply folded into
     its A staging (AX mode 3: dy2 = k1*gate(da2) + k2*y2 + k3, the ReLU gate recomputed from y2
     as ``pdt_bn_bwd_apply`` does), dy2 written once (centre tap) for the weight gradient; bn1's
     backward partials in the epilogue. Returns (da1, _BnbPartials) or None (not covered / the
-    element pass + plain data gradient tuned faster)."""
+    element pass + plain data gradient tuned faster).
+    The same fold serves conv1's data gradient (``u2`` = the block's conv1 unit, ``u1`` = the
+    previous block's conv3 unit, ``bnb_mask`` = its ReLU bit mask): there the epilogue also adds
+    the shortcut gradient ``addend`` (gated by ``addend_mask``), as ``_unit_dx`` does."""
     g = u2.g
     N, Cout, Ho, Wo = u2.y.shape
     Cin = u2.C
@@ -1338,30 +1348,36 @@ def _conv2_dgrad_bn_bwd(da2, u2, k1, k2, k3, dy2, u1):
              ldo=Cin)
     M = N * u2.H * u2.W
     ax = (3, u2.y, k1, k2, k3, u2.scale, u2.shift, None, None, dy2)
+    if addend is not None:
+        _check_addend(addend, da1, addend_mask, Cin)
+    if bnb_mask is not None:
+        assert bnb_mask.dtype == torch.uint8 and bnb_mask.numel() * 8 == da1.numel()
 
     def bnb(part, R):
-        return (u1.y, u1.mean, u1.scale, u1.shift, None, part, 1, 0, R)
+        return (u1.y, u1.mean, u1.scale, u1.shift, bnb_mask, part, 1, 0, R)
 
     def run(v):
         R = lib.pdt_conv_nt_bnb_rows(M, Cin, a["K"], v)
         part = torch.empty(2 * R * Cin, dtype=torch.float32, device=da2.device)
-        return _ax2_launch(lib, da2, wt, da1, v, a, bnb=bnb(part, R), ax=ax)
+        return _ax2_launch(lib, da2, wt, da1, v, a, bnb=bnb(part, R), ax=ax, addend=addend, addend_mask=addend_mask)
 
     def run_ref():
         _chk(lib.pdt_bn_bwd_apply(_p(da2), _p(u2.y), None, _p(u2.scale), _p(u2.shift), _p(k1), _p(k2), _p(k3),
                                   _p(dy2), None, N * Ho * Wo, Cout, 1, None, _s()), "bn_bwd_apply")
-        _unit_dx(dy2, u2, bnb_unit=u1)
+        _unit_dx(dy2, u2, addend=addend, addend_mask=addend_mask, bnb_unit=u1, bnb_mask=bnb_mask)
 
     key = "ax3:" + ",".join(str(x) for x in (Ho, Wo, Cout, N, Cin, KH, KW, ph))
+    if addend is not None or bnb_mask is not None:
+        key += f",a{int(addend is not None)}{int(addend_mask is not None)}m{int(bnb_mask is not None)}"
     v = _ax_select(key, run, run_ref)
     if v < 0:
         return None
     R = lib.pdt_conv_nt_bnb_rows(M, Cin, a["K"], v)
     part = torch.empty(2 * R * Cin + lib.pdt_rows_reduce_workspace(R, Cin), dtype=torch.float32, device=da2.device)
-    rc = _ax2_launch(lib, da2, wt, da1, v, a, bnb=bnb(part, R), ax=ax)
+    rc = _ax2_launch(lib, da2, wt, da1, v, a, bnb=bnb(part, R), ax=ax, addend=addend, addend_mask=addend_mask)
     if rc == NOT_APPLICABLE:
         return None
-    _chk(rc, "conv_nt_ax (bn2 backward apply + conv2 dgrad)")
+    _chk(rc, "conv_nt_ax (BN backward apply + conv dgrad)")
     return da1, _BnbPartials(part, R, u1)
 
 
@@ -1590,7 +1606,14 @@ class _Bottleneck(torch.autograd.Function):
         else:
             da1, pre1 = _unit_dx(dy2, u2), None
         dw2 = wg.dw(dy2, u2)
-        dy1, _, dg1, db1 = _bn_bwd(da1, u1, False, pre=pre1)
+        prev = ctx.prev() if ctx.prev is not None else None
+        fold1 = fuse and _ax_enabled() and need[0] and prev is not None and prev.mask is not None and \
+            prev.Cout == u1.C and u1.Cs == u1.C and _conv1_fold_enabled()
+        if fold1:  # bn1's backward apply inside conv1's data gradient (below)
+            dg1, db1, e1, e2, e3 = _bn_bwd(da1, u1, False, pre=pre1, coeffs_only=True)
+            dy1 = torch.empty_like(u1.y, memory_format=torch.channels_last)
+        else:
+            dy1, _, dg1, db1 = _bn_bwd(da1, u1, False, pre=pre1)
         grads_ds = ()
         # shortcut gradient = dout * relu_mask(out): never materialised -- the downsample
         # BN backward gates dout with the mask itself, and an identity shortcut is added
@@ -1604,9 +1627,20 @@ class _Bottleneck(torch.autograd.Function):
             grads_ds = (dwd, dgd, dbd)
         else:
             addend, addend_mask = dout, u3.mask
-        prev = ctx.prev() if ctx.prev is not None else None
         dx = None
-        if need[0] and prev is not None and prev.mask is not None and prev.Cout == u1.C and u1.Cs == u1.C:
+        if fold1:
+            r1 = _conv2_dgrad_bn_bwd(da1, u1, e1, e2, e3, dy1, prev, bnb_mask=prev.mask, addend=addend,
+                                     addend_mask=addend_mask)
+            if r1 is not None:
+                dx, pre = r1
+                prev.bnb_pre = (dx.data_ptr(), dx._version, tuple(dx.shape), pre)
+            else:  # not covered / tuned slower: the element pass, then the plain data gradient below
+                _chk(_load().pdt_bn_bwd_apply(_p(da1), _p(u1.y), None, _p(u1.scale), _p(u1.shift), _p(e1), _p(e2),
+                                              _p(e3), _p(dy1), None, u1.y.numel() // u1.Cout, u1.Cout, 1, None,
+                                              _s()), "bn_bwd_apply")
+        if dx is not None:
+            pass
+        elif need[0] and prev is not None and prev.mask is not None and prev.Cout == u1.C and u1.Cs == u1.C:
             # the previous block's bn3 backward partials from this epilogue
             dx, pre = _unit_dx(dy1, u1, addend=addend, addend_mask=addend_mask, bnb_unit=prev, bnb_mask=prev.mask)
             prev.bnb_pre = (dx.data_ptr(), dx._version, tuple(dx.shape), pre)

@@ -196,3 +196,55 @@ def test_bottleneck_chain_fold_matches_unfolded(monkeypatch, train, force):
         assert e1 <= 1.5 * e0 + 5e-3, (i, e1, e0)
     for a, b, r in zip(b1, b0, br):
         assert nrmerr(a, r) <= 1.5 * nrmerr(b, r) + 1e-3
+
+
+def test_ax_mode3_conv1_dgrad_with_addend():
+    """mode 3 on a 1x1 geometry with an addend: a bottleneck's conv1 data gradient with bn1's
+    backward apply in its A staging (ReLU gate recomputed from y1), the shortcut gradient
+    (masked by the block's ReLU bits) added in the epilogue, and the previous block's bn3
+    backward partials (gated by its ReLU bit mask) -- against the element pass followed by
+    the plain fused-epilogue data gradient (``pdt_conv_nt_bnb``), for every AX tile."""
+    torch.manual_seed(5)
+    lib = no._load()
+    N, Cin, C1, H = 6, 256, 64, 14
+    M = N * H * H
+    da1 = _cl(torch.randn(N, C1, H, H, device="cuda").to(torch.bfloat16))
+    y1 = _cl(torch.randn(N, C1, H, H, device="cuda").to(torch.bfloat16))
+    sc1, sh1 = torch.rand(C1, device="cuda") + 0.5, torch.randn(C1, device="cuda") * 0.2
+    k1, k2, k3 = (torch.randn(C1, device="cuda") for _ in range(3))
+    dy_ref = torch.empty_like(y1)
+    no._chk(lib.pdt_bn_bwd_apply(no._p(da1), no._p(y1), None, no._p(sc1), no._p(sh1), no._p(k1), no._p(k2),
+                                 no._p(k3), no._p(dy_ref), None, M, C1, 1, None, no._s()), "apply")
+    w = _cl(torch.randn(C1, Cin, 1, 1, device="cuda") * 0.05)
+    wt = torch.empty(Cin * C1, dtype=torch.bfloat16, device="cuda")
+    no._chk(lib.pdt_wt_dgrad(no._p(w), no._p(wt), C1, 1, 1, Cin, 0, 0, 1, 1, 1, no._s()), "wt")
+    addend = _cl(torch.randn(N, Cin, H, H, device="cuda").to(torch.bfloat16))
+    amask = torch.randint(0, 256, (addend.numel() // 8,), dtype=torch.uint8, device="cuda")
+    yp = _cl(torch.randn(N, Cin, H, H, device="cuda").to(torch.bfloat16))
+    pmask = torch.randint(0, 256, (yp.numel() // 8,), dtype=torch.uint8, device="cuda")
+    mean = torch.randn(Cin, device="cuda") * 0.1
+    a = dict(Hs=H, Ws=H, Cs=C1, Nimg=N, Hm=H, Wm=H, Ncol=Cin, K=C1, ldb=C1, sh=1, sw=1, oh0=0, ow0=0, dh=-1, dw=-1,
+             nth=1, ntw=1, Ho=H, Wo=H, osh=1, osw=1, oph=0, opw=0, ldo=Cin)
+    Rr = lib.pdt_conv_nt_bnb_rows(M, Cin, C1, 0)
+    part_ref = torch.empty(2 * Rr * Cin, device="cuda")
+    out_ref = torch.empty_like(addend)
+    no._chk(lib.pdt_conv_nt_bnb(no._p(dy_ref), no._p(wt), no._p(out_ref), no._p(addend), no._p(amask), H, H, C1, N,
+                                H, H, Cin, C1, C1, 1, 1, 0, 0, -1, -1, 1, 1, H, H, 1, 1, 0, 0, Cin, 0, no._p(yp),
+                                no._p(mean), None, None, no._p(pmask), no._p(part_ref), 1, 0, Rr, no._s()), "bnb ref")
+    sums_ref = part_ref.view(2, Rr, Cin).sum(1)
+    ran = 0
+    for v in no.AX_VARIANTS:
+        R = lib.pdt_conv_nt_bnb_rows(M, Cin, C1, v)
+        part = torch.empty(2 * R * Cin, device="cuda")
+        dy = torch.full_like(y1, float("nan"))
+        out = torch.full_like(addend, float("nan"))
+        rc = no._ax2_launch(lib, da1, wt, out, v, a, bnb=(yp, mean, None, None, pmask, part, 1, 0, R),
+                            ax=(3, y1, k1, k2, k3, sc1, sh1, None, None, dy), addend=addend, addend_mask=amask)
+        if rc == no.NOT_APPLICABLE:
+            continue
+        assert rc == 0, (v, rc)
+        ran += 1
+        assert_one_rounding(dy, dy_ref, v)
+        assert nrmerr(out, out_ref) < 1e-2, v
+        assert nrmerr(part.view(2, R, Cin).sum(1), sums_ref) < 1e-2, v
+    assert ran >= len(no.AX_VARIANTS) - 3
