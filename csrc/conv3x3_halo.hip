@@ -116,7 +116,7 @@ __global__ void __launch_bounds__(NTH, 1) conv3x3_halo_kernel(NTParams p, int rs
     for (int j = 0; j < LB; ++j) {
       const int r = (tid >> 3) + (NTH / 8) * j;
       const void* g = live ? (const void*)(p.b + (size_t)(n0 + r) * K + tap * Cin + cc * 64 + swz(r, tid & 7) * 8)
-                           : (const void*)pdt_zero_chunk;
+                           : p.zero;
       __builtin_amdgcn_global_load_lds(g, (__attribute__((address_space(3))) void*)(sb + (8 * wave + (NTH / 8) * j) * 128),
                                        16, 0, 0);
     }
@@ -136,7 +136,7 @@ __global__ void __launch_bounds__(NTH, 1) conv3x3_halo_kernel(NTParams p, int rs
       const bool ok = live && q < P && g >= 0 && g < NH && w >= 0 && w < W;
       const int ch = (tid & 7) ^ ((q >> 1) & 7);
       const void* src = ok ? (const void*)(p.src + ((size_t)g * W + w) * Cin + cc * 64 + ch * 8)
-                           : (const void*)pdt_zero_chunk;
+                           : p.zero;
       __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)(sp + (8 * wave + GP * l) * 128),
                                        16, 0, 0);
     }
@@ -366,6 +366,7 @@ int run_halo(int hv, const NTParams& p_in, hipStream_t st) {
   if (rc) return rc;
   NTParams p = p_in;
   p.div_HWm = make_fastdiv(p.Hs);  // the kernel divides global rows by H
+  p.zero = zero_chunk_addr();
   switch (hv) {
     case 0: return launch_halo<64, 256>(p, sgn, rs_log2, st);
     case 1: return launch_halo<128, 512>(p, sgn, rs_log2, st);
@@ -397,6 +398,7 @@ struct HWParams {
   const u16* dy;   // [M][Mo]
   const u16* x;    // [M][C] (the conv input; same pixel grid as dY)
   float* slab;     // [splits][Mo][9 * C]
+  const void* zero;  // the LDS-DMA padding source (kernel argument: no per-issue GOT reload)
   int M, Mo, C, H, W, rs_log2, ntiles, tps, nco, ncc;
   FastDiv div_H;
 };
@@ -470,7 +472,7 @@ __global__ void __launch_bounds__(512, 1) wgrad3x3_halo_kernel(HWParams p) {
       const bool ok = live && qq < P && gr >= 0 && gr < NH && w >= 0 && w < W;
       const int ch = (tid & 7) ^ ((qq >> 1) & 7);
       const void* src = ok ? (const void*)(p.x + ((size_t)gr * W + w) * C + cc * 64 + ch * 8)
-                           : (const void*)pdt_nt::pdt_zero_chunk;
+                           : p.zero;
       __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)(sp + (8 * wave + 64 * l) * 128),
                                        16, 0, 0);
     }
@@ -483,7 +485,7 @@ __global__ void __launch_bounds__(512, 1) wgrad3x3_halo_kernel(HWParams p) {
       const int m = m0 + r;
       const int ch = (tid & 7) ^ ((r >> 1) & 7);
       const void* src = (live && m < p.M) ? (const void*)(p.dy + (size_t)m * p.Mo + co0 + ch * 8)
-                                          : (const void*)pdt_nt::pdt_zero_chunk;
+                                          : p.zero;
       __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)(sd + (8 * wave + 64 * l) * 128),
                                        16, 0, 0);
     }
@@ -587,6 +589,7 @@ int run_halo_wgrad(const void* dy, const void* x, float* slab, int M, int Mo, in
   p.dy = (const u16*)dy;
   p.x = (const u16*)x;
   p.slab = slab;
+  p.zero = zero_chunk_addr();
   p.M = M; p.Mo = Mo; p.C = C; p.H = Hs; p.W = Ws;
   int l = 4, rs = 16;
   while (rs < Ws + 2) { rs <<= 1; ++l; }

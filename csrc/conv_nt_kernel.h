@@ -93,6 +93,7 @@ struct NTParams {
   float* q8_part;
   int q8_fmt;          // 0 e4m3, 1 e5m2
   int q8_only;         // 1: the bf16 output itself is not written
+  const void* zero;    // 16 zero bytes in device memory (set by launch(): the LDS-DMA padding source)
 };
 
 constexpr int BK = 64;
@@ -116,6 +117,15 @@ __device__ __forceinline__ i32x8 cat8(const bf16x8& lo, const bf16x8& hi) {
 
 // 16 zero bytes: the global_load_lds source for padding / out-of-range rows
 static __device__ __attribute__((aligned(64))) u32x4 pdt_zero_chunk[4];
+// its device address (host side, resolved once per translation unit)
+static inline const void* zero_chunk_addr() {
+  static const void* a = nullptr;
+  if (a == nullptr) {
+    void* d = nullptr;
+    if (hipGetSymbolAddress(&d, HIP_SYMBOL(pdt_zero_chunk)) == hipSuccess) a = d;
+  }
+  return a;
+}
 
 // F8 = 0: bf16 operands. F8 = 1 / 2: fp8 operands (B = OCP e4m3; src = e4m3 / e5m2)
 // handled as byte PAIRS -- every index below is in 2-byte units, so staging,
@@ -151,6 +161,11 @@ __global__ void __launch_bounds__(NTH, PIPE ? 1 : 2) conv_nt_kernel(NTParams p) 
   const int lane = tid & 63;
   const int wave = tid >> 6;
   const int wm = wave / WN, wn = wave % WN;
+  // the zero page's address comes in the kernel arguments (SGPRs for the whole kernel):
+  // referenced as a symbol, every LDS-DMA issue reloads it through the GOT (s_load +
+  // s_waitcnt lgkmcnt(0)), and that wait also drains the fragment ds_reads the memory
+  // section just issued
+  const void* zchunk = p.zero;
   // tile column of this wave's j-th 16-column block. PIPE 2 gives each wave one 32-column
   // block in each HALF of the tile, so a K-tile's B operand arrives as two contiguous
   // 128-row halves (one per phase pair).
@@ -403,7 +418,7 @@ __global__ void __launch_bounds__(NTH, PIPE ? 1 : 2) conv_nt_kernel(NTParams p) 
     const int k0 = kt * BK;
     const int r = (tid >> 3) + RS * i;
     const int c = swz(r, ca);  // logical chunk for this lane's LDS slot
-    const void* g = pdt_zero_chunk;
+    const void* g = zchunk;
     if constexpr (F8 != 0) {  // the fp8 GEMM's A is a dense [M][K] matrix (pdt_gemm_f8): no gather math
       if (m0 + r < p.M) g = p.src + (size_t)(m0 + r) * p.Cs + k0 + c * 8;
     } else if (CS64) {
@@ -432,7 +447,7 @@ __global__ void __launch_bounds__(NTH, PIPE ? 1 : 2) conv_nt_kernel(NTParams p) 
     const int r = (tid >> 3) + RS * j;
     const int kb = kt * BK + swz(r, ca) * 8;
     const void* g = (b_ok[j] && kb < p.K) ? (const void*)(p.b + (size_t)b_row[j] * p.ldb + kb)
-                                          : (const void*)pdt_zero_chunk;
+                                          : zchunk;
     __builtin_amdgcn_global_load_lds(g, (__attribute__((address_space(3))) void*)(sb + (8 * wave + RS * j) * 128),
                                      16, 0, 0);
   };
@@ -1085,8 +1100,10 @@ template <int BM, int BN, int NS, bool CS64, bool DIRECT, bool GLDS = false, int
           int PIPE = 0, bool BNB = false, int AX = 0>
 int launch(const NTParams& p, hipStream_t st) {
   int ntm = (p.M + BM - 1) / BM, ntn = (p.Ncol + BN - 1) / BN;
+  NTParams q = p;
+  q.zero = zero_chunk_addr();
   hipLaunchKernelGGL((conv_nt_kernel<BM, BN, NS, CS64, DIRECT, GLDS, NTH, WM, F8, PIPE, BNB, AX>),
-                     dim3(ntm * ntn), dim3(NTH), 0, st, p);
+                     dim3(ntm * ntn), dim3(NTH), 0, st, q);
   PDT_RETURN_LAUNCH();
 }
 

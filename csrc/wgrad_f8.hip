@@ -43,6 +43,7 @@ struct WG8Params {
   int M, Mo, No, ldy, ldx;
   int ktiles_per_split;
   int xcd;
+  const void* zero;     // wg8_zero_chunk's address (kernel argument: no per-issue GOT reload)
 };
 
 // physical 16-B chunk of logical chunk c in row r of a RB-byte LDS row
@@ -162,7 +163,7 @@ __global__ void __launch_bounds__(NTH, NTH == 256 && !GL ? 2 : 1) wgrad_f8_kerne
       const int r = i * AROWS + wave * (1024 / RBA) + lane / ACH;
       const int c = chunk_swz<RBA>(r, lane % ACH);  // logical chunk stored at this physical slot
       const int m = k0 + r, co = co0 + c * 16;
-      const void* g = (co < p.Mo && m < p.M) ? (const void*)(p.dy + (size_t)m * p.ldy + co) : (const void*)wg8_zero_chunk;
+      const void* g = (co < p.Mo && m < p.M) ? (const void*)(p.dy + (size_t)m * p.ldy + co) : p.zero;
       __builtin_amdgcn_global_load_lds(
           g, (__attribute__((address_space(3))) void*)(sa + (i * AROWS + wave * (1024 / RBA)) * RBA), 16, 0, 0);
     }
@@ -171,7 +172,7 @@ __global__ void __launch_bounds__(NTH, NTH == 256 && !GL ? 2 : 1) wgrad_f8_kerne
       const int r = i * BROWS + wave * (1024 / RBB) + lane / BCH;
       const int c = chunk_swz<RBB>(r, lane % BCH);
       const int m = k0 + r, tc = tc0 + c * 16;
-      const void* g = (tc < p.No && m < p.M) ? (const void*)(p.x + (size_t)m * p.ldx + tc) : (const void*)wg8_zero_chunk;
+      const void* g = (tc < p.No && m < p.M) ? (const void*)(p.x + (size_t)m * p.ldx + tc) : p.zero;
       __builtin_amdgcn_global_load_lds(
           g, (__attribute__((address_space(3))) void*)(sb + (i * BROWS + wave * (1024 / RBB)) * RBB), 16, 0, 0);
     }
@@ -319,7 +320,14 @@ constexpr WG8Var WG8_VARS[WG8_NVAR] = {
 WG8Var wg8_variant(int v) { return (v < 0 || v >= WG8_NVAR) ? WG8_VARS[0] : WG8_VARS[v]; }
 
 template <bool BIAS>
-void launch8(const WG8Var& w, dim3 grid, const WG8Params& p, hipStream_t st) {
+void launch8(const WG8Var& w, dim3 grid, const WG8Params& p_in, hipStream_t st) {
+  static const void* zaddr = nullptr;
+  if (zaddr == nullptr) {
+    void* d = nullptr;
+    if (hipGetSymbolAddress(&d, HIP_SYMBOL(wg8_zero_chunk)) == hipSuccess) zaddr = d;
+  }
+  WG8Params p = p_in;
+  p.zero = zaddr;
 #define L8(a, b, ns, t, wm) hipLaunchKernelGGL((wgrad_f8_kernel<a, b, ns, t, wm, BIAS>), grid, dim3(t), 0, st, p)
 #define G8(a, b, ns, t, wm) hipLaunchKernelGGL((wgrad_f8_kernel<a, b, ns, t, wm, BIAS, 1, true>), grid, dim3(t), 0, st, p)
   if (w.GL) {
