@@ -140,7 +140,16 @@ __global__ void __launch_bounds__(512) attn_bwd_f8_kernel(AttnBwdF8Params p) {
   constexpr int P_EXP = 8;  // P in [0, 1] -> codes of 256 P
 
   // ---------------------------------------------------------------- phase 1: dK, dV
-  if (wave < NT2) {
+  // A key tile wholly past T (T = 197: keys 224..255) contributes nothing: its wave only
+  // zeroes its rows of the dS^T image (phase 2 reads them, times zero K rows: stale LDS
+  // bytes could hold e4m3 NaN codes) and sets its tiles' unit scales.
+  if (wave < NT2 && 32 * wave >= p.T) {
+    for (int i = lane; i < 32 * ROWS / 16; i += 64) {
+      const int r = i / (ROWS / 16), c = i % (ROWS / 16);
+      *reinterpret_cast<u32x4*>(dSt + (32 * wave + r) * DSR + 16 * c) = u32x4{0u, 0u, 0u, 0u};
+    }
+    if (lane < NT2) tsc[lane * NT2 + wave] = 127;
+  } else if (wave < NT2) {
     const int kt = wave, k0 = 32 * kt;
     const int key = k0 + col;
     const bool kok = key < p.T;
@@ -158,6 +167,12 @@ __global__ void __launch_bounds__(512) attn_bwd_f8_kernel(AttnBwdF8Params p) {
 #pragma unroll
       for (int u = 0; u < 2; ++u) {
         const int qt = 2 * qp + u;
+        if (32 * qt >= p.T) {  // a query tile wholly past T: P = dS = 0 (phase 2 never reads its dS^T columns)
+#pragma unroll
+          for (int w = 0; w < 4; ++w) pc[u][w] = dc[u][w] = 0u;
+          de[u] = 0;
+          continue;
+        }
         const f32x16 z = {};
         // S[q = 32 qt + 8 (r >> 2) + 4 hh + (r & 3)][key]
         const f32x16 s = mfma8(row_frag(Qi, 32 * qt + col, hh), kf, z, dq_q, dq_k);
