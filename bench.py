@@ -9,7 +9,11 @@ Each timed step is a full training step: forward, softmax-cross-entropy,
 backward (DDP bucketed all-reduce over RCCL overlapped with it), optimizer
 step (SGD momentum + weight decay). Nothing is skipped or cached. N = 1 runs
 the same path: a 1-rank RCCL process group and the DDP reducer (``--no-ddp``
-drops both for an A/B).
+drops both for an A/B). On the native GPU path the whole step -- kernels, DDP
+reducer and its RCCL all-reduces -- is captured once as a HIP graph and replayed
+(PyTorch's whole-network DDP capture recipe; at N > 1 a capture + replay of one
+RCCL all-reduce is checked first and the run falls back to eager launches if it
+fails anywhere); ``--eager`` launches kernel by kernel.
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B]
                     [--model resnet50|resnet152|vit_b_16] [--backend native|torch]
@@ -71,7 +75,11 @@ def parse():
     ap.add_argument("--backend", default="native", choices=["native", "torch"])
     ap.add_argument("--bucket-mb", type=float, default=64.0)
     ap.add_argument("--comm-hook", default=None, choices=[None, "bf16"])
-    ap.add_argument("--graph", action="store_true", help="capture the whole training step in a HIP graph")
+    ap.add_argument("--graph", dest="graph", action="store_true", default=None,
+                    help="capture the whole training step (DDP all-reduce included) in one HIP graph; the "
+                         "default on the native GPU path")
+    ap.add_argument("--eager", dest="graph", action="store_false",
+                    help="launch the step's kernels one by one (no HIP graph)")
     ap.add_argument("--json-out", default=None)
     ap.add_argument("--miopen-find", type=int, default=1, choices=[0, 1],
                     help="torch backend: 1 = cudnn.benchmark (MIOpen find), 0 = immediate mode")
@@ -89,8 +97,12 @@ def parse():
     a = ap.parse_args()
     if a.batch is None:
         a.batch = DEFAULT_BATCH.get(a.model, 256)
+    if a.graph is None:
+        # the stock stack stays eager (it is the reference-equivalent baseline); gloo
+        # rehearsals and CPU runs have no capturable collectives
+        a.graph = a.backend == "native" and a.device == "cuda" and a.dist_backend != "gloo"
     if a.device == "cpu":
-        a.backend, a.dist_backend = "torch", "gloo"
+        a.backend, a.dist_backend, a.graph = "torch", "gloo", False
     elif a.image_size != 224:
         ap.error("--image-size is a CPU-rehearsal knob; GPU runs measure 224x224")
     return a
@@ -127,6 +139,44 @@ def launch_ranks(args) -> int | None:
     env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
     env.setdefault("OMP_NUM_THREADS", "4")
     return subprocess.call(cmd, env=env)
+
+
+def graph_collectives_ok(device, world, check_single=False):
+    """Can this job's RCCL collectives be captured in a HIP graph and replayed? Checked before
+    the training step is captured, on a throwaway process group (a failed capture cannot leave
+    the main group's communicator in a bad state): warm one all-reduce eagerly, capture it on a
+    side stream, replay, check the sum; every rank learns the verdict on the main group.
+    World 1 needs no check (the N = 1 step capture itself exercises that path).
+    Returns (ok, reason)."""
+    if world == 1 and not check_single:
+        return True, None
+    import torch.distributed as dist
+    ok, why = 1, None
+    try:
+        pg = dist.new_group(backend="nccl")
+        t = torch.ones(4096, device=device)
+        dist.all_reduce(t, group=pg)
+        torch.cuda.synchronize()
+        side = torch.cuda.Stream()
+        side.wait_stream(torch.cuda.current_stream())
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.stream(side):
+            t.fill_(1.0)
+            with torch.cuda.graph(g, stream=side):
+                dist.all_reduce(t, group=pg)
+        torch.cuda.current_stream().wait_stream(side)
+        t.fill_(1.0)
+        g.replay()
+        torch.cuda.synchronize()
+        if not bool((t == float(world)).all()):
+            ok, why = 0, f"replayed all-reduce returned {t[0].item()} instead of {world}"
+    except Exception as e:  # noqa: BLE001 -- any failure means: run eager
+        ok, why = 0, f"{type(e).__name__}: {e}"
+    flag = torch.tensor([ok], dtype=torch.int32, device=device)
+    dist.all_reduce(flag, op=dist.ReduceOp.MIN)
+    if not bool(flag.item()) and why is None:
+        why = "another rank could not capture its collectives"
+    return bool(flag.item()), why
 
 
 def _rccl_version():
@@ -278,6 +328,13 @@ def main():
     # N ranks: rank 0 tunes the kernel variants once and broadcasts them (no per-rank timing)
     pretune_for_ddp(model, _pretune_step)
     ar = allreduce_probe(model, device, world)
+    graph_fallback = None
+    if args.graph and not args.no_ddp:
+        ok, graph_fallback = graph_collectives_ok(device, world)
+        if not ok:
+            print(f"[bench] HIP-graph capture of the RCCL collectives failed ({graph_fallback}); running eager",
+                  file=sys.stderr, flush=True)
+            args.graph = False
     side = torch.cuda.Stream() if args.graph else None
     if side is not None:  # graph capture of DDP: the reducer is built on the capture side stream
         side.wait_stream(torch.cuda.current_stream())
@@ -399,7 +456,7 @@ def main():
                    "bucket_cap_mb": args.bucket_mb, "dist_backend": (torch.distributed.get_backend() if pdist_ready() else "none (no process group)"),
                    "ddp": type(model).__name__ == "DistributedDataParallel",
                    "rccl_version": _rccl_version(), "device": args.device,
-                   "final_loss": round(final_loss, 4), "hip_graph": args.graph,
+                   "final_loss": round(final_loss, 4), "hip_graph": args.graph, "graph_fallback": graph_fallback,
                    "cpu_issue_ms_per_step": round(cpu_issue / args.steps * 1e3, 3),
                    "host_enqueue_ms_idle_gpu": round(host_enqueue_ms, 3),
                    "baseline": stock_ref,
