@@ -99,8 +99,11 @@ def parse():
         a.batch = DEFAULT_BATCH.get(a.model, 256)
     if a.graph is None:
         # the stock stack stays eager (it is the reference-equivalent baseline); gloo
-        # rehearsals and CPU runs have no capturable collectives
-        a.graph = a.backend == "native" and a.device == "cuda" and a.dist_backend != "gloo"
+        # rehearsals and CPU runs have no capturable collectives; the ViT bench's AdamW takes
+        # its bias corrections as launch arguments, which a replayed graph would freeze at the
+        # capture step, so it stays eager too (SGD's arguments are step-invariant)
+        a.graph = a.backend == "native" and a.device == "cuda" and a.dist_backend != "gloo" and \
+            not a.model.startswith("vit")
     if a.device == "cpu":
         a.backend, a.dist_backend, a.graph = "torch", "gloo", False
     elif a.image_size != 224:
