@@ -99,11 +99,8 @@ def parse():
         a.batch = DEFAULT_BATCH.get(a.model, 256)
     if a.graph is None:
         # the stock stack stays eager (it is the reference-equivalent baseline); gloo
-        # rehearsals and CPU runs have no capturable collectives; the ViT bench's AdamW takes
-        # its bias corrections as launch arguments, which a replayed graph would freeze at the
-        # capture step, so it stays eager too (SGD's arguments are step-invariant)
-        a.graph = a.backend == "native" and a.device == "cuda" and a.dist_backend != "gloo" and \
-            not a.model.startswith("vit")
+        # rehearsals and CPU runs have no capturable collectives
+        a.graph = a.backend == "native" and a.device == "cuda" and a.dist_backend != "gloo"
     if a.device == "cpu":
         a.backend, a.dist_backend, a.graph = "torch", "gloo", False
     elif a.image_size != 224:
@@ -288,12 +285,15 @@ def main():
     from pytorch_distributed_template_amd.optim import FusedAdamW, FusedSGD
     if args.model.startswith("vit"):
         opt_name = "AdamW(lr=1e-3, wd=0.05)"
-        opt = (FusedAdamW if args.backend == "native" else torch.optim.AdamW)(model.parameters(), lr=1e-3,
-                                                                              weight_decay=0.05)
+        # capturable under --graph: lr and Adam's step count in device memory, so every replay
+        # applies the bias corrections of its own step (optim/fused.py)
+        opt = FusedAdamW(model.parameters(), lr=1e-3, weight_decay=0.05, capturable=args.graph) \
+            if args.backend == "native" else torch.optim.AdamW(model.parameters(), lr=1e-3, weight_decay=0.05)
     else:
         opt_name = "SGD(momentum=0.9, wd=5e-5)"
-        opt = (FusedSGD if args.backend == "native" else torch.optim.SGD)(model.parameters(), lr=0.1, momentum=0.9,
-                                                                          weight_decay=5e-5)
+        opt = FusedSGD(model.parameters(), lr=0.1, momentum=0.9, weight_decay=5e-5, capturable=args.graph) \
+            if args.backend == "native" else torch.optim.SGD(model.parameters(), lr=0.1, momentum=0.9,
+                                                             weight_decay=5e-5)
     dtype = "float32" if cpu else "bfloat16"
     if args.data == "pool":
         loader = SyntheticImageLoader(args.batch, num_samples=args.batch * (args.steps + args.warmup + 2) * world,

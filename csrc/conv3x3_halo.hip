@@ -361,6 +361,7 @@ int halo_geometry(const NTParams& p, int hv, int* sgn, int* rs_log2) {
 int halo_rows(int M) { return ((M + HBM - 1) / HBM) * HWM; }
 
 int run_halo(int hv, const NTParams& p_in, hipStream_t st) {
+  if (p_in.bnb.part2 != nullptr) return -5;  // (no second-unit partials in the halo epilogue)
   int sgn = 0, rs_log2 = 0;
   const int rc = halo_geometry(p_in, hv, &sgn, &rs_log2);
   if (rc) return rc;

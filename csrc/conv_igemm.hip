@@ -96,8 +96,11 @@ __global__ void __launch_bounds__(256) gemm_stream_kernel(SParams p) {
   for (int j = 0; j < NJ; ++j)
 #pragma unroll
     for (int r = 0; r < 4; ++r) s[j][r] = q[j][r] = 0.f;
-  // BNB: per-channel mean / ReLU-gate coefficients of this lane's 4 x NJ columns
-  float mu[BNB ? NJ : 1][4], gsc[BNB ? NJ : 1][4], gsh[BNB ? NJ : 1][4];
+  // BNB: per-channel mean / ReLU-gate coefficients of this lane's 4 x NJ columns (and the
+  // second unit's mean / partials when BnbArgs.part2 is set)
+  const bool two = BNB && p.bnb.part2 != nullptr;
+  float mu[BNB ? NJ : 1][4], gsc[BNB ? NJ : 1][4], gsh[BNB ? NJ : 1][4], mu2[BNB ? NJ : 1][4],
+      q2[BNB ? NJ : 1][4];
   if constexpr (BNB) {
 #pragma unroll
     for (int j = 0; j < NJ; ++j)
@@ -105,6 +108,8 @@ __global__ void __launch_bounds__(256) gemm_stream_kernel(SParams p) {
       for (int r = 0; r < 4; ++r) {
         const int c = n0 + j * 16 + (lane >> 4) * 4 + r;
         mu[j][r] = p.bnb.mean[c];
+        mu2[j][r] = two ? p.bnb.mean2[c] : 0.f;
+        q2[j][r] = 0.f;
         const bool from_y = p.bnb.relu && p.bnb.mask == nullptr;
         gsc[j][r] = from_y ? p.bnb.scale[c] : 0.f;
         gsh[j][r] = from_y ? p.bnb.shift[c] : 0.f;
@@ -128,13 +133,14 @@ __global__ void __launch_bounds__(256) gemm_stream_kernel(SParams p) {
     }
     const size_t m = (size_t)t * 16 + lr;
     // epilogue operands of THIS tile issued before its MFMAs (latency hidden behind them)
-    uint2 adv[BNB ? NJ : 1], yyv[BNB ? NJ : 1];
+    uint2 adv[BNB ? NJ : 1], yyv[BNB ? NJ : 1], yyb[BNB ? NJ : 1];
     if constexpr (BNB) {
 #pragma unroll
       for (int j = 0; j < NJ; ++j) {
         const size_t e = m * p.ldo + n0 + j * 16 + (lane >> 4) * 4;
         adv[j] = p.addend != nullptr ? *reinterpret_cast<const uint2*>(p.addend + e) : uint2{0u, 0u};
         yyv[j] = *reinterpret_cast<const uint2*>(p.bnb.y + e);
+        yyb[j] = two ? *reinterpret_cast<const uint2*>(p.bnb.y2 + e) : uint2{0u, 0u};
       }
     }
     f32x4 acc[NJ];
@@ -183,6 +189,10 @@ __global__ void __launch_bounds__(256) gemm_stream_kernel(SParams p) {
           const float g = on ? g0[r] : 0.f;
           s[j][r] += g;
           q[j][r] += g * (yv[r] - mu[j][r]);
+          if (two) {
+            const uint32_t w = r < 2 ? yyb[BNB ? j : 0].x : yyb[BNB ? j : 0].y;
+            q2[BNB ? j : 0][r] += g * ((r & 1 ? hi_bf(w) : lo_bf(w)) - mu2[BNB ? j : 0][r]);
+          }
         }
       }
     }
@@ -200,6 +210,7 @@ __global__ void __launch_bounds__(256) gemm_stream_kernel(SParams p) {
       for (int r = 0; r < 4; ++r) {  // DPP row = the 16 lanes sharing these columns
         s[j][r] = row16_sum(s[j][r]);
         q[j][r] = row16_sum(q[j][r]);
+        if (two) q2[BNB ? j : 0][r] = row16_sum(q2[BNB ? j : 0][r]);
       }
       if (lr == 0) {
         const int col = n0 + j * 16 + (lane >> 4) * 4;
@@ -207,6 +218,10 @@ __global__ void __launch_bounds__(256) gemm_stream_kernel(SParams p) {
         for (int r = 0; r < 4; ++r) {
           part[(size_t)prow * p.N + col + r] = s[j][r];
           part[(size_t)(ptot + prow) * p.N + col + r] = q[j][r];
+          if (two) {
+            p.bnb.part2[(size_t)prow * p.N + col + r] = s[j][r];
+            p.bnb.part2[(size_t)(ptot + prow) * p.N + col + r] = q2[BNB ? j : 0][r];
+          }
         }
       }
     }
@@ -378,6 +393,7 @@ static int conv_nt_impl(const void* src, const void* b, void* out, float* stats,
     }
     return launch_variant_ax(v, p, stream);
   }
+  if (bnb.part2 != nullptr && v >= 34 && v < NVAR) return -5;  // ring tiles: no second-unit partials
   if (v >= HALO0) return run_halo(v - HALO0, p, stream);
   if (v >= NVAR) return run_stream(v - NVAR, p, stream);
   const bool cs64 = (Cs % 64) == 0;
@@ -410,6 +426,28 @@ PDT_API int pdt_conv_nt_bnb(const void* src, const void* b, void* out, const voi
   if ((long long)Nimg * Ho * Wo * ldo >= (1LL << 31)) return -9;  // 32-bit element offsets in the epilogue
   if (relu && bn_mask == nullptr && (bn_scale == nullptr || bn_shift == nullptr)) return -8;
   BnbArgs bnb{(const u16*)bn_y, bn_mean, bn_scale, bn_shift, (const uint8_t*)bn_mask, part, relu, row0, R};
+  return conv_nt_impl(src, b, out, nullptr, nullptr, addend, addend_mask, Hs, Ws, Cs, Nimg, Hm, Wm, Ncol, K, ldb, sh,
+                      sw, oh0, ow0, dh, dw, nth, ntw, Ho, Wo, osh, osw, oph, opw, ldo, 0, nullptr, variant, bnb, 0,
+                      stream);
+}
+
+// The same, also producing the partials of a second unit fed by the same gated gradient
+// (BnbArgs.y2 / mean2 / part2: a downsample block's shortcut BN, gated by the block's ReLU
+// mask like its bn3), part2 laid out like part. The 3x3 halo tiles return NOT_APPLICABLE.
+PDT_API int pdt_conv_nt_bnb2(const void* src, const void* b, void* out, const void* addend, const void* addend_mask,
+                             int Hs, int Ws, int Cs, int Nimg, int Hm, int Wm, int Ncol, int K, int ldb,
+                             int sh, int sw, int oh0, int ow0, int dh, int dw, int nth, int ntw,
+                             int Ho, int Wo, int osh, int osw, int oph, int opw, int ldo, int variant,
+                             const void* bn_y, const float* bn_mean, const float* bn_scale, const float* bn_shift,
+                             const void* bn_mask, float* part, int relu, int row0, int R, const void* bn_y2,
+                             const float* bn_mean2, float* part2, hipStream_t stream) {
+  if (part == nullptr || bn_y == nullptr || bn_mean == nullptr || bn_y2 == nullptr || bn_mean2 == nullptr ||
+      part2 == nullptr)
+    return -8;
+  if ((long long)Nimg * Ho * Wo * ldo >= (1LL << 31)) return -9;
+  if (relu && bn_mask == nullptr && (bn_scale == nullptr || bn_shift == nullptr)) return -8;
+  BnbArgs bnb{(const u16*)bn_y, bn_mean, bn_scale, bn_shift, (const uint8_t*)bn_mask, part, relu, row0, R,
+              (const u16*)bn_y2, bn_mean2, part2};
   return conv_nt_impl(src, b, out, nullptr, nullptr, addend, addend_mask, Hs, Ws, Cs, Nimg, Hm, Wm, Ncol, K, ldb, sh,
                       sw, oh0, ow0, dh, dw, nth, ntw, Ho, Wo, osh, osw, oph, opw, ldo, 0, nullptr, variant, bnb, 0,
                       stream);

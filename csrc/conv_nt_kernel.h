@@ -23,6 +23,12 @@ struct BnbArgs {
   const uint8_t* mask;   // optional ReLU bit mask of the unit's output
   float* part;           // nullptr = disabled
   int relu, row0, R;
+  // optional second unit fed by the SAME gated gradient (a downsample block's shortcut BN,
+  // gated by the block's ReLU mask like bn3): its partials [sum g | sum g * (y2 - mean2)]
+  // go to part2 with part's row layout (sum g is shared, written to both)
+  const u16* y2 = nullptr;
+  const float* mean2 = nullptr;
+  float* part2 = nullptr;
 };
 
 // BatchNorm apply folded into the A-operand staging of a 1x1 GEMM (register-staged
@@ -775,7 +781,9 @@ __global__ void __launch_bounds__(NTH, PIPE ? 1 : 2) conv_nt_kernel(NTParams p) 
     const int colc = cok ? col : 0;
     const bool has_add = p.addend != nullptr, has_amask = p.addend_mask != nullptr;
     const bool has_mask = p.bnb.mask != nullptr, gate_y = p.bnb.relu && !has_mask;
-    float mu[8], sc[8], sh[8], s[8], q[8];
+    // (not in the ring tiles: their 256-VGPR budget spills; the host refuses part2 there)
+    const bool two = PIPE == 0 && p.bnb.part2 != nullptr;
+    float mu[8], sc[8], sh[8], s[8], q[8], mu2[8], q2[8];
     {
       const f32x4 m0v = *reinterpret_cast<const f32x4*>(p.bnb.mean + colc);
       const f32x4 m1v = *reinterpret_cast<const f32x4*>(p.bnb.mean + colc + 4);
@@ -793,13 +801,19 @@ __global__ void __launch_bounds__(NTH, PIPE ? 1 : 2) conv_nt_kernel(NTParams p) 
         sh[k] = h0[k]; sh[k + 4] = h1[k];
       }
 #pragma unroll
-      for (int k = 0; k < 8; ++k) s[k] = q[k] = 0.f;
+      for (int k = 0; k < 8; ++k) s[k] = q[k] = q2[k] = mu2[k] = 0.f;
+      if (two) {
+        const f32x4 a0 = *reinterpret_cast<const f32x4*>(p.bnb.mean2 + colc);
+        const f32x4 a1 = *reinterpret_cast<const f32x4*>(p.bnb.mean2 + colc + 4);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) { mu2[k] = a0[k]; mu2[k + 4] = a1[k]; }
+      }
     }
 #pragma unroll
     for (int it0 = 0; it0 < NIT; it0 += IB) {
       uint32_t eo[IB];
       bool rok[IB];
-      u32x4 yv4[IB], ad4[IB];
+      u32x4 yv4[IB], ad4[IB], yb4[IB];
       uint32_t amb[IB], mkb[IB];
 #pragma unroll
       for (int b = 0; b < IB; ++b) {
@@ -816,6 +830,7 @@ __global__ void __launch_bounds__(NTH, PIPE ? 1 : 2) conv_nt_kernel(NTParams p) 
         }
         eo[b] = orow * (uint32_t)p.ldo + colc;  // host guarantees rows * ldo < 2^31
         yv4[b] = *reinterpret_cast<const u32x4*>(p.bnb.y + eo[b]);
+        yb4[b] = two ? *reinterpret_cast<const u32x4*>(p.bnb.y2 + eo[b]) : u32x4{0u, 0u, 0u, 0u};
         ad4[b] = has_add ? *reinterpret_cast<const u32x4*>(p.addend + eo[b]) : u32x4{0u, 0u, 0u, 0u};
         amb[b] = has_amask ? (uint32_t)p.addend_mask[eo[b] >> 3] : 0xffu;
         mkb[b] = has_mask ? (uint32_t)p.bnb.mask[eo[b] >> 3] : 0xffu;
@@ -846,6 +861,7 @@ __global__ void __launch_bounds__(NTH, PIPE ? 1 : 2) conv_nt_kernel(NTParams p) 
           const float gg = on ? g[k] : 0.f;
           s[k] += gg;
           q[k] += gg * (yf[k] - mu[k]);
+          if (two) q2[k] += gg * ((k & 1 ? hi_bf(yb4[b][k >> 1]) : lo_bf(yb4[b][k >> 1])) - mu2[k]);
         }
       }
     }
@@ -857,35 +873,49 @@ __global__ void __launch_bounds__(NTH, PIPE ? 1 : 2) conv_nt_kernel(NTParams p) 
       for (int k = 0; k < 8; ++k) {
         s[k] += __shfl_xor(s[k], o, 64);
         q[k] += __shfl_xor(q[k], o, 64);
+        if (two) q2[k] += __shfl_xor(q2[k], o, 64);
       }
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
       if constexpr (CPR <= 16) {
         s[k] = xor16_reduce(s[k], AddOp{});
         q[k] = xor16_reduce(q[k], AddOp{});
+        if (two) q2[k] = xor16_reduce(q2[k], AddOp{});
       }
       s[k] = xor32_reduce(s[k], AddOp{});
       q[k] = xor32_reduce(q[k], AddOp{});
+      if (two) q2[k] = xor32_reduce(q2[k], AddOp{});
     }
     constexpr int NW = NTH / 64;
-    float* red = reinterpret_cast<float*>(smem);  // [NW][CPR][16], staging reads are done after the barrier
+    constexpr int RW = PIPE == 0 ? 24 : 16;  // floats per (wave, chunk column): s[8] q[8] (q2[8])
+    float* red = reinterpret_cast<float*>(smem);  // [NW][CPR][RW], staging reads are done after the barrier
     __syncthreads();
     if (lane < CPR) {
 #pragma unroll
       for (int k = 0; k < 8; ++k) {
-        red[(wave * CPR + lane) * 16 + k] = s[k];
-        red[(wave * CPR + lane) * 16 + 8 + k] = q[k];
+        red[(wave * CPR + lane) * RW + k] = s[k];
+        red[(wave * CPR + lane) * RW + 8 + k] = q[k];
+        if (two) red[(wave * CPR + lane) * RW + 16 + k] = q2[k];
       }
     }
     __syncthreads();
     const int srow = p.bnb.row0 + tm;
-    for (int t = tid; t < CPR * 16; t += NTH) {
-      const int c8 = t / 16, k = t % 16;
+    const int nred = two ? 24 : 16;
+    for (int t = tid; t < CPR * nred; t += NTH) {
+      const int c8 = t / nred, k = t % nred;
       float acc_w = 0.f;
 #pragma unroll
-      for (int w = 0; w < NW; ++w) acc_w += red[(w * CPR + c8) * 16 + k];
+      for (int w = 0; w < NW; ++w) acc_w += red[(w * CPR + c8) * RW + k];
       const int cl = n0 + c8 * 8 + (k & 7);
-      if (cl < p.Ncol) p.bnb.part[(size_t)(k < 8 ? srow : p.bnb.R + srow) * p.Ncol + cl] = acc_w;
+      if (cl < p.Ncol) {
+        if (k < 8) {
+          p.bnb.part[(size_t)srow * p.Ncol + cl] = acc_w;
+          if (two) p.bnb.part2[(size_t)srow * p.Ncol + cl] = acc_w;
+        } else {
+          float* dst = k < 16 ? p.bnb.part : p.bnb.part2;
+          dst[(size_t)(p.bnb.R + srow) * p.Ncol + cl] = acc_w;
+        }
+      }
     }
     return;
   }

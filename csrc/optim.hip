@@ -26,7 +26,8 @@ constexpr int NT = 256;
 __global__ void sgd_kernel(const Chunk* __restrict__ chunks, int nchunks, float* const* __restrict__ params,
                            const float* const* __restrict__ grads, float* const* __restrict__ bufs,
                            u16* const* __restrict__ shadows, float lr, float momentum, float dampening, float wd,
-                           int nesterov, int first, float grad_scale) {
+                           int nesterov, int first, float grad_scale, const float* __restrict__ dev) {
+  if (dev != nullptr) lr = dev[0];  // capturable: the lr a replayed graph must not freeze
   // one element: returns the new parameter, updates the momentum buffer value in place
   auto upd = [&](float gi, float pi, float& bi, bool has_b) {
     gi *= grad_scale;
@@ -86,7 +87,12 @@ __global__ void adam_kernel(const Chunk* __restrict__ chunks, int nchunks, float
                             const float* const* __restrict__ grads, float* const* __restrict__ exp_avg,
                             float* const* __restrict__ exp_avg_sq, float* const* __restrict__ max_sq,
                             u16* const* __restrict__ shadows, float lr, float b1, float b2, float eps, float wd,
-                            int decoupled, float bc1, float bc2, float grad_scale) {
+                            int decoupled, float bc1, float bc2, float grad_scale, const float* __restrict__ dev) {
+  if (dev != nullptr) {  // capturable: lr and the step count t live in device memory
+    lr = dev[0];
+    bc1 = 1.f - powf(b1, dev[1]);
+    bc2 = 1.f - powf(b2, dev[1]);
+  }
   const float step_size = lr / bc1;
   const float inv_sqrt_bc2 = 1.f / sqrtf(bc2);
   for (int c = blockIdx.x; c < nchunks; c += gridDim.x) {
@@ -123,25 +129,55 @@ __global__ void adam_kernel(const Chunk* __restrict__ chunks, int nchunks, float
 
 int grid_for(int n) { return n < 2048 ? (n < 1 ? 1 : n) : 2048; }
 
+// capturable Adam: t += 1 on the device, ahead of the step kernel in the same stream
+__global__ void opt_tick_kernel(float* dev) {
+  if (threadIdx.x == 0) dev[1] += 1.f;
+}
+
 }  // namespace
 
 PDT_API int pdt_chunk_struct_size() { return (int)sizeof(Chunk); }
 
+// dev (optional, "capturable"): [lr] for SGD, [lr, t] for Adam in device memory, read by the
+// kernels instead of the lr / bias-correction arguments, so a HIP graph that captured the step
+// replays it with the current learning rate and step count (the host rewrites dev[0] when the
+// lr changes; Adam's t is incremented on the device by opt_tick_kernel when tick != 0).
+PDT_API int pdt_sgd_step2(const void* chunks, int nchunks, void* params, const void* grads, void* bufs, void* shadows,
+                          float lr, float momentum, float dampening, float wd, int nesterov, int first,
+                          float grad_scale, const float* dev, hipStream_t st) {
+  hipLaunchKernelGGL(sgd_kernel, dim3(grid_for(nchunks)), dim3(NT), 0, st, (const Chunk*)chunks, nchunks,
+                     (float* const*)params, (const float* const*)grads, (float* const*)bufs,
+                     (u16* const*)shadows, lr, momentum, dampening, wd, nesterov, first, grad_scale, dev);
+  PDT_RETURN_LAUNCH();
+}
+
 PDT_API int pdt_sgd_step(const void* chunks, int nchunks, void* params, const void* grads, void* bufs, void* shadows,
                          float lr, float momentum, float dampening, float wd, int nesterov, int first,
                          float grad_scale, hipStream_t st) {
-  hipLaunchKernelGGL(sgd_kernel, dim3(grid_for(nchunks)), dim3(NT), 0, st, (const Chunk*)chunks, nchunks,
-                     (float* const*)params, (const float* const*)grads, (float* const*)bufs,
-                     (u16* const*)shadows, lr, momentum, dampening, wd, nesterov, first, grad_scale);
+  return pdt_sgd_step2(chunks, nchunks, params, grads, bufs, shadows, lr, momentum, dampening, wd, nesterov, first,
+                       grad_scale, nullptr, st);
+}
+
+PDT_API int pdt_adam_step2(const void* chunks, int nchunks, void* params, const void* grads, void* exp_avg,
+                           void* exp_avg_sq, void* max_sq, void* shadows, float lr, float b1, float b2, float eps,
+                           float wd, int decoupled, float bc1, float bc2, float grad_scale, float* dev, int tick,
+                           hipStream_t st) {
+  if (tick && dev == nullptr) return -1;
+  if (tick) {
+    hipLaunchKernelGGL(opt_tick_kernel, dim3(1), dim3(64), 0, st, dev);
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return (int)e;
+  }
+  hipLaunchKernelGGL(adam_kernel, dim3(grid_for(nchunks)), dim3(NT), 0, st, (const Chunk*)chunks, nchunks,
+                     (float* const*)params, (const float* const*)grads, (float* const*)exp_avg,
+                     (float* const*)exp_avg_sq, (float* const*)max_sq, (u16* const*)shadows, lr, b1, b2, eps, wd,
+                     decoupled, bc1, bc2, grad_scale, (const float*)dev);
   PDT_RETURN_LAUNCH();
 }
 
 PDT_API int pdt_adam_step(const void* chunks, int nchunks, void* params, const void* grads, void* exp_avg,
                           void* exp_avg_sq, void* max_sq, void* shadows, float lr, float b1, float b2, float eps,
                           float wd, int decoupled, float bc1, float bc2, float grad_scale, hipStream_t st) {
-  hipLaunchKernelGGL(adam_kernel, dim3(grid_for(nchunks)), dim3(NT), 0, st, (const Chunk*)chunks, nchunks,
-                     (float* const*)params, (const float* const*)grads, (float* const*)exp_avg,
-                     (float* const*)exp_avg_sq, (float* const*)max_sq, (u16* const*)shadows, lr, b1, b2, eps, wd,
-                     decoupled, bc1, bc2, grad_scale);
-  PDT_RETURN_LAUNCH();
+  return pdt_adam_step2(chunks, nchunks, params, grads, exp_avg, exp_avg_sq, max_sq, shadows, lr, b1, b2, eps, wd,
+                        decoupled, bc1, bc2, grad_scale, nullptr, 0, st);
 }

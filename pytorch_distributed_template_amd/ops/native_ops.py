@@ -40,6 +40,7 @@ _SIGS = {
     "pdt_conv_nt_resolve_variant": (c_int, [c_int, c_int, c_int, c_int]),
     "pdt_conv_nt": (c_int, [P, P, P, P, P, P, P] + [c_int] * 25 + [P, c_int, c_int, P]),
     "pdt_conv_nt_bnb": (c_int, [P] * 5 + [c_int] * 25 + [P] * 6 + [c_int] * 3 + [P]),
+    "pdt_conv_nt_bnb2": (c_int, [P] * 5 + [c_int] * 25 + [P] * 6 + [c_int] * 3 + [P] * 3 + [P]),
     "pdt_ln_fwd": (c_int, [P, P, P, P, P, P, c_int, c_int, c_float, P]),
     "pdt_gemm_f8_q8": (c_int, [P] * 6 + [c_int] * 8 + [P, P, c_int, P, P, P, c_int, c_int, P, P]),
     "pdt_gemm_f8_q8_part": (c_long, [c_int, c_int]),
@@ -83,6 +84,9 @@ _SIGS = {
     "pdt_chunk_struct_size": (c_int, []),
     "pdt_sgd_step": (c_int, [P, c_int, P, P, P, P, c_float, c_float, c_float, c_float, c_int, c_int, c_float, P]),
     "pdt_adam_step": (c_int, [P, c_int, P, P, P, P, P, P] + [c_float] * 5 + [c_int, c_float, c_float, c_float, P]),
+    "pdt_sgd_step2": (c_int, [P, c_int, P, P, P, P, c_float, c_float, c_float, c_float, c_int, c_int, c_float, P, P]),
+    "pdt_adam_step2": (c_int, [P, c_int, P, P, P, P, P, P] + [c_float] * 5 + [c_int, c_float, c_float, c_float, P,
+                                                                            c_int, P]),
     "pdt_fill_uniform_bf16": (c_int, [P, c_long, c_uint, P]),
     "pdt_cast_f32_bf16": (c_int, [P, P, c_long, P]),
     "pdt_synth_images_bf16": (c_int, [P, P, c_long, c_int, c_int, c_int, c_uint, P, c_int, P]),
@@ -790,23 +794,35 @@ _DGRAD_W = _DgradWeights()
 
 class _BnbPartials:
     """BatchNorm-backward partial sums produced by a data-gradient epilogue for one
-    unit (see ``BnbArgs`` in csrc/conv_igemm.hip): [2][R][C] fp32 (+ rows_reduce tail)."""
-    __slots__ = ("part", "R", "unit")
+    unit (see ``BnbArgs`` in csrc/conv_igemm.hip): [2][R][C] fp32 (+ rows_reduce tail).
+    ``second``: the same epilogue's partials for a second unit fed by the same gated
+    gradient (a downsample block's shortcut BN), or None."""
+    __slots__ = ("part", "R", "unit", "second")
 
-    def __init__(self, part, R, unit):
-        self.part, self.R, self.unit = part, R, unit
+    def __init__(self, part, R, unit, second=None):
+        self.part, self.R, self.unit, self.second = part, R, unit, second
 
 
 def _bnb_enabled() -> bool:
     return os.environ.get("PDT_FUSE_BN_BWD", "1") != "0"
 
 
-def _conv_dgrad(dy, w32, N, H, W, Cin, Cout, g, addend=None, addend_mask=None, bnb_unit=None, bnb_mask=None):
+def _bnb2_enabled() -> bool:
+    """A downsample block's shortcut-BN backward partials in the next block's data-gradient
+    epilogue (PDT_FUSE_BN_BWD2=0: its own reduce pass over dout and the shortcut output)."""
+    return os.environ.get("PDT_FUSE_BN_BWD2", "1") != "0"
+
+
+def _conv_dgrad(dy, w32, N, H, W, Cin, Cout, g, addend=None, addend_mask=None, bnb_unit=None, bnb_mask=None,
+                bnb_unit2=None):
     """dX [N,Cin,H,W] (+ addend) from dY [N,Cout,Ho,Wo] (stride phases, see csrc/conv_igemm.hip).
 
     ``bnb_unit``: the conv->BN(->ReLU) unit whose output dX is the gradient of; its
     BatchNorm-backward reduction (gated by its ReLU -- ``bnb_mask`` or recomputed
-    from y) is computed in the GEMM epilogue. Returns ``(dx, _BnbPartials)`` then."""
+    from y) is computed in the GEMM epilogue. Returns ``(dx, _BnbPartials)`` then.
+    ``bnb_unit2``: a second unit fed by the same gated gradient (``bnb_mask`` required),
+    whose partials the same epilogue also produces (``_BnbPartials.second``; None where
+    the tuned tile cannot)."""
     KH, KW, s_h, s_w, ph, pw = g["KH"], g["KW"], g["sh"], g["sw"], g["ph"], g["pw"]
     assert w32.shape[0] == Cout and w32.shape[1] == Cin, (tuple(w32.shape), Cout, Cin)
     assert dy.shape[1] == Cout and dy.numel() == N * Cout * g["Ho"] * g["Wo"]
@@ -852,12 +868,14 @@ def _conv_dgrad(dy, w32, N, H, W, Cin, Cout, g, addend=None, addend_mask=None, b
     if bnb_mask is not None:
         assert bnb_mask.dtype == torch.uint8 and bnb_mask.numel() * 8 == dx.numel()
 
-    def launch(wt, a, v, part, row0, R):
-        return lib.pdt_conv_nt_bnb(
-            _p(dy), _p(wt), _p(dx), _p(addend), _p(addend_mask), a["Hs"], a["Ws"], a["Cs"], a["Nimg"], a["Hm"],
-            a["Wm"], a["Ncol"], a["K"], a["ldb"], a["sh"], a["sw"], a["oh0"], a["ow0"], a["dh"], a["dw"], a["nth"],
-            a["ntw"], a["Ho"], a["Wo"], a["osh"], a["osw"], a["oph"], a["opw"], a["ldo"], int(v), _p(u.y),
-            _p(u.mean), _p(u.scale), _p(u.shift), _p(bnb_mask), _p(part), int(relu), int(row0), int(R), _s())
+    def launch(wt, a, v, part, row0, R, part2=None):
+        args = (_p(dy), _p(wt), _p(dx), _p(addend), _p(addend_mask), a["Hs"], a["Ws"], a["Cs"], a["Nimg"], a["Hm"],
+                a["Wm"], a["Ncol"], a["K"], a["ldb"], a["sh"], a["sw"], a["oh0"], a["ow0"], a["dh"], a["dw"], a["nth"],
+                a["ntw"], a["Ho"], a["Wo"], a["osh"], a["osw"], a["oph"], a["opw"], a["ldo"], int(v), _p(u.y),
+                _p(u.mean), _p(u.scale), _p(u.shift), _p(bnb_mask), _p(part), int(relu), int(row0), int(R))
+        if part2 is None:
+            return lib.pdt_conv_nt_bnb(*args, _s())
+        return lib.pdt_conv_nt_bnb2(*args, _p(u2.y), _p(u2.mean), _p(part2), _s())
 
     plan, R = [], 0
     for wt, a in launches:
@@ -867,10 +885,30 @@ def _conv_dgrad(dy, w32, N, H, W, Cin, Cout, g, addend=None, addend_mask=None, b
         rows = lib.pdt_conv_nt_bnb_rows(a["Nimg"] * a["Hm"] * a["Wm"], Cin, a["K"], v)
         plan.append((wt, a, v, R))
         R += rows
-    part = torch.empty(2 * R * Cin + lib.pdt_rows_reduce_workspace(R, Cin), dtype=torch.float32, device=dy.device)
+    u2 = bnb_unit2
+    if u2 is not None and (bnb_mask is None or u2.Cout != Cin or u2.y.shape != u.y.shape or
+                           not u2.y.is_contiguous(memory_format=torch.channels_last)):
+        u2 = None
+    one = 2 * R * Cin + lib.pdt_rows_reduce_workspace(R, Cin)
+    if u2 is None:
+        part = torch.empty(one, dtype=torch.float32, device=dy.device)
+        for wt, a, v, row0 in plan:
+            _chk(launch(wt, a, v, part, row0, R), "conv_nt_bnb")
+        return dx, _BnbPartials(part, R, u)
+    # both units' [2][R][C] blocks (+ their reduce tails) in one buffer, the second 256-B aligned
+    off = (one + 63) // 64 * 64
+    buf = torch.empty(off + one, dtype=torch.float32, device=dy.device)
+    part, part2 = buf[:one], buf[off:]
+    second = True
     for wt, a, v, row0 in plan:
-        _chk(launch(wt, a, v, part, row0, R), "conv_nt_bnb")
-    return dx, _BnbPartials(part, R, u)
+        rc = launch(wt, a, v, part, row0, R, part2 if second else None)
+        if rc == NOT_APPLICABLE and second:  # tuned tile without the second-unit epilogue
+            second = False
+            for wt_, a_, v_, row0_ in plan:  # redo every phase launch without it
+                _chk(launch(wt_, a_, v_, part, row0_, R), "conv_nt_bnb")
+            break
+        _chk(rc, "conv_nt_bnb2")
+    return dx, _BnbPartials(part, R, u, _BnbPartials(part2, R, u2) if second else None)
 
 
 _NTB_KEYS: dict = {}
@@ -936,7 +974,7 @@ class _BNArgs:
 class _Unit:
     """Saved state of one conv->BN->act unit between forward and backward."""
     __slots__ = ("x", "w", "gamma", "y", "act", "mask", "mean", "invstd", "scale", "shift", "N", "C", "Cs", "H",
-                 "W", "Cout", "g", "relu", "has_res", "bnb_pre", "pend", "__weakref__")
+                 "W", "Cout", "g", "relu", "has_res", "bnb_pre", "pend", "res_unit", "__weakref__")
 
 
 def nhwc_padded_view(x, cp):
@@ -1003,7 +1041,7 @@ def _unit_fwd(x, w, gamma, beta, residual, conv, relu, bna: _BNArgs, apply: bool
     if not apply:  # the consumer applies the BN affine (+ReLU) itself (stem max-pool)
         u = _Unit()
         u.x, u.w, u.gamma, u.y = x, w, gamma, y
-        u.act, u.mask, u.bnb_pre, u.pend = None, None, None, None
+        u.act, u.mask, u.bnb_pre, u.pend, u.res_unit = None, None, None, None, None
         u.mean, u.invstd, u.scale, u.shift = mean, invstd, scale, shift
         u.N, u.C, u.Cs, u.H, u.W, u.Cout, u.g, u.relu, u.has_res = N, C, Cs, H, W, Cout, g, relu, False
         return None, u
@@ -1031,6 +1069,7 @@ def _unit_fwd(x, w, gamma, beta, residual, conv, relu, bna: _BNArgs, apply: bool
     u.x, u.w, u.gamma, u.y = x, w, gamma, y
     u.act = None
     u.mask = mask
+    u.res_unit = res_unit  # the downsample unit whose raw output is this unit's residual (or None)
     u.bnb_pre = None
     u.mean, u.invstd, u.scale, u.shift = mean, invstd, scale, shift
     u.N, u.C, u.Cs, u.H, u.W, u.Cout, u.g, u.relu, u.has_res = N, C, Cs, H, W, Cout, g, relu, residual is not None
@@ -1103,7 +1142,7 @@ def _bn_bwd_pool(dout, idx, u: _Unit, k, s, p):
     return dy, dgamma, dbeta
 
 
-def _unit_dx(dy, u: _Unit, addend=None, addend_mask=None, bnb_unit=None, bnb_mask=None):
+def _unit_dx(dy, u: _Unit, addend=None, addend_mask=None, bnb_unit=None, bnb_mask=None, bnb_unit2=None):
     """Data gradient of unit ``u``'s conv. With ``bnb_unit`` (the unit whose output
     this gradient flows into) returns ``(dx, _BnbPartials)``."""
     wd = u.w
@@ -1111,7 +1150,7 @@ def _unit_dx(dy, u: _Unit, addend=None, addend_mask=None, bnb_unit=None, bnb_mas
         wd = torch.nn.functional.pad(u.w.detach().float(), (0, 0, 0, 0, 0, u.Cs - u.C))
         assert addend is None and bnb_unit is None
     dx = _conv_dgrad(dy, wd, u.N, u.H, u.W, u.Cs, u.Cout, u.g, addend=addend, addend_mask=addend_mask,
-                     bnb_unit=bnb_unit, bnb_mask=bnb_mask)
+                     bnb_unit=bnb_unit, bnb_mask=bnb_mask, bnb_unit2=bnb_unit2)
     return dx[:, :u.C] if u.Cs != u.C else dx
 
 
@@ -1548,12 +1587,16 @@ class _Bottleneck(torch.autograd.Function):
         u1, u2, u3, ud = ctx.units
         need = ctx.needs_input_grad
         dout = _cl(dout.to(torch.bfloat16))
+        # bn3's backward partials from the next block's data-gradient epilogue (and, in a
+        # downsample block, the shortcut BN's from the same epilogue: same gated gradient)
+        pre3 = _take_bnb(u3, dout)
+        pre_d = pre3.second if (pre3 is not None and pre3.second is not None and pre3.second.unit is ud) else None
         dual = ctx.has_ds and u3.mask is not None and os.environ.get("PDT_BN_DUAL_APPLY", "1") == "1"
         if dual:
             # both BN backwards fed by dout (bn3 and the shortcut's BN): coefficients first, then
             # ONE apply pass that reads dout and the ReLU mask once and writes both gradients
-            dg3, db3, a1, a2, a3 = _bn_bwd(dout, u3, False, pre=_take_bnb(u3, dout), coeffs_only=True)
-            dgd, dbd, b1, b2, b3 = _bn_bwd(dout, ud, False, mask=u3.mask, coeffs_only=True)
+            dg3, db3, a1, a2, a3 = _bn_bwd(dout, u3, False, pre=pre3, coeffs_only=True)
+            dgd, dbd, b1, b2, b3 = _bn_bwd(dout, ud, False, mask=u3.mask, pre=pre_d, coeffs_only=True)
             dy3 = torch.empty_like(u3.y, memory_format=torch.channels_last)
             dyd = torch.empty_like(ud.y, memory_format=torch.channels_last)
             fused3 = None
@@ -1570,7 +1613,7 @@ class _Bottleneck(torch.autograd.Function):
         if not dual and fuse and _ax_enabled() and u3.mask is not None:
             # bn3's backward apply inside conv3's data-gradient A staging (dy3 written once, for
             # the weight gradient): no separate element pass, no re-read of dy3 by the dgrad
-            dg3, db3, k1, k2, k3 = _bn_bwd(dout, u3, False, pre=_take_bnb(u3, dout), coeffs_only=True)
+            dg3, db3, k1, k2, k3 = _bn_bwd(dout, u3, False, pre=pre3, coeffs_only=True)
             dy3 = torch.empty_like(u3.y, memory_format=torch.channels_last)
             fused3 = _conv3_dgrad_bn_bwd(dout, u3, k1, k2, k3, dy3, u2)
             if fused3 is None:  # not covered: the element pass
@@ -1578,7 +1621,7 @@ class _Bottleneck(torch.autograd.Function):
                                               _p(k3), _p(dy3), None, u3.y.numel() // u3.Cout, u3.Cout, 1,
                                               _p(u3.mask), _s()), "bn_bwd_apply")
         elif not dual:
-            dy3, _, dg3, db3 = _bn_bwd(dout, u3, False, pre=_take_bnb(u3, dout))
+            dy3, _, dg3, db3 = _bn_bwd(dout, u3, False, pre=pre3)
         if fused3 is not None:
             da2, pre2 = fused3
         elif fuse:  # bn2 / bn1 backward reductions in the epilogues of the conv3 / conv2 dgrads
@@ -1621,7 +1664,7 @@ class _Bottleneck(torch.autograd.Function):
         addend_mask = None
         if ctx.has_ds:
             if not dual:
-                dyd, _, dgd, dbd = _bn_bwd(dout, ud, False, mask=u3.mask)
+                dyd, _, dgd, dbd = _bn_bwd(dout, ud, False, mask=u3.mask, pre=pre_d)
             addend = _unit_dx(dyd, ud) if need[0] else None
             dwd = wg.dw(dyd, ud)
             grads_ds = (dwd, dgd, dbd)
@@ -1641,8 +1684,10 @@ class _Bottleneck(torch.autograd.Function):
         if dx is not None:
             pass
         elif need[0] and prev is not None and prev.mask is not None and prev.Cout == u1.C and u1.Cs == u1.C:
-            # the previous block's bn3 backward partials from this epilogue
-            dx, pre = _unit_dx(dy1, u1, addend=addend, addend_mask=addend_mask, bnb_unit=prev, bnb_mask=prev.mask)
+            # the previous block's bn3 backward partials from this epilogue (and its shortcut
+            # BN's, when it is a downsample block)
+            dx, pre = _unit_dx(dy1, u1, addend=addend, addend_mask=addend_mask, bnb_unit=prev, bnb_mask=prev.mask,
+                               bnb_unit2=prev.res_unit if _bnb2_enabled() else None)
             prev.bnb_pre = (dx.data_ptr(), dx._version, tuple(dx.shape), pre)
         elif need[0]:
             dx = _unit_dx(dy1, u1, addend=addend, addend_mask=addend_mask)
@@ -2819,6 +2864,8 @@ class _TargetCheck:
         self.pending = []  # (event, pinned host tensor)
 
     def record(self, bad: torch.Tensor):
+        if _capturing():  # inside a HIP-graph capture: no host copies / events (the NaN loss remains)
+            return
         if os.environ.get("PDT_CHECK_TARGETS", "lazy") == "sync":
             n = float(bad.item())
             if n:
@@ -2831,6 +2878,8 @@ class _TargetCheck:
         self.pending.append((ev, host))
 
     def poll(self):
+        if _capturing():
+            return
         keep = []
         for ev, host in self.pending:
             if not ev.query():

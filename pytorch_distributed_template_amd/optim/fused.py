@@ -13,6 +13,14 @@ tables only when a tensor moved (asynchronously, from pinned memory: nothing in
 ``step()`` blocks the host) and each step is a single launch that also writes the
 bf16 shadow copy of each parameter that the conv/GEMM kernels consume. On CPU
 (gloo plumbing) the step falls back to torch's reference implementation.
+
+``capturable=True`` (what a HIP-graph training step needs, cf. torch's capturable
+Adam): the learning rate and Adam's step count live in a small device tensor per
+param group that the kernels read, so a captured ``step()`` replays with the
+current lr (the host rewrites it, outside the graph, in ``refresh_scalars()`` --
+called by every eager ``step()`` too) and with the bias corrections of the current
+step (t is incremented on the device, in the graph). ``state_dict()`` writes the
+device step count back into each parameter's ``step`` so checkpoints stay torch's.
 """
 from __future__ import annotations
 
@@ -100,11 +108,44 @@ def _native_ok(params):
 
 
 class _FusedBase(Optimizer):
-    def __init__(self, params, defaults, write_bf16_shadow=True):
+    def __init__(self, params, defaults, write_bf16_shadow=True, capturable=False):
         super().__init__(params, defaults)
         self.write_bf16_shadow = write_bf16_shadow
+        self.capturable = bool(capturable)
         self._plans = {}
         self._shadows = {}
+        self._dev = {}      # capturable: group index -> device [lr, t]
+        self._dev_lr = {}   # the lr last written into it
+
+    def _dev_scalars(self, gi, group, device, t0=0.0):
+        """The group's device [lr, t] (created from the host values on first use)."""
+        d = self._dev.get(gi)
+        if d is None:
+            d = torch.tensor([float(group["lr"]), float(t0)], dtype=torch.float32, device=device)
+            self._dev[gi] = d
+            self._dev_lr[gi] = float(group["lr"])
+        return d
+
+    def refresh_scalars(self):
+        """Write each group's current lr into its device scalars (capturable mode): call it
+        before replaying a graph that captured ``step()`` -- an LR scheduler changes only the
+        host value. A no-op for groups whose lr did not change (and outside capturable mode)."""
+        if not self.capturable:
+            return
+        for gi, group in enumerate(self.param_groups):
+            d = self._dev.get(gi)
+            if d is not None and self._dev_lr.get(gi) != float(group["lr"]):
+                d[0].fill_(float(group["lr"]))
+                self._dev_lr[gi] = float(group["lr"])
+
+    def _step_prologue(self):
+        if self.capturable and not torch.cuda.is_current_stream_capturing():
+            self.refresh_scalars()
+
+    def load_state_dict(self, state_dict):
+        super().load_state_dict(state_dict)
+        self._dev.clear()  # rebuilt from the loaded lr / step on the next step()
+        self._dev_lr.clear()
 
     def _shadow(self, p):
         if not self.write_bf16_shadow:
@@ -135,10 +176,10 @@ class FusedSGD(_FusedBase):
     """torch.optim.SGD semantics (momentum, dampening, nesterov, weight_decay)."""
 
     def __init__(self, params, lr=0.1, momentum=0.0, dampening=0.0, weight_decay=0.0, nesterov=False,
-                 write_bf16_shadow=True):
+                 write_bf16_shadow=True, capturable=False):
         defaults = dict(lr=lr, momentum=momentum, dampening=dampening, weight_decay=weight_decay,
                         nesterov=nesterov)
-        super().__init__(params, defaults, write_bf16_shadow)
+        super().__init__(params, defaults, write_bf16_shadow, capturable)
 
     @torch.no_grad()
     def step(self, closure=None):
@@ -146,6 +187,7 @@ class FusedSGD(_FusedBase):
         if closure is not None:
             with torch.enable_grad():
                 loss = closure()
+        self._step_prologue()
         for gi, group in enumerate(self.param_groups):
             params = [p for p in group["params"] if p.grad is not None]
             if not params:
@@ -173,12 +215,14 @@ class FusedSGD(_FusedBase):
             roles = {"p": params, "g": grads, "b": bufs if group["momentum"] != 0 else [None] * len(params),
                      "s": shadows if self.write_bf16_shadow else [None] * len(params)}
             plan = self._plan(gi, params, roles, params[0].device)
-            rc = native_ops._load().pdt_sgd_step(
+            dev = self._dev_scalars(gi, group, params[0].device) if self.capturable else None
+            rc = native_ops._load().pdt_sgd_step2(
                 plan.chunks.data_ptr(), plan.nchunks, plan.ptr("p"), plan.ptr("g"),
                 plan.ptr("b") if group["momentum"] != 0 else None,
                 plan.ptr("s") if self.write_bf16_shadow else None,
                 float(group["lr"]), float(group["momentum"]), float(group["dampening"]),
-                float(group["weight_decay"]), int(group["nesterov"]), int(first), 1.0, self._stream())
+                float(group["weight_decay"]), int(group["nesterov"]), int(first), 1.0,
+                dev.data_ptr() if dev is not None else None, self._stream())
             native_ops._chk(rc, "sgd_step")
             _bump_versions(params)
             if self.write_bf16_shadow:
@@ -208,9 +252,23 @@ class FusedAdam(_FusedBase):
     decoupled = False
 
     def __init__(self, params, lr=1e-3, betas=(0.9, 0.999), eps=1e-8, weight_decay=0.0, amsgrad=False,
-                 write_bf16_shadow=True):
+                 write_bf16_shadow=True, capturable=False):
         defaults = dict(lr=lr, betas=tuple(betas), eps=eps, weight_decay=weight_decay, amsgrad=amsgrad)
-        super().__init__(params, defaults, write_bf16_shadow)
+        super().__init__(params, defaults, write_bf16_shadow, capturable)
+
+    def state_dict(self):
+        """torch's format; in capturable mode each parameter's ``step`` is first set from the
+        group's device step count (replayed graphs advance only that)."""
+        if self.capturable:
+            for gi, group in enumerate(self.param_groups):
+                d = self._dev.get(gi)
+                if d is None:
+                    continue
+                t = float(d[1].item())
+                for p in group["params"]:
+                    if p in self.state and "step" in self.state[p]:
+                        self.state[p]["step"] = torch.tensor(t)
+        return super().state_dict()
 
     @torch.no_grad()
     def step(self, closure=None):
@@ -218,11 +276,14 @@ class FusedAdam(_FusedBase):
         if closure is not None:
             with torch.enable_grad():
                 loss = closure()
+        self._step_prologue()
         for gi, group in enumerate(self.param_groups):
             params = [p for p in group["params"] if p.grad is not None]
             if not params:
                 continue
             b1, b2 = group["betas"]
+            native = _native_ok(params)
+            dev_step = self.capturable and native
             for p in params:
                 st = self.state[p]
                 if len(st) == 0:
@@ -231,11 +292,12 @@ class FusedAdam(_FusedBase):
                     st["exp_avg_sq"] = torch.zeros_like(p, memory_format=torch.preserve_format)
                     if group["amsgrad"]:
                         st["max_exp_avg_sq"] = torch.zeros_like(p, memory_format=torch.preserve_format)
-                st["step"] += 1
-            step = float(self.state[params[0]]["step"])
+                if not dev_step:  # (capturable: the device count is the step, see state_dict)
+                    st["step"] += 1
+            step = float(self.state[params[0]]["step"]) if not dev_step else 1.0
             bc1 = 1 - b1 ** step
             bc2 = 1 - b2 ** step
-            if not _native_ok(params):
+            if not native:
                 self._torch_step(group, params, bc1, bc2)
                 continue
             from ..ops import native_ops
@@ -250,11 +312,14 @@ class FusedAdam(_FusedBase):
                      else [None] * len(params),
                      "s": shadows if self.write_bf16_shadow else [None] * len(params)}
             plan = self._plan(gi, params, roles, params[0].device)
-            rc = native_ops._load().pdt_adam_step(
+            dev = self._dev_scalars(gi, group, params[0].device, t0=float(self.state[params[0]]["step"])) \
+                if dev_step else None
+            rc = native_ops._load().pdt_adam_step2(
                 plan.chunks.data_ptr(), plan.nchunks, plan.ptr("p"), plan.ptr("g"), plan.ptr("m"), plan.ptr("v"),
                 plan.ptr("vm") if group["amsgrad"] else None, plan.ptr("s") if self.write_bf16_shadow else None,
                 float(group["lr"]), float(b1), float(b2), float(group["eps"]), float(group["weight_decay"]),
-                int(self.decoupled), float(bc1), float(bc2), 1.0, self._stream())
+                int(self.decoupled), float(bc1), float(bc2), 1.0, dev.data_ptr() if dev is not None else None,
+                int(dev is not None), self._stream())
             native_ops._chk(rc, "adam_step")
             _bump_versions(params)
             if self.write_bf16_shadow:
@@ -287,5 +352,5 @@ class FusedAdamW(FusedAdam):
     decoupled = True
 
     def __init__(self, params, lr=1e-3, betas=(0.9, 0.999), eps=1e-8, weight_decay=1e-2, amsgrad=False,
-                 write_bf16_shadow=True):
-        super().__init__(params, lr, betas, eps, weight_decay, amsgrad, write_bf16_shadow)
+                 write_bf16_shadow=True, capturable=False):
+        super().__init__(params, lr, betas, eps, weight_decay, amsgrad, write_bf16_shadow, capturable)

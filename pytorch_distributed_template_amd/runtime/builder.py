@@ -14,7 +14,9 @@ Registries (``init_obj`` lookups, searched in order):
 Extra (optional) ``trainer`` keys, all defaulting to reference behaviour:
   precision "fp32"|"bf16", channels_last bool, backend "auto"|"native"|"torch",
   ddp {bucket_cap_mb, broadcast_buffers, gradient_as_bucket_view, comm_hook},
-  len_epoch int (iteration-based epochs), log_images bool, fused_optimizer bool.
+  len_epoch int (iteration-based epochs), log_images bool, fused_optimizer bool,
+  hip_graph bool (capture the training step -- DDP all-reduce included -- as one HIP
+  graph after a warm-up and replay it; needs a fused optimizer, built capturable).
 """
 from __future__ import annotations
 
@@ -67,9 +69,14 @@ def build_optimizer(config, model):
             and set(ocfg.get("args", {})) <= allowed and fused.use_native(params[0])):
         # fp32-only models (LeNet) read no bf16 weight shadow
         optimizer = getattr(module_optim, fused_name)(params, **dict(ocfg.get("args", {})),
-                                                      write_bf16_shadow=config["trainer"].get("precision") == "bf16")
+                                                      write_bf16_shadow=config["trainer"].get("precision") == "bf16",
+                                                      capturable=bool(config["trainer"].get("hip_graph", False)))
     else:
-        optimizer = config.init_obj("optimizer", [module_optim, torch.optim], params)
+        extra = {}
+        if config["trainer"].get("hip_graph", False) and str(ocfg["type"]).startswith("Fused") \
+                and "capturable" not in ocfg.get("args", {}):
+            extra["capturable"] = True  # (optim.Fused*: lr / step counts in device memory)
+        optimizer = config.init_obj("optimizer", [module_optim, torch.optim], params, **extra)
     lr_scheduler = None
     if config.get("lr_scheduler"):
         lr_scheduler = config.init_obj("lr_scheduler", torch.optim.lr_scheduler, optimizer)
@@ -78,12 +85,25 @@ def build_optimizer(config, model):
 
 def wrap_model(config, model, device):
     ddp_cfg = dict(config["trainer"].get("ddp", {}))
-    return wrap_ddp(model, device,
-                    bucket_cap_mb=ddp_cfg.get("bucket_cap_mb", 64),
-                    broadcast_buffers=ddp_cfg.get("broadcast_buffers", True),
-                    gradient_as_bucket_view=ddp_cfg.get("gradient_as_bucket_view", True),
-                    comm_hook=ddp_cfg.get("comm_hook"),
-                    find_unused_parameters=ddp_cfg.get("find_unused_parameters", False))
+
+    def wrap():
+        return wrap_ddp(model, device,
+                        bucket_cap_mb=ddp_cfg.get("bucket_cap_mb", 64),
+                        broadcast_buffers=ddp_cfg.get("broadcast_buffers", True),
+                        gradient_as_bucket_view=ddp_cfg.get("gradient_as_bucket_view", True),
+                        comm_hook=ddp_cfg.get("comm_hook"),
+                        find_unused_parameters=ddp_cfg.get("find_unused_parameters", False))
+
+    if config["trainer"].get("hip_graph", False) and device.type == "cuda":
+        # PyTorch's whole-network DDP capture recipe: the reducer is built on a side stream
+        # (the Trainer runs its warm-up steps and the capture on that stream too)
+        side = torch.cuda.Stream(device=device)
+        side.wait_stream(torch.cuda.current_stream(device))
+        with torch.cuda.stream(side):
+            model = wrap()
+        torch.cuda.current_stream(device).wait_stream(side)
+        return model
+    return wrap()
 
 
 def pretune_model(config, model, data_loader, criterion, device):

@@ -20,7 +20,13 @@ MI355X-first changes to the hot loop:
   * ``len_epoch`` is honoured exactly (the reference ran ``len_epoch+1`` steps);
   * validation computes a real ``val_loss`` (the reference's was always 0 -- Q1)
     and gathers *unpadded* per-rank predictions as fixed-shape tensors;
-  * throughput (images/sec, whole job) is measured per epoch with device syncs.
+  * throughput (images/sec, whole job) is measured per epoch with device syncs;
+  * ``trainer.hip_graph``: after ``GRAPH_WARMUP`` eager steps (DDP samples its runtime
+    stats over the first 10 iterations) the whole step -- zero_grad, forward, loss,
+    backward with DDP's RCCL all-reduces, the fused optimizer -- is captured once as a
+    HIP graph and replayed for every later full-size batch (copied into the graph's
+    static input buffers); the optimizer is capturable, so replays use the scheduler's
+    current lr and Adam's current step. Partial batches and validation run eagerly.
 """
 from __future__ import annotations
 
@@ -33,6 +39,10 @@ from ..base.base_trainer import BaseTrainer
 from ..utils import MetricTracker, inf_loop
 from ..utils import dist as pdist
 from ..utils.profiling import PhaseTimer
+
+
+GRAPH_WARMUP = 11  # eager steps before the capture (DDP's runtime statistics cover iterations 1..10)
+
 
 
 class Trainer(BaseTrainer):
@@ -61,6 +71,16 @@ class Trainer(BaseTrainer):
         # optional per-phase device timing (HIP events + ROCTx ranges): trainer.profile_phases
         self.phase_timer = PhaseTimer(enabled=bool(config["trainer"].get("profile_phases", False))
                                       and device.type == "cuda")
+        # HIP-graph step (trainer.hip_graph): needs a capturable fused optimizer
+        self.hip_graph = bool(config["trainer"].get("hip_graph", False)) and device.type == "cuda"
+        if self.hip_graph and not getattr(optimizer, "capturable", False):
+            self.logger.warning("trainer.hip_graph needs a capturable fused optimizer (optim.Fused*, "
+                                "trainer.fused_optimizer); training eagerly")
+            self.hip_graph = False
+        self._graph = None
+        self._graph_io = None  # (static data, static target, static loss)
+        self._graph_eager_steps = 0
+        self._side = torch.cuda.Stream(device=device) if self.hip_graph else None
 
     # ------------------------------------------------------------------ helpers
     def _on_epoch_start(self, epoch):
@@ -102,15 +122,18 @@ class Trainer(BaseTrainer):
                 n_images = 0
             data, target = self._to_device(data, target)
 
-            pt = self.phase_timer
-            self.optimizer.zero_grad(set_to_none=True)
-            with pt.phase("forward"), self._autocast():
-                output = self.model(data)
-                loss = self.criterion(output, target)
-            with pt.phase("backward"):
-                loss.backward()
-            with pt.phase("optimizer"):
-                self.optimizer.step()
+            if self.hip_graph:
+                loss = self._graph_step(data, target)
+            else:
+                pt = self.phase_timer
+                self.optimizer.zero_grad(set_to_none=True)
+                with pt.phase("forward"), self._autocast():
+                    output = self.model(data)
+                    loss = self.criterion(output, target)
+                with pt.phase("backward"):
+                    loss.backward()
+                with pt.phase("optimizer"):
+                    self.optimizer.step()
 
             loss_sum += loss.detach().float()
             n_iter += 1
@@ -152,6 +175,60 @@ class Trainer(BaseTrainer):
         if self.lr_scheduler is not None:
             self.lr_scheduler.step()
         return log
+
+    # ------------------------------------------------------------------ HIP graph
+    def _step_body(self, data, target):
+        # grads stay allocated (set_to_none=False): the captured kernels write fixed addresses
+        self.optimizer.zero_grad(set_to_none=False)
+        with self._autocast():
+            output = self.model(data)
+            loss = self.criterion(output, target)
+        loss.backward()
+        self.optimizer.step()
+        return loss
+
+    def _graph_step(self, data, target):
+        """One training step in ``trainer.hip_graph`` mode: eager (on the capture side
+        stream) during the warm-up and for batches whose shape differs from the captured
+        one; the capture right after the warm-up (it records the step without running it:
+        the batch is then replayed like every later one); a replay otherwise."""
+        cur = torch.cuda.current_stream(self.device)
+        side = self._side
+        if self._graph is None and self._graph_eager_steps >= GRAPH_WARMUP:
+            side.wait_stream(cur)
+            with torch.cuda.stream(side):
+                self._capture(data, target)
+            cur.wait_stream(side)
+        io = self._graph_io
+        if self._graph is not None and io[0].shape == data.shape and io[1].shape == target.shape:
+            io[0].copy_(data)
+            io[1].copy_(target)
+            self.optimizer.refresh_scalars()  # the scheduler's lr (written outside the graph)
+            self._graph.replay()
+            return io[2]
+        side.wait_stream(cur)
+        with torch.cuda.stream(side):
+            loss = self._step_body(data, target)
+        cur.wait_stream(side)
+        self._graph_eager_steps += 1
+        return loss
+
+    def _capture(self, data, target):
+        from ..ops.native_ops import nhwc_padded_view
+        gx = data.clone()
+        if getattr(data, "pdt_nhwc_pad", None):  # keep the padded-NHWC view the native stem reads in place
+            cp = data.pdt_nhwc_pad
+            buf = nhwc_padded_view(data, cp).clone(memory_format=torch.channels_last)
+            gx = buf[:, :data.shape[1]]
+            gx.pdt_nhwc_pad = cp
+        gy = target.clone()
+        self.optimizer.refresh_scalars()
+        graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(graph, stream=self._side):
+            gloss = self._step_body(gx, gy)
+        self._graph, self._graph_io = graph, (gx, gy, gloss)
+        self.logger.info("captured the training step as a HIP graph after {} eager steps".format(
+            self._graph_eager_steps))
 
     # ------------------------------------------------------------------ validate
     @torch.no_grad()

@@ -248,3 +248,46 @@ def test_ax_mode3_conv1_dgrad_with_addend():
         assert nrmerr(out, out_ref) < 1e-2, v
         assert nrmerr(part.view(2, R, Cin).sum(1), sums_ref) < 1e-2, v
     assert ran >= len(no.AX_VARIANTS) - 3
+
+
+class _FakeUnit:
+    def __init__(self, y, mean, scale=None, shift=None, relu=True):
+        self.y, self.mean, self.scale, self.shift, self.relu = y, mean, scale, shift, relu
+        self.Cout = y.shape[1]
+
+
+@pytest.mark.parametrize("v", [5, 15, 25, 27, 38, 40, 37])
+def test_dgrad_epilogue_second_unit_partials(monkeypatch, v):
+    """A data-gradient epilogue producing the BN-backward partials of TWO units fed by the
+    same ReLU-gated gradient (a downsample block's bn3 and shortcut BN): both partial sets
+    against fp32 sums over the stored gradient; variant 37 (a ring tile) falls back to
+    the single-unit epilogue (second = None)."""
+    torch.manual_seed(v)
+    N, Cin, Cm, H = 4, 256, 64, 14
+    dy = _cl(torch.randn(N, Cm, H, H, device="cuda").to(torch.bfloat16))
+    w = _cl(torch.randn(Cm, Cin, 1, 1, device="cuda") * 0.05)
+    y3 = _cl(torch.randn(N, Cin, H, H, device="cuda").to(torch.bfloat16))
+    yd = _cl(torch.randn(N, Cin, H, H, device="cuda").to(torch.bfloat16))
+    m3, md = torch.randn(Cin, device="cuda") * 0.1, torch.randn(Cin, device="cuda") * 0.1
+    mask = torch.randint(0, 256, (y3.numel() // 8,), dtype=torch.uint8, device="cuda")
+    u3, ud = _FakeUnit(y3, m3), _FakeUnit(yd, md, relu=False)
+    monkeypatch.setattr(no, "_select_bnb_variant", lambda *a, **k: v)
+    g = {"KH": 1, "KW": 1, "sh": 1, "sw": 1, "ph": 0, "pw": 0, "Ho": H, "Wo": H}
+    dx, pre = no._conv_dgrad(dy, w, N, H, H, Cin, Cm, g, bnb_unit=u3, bnb_mask=mask, bnb_unit2=ud)
+    torch.cuda.synchronize()
+    ref = torch.nn.functional.conv2d(dy.float(), w.to(torch.bfloat16).float().transpose(0, 1))
+    assert nrmerr(dx, ref) < 1e-2
+    bits = torch.stack([(mask >> k) & 1 for k in range(8)], 1).reshape(-1).bool()
+    gate = dx.float().permute(0, 2, 3, 1).reshape(-1, Cin) * bits.view(-1, Cin)
+    s_ref = gate.sum(0)
+    q3_ref = (gate * (y3.float().permute(0, 2, 3, 1).reshape(-1, Cin) - m3)).sum(0)
+    qd_ref = (gate * (yd.float().permute(0, 2, 3, 1).reshape(-1, Cin) - md)).sum(0)
+    R = pre.R
+    p3 = pre.part[:2 * R * Cin].view(2, R, Cin).sum(1)
+    assert nrmerr(p3[0], s_ref) < 1e-3 and nrmerr(p3[1], q3_ref) < 1e-3
+    if v == 37:
+        assert pre.second is None
+        return
+    assert pre.second is not None and pre.second.unit is ud
+    pd = pre.second.part[:2 * R * Cin].view(2, R, Cin).sum(1)
+    assert nrmerr(pd[0], s_ref) < 1e-3 and nrmerr(pd[1], qd_ref) < 1e-3
