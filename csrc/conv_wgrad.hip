@@ -50,6 +50,11 @@ struct WGParams {
   int xcd;           // 1: XCD-aware block mapping (PDT_WGRAD_XCD=0 disables, for A/B runs)
   float* bslab;      // optional [splits][Mo]: per-split column sums of dY (nn.Linear bias gradient),
                      // accumulated by the tn == 0 blocks from the dY tiles they stage anyway
+  // BNA instantiations: `dy` is dA, the gradient at a BN+ReLU unit's output, and the unit's
+  // BatchNorm backward apply is computed while staging it (no dy tensor is written):
+  //   dY = k1 * (y*scale + shift > 0 ? dA : 0) + k2 * y + k3   (csrc/bn_act.hip bn_bwd_apply)
+  const u16* bn_y;   // [M][ldy] the unit's pre-BN conv output
+  const float* bn_c; // [5][Mo]: k1, k2, k3, scale, shift
   FastDiv div_Wm, div_HWm, div_C, div_ntw;
 };
 
@@ -96,8 +101,9 @@ __device__ __forceinline__ bf16x8 tr_frag(const char* base, int krow0, int col0,
 // of tile k+3 are issued right after tile k's barrier and land in LDS two
 // compute phases later (PF = 1: one), so a workgroup keeps ~2x the bytes in
 // flight -- the large weight gradients are load-latency bound otherwise.
-template <int BM, int BN, int NSTAGE, int NTH = NT, int WM = 2, int PF = 1, bool BIAS = false>
+template <int BM, int BN, int NSTAGE, int NTH = NT, int WM = 2, int PF = 1, bool BIAS = false, bool BNA = false>
 __global__ void __launch_bounds__(NTH, NTH == NT ? 2 : 1) wgrad_kernel(WGParams p) {
+  static_assert(!BNA || (PF == 1 && !BIAS), "the staged BN-backward apply: single register slot, no bias");
   constexpr int WN = NTH / 64 / WM;    // waves along the (tap, c) columns
   constexpr int RBA = BM * 2;   // bytes per A row (co)
   constexpr int RBB = BN * 2;   // bytes per B row (tap,c)
@@ -147,6 +153,21 @@ __global__ void __launch_bounds__(NTH, NTH == NT ? 2 : 1) wgrad_kernel(WGParams 
   const int offh = p.oh0 + p.dh * th, offw = p.ow0 + p.dw * tw;
 
   u32x4 ra[NA], rb[NB];
+  // BNA: the y chunks beside the dA chunks, row validity, this thread's 8 channels' coefficients
+  u32x4 ry[BNA ? NA : 1];
+  bool rv[BNA ? NA : 1];
+  float c1[BNA ? 8 : 1], c2[BNA ? 8 : 1], c3[BNA ? 8 : 1], csc[BNA ? 8 : 1], csh[BNA ? 8 : 1];
+  if constexpr (BNA) {
+    const int c0 = okA ? coA : 0;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      c1[e] = p.bn_c[c0 + e];
+      c2[e] = p.bn_c[p.Mo + c0 + e];
+      c3[e] = p.bn_c[2 * p.Mo + c0 + e];
+      csc[e] = p.bn_c[3 * p.Mo + c0 + e];
+      csh[e] = p.bn_c[4 * p.Mo + c0 + e];
+    }
+  }
   // bias gradient on the matrix cores: the tn == 0 blocks also multiply their
   // dY fragments by a fragment of ones (the wn == 0 waves' sums are written) (D[tc][co] = sum_m dY[m][co]
   // in every tc lane), MI extra MFMAs per 16*NI; they run their OWN copy of the
@@ -166,6 +187,10 @@ __global__ void __launch_bounds__(NTH, NTH == NT ? 2 : 1) wgrad_kernel(WGParams 
         ra[i] = *reinterpret_cast<const u32x4*>(p.dy + (size_t)m * p.ldy + coA);
       else
         ra[i] = u32x4{0, 0, 0, 0};
+      if constexpr (BNA) {
+        rv[i] = okA && m < p.M;
+        ry[i] = rv[i] ? *reinterpret_cast<const u32x4*>(p.bn_y + (size_t)m * p.ldy + coA) : u32x4{0, 0, 0, 0};
+      }
     }
 #pragma unroll
     for (int i = 0; i < NB; ++i) {
@@ -189,8 +214,25 @@ __global__ void __launch_bounds__(NTH, NTH == NT ? 2 : 1) wgrad_kernel(WGParams 
     char* sa = smem + buf * STAGE;
     char* sb = sa + A_BYTES;
 #pragma unroll
-    for (int i = 0; i < NA; ++i)
-      *reinterpret_cast<u32x4*>(sa + lds_off<RBA>(rA0 + AROWS * i, cA * 16)) = ra[i];
+    for (int i = 0; i < NA; ++i) {
+      u32x4 v = ra[i];
+      if constexpr (BNA) {  // dY from dA and y (rows past M stay zero)
+        float g[8], y[8];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          g[2 * e] = lo_bf(v[e]); g[2 * e + 1] = hi_bf(v[e]);
+          y[2 * e] = lo_bf(ry[i][e]); y[2 * e + 1] = hi_bf(ry[i][e]);
+        }
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          g[k] = (y[k] * csc[k] + csh[k]) > 0.f ? g[k] : 0.f;
+          g[k] = c1[k] * g[k] + c2[k] * y[k] + c3[k];
+        }
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[e] = rv[i] ? pack2bf(g[2 * e], g[2 * e + 1]) : 0u;
+      }
+      *reinterpret_cast<u32x4*>(sa + lds_off<RBA>(rA0 + AROWS * i, cA * 16)) = v;
+    }
 #pragma unroll
     for (int i = 0; i < NB; ++i)
       *reinterpret_cast<u32x4*>(sb + lds_off<RBB>(rB0 + BROWS * i, cB * 16)) = rb[i];
@@ -392,6 +434,23 @@ static WGVar wg_variant(int v, int Mo, int No) {
 // + 1: the 3x3 halo-patch kernel (id WG_NVAR; NOT_APPLICABLE (-5) outside stride-1 3x3 geometry)
 PDT_API int pdt_wgrad_num_variants() { return WG_NVAR + 1; }
 
+// the BN-backward-apply instantiations: the 4-wave, 1/2-stage tiles (variants 0..11)
+static void launch_wg_bna(const WGVar& w, dim3 grid, const WGParams& p, hipStream_t stream) {
+#define WG_LAUNCH_B(a, b, c) hipLaunchKernelGGL((wgrad_kernel<a, b, c, NT, 2, 1, false, true>), grid, dim3(NT), 0, stream, p)
+  if (w.NS == 2) {
+    if (w.BM == 64 && w.BN == 64) WG_LAUNCH_B(64, 64, 2);
+    else if (w.BM == 64) WG_LAUNCH_B(64, 128, 2);
+    else if (w.BN == 64) WG_LAUNCH_B(128, 64, 2);
+    else WG_LAUNCH_B(128, 128, 2);
+  } else {
+    if (w.BM == 64 && w.BN == 64) WG_LAUNCH_B(64, 64, 1);
+    else if (w.BM == 64) WG_LAUNCH_B(64, 128, 1);
+    else if (w.BN == 64) WG_LAUNCH_B(128, 64, 1);
+    else WG_LAUNCH_B(128, 128, 1);
+  }
+#undef WG_LAUNCH_B
+}
+
 template <bool BIAS>
 static void launch_wg(const WGVar& w, dim3 grid, const WGParams& p, hipStream_t stream) {
   const int BM = w.BM, BN = w.BN, NS = w.NS;
@@ -478,11 +537,30 @@ PDT_API long pdt_wgrad_workspace(int splits, int Mo, int No) {
 PDT_API int pdt_wgrad_reduce(float* slab, float* out, const float* bslab, float* bias_out, int splits, int Mo, int No,
                              float scale, int accumulate, hipStream_t stream);
 
+// pdt_conv_wgrad2: the same with an optional BatchNorm backward apply on the dY operand
+// (WGParams.bn_y / bn_c: `dy` is then dA); variants 0..11 only (NOT_APPLICABLE otherwise).
+PDT_API int pdt_conv_wgrad2(const void* dy, const void* x, float* slab, float* out, int M, int Mo, int No,
+                            int ldy, int Hs, int Ws, int C, int Hm, int Wm, int sh, int sw, int oh0, int ow0,
+                            int dh, int dw, int ntw, int splits, int ktiles_per_split, float scale,
+                            int accumulate, int variant, int pix, float* bias_out, const void* bn_y,
+                            const float* bn_c, hipStream_t stream);
+
 PDT_API int pdt_conv_wgrad(const void* dy, const void* x, float* slab, float* out, int M, int Mo, int No,
                            int ldy, int Hs, int Ws, int C, int Hm, int Wm, int sh, int sw, int oh0, int ow0,
                            int dh, int dw, int ntw, int splits, int ktiles_per_split, float scale,
                            int accumulate, int variant, int pix, float* bias_out, hipStream_t stream) {
+  return pdt_conv_wgrad2(dy, x, slab, out, M, Mo, No, ldy, Hs, Ws, C, Hm, Wm, sh, sw, oh0, ow0, dh, dw, ntw, splits,
+                         ktiles_per_split, scale, accumulate, variant, pix, bias_out, nullptr, nullptr, stream);
+}
+
+PDT_API int pdt_conv_wgrad2(const void* dy, const void* x, float* slab, float* out, int M, int Mo, int No,
+                            int ldy, int Hs, int Ws, int C, int Hm, int Wm, int sh, int sw, int oh0, int ow0,
+                            int dh, int dw, int ntw, int splits, int ktiles_per_split, float scale,
+                            int accumulate, int variant, int pix, float* bias_out, const void* bn_y,
+                            const float* bn_c, hipStream_t stream) {
   if (C % 8 != 0 || Mo % 8 != 0 || No % 8 != 0 || ldy % 8 != 0) return -1;
+  const bool bna = bn_y != nullptr;
+  if (bna && (bn_c == nullptr || variant < 0 || variant >= 12 || bias_out != nullptr)) return -5;
   if (pix != 0 && (pix % 4 != 0 || pix > C)) return -10;
   if (variant == WG_NVAR) {  // 3x3 / stride 1 / pad 1 halo-patch kernel
     if (ntw != 3 || No != 9 * C || sh != 1 || sw != 1 || oh0 != -1 || ow0 != -1 || dh != 1 || dw != 1 ||
@@ -501,6 +579,8 @@ PDT_API int pdt_conv_wgrad(const void* dy, const void* x, float* slab, float* ou
   p.pix = pix > 0 ? pix : C;
   p.sh = sh; p.sw = sw; p.oh0 = oh0; p.ow0 = ow0; p.dh = dh; p.dw = dw; p.ntw = ntw;
   p.ktiles_per_split = ktiles_per_split; p.splits = splits;
+  p.bn_y = (const u16*)bn_y;
+  p.bn_c = bn_c;
   const int G = reduce_groups(splits, Mo, No);
   // bias_out (optional, fp32 [Mo]): also the column sums of dY, from the same pass
   p.bslab = bias_out ? slab + (long)splits * Mo * No + (G > 1 ? (long)G * Mo * No : 0) : nullptr;
@@ -519,7 +599,8 @@ PDT_API int pdt_conv_wgrad(const void* dy, const void* x, float* slab, float* ou
   const WGVar w = wg_variant(variant, Mo, No);
   int tiles = ((Mo + w.BM - 1) / w.BM) * ((No + w.BN - 1) / w.BN);
   dim3 grid(tiles * splits);
-  if (bias_out) launch_wg<true>(w, grid, p, stream);
+  if (bna) launch_wg_bna(w, grid, p, stream);
+  else if (bias_out) launch_wg<true>(w, grid, p, stream);
   else launch_wg<false>(w, grid, p, stream);
   int e = (int)hipGetLastError();
   if (e) return e;

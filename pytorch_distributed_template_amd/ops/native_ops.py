@@ -62,6 +62,8 @@ _SIGS = {
     "pdt_wgrad_num_variants": (c_int, []),
     "pdt_wgrad_workspace": (c_long, [c_int, c_int, c_int]),
     "pdt_conv_wgrad": (c_int, [P, P, P, P] + [c_int] * 16 + [c_int, c_int, c_float, c_int, c_int, c_int, P, P]),
+    "pdt_conv_wgrad2": (c_int, [P, P, P, P] + [c_int] * 16 + [c_int, c_int, c_float, c_int, c_int, c_int, P, P, P,
+                                                                P]),
     "pdt_bn_stats_blocks": (c_int, [c_long, c_int]),
     "pdt_bn_bwd_reduce_pool": (c_int, [P] * 7 + [c_int] * 10 + [P]),
     "pdt_bn_bwd_apply_pool": (c_int, [P] * 9 + [c_int] * 9 + [P]),
@@ -593,18 +595,54 @@ def conv_stat_rows(M, Ncol, K, variant):
     return _load().pdt_conv_nt_stat_rows(M, Ncol, K, variant)
 
 
-def _wgrad_launch(lib, dy, x, out, v, scale, accumulate, a, bias_out=None):
+def _wgrad_launch(lib, dy, x, out, v, scale, accumulate, a, bias_out=None, bna=None):
     """One weight-gradient launch (+ slab reduction); returns the kernel's return code
-    (NOT_APPLICABLE: variant ``v`` cannot run this geometry)."""
+    (NOT_APPLICABLE: variant ``v`` cannot run this geometry). ``bna`` = (y, coef [5][Mo]):
+    ``dy`` is dA and the BN backward apply runs in the dY staging (``pdt_conv_wgrad2``)."""
     kps = c_int(0)
     splits = lib.pdt_wgrad_plan2(a["M"], a["Mo"], a["No"], a["Hs"], a["Ws"], a["C"], v, ctypes.byref(kps))
     if splits < 0:
         return splits
     slab = torch.empty(lib.pdt_wgrad_workspace(splits, a["Mo"], a["No"]), dtype=torch.float32, device=dy.device)
-    return lib.pdt_conv_wgrad(_p(dy), _p(x), _p(slab), _p(out), a["M"], a["Mo"], a["No"], a["ldy"], a["Hs"], a["Ws"],
-                              a["C"], a["Hm"], a["Wm"], a["sh"], a["sw"], a["oh0"], a["ow0"], a["dh"], a["dw"],
-                              a["ntw"], splits, kps.value, float(scale), int(accumulate), int(v),
-                              int(a.get("pix", 0)), _p(bias_out), _s())
+    by, bc = bna if bna is not None else (None, None)
+    return lib.pdt_conv_wgrad2(_p(dy), _p(x), _p(slab), _p(out), a["M"], a["Mo"], a["No"], a["ldy"], a["Hs"],
+                               a["Ws"], a["C"], a["Hm"], a["Wm"], a["sh"], a["sw"], a["oh0"], a["ow0"], a["dh"],
+                               a["dw"], a["ntw"], splits, kps.value, float(scale), int(accumulate), int(v),
+                               int(a.get("pix", 0)), _p(bias_out), _p(by), _p(bc), _s())
+
+
+WGB_VARIANTS = tuple(range(12))  # the 4-wave 1/2-stage tiles carry the BN-apply instantiation
+
+
+def conv_wgrad_bn(dA, x, out, y, coef, run_ref, **a):
+    """Weight gradient whose dY = k1*gate(dA) + k2*y + k3 (a BN+ReLU unit's backward apply,
+    ``coef`` = [k1; k2; k3; scale; shift] fp32 [5][Mo], gate = y*scale+shift > 0) is formed
+    while staging dA (``pdt_conv_wgrad2``): the apply pass and its dy tensor disappear.
+    Tuned per geometry against ``run_ref()`` (the element pass + the plain weight gradient):
+    returns False when that is faster (the caller runs it), True when done here."""
+    lib = _load()
+    assert coef.dtype == torch.float32 and coef.is_contiguous() and coef.numel() == 5 * a["Mo"]
+    assert y.dtype == torch.bfloat16 and y.shape == dA.shape
+    key = "wgb:" + ",".join(str(a[k]) for k in ("M", "Mo", "No", "Hs", "Ws", "C", "Hm", "Wm", "sh", "ntw")) + \
+        (f",p{a['pix']}" if a.get("pix") else "")
+    table = _tuned()
+    v = table.get(key)
+    if v is None:
+        if not _tune_allowed():
+            return False
+
+        def run(v):
+            return _wgrad_launch(lib, dA, x, out, v, 1.0, False, a, bna=(y, coef))
+        best = _time_variants(max(WGB_VARIANTS) + 1, run, set(WGB_VARIANTS))
+        if best >= 0 and _time_fn(run_ref) < _time_fn(lambda: run(best)):
+            best = AX_UNFUSED
+        table[key] = v = best
+        _save_tuned()
+    v = int(v)
+    if v < 0:
+        return False
+    _chk(_wgrad_launch(lib, dA, x, out, v, 1.0, False, a, bna=(y, coef)), "conv_wgrad (BN backward apply)")
+    return True
 
 
 _WG_KEYS: dict = {}
@@ -1857,11 +1895,33 @@ def _unit_fwd_s2d(x, w, gamma, beta, bna: _BNArgs):
     return u
 
 
-def _unit_dw_s2d(dy, u: _Unit):
+def _unit_dw_s2d(dy, u: _Unit, bn_dA=None):
+    """Stem weight gradient (space-to-depth GEMM). ``bn_dA`` = (dA, k1, k2, k3): ``dy`` is
+    not given (None) and the stem BN's backward apply is formed inside the weight
+    gradient's dY staging when the tuner finds that faster than the element pass."""
     a = _s2d_geom(u.N, u.H, u.W, u.Cout)
-    dw256 = torch.empty((u.Cout, 256), dtype=torch.float32, device=dy.device)
-    conv_wgrad(dy, u.x, dw256, M=u.N * a["Ho"] * a["Wo"], Mo=u.Cout, No=256, ldy=u.Cout, Hs=u.H, Ws=u.W, C=8,
-               Hm=a["Ho"], Wm=a["Wo"], sh=2, sw=2, oh0=-3, ow0=-4, dh=1, dw=2, ntw=4, pix=4)
+    dw256 = torch.empty((u.Cout, 256), dtype=torch.float32, device=u.y.device)
+    g = dict(M=u.N * a["Ho"] * a["Wo"], Mo=u.Cout, No=256, ldy=u.Cout, Hs=u.H, Ws=u.W, C=8, Hm=a["Ho"], Wm=a["Wo"],
+             sh=2, sw=2, oh0=-3, ow0=-4, dh=1, dw=2, ntw=4, pix=4)
+    if bn_dA is not None:
+        dA, k1, k2, k3 = bn_dA
+        coef = torch.stack([k1, k2, k3, u.scale, u.shift]).contiguous()
+        lib = _load()
+        M = u.y.numel() // u.Cout
+
+        def apply_pass():
+            dy = torch.empty_like(u.y, memory_format=torch.channels_last)
+            _chk(lib.pdt_bn_bwd_apply(_p(dA), _p(u.y), None, _p(u.scale), _p(u.shift), _p(k1), _p(k2), _p(k3),
+                                      _p(dy), None, M, u.Cout, 1, None, _s()), "bn_bwd_apply")
+            return dy
+
+        def run_ref():
+            conv_wgrad(apply_pass(), u.x, dw256, **g)
+
+        if not conv_wgrad_bn(dA, u.x, dw256, u.y, coef, run_ref, **g):
+            conv_wgrad(apply_pass(), u.x, dw256, **g)
+    else:
+        conv_wgrad(dy, u.x, dw256, **g)
     dw = _s2d_unfold_grad(dw256, u.C).contiguous(memory_format=torch.channels_last)
     return dw.to(u.w.dtype) if dw.dtype != u.w.dtype else dw
 
@@ -1907,6 +1967,14 @@ class _StemPool(torch.autograd.Function):
             dA = _empty_cl(N, C, H, W, torch.bfloat16, dout.device)
             _chk(_load().pdt_maxpool_bwd(_p(dout), _p(idx), _p(dA), N, H, W, C, Ho, Wo, k, s, p, _s()),
                  "maxpool_bwd")
+            s2d = u.g.get("s2d", False)
+            if s2d and ctx.needs_input_grad[1] and os.environ.get("PDT_STEM_WGRAD_BN", "1") == "1":
+                # the stem's only consumer of dy is its weight gradient (no data gradient of the
+                # image): the BN backward apply is formed in that GEMM's dY staging (tuned per shape)
+                dgamma, dbeta, k1, k2, k3 = _bn_bwd(dA, u, False, coeffs_only=True)
+                dw = _unit_dw_s2d(None, u, bn_dA=(dA, k1, k2, k3))
+                del ctx.u
+                return None, dw, dgamma, dbeta, None, None, None, None, None
             dy, _, dgamma, dbeta = _bn_bwd(dA, u, False)
         s2d = u.g.get("s2d", False)
         dx = _unit_dx(dy, u) if ctx.needs_input_grad[0] and not s2d else None

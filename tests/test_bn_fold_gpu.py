@@ -291,3 +291,43 @@ def test_dgrad_epilogue_second_unit_partials(monkeypatch, v):
     assert pre.second is not None and pre.second.unit is ud
     pd = pre.second.part[:2 * R * Cin].view(2, R, Cin).sum(1)
     assert nrmerr(pd[0], s_ref) < 1e-3 and nrmerr(pd[1], qd_ref) < 1e-3
+
+
+@pytest.mark.parametrize("geom", ["3x3", "stem_s2d"])
+def test_wgrad_bn_backward_apply_in_staging(geom):
+    """The weight gradient forming dY = k1*gate(dA) + k2*y + k3 while staging dA
+    (pdt_conv_wgrad2; the stem's BN backward apply) against the element pass followed by
+    the plain weight gradient, for every tile that carries it."""
+    torch.manual_seed(3)
+    lib = no._load()
+    if geom == "3x3":
+        N, C, Co, H = 4, 64, 64, 14
+        x = _cl(torch.randn(N, C, H, H, device="cuda").to(torch.bfloat16))
+        a = dict(M=N * H * H, Mo=Co, No=9 * C, ldy=Co, Hs=H, Ws=H, C=C, Hm=H, Wm=H, sh=1, sw=1, oh0=-1, ow0=-1,
+                 dh=1, dw=1, ntw=3)
+        shp = (N, Co, H, H)
+    else:  # the space-to-depth stem: NHWC padded to 4 channels, 8 x 4 taps of 8 "channels"
+        N, Co, H = 2, 64, 224
+        x = torch.zeros(N, H, H, 4, device="cuda", dtype=torch.bfloat16)
+        x[..., :3] = torch.randn(N, H, H, 3, device="cuda").to(torch.bfloat16)
+        a = dict(M=N * 112 * 112, Mo=Co, No=256, ldy=Co, Hs=H, Ws=H, C=8, Hm=112, Wm=112, sh=2, sw=2, oh0=-3,
+                 ow0=-4, dh=1, dw=2, ntw=4, pix=4)
+        shp = (N, Co, 112, 112)
+    dA = _cl(torch.randn(shp, device="cuda").to(torch.bfloat16))
+    y = _cl(torch.randn(shp, device="cuda").to(torch.bfloat16))
+    k1, k2, k3 = (torch.randn(Co, device="cuda") * 0.5 for _ in range(3))
+    sc, sh = torch.rand(Co, device="cuda") + 0.5, torch.randn(Co, device="cuda") * 0.2
+    coef = torch.stack([k1, k2, k3, sc, sh]).contiguous()
+    dy = torch.empty_like(y)
+    no._chk(lib.pdt_bn_bwd_apply(no._p(dA), no._p(y), None, no._p(sc), no._p(sh), no._p(k1), no._p(k2), no._p(k3),
+                                 no._p(dy), None, y.numel() // Co, Co, 1, None, no._s()), "apply")
+    ran = 0
+    for v in no.WGB_VARIANTS:
+        ref = torch.zeros(Co * a["No"], device="cuda")
+        got = torch.full_like(ref, float("nan"))
+        assert no._wgrad_launch(lib, dy, x, ref, v, 1.0, False, a) == 0
+        rc = no._wgrad_launch(lib, dA, x, got, v, 1.0, False, a, bna=(y, coef))
+        assert rc == 0, (v, rc)
+        ran += 1
+        assert nrmerr(got, ref) < 2e-3, (v, nrmerr(got, ref))
+    assert ran == len(no.WGB_VARIANTS)
