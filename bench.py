@@ -388,6 +388,11 @@ def main():
                 sy.copy_(yb)
                 gstep()
         torch.cuda.current_stream().wait_stream(side)
+        # hand the warm-up's cached activation blocks back before the capture allocates the
+        # graph's private pool: otherwise both stay reserved (2x the activations: ResNet-152
+        # at 2048 images/GPU would not fit in 288 GB)
+        torch.cuda.synchronize()
+        torch.cuda.empty_cache()
         graph = torch.cuda.CUDAGraph()
         with torch.cuda.graph(graph):
             static_loss = gstep()

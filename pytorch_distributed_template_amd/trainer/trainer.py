@@ -223,6 +223,10 @@ class Trainer(BaseTrainer):
             gx.pdt_nhwc_pad = cp
         gy = target.clone()
         self.optimizer.refresh_scalars()
+        # the eager warm-up's cached activation blocks go back first (the graph gets a private
+        # pool: both reserved at once would double the activation memory)
+        torch.cuda.synchronize(self.device)
+        torch.cuda.empty_cache()
         graph = torch.cuda.CUDAGraph()
         with torch.cuda.graph(graph, stream=self._side):
             gloss = self._step_body(gx, gy)
