@@ -99,8 +99,11 @@ def parse():
         a.batch = DEFAULT_BATCH.get(a.model, 256)
     if a.graph is None:
         # the stock stack stays eager (it is the reference-equivalent baseline); gloo
-        # rehearsals and CPU runs have no capturable collectives
-        a.graph = a.backend == "native" and a.device == "cuda" and a.dist_backend != "gloo"
+        # rehearsals and CPU runs have no capturable collectives. ViT-B/16 fp8 at 1024
+        # images/GPU measured 2 % slower replayed than eager on one box (7.52k vs 7.68k,
+        # profiles/bench_runs_round3.jsonl s4k): its default stays eager (--graph opts in)
+        a.graph = a.backend == "native" and a.device == "cuda" and a.dist_backend != "gloo" and \
+            not a.model.startswith("vit")
     if a.device == "cpu":
         a.backend, a.dist_backend, a.graph = "torch", "gloo", False
     elif a.image_size != 224:
