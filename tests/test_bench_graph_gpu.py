@@ -2,6 +2,7 @@
 all-reduce on a throwaway group, replay it, agree on the main group. On one GPU the group has
 one rank (the N > 1 case runs the same code on the driver's multi-GPU node)."""
 import os
+import socket
 import subprocess
 import sys
 
@@ -24,8 +25,14 @@ dist.destroy_process_group()
 """
 
 
+def _port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
 def test_graph_collectives_preflight_one_rank():
-    env = dict(os.environ, PDT_ROOT=ROOT, MASTER_ADDR="127.0.0.1", MASTER_PORT="29611",
+    env = dict(os.environ, PDT_ROOT=ROOT, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_port()),
                TORCH_NCCL_ASYNC_ERROR_HANDLING="0")
     r = subprocess.run([sys.executable, "-c", SCRIPT], cwd=ROOT, env=env, capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stderr[-3000:]
