@@ -20,8 +20,12 @@
 //
 // Patch LDS image: pixel q of the patch (row q / rs, column q % rs; column c
 // holds input column c - 1, zero outside the image) is 128 B with its 16-B
-// chunks XOR-swizzled by ((q >> 1) & 7) -- the swizzle of the generic kernel's
-// LDS rows. rs is a multiple of 16, so a row shift (a * rs) leaves the swizzle
+// chunks XOR-swizzled by (q & 7). (The generic kernel's (q >> 1) & 7 is
+// conflict-free only for fragments starting at a multiple of 4 pixels; the column
+// shifts b = +-1 start them anywhere: 2-way conflicts on 2 of 3 taps, measured 3.1
+// conflict cycles per LDS instruction; with q & 7 a fragment of 16 consecutive
+// pixels is conflict-free at any start -- rows that wrap inside a fragment, W = 14,
+// still collide.) rs is a multiple of 16, so a row shift (a * rs) leaves the swizzle
 // unchanged and every A-fragment address is a per-lane constant (precomputed
 // per column shift b) plus a wave-uniform offset: ~1.5 VALU per ds_read.
 // Rows above / below the image (the tile may straddle images: rows are counted
@@ -88,7 +92,7 @@ __global__ void __launch_bounds__(NTH, 1) conv3x3_halo_kernel(NTParams p, int rs
     for (int b = 0; b < 3; ++b) {
       const int q = pb + b - 1;
 #pragma unroll
-      for (int kk = 0; kk < 2; ++kk) aoff[i][b][kk] = q * 128 + ((((q >> 1) & 7) ^ (kk * 4 + (lane >> 4))) << 4);
+      for (int kk = 0; kk < 2; ++kk) aoff[i][b][kk] = q * 128 + (((q & 7) ^ (kk * 4 + (lane >> 4))) << 4);
     }
   }
   // B fragments: slot row = this wave's column, 16-B chunk swizzled like the generic kernel
@@ -134,7 +138,7 @@ __global__ void __launch_bounds__(NTH, 1) conv3x3_halo_kernel(NTParams p, int rs
       const int g = g0 + (q >> rs_log2);
       const int w = (q & (rs - 1)) - 1;
       const bool ok = live && q < P && g >= 0 && g < NH && w >= 0 && w < W;
-      const int ch = (tid & 7) ^ ((q >> 1) & 7);
+      const int ch = (tid & 7) ^ (q & 7);
       const void* src = ok ? (const void*)(p.src + ((size_t)g * W + w) * Cin + cc * 64 + ch * 8)
                            : p.zero;
       __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)(sp + (8 * wave + GP * l) * 128),
