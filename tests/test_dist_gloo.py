@@ -183,3 +183,24 @@ def test_pretune_broadcasts_rank0_table():
     assert res[0]["calls"] == [0] and res[1]["calls"] == []
     assert res[0]["entry"] == 7 and res[1]["entry"] == 7
     assert not res[0]["allowed"] and not res[1]["allowed"]
+
+
+def _w_graph_preflight(rank, world, port, q):
+    try:
+        _init(rank, world, port)
+        import sys
+        sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+        import bench
+        # no capturable RCCL group on these CPU ranks: the check must fail on every rank and
+        # every rank must learn it (the agreement all-reduce runs on the job's own group)
+        ok, why = bench.graph_collectives_ok(torch.device("cpu"), world)
+        q.put((rank, {"ok": ok, "why": why}))
+        dist.destroy_process_group()
+    except Exception as e:  # pragma: no cover
+        q.put((rank, repr(e)))
+
+
+def test_bench_graph_preflight_falls_back_on_every_rank():
+    res = _run(_w_graph_preflight)
+    assert res[0]["ok"] is False and res[1]["ok"] is False
+    assert res[0]["why"] and res[1]["why"]
