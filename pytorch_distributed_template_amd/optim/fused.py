@@ -138,6 +138,24 @@ class _FusedBase(Optimizer):
                 d[0].fill_(float(group["lr"]))
                 self._dev_lr[gi] = float(group["lr"])
 
+    def zero_grad(self, set_to_none: bool = True):
+        """torch semantics; ``set_to_none=False`` (a graph-captured step must keep its gradient
+        buffers) zeroes every gradient with one multi-tensor launch per device / dtype instead
+        of one fill kernel per parameter (161 for ResNet-50)."""
+        if set_to_none:
+            return super().zero_grad(set_to_none=True)
+        groups = {}
+        for group in self.param_groups:
+            for p in group["params"]:
+                if p.grad is not None:
+                    if p.grad.grad_fn is not None:
+                        p.grad.detach_()
+                    else:
+                        p.grad.requires_grad_(False)
+                    groups.setdefault((p.grad.device, p.grad.dtype), []).append(p.grad)
+        for grads in groups.values():
+            torch._foreach_zero_(grads)
+
     def _step_prologue(self):
         if self.capturable and not torch.cuda.is_current_stream_capturing():
             self.refresh_scalars()
