@@ -160,6 +160,8 @@ def graph_collectives_ok(device, world, check_single=False):
         t = torch.ones(4096, device=device)
         dist.all_reduce(t, group=pg)
         torch.cuda.synchronize()
+        from pytorch_distributed_template_amd.utils import dist as pdist
+        pdist.quiesce_for_capture(device)
         side = torch.cuda.Stream()
         side.wait_stream(torch.cuda.current_stream())
         g = torch.cuda.CUDAGraph()
@@ -396,6 +398,7 @@ def main():
         # at 2048 images/GPU would not fit in 288 GB)
         torch.cuda.synchronize()
         torch.cuda.empty_cache()
+        pdist.quiesce_for_capture(device)  # the RCCL watchdog retires the warm-up's collectives first
         graph = torch.cuda.CUDAGraph()
         with torch.cuda.graph(graph):
             static_loss = gstep()

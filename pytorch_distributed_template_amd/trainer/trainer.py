@@ -227,6 +227,7 @@ class Trainer(BaseTrainer):
         # pool: both reserved at once would double the activation memory)
         torch.cuda.synchronize(self.device)
         torch.cuda.empty_cache()
+        pdist.quiesce_for_capture(self.device)  # the RCCL watchdog retires the warm-up's collectives first
         graph = torch.cuda.CUDAGraph()
         with torch.cuda.graph(graph, stream=self._side):
             gloss = self._step_body(gx, gy)

@@ -117,6 +117,21 @@ def init_distributed(local_rank: Optional[int] = None, backend: Optional[str] = 
     return device
 
 
+def quiesce_for_capture(device=None, wait_s: float = 1.0) -> None:
+    """Call right before capturing RCCL collectives in a HIP graph. ProcessGroupNCCL's
+    watchdog thread polls the end events of every collective it still tracks; on ROCm that
+    query fails (hipErrorCapturedEvent, and the watchdog aborts the process) once the RCCL
+    stream those events were recorded on joins a capture. Finishing all queued work and
+    giving the watchdog a few of its polling periods (100 ms) lets it retire every tracked
+    collective first; collectives issued during the capture are never tracked, replays
+    issue none."""
+    if not (dist.is_available() and dist.is_initialized()) or dist.get_backend() != "nccl":
+        return
+    import time
+    torch.cuda.synchronize(device)
+    time.sleep(wait_s)
+
+
 def cleanup():
     if is_dist_ready():
         dist.destroy_process_group()
