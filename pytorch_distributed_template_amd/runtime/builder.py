@@ -102,6 +102,9 @@ def wrap_model(config, model, device):
         with torch.cuda.stream(side):
             model = wrap()
         torch.cuda.current_stream(device).wait_stream(side)
+        # the Trainer runs the warm-up and the capture on THIS stream: DDP binds its gradient
+        # accumulators to the construction stream (another stream: NaN gradients after capture)
+        model._pdt_capture_stream = side
         return model
     return wrap()
 

@@ -80,7 +80,9 @@ class Trainer(BaseTrainer):
         self._graph = None
         self._graph_io = None  # (static data, static target, static loss)
         self._graph_eager_steps = 0
-        self._side = torch.cuda.Stream(device=device) if self.hip_graph else None
+        # the capture side stream: the one DDP was built on (runtime.builder.wrap_model), if any
+        self._side = (getattr(model, "_pdt_capture_stream", None) or torch.cuda.Stream(device=device)) \
+            if self.hip_graph else None
 
     # ------------------------------------------------------------------ helpers
     def _on_epoch_start(self, epoch):

@@ -107,3 +107,38 @@ def test_trainer_hip_graph_matches_eager(tmp_path):
     for k, v in weights["eager"].items():
         if v.is_floating_point():
             torch.testing.assert_close(weights["graph"][k].float(), v.float(), rtol=1e-3, atol=1e-4, msg=k)
+
+
+def _free_port():
+    import socket
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def test_trainer_hip_graph_under_torchrun_ddp_rccl(tmp_path):
+    """``trainer.hip_graph`` with DDP over a 1-rank RCCL group (torchrun): the reducer is
+    built on the capture side stream, the RCCL watchdog is drained before the capture, the
+    captured step (bucketed all-reduce included) is replayed, a scheduler changes the lr
+    between the epochs, checkpoints are written; then resume -> test."""
+    cfg = json.loads((ROOT / "config" / "resnet50_bf16.json").read_text())
+    cfg["trainer"].update(save_dir=str(tmp_path), len_epoch=14, epochs=2, monitor="off", save_period=2,
+                          hip_graph=True)
+    cfg["train_loader"]["args"].update(batch_size=16, num_samples=16 * 14)
+    cfg["lr_scheduler"] = {"type": "StepLR", "args": {"step_size": 1, "gamma": 0.5}}
+    for k in ("valid_loader", "test_loader"):
+        cfg[k]["args"].update(batch_size=16, num_samples=32)
+    p = tmp_path / "cfg.json"
+    p.write_text(json.dumps(cfg))
+    env = dict(os.environ, PYTHONPATH=str(ROOT), PDT_RUN_ID="gd", HSA_ENABLE_IPC_MODE_LEGACY="0")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=1",
+           "--master-addr=127.0.0.1", f"--master-port={_free_port()}", "train.py", "-c", str(p), "--backend", "native"]
+    r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=900)
+    out = r.stdout + r.stderr
+    assert r.returncode == 0, out[-4000:]
+    assert "process group: nccl, world size 1" in out and "captured the training step as a HIP graph" in out, \
+        out[-3000:]
+    ck = tmp_path / cfg["name"] / "train" / "gd" / "checkpoint-epoch2.pth"
+    state = torch.load(ck, weights_only=True, map_location="cpu")
+    assert all(torch.isfinite(v).all() for v in state["state_dict"].values() if v.is_floating_point())
+    assert abs(state["optimizer"]["param_groups"][0]["lr"] - 0.1 * 0.25) < 1e-9  # two StepLR steps
