@@ -9,11 +9,11 @@ Each timed step is a full training step: forward, softmax-cross-entropy,
 backward (DDP bucketed all-reduce over RCCL overlapped with it), optimizer
 step (SGD momentum + weight decay). Nothing is skipped or cached. N = 1 runs
 the same path: a 1-rank RCCL process group and the DDP reducer (``--no-ddp``
-drops both for an A/B). On the native GPU path the whole step -- kernels, DDP
-reducer and its RCCL all-reduces -- is captured once as a HIP graph and replayed
-(PyTorch's whole-network DDP capture recipe; at N > 1 a capture + replay of one
-RCCL all-reduce is checked first and the run falls back to eager launches if it
-fails anywhere); ``--eager`` launches kernel by kernel.
+drops both for an A/B). ``--graph`` captures the whole step -- kernels, DDP
+reducer and its RCCL all-reduces -- once as a HIP graph and replays it (PyTorch's
+whole-network DDP capture recipe, on the stream DDP was built on; at N > 1 a capture
++ replay of one RCCL all-reduce is checked first and the run falls back to eager
+launches if it fails anywhere).
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B]
                     [--model resnet50|resnet152|vit_b_16] [--backend native|torch]
@@ -76,10 +76,10 @@ def parse():
     ap.add_argument("--bucket-mb", type=float, default=64.0)
     ap.add_argument("--comm-hook", default=None, choices=[None, "bf16"])
     ap.add_argument("--graph", dest="graph", action="store_true", default=None,
-                    help="capture the whole training step (DDP all-reduce included) in one HIP graph; the "
-                         "default on the native GPU path")
+                    help="capture the whole training step (DDP all-reduce included) in one HIP graph and "
+                         "replay it")
     ap.add_argument("--eager", dest="graph", action="store_false",
-                    help="launch the step's kernels one by one (no HIP graph)")
+                    help="launch the step's kernels one by one (the default)")
     ap.add_argument("--json-out", default=None)
     ap.add_argument("--miopen-find", type=int, default=1, choices=[0, 1],
                     help="torch backend: 1 = cudnn.benchmark (MIOpen find), 0 = immediate mode")
@@ -98,12 +98,13 @@ def parse():
     if a.batch is None:
         a.batch = DEFAULT_BATCH.get(a.model, 256)
     if a.graph is None:
-        # the stock stack stays eager (it is the reference-equivalent baseline); gloo
-        # rehearsals and CPU runs have no capturable collectives. ViT-B/16 fp8 at 1024
-        # images/GPU measured 2 % slower replayed than eager on one box (7.52k vs 7.68k,
-        # profiles/bench_runs_round3.jsonl s4k): its default stays eager (--graph opts in)
-        a.graph = a.backend == "native" and a.device == "cuda" and a.dist_backend != "gloo" and \
-            not a.model.startswith("vit")
+        # eager by default: once captured on the stream DDP was built on (see below) the
+        # replayed step runs at the eager rate (ResNet-50 bs2048 14.06k vs 14.08k, bs512
+        # 12.23k vs 12.27k; profiles/bench_runs_round3.jsonl s4z), and an N > 1 capture of
+        # RCCL collectives is one more thing that can fail on the driver's node
+        a.graph = False
+    if a.graph and (a.backend != "native" or a.device != "cuda" or a.dist_backend == "gloo"):
+        ap.error("--graph needs the native backend on the GPU with RCCL collectives")
     if a.device == "cpu":
         a.backend, a.dist_backend, a.graph = "torch", "gloo", False
     elif a.image_size != 224:
@@ -400,7 +401,9 @@ def main():
         torch.cuda.empty_cache()
         pdist.quiesce_for_capture(device)  # the RCCL watchdog retires the warm-up's collectives first
         graph = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(graph):
+        # captured on the stream DDP was built and warmed up on: DDP binds its gradient
+        # accumulators to that stream (torch.cuda.graph's own private stream: NaN gradients)
+        with torch.cuda.graph(graph, stream=side):
             static_loss = gstep()
 
         def step(i):  # noqa: F811
