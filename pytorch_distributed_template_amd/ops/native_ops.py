@@ -464,7 +464,9 @@ def _time_variants(nvar, launch, allowed=None):
     if not cand:
         return -1
     best_t = {v: float("inf") for v in cand}
-    for _ in range(2):
+    # PDT_TUNE_ROUNDS (default 2): interleaved rounds; more rounds cut the timing noise of a
+    # (re)tune run at the cost of its length
+    for _ in range(max(1, int(os.environ.get("PDT_TUNE_ROUNDS", "2")))):
         for v in cand:
             ev0.record()
             for _ in range(3):
