@@ -29,6 +29,7 @@ from __future__ import annotations
 
 import argparse
 import json
+import math
 import os
 import socket
 import subprocess
@@ -62,6 +63,8 @@ STOCK_BEST_1GPU_IMG_S = {"resnet50": (6969.13, 2048), "vit_b_16": (4059.96, 1024
 # 1024 (stock autocast: 3.55k at 256, 4.06k at 1024). At 256 the host-side issue
 # time (~35 ms) is close to the 40 ms step: the GPU idles between kernels.
 DEFAULT_BATCH = {"resnet50": 2048, "vit_b_16": 1024}
+# --graph: batches run eagerly and replayed (lr 0) before the timed run; losses must agree
+GRAPH_CHECK_STEPS = 3
 
 
 def parse():
@@ -73,6 +76,7 @@ def parse():
     ap.add_argument("--model", default="resnet50")
     ap.add_argument("--fp8", action="store_true", help="ViT: fp8 (e4m3/e5m2) GEMMs on the native path")
     ap.add_argument("--backend", default="native", choices=["native", "torch"])
+    ap.add_argument("--lr", type=float, default=None, help="learning rate (default: 0.1 SGD / 1e-3 AdamW)")
     ap.add_argument("--bucket-mb", type=float, default=64.0)
     ap.add_argument("--comm-hook", default=None, choices=[None, "bf16"])
     ap.add_argument("--graph", dest="graph", action="store_true", default=None,
@@ -149,13 +153,23 @@ def graph_collectives_ok(device, world, check_single=False):
     """Can this job's RCCL collectives be captured in a HIP graph and replayed? Checked before
     the training step is captured, on a throwaway process group (a failed capture cannot leave
     the main group's communicator in a bad state): warm one all-reduce eagerly, capture it on a
-    side stream, replay, check the sum; every rank learns the verdict on the main group.
-    World 1 needs no check (the N = 1 step capture itself exercises that path).
-    Returns (ok, reason)."""
+    side stream, replay, check the sum. World 1 needs no check (the N = 1 step capture itself
+    exercises that path).
+
+    The ranks agree TWICE on the main group: first on "every rank captured" -- only then does
+    any rank replay (a replay joined by fewer ranks than the group would block forever, and
+    ``--graph`` runs without the RCCL watchdog's async abort) -- and then on "every replay
+    summed correctly". Returns (ok, reason)."""
     if world == 1 and not check_single:
         return True, None
     import torch.distributed as dist
-    ok, why = 1, None
+
+    def agree(v):
+        flag = torch.tensor([int(v)], dtype=torch.int32, device=device)
+        dist.all_reduce(flag, op=dist.ReduceOp.MIN)
+        return bool(flag.item())
+
+    why, g, t, pg = None, None, None, None
     try:
         pg = dist.new_group(backend="nccl")
         t = torch.ones(4096, device=device)
@@ -171,18 +185,22 @@ def graph_collectives_ok(device, world, check_single=False):
             with torch.cuda.graph(g, stream=side):
                 dist.all_reduce(t, group=pg)
         torch.cuda.current_stream().wait_stream(side)
+        torch.cuda.synchronize()
+    except Exception as e:  # noqa: BLE001 -- any failure means: run eager
+        why, g = f"capture: {type(e).__name__}: {e}", None
+    if not agree(g is not None):
+        return False, why or "another rank could not capture its collectives"
+    try:
         t.fill_(1.0)
         g.replay()
         torch.cuda.synchronize()
         if not bool((t == float(world)).all()):
-            ok, why = 0, f"replayed all-reduce returned {t[0].item()} instead of {world}"
-    except Exception as e:  # noqa: BLE001 -- any failure means: run eager
-        ok, why = 0, f"{type(e).__name__}: {e}"
-    flag = torch.tensor([ok], dtype=torch.int32, device=device)
-    dist.all_reduce(flag, op=dist.ReduceOp.MIN)
-    if not bool(flag.item()) and why is None:
-        why = "another rank could not capture its collectives"
-    return bool(flag.item()), why
+            why = f"replayed all-reduce returned {t[0].item()} instead of {world}"
+    except Exception as e:  # noqa: BLE001
+        why = f"replay: {type(e).__name__}: {e}"
+    if not agree(why is None):
+        return False, why or "another rank's replayed all-reduce failed"
+    return True, None
 
 
 def _rccl_version():
@@ -212,8 +230,10 @@ def pdist_ready() -> bool:
 def allreduce_probe(model, device, world, iters=10):
     """Time an all-reduce of one gradient-sized fp32 buffer on the job's process group
     (outside the timed region): the xGMI/RCCL evidence of a multi-GPU run, recorded in
-    the JSON next to the throughput. busbw = 2(n-1)/n * bytes / time (ring-equivalent)."""
-    if not pdist_ready() or device.type != "cuda":
+    the JSON next to the throughput. busbw = 2(n-1)/n * bytes / time (ring-equivalent).
+    None at N = 1: a 1-rank RCCL all-reduce moves no bytes between GPUs (it is a local
+    copy), so its time says nothing about xGMI."""
+    if not pdist_ready() or device.type != "cuda" or world == 1:
         return None
     n = sum(p.numel() for p in model.parameters() if p.requires_grad)
     buf = torch.ones(n, dtype=torch.float32, device=device)
@@ -230,6 +250,30 @@ def allreduce_probe(model, device, world, iters=10):
     nbytes = n * 4
     return {"bytes": nbytes, "median_ms": round(ms, 3),
             "busbw_GBps": round(2 * (world - 1) / world * nbytes / (ms / 1e3) / 1e9, 1)}
+
+
+def any_rank(flag: bool, device) -> bool:
+    """True on every rank if ``flag`` is True on any rank (so all ranks take the same exit)."""
+    if not pdist_ready():
+        return bool(flag)
+    t = torch.tensor([int(bool(flag))], dtype=torch.int32, device=device)
+    torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
+    return bool(t.item())
+
+
+def refuse(rank, rec, reason, json_out=None):
+    """Print the record with ``value: null`` and the reason, and exit non-zero: a step that
+    produced a non-finite loss, or a replayed graph that disagrees with the eager step, is
+    not a throughput measurement."""
+    rec = dict(rec, value=None, vs_baseline=None, error=reason)
+    if rank == 0:
+        line = json.dumps(rec)
+        print(line, flush=True)
+        if json_out:
+            with open(json_out, "w") as f:
+                f.write(line + "\n")
+    print(f"bench.py: {reason}", file=sys.stderr, flush=True)
+    sys.exit(3)
 
 
 def heartbeat(rank, state, every_s=30.0):
@@ -290,15 +334,17 @@ def main():
     model = ctor(num_classes=1000, **kw).to(device).to(memory_format=torch.channels_last)
     from pytorch_distributed_template_amd.optim import FusedAdamW, FusedSGD
     if args.model.startswith("vit"):
-        opt_name = "AdamW(lr=1e-3, wd=0.05)"
+        lr = 1e-3 if args.lr is None else args.lr
+        opt_name = f"AdamW(lr={lr:g}, wd=0.05)"
         # capturable under --graph: lr and Adam's step count in device memory, so every replay
         # applies the bias corrections of its own step (optim/fused.py)
-        opt = FusedAdamW(model.parameters(), lr=1e-3, weight_decay=0.05, capturable=args.graph) \
-            if args.backend == "native" else torch.optim.AdamW(model.parameters(), lr=1e-3, weight_decay=0.05)
+        opt = FusedAdamW(model.parameters(), lr=lr, weight_decay=0.05, capturable=args.graph) \
+            if args.backend == "native" else torch.optim.AdamW(model.parameters(), lr=lr, weight_decay=0.05)
     else:
-        opt_name = "SGD(momentum=0.9, wd=5e-5)"
-        opt = FusedSGD(model.parameters(), lr=0.1, momentum=0.9, weight_decay=5e-5, capturable=args.graph) \
-            if args.backend == "native" else torch.optim.SGD(model.parameters(), lr=0.1, momentum=0.9,
+        lr = 0.1 if args.lr is None else args.lr
+        opt_name = f"SGD(lr={lr:g}, momentum=0.9, wd=5e-5)"
+        opt = FusedSGD(model.parameters(), lr=lr, momentum=0.9, weight_decay=5e-5, capturable=args.graph) \
+            if args.backend == "native" else torch.optim.SGD(model.parameters(), lr=lr, momentum=0.9,
                                                              weight_decay=5e-5)
     dtype = "float32" if cpu else "bfloat16"
     if args.data == "pool":
@@ -338,6 +384,7 @@ def main():
     pretune_for_ddp(model, _pretune_step)
     ar = allreduce_probe(model, device, world)
     graph_fallback = None
+    graph_check, bad = None, False
     if args.graph and not args.no_ddp:
         ok, graph_fallback = graph_collectives_ok(device, world)
         if not ok:
@@ -384,7 +431,20 @@ def main():
             opt.step()
             return loss
 
+        # replay check: GRAPH_CHECK_STEPS batches run eagerly and then replayed, both at lr 0
+        # (weights unchanged, so each loss depends only on its batch; BatchNorm normalises
+        # with batch statistics in training mode): a capture that records the wrong stream,
+        # buffer or order shows up as a loss mismatch instead of as throughput
+        check_batches = [tuple(t.clone() for t in next_batch(i)) for i in range(GRAPH_CHECK_STEPS)]
+        saved_lr = [g["lr"] for g in opt.param_groups]
+
+        def set_lr(lrs):
+            for g, lr in zip(opt.param_groups, lrs):
+                g["lr"] = lr
+            opt.refresh_scalars()
+
         side.wait_stream(torch.cuda.current_stream())
+        eager_losses = []
         with torch.cuda.stream(side):
             # >= 11 eager iterations: DDP samples runtime stats (host-synchronising) on
             # iterations 1..10, which must all precede the capture
@@ -393,6 +453,11 @@ def main():
                 sx.copy_(xb)
                 sy.copy_(yb)
                 gstep()
+            set_lr([0.0] * len(saved_lr))
+            for xb, yb in check_batches:
+                sx.copy_(xb)
+                sy.copy_(yb)
+                eager_losses.append(gstep().detach().clone())
         torch.cuda.current_stream().wait_stream(side)
         # hand the warm-up's cached activation blocks back before the capture allocates the
         # graph's private pool: otherwise both stay reserved (2x the activations: ResNet-152
@@ -406,12 +471,71 @@ def main():
         with torch.cuda.graph(graph, stream=side):
             static_loss = gstep()
 
+        graph_losses = []
+        for xb, yb in check_batches:
+            sx.copy_(xb)
+            sy.copy_(yb)
+            graph.replay()
+            graph_losses.append(static_loss.detach().clone())
+        set_lr(saved_lr)
+        le = torch.stack(eager_losses).double().cpu()
+        lg = torch.stack(graph_losses).double().cpu()
+        rel = float(((le - lg).abs() / le.abs().clamp_min(1e-12)).max())
+        graph_check = {"eager": [round(float(v), 6) for v in le], "replay": [round(float(v), 6) for v in lg],
+                       "max_rel_diff": rel}
+        del check_batches
+        bad = not (torch.isfinite(le).all() and torch.isfinite(lg).all() and rel <= 1e-3)
+
         def step(i):  # noqa: F811
             xb, yb = next_batch(i)
             sx.copy_(xb)
             sy.copy_(yb)
             graph.replay()
             return static_loss
+
+    # vs_baseline only against the stock stack measured at the SAME per-GPU batch (else
+    # null); the ratio to the stock stack's best measured batch is a separately named field
+    stock = STOCK_1GPU_IMG_S.get((args.model, args.batch))
+    stock_ref = f"stock PyTorch-ROCm at per-GPU batch {args.batch}" if stock else None
+    best = STOCK_BEST_1GPU_IMG_S.get(args.model)
+
+    def record(value, ms, extra):
+        cfg = {"model": args.model, "global_batch": args.batch * world, "per_gpu_batch": args.batch,
+               "seq_len": None, "image_size": args.image_size, "parallelism": f"dp{world}",
+               "backend": args.backend, "optimizer": opt_name,
+               "bucket_cap_mb": args.bucket_mb,
+               "dist_backend": (torch.distributed.get_backend() if pdist_ready() else "none (no process group)"),
+               "ddp": type(model).__name__ == "DistributedDataParallel",
+               "rccl_version": _rccl_version(), "device": args.device,
+               "hip_graph": args.graph, "graph_fallback": graph_fallback, "graph_check": graph_check,
+               "baseline": stock_ref,
+               "vs_best_stock": ({"ratio": round(value / (best[0] * world), 4), "stock_img_s": best[0],
+                                  "stock_per_gpu_batch": best[1]} if best and value else None),
+               "grad_allreduce_probe": ar,
+               "max_mem_gib": round(torch.cuda.max_memory_allocated() / 2 ** 30, 2) if not cpu else None}
+        cfg.update(extra)
+        return {
+            "metric": BASELINE_METRIC if args.model == "resnet50" else f"images/sec (whole node) {args.model} synthetic",
+            "value": round(value, 2) if value else None,
+            "unit": "images/sec",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(ms, 3) if ms else None,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": round(value / (stock * world), 4) if stock and value else None,
+            "dtype": _dtype_label(args),
+            "data": (f"synthetic 3x{args.image_size}x{args.image_size}, random-init weights; " +
+                     ("SyntheticImageNet index batches from DistributedSampler, images generated on device each step"
+                      if args.data == "sampler" else "two pre-made device-resident batches")),
+            "config": cfg,
+        }
+
+    if args.graph and any_rank(bad, device):
+        hb.set()
+        refuse(rank, record(None, None, {}), f"the replayed graph disagrees with the eager step: {graph_check}",
+               args.json_out)
 
     state["phase"] = "warmup"
     for i in range(args.warmup):
@@ -423,10 +547,13 @@ def main():
     state["phase"] = "timed"
     t0 = time.perf_counter()
     cpu_issue = 0.0
+    first_loss = None
     for i in range(args.steps):
         state["step"] = i
         c0 = time.perf_counter()
         loss = step(i)
+        if i == 0:  # (a graph replay overwrites its static loss: keep a copy)
+            first_loss = loss.detach().clone() if args.graph else loss
         cpu_issue += time.perf_counter() - c0
     pdist.synchronize()
     sync()
@@ -436,7 +563,18 @@ def main():
     if pdist_ready():
         torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
     elapsed = float(t.item())
-    final_loss = float(loss.item())
+    loss_first = float(first_loss.item())
+    loss_last = float(loss.item())
+    ms = elapsed / args.steps * 1e3
+    value = world * args.batch * args.steps / elapsed
+    def _r(v):  # JSON has no NaN / inf: a non-finite loss is reported as null
+        return round(v, 4) if math.isfinite(v) else None
+
+    losses = {"loss_first": _r(loss_first), "loss_last": _r(loss_last), "final_loss": _r(loss_last)}
+    # a broken step (NaN / inf loss on any rank) is not a throughput measurement
+    if any_rank(not (math.isfinite(loss_first) and math.isfinite(loss_last)), device):
+        refuse(rank, record(None, ms, losses), f"non-finite training loss (first {loss_first}, last {loss_last})",
+               args.json_out)
     # host enqueue cost of one step with an idle GPU (cpu_issue above includes the time the
     # host waits on a full submission queue while the GPU is busy)
     sync()
@@ -445,43 +583,9 @@ def main():
     host_enqueue_ms = (time.perf_counter() - h0) * 1e3
     sync()
 
-    ms = elapsed / args.steps * 1e3
-    value = world * args.batch * args.steps / elapsed
-    # vs_baseline only against the stock stack measured at the SAME per-GPU batch (else
-    # null); the ratio to the stock stack's best measured batch is a separately named field
-    stock = STOCK_1GPU_IMG_S.get((args.model, args.batch))
-    stock_ref = f"stock PyTorch-ROCm at per-GPU batch {args.batch}" if stock else None
-    best = STOCK_BEST_1GPU_IMG_S.get(args.model)
-    rec = {
-        "metric": BASELINE_METRIC if args.model == "resnet50" else f"images/sec (whole node) {args.model} synthetic",
-        "value": round(value, 2),
-        "unit": "images/sec",
-        "n_gpus": world,
-        "steps": args.steps,
-        "warmup": args.warmup,
-        "ms_per_step": round(ms, 3),
-        "higher_is_better": True,
-        "scaling": "weak",
-        "vs_baseline": round(value / (stock * world), 4) if stock else None,
-        "dtype": _dtype_label(args),
-        "data": (f"synthetic 3x{args.image_size}x{args.image_size}, random-init weights; " +
-                 ("SyntheticImageNet index batches from DistributedSampler, images generated on device each step"
-                  if args.data == "sampler" else "two pre-made device-resident batches")),
-        "config": {"model": args.model, "global_batch": args.batch * world, "per_gpu_batch": args.batch,
-                   "seq_len": None, "image_size": args.image_size, "parallelism": f"dp{world}",
-                   "backend": args.backend, "optimizer": opt_name,
-                   "bucket_cap_mb": args.bucket_mb, "dist_backend": (torch.distributed.get_backend() if pdist_ready() else "none (no process group)"),
-                   "ddp": type(model).__name__ == "DistributedDataParallel",
-                   "rccl_version": _rccl_version(), "device": args.device,
-                   "final_loss": round(final_loss, 4), "hip_graph": args.graph, "graph_fallback": graph_fallback,
-                   "cpu_issue_ms_per_step": round(cpu_issue / args.steps * 1e3, 3),
-                   "host_enqueue_ms_idle_gpu": round(host_enqueue_ms, 3),
-                   "baseline": stock_ref,
-                   "vs_best_stock": ({"ratio": round(value / (best[0] * world), 4), "stock_img_s": best[0],
-                                      "stock_per_gpu_batch": best[1]} if best else None),
-                   "grad_allreduce_probe": ar,
-                   "max_mem_gib": round(torch.cuda.max_memory_allocated() / 2 ** 30, 2) if not cpu else None},
-    }
+    losses.update({"cpu_issue_ms_per_step": round(cpu_issue / args.steps * 1e3, 3),
+                   "host_enqueue_ms_idle_gpu": round(host_enqueue_ms, 3)})
+    rec = record(value, ms, losses)
     if rank == 0:
         line = json.dumps(rec)
         print(line, flush=True)

@@ -372,6 +372,7 @@ int run_halo(int hv, const NTParams& p_in, hipStream_t st) {
   NTParams p = p_in;
   p.div_HWm = make_fastdiv(p.Hs);  // the kernel divides global rows by H
   p.zero = zero_chunk_addr();
+  if (p.zero == nullptr) return PDT_ERR_SYMBOL;
   switch (hv) {
     case 0: return launch_halo<64, 256>(p, sgn, rs_log2, st);
     case 1: return launch_halo<128, 512>(p, sgn, rs_log2, st);
@@ -595,6 +596,7 @@ int run_halo_wgrad(const void* dy, const void* x, float* slab, int M, int Mo, in
   p.x = (const u16*)x;
   p.slab = slab;
   p.zero = zero_chunk_addr();
+  if (p.zero == nullptr) return PDT_ERR_SYMBOL;
   p.M = M; p.Mo = Mo; p.C = C; p.H = Hs; p.W = Ws;
   int l = 4, rs = 16;
   while (rs < Ws + 2) { rs <<= 1; ++l; }

@@ -123,14 +123,10 @@ __device__ __forceinline__ i32x8 cat8(const bf16x8& lo, const bf16x8& hi) {
 
 // 16 zero bytes: the global_load_lds source for padding / out-of-range rows
 static __device__ __attribute__((aligned(64))) u32x4 pdt_zero_chunk[4];
-// its device address (host side, resolved once per translation unit)
+// its device address on the current device (host side, cached per device; nullptr on failure)
 static inline const void* zero_chunk_addr() {
-  static const void* a = nullptr;
-  if (a == nullptr) {
-    void* d = nullptr;
-    if (hipGetSymbolAddress(&d, HIP_SYMBOL(pdt_zero_chunk)) == hipSuccess) a = d;
-  }
-  return a;
+  static const void* cache[PDT_MAX_DEV] = {};
+  return pdt_symbol_addr(HIP_SYMBOL(pdt_zero_chunk), cache);
 }
 
 // F8 = 0: bf16 operands. F8 = 1 / 2: fp8 operands (B = OCP e4m3; src = e4m3 / e5m2)
@@ -1132,6 +1128,7 @@ int launch(const NTParams& p, hipStream_t st) {
   int ntm = (p.M + BM - 1) / BM, ntn = (p.Ncol + BN - 1) / BN;
   NTParams q = p;
   q.zero = zero_chunk_addr();
+  if (q.zero == nullptr) return PDT_ERR_SYMBOL;
   hipLaunchKernelGGL((conv_nt_kernel<BM, BN, NS, CS64, DIRECT, GLDS, NTH, WM, F8, PIPE, BNB, AX>),
                      dim3(ntm * ntn), dim3(NTH), 0, st, q);
   PDT_RETURN_LAUNCH();

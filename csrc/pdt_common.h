@@ -151,3 +151,20 @@ __device__ __forceinline__ uint32_t xcd_remap(uint32_t bid, uint32_t nwg) {
 }
 
 #define PDT_RETURN_LAUNCH() return (int)hipGetLastError()
+
+// Launcher error code: a __device__ symbol's address could not be resolved (the kernel is
+// not launched -- a null LDS-DMA source would fault on the GPU).
+#define PDT_ERR_SYMBOL (-7)
+#define PDT_MAX_DEV 64
+
+// Device address of a __device__ symbol, cached per device id (each device the code object
+// is loaded on has its own copy of the symbol). nullptr if the lookup fails.
+static inline const void* pdt_symbol_addr(const void* sym, const void** cache) {
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= PDT_MAX_DEV) return nullptr;
+  if (cache[dev] == nullptr) {
+    void* d = nullptr;
+    if (hipGetSymbolAddress(&d, sym) == hipSuccess) cache[dev] = d;
+  }
+  return cache[dev];
+}

@@ -320,14 +320,11 @@ constexpr WG8Var WG8_VARS[WG8_NVAR] = {
 WG8Var wg8_variant(int v) { return (v < 0 || v >= WG8_NVAR) ? WG8_VARS[0] : WG8_VARS[v]; }
 
 template <bool BIAS>
-void launch8(const WG8Var& w, dim3 grid, const WG8Params& p_in, hipStream_t st) {
-  static const void* zaddr = nullptr;
-  if (zaddr == nullptr) {
-    void* d = nullptr;
-    if (hipGetSymbolAddress(&d, HIP_SYMBOL(wg8_zero_chunk)) == hipSuccess) zaddr = d;
-  }
+int launch8(const WG8Var& w, dim3 grid, const WG8Params& p_in, hipStream_t st) {
+  static const void* cache[PDT_MAX_DEV] = {};
   WG8Params p = p_in;
-  p.zero = zaddr;
+  p.zero = pdt_symbol_addr(HIP_SYMBOL(wg8_zero_chunk), cache);
+  if (p.zero == nullptr) return PDT_ERR_SYMBOL;
 #define L8(a, b, ns, t, wm) hipLaunchKernelGGL((wgrad_f8_kernel<a, b, ns, t, wm, BIAS>), grid, dim3(t), 0, st, p)
 #define G8(a, b, ns, t, wm) hipLaunchKernelGGL((wgrad_f8_kernel<a, b, ns, t, wm, BIAS, 1, true>), grid, dim3(t), 0, st, p)
   if (w.GL) {
@@ -360,6 +357,7 @@ void launch8(const WG8Var& w, dim3 grid, const WG8Params& p_in, hipStream_t st) 
   }
 #undef L8
 #undef G8
+  return 0;
 }
 
 int reduce_groups8(int splits, int Mo, int No) {
@@ -425,8 +423,8 @@ PDT_API int pdt_linear_wgrad_f8(const void* dy8, const void* x8, const float* dq
   }
   const int tiles = ((Mo + w.BM - 1) / w.BM) * ((No + w.BN - 1) / w.BN);
   dim3 grid(tiles * splits);
-  if (bias_out) launch8<true>(w, grid, p, stream);
-  else launch8<false>(w, grid, p, stream);
+  const int lrc = bias_out ? launch8<true>(w, grid, p, stream) : launch8<false>(w, grid, p, stream);
+  if (lrc) return lrc;
   int e = (int)hipGetLastError();
   if (e) return e;
   return pdt_wgrad_reduce(slab, out, p.bslab, bias_out, splits, Mo, No, 1.f, accumulate, stream);

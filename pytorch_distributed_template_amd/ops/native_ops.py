@@ -2947,19 +2947,32 @@ class _TargetCheck:
         ev.record()
         self.pending.append((ev, host))
 
-    def poll(self):
+    MAX_PENDING = 64  # beyond this the oldest check is waited for (never dropped)
+
+    def poll(self, block=False):
+        """Raise if any finished check saw an out-of-range target. ``block``: wait for every
+        pending check (end of an epoch / run: the last batches' checks are read too). Every
+        check is kept until it has been read; when more than MAX_PENDING are queued the
+        oldest is waited for instead of dropped."""
         if _capturing():
             return
         keep = []
-        for ev, host in self.pending:
-            if not ev.query():
+        for i, (ev, host) in enumerate(self.pending):
+            if not (block or len(self.pending) - i > self.MAX_PENDING) and not ev.query():
                 keep.append((ev, host))
                 continue
+            ev.synchronize()
             if float(host[0]):
                 self.pending = []
                 raise ValueError(f"nll_loss: {int(host[0])} target(s) out of range [0, num_classes) "
                                  "in an earlier batch (its loss was NaN)")
-        self.pending = keep[-8:]
+        self.pending = keep
+
+
+def check_targets_pending():
+    """Read every outstanding NLL target check (blocking); raises on an out-of-range target.
+    The Trainer calls it at the end of each epoch."""
+    _TARGETS.poll(block=True)
 
 
 _TARGETS = _TargetCheck()

@@ -21,6 +21,11 @@ current lr (the host rewrites it, outside the graph, in ``refresh_scalars()`` --
 called by every eager ``step()`` too) and with the bias corrections of the current
 step (t is incremented on the device, in the graph). ``state_dict()`` writes the
 device step count back into each parameter's ``step`` so checkpoints stay torch's.
+Capturable Adam keeps ONE step count per param group, so it requires every parameter of
+a group to receive a gradient on every step (a captured graph assumes that anyway):
+``step()`` raises if the set of parameters with gradients changes between steps --
+torch's per-parameter counts would diverge from the group count there, and a checkpoint
+reloaded into torch.optim would apply different bias corrections.
 """
 from __future__ import annotations
 
@@ -116,6 +121,7 @@ class _FusedBase(Optimizer):
         self._shadows = {}
         self._dev = {}      # capturable: group index -> device [lr, t]
         self._dev_lr = {}   # the lr last written into it
+        self._grad_sets = {}  # capturable Adam: group index -> ids of the params stepped first
 
     def _dev_scalars(self, gi, group, device, t0=0.0):
         """The group's device [lr, t] (created from the host values on first use)."""
@@ -302,6 +308,14 @@ class FusedAdam(_FusedBase):
             b1, b2 = group["betas"]
             native = _native_ok(params)
             dev_step = self.capturable and native
+            if dev_step:
+                key = tuple(id(p) for p in params)
+                seen = self._grad_sets.setdefault(gi, key)
+                if seen != key:
+                    raise RuntimeError(
+                        "capturable FusedAdam: the set of parameters with gradients changed between steps "
+                        f"(group {gi}: {len(seen)} -> {len(key)} params); the group's single device step "
+                        "count requires every parameter to receive a gradient on every step")
             for p in params:
                 st = self.state[p]
                 if len(st) == 0:

@@ -44,6 +44,53 @@ from ..utils.profiling import PhaseTimer
 GRAPH_WARMUP = 11  # eager steps before the capture (DDP's runtime statistics cover iterations 1..10)
 
 
+class _LossCurve:
+    """The per-iteration ``loss/train`` scalar of the reference (``trainer.py:60-62`` ->
+    ``MetricTracker.update`` -> ``writer.add_scalar``) without its per-iteration host sync:
+    every ``log_step`` iterations the rank-mean loss is copied device -> pinned host
+    (non-blocking, behind the step's kernels) and written once that copy has landed --
+    checked at the next log point, flushed at the end of the epoch. On CPU it is written
+    at once (no device to wait for)."""
+
+    def __init__(self, writer, device, enabled):
+        self.writer = writer
+        self.device = device
+        self.enabled = bool(enabled)  # the same on every rank (it gates a collective)
+        self._pending = []  # (global step, pinned host scalar, event)
+
+    def push(self, step, loss):
+        if not self.enabled:
+            return
+        mean = pdist.all_reduce_mean(loss.detach().float().reshape(1))  # collective: every rank
+        if not pdist.is_main_process() or getattr(self.writer, "writer", None) is None:
+            return
+        if self.device.type != "cuda":
+            self._write(step, float(mean.item()))
+            return
+        host = torch.empty(1, dtype=torch.float32, pin_memory=True)
+        host.copy_(mean, non_blocking=True)
+        ev = torch.cuda.Event()
+        ev.record()
+        self._pending.append((step, host, ev))
+        self.drain(block=False)
+
+    def drain(self, block=False):
+        while self._pending:
+            step, host, ev = self._pending[0]
+            if not block and not ev.query():
+                return
+            ev.synchronize()
+            self._write(step, float(host[0]))
+            self._pending.pop(0)
+
+    def _write(self, step, value):
+        w = self.writer
+        saved = (w.step, w.mode)
+        w.step, w.mode = step, "train"
+        w.add_scalar("loss", value)
+        w.step, w.mode = saved
+
+
 
 class Trainer(BaseTrainer):
     def __init__(self, model, criterion, metric_ftns, optimizer, config, device,
@@ -66,6 +113,7 @@ class Trainer(BaseTrainer):
         self.channels_last = channels_last
 
         self.train_metrics = MetricTracker("loss", writer=self.writer)
+        self.loss_curve = _LossCurve(self.writer, device, config["trainer"].get("tensorboard", False))
         self.valid_metrics = MetricTracker("loss", *[m.__name__ for m in self.metric_ftns], writer=self.writer)
         self.last_throughput = None
         # optional per-phase device timing (HIP events + ROCTx ranges): trainer.profile_phases
@@ -141,8 +189,11 @@ class Trainer(BaseTrainer):
             n_iter += 1
             n_images += data.shape[0]
 
+            gstep = (epoch - 1) * self.len_epoch + batch_idx
             if pdist.is_main_process():
-                self.writer.set_step((epoch - 1) * self.len_epoch + batch_idx)
+                self.writer.set_step(gstep)
+            if batch_idx % self.log_step == 0:
+                self.loss_curve.push(gstep, loss)
             if batch_idx % self.log_step == 0 and self.logger.isEnabledFor(10):  # DEBUG
                 loss_reduced = self.reduce_loss(loss)
                 if pdist.is_main_process():
@@ -161,8 +212,13 @@ class Trainer(BaseTrainer):
             dt = time.perf_counter() - t_start
             self.last_throughput = n_images * pdist.get_world_size() / max(dt, 1e-9)
 
+        self.loss_curve.drain(block=True)
+        if self.device.type == "cuda":
+            from ..ops.native_ops import check_targets_pending
+            check_targets_pending()  # the epoch's last NLL target checks (native loss)
         mean_loss = pdist.all_reduce_mean(loss_sum / max(n_iter, 1))
-        self.train_metrics.update("loss", mean_loss.item(), n=1)
+        # the TB curve got its per-log-step points above: the epoch mean is not written again
+        self.train_metrics.update("loss", mean_loss.item(), n=1, write=False)
         log = self.train_metrics.result()
         if self.last_throughput is not None:
             log["images_per_sec"] = round(self.last_throughput, 2)
@@ -196,7 +252,12 @@ class Trainer(BaseTrainer):
         the batch is then replayed like every later one); a replay otherwise."""
         cur = torch.cuda.current_stream(self.device)
         side = self._side
-        if self._graph is None and self._graph_eager_steps >= GRAPH_WARMUP:
+        # capture only a FULL batch (the loader's batch_size): a partial last batch captured
+        # here would fix the graph to the short shape and every later full batch would run
+        # eagerly; a partial batch arriving after the warm-up runs eagerly and the capture
+        # waits for the next full one
+        full = data.shape[0] == getattr(self._base_loader, "batch_size", data.shape[0])
+        if self._graph is None and self._graph_eager_steps >= GRAPH_WARMUP and full:
             side.wait_stream(cur)
             with torch.cuda.stream(side):
                 self._capture(data, target)

@@ -67,9 +67,9 @@ class MetricTracker:
             self._counts[key] = 0
             self._pending[key] = []
 
-    def update(self, key, value, n=1):
+    def update(self, key, value, n=1, write=True):
         self._ensure(key)
-        if self.writer is not None:
+        if self.writer is not None and write:
             self.writer.add_scalar(key, value)
         if isinstance(value, torch.Tensor):
             self._pending[key].append(value.detach().float() * n)

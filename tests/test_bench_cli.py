@@ -76,3 +76,30 @@ def test_bench_one_rank_runs_ddp_over_a_process_group():
     assert r.returncode == 0, r.stderr[-3000:]
     rec = _json_line(r.stdout)
     assert rec["config"]["ddp"] is False and rec["config"]["dist_backend"].startswith("none")
+
+
+def test_bench_eight_cpu_ranks_one_json_line():
+    """The driver's N = 8 launch, rehearsed on 8 gloo ranks: one JSON line from rank 0 with
+    the whole-job numbers (dp8), finite first / last losses."""
+    r = subprocess.run([sys.executable, BENCH, "--gpus", "8", "--device", "cpu", "--batch", "2", "--image-size", "32",
+                        "--steps", "2", "--warmup", "1"], cwd=ROOT, env=_env(), capture_output=True, text=True,
+                       timeout=900)
+    assert r.returncode == 0, r.stderr[-3000:]
+    rec = _json_line(r.stdout)
+    assert rec["n_gpus"] == 8 and rec["config"]["parallelism"] == "dp8"
+    assert rec["config"]["global_batch"] == 16
+    assert rec["config"]["loss_first"] is not None and rec["config"]["loss_last"] is not None
+    assert rec["config"]["grad_allreduce_probe"] is None  # CPU ranks: no RCCL probe
+
+
+def test_bench_refuses_a_nan_step():
+    """A diverged step (lr 1e30 -> NaN loss) is reported with value null and a non-zero exit,
+    never as throughput."""
+    r = subprocess.run([sys.executable, BENCH, "--gpus", "1", "--device", "cpu", "--batch", "2", "--image-size", "32",
+                        "--steps", "2", "--warmup", "2", "--lr", "1e30"], cwd=ROOT, env=_env(), capture_output=True,
+                       text=True, timeout=600)
+    assert r.returncode == 3, (r.returncode, r.stderr[-2000:])
+    rec = _json_line(r.stdout)
+    assert rec["value"] is None and rec["vs_baseline"] is None
+    assert "non-finite" in rec["error"]
+    assert rec["config"]["loss_last"] is None

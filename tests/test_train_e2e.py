@@ -88,3 +88,16 @@ def test_legacy_local_rank_flag_accepted(tmp_path):
     cfg = _cfg(tmp_path, epochs=1, monitor="off")
     _run(["train.py", "-c", str(cfg), "--local-rank=0", "--no-validate"], {"PDT_RUN_ID": "lr1"})
     _run(["train.py", "-c", str(cfg), "--local_rank", "0", "--no-validate"], {"PDT_RUN_ID": "lr2"})
+
+
+def test_tensorboard_loss_curve_per_log_step(tmp_path):
+    """loss/train is written every log_step iterations (reference trainer.py:60-62 writes it
+    every iteration), not once per epoch: 2048 synthetic images / batch 128 = 16 iterations,
+    log_step = int(sqrt(128)) = 11 -> iterations 0 and 11 of each epoch."""
+    cfg = _cfg(tmp_path, epochs=2, monitor="off")
+    _run(["train.py", "-c", str(cfg), "--no-validate"], {"PDT_RUN_ID": "tb"})
+    run = tmp_path / "saved" / "Mnist_LeNet_cpu" / "train" / "tb"
+    recs = [json.loads(ln) for ln in (run / "scalars.jsonl").read_text().splitlines()]
+    loss = [r for r in recs if r["tag"] == "loss/train"]
+    assert [r["step"] for r in loss] == [0, 11, 16, 27], loss
+    assert all(r["value"] > 0 for r in loss)
