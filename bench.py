@@ -306,7 +306,7 @@ def main():
     from pytorch_distributed_template_amd.utils import dist as pdist
     from pytorch_distributed_template_amd.ops import fused
     from pytorch_distributed_template_amd import models
-    from pytorch_distributed_template_amd.parallel import pretune_for_ddp, wrap_ddp
+    from pytorch_distributed_template_amd.parallel import is_data_parallel, pretune_for_ddp, wrap_ddp
     from pytorch_distributed_template_amd.data.synthetic import SyntheticImageLoader, SyntheticImageNetLoader
 
     cpu = args.device == "cpu"
@@ -505,7 +505,7 @@ def main():
                "backend": args.backend, "optimizer": opt_name,
                "bucket_cap_mb": args.bucket_mb,
                "dist_backend": (torch.distributed.get_backend() if pdist_ready() else "none (no process group)"),
-               "ddp": type(model).__name__ == "DistributedDataParallel",
+               "ddp": is_data_parallel(model), "ddp_impl": type(model).__name__ if is_data_parallel(model) else None,
                "rccl_version": _rccl_version(), "device": args.device,
                "hip_graph": args.graph, "graph_fallback": graph_fallback, "graph_check": graph_check,
                "baseline": stock_ref,

@@ -223,6 +223,20 @@ def _chk(rc, name):
         raise RuntimeError(f"{name} failed with code {rc}")
 
 
+def _grad_buf(param, shape, memory_format=None):
+    """fp32 output buffer for ``param``'s gradient: its slot in the data-parallel reducer's
+    bucket when it has one (``parallel/reducer.py``: the kernel then writes the gradient where
+    the all-reduce reads it, and autograd adopts that view as ``param.grad`` with no copy),
+    else a new tensor of ``shape``."""
+    if param is not None and getattr(param, "_pdt_grad_slot", None) is not None:
+        from ..parallel.reducer import grad_out
+        return grad_out(param, *shape, memory_format=memory_format)
+    dev = param.device if param is not None else None
+    if memory_format is not None:
+        return torch.empty(shape, dtype=torch.float32, device=dev, memory_format=memory_format)
+    return torch.empty(shape, dtype=torch.float32, device=dev)
+
+
 _FALLBACK_WARNED: set = set()
 
 
@@ -1013,7 +1027,7 @@ class _BNArgs:
 
 class _Unit:
     """Saved state of one conv->BN->act unit between forward and backward."""
-    __slots__ = ("x", "w", "gamma", "y", "act", "mask", "mean", "invstd", "scale", "shift", "N", "C", "Cs", "H",
+    __slots__ = ("x", "w", "gamma", "beta", "y", "act", "mask", "mean", "invstd", "scale", "shift", "N", "C", "Cs", "H",
                  "W", "Cout", "g", "relu", "has_res", "bnb_pre", "pend", "res_unit", "__weakref__")
 
 
@@ -1080,7 +1094,7 @@ def _unit_fwd(x, w, gamma, beta, residual, conv, relu, bna: _BNArgs, apply: bool
     assert y.numel() == M * Cout
     if not apply:  # the consumer applies the BN affine (+ReLU) itself (stem max-pool)
         u = _Unit()
-        u.x, u.w, u.gamma, u.y = x, w, gamma, y
+        u.x, u.w, u.gamma, u.beta, u.y = x, w, gamma, beta, y
         u.act, u.mask, u.bnb_pre, u.pend, u.res_unit = None, None, None, None, None
         u.mean, u.invstd, u.scale, u.shift = mean, invstd, scale, shift
         u.N, u.C, u.Cs, u.H, u.W, u.Cout, u.g, u.relu, u.has_res = N, C, Cs, H, W, Cout, g, relu, False
@@ -1106,7 +1120,7 @@ def _unit_fwd(x, w, gamma, beta, residual, conv, relu, bna: _BNArgs, apply: bool
     else:
         _chk(lib.pdt_bn_apply(_p(y), _p(res), _p(out), _p(scale), _p(shift), M, Cout, int(relu), _p(mask), st),
              "bn_apply")
-    u.x, u.w, u.gamma, u.y = x, w, gamma, y
+    u.x, u.w, u.gamma, u.beta, u.y = x, w, gamma, beta, y
     u.act = None
     u.mask = mask
     u.res_unit = res_unit  # the downsample unit whose raw output is this unit's residual (or None)
@@ -1139,8 +1153,9 @@ def _bn_bwd(dA, u: _Unit, want_dres: bool, mask=None, pre: _BnbPartials | None =
         part = torch.empty(2 * blocks * Cout + lib.pdt_rows_reduce_workspace(blocks, Cout), **f32)
         _chk(lib.pdt_bn_bwd_reduce(_p(dA), _p(u.y), _p(u.act), _p(u.mean), _p(u.scale), _p(u.shift), _p(part), M,
                                    Cout, int(relu), blocks, _p(mask), st), "bn_bwd_reduce")
-    vec = torch.empty((5, Cout), **f32)
-    dgamma, dbeta, k1, k2, k3 = vec[0], vec[1], vec[2], vec[3], vec[4]
+    vec = torch.empty((3, Cout), **f32)
+    k1, k2, k3 = vec[0], vec[1], vec[2]
+    dgamma, dbeta = _grad_buf(u.gamma, (Cout,)), _grad_buf(u.beta, (Cout,))
     _chk(lib.pdt_bn_bwd_finalize(_p(part), blocks, Cout, float(M), _p(u.gamma), _p(u.mean), _p(u.invstd),
                                  _p(dgamma), _p(dbeta), _p(k1), _p(k2), _p(k3), 0, st), "bn_bwd_finalize")
     if coeffs_only:
@@ -1172,8 +1187,9 @@ def _bn_bwd_pool(dout, idx, u: _Unit, k, s, p):
     part = torch.empty(2 * blocks * C + lib.pdt_rows_reduce_workspace(blocks, C), **f32)
     _chk(lib.pdt_bn_bwd_reduce_pool(_p(dout), _p(idx), _p(u.y), _p(u.mean), _p(u.scale), _p(u.shift), _p(part),
                                     N, H, W, C, Ho, Wo, k, s, p, blocks, st), "bn_bwd_reduce_pool")
-    vec = torch.empty((5, C), **f32)
-    dgamma, dbeta, k1, k2, k3 = vec[0], vec[1], vec[2], vec[3], vec[4]
+    vec = torch.empty((3, C), **f32)
+    k1, k2, k3 = vec[0], vec[1], vec[2]
+    dgamma, dbeta = _grad_buf(u.gamma, (C,)), _grad_buf(u.beta, (C,))
     _chk(lib.pdt_bn_bwd_finalize(_p(part), blocks, C, float(M), _p(u.gamma), _p(u.mean), _p(u.invstd),
                                  _p(dgamma), _p(dbeta), _p(k1), _p(k2), _p(k3), 0, st), "bn_bwd_finalize")
     dy = torch.empty_like(u.y, memory_format=torch.channels_last)
@@ -1464,13 +1480,13 @@ def _unit_dw(dy, u: _Unit):
     w = u.w
     KH, KW = u.g["KH"], u.g["KW"]
     if u.Cs == u.C and w.is_contiguous(memory_format=torch.channels_last):
-        dw = torch.empty_like(w, dtype=torch.float32, memory_format=torch.channels_last)
+        dw = _grad_buf(w, tuple(w.shape), torch.channels_last)
         _conv_wgrad(dy, u.x, u.N, u.H, u.W, u.Cs, u.Cout, u.g, dw)
     else:
         tmp = torch.empty((u.Cout, u.Cs, KH, KW), dtype=torch.float32, device=dy.device,
                           memory_format=torch.channels_last)
         _conv_wgrad(dy, u.x, u.N, u.H, u.W, u.Cs, u.Cout, u.g, tmp)
-        dw = tmp[:, :u.C].contiguous(memory_format=torch.channels_last) if u.Cs != u.C else tmp
+        dw = _grad_buf(w, tuple(w.shape), torch.channels_last).copy_(tmp[:, :u.C]) if u.Cs != u.C else tmp
     return dw.to(w.dtype) if dw.dtype != w.dtype else dw
 
 
@@ -1889,7 +1905,7 @@ def _unit_fwd_s2d(x, w, gamma, beta, bna: _BNArgs):
         scale = (gamma.float() * invstd).contiguous()
         shift = (beta.float() - mean * scale).contiguous()
     u = _Unit()
-    u.x, u.w, u.gamma, u.y = x4, w, gamma, y
+    u.x, u.w, u.gamma, u.beta, u.y = x4, w, gamma, beta, y
     u.act, u.mask, u.bnb_pre = None, None, None
     u.mean, u.invstd, u.scale, u.shift = mean, invstd, scale, shift
     g = dict(KH=7, KW=7, sh=2, sw=2, ph=3, pw=3, Ho=Ho, Wo=Wo, s2d=True)
@@ -1924,7 +1940,7 @@ def _unit_dw_s2d(dy, u: _Unit, bn_dA=None):
             conv_wgrad(apply_pass(), u.x, dw256, **g)
     else:
         conv_wgrad(dy, u.x, dw256, **g)
-    dw = _s2d_unfold_grad(dw256, u.C).contiguous(memory_format=torch.channels_last)
+    dw = _grad_buf(u.w, tuple(u.w.shape), torch.channels_last).copy_(_s2d_unfold_grad(dw256, u.C))
     return dw.to(u.w.dtype) if dw.dtype != u.w.dtype else dw
 
 
@@ -2065,19 +2081,19 @@ def _linear_dgrad(dy2, w):
     return dx
 
 
-def _linear_wgrad(dy2, x2, w, with_bias=False):
+def _linear_wgrad(dy2, x2, w, with_bias=False, bias=None):
     """(dW fp32 [Nout][K], db fp32 [Nout] or None): db comes out of the same kernel."""
     Nout, K = w.shape
-    dw = torch.empty((Nout, K), dtype=torch.float32, device=dy2.device)
-    db = torch.empty(Nout, dtype=torch.float32, device=dy2.device) if with_bias else None
+    dw = _grad_buf(w, (Nout, K))
+    db = _grad_buf(bias, (Nout,)) if with_bias else None
     conv_wgrad(dy2, x2, dw, M=dy2.shape[0], Mo=Nout, No=K, ldy=Nout, Hs=1, Ws=1, C=K, Hm=1, Wm=1, sh=1, sw=1,
                oh0=0, ow0=0, dh=1, dw=1, ntw=1, bias_out=db)
     return dw, db
 
 
-def _linear_grads(dy2, x2, w, want_db, want_dw):
+def _linear_grads(dy2, x2, w, want_db, want_dw, bias=None):
     if want_dw:
-        dw, db = _linear_wgrad(dy2, x2, w, with_bias=want_db)
+        dw, db = _linear_wgrad(dy2, x2, w, with_bias=want_db, bias=bias)
         return dw, db
     return None, (colsum(dy2, dy2.shape[0], w.shape[0]) if want_db else None)
 
@@ -2106,6 +2122,7 @@ class _Linear(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, x, w, b, act, residual):
+        ctx.bref = b  # the bias parameter: its gradient goes to its reducer slot
         shp = x.shape
         x2 = x.reshape(-1, shp[-1]).to(torch.bfloat16).contiguous()
         Mrows, K = x2.shape
@@ -2135,7 +2152,8 @@ class _Linear(torch.autograd.Function):
             dy2 = dz
         Mrows = dy2.shape[0]
         dx = _linear_dgrad(dy2, w).reshape(*shp[:-1], K) if ctx.needs_input_grad[0] else None
-        dw, db = _linear_grads(dy2, x2, w, has_b and ctx.needs_input_grad[2], ctx.needs_input_grad[1])
+        dw, db = _linear_grads(dy2, x2, w, has_b and ctx.needs_input_grad[2], ctx.needs_input_grad[1],
+                               bias=ctx.bref)
         return dx, dw, db, None, (dy if ctx.needs_input_grad[4] else None)
 
 
@@ -2268,7 +2286,7 @@ def _wgrad_f8_launch(lib, dyq, xq, dq_dy, dq_x, dy16, dw, db, v):
                                  Mo, No, splits, kps.value, 0, int(v), _s()), "linear_wgrad_f8")
 
 
-def linear_wgrad_f8(dyq, xq, dq_dy, dq_x, dy16=None, with_bias=False, variant=None):
+def linear_wgrad_f8(dyq, xq, dq_dy, dq_x, dy16=None, with_bias=False, variant=None, w=None, b=None):
     """(dW fp32 [Nout][K], db fp32 [Nout] or None) of nn.Linear from the fp8 codes the
     data-gradient and forward GEMMs consumed: dyq [M][Nout] e5m2, xq [M][K] e4m3, device
     dequant scales. db = column sums of the bf16 ``dy16`` (csrc/wgrad_f8.hip)."""
@@ -2279,8 +2297,10 @@ def linear_wgrad_f8(dyq, xq, dq_dy, dq_x, dy16=None, with_bias=False, variant=No
     if with_bias:
         assert dy16 is not None and dy16.dtype == torch.bfloat16 and dy16.shape == (M, Nout) and dy16.is_contiguous()
     lib = _load()
-    dw = torch.empty((Nout, K), dtype=torch.float32, device=dyq.device)
-    db = torch.empty(Nout, dtype=torch.float32, device=dyq.device) if with_bias else None
+    dw = _grad_buf(w, (Nout, K)) if w is not None else torch.empty((Nout, K), dtype=torch.float32,
+                                                                  device=dyq.device)
+    db = (_grad_buf(b, (Nout,)) if b is not None else torch.empty(Nout, dtype=torch.float32, device=dyq.device)) \
+        if with_bias else None
     if variant is None:
         key = f"wg8:{M},{Nout},{K}"
         table = _tuned()
@@ -2331,6 +2351,7 @@ def _quant_grad(g2, owner, attr, src=None):
 class _LinearF8(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, w, b, act, fc, residual):
+        ctx.bref = b
         shp = x.shape
         x2 = x.reshape(-1, shp[-1]).to(torch.bfloat16).contiguous()
         Mrows, K = x2.shape
@@ -2386,11 +2407,11 @@ class _LinearF8(torch.autograd.Function):
             dx = dx.reshape(*shp[:-1], K)
         want_db = has_b and need[2]
         if ctx.f8w and need[1]:
-            dw, db = linear_wgrad_f8(dyq, ctx.xq, dqdy, ctx.dqx, dy16=dy2, with_bias=want_db)
+            dw, db = linear_wgrad_f8(dyq, ctx.xq, dqdy, ctx.dqx, dy16=dy2, with_bias=want_db, w=w, b=ctx.bref)
         elif ctx.f8w:
             dw, db = None, (colsum(dy2, Mrows, Nout) if want_db else None)
         else:
-            dw, db = _linear_grads(dy2, x2, w, want_db, need[1])
+            dw, db = _linear_grads(dy2, x2, w, want_db, need[1], bias=ctx.bref)
         ctx.xq = ctx.dqx = None
         return dx, dw, db, None, None, (dy if need[5] else None)
 
@@ -2421,6 +2442,7 @@ def linear(x, fc: nn.Linear, act=None, fp8=False, residual=None):
 class _Mlp(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, w1, b1, w2, b2, residual, mlp, fp8):
+        ctx.brefs = (b1, b2)
         shp = x.shape
         x2 = x.reshape(-1, shp[-1]).to(torch.bfloat16).contiguous()
         Mrows, K = x2.shape
@@ -2484,10 +2506,11 @@ class _Mlp(torch.autograd.Function):
         else:
             _gemm_bf16(g2, bf16_weight_t(w2), dz, act=3, addend=z)  # dz = (g W2) * gelu'(z)
         if f8 is not None:
-            dw2, db2 = linear_wgrad_f8(gq, f8[2], dqg, f8[3], dy16=g2, with_bias=need[4]) if need[3] \
+            dw2, db2 = linear_wgrad_f8(gq, f8[2], dqg, f8[3], dy16=g2, with_bias=need[4], w=w2,
+                                       b=ctx.brefs[1]) if need[3] \
                 else (None, colsum(g2, Mrows, Nout) if need[4] else None)
         else:
-            dw2, db2 = _linear_grads(g2, a, w2, need[4], need[3])
+            dw2, db2 = _linear_grads(g2, a, w2, need[4], need[3], bias=ctx.brefs[1])
         dx = None
         if dzq is None and ctx.fp8_dgrad and (need[0] or (f8 is not None and need[1])):
             dzq, dqdz = _quant_grad(dz, ctx.mlp.fc1, "_pdt_fp8_gmeta")
@@ -2500,10 +2523,11 @@ class _Mlp(torch.autograd.Function):
                 _gemm_bf16(dz, bf16_weight_t(w1), dx)
             dx = dx.reshape(ctx.shp)
         if f8 is not None:
-            dw1, db1 = linear_wgrad_f8(dzq, f8[0], dqdz, f8[1], dy16=dz, with_bias=need[2]) if need[1] \
+            dw1, db1 = linear_wgrad_f8(dzq, f8[0], dqdz, f8[1], dy16=dz, with_bias=need[2], w=w1,
+                                       b=ctx.brefs[0]) if need[1] \
                 else (None, colsum(dz, Mrows, Hd) if need[2] else None)
         else:
-            dw1, db1 = _linear_grads(dz, x2, w1, need[2], need[1])
+            dw1, db1 = _linear_grads(dz, x2, w1, need[2], need[1], bias=ctx.brefs[0])
         ctx.f8 = None
         return dx, dw1, db1, dw2, db2, (g if need[5] else None), None, None
 
@@ -2529,6 +2553,7 @@ def mlp(x, m, fp8=False, residual=None):
 class _LayerNorm(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, g, b, eps):
+        ctx.refs = (g, b)  # the affine parameters: their gradients go to their reducer slots
         shp = x.shape
         D = shp[-1]
         x2 = x.reshape(-1, D).to(torch.bfloat16).contiguous()
@@ -2552,8 +2577,7 @@ class _LayerNorm(torch.autograd.Function):
         dx = torch.empty_like(x2)
         blocks = lib.pdt_ln_bwd_blocks(rows)
         part = torch.empty(2 * blocks * D, dtype=torch.float32, device=dy.device)
-        dg = torch.empty(D, dtype=torch.float32, device=dy.device)
-        db = torch.empty(D, dtype=torch.float32, device=dy.device)
+        dg, db = _grad_buf(ctx.refs[0], (D,)), _grad_buf(ctx.refs[1], (D,))
         _chk(lib.pdt_ln_bwd(_p(dy2), _p(x2), _p(gf), _p(stats[0]), _p(stats[1]), _p(dx), _p(dg), _p(db), _p(part),
                             rows, D, 0, None, _s()), "ln_bwd")
         return dx.reshape(ctx.shp), dg, db, None
@@ -2575,6 +2599,7 @@ class _LNFork(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, x, g, b, eps, f8meta, f8box, grad_owner):
+        ctx.refs = (g, b)
         shp = x.shape
         D = shp[-1]
         x2 = x.reshape(-1, D).contiguous()
@@ -2612,8 +2637,7 @@ class _LNFork(torch.autograd.Function):
         dx = torch.empty_like(x2)
         blocks = lib.pdt_ln_bwd_blocks(rows)
         part = torch.empty(2 * blocks * D, dtype=torch.float32, device=dev)
-        dg = torch.empty(D, dtype=torch.float32, device=dev)
-        db = torch.empty(D, dtype=torch.float32, device=dev)
+        dg, db = _grad_buf(ctx.refs[0], (D,)), _grad_buf(ctx.refs[1], (D,))
         owner = ctx.grad_owner
         gmeta = getattr(owner, "_pdt_fp8_gmeta", None) if owner is not None else None
         if gmeta is not None and fp8_settings()["scaling"] == "delayed":

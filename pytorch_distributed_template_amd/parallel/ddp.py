@@ -23,24 +23,43 @@ MI355X node instead of NVSwitch defaults:
 """
 from __future__ import annotations
 
+import os
+
 import torch
 from torch.nn.parallel import DistributedDataParallel
 
 from ..utils.dist import get_world_size, is_dist_ready
 
 DEFAULT_BUCKET_MB = 64
+# the first bucket (the classifier and the last stage: the gradients backward produces first)
+# starts moving while the rest of backward runs
+DEFAULT_FIRST_BUCKET_MB = 8
 
 
 def wrap_ddp(model: torch.nn.Module, device: torch.device, bucket_cap_mb: float = DEFAULT_BUCKET_MB,
              broadcast_buffers: bool = True, gradient_as_bucket_view: bool = True,
              comm_hook: str | None = None, static_graph: bool = False,
-             find_unused_parameters: bool = False):
-    """Wrap in DDP whenever a process group exists -- a 1-rank RCCL group too
-    (``torchrun --nproc-per-node 1``, ``bench.py --gpus 1``): the reducer, its
-    bucket views and the RCCL all-reduce on its own stream then run at N = 1
-    exactly as at N > 1. Without a process group the model is returned unchanged."""
+             find_unused_parameters: bool = False, impl: str | None = None,
+             first_bucket_mb: float = DEFAULT_FIRST_BUCKET_MB):
+    """Wrap for data parallelism whenever a process group exists -- a 1-rank RCCL group too
+    (``torchrun --nproc-per-node 1``, ``bench.py --gpus 1``): the reducer, its buckets and the
+    RCCL all-reduce then run at N = 1 exactly as at N > 1. Without a process group the model
+    is returned unchanged.
+
+    ``impl``: ``"native"`` (default; ``PDT_DDP`` overrides) is the framework's reducer
+    (``parallel/reducer.py``: gradients written by the native kernels straight into aligned
+    bucket slots, ``ReduceOp.AVG`` all-reduce, a small first bucket); ``"torch"`` is torch's
+    ``DistributedDataParallel`` with the same bucket size (kept for A/B runs and for the
+    compression comm hooks, which only it implements)."""
     if not is_dist_ready():
         return model
+    impl = impl or os.environ.get("PDT_DDP", "native")
+    if comm_hook in ("bf16", "fp16"):
+        impl = "torch"
+    if impl == "native":
+        from .reducer import DataParallel
+        return DataParallel(model, device, bucket_cap_mb=bucket_cap_mb, first_bucket_mb=first_bucket_mb,
+                            broadcast_buffers=broadcast_buffers)
     kwargs = dict(bucket_cap_mb=bucket_cap_mb, broadcast_buffers=broadcast_buffers,
                   gradient_as_bucket_view=gradient_as_bucket_view, static_graph=static_graph,
                   find_unused_parameters=find_unused_parameters)
@@ -52,6 +71,11 @@ def wrap_ddp(model: torch.nn.Module, device: torch.device, bucket_cap_mb: float 
         hook = default_hooks.bf16_compress_hook if comm_hook == "bf16" else default_hooks.fp16_compress_hook
         ddp.register_comm_hook(state=None, hook=hook)
     return ddp
+
+
+def is_data_parallel(model) -> bool:
+    from .reducer import DataParallel
+    return isinstance(model, (DistributedDataParallel, DataParallel))
 
 
 def pretune_for_ddp(model: torch.nn.Module, step_fn) -> None:

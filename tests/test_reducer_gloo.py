@@ -1,0 +1,97 @@
+"""The framework's own data-parallel reducer (parallel/reducer.py) on gloo, world 2 (CPU):
+gradients equal the single-process full-batch gradients, every gradient lives in its
+64-byte-aligned bucket slot, a gradient written into the slot by its producer (what the
+native kernels do) is adopted without a copy, an unused parameter reduces as zeros instead of
+hanging, and ``no_sync`` accumulates."""
+import torch
+
+from test_dist_gloo import _init, _run
+
+
+class _SlotLinear(torch.autograd.Function):
+    """y = x W^T whose weight gradient is written straight into the reducer slot (as the native
+    wgrad kernels do through ``grad_out``); records the data pointer it produced."""
+    produced = {}
+
+    @staticmethod
+    def forward(ctx, x, w):
+        ctx.save_for_backward(x, w)
+        return x @ w.t()
+
+    @staticmethod
+    def backward(ctx, g):
+        from pytorch_distributed_template_amd.parallel.reducer import grad_out
+        x, w = ctx.saved_tensors
+        dw = grad_out(w, *w.shape)
+        torch.matmul(g.t(), x, out=dw)
+        _SlotLinear.produced[id(w)] = dw.data_ptr()
+        return g @ w, dw
+
+
+class Net(torch.nn.Module):
+    def __init__(self):
+        super().__init__()
+        self.conv = torch.nn.Conv2d(3, 4, 3, padding=1)
+        self.bn = torch.nn.BatchNorm2d(4)
+        self.w = torch.nn.Parameter(torch.randn(5, 4) * 0.3)
+        self.fc = torch.nn.Linear(5, 3)
+        self.unused = torch.nn.Parameter(torch.ones(7))
+
+    def forward(self, x):
+        h = torch.relu(self.bn(self.conv(x))).mean((2, 3))
+        return self.fc(_SlotLinear.apply(h, self.w))
+
+
+def _w_reducer(rank, world, port, q):
+    try:
+        pdist = _init(rank, world, port)
+        from pytorch_distributed_template_amd.parallel.reducer import DataParallel, SLOT_ALIGN
+        torch.manual_seed(0)
+        model, ref = Net(), Net()
+        ref.load_state_dict(model.state_dict())
+        dp = DataParallel(model, torch.device("cpu"), bucket_cap_mb=0.0001, first_bucket_mb=0.00001)
+        torch.manual_seed(1)
+        X = torch.randn(8, 3, 6, 6)
+        Y = torch.randint(0, 3, (8,))
+        xs, ys = X[rank * 4:(rank + 1) * 4], Y[rank * 4:(rank + 1) * 4]
+        out = {}
+        torch.nn.functional.cross_entropy(dp(xs), ys).backward()
+        # reference: the full batch in one process, BN statistics per shard (as DDP without SyncBN)
+        loss = sum(torch.nn.functional.cross_entropy(ref(X[r * 4:(r + 1) * 4]), Y[r * 4:(r + 1) * 4])
+                   for r in range(world)) / world
+        loss.backward()
+        pr = dict(ref.named_parameters())
+        out["diff"] = max(float((p.grad - pr[n].grad).abs().max()) for n, p in model.named_parameters()
+                          if n != "unused")
+        out["unused_zero"] = bool((model.unused.grad == 0).all())
+        flats = {b.flat.data_ptr(): b.flat for b in dp.buckets}
+        ok = True
+        for p in model.parameters():
+            b = dp.buckets[dp._bucket_of[id(p)]].flat
+            off = (p.grad.data_ptr() - b.data_ptr()) // 4
+            ok &= 0 <= off < b.numel() and off % SLOT_ALIGN == 0
+        out["in_slots"] = bool(ok) and len(flats) == len(dp.buckets) and len(dp.buckets) > 2
+        out["adopted"] = model.w.grad.data_ptr() == _SlotLinear.produced[id(model.w)]
+        # no_sync: two local backwards, then a synced one -> 3 x the averaged gradient of one batch
+        g1 = model.fc.weight.grad.clone()
+        for p in model.parameters():
+            p.grad = None
+        with dp.no_sync():
+            torch.nn.functional.cross_entropy(dp(xs), ys).backward()
+            torch.nn.functional.cross_entropy(dp(xs), ys).backward()
+        torch.nn.functional.cross_entropy(dp(xs), ys).backward()
+        out["nosync"] = float((model.fc.weight.grad - 3 * g1).abs().max())
+        q.put((rank, out))
+        pdist.cleanup()
+    except Exception as e:  # pragma: no cover
+        import traceback
+        q.put((rank, repr(e) + traceback.format_exc()))
+
+
+def test_reducer_matches_single_process_and_uses_slots():
+    res = _run(_w_reducer)
+    for r in (0, 1):
+        o = res[r]
+        assert o["diff"] < 1e-5, o
+        assert o["unused_zero"] and o["in_slots"] and o["adopted"], o
+        assert o["nosync"] < 1e-5, o
