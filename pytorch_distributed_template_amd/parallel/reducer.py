@@ -122,6 +122,7 @@ class DataParallel(torch.nn.Module):
         self._avg = dist.get_backend(process_group) == "nccl"  # RCCL: ReduceOp.AVG; gloo: SUM + scale
         self._sync = True
         self._in_backward = False
+        self.fallback_copies = 0  # gradients that had to be copied into their slot (stock ops)
         self.params = [p for p in module.parameters() if p.requires_grad]
         self._verify_shapes()
         self._broadcast_state()
@@ -195,6 +196,7 @@ class DataParallel(torch.nn.Module):
             # a stock op's gradient: copy it into the slot once (native kernels wrote in place)
             slot.copy_(g)
             p.grad = slot
+            self.fallback_copies += 1
         b = self.buckets[self._bucket_of[id(p)]]
         b.ready += 1
         if b.ready == len(b.params):

@@ -73,7 +73,7 @@ __device__ __forceinline__ void tile_of(uint32_t bid, int ntm, int ntn, int& tm,
 // V0: the 4-phase ping-pong ring (two wave groups one barrier apart; each K-tile = four
 // C-quadrant phases; the next K-tile's quarters are issued one per phase with counted vmcnt).
 // GM: tile grouping; PRIO: s_setprio around the MFMA bursts.
-template <int GM, bool PRIO>
+template <int GM, bool PRIO, int EPI = 0, bool SPRIO = false, bool PERSIST = false>
 __global__ void __launch_bounds__(NTH, 1) gemm_v0(GP p) {
   constexpr int WM = 2, WN = 4;
   constexpr int MI = BM / WM / 16;  // 8
@@ -84,8 +84,11 @@ __global__ void __launch_bounds__(NTH, 1) gemm_v0(GP p) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave / WN, wn = wave % WN;
   const int ntm = p.M / BM, ntn = p.N / BN;
+  const int ntiles = ntm * ntn;
+  for (int tile = blockIdx.x; tile < ntiles; tile += PERSIST ? gridDim.x : ntiles) {
+  if (PERSIST && tile != (int)blockIdx.x) __syncthreads();  // LDS of the previous tile fully read
   int tm, tn;
-  tile_of<GM>(blockIdx.x, ntm, ntn, tm, tn);
+  tile_of<GM>(tile, ntm, ntn, tm, tn);
   const int m0 = tm * BM, n0 = tn * BN;
   const int ca = tid & 7;
   const int nk = p.K / BK;
@@ -164,6 +167,7 @@ __global__ void __launch_bounds__(NTH, 1) gemm_v0(GP p) {
   asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
   bar();
   if (wm == 1) bar();
+  if (SPRIO && __builtin_amdgcn_readfirstlane(tid) >= 256) __builtin_amdgcn_s_setprio(1);
   for (int kt = 0; kt < nk; ++kt) {
     const int cur = kt & 1, nxt = cur ^ 1;
     const bool more = kt + 1 < nk;
@@ -190,18 +194,47 @@ __global__ void __launch_bounds__(NTH, 1) gemm_v0(GP p) {
     mma_phase(1, 0);
   }
   if (wm == 0) bar();
-  // direct epilogue: each lane stores its 4 consecutive channels (8 B)
   const int lrow = lane & 15, lcol = (lane >> 4) * 4;
+  if constexpr (EPI == 0) {
+    // direct epilogue: each lane stores its 4 consecutive channels (8 B)
 #pragma unroll
-  for (int i = 0; i < MI; ++i) {
-    const int m = m0 + wm * (BM / WM) + i * 16 + lrow;
+    for (int i = 0; i < MI; ++i) {
+      const int m = m0 + wm * (BM / WM) + i * 16 + lrow;
 #pragma unroll
-    for (int j = 0; j < NI; ++j) {
-      const int col = n0 + wcol(j) + lcol;
-      u32x2 w = {pack2bf(acc[i][j][0], acc[i][j][1]), pack2bf(acc[i][j][2], acc[i][j][3])};
-      *reinterpret_cast<u32x2*>(p.C + (size_t)m * p.N + col) = w;
+      for (int j = 0; j < NI; ++j) {
+        const int col = n0 + wcol(j) + lcol;
+        u32x2 w = {pack2bf(acc[i][j][0], acc[i][j][1]), pack2bf(acc[i][j][2], acc[i][j][3])};
+        *reinterpret_cast<u32x2*>(p.C + (size_t)m * p.N + col) = w;
+      }
+    }
+  } else {
+    // 16-B stores: lanes l and l ^ 16 hold columns 0-3 / 4-7 of the same row in the same
+    // 16-column block; one v_permlane16_swap per dword pairs block j's upper quad with block
+    // j+1's lower quad, so lane l (l & 16 == 0) gets cols 0-7 of block j and lane l|16 cols 0-7
+    // of block j+1 ... per pair of blocks (j, j+1) with the same row.
+#pragma unroll
+    for (int i = 0; i < MI; ++i) {
+      const int m = m0 + wm * (BM / WM) + i * 16 + lrow;
+#pragma unroll
+      for (int j = 0; j < NI; j += 2) {
+        uint32_t a0 = pack2bf(acc[i][j][0], acc[i][j][1]), a1 = pack2bf(acc[i][j][2], acc[i][j][3]);
+        uint32_t b0 = pack2bf(acc[i][j + 1][0], acc[i][j + 1][1]), b1 = pack2bf(acc[i][j + 1][2], acc[i][j + 1][3]);
+        // lane groups g = lane >> 4: g even holds cols 8k..8k+3 (k = g/2), g odd cols 8k+4..8k+7.
+        // swap between lane l (g even) and l+16 (g odd): even lanes take the odd lanes' block-j
+        // quad, odd lanes take the even lanes' block-(j+1) quad.
+        const auto r0 = __builtin_amdgcn_permlane16_swap(a0, b0, false, false);
+        const auto r1 = __builtin_amdgcn_permlane16_swap(a1, b1, false, false);
+        const bool odd = (lane >> 4) & 1;
+        // after the swap: even lanes: r[0] = own a (block j, cols lo) , r[1] = partner's a (block j, cols hi)
+        //                 odd lanes:  r[0] = partner's b (block j+1, cols lo), r[1] = own b (block j+1, cols hi)
+        u32x4 v = {r0[0], r1[0], r0[1], r1[1]};
+        const int blk = odd ? j + 1 : j;
+        const int col = n0 + wcol(blk) + ((lane >> 5) * 8);
+        *reinterpret_cast<u32x4*>(p.C + (size_t)m * p.N + col) = v;
+      }
     }
   }
+  }  // tile loop
 }
 
 // V2: 2-phase ping-pong. Each K-tile = two row-half phases of the 128x64 wave tile (32 MFMAs,
@@ -334,6 +367,121 @@ __global__ void __launch_bounds__(NTH, 1) gemm_v2(GP p) {
     }
 }
 
+// V6: narrow-N tile (BN = 64: ResNet's 64-channel convs). Each wave owns 64 (or 128) rows x all
+// 64 columns, so an A row is read by exactly one wave: A goes global -> VGPRs in the MFMA fragment
+// layout (lane: row lane & 15 of a 16-row block, 16 B at k = 8 * (lane >> 4) + 32 kk), double-
+// buffered one K-tile ahead, never through LDS. B (64 x BK, shared by every wave) goes through a
+// 2-stage LDS-DMA ring. LDS traffic is B's fragments only.
+template <int NW, int RW>
+__global__ void __launch_bounds__(NW * 64, 2) gemm_v6(GP p) {
+  constexpr int BNn = 64, MIw = RW / 16, NIw = 4;
+  constexpr int BMn = NW * RW;
+  constexpr int BSTAGE = BNn * BK * 2;  // 8 KB
+  constexpr int NT = NW * 64;
+  __shared__ __attribute__((aligned(16))) char smem[2 * BSTAGE];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // provably wave-uniform (no waterfall loops)
+  const int ntm = p.M / BMn, ntn = p.N / BNn;
+  int tm, tn;
+  tile_of<1>(blockIdx.x, ntm, ntn, tm, tn);
+  const int m0 = tm * BMn + wave * RW, n0 = tn * BNn;
+  const int nk = p.K / BK;
+  const u16* Bb = p.B + (size_t)n0 * p.K;
+  // B DMA: 64 rows x 128 B = 8 KB = NT * 16 B * (8 KB / (NT * 16))
+  constexpr int LBn = BSTAGE / (NT * 16);
+  auto glds_b = [&](int kt, int buf) __attribute__((always_inline)) {
+#pragma unroll
+    for (int j = 0; j < LBn; ++j) {
+      const int r = (tid >> 3) + (NT / 8) * j;
+      const u16* g = Bb + (size_t)r * p.K + kt * BK + swz(r, tid & 7) * 8;
+      __builtin_amdgcn_global_load_lds(g, (__attribute__((address_space(3))) void*)(smem + buf * BSTAGE +
+                                                                                    (8 * wave + (NT / 8) * j) * 128),
+                                       16, 0, 0);
+    }
+  };
+  bf16x8 a0[MIw][2], a1[MIw][2];
+  // buffer loads: one 32-bit lane offset, the rest in the scalar offset (few VGPRs)
+  const u16* Aw = p.A + (size_t)m0 * p.K;
+  const __amdgpu_buffer_rsrc_t ra = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<u16*>(Aw), (short)0, RW * p.K * 2, 0x00020000);
+  const int voff = ((lane & 15) * p.K + (lane >> 4) * 8) * 2;
+  auto load_a = [&](bf16x8 (&a)[MIw][2], int kt) __attribute__((always_inline)) {
+#pragma unroll
+    for (int i = 0; i < MIw; ++i)
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk)
+        a[i][kk] = __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(
+                                                  ra, voff, (i * 16 * p.K + kt * BK + kk * 32) * 2, 0));
+  };
+  f32x4 acc[MIw][NIw];
+#pragma unroll
+  for (int i = 0; i < MIw; ++i)
+#pragma unroll
+    for (int j = 0; j < NIw; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  auto compute = [&](const bf16x8 (&a)[MIw][2], int buf) __attribute__((always_inline)) {
+    const char* sb = smem + buf * BSTAGE;
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      bf16x8 bq[NIw];
+#pragma unroll
+      for (int j = 0; j < NIw; ++j) {
+        const int row = j * 16 + (lane & 15);
+        bq[j] = *reinterpret_cast<const bf16x8*>(sb + row * 128 + swz(row, kk * 4 + (lane >> 4)) * 16);
+      }
+#pragma unroll
+      for (int i = 0; i < MIw; ++i)
+#pragma unroll
+        for (int j = 0; j < NIw; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bq[j], a[i][kk], acc[i][j], 0, 0, 0);
+    }
+  };
+  // B register-staged (plain loads + ds_write after the barrier), so every VMEM load is an
+  // ordinary VGPR load and the compiler's counted vmcnt keeps A(kt+1) in flight across the
+  // K-tile (an LDS-DMA beside VGPR loads makes hipcc wait vmcnt(0) at each A use).
+  u32x4 rb[LBn];
+  auto load_b = [&](int kt) __attribute__((always_inline)) {
+#pragma unroll
+    for (int j = 0; j < LBn; ++j) {
+      const int r = (tid >> 3) + (NT / 8) * j;
+      rb[j] = *reinterpret_cast<const u32x4*>(Bb + (size_t)r * p.K + kt * BK + (tid & 7) * 8);
+    }
+  };
+  auto store_b = [&](int buf) __attribute__((always_inline)) {
+#pragma unroll
+    for (int j = 0; j < LBn; ++j) {
+      const int r = (tid >> 3) + (NT / 8) * j;
+      *reinterpret_cast<u32x4*>(smem + buf * BSTAGE + r * 128 + swz(r, tid & 7) * 16) = rb[j];
+    }
+  };
+  (void)glds_b;
+  load_b(0);
+  load_a(a0, 0);
+  store_b(0);
+  __syncthreads();
+  for (int kt = 0; kt < nk; kt += 2) {
+    if (kt + 1 < nk) { load_b(kt + 1); load_a(a1, kt + 1); }
+    compute(a0, 0);
+    if (kt + 1 >= nk) break;
+    store_b(1);
+    __syncthreads();
+    if (kt + 2 < nk) { load_b(kt + 2); load_a(a0, kt + 2); }
+    compute(a1, 1);
+    if (kt + 2 < nk) store_b(0);
+    __syncthreads();
+  }
+  const int lrow = lane & 15, lcol = (lane >> 4) * 4;
+#pragma unroll
+  for (int i = 0; i < MIw; ++i) {
+    const int m = m0 + i * 16 + lrow;
+#pragma unroll
+    for (int j = 0; j < NIw; ++j) {
+      const int col = n0 + j * 16 + lcol;
+      u32x2 w = {pack2bf(acc[i][j][0], acc[i][j][1]), pack2bf(acc[i][j][2], acc[i][j][3])};
+      *reinterpret_cast<u32x2*>(p.C + (size_t)m * p.N + col) = w;
+    }
+  }
+}
+
 // ------------------------------------------------------------------------------ harness
 __global__ void fill_kernel(u16* x, size_t n, uint32_t seed) {
   size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
@@ -368,14 +516,23 @@ typedef void (*Kern)(GP);
 struct Var {
   const char* name;
   Kern k;
+  int persist = 0;  // 1: grid = min(tiles, 256 CUs) and the kernel loops over tiles
+  int bm = 256, bn = 256, nth = 512;
 };
 static const Var VARS[] = {
     {"v0 4phase gm1", gemm_v0<1, true>},
     {"v0 4phase gm4", gemm_v0<4, true>},
     {"v0 4phase gm8", gemm_v0<8, true>},
     {"v0 4phase gm4 noprio", gemm_v0<4, false>},
+    {"v0 epi16 gm4", gemm_v0<4, true, 1>},
+    {"v0 epi16 gm4 static-prio", gemm_v0<4, true, 1, true>},
+    {"v0 epi16 gm4 static-prio only", gemm_v0<4, false, 1, true>},
+    {"v0 epi16 gm4 persistent", gemm_v0<4, true, 1, false, true>, 1},
     {"v2 2phase gm1", gemm_v2<1>},
     {"v2 2phase gm4", gemm_v2<4>},
+    {"v6 narrowN 4w x 64r", gemm_v6<4, 64>, 0, 256, 64, 256},
+    {"v6 narrowN 4w x 128r", gemm_v6<4, 128>, 0, 512, 64, 256},
+    {"v6 narrowN 8w x 64r", gemm_v6<8, 64>, 0, 512, 64, 512},
 };
 constexpr int NVARS = sizeof(VARS) / sizeof(VARS[0]);
 
@@ -388,8 +545,8 @@ int main(int argc, char** argv) {
   for (int i = 5; i < argc; ++i) sel.push_back(atoi(argv[i]));
   if (sel.empty())
     for (int i = 0; i < NVARS; ++i) sel.push_back(i);
-  if (M % BM || N % BN || K % BK) {
-    fprintf(stderr, "M, N must be multiples of 256 and K of 64\n");
+  if (M % 64 || N % 64 || K % BK) {
+    fprintf(stderr, "M, N must be multiples of 64 and K of 64\n");
     return 2;
   }
   u16 *A, *B, *C;
@@ -417,15 +574,18 @@ int main(int argc, char** argv) {
   CHECK(hipMemcpy(ref.data(), dref, NS * 4, hipMemcpyDeviceToHost));
   const double flop = 2.0 * M * N * (double)K;
   GP p{A, B, C, M, N, K};
-  const dim3 grid((M / BM) * (N / BN));
+
   hipEvent_t e0, e1;
   CHECK(hipEventCreate(&e0));
   CHECK(hipEventCreate(&e1));
   std::vector<u16> hC((size_t)M * N);
   for (int v : sel) {
     if (v < 0 || v >= NVARS) continue;
+    if (M % VARS[v].bm || N % VARS[v].bn) continue;
+    const int ntiles = (M / VARS[v].bm) * (N / VARS[v].bn);
+    const dim3 grid(VARS[v].persist ? (ntiles < 256 ? ntiles : 256) : ntiles);
     CHECK(hipMemset(C, 0xff, (size_t)M * N * 2));
-    hipLaunchKernelGGL(VARS[v].k, grid, dim3(NTH), 0, 0, p);
+    hipLaunchKernelGGL(VARS[v].k, grid, dim3(VARS[v].nth), 0, 0, p);
     CHECK(hipDeviceSynchronize());
     CHECK(hipMemcpy(hC.data(), C, (size_t)M * N * 2, hipMemcpyDeviceToHost));
     double maxerr = 0.0;
@@ -434,9 +594,9 @@ int main(int argc, char** argv) {
       const double err = fabs((double)got - ref[s]) / (1.0 + fabs((double)ref[s]));
       if (!(err <= maxerr)) maxerr = err;  // NaN-propagating
     }
-    for (int w = 0; w < 3; ++w) hipLaunchKernelGGL(VARS[v].k, grid, dim3(NTH), 0, 0, p);
+    for (int w = 0; w < 3; ++w) hipLaunchKernelGGL(VARS[v].k, grid, dim3(VARS[v].nth), 0, 0, p);
     CHECK(hipEventRecord(e0));
-    for (int it = 0; it < iters; ++it) hipLaunchKernelGGL(VARS[v].k, grid, dim3(NTH), 0, 0, p);
+    for (int it = 0; it < iters; ++it) hipLaunchKernelGGL(VARS[v].k, grid, dim3(VARS[v].nth), 0, 0, p);
     CHECK(hipEventRecord(e1));
     CHECK(hipEventSynchronize(e1));
     float ms = 0.f;

@@ -77,11 +77,14 @@ def _worker(port, hook, q):
             werr = max(float((a - b).abs().max()) for a, b in zip(model.parameters(), ref.parameters()))
         else:
             werr = 0.0
+        # the native reducer: every gradient was written into its bucket slot by the kernel that
+        # produced it (no per-parameter copy / scale launches)
+        copies = getattr(ddp, "fallback_copies", 0)
         # a plain RCCL all-reduce on the same communicator
         t = torch.full((1024,), 3.0, device=dev)
         dist.all_reduce(t)
         torch.cuda.synchronize()
-        q.put((max(errs), views, werr, float(t.sum())))
+        q.put((max(errs), views, werr, float(t.sum()), copies))
         dist.destroy_process_group()
     except Exception:  # pragma: no cover
         import traceback
@@ -97,8 +100,9 @@ def test_rccl_one_rank_ddp_native_grads(hook):
     res = q.get(timeout=300)
     p.join(60)
     assert not isinstance(res, str), res
-    err, views, werr, tsum = res
+    err, views, werr, tsum, copies = res
     assert views > 100, views
+    assert copies == 0, copies
     assert tsum == 3.0 * 1024
     if hook is None:
         assert err == 0.0, err      # 1 rank, fp32 buckets: the all-reduce is exact
