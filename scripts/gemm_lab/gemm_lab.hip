@@ -560,7 +560,7 @@ int main(int argc, char** argv) {
   srand(7);
   for (int s = 0; s < NS; ++s) {
     hr[s] = (s < 8) ? s * (M / 8) + (s % 3) : rand() % M;
-    hc[s] = (s < 8) ? s * (N / 8) + 255 - s : rand() % N;
+    hc[s] = (s < 8) ? s * (N / 8) + (N / 8 > 8 ? N / 8 - 1 - s : 0) : rand() % N;  // last columns of each 1/8
   }
   int *dr, *dc;
   float* dref;

@@ -1,7 +1,6 @@
 """bench.py rejects a broken step: a short ResNet-50 run at batch 256,
 eager and ``--graph``, must report finite first / last losses; the graph run must also pass
-its eager-vs-replay check (the same batches at lr 0 give the same losses), and both runs start
-from the same seed, so their first timed losses agree to bf16 noise."""
+its eager-vs-replay check (the same batches at lr 0 give the same losses)."""
 import json
 import os
 import subprocess
@@ -38,6 +37,7 @@ def test_bench_eager_and_graph_losses_finite_and_agree():
     gc = graph["config"]["graph_check"]
     assert graph["config"]["hip_graph"] is True and gc is not None
     assert gc["max_rel_diff"] <= 1e-3, gc
-    # same seed and data: the graph run only warms up longer (11 steps), so its losses sit in the
-    # same range as the eager run's (random init, 1000 classes: ~ln(1000) = 6.9)
-    assert abs(eager["config"]["loss_first"] - graph["config"]["loss_first"]) < 1.0
+    # (no cross-run loss comparison: the graph run warms up 11 steps at lr 0.1 before its first
+    # timed step, the eager run 2, so their first timed losses sit at different points of an
+    # unstable random-label trajectory -- 7.25 vs 9.53 on one box. The same-batch agreement that
+    # matters is graph_check above: eager and replayed steps from one state, lr 0.)
