@@ -288,35 +288,45 @@ int run_stream(int s, const NTParams& p, hipStream_t st) {
 }  // namespace
 
 // variant ids: [0, NVAR) the LDS-tiled kernels, then NVAR_STREAM streaming 1x1 kernels,
-// then NVAR_HALO 3x3 halo-patch kernels (conv3x3_halo.hip)
+// then NVAR_HALO 3x3 halo-patch kernels (conv3x3_halo.hip), then NVAR_PERS persistent
+// ring tiles (conv_nt_kernel.h PERS_BASE: appended, so the ids of the shipped tune table hold)
 constexpr int HALO0 = NVAR + NVAR_STREAM;
+constexpr int PERS0 = HALO0 + NVAR_HALO;
+constexpr int NVAR_ALL = PERS0 + NVAR_PERS;
 
-PDT_API int pdt_conv_nt_num_variants() { return NVAR + NVAR_STREAM + NVAR_HALO; }
+PDT_API int pdt_conv_nt_num_variants() { return NVAR_ALL; }
 
-// 0: LDS-tiled, 1: streaming 1x1, 2: 3x3 halo-patch (conv3x3_halo.hip); -1: no such variant
+// 0: LDS-tiled (persistent ones included), 1: streaming 1x1, 2: 3x3 halo-patch
+// (conv3x3_halo.hip); -1: no such variant
 PDT_API int pdt_conv_nt_variant_kind(int v) {
-  if (v < 0 || v >= HALO0 + NVAR_HALO) return -1;
+  if (v < 0 || v >= NVAR_ALL) return -1;
+  if (v >= PERS0) return 0;
   return v >= HALO0 ? 2 : (v >= NVAR ? 1 : 0);
 }
 
 PDT_API int pdt_conv_nt_resolve_variant(int variant, int M, int Ncol, int K) {
-  return (variant >= 0 && variant < HALO0 + NVAR_HALO) ? variant : heuristic_variant(M, Ncol, K);
+  return (variant >= 0 && variant < NVAR_ALL) ? variant : heuristic_variant(M, Ncol, K);
 }
+
+// the LDS-tiled variant whose tile (BM, BN, WM) a variant id uses
+static inline int tile_of_variant(int v) { return v >= PERS0 ? PERS_BASE[v - PERS0] : v; }
 
 // Number of BN-statistics partial rows a launch of `variant` writes (sizes the stats buffer).
 // Partial rows a fused BN-backward launch (pdt_conv_nt_bnb) of `variant` writes:
 // one per M-tile (lanes and waves reduced in-block), or the stream kernel's row groups.
 PDT_API int pdt_conv_nt_bnb_rows(int M, int Ncol, int K, int variant) {
   int v = pdt_conv_nt_resolve_variant(variant, M, Ncol, K);
-  if (v >= HALO0) return halo_rows(M);
-  if (v >= NVAR) return stream_rows(v - NVAR, M, Ncol);
+  if (v >= HALO0 && v < PERS0) return halo_rows(M);
+  if (v >= NVAR && v < PERS0) return stream_rows(v - NVAR, M, Ncol);
+  v = tile_of_variant(v);
   return (M + VAR_BM[v] - 1) / VAR_BM[v];
 }
 
 PDT_API int pdt_conv_nt_stat_rows(int M, int Ncol, int K, int variant) {
   int v = pdt_conv_nt_resolve_variant(variant, M, Ncol, K);
-  if (v >= HALO0) return halo_rows(M);
-  if (v >= NVAR) return stream_rows(v - NVAR, M, Ncol);
+  if (v >= HALO0 && v < PERS0) return halo_rows(M);
+  if (v >= NVAR && v < PERS0) return stream_rows(v - NVAR, M, Ncol);
+  v = tile_of_variant(v);
   int BM = VAR_BM[v];
   return ((M + BM - 1) / BM) * VAR_WM[v];
 }
@@ -393,10 +403,15 @@ static int conv_nt_impl(const void* src, const void* b, void* out, float* stats,
     }
     return launch_variant_ax(v, p, stream);
   }
-  if (bnb.part2 != nullptr && v >= 34 && v < NVAR) return -5;  // ring tiles: no second-unit partials
+  // ring tiles: no second-unit partials
+  if (bnb.part2 != nullptr && ((v >= 34 && v < NVAR) || v >= PERS0)) return -5;
+  const bool cs64 = (Cs % 64) == 0;
+  if (v >= PERS0) {
+    if (bnb.part != nullptr) return launch_variant_pers_bnb(v - PERS0, cs64, p, stream);
+    return cs64 ? launch_variant_pers<true>(v - PERS0, p, stream) : launch_variant_pers<false>(v - PERS0, p, stream);
+  }
   if (v >= HALO0) return run_halo(v - HALO0, p, stream);
   if (v >= NVAR) return run_stream(v - NVAR, p, stream);
-  const bool cs64 = (Cs % 64) == 0;
   if (bnb.part != nullptr) return launch_variant_bnb(v, cs64, p, stream);
   return cs64 ? launch_variant<true>(v, p, stream) : launch_variant<false>(v, p, stream);
 }

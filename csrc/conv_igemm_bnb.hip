@@ -11,4 +11,8 @@ int launch_variant_bnb(int v, bool cs64, const NTParams& p, hipStream_t st) {
   return cs64 ? launch_variant<true, true>(v, p, st) : launch_variant<false, true>(v, p, st);
 }
 
+int launch_variant_pers_bnb(int i, bool cs64, const NTParams& p, hipStream_t st) {
+  return cs64 ? launch_variant_pers<true, true>(i, p, st) : launch_variant_pers<false, true>(i, p, st);
+}
+
 }  // namespace pdt_nt

@@ -141,10 +141,17 @@ static inline const void* zero_chunk_addr() {
 // is fetched one quarter per phase with counted vmcnt (never 0 in the loop), so three
 // quarters stay in flight across every barrier (the schedule of the guide's 256^2 8-phase
 // template, 4 phases per K-tile).
+// PERS: persistent -- a grid of one workgroup per CU walks the output tiles (tile t, t + grid,
+// ...) in the XCD-grouped order of the one-tile-per-workgroup launch, so the tiles one XCD has
+// in flight stay neighbours in its L2; the workgroup's first wave of tiles starts at once and the
+// ring's next tile needs no new dispatch (short-K shapes: 5-18 % in scripts/gemm_lab, v7 vs v4).
+// Every tile runs the whole body (operand prologue .. epilogue); one barrier between tiles frees
+// the LDS the previous epilogue staged through.
 template <int BM, int BN, int NSTAGE, bool CS64, bool DIRECT, bool GLDS, int NTH = 256, int WM = 2, int F8 = 0,
-          int PIPE = 0, bool BNB = false, int AX = 0>
+          int PIPE = 0, bool BNB = false, int AX = 0, bool PERS = false>
 __global__ void __launch_bounds__(NTH, PIPE ? 1 : 2) conv_nt_kernel(NTParams p) {
   static_assert(AX == 0 || (!PIPE && F8 == 0 && CS64), "the A-staging BN apply: bf16, 64-channel chunks, no ring");
+  static_assert(!PERS || (PIPE && AX == 0), "persistent: the 1-workgroup-per-CU ring tiles");
   constexpr int WN = NTH / 64 / WM;       // waves along N
   constexpr int MI = BM / (WM * 16);      // 16-row MFMA tiles per wave
   constexpr int NI = BN / (WN * 16);
@@ -180,7 +187,10 @@ __global__ void __launch_bounds__(NTH, PIPE ? 1 : 2) conv_nt_kernel(NTParams p) 
 
   const int ntm = (p.M + BM - 1) / BM;
   const int ntn = (p.Ncol + BN - 1) / BN;
-  const uint32_t logical = xcd_remap(blockIdx.x, ntm * ntn);
+  const int ntiles = ntm * ntn;
+  for (int tile = blockIdx.x; tile < ntiles; tile += PERS ? (int)gridDim.x : ntiles) {
+  if (PERS && tile != (int)blockIdx.x) __syncthreads();  // the previous tile's epilogue LDS reads are done
+  const uint32_t logical = xcd_remap(tile, ntiles);
   const int tm = logical / ntn, tn = logical % ntn;
   const int m0 = tm * BM, n0 = tn * BN;
 
@@ -913,7 +923,7 @@ __global__ void __launch_bounds__(NTH, PIPE ? 1 : 2) conv_nt_kernel(NTParams p) 
         }
       }
     }
-    return;
+    continue;  // (next tile of a persistent workgroup; the loop ends otherwise)
   }
 
   if (p.stats != nullptr) {
@@ -1120,17 +1130,21 @@ __global__ void __launch_bounds__(NTH, PIPE ? 1 : 2) conv_nt_kernel(NTParams p) 
         }
   }
   stage_store(p.out, p.addend, !DIRECT && p.q8 != nullptr);
+  }  // tile loop
 }
 
 template <int BM, int BN, int NS, bool CS64, bool DIRECT, bool GLDS = false, int NTH = 256, int WM = 2, int F8 = 0,
-          int PIPE = 0, bool BNB = false, int AX = 0>
+          int PIPE = 0, bool BNB = false, int AX = 0, bool PERS = false>
 int launch(const NTParams& p, hipStream_t st) {
   int ntm = (p.M + BM - 1) / BM, ntn = (p.Ncol + BN - 1) / BN;
+  if (PERS && p.q8 != nullptr) return -5;  // the fp8 side output keeps one max per workgroup AND tile
   NTParams q = p;
   q.zero = zero_chunk_addr();
   if (q.zero == nullptr) return PDT_ERR_SYMBOL;
-  hipLaunchKernelGGL((conv_nt_kernel<BM, BN, NS, CS64, DIRECT, GLDS, NTH, WM, F8, PIPE, BNB, AX>),
-                     dim3(ntm * ntn), dim3(NTH), 0, st, q);
+  // persistent: one workgroup per CU (the ring tiles hold >= 128 KB of LDS), all 256 CUs
+  const int grid = PERS ? (ntm * ntn < 256 ? ntm * ntn : 256) : ntm * ntn;
+  hipLaunchKernelGGL((conv_nt_kernel<BM, BN, NS, CS64, DIRECT, GLDS, NTH, WM, F8, PIPE, BNB, AX, PERS>),
+                     dim3(grid), dim3(NTH), 0, st, q);
   PDT_RETURN_LAUNCH();
 }
 
@@ -1213,9 +1227,26 @@ int launch_variant(int v, const NTParams& p, hipStream_t st) {
   return -3;
 }
 
+// persistent ring tiles (variant ids PERS0 + i in conv_igemm.hip): the tiles of ids
+// PERS_BASE[i], one workgroup per CU walking the output tiles (see PERS above)
+constexpr int NVAR_PERS = 4;
+constexpr int PERS_BASE[NVAR_PERS] = {37, 36, 34, 35};
+
+template <bool CS64, bool BNB = false>
+int launch_variant_pers(int i, const NTParams& p, hipStream_t st) {
+  switch (i) {
+    case 0: return launch<256, 256, 2, CS64, false, true, 512, 2, 0, 2, BNB, 0, true>(p, st);
+    case 1: return launch<256, 256, 2, CS64, false, true, 512, 2, 0, true, BNB, 0, true>(p, st);
+    case 2: return launch<256, 128, 3, CS64, false, true, 512, 4, 0, true, BNB, 0, true>(p, st);
+    case 3: return launch<128, 256, 3, CS64, false, true, 512, 2, 0, true, BNB, 0, true>(p, st);
+  }
+  return -3;
+}
+
 
 // the fused BatchNorm-backward instantiations (defined in conv_igemm_bnb.hip)
 int launch_variant_bnb(int v, bool cs64, const NTParams& p, hipStream_t st);
+int launch_variant_pers_bnb(int i, bool cs64, const NTParams& p, hipStream_t st);
 
 // The A-staging BN apply (AXArgs) is instantiated for some register-staged tiles
 // (conv_igemm_ax.hip: mode 1 plain epilogue, mode 2 with the BN-backward epilogue);

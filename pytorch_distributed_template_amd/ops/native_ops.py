@@ -502,16 +502,32 @@ def _autotune(key, nvar, launch, default=0):
     return table[key]
 
 
-def _variant_filter():
-    """PDT_NT_VARIANTS="0-29,31" restricts the conv_nt variants the tuner may pick."""
-    spec = os.environ.get("PDT_NT_VARIANTS")
-    if not spec:
-        return None
+def _id_set(spec):
     out = set()
     for part in spec.split(","):
         lo, _, hi = part.partition("-")
         out.update(range(int(lo), int(hi or lo) + 1))
     return out
+
+
+def _variant_filter():
+    """PDT_NT_VARIANTS="0-29,31" restricts the conv_nt variants the tuner may pick."""
+    spec = os.environ.get("PDT_NT_VARIANTS")
+    return _id_set(spec) if spec else None
+
+
+_RETUNED: set = set()
+
+
+def _retune_candidates(key, table):
+    """PDT_RETUNE_WITH="45-48": a targeted re-tune of the table -- every conv_nt key already in
+    it is timed once more against these new variant ids only (its current choice included),
+    and switches when one of them is faster. Returns the allowed id set, or None (no re-tune)."""
+    spec = os.environ.get("PDT_RETUNE_WITH")
+    if not spec or key in _RETUNED or key not in table or not _tune_allowed():
+        return None
+    _RETUNED.add(key)
+    return _id_set(spec) | {int(table[key])}
 
 
 def _nt_args(src, b, out, stats, bias, a, act, variant, addend=None, aux=None, addend_mask=None):
@@ -553,7 +569,8 @@ def select_nt_variant(src, b, out, *, with_stats=False, bias=None, act=0, aux=No
             key += f",a{int(act)}"
         _NT_KEYS[geom] = key
     table = _tuned()
-    if key in table:
+    allowed = _retune_candidates(key, table)
+    if key in table and allowed is None:
         return int(table[key])
     lib = _load()
     if not _tune_allowed():
@@ -566,7 +583,7 @@ def select_nt_variant(src, b, out, *, with_stats=False, bias=None, act=0, aux=No
     tune_add = addend if act == 3 else None  # act 3 reads its operand through the addend pointer
     best = _time_variants(nvar, lambda v: lib.pdt_conv_nt(*_nt_args(src, b, out, stats, bias, a, act, v, aux=aux,
                                                                     addend=tune_add)),
-                          _variant_filter())
+                          allowed if allowed is not None else _variant_filter())
     table[key] = best
     _save_tuned()
     return best
@@ -978,7 +995,8 @@ def _select_bnb_variant(launch, a, has_addend, has_mask, device):
         key = _NTB_KEYS[gt] = "ntb2:" + ",".join(str(x) for x in gt)
     geom = key[5:].rsplit(",", 2)[0]
     table = _tuned()
-    if key in table:
+    allowed = _retune_candidates(key, table)
+    if key in table and allowed is None:
         return int(table[key])
     lib = _load()
     M = a["Nimg"] * a["Hm"] * a["Wm"]
@@ -989,7 +1007,7 @@ def _select_bnb_variant(launch, a, has_addend, has_mask, device):
     rows = max(lib.pdt_conv_nt_bnb_rows(M, a["Ncol"], a["K"], v) for v in range(nvar))
     part = torch.empty(2 * rows * a["Ncol"], dtype=torch.float32, device=device)
     table[key] = _time_variants(nvar, lambda v: launch(v, part, lib.pdt_conv_nt_bnb_rows(M, a["Ncol"], a["K"], v)),
-                                _variant_filter())
+                                allowed if allowed is not None else _variant_filter())
     _save_tuned()
     return table[key]
 

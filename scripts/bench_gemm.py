@@ -2,7 +2,7 @@
 conv_nt GEMM (every tile variant), native fp8 GEMM (every variant), and the
 library paths torch.matmul (hipBLASLt) / torch._scaled_mm for reference.
 
-    python scripts/bench_gemm.py [--iters 10]
+    python scripts/bench_gemm.py [--iters 10] [--shapes vit|resnet]
 """
 import argparse
 import os
@@ -21,6 +21,10 @@ SHAPES = [  # M, N, K  (tokens x out x in)
     (50432, 768, 2304),   # qkv dgrad
     (50432, 3072, 768),   # fc2 dgrad (K=768 -> N=3072)
 ]
+RESNET_SHAPES = [  # 1x1 convs of ResNet-50 at 2048 images as plain GEMMs (pixels x Cout x Cin) + the square reference
+    (401408, 256, 1024), (401408, 1024, 256), (100352, 512, 2048), (100352, 2048, 512),
+    (1605632, 128, 512), (1605632, 512, 128), (8192, 8192, 8192),
+]
 
 
 def timeit(fn, iters):
@@ -38,9 +42,11 @@ def timeit(fn, iters):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--iters", type=int, default=10)
+    ap.add_argument("--shapes", default="vit", choices=["vit", "resnet"])
+    ap.add_argument("--variants", default="", help="also print these bf16 variant ids' own times (e.g. 36,37,45,46)")
     a = ap.parse_args()
     lib = no._load()
-    for M, N, K in SHAPES:
+    for M, N, K in (SHAPES if a.shapes == "vit" else RESNET_SHAPES):
         fl = 2.0 * M * N * K
         x = torch.randn(M, K, device="cuda").to(torch.bfloat16)
         w = torch.randn(N, K, device="cuda").to(torch.bfloat16)
@@ -48,9 +54,16 @@ def main():
         geo = dict(Hs=1, Ws=1, Cs=K, Nimg=M, Hm=1, Wm=1, Ncol=N, K=K, ldb=K, sh=1, sw=1, oh0=0, ow0=0, dh=1, dw=1,
                    nth=1, ntw=1, Ho=1, Wo=1, osh=1, osw=1, oph=0, opw=0, ldo=N)
         best = (1e9, -1)
+        per_v = {}
         for v in range(lib.pdt_conv_nt_num_variants()):
+            if lib.pdt_conv_nt(*no._nt_args(x, w, y, None, None, geo, 0, v)) == no.NOT_APPLICABLE:
+                continue
             t = timeit(lambda: no.conv_nt(x, w, y, variant=v, **geo), a.iters)
+            per_v[v] = t
             best = min(best, (t, v))
+        if a.variants:
+            print(f"M={M} N={N} K={K}: " + "  ".join(
+                f"v{v} {per_v[int(v)] * 1e3:.1f} us" for v in a.variants.split(",") if int(v) in per_v), flush=True)
         t_lib = timeit(lambda: torch.matmul(x, w.t()), a.iters)
         xq, dqx = no.quantize_fp8(x)
         wq, dqw = no.quantize_fp8(w)

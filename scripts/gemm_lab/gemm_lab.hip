@@ -482,6 +482,105 @@ __global__ void __launch_bounds__(NW * 64, 2) gemm_v6(GP p) {
   }
 }
 
+// V8: two workgroups per CU. 256 threads = 2 x 2 waves, wave tile (TBM/2) x (TBN/2) (128 x 64
+// for 256 x 128), BK = 32 (64-B LDS rows), 3-stage LDS-DMA ring (24 KB per stage at 256 x 128,
+// 72 KB per workgroup), ONE raw barrier per K-tile with a counted vmcnt that keeps the next
+// K-tile's DMA in flight across it. The second workgroup on the CU runs its MFMAs while the first
+// waits or stores its epilogue: on short-K shapes the output stores of one tile overlap the other
+// workgroup's mainloop instead of idling the CU.
+// LDS row r (64 B = 4 16-B chunks) holds logical chunk c at physical chunk c ^ ((r >> 2) & 3):
+// a ds_read_b128 16-lane group (rows 16b .. 16b+15, one logical chunk) covers all 16 slots of a
+// 256-B bank row.
+template <int TBM, int TBN, int NS = 3>
+__global__ void __launch_bounds__(256, 2) gemm_v8(GP p) {
+  constexpr int BKs = 32, ROWB = 64;
+  constexpr int MI = TBM / 2 / 16, NI = TBN / 2 / 16;
+  constexpr int AB = TBM * ROWB, BB = TBN * ROWB, ST = AB + BB;
+  constexpr int LA = TBM / 64, LB = TBN / 64;  // DMA instructions per thread per K-tile
+  __shared__ __attribute__((aligned(16))) char smem[NS * ST];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave >> 1, wn = wave & 1;
+  const int ntm = p.M / TBM, ntn = p.N / TBN;
+  int tm, tn;
+  tile_of<4>(blockIdx.x, ntm, ntn, tm, tn);
+  const int m0 = tm * TBM, n0 = tn * TBN;
+  const int nk = p.K / BKs;
+  const int rr = tid >> 2, pc = tid & 3;  // DMA: row within a 64-row pass, physical chunk
+  const u16* Ab = p.A + (size_t)m0 * p.K;
+  const u16* Bb = p.B + (size_t)n0 * p.K;
+  auto issue = [&](int kt, int buf) __attribute__((always_inline)) {
+    char* sa = smem + buf * ST;
+#pragma unroll
+    for (int i = 0; i < LA; ++i) {
+      const int r = rr + 64 * i;
+      const u16* g = Ab + (size_t)r * p.K + kt * BKs + ((pc ^ ((r >> 2) & 3)) * 8);
+      __builtin_amdgcn_global_load_lds(g, (__attribute__((address_space(3))) void*)(sa + (64 * i + 16 * wave) * ROWB),
+                                       16, 0, 0);
+    }
+#pragma unroll
+    for (int j = 0; j < LB; ++j) {
+      const int r = rr + 64 * j;
+      const u16* g = Bb + (size_t)r * p.K + kt * BKs + ((pc ^ ((r >> 2) & 3)) * 8);
+      __builtin_amdgcn_global_load_lds(g, (__attribute__((address_space(3))) void*)(sa + AB + (64 * j + 16 * wave) * ROWB),
+                                       16, 0, 0);
+    }
+  };
+  f32x4 acc[MI][NI];
+#pragma unroll
+  for (int i = 0; i < MI; ++i)
+#pragma unroll
+    for (int j = 0; j < NI; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const int lr = lane & 15, lc = lane >> 4;
+#pragma unroll
+  for (int t = 0; t < NS - 1; ++t)
+    if (t < nk) issue(t, t);
+  for (int kt = 0; kt < nk; ++kt) {
+    if (kt + NS - 2 < nk) asm volatile("s_waitcnt vmcnt(%0)" ::"n"((NS - 2) * (LA + LB)) : "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    if (kt + NS - 1 < nk) issue(kt + NS - 1, (kt + NS - 1) % NS);
+    const char* sa = smem + (kt % NS) * ST;
+    const char* sb = sa + AB;
+    bf16x8 af[MI], bq[NI];
+#pragma unroll
+    for (int j = 0; j < NI; ++j) {
+      const int row = wn * (TBN / 2) + j * 16 + lr;
+      bq[j] = *reinterpret_cast<const bf16x8*>(sb + row * ROWB + ((lc ^ ((row >> 2) & 3)) << 4));
+    }
+#pragma unroll
+    for (int i = 0; i < MI; ++i) {
+      const int row = wm * (TBM / 2) + i * 16 + lr;
+      af[i] = *reinterpret_cast<const bf16x8*>(sa + row * ROWB + ((lc ^ ((row >> 2) & 3)) << 4));
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int i = 0; i < MI; ++i)
+#pragma unroll
+      for (int j = 0; j < NI; ++j)
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bq[j], af[i], acc[i][j], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
+  }
+  // 16-B stores (the v0 epi16 lane exchange)
+#pragma unroll
+  for (int i = 0; i < MI; ++i) {
+    const int m = m0 + wm * (TBM / 2) + i * 16 + lr;
+#pragma unroll
+    for (int j = 0; j < NI; j += 2) {
+      uint32_t a0 = pack2bf(acc[i][j][0], acc[i][j][1]), a1 = pack2bf(acc[i][j][2], acc[i][j][3]);
+      uint32_t b0 = pack2bf(acc[i][j + 1][0], acc[i][j + 1][1]), b1 = pack2bf(acc[i][j + 1][2], acc[i][j + 1][3]);
+      const auto r0 = __builtin_amdgcn_permlane16_swap(a0, b0, false, false);
+      const auto r1 = __builtin_amdgcn_permlane16_swap(a1, b1, false, false);
+      const bool odd = (lane >> 4) & 1;
+      u32x4 v = {r0[0], r1[0], r0[1], r1[1]};
+      const int blk = odd ? j + 1 : j;
+      const int col = n0 + wn * (TBN / 2) + blk * 16 + ((lane >> 5) * 8);
+      *reinterpret_cast<u32x4*>(p.C + (size_t)m * p.N + col) = v;
+    }
+  }
+}
+
 // ------------------------------------------------------------------------------ harness
 __global__ void fill_kernel(u16* x, size_t n, uint32_t seed) {
   size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
@@ -533,6 +632,10 @@ static const Var VARS[] = {
     {"v6 narrowN 4w x 64r", gemm_v6<4, 64>, 0, 256, 64, 256},
     {"v6 narrowN 4w x 128r", gemm_v6<4, 128>, 0, 512, 64, 256},
     {"v6 narrowN 8w x 64r", gemm_v6<8, 64>, 0, 512, 64, 512},
+    {"v8 2wg 256x128 bk32 3st", gemm_v8<256, 128>, 0, 256, 128, 256},
+    {"v8 2wg 128x256 bk32 3st", gemm_v8<128, 256>, 0, 128, 256, 256},
+    {"v8 2wg 256x128 bk32 2st", gemm_v8<256, 128, 2>, 0, 256, 128, 256},
+    {"v8 2wg 128x128 bk32 3st", gemm_v8<128, 128>, 0, 128, 128, 256},
 };
 constexpr int NVARS = sizeof(VARS) / sizeof(VARS[0]);
 
@@ -545,7 +648,7 @@ int main(int argc, char** argv) {
   for (int i = 5; i < argc; ++i) sel.push_back(atoi(argv[i]));
   if (sel.empty())
     for (int i = 0; i < NVARS; ++i) sel.push_back(i);
-  if (M % 64 || N % 64 || K % BK) {
+  if (M % 64 || N % 64 || K % BK) {  // (BK = 64 covers the BK = 32 variants too)
     fprintf(stderr, "M, N must be multiples of 64 and K of 64\n");
     return 2;
   }

@@ -17,6 +17,8 @@
 #   hiptrace[:ARGS]  rocprofv3 HIP-API + kernel trace (host-sync hunting)
 #   pmc:CTRS:ARGS    one counter pass (CTRS: commas -> spaces) over bench.py ARGS
 #   py:SCRIPT[:ARGS] python SCRIPT ARGS
+#   retunewith:NAME:IDS[:ARGS]  targeted re-tune of the shipped conv_nt keys against ids IDS
+#                    (e.g. 45-48+50: '+' separates ranges) -> gpurun_out/tune_NAME.json
 source "$(dirname "$0")/gpurun_lib.sh"
 TAG=$1; shift
 for job in "$@"; do
@@ -55,6 +57,9 @@ for job in "$@"; do
     retune)  # fresh autotune of every kernel variant for a bench config -> gpurun_out/tune_NAME.json
       nm=${rest%%:*}; bargs=""; [[ "$rest" == *:* ]] && bargs=${rest#*:}
       PDT_AUTOTUNE_SHIPPED=0 PDT_AUTOTUNE_CACHE=$PWD/gpurun_out/tune_$nm.json run ${TAG}_retune_$nm.txt 600 python bench.py --steps 5 --warmup 3 ${bargs//,/ } ;;
+    retunewith)  # targeted re-tune: every shipped conv_nt key vs the ids IDS only -> gpurun_out/tune_NAME.json
+      nm=${rest%%:*}; r2=${rest#*:}; ids=${r2%%:*}; bargs=""; [[ "$r2" == *:* ]] && bargs=${r2#*:}
+      PDT_TUNE_ROUNDS=4 PDT_RETUNE_WITH=${ids//+/,} PDT_AUTOTUNE_CACHE=$PWD/gpurun_out/tune_$nm.json run ${TAG}_retunewith_$nm.txt 600 python bench.py --steps 5 --warmup 3 ${bargs//,/ } ;;
     py)
       scr=${rest%%:*}; sargs=""; [[ "$rest" == *:* ]] && sargs=${rest#*:}
       run ${TAG}_py_$(basename $scr .py)$(echo "$sargs" | tr -c 'a-zA-Z0-9_\n' '_' | cut -c1-30).txt 600 python -u $scr ${sargs//,/ } ;;

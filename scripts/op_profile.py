@@ -27,6 +27,8 @@ def main():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--fp8", action="store_true")
     ap.add_argument("--top", type=int, default=70)
+    ap.add_argument("--gap", type=int, default=40,
+                    help="also print the N GEMM-family entries with the most time over their roofline floor")
     ap.add_argument("--cprofile", action="store_true",
                     help="instead: host-side cProfile of --steps steps (where the Python issue time goes)")
     ap.add_argument("--set", action="append", default=[], metavar="K=V",
@@ -111,6 +113,53 @@ def main():
     print("top (entry point, integer args):")
     for ms, n, name, key in rows[:a.top]:
         print(f"  {ms / a.steps:8.3f} ms {n // a.steps:3d}x  {name} {key}")
+    if a.gap:
+        gap_table(rows, a.steps, a.gap)
+
+
+PEAK_FLOPS = 1.3e15  # achievable bf16 MFMA rate under load (gemm lab, 8192^3 at ~1.9 GHz)
+PEAK_BYTES = 5.5e12  # achievable HBM bandwidth
+
+
+def gemm_floor(name, k):
+    """(GFLOP, GB, floor_us) of one call of a GEMM-family entry point from its integer args,
+    or None. Bytes: the operands once and the output once (+ the fused epilogue's extra
+    tensors), i.e. what an ideal kernel would move."""
+    if name.startswith("pdt_conv_nt"):
+        Hs, Ws, Cs, Nimg, Hm, Wm, Ncol, K = k[:8]
+        M = Nimg * Hm * Wm
+        fl = 2.0 * M * Ncol * K
+        by = 2.0 * (Nimg * Hs * Ws * Cs + M * Ncol + Ncol * K)
+        if name.startswith(("pdt_conv_nt_bnb", "pdt_conv_nt_ax")):
+            by += 2.0 * M * Ncol  # y (BN-backward partials) / the second A operand or the written copy
+        if name.endswith("bnb2"):
+            by += 2.0 * M * Ncol
+    elif name == "pdt_conv_wgrad" or name == "pdt_conv_wgrad_bn":
+        M, Mo, No = k[:3]
+        Hs, Ws, C, Hm, Wm = k[4:9]
+        fl = 2.0 * M * Mo * No
+        by = 2.0 * (M * Mo + (M // max(1, Hm * Wm)) * Hs * Ws * C) + 4.0 * Mo * No
+    else:
+        return None
+    return fl / 1e9, by / 1e9, max(fl / PEAK_FLOPS, by / PEAK_BYTES) * 1e6
+
+
+def gap_table(rows, steps, top):
+    out, tot_t, tot_f = [], 0.0, 0.0
+    for ms, n, name, key in rows:
+        g = gemm_floor(name, key)
+        if g is None:
+            continue
+        calls = n // steps
+        t_us = 1e3 * ms / n
+        tot_t += ms / steps
+        tot_f += g[2] * calls / 1e3
+        out.append(((t_us - g[2]) * calls / 1e3, calls, t_us, g, name, key))
+    print(f"GEMM family: {tot_t:.2f} ms/step, floor {tot_f:.2f} ms (at {PEAK_FLOPS / 1e15:.2f} PF/s, "
+          f"{PEAK_BYTES / 1e12:.1f} TB/s)")
+    print("  excess_ms calls   us/call  floor_us  eff   GFLOP     GB  entry args")
+    for ex, calls, t_us, (gf, gb, fl), name, key in sorted(out, key=lambda r: -r[0])[:top]:
+        print(f"  {ex:8.3f} {calls:4d}  {t_us:8.1f}  {fl:8.1f} {100 * fl / t_us:4.0f}%  {gf:6.1f} {gb:6.2f}  {name} {key}")
 
 
 if __name__ == "__main__":
