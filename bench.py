@@ -49,10 +49,11 @@ BASELINE_METRIC = "images/sec (whole node) ResNet-50 synthetic 3x224x224 at 1/2/
 # a cold find at that batch runs ~20 min, and immediate mode without it falls back to
 # naive kernels.
 STOCK_1GPU_IMG_S = {("resnet50", 256): 6605.4, ("resnet50", 512): 6863.8, ("resnet50", 2048): 6969.13,
+                    ("resnet152", 2048): 2842.36,
                     ("vit_b_16", 256): 3547.25, ("vit_b_16", 1024): 4059.96}
 # The stock stack's BEST measured per-GPU throughput (and its batch): reported as
 # ``vs_best_stock``, never as ``vs_baseline``.
-STOCK_BEST_1GPU_IMG_S = {"resnet50": (6969.13, 2048), "vit_b_16": (4059.96, 1024)}
+STOCK_BEST_1GPU_IMG_S = {"resnet50": (6969.13, 2048), "resnet152": (2842.36, 2048), "vit_b_16": (4059.96, 1024)}
 # Per-GPU batch: 2048 images (82 GiB of the 288 GiB HBM3E; weak scaling, so the
 # 8-GPU job holds 16384 images). The stage-3/4 GEMMs (M = N*14*14, N*7*7) fill all
 # 256 CUs only from ~512 images up and every per-launch cost amortises over more
@@ -62,7 +63,11 @@ STOCK_BEST_1GPU_IMG_S = {"resnet50": (6969.13, 2048), "vit_b_16": (4059.96, 1024
 # fp8: 6.46k img/s at 256, 6.96k at 512, 7.31k at 1024, 7.49k at 2048; bf16 5.38k at
 # 1024 (stock autocast: 3.55k at 256, 4.06k at 1024). At 256 the host-side issue
 # time (~35 ms) is close to the 40 ms step: the GPU idles between kernels.
-DEFAULT_BATCH = {"resnet50": 2048, "vit_b_16": 1024}
+# ResNet-152 (BASELINE config 4, "per-GPU batch sized to 288 GB HBM"): 2560 images, 213 GiB --
+# the largest multiple of 256 whose stem activation (N x 112 x 112 x 64) stays under the kernels'
+# 2^31-element index limit (2730 images); 5.96k img/s vs 5.88k at 2048 (170.6 GiB), the stock stack
+# 2.84k at 2048 with the seeded MIOpen find db (profiles/bench_runs_round4.jsonl)
+DEFAULT_BATCH = {"resnet50": 2048, "resnet152": 2560, "vit_b_16": 1024}
 # --graph: batches run eagerly and replayed (lr 0) before the timed run; losses must agree
 GRAPH_CHECK_STEPS = 3
 

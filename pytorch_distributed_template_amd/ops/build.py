@@ -42,7 +42,7 @@ def build(verbose: bool = True) -> Path:
     OBJ_DIR.mkdir(parents=True, exist_ok=True)
     OUT_DIR.mkdir(parents=True, exist_ok=True)
     sources = sorted(CSRC.glob("*.hip"))
-    headers = list(CSRC.glob("*.h"))
+    headers = list(CSRC.glob("*.h")) + list(CSRC.glob("*.inc"))
     hm = max([h.stat().st_mtime for h in headers] + [0.0])
     with cf.ThreadPoolExecutor(max_workers=min(8, len(sources))) as ex:
         objs = list(ex.map(lambda s: _compile(s, hm), sources))

@@ -11,7 +11,7 @@ from pytorch_distributed_template_amd.ops import native_ops as no
 
 pytestmark = pytest.mark.gpu
 
-PERS_BASE = {0: 37, 1: 36, 2: 34, 3: 35}  # persistent id - PERS0 -> its tile's one-shot variant
+PERS_BASE = {0: 34, 1: 35}  # persistent id - PERS0 -> its tile's one-shot variant
 
 
 def _pers_ids(lib):
