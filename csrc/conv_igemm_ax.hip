@@ -36,6 +36,10 @@ static int launch_ax(int v, const NTParams& p, hipStream_t st) {
     case 25: return launch<128, 128, 1, true, false, true, 256, 2, 0, 0, BNB, AX>(p, st);
     case 26: return launch<256, 64, 1, true, false, true, 256, 2, 0, 0, BNB, AX>(p, st);
     case 28: return launch<128, 64, 1, true, false, true, 256, 2, 0, 0, BNB, AX>(p, st);
+    // the 8-wave 2-stage LDS-DMA tiles (64 x 64 per wave): one 256-row (128-row) workgroup tile
+    // covers N = 128 (256) output channels, so an A row is applied by fewer column tiles
+    case 30: return launch<256, 128, 2, true, false, true, 512, 4, 0, 0, BNB, AX>(p, st);
+    case 31: return launch<128, 256, 2, true, false, true, 512, 2, 0, 0, BNB, AX>(p, st);
   }
   return -5;  // NOT_APPLICABLE: no AX instantiation of this tile
 }

@@ -1233,7 +1233,7 @@ def _unit_dx(dy, u: _Unit, addend=None, addend_mask=None, bnb_unit=None, bnb_mas
 # the BN'd tensor is produced by the GEMM that consumes it (and written once for its
 # other consumers) instead of by an element pass + a re-read. PDT_FUSE_BN_AX=0 disables.
 # -----------------------------------------------------------------------------
-AX_VARIANTS = (0, 1, 3, 5, 6, 8, 10, 13, 15, 16, 18, 20, 23, 25, 26, 28)  # csrc/conv_igemm_ax.hip
+AX_VARIANTS = (0, 1, 3, 5, 6, 8, 10, 13, 15, 16, 18, 20, 23, 25, 26, 28, 30, 31)  # csrc/conv_igemm_ax.hip
 
 
 def _ax_enabled() -> bool:
@@ -1295,11 +1295,17 @@ def _ax_select(key, run, run_ref=None):
     when it is faster the key records ``AX_UNFUSED`` and the caller takes that path (the
     fold is a per-geometry tuning decision, not a blanket switch)."""
     table = _tuned()
-    if key in table:
+    extra = os.environ.get("PDT_RETUNE_AX")  # targeted re-tune of shipped AX keys (as PDT_RETUNE_WITH)
+    if key in table and not (extra and key not in _RETUNED and _tune_allowed()):
         return int(table[key])
     if not _tune_allowed():
         return AX_VARIANTS[3]  # 128x128, one LDS stage
-    best = _time_variants(max(AX_VARIANTS) + 1, run, set(AX_VARIANTS))
+    cand = set(AX_VARIANTS)
+    if key in table:
+        _RETUNED.add(key)
+        cur = int(table[key])
+        cand = _id_set(extra) | ({cur} if cur >= 0 else set())
+    best = _time_variants(max(cand) + 1, run, cand)
     if best >= 0 and run_ref is not None and _time_fn(run_ref) < _time_fn(lambda: run(best)):
         best = AX_UNFUSED
     table[key] = best
