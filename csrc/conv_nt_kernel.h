@@ -229,7 +229,7 @@ __global__ void __launch_bounds__(NTH, 1) conv_nt_kernel_pers(NTParams p_arg) {
     if (tile != (int)blockIdx.x) __syncthreads();  // the previous tile's epilogue LDS reads are done
     KP kp = kp0;
     asm volatile("" : "+s"(kp));
-    const NTParams p = *kp;
+    const NTParams p = *(const NTParams*)kp;  // (addrspace cast back to generic; inferred constant again)
     const void* zchunk = p.zero;
 #define PDT_TILE_DONE continue
 #define PDT_TILE_ID tile

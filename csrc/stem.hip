@@ -1,0 +1,218 @@
+// ResNet stem forward (7x7 / stride 2 / pad 3 conv over <= 4 input channels, 64 output
+// channels) as a halo-patch implicit GEMM with the BatchNorm statistics in the epilogue.
+//
+// Why: the generic implicit GEMM runs the stem as the space-to-depth GEMM (K = 256, see
+// native_ops._s2d_weight) and gathers 32 taps x 16 B per output pixel through L2; at 2048
+// images that GEMM took 1.64 ms for 842 GFLOP and 4.1 GB of compulsory traffic (a ~0.75 ms
+// floor). Here a workgroup owns 8 output rows of one image (8 x 112 pixels x 64 channels)
+// and stages the 21 input rows they read ONCE into LDS; every tap's A fragment is then a
+// ds_read of that patch at a (row, pair) offset.
+//
+// Space-to-depth view (native_ops._s2d_weight): the NHWC input padded to 4 channels is read
+// as PAIRS of horizontally adjacent pixels (16 B = 2 px x 4 ch), and
+//   y[n, oh, ow, co] = sum_{kh < 7, t < 4} sum_{j < 8} X[n, 2oh + kh - 3, pair ow + t - 2, j]
+//                                                     * W'[co, (kh * 4 + t) * 8 + j]
+// (kh = 7 is the zero row of the padded 8x8 kernel: skipped, K = 224 per pixel).
+//
+// Layout: patch [21 (24 allocated) rows][128 slots] of 16-B pairs (slot s = pair s - 2; slots past the image
+// are zero), double-buffered; the weight [64 co][32 chunks] with chunk c of row co at physical
+// chunk c ^ (co & 15) (a B fragment's 16 rows hit 16 distinct bank groups). A fragments are
+// 16 consecutive slots per 16-lane group: conflict-free without a swizzle.
+//
+// Waves: 8, wave w computes output row oh0 + w (7 blocks of 16 pixels x 4 blocks of 16
+// channels, the swapped-operand MFMA so a lane holds 4 consecutive channels of one pixel).
+// Persistent: one workgroup per CU walks tiles (image, 8-row band); the next band's patch is
+// DMA'd into the other buffer while this one computes, and this band's output stores are
+// issued AFTER that DMA, so the next band's counted vmcnt wait retires the patch without
+// waiting for the stores (the store stream of band i overlaps the MFMAs of band i + 1).
+// BatchNorm statistics: each lane accumulates its 16 channels' sum / sum of squares over every
+// band it computes (fp32, from the accumulators as the generic epilogue does); one partial row
+// per (workgroup, wave) at the end, reduced by pdt_bn_finalize.
+#include "pdt_common.h"
+
+namespace {
+
+constexpr int NW = 8, NTH = NW * 64;
+constexpr int ROWS = 2 * NW + 5;     // input rows a band reads (2 * 8 output rows + 7 - 2)
+constexpr int PROWS = 24;            // patch rows allocated: PROWS * SLOTS = 6 DMA passes of 512 x 16 B
+constexpr int SLOTS = 128;           // 16-B pair slots per patch row (116 used)
+constexpr int PATCH = PROWS * SLOTS * 16;
+constexpr int WBYTES = 64 * 32 * 16;  // weight: 64 rows x 32 chunks x 16 B
+constexpr int LP = PROWS * SLOTS / NTH;             // patch DMA instructions per thread (6)
+static_assert(PROWS * SLOTS % NTH == 0 && PROWS >= ROWS, "whole DMA passes");
+constexpr int LW = 64 * 32 / NTH;                   // weight DMA instructions per thread (4)
+constexpr int WO = 112, MI = WO / 16;               // output row width, 16-pixel blocks
+
+static __device__ __attribute__((aligned(64))) u32x4 stem_zero[4];
+
+typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+
+struct StemParams {
+  const u16* x;     // [N][H][W][4] bf16 (NHWC padded to 4 channels): pairs [N][H][W/2][8]
+  const u16* w;     // [64][256] bf16 space-to-depth weight
+  u16* y;           // [N][H/2][W/2][64]
+  float* part;      // [2][R][64]: per (workgroup, wave) sum / sum of squares; R = grid * 8
+  const void* zero;
+  int N, H, W;      // W / 2 == 112 (one output row = 7 x 16 pixels)
+  int ntiles, R;
+};
+
+__global__ void __launch_bounds__(NTH, 1) stem_fwd_kernel(StemParams p) {
+  __shared__ __attribute__((aligned(16))) char smem[2 * PATCH + WBYTES];
+  char* const sw = smem + 2 * PATCH;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int Ho = p.H / 2, bands = Ho / NW, Wp = p.W / 2;  // Wp: pairs per input row (= WO)
+
+  // weight -> LDS once (lane-linear image, swizzle on the source: physical chunk pc of row co
+  // holds logical chunk pc ^ (co & 15))
+#pragma unroll
+  for (int l = 0; l < LW; ++l) {
+    const int q = tid + NTH * l;
+    const int co = q >> 5, pc = q & 31;
+    const void* src = p.w + co * 256 + ((pc ^ (co & 15)) * 8);
+    __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)(sw + (64 * wave + NTH * l) * 16),
+                                     16, 0, 0);
+  }
+  auto issue_patch = [&](int tile, int buf) __attribute__((always_inline)) {
+    const bool live = tile < p.ntiles;
+    const int n = live ? tile / bands : 0, band = live ? tile - (tile / bands) * bands : 0;
+    const int ih0 = 2 * band * NW - 3;
+    char* sp = smem + buf * PATCH;
+#pragma unroll
+    for (int l = 0; l < LP; ++l) {
+      const int q = tid + NTH * l;
+      const int r = q >> 7, s = q & (SLOTS - 1);
+      const int ih = ih0 + r, pr = s - 2;
+      const bool ok = live && r < ROWS && (unsigned)ih < (unsigned)p.H && (unsigned)pr < (unsigned)Wp;
+      const void* src = ok ? (const void*)(p.x + (((size_t)n * p.H + ih) * Wp + pr) * 8) : p.zero;
+      __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)(sp + (64 * wave + NTH * l) * 16),
+                                       16, 0, 0);
+    }
+  };
+
+  // per-lane statistics of its 16 channels (co = j * 16 + (lane >> 4) * 4 + r)
+  float ssum[4][4], ssq[4][4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) ssum[j][r] = ssq[j][r] = 0.f;
+
+
+  int tile = blockIdx.x;
+  if (tile < p.ntiles) issue_patch(tile, 0);
+  bool first = true;
+  for (int it = 0; tile < p.ntiles; ++it, tile += gridDim.x) {
+    const int buf = it & 1;
+    // retire this band's patch (and at the first band the weight); the previous band's
+    // output stores (issued after this DMA) stay in flight
+    if (first) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(MI * 2) : "memory");
+    first = false;
+    __builtin_amdgcn_s_barrier();  // every wave's DMA landed; the other buffer's readers are done
+    asm volatile("" ::: "memory");
+    issue_patch(tile + gridDim.x, buf ^ 1);
+
+    const int n = tile / bands, band = tile - n * bands;
+    const int oh = band * NW + wave;
+    const char* sp = smem + buf * PATCH;
+    f32x4 acc[MI][4];
+#pragma unroll
+    for (int i = 0; i < MI; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int kh = 0; kh < 7; ++kh) {
+      // B fragment: weight row co = j * 16 + (lane & 15), logical chunk kh * 4 + (lane >> 4)
+      bf16x8 bq[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int co = j * 16 + (lane & 15);
+        const int c = kh * 4 + (lane >> 4);
+        bq[j] = *reinterpret_cast<const bf16x8*>(sw + co * 512 + ((c ^ (co & 15)) << 4));
+      }
+      const char* prow = sp + (2 * wave + kh) * (SLOTS * 16);
+#pragma unroll
+      for (int i = 0; i < MI; ++i) {
+        // pixel ow = 16 i + (lane & 15), tap t = lane >> 4: slot ow + t (pair ow + t - 2)
+        const bf16x8 af = *reinterpret_cast<const bf16x8*>(prow + (16 * i + (lane & 15) + (lane >> 4)) * 16);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bq[j], af, acc[i][j], 0, 0, 0);
+      }
+    }
+    // epilogue: statistics, then 16-B stores (lanes l and l ^ 16 exchange quads of blocks j, j + 1)
+    u16* yrow = p.y + (((size_t)n * Ho + oh) * WO) * 64;
+#pragma unroll
+    for (int i = 0; i < MI; ++i) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          ssum[j][r] += acc[i][j][r];
+          ssq[j][r] = fmaf(acc[i][j][r], acc[i][j][r], ssq[j][r]);
+        }
+      const int ow = 16 * i + (lane & 15);
+#pragma unroll
+      for (int j = 0; j < 4; j += 2) {
+        const uint32_t a0 = pack2bf(acc[i][j][0], acc[i][j][1]), a1 = pack2bf(acc[i][j][2], acc[i][j][3]);
+        const uint32_t b0 = pack2bf(acc[i][j + 1][0], acc[i][j + 1][1]),
+                       b1 = pack2bf(acc[i][j + 1][2], acc[i][j + 1][3]);
+        const auto r0 = __builtin_amdgcn_permlane16_swap(a0, b0, false, false);
+        const auto r1 = __builtin_amdgcn_permlane16_swap(a1, b1, false, false);
+        const bool odd = (lane >> 4) & 1;
+        const u32x4 v = {r0[0], r1[0], r0[1], r1[1]};
+        const int co = (odd ? j + 1 : j) * 16 + (lane >> 5) * 8;
+        *reinterpret_cast<u32x4*>(yrow + (size_t)ow * 64 + co) = v;
+      }
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no DMA / store outlives the workgroup
+  // partial row (workgroup, wave): the 16 lanes of a DPP row hold 16 pixels of the same channels
+  const int prow = blockIdx.x * NW + wave;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    float s[4], q[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      s[r] = row16_sum(ssum[j][r]);
+      q[r] = row16_sum(ssq[j][r]);
+    }
+    if ((lane & 15) < 8) {
+      const int r = lane & 3;
+      const float sv = (r & 2) ? ((r & 1) ? s[3] : s[2]) : ((r & 1) ? s[1] : s[0]);
+      const float qv = (r & 2) ? ((r & 1) ? q[3] : q[2]) : ((r & 1) ? q[1] : q[0]);
+      const int co = j * 16 + (lane >> 4) * 4 + r;
+      p.part[(size_t)(((lane & 15) < 4 ? 0 : p.R) + prow) * 64 + co] = (lane & 15) < 4 ? sv : qv;
+    }
+  }
+}
+
+}  // namespace
+
+// Applicability (0 = ok) and the number of statistics partial rows of the halo stem.
+PDT_API int pdt_stem_fwd_rows(int N, int H, int W, int Cout) {
+  if (Cout != 64 || H % (2 * NW) != 0 || W != 2 * WO || N < 1) return -5;
+  const int ntiles = N * (H / 2 / NW);
+  return (ntiles < 256 ? ntiles : 256) * NW;
+}
+
+// y = stem conv of x (see the header), BN partial statistics into part[2][R][64],
+// R = pdt_stem_fwd_rows(...). -5: geometry not covered (the caller takes the generic path).
+PDT_API int pdt_stem_fwd(const void* x4, const void* w256, void* y, float* part, int N, int H, int W, int Cout,
+                         hipStream_t stream) {
+  const int R = pdt_stem_fwd_rows(N, H, W, Cout);
+  if (R < 0) return R;
+  if ((long long)N * H * W * 4 >= (1LL << 31) || (long long)N * (H / 2) * (W / 2) * 64 >= (1LL << 31)) return -5;
+  static const void* zcache[PDT_MAX_DEV] = {};
+  StemParams p;
+  p.x = (const u16*)x4;
+  p.w = (const u16*)w256;
+  p.y = (u16*)y;
+  p.part = part;
+  p.zero = pdt_symbol_addr(HIP_SYMBOL(stem_zero), zcache);
+  if (p.zero == nullptr) return PDT_ERR_SYMBOL;
+  p.N = N; p.H = H; p.W = W;
+  p.ntiles = N * (H / 2 / NW);
+  p.R = R;
+  hipLaunchKernelGGL(stem_fwd_kernel, dim3(R / NW), dim3(NTH), 0, stream, p);
+  PDT_RETURN_LAUNCH();
+}

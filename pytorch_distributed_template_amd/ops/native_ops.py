@@ -33,6 +33,8 @@ _SIGS = {
     "pdt_conv_nt_ax": (c_int, [P] * 4 + [c_int] * 11 + [P] * 6 + [c_int] * 3 + [c_int] + [P] * 9 + [P]),
     "pdt_conv_nt_ax2": (c_int, [P] * 4 + [c_int] * 25 + [P] * 6 + [c_int] * 3 + [c_int] + [P] * 9 + [P]),
     "pdt_conv_nt_ax3": (c_int, [P] * 6 + [c_int] * 25 + [P] * 6 + [c_int] * 3 + [c_int] + [P] * 9 + [P]),
+    "pdt_stem_fwd_rows": (c_int, [c_int, c_int, c_int, c_int]),
+    "pdt_stem_fwd": (c_int, [P, P, P, P, c_int, c_int, c_int, c_int, P]),
     "pdt_conv_nt_stat_rows": (c_int, [c_int, c_int, c_int, c_int]),
     "pdt_conv_nt_bnb_rows": (c_int, [c_int, c_int, c_int, c_int]),
     "pdt_conv_nt_num_variants": (c_int, []),
@@ -1896,6 +1898,34 @@ def _s2d_geom(N, H, W, Cout):
                 dh=1, dw=2, nth=8, ntw=4, Ho=Ho, Wo=Wo, osh=1, osw=1, oph=0, opw=0, ldo=Cout, pix=4)
 
 
+def _stem_halo_choice(x4, wb, y, N, H, W, Cout, a, v) -> bool:
+    """Halo-patch stem kernel (csrc/stem.hip) or the generic space-to-depth GEMM (tile ``v``):
+    a tuned per-geometry choice (both with their BN statistics epilogue); ``PDT_STEM_HALO=0``
+    forces the generic GEMM."""
+    lib = _load()
+    if os.environ.get("PDT_STEM_HALO", "1") == "0" or lib.pdt_stem_fwd_rows(N, H, W, Cout) < 0:
+        return False
+    key = f"stem1:{N},{H},{W},{Cout}"
+    table = _tuned()
+    if key in table:
+        return int(table[key]) == 1
+    if not _tune_allowed():
+        return True
+    f32 = dict(dtype=torch.float32, device=x4.device)
+    Rh = lib.pdt_stem_fwd_rows(N, H, W, Cout)
+    ph = torch.empty(2 * Rh * Cout, **f32)
+    Rg = conv_stat_rows(N * H * W // 4, Cout, a["K"], v)
+    pg = torch.empty(2 * Rg * Cout, **f32)
+
+    def launch(k):
+        if k == 1:
+            return lib.pdt_stem_fwd(_p(x4), _p(wb), _p(y), _p(ph), N, H, W, Cout, _s())
+        return lib.pdt_conv_nt(*_nt_args(x4, wb, y, pg, None, a, 0, v))
+    table[key] = _time_variants(2, launch)
+    _save_tuned()
+    return int(table[key]) == 1
+
+
 def _unit_fwd_s2d(x, w, gamma, beta, bna: _BNArgs):
     """Stem conv (space-to-depth GEMM) + BN statistics/finalize; no apply."""
     lib = _load()
@@ -1913,10 +1943,16 @@ def _unit_fwd_s2d(x, w, gamma, beta, bna: _BNArgs):
     y = _empty_cl(N, Cout, Ho, Wo, torch.bfloat16, x.device)
     f32 = dict(dtype=torch.float32, device=x.device)
     v = select_nt_variant(x4, wb, y, with_stats=bna.training, **a)
-    if bna.training:
+    halo = _stem_halo_choice(x4, wb, y, N, H, W, Cout, a, v) if bna.training else False
+    if halo:  # the halo-patch stem kernel (csrc/stem.hip), statistics in its epilogue
+        R = lib.pdt_stem_fwd_rows(N, H, W, Cout)
+        part = torch.empty(2 * R * Cout + lib.pdt_rows_reduce_workspace(R, Cout), **f32)
+        _chk(lib.pdt_stem_fwd(_p(x4), _p(wb), _p(y), _p(part), N, H, W, Cout, st), "stem_fwd")
+    elif bna.training:
         R = conv_stat_rows(M, Cout, a["K"], v)
         part = torch.empty(2 * R * Cout + lib.pdt_rows_reduce_workspace(R, Cout), **f32)
         conv_nt(x4, wb, y, stats=part, variant=v, **a)
+    if bna.training:
         vec = torch.empty((4, Cout), **f32)
         mean, invstd, scale, shift = vec[0], vec[1], vec[2], vec[3]
         _chk(lib.pdt_bn_finalize(_p(part), R, Cout, float(M), float(bna.eps), float(bna.momentum), _p(gamma),
