@@ -223,13 +223,9 @@ __global__ void __launch_bounds__(NTH, 1) conv_nt_kernel_pers(NTParams p_arg) {
   const int ntm = (p_arg.M + BM - 1) / BM;
   const int ntn = (p_arg.Ncol + BN - 1) / BN;
   const int ntiles = ntm * ntn;
-  typedef __attribute__((address_space(4))) const NTParams* KP;
-  const KP kp0 = (KP)__builtin_amdgcn_kernarg_segment_ptr();
   for (int tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
     if (tile != (int)blockIdx.x) __syncthreads();  // the previous tile's epilogue LDS reads are done
-    KP kp = kp0;
-    asm volatile("" : "+s"(kp));
-    const NTParams p = *(const NTParams*)kp;  // (addrspace cast back to generic; inferred constant again)
+    const NTParams& p = p_arg;
     const void* zchunk = p.zero;
 #define PDT_TILE_DONE continue
 #define PDT_TILE_ID tile
