@@ -35,6 +35,8 @@ _SIGS = {
     "pdt_conv_nt_ax3": (c_int, [P] * 6 + [c_int] * 25 + [P] * 6 + [c_int] * 3 + [c_int] + [P] * 9 + [P]),
     "pdt_stem_fwd_rows": (c_int, [c_int, c_int, c_int, c_int]),
     "pdt_stem_fwd": (c_int, [P, P, P, P, c_int, c_int, c_int, c_int, P]),
+    "pdt_stem_wgrad_splits": (c_int, [c_int, c_int, c_int, c_int]),
+    "pdt_stem_wgrad": (c_int, [P, P, P, P, P, c_int, c_int, c_int, c_int, P]),
     "pdt_conv_nt_stat_rows": (c_int, [c_int, c_int, c_int, c_int]),
     "pdt_conv_nt_bnb_rows": (c_int, [c_int, c_int, c_int, c_int]),
     "pdt_conv_nt_num_variants": (c_int, []),
@@ -63,6 +65,7 @@ _SIGS = {
     "pdt_wgrad_plan2": (c_int, [c_int] * 7 + [ctypes.POINTER(c_int)]),
     "pdt_wgrad_num_variants": (c_int, []),
     "pdt_wgrad_workspace": (c_long, [c_int, c_int, c_int]),
+    "pdt_wgrad_reduce": (c_int, [P, P, P, P, c_int, c_int, c_int, c_float, c_int, P]),
     "pdt_conv_wgrad": (c_int, [P, P, P, P] + [c_int] * 16 + [c_int, c_int, c_float, c_int, c_int, c_int, P, P]),
     "pdt_conv_wgrad2": (c_int, [P, P, P, P] + [c_int] * 16 + [c_int, c_int, c_float, c_int, c_int, c_int, P, P, P,
                                                                 P]),
@@ -1973,6 +1976,42 @@ def _unit_fwd_s2d(x, w, gamma, beta, bna: _BNArgs):
     return u
 
 
+def _stem_wgrad_halo(u: _Unit, dA, coef, dw256, generic) -> bool:
+    """The halo-patch stem weight gradient (csrc/stem.hip, the BN backward apply in its dY
+    staging) into ``dw256``; a tuned per-geometry choice against ``generic()`` (the generic
+    weight gradient path, itself tuned; key stem1w; ``PDT_STEM_HALO=0`` forces it). False:
+    not taken here (the caller runs ``generic``)."""
+    lib = _load()
+    N, H, W, Cout = u.N, u.H, u.W, u.Cout
+    splits = lib.pdt_stem_wgrad_splits(N, H, W, Cout)
+    if os.environ.get("PDT_STEM_HALO", "1") == "0" or splits < 0 or u.x.shape[1] != 4:
+        return False
+    ws = torch.empty(lib.pdt_wgrad_workspace(splits, Cout, 256), dtype=torch.float32, device=dA.device)
+
+    def run_halo():
+        rc = lib.pdt_stem_wgrad(_p(u.x), _p(dA), _p(u.y), _p(coef), _p(ws), N, H, W, Cout, _s())
+        if rc == 0:
+            rc = lib.pdt_wgrad_reduce(_p(ws), _p(dw256), None, None, splits, Cout, 256, 1.0, 0, _s())
+        return rc
+
+    key = f"stem1w:{N},{H},{W},{Cout}"
+    table = _tuned()
+    if key in table:
+        choice = int(table[key])
+    elif not _tune_allowed():
+        choice = 1
+    else:
+        _chk(run_halo(), "stem_wgrad")
+        generic()  # settles the generic path's own tuning before it is timed
+        choice = 1 if _time_fn(run_halo) < _time_fn(generic) else 0
+        table[key] = choice
+        _save_tuned()
+    if choice != 1:
+        return False
+    _chk(run_halo(), "stem_wgrad")
+    return True
+
+
 def _unit_dw_s2d(dy, u: _Unit, bn_dA=None):
     """Stem weight gradient (space-to-depth GEMM). ``bn_dA`` = (dA, k1, k2, k3): ``dy`` is
     not given (None) and the stem BN's backward apply is formed inside the weight
@@ -1996,8 +2035,12 @@ def _unit_dw_s2d(dy, u: _Unit, bn_dA=None):
         def run_ref():
             conv_wgrad(apply_pass(), u.x, dw256, **g)
 
-        if not conv_wgrad_bn(dA, u.x, dw256, u.y, coef, run_ref, **g):
-            conv_wgrad(apply_pass(), u.x, dw256, **g)
+        def generic():
+            if not conv_wgrad_bn(dA, u.x, dw256, u.y, coef, run_ref, **g):
+                conv_wgrad(apply_pass(), u.x, dw256, **g)
+
+        if not _stem_wgrad_halo(u, dA, coef, dw256, generic):
+            generic()
     else:
         conv_wgrad(dy, u.x, dw256, **g)
     dw = _grad_buf(u.w, tuple(u.w.shape), torch.channels_last).copy_(_s2d_unfold_grad(dw256, u.C))
