@@ -171,6 +171,103 @@ __global__ void __launch_bounds__(NT) maxpool_bwd_k3s2_kernel(const u16* __restr
   }
 }
 
+// The same k3 s2 p1 quad-gather backward for the ResNet stem, fused with the stem BatchNorm's
+// backward REDUCTION: while dA is formed (and stored: the stem weight gradient reads it), each
+// thread also reads y at the pixels it writes and accumulates, per channel,
+//   s = sum g,  q = sum g * (y - mean),  g = dA (bf16 as stored) gated by relu(y*scale + shift)
+// -- exactly bn_bwd_reduce_kernel's partials, without its second full read of dA. Grid-stride
+// over quad rows; one partial row per workgroup (part[2][gridDim.x][64], pdt_bn_bwd_finalize).
+__global__ void __launch_bounds__(NT) maxpool_bwd_k3s2_bnred_kernel(
+    const u16* __restrict__ dy, const uint8_t* __restrict__ idx, u16* __restrict__ dx, const u16* __restrict__ yb,
+    const float* __restrict__ mean, const float* __restrict__ scale, const float* __restrict__ shift,
+    float* __restrict__ part, int N, int H, int W, int Ho, int Wo) {
+  constexpr int CPR = 8;  // C = 64
+  __shared__ float red[2][NT][8];
+  const int Hq = (H + 1) >> 1, Wq = (W + 1) >> 1;
+  const int cc = threadIdx.x % CPR;  // NT % CPR == 0: a thread's channel chunk is fixed
+  float mu[8], sc[8], sh[8], s[8], q[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    mu[e] = mean[cc * 8 + e];
+    sc[e] = scale[cc * 8 + e];
+    sh[e] = shift[cc * 8 + e];
+    s[e] = q[e] = 0.f;
+  }
+  for (int row = blockIdx.x; row < N * Hq; row += gridDim.x) {
+    const int n = row / Hq, a = row - n * Hq;
+    for (int t = threadIdx.x; t < Wq * CPR; t += NT) {
+      const int b = t / CPR;
+      float g[2][2][8];
+      uint32_t bi[2][2][2];
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+          const bool ok = a + i < Ho && b + j < Wo;
+          const size_t o = (((size_t)n * Ho + (ok ? a + i : a)) * Wo + (ok ? b + j : b)) * CPR + cc;
+          const uint2 v = ok ? reinterpret_cast<const uint2*>(idx)[o] : uint2{0xffffffffu, 0xffffffffu};
+          bi[i][j][0] = v.x;
+          bi[i][j][1] = v.y;
+          if (ok) {
+            unpack8(reinterpret_cast<const u32x4*>(dy)[o], g[i][j]);
+          } else {
+#pragma unroll
+            for (int e = 0; e < 8; ++e) g[i][j][e] = 0.f;
+          }
+        }
+#pragma unroll
+      for (int dh = 0; dh < 2; ++dh) {
+        const int h = 2 * a + dh;
+        if (h >= H) break;
+#pragma unroll
+        for (int dw = 0; dw < 2; ++dw) {
+          const int w = 2 * b + dw;
+          if (w >= W) continue;
+          float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+#pragma unroll
+          for (int i = 0; i < 2; ++i) {
+            if (dh == 0 && i == 1) continue;
+            const int kh = dh == 0 ? 1 : (i == 0 ? 2 : 0);
+#pragma unroll
+            for (int j = 0; j < 2; ++j) {
+              if (dw == 0 && j == 1) continue;
+              const int kw = dw == 0 ? 1 : (j == 0 ? 2 : 0);
+              const uint32_t me = (uint32_t)(kh * 3 + kw);
+#pragma unroll
+              for (int e = 0; e < 8; ++e)
+                if (((bi[i][j][e >> 2] >> (8 * (e & 3))) & 0xffu) == me) acc[e] += g[i][j][e];
+            }
+          }
+          const size_t po = (((size_t)n * H + h) * W + w) * CPR + cc;
+          const u32x4 pk = pack8(acc);
+          reinterpret_cast<u32x4*>(dx)[po] = pk;
+          float gv[8], yv[8];
+          unpack8(pk, gv);
+          unpack8(reinterpret_cast<const u32x4*>(yb)[po], yv);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {
+            const float gg = (yv[e] * sc[e] + sh[e]) > 0.f ? gv[e] : 0.f;
+            s[e] += gg;
+            q[e] += gg * (yv[e] - mu[e]);
+          }
+        }
+      }
+    }
+  }
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    red[0][threadIdx.x][e] = s[e];
+    red[1][threadIdx.x][e] = q[e];
+  }
+  __syncthreads();
+  if (threadIdx.x < 2 * 64) {  // (sum | sumsq) x 64 channels: thread = (half, channel)
+    const int half = threadIdx.x >> 6, c = threadIdx.x & 63, ch = c >> 3, e = c & 7;
+    float acc = 0.f;
+    for (int t = ch; t < NT; t += CPR) acc += red[half][t][e];
+    part[((size_t)half * gridDim.x + blockIdx.x) * 64 + c] = acc;
+  }
+}
+
 // x [N][HW][C] -> y [N][C]  (bf16 out, fp32 sum)
 __global__ void avgpool_fwd_kernel(const u16* __restrict__ x, u16* __restrict__ y, int N, int HW, int C) {
   const int cpr = C / 8;
@@ -272,5 +369,18 @@ PDT_API int pdt_avgpool_bwd(const void* dy, void* dx, int N, int HW, int C, hipS
   long total = (long)N * HW * (C / 8);
   hipLaunchKernelGGL(avgpool_bwd_kernel, dim3(grid_for(total)), dim3(NT), 0, st, (const u16*)dy, (u16*)dx, N, HW,
                      C);
+  PDT_RETURN_LAUNCH();
+}
+
+// Stem max-pool backward (k3 s2 p1, 64 channels) fused with the stem BN backward reduction
+// (see maxpool_bwd_k3s2_bnred_kernel): writes dx and part[2][blocks][64]; -5 when not covered.
+PDT_API int pdt_maxpool_bwd_bnred(const void* dy, const void* idx, void* dx, const void* y, const float* mean,
+                                  const float* scale, const float* shift, float* part, int N, int H, int W, int C,
+                                  int Ho, int Wo, int blocks, hipStream_t st) {
+  if (C != 64 || Ho != (H + 1) / 2 || Wo != (W + 1) / 2 || blocks < 1 || (long)N * ((H + 1) / 2) >= (1L << 31) ||
+      (long)N * H * W * C >= (1L << 31))
+    return -5;
+  hipLaunchKernelGGL(maxpool_bwd_k3s2_bnred_kernel, dim3(blocks), dim3(NT), 0, st, (const u16*)dy, (const uint8_t*)idx,
+                     (u16*)dx, (const u16*)y, mean, scale, shift, part, N, H, W, Ho, Wo);
   PDT_RETURN_LAUNCH();
 }

@@ -82,6 +82,7 @@ _SIGS = {
     "pdt_maxpool_fwd": (c_int, [P, P, P] + [c_int] * 9 + [P]),
     "pdt_maxpool_fwd_affine": (c_int, [P] * 5 + [c_int] * 9 + [P]),
     "pdt_maxpool_bwd": (c_int, [P, P, P] + [c_int] * 9 + [P]),
+    "pdt_maxpool_bwd_bnred": (c_int, [P] * 8 + [c_int] * 7 + [P]),
     "pdt_avgpool_fwd": (c_int, [P, P, c_int, c_int, c_int, P]),
     "pdt_avgpool_bwd": (c_int, [P, P, c_int, c_int, c_int, P]),
     "pdt_xent_fwd": (c_int, [P, c_int, P, P, P, P, c_int, c_int, c_float, P]),
@@ -2047,6 +2048,28 @@ def _unit_dw_s2d(dy, u: _Unit, bn_dA=None):
     return dw.to(u.w.dtype) if dw.dtype != u.w.dtype else dw
 
 
+def _pool_bwd_bnred(dout, idx, dA, u: _Unit, k, s, p):
+    """Stem max-pool backward fused with the stem BN backward reduction
+    (``pdt_maxpool_bwd_bnred``): writes ``dA`` and returns its BN partials as a
+    ``_BnbPartials`` for ``_bn_bwd(pre=...)``, or None when not covered
+    (``PDT_POOL_BNRED=0`` forces the separate passes)."""
+    if os.environ.get("PDT_POOL_BNRED", "1") == "0" or (k, s, p) != (3, 2, 1) or not u.relu or u.mask is not None \
+            or u.act is not None:
+        return None
+    lib = _load()
+    N, C, H, W = u.N, u.Cout, u.g["Ho"], u.g["Wo"]
+    Ho, Wo = dout.shape[2], dout.shape[3]
+    blocks = min(2048, N * ((H + 1) // 2))
+    part = torch.empty(2 * blocks * C + lib.pdt_rows_reduce_workspace(blocks, C), dtype=torch.float32,
+                       device=dout.device)
+    rc = lib.pdt_maxpool_bwd_bnred(_p(dout), _p(idx), _p(dA), _p(u.y), _p(u.mean), _p(u.scale), _p(u.shift),
+                                   _p(part), N, H, W, C, Ho, Wo, blocks, _s())
+    if rc == NOT_APPLICABLE:
+        return None
+    _chk(rc, "maxpool_bwd_bnred")
+    return _BnbPartials(part, blocks, u)
+
+
 class _StemPool(torch.autograd.Function):
     """conv -> BN -> ReLU -> max-pool (the ResNet stem) with the BN apply folded into
     the max-pool: the full-resolution post-ReLU activation is never written or read.
@@ -2086,13 +2109,16 @@ class _StemPool(torch.autograd.Function):
             dy, dgamma, dbeta = _bn_bwd_pool(dout, idx, u, k, s, p)
         else:
             dA = _empty_cl(N, C, H, W, torch.bfloat16, dout.device)
-            _chk(_load().pdt_maxpool_bwd(_p(dout), _p(idx), _p(dA), N, H, W, C, Ho, Wo, k, s, p, _s()),
-                 "maxpool_bwd")
             s2d = u.g.get("s2d", False)
-            if s2d and ctx.needs_input_grad[1] and os.environ.get("PDT_STEM_WGRAD_BN", "1") == "1":
+            fuse_red = s2d and ctx.needs_input_grad[1] and os.environ.get("PDT_STEM_WGRAD_BN", "1") == "1"
+            pre = _pool_bwd_bnred(dout, idx, dA, u, k, s, p) if fuse_red else None
+            if pre is None:
+                _chk(_load().pdt_maxpool_bwd(_p(dout), _p(idx), _p(dA), N, H, W, C, Ho, Wo, k, s, p, _s()),
+                     "maxpool_bwd")
+            if fuse_red:
                 # the stem's only consumer of dy is its weight gradient (no data gradient of the
                 # image): the BN backward apply is formed in that GEMM's dY staging (tuned per shape)
-                dgamma, dbeta, k1, k2, k3 = _bn_bwd(dA, u, False, coeffs_only=True)
+                dgamma, dbeta, k1, k2, k3 = _bn_bwd(dA, u, False, coeffs_only=True, pre=pre)
                 dw = _unit_dw_s2d(None, u, bn_dA=(dA, k1, k2, k3))
                 del ctx.u
                 return None, dw, dgamma, dbeta, None, None, None, None, None

@@ -93,3 +93,36 @@ def test_stem_halo_weight_gradient_with_bn_backward_apply(N):
     got = no._s2d_unfold_grad(dw256, 3)
     assert torch.isfinite(dw256).all()
     assert nrmerr(got, ref) < 1e-2
+
+
+def test_stem_pool_backward_fused_bn_reduction():
+    """pdt_maxpool_bwd_bnred = pdt_maxpool_bwd (dA, bit for bit) + the stem BN backward partials
+    (sum of the ReLU-gated dA and of gated dA * (y - mean)) in one pass."""
+    lib = no._load()
+    dev = "cuda"
+    torch.manual_seed(14)
+    N, H, W, C = 6, 112, 112, 64
+    Ho, Wo = 56, 56
+    y = torch.randn(N, H, W, C, device=dev).to(torch.bfloat16)
+    mean = torch.randn(C, device=dev) * 0.1
+    scale = torch.rand(C, device=dev) + 0.5
+    shift = torch.randn(C, device=dev) * 0.2
+    pooled = torch.empty(N, Ho, Wo, C, device=dev, dtype=torch.bfloat16)
+    idx = torch.empty(N * Ho * Wo * C, dtype=torch.uint8, device=dev)
+    assert lib.pdt_maxpool_fwd_affine(no._p(y), no._p(pooled), no._p(idx), no._p(scale), no._p(shift), N, H, W, C,
+                                      Ho, Wo, 3, 2, 1, no._s()) == 0
+    dout = torch.randn(N, Ho, Wo, C, device=dev).to(torch.bfloat16)
+    dA_ref = torch.empty(N, H, W, C, device=dev, dtype=torch.bfloat16)
+    assert lib.pdt_maxpool_bwd(no._p(dout), no._p(idx), no._p(dA_ref), N, H, W, C, Ho, Wo, 3, 2, 1, no._s()) == 0
+    blocks = 200
+    part = torch.full((2 * blocks * C,), float("nan"), device=dev)
+    dA = torch.empty_like(dA_ref)
+    assert lib.pdt_maxpool_bwd_bnred(no._p(dout), no._p(idx), no._p(dA), no._p(y), no._p(mean), no._p(scale),
+                                     no._p(shift), no._p(part), N, H, W, C, Ho, Wo, blocks, no._s()) == 0
+    torch.cuda.synchronize()
+    assert torch.equal(dA, dA_ref)
+    yf = y.float()
+    g = torch.where(yf * scale + shift > 0, dA_ref.float(), torch.zeros_like(yf)).reshape(-1, C)
+    ps = part.view(2, blocks, C).sum(1)
+    assert nrmerr(ps[0], g.sum(0)) < 1e-4
+    assert nrmerr(ps[1], (g * (yf.reshape(-1, C) - mean)).sum(0)) < 1e-4
