@@ -197,7 +197,7 @@ __global__ void __launch_bounds__(NT) maxpool_bwd_k3s2_bnred_kernel(
     const int n = row / Hq, a = row - n * Hq;
     for (int t = threadIdx.x; t < Wq * CPR; t += NT) {
       const int b = t / CPR;
-      float g[2][2][8];
+      u32x4 gq[2][2];  // window gradients, packed (unpacked per use: fewer VGPRs, more waves)
       uint32_t bi[2][2][2];
 #pragma unroll
       for (int i = 0; i < 2; ++i)
@@ -208,12 +208,18 @@ __global__ void __launch_bounds__(NT) maxpool_bwd_k3s2_bnred_kernel(
           const uint2 v = ok ? reinterpret_cast<const uint2*>(idx)[o] : uint2{0xffffffffu, 0xffffffffu};
           bi[i][j][0] = v.x;
           bi[i][j][1] = v.y;
-          if (ok) {
-            unpack8(reinterpret_cast<const u32x4*>(dy)[o], g[i][j]);
-          } else {
+          gq[i][j] = ok ? reinterpret_cast<const u32x4*>(dy)[o] : u32x4{0u, 0u, 0u, 0u};
+        }
+      // y of the (up to) four pixels this item writes, loaded with the window reads (all loads
+      // of the item in flight together: the kernel is load-latency bound)
+      u32x4 yq[2][2];
 #pragma unroll
-            for (int e = 0; e < 8; ++e) g[i][j][e] = 0.f;
-          }
+      for (int dh = 0; dh < 2; ++dh)
+#pragma unroll
+        for (int dw = 0; dw < 2; ++dw) {
+          const int h = 2 * a + dh, w = 2 * b + dw;
+          yq[dh][dw] = (h < H && w < W) ? reinterpret_cast<const u32x4*>(yb)[(((size_t)n * H + h) * W + w) * CPR + cc]
+                                        : u32x4{0u, 0u, 0u, 0u};
         }
 #pragma unroll
       for (int dh = 0; dh < 2; ++dh) {
@@ -233,9 +239,11 @@ __global__ void __launch_bounds__(NT) maxpool_bwd_k3s2_bnred_kernel(
               if (dw == 0 && j == 1) continue;
               const int kw = dw == 0 ? 1 : (j == 0 ? 2 : 0);
               const uint32_t me = (uint32_t)(kh * 3 + kw);
+              float g[8];
+              unpack8(gq[i][j], g);
 #pragma unroll
               for (int e = 0; e < 8; ++e)
-                if (((bi[i][j][e >> 2] >> (8 * (e & 3))) & 0xffu) == me) acc[e] += g[i][j][e];
+                if (((bi[i][j][e >> 2] >> (8 * (e & 3))) & 0xffu) == me) acc[e] += g[e];
             }
           }
           const size_t po = (((size_t)n * H + h) * W + w) * CPR + cc;
@@ -243,7 +251,7 @@ __global__ void __launch_bounds__(NT) maxpool_bwd_k3s2_bnred_kernel(
           reinterpret_cast<u32x4*>(dx)[po] = pk;
           float gv[8], yv[8];
           unpack8(pk, gv);
-          unpack8(reinterpret_cast<const u32x4*>(yb)[po], yv);
+          unpack8(yq[dh][dw], yv);
 #pragma unroll
           for (int e = 0; e < 8; ++e) {
             const float gg = (yv[e] * sc[e] + sh[e]) > 0.f ? gv[e] : 0.f;

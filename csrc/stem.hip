@@ -231,29 +231,28 @@ PDT_API int pdt_stem_fwd(const void* x4, const void* w256, void* y, float* part,
 // pixel-major, so MFMA fragments come through the transposing ds_read_b64_tr_b16 --
 // 16x16x16 MFMAs, reduction over 16 pixels per step: dy^T (4 blocks of 16 channels) x X
 // (14 blocks of 16 k = two taps of one kernel row each; kh = 7 is the zero row).
-// 8 waves (two per SIMD): wave w accumulates output row w & 3 of each band for the k half
-// w >> 2 (64 x 112 fp32 = 28 accumulators) over every band of the workgroup, and the wave
-// pair of a row writes its slab row; pdt_wgrad_reduce sums the slabs. (One wave per SIMD
-// holding all 224 k in AGPRs ran at 2.05 ms.)
+// Wave w accumulates output row w of each band over every band of the workgroup (64 x 224
+// fp32 = 56 accumulators, one wave per SIMD, in AGPRs) and writes its own slab row;
+// pdt_wgrad_reduce sums the slabs. (8 waves, two per SIMD over k halves, spilled 19 VGPRs and
+// ran 2.33 vs 2.05 ms at 2048 images.)
 namespace {
 
 constexpr int WB = 4;                  // output rows per band
-constexpr int WNW = 8, WNTH = WNW * 64;  // 2 waves per SIMD: wave w = output row w & 3, k half w >> 2
+constexpr int WNW = 4, WNTH = WNW * 64;
 constexpr int WROWS = 2 * WB + 5;      // input rows a band reads (13)
 constexpr int WPROWS = 16;             // allocated: 16 x 128 slots = 8 DMA passes of 256 x 16 B
 constexpr int WPATCH = WPROWS * SLOTS * 16;
 constexpr int WPX = WB * WO;           // band pixels (448)
 constexpr int DYT = WPX * 128;         // dy tile bytes
 constexpr int WLP = WPROWS * SLOTS / WNTH;
-constexpr int WLC = WPX * 8 / WNTH;    // 16-B dA / y chunks per thread per band (7)
-constexpr int KB = 7;                  // 16-column k blocks per wave (half of the 14)
+constexpr int WLC = WPX * 8 / WNTH;    // 16-B dA / y chunks per thread per band (14)
 
 struct StemWgParams {
   const u16* x;      // [N][H][W][4] bf16 = pairs [N][H][W/2][8]
   const u16* dA;     // [N][H/2][W/2][64]: the gradient at the stem BN's output (before its backward)
   const u16* y;      // [N][H/2][W/2][64]: the stem conv output
   const float* bnc;  // [5][64]: k1, k2, k3, scale, shift
-  float* slab;       // [grid * 4][64][256] (one row per output row of a band; the two k halves)
+  float* slab;       // [grid * 4][64][256]
   const void* zero;
   int N, H, W, ntiles;
 };
@@ -270,7 +269,7 @@ __device__ __forceinline__ bf16x4 tr4(const char* p) {
       (__attribute__((address_space(3))) char*)(uintptr_t)(uint32_t)(uintptr_t)p));
 }
 
-__global__ void __launch_bounds__(WNTH, 1) stem_wgrad_kernel(StemWgParams p) {
+__global__ void __launch_bounds__(WNTH, 1) __attribute__((amdgpu_waves_per_eu(1, 1))) stem_wgrad_kernel(StemWgParams p) {
   __shared__ __attribute__((aligned(16))) char smem[DYT + 2 * WPATCH];
   __shared__ float coef[5 * 64];  // k1, k2, k3, scale, shift (read at each apply: registers go to the prefetch)
   char* const dyt = smem;
@@ -308,12 +307,11 @@ __global__ void __launch_bounds__(WNTH, 1) stem_wgrad_kernel(StemWgParams p) {
     }
   };
 
-  const int wr = wave & 3, kh0 = (wave >> 2) * KB;  // this wave's output row of the band, first k block
-  f32x4 acc[4][KB];
+  f32x4 acc[4][14];
 #pragma unroll
   for (int cb = 0; cb < 4; ++cb)
 #pragma unroll
-    for (int kb = 0; kb < KB; ++kb) acc[cb][kb] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int kb = 0; kb < 14; ++kb) acc[cb][kb] = f32x4{0.f, 0.f, 0.f, 0.f};
   const int g = lane >> 4, q = (lane >> 2) & 3, pp = lane & 3;
 
   int tile = blockIdx.x;
@@ -325,18 +323,14 @@ __global__ void __launch_bounds__(WNTH, 1) stem_wgrad_kernel(StemWgParams p) {
     __builtin_amdgcn_s_barrier();                      // every wave is done with the previous band's tiles
     asm volatile("" ::: "memory");
     // dy = BN backward apply -> LDS tile (bf16)
-    // (an opaque offset keeps these LDS reads inside the band loop: hoisted, the 40
-    // coefficients would stay live across the MFMA loop and spill)
-    int co8 = cc * 8;
-    asm volatile("" : "+v"(co8));
     float k1[8], k2[8], k3[8], sc[8], sh[8];
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
-      k1[e] = coef[co8 + e];
-      k2[e] = coef[64 + co8 + e];
-      k3[e] = coef[128 + co8 + e];
-      sc[e] = coef[192 + co8 + e];
-      sh[e] = coef[256 + co8 + e];
+      k1[e] = coef[cc * 8 + e];
+      k2[e] = coef[64 + cc * 8 + e];
+      k3[e] = coef[128 + cc * 8 + e];
+      sc[e] = coef[192 + cc * 8 + e];
+      sh[e] = coef[256 + cc * 8 + e];
     }
 #pragma unroll
     for (int l = 0; l < WLC; ++l) {
@@ -370,15 +364,15 @@ __global__ void __launch_bounds__(WNTH, 1) stem_wgrad_kernel(StemWgParams p) {
     const char* sp = smem + DYT + buf * WPATCH;
 #pragma unroll 1
     for (int s = 0; s < WO / 16; ++s) {
-      const int m0 = wr * WO + 16 * s;         // band pixel of this step's first row
+      const int m0 = wave * WO + 16 * s;       // band pixel of this step's first row
       const int ow = 16 * s + 4 * g + q;       // this lane's pixel (row of the stored matrices)
       bf16x4 af[4];
 #pragma unroll
       for (int cb = 0; cb < 4; ++cb) af[cb] = tr4(dyt + dyt_off(m0 + 4 * g + q, cb * 32 + pp * 8));
 #pragma unroll
-      for (int kb = 0; kb < KB; ++kb) {
-        const int kh = (kh0 + kb) >> 1, t0 = 2 * ((kh0 + kb) & 1);
-        const bf16x4 xf = tr4(sp + (2 * wr + kh) * (SLOTS * 16) + (ow + t0 + (pp >> 1)) * 16 + (pp & 1) * 8);
+      for (int kb = 0; kb < 14; ++kb) {
+        const int kh = kb >> 1, t0 = 2 * (kb & 1);
+        const bf16x4 xf = tr4(sp + (2 * wave + kh) * (SLOTS * 16) + (ow + t0 + (pp >> 1)) * 16 + (pp & 1) * 8);
 #pragma unroll
         for (int cb = 0; cb < 4; ++cb)
           acc[cb][kb] = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(af[cb], xf, acc[cb][kb], 0, 0, 0);
@@ -387,18 +381,16 @@ __global__ void __launch_bounds__(WNTH, 1) stem_wgrad_kernel(StemWgParams p) {
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no DMA outlives the workgroup
   // slab row (workgroup, wave): D[co][k], lane holds co = cb*16 + 4*(lane >> 4) + r, k = kb*16 + (lane & 15)
-  float* out = p.slab + (size_t)(blockIdx.x * 4 + wr) * 64 * 256;
+  float* out = p.slab + (size_t)(blockIdx.x * WNW + wave) * 64 * 256;
 #pragma unroll
   for (int cb = 0; cb < 4; ++cb)
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int co = cb * 16 + 4 * (lane >> 4) + r;
 #pragma unroll
-      for (int kb = 0; kb < KB; ++kb) out[co * 256 + (kh0 + kb) * 16 + (lane & 15)] = acc[cb][kb][r];
-      if (kh0 != 0) {  // kh = 7: the zero row of the padded kernel
-        out[co * 256 + 224 + (lane & 15)] = 0.f;
-        out[co * 256 + 240 + (lane & 15)] = 0.f;
-      }
+      for (int kb = 0; kb < 14; ++kb) out[co * 256 + kb * 16 + (lane & 15)] = acc[cb][kb][r];
+      out[co * 256 + 224 + (lane & 15)] = 0.f;  // kh = 7: the zero row of the padded kernel
+      out[co * 256 + 240 + (lane & 15)] = 0.f;
     }
 }
 
@@ -408,7 +400,7 @@ __global__ void __launch_bounds__(WNTH, 1) stem_wgrad_kernel(StemWgParams p) {
 PDT_API int pdt_stem_wgrad_splits(int N, int H, int W, int Cout) {
   if (Cout != 64 || H % (2 * WB) != 0 || W != 2 * WO || N < 1) return -5;
   const int ntiles = N * (H / 2 / WB);
-  return (ntiles < 256 ? ntiles : 256) * 4;
+  return (ntiles < 256 ? ntiles : 256) * WNW;
 }
 
 // slab[splits][64][256] = per-wave partials of the stem weight gradient (space-to-depth layout)
@@ -430,6 +422,6 @@ PDT_API int pdt_stem_wgrad(const void* x4, const void* dA, const void* y, const 
   if (p.zero == nullptr) return PDT_ERR_SYMBOL;
   p.N = N; p.H = H; p.W = W;
   p.ntiles = N * (H / 2 / WB);
-  hipLaunchKernelGGL(stem_wgrad_kernel, dim3(splits / 4), dim3(WNTH), 0, stream, p);
+  hipLaunchKernelGGL(stem_wgrad_kernel, dim3(splits / WNW), dim3(WNTH), 0, stream, p);
   PDT_RETURN_LAUNCH();
 }

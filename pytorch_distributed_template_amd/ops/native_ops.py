@@ -2059,7 +2059,7 @@ def _pool_bwd_bnred(dout, idx, dA, u: _Unit, k, s, p):
     lib = _load()
     N, C, H, W = u.N, u.Cout, u.g["Ho"], u.g["Wo"]
     Ho, Wo = dout.shape[2], dout.shape[3]
-    blocks = min(2048, N * ((H + 1) // 2))
+    blocks = min(int(os.environ.get("PDT_POOL_BNRED_BLOCKS", "8192")), N * ((H + 1) // 2))
     part = torch.empty(2 * blocks * C + lib.pdt_rows_reduce_workspace(blocks, C), dtype=torch.float32,
                        device=dout.device)
     rc = lib.pdt_maxpool_bwd_bnred(_p(dout), _p(idx), _p(dA), _p(u.y), _p(u.mean), _p(u.scale), _p(u.shift),
