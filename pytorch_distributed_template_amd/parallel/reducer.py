@@ -27,7 +27,10 @@ by one ~153 GB/s link per direction and RCCL spreads channels over the 7 links, 
 of large buckets keeps every channel streaming. The FIRST bucket is small (the gradients that
 are ready first -- the classifier -- start moving while the rest of backward runs), the others
 ``bucket_cap_mb`` (default 64 MiB: ResNet-50's 97.5 MiB of fp32 gradients become 1 + 2
-buckets, ResNet-152's 230 MiB 1 + 4). ``docs/DDP_XGMI.md`` has the readiness measurements.
+buckets, ResNet-152's 230 MiB 1 + 4), and the LAST bucket is split so that at most 4 MiB (the
+stem and first stage: ready at the very end of backward) is left exposed after backward
+(ResNet-50 at bs 2048: 25.1 MiB of the last bucket are ready only at the end otherwise).
+``docs/DDP_XGMI.md`` has the readiness measurements.
 
 ``broadcast_buffers`` (reference default True: BN running statistics from rank 0 before every
 forward) is supported and off by default (training-mode BN never reads them). Parameters and
@@ -88,9 +91,13 @@ def grad_out(param: torch.Tensor, *shape, memory_format=None) -> torch.Tensor:
     return torch.empty(shape, dtype=torch.float32, device=param.device)
 
 
-def plan_buckets(params: List[torch.Tensor], bucket_cap_mb: float, first_bucket_mb: float) -> List[List[int]]:
+def plan_buckets(params: List[torch.Tensor], bucket_cap_mb: float, first_bucket_mb: float,
+                 last_bucket_mb: float = 0.0) -> List[List[int]]:
     """Indices of ``params`` per bucket, in reverse registration order (the order backward
-    produces gradients in); the first bucket is capped at ``first_bucket_mb``."""
+    produces gradients in); the first bucket is capped at ``first_bucket_mb``. ``last_bucket_mb``
+    > 0: the LAST bucket is split so that its final part -- the gradients backward produces
+    last (the stem and first stage of a CNN), whose all-reduce nothing is left to hide -- holds
+    at most that much; the rest of it is reduced while those are still being computed."""
     buckets, cur, cur_bytes = [], [], 0
     cap = first_bucket_mb * 2 ** 20
     for i in reversed(range(len(params))):
@@ -103,6 +110,13 @@ def plan_buckets(params: List[torch.Tensor], bucket_cap_mb: float, first_bucket_
         cur_bytes += nbytes
     if cur:
         buckets.append(cur)
+    if last_bucket_mb > 0 and len(buckets) > 1:
+        last, tail_bytes, cut = buckets[-1], 0, len(buckets[-1])
+        while cut > 1 and tail_bytes + params[last[cut - 1]].numel() * 4 <= last_bucket_mb * 2 ** 20:
+            cut -= 1
+            tail_bytes += params[last[cut]].numel() * 4
+        if 0 < cut < len(last):
+            buckets[-1:] = [last[:cut], last[cut:]]
     return buckets
 
 
@@ -112,7 +126,8 @@ class DataParallel(torch.nn.Module):
     averaged over the ranks when backward returns -- with the bucketing above."""
 
     def __init__(self, module: torch.nn.Module, device: torch.device | None = None, process_group=None,
-                 bucket_cap_mb: float = 64.0, first_bucket_mb: float = 8.0, broadcast_buffers: bool = False):
+                 bucket_cap_mb: float = 64.0, first_bucket_mb: float = 8.0, broadcast_buffers: bool = False,
+                 last_bucket_mb: float = 4.0):
         super().__init__()
         self.module = module
         self.process_group = process_group
@@ -126,7 +141,7 @@ class DataParallel(torch.nn.Module):
         self.params = [p for p in module.parameters() if p.requires_grad]
         self._verify_shapes()
         self._broadcast_state()
-        self.bucket_index = plan_buckets(self.params, bucket_cap_mb, first_bucket_mb)
+        self.bucket_index = plan_buckets(self.params, bucket_cap_mb, first_bucket_mb, last_bucket_mb)
         self.buckets: List[_Bucket] = []
         self._bucket_of = {}
         for bi, idx in enumerate(self.bucket_index):

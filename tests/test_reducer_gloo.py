@@ -95,3 +95,18 @@ def test_reducer_matches_single_process_and_uses_slots():
         assert o["diff"] < 1e-5, o
         assert o["unused_zero"] and o["in_slots"] and o["adopted"], o
         assert o["nosync"] < 1e-5, o
+
+
+def test_plan_buckets_small_last_bucket():
+    """The last bucket is split so that only the gradients produced last (<= last_bucket_mb: the
+    stem and first stage of ResNet-50) stay exposed after backward."""
+    from pytorch_distributed_template_amd import models
+    from pytorch_distributed_template_amd.parallel.reducer import plan_buckets
+    ps = [p for p in models.resnet50(num_classes=1000).parameters() if p.requires_grad]
+    mib = lambda b: sum(ps[i].numel() * 4 for i in b) / 2 ** 20  # noqa: E731
+    plain = plan_buckets(ps, 64.0, 8.0)
+    split = plan_buckets(ps, 64.0, 8.0, 4.0)
+    assert len(split) == len(plain) + 1
+    assert mib(split[-1]) <= 4.0 and 0 in split[-1]  # the stem conv (registered first) is in the tail
+    assert sorted(i for b in split for i in b) == list(range(len(ps)))
+    assert split[:-2] == plain[:-1] and split[-2] + split[-1] == plain[-1]
