@@ -396,8 +396,165 @@ __global__ void __launch_bounds__(WNTH, 1) __attribute__((amdgpu_waves_per_eu(1,
 
 }  // namespace
 
+static int pdt_stem_wgrad_splits_v1(int N, int H, int W, int Cout);
+constexpr int KB2 = 7;  // 16-column k blocks per v2 wave (half of the 14)
+
+// ---------------------------------------------------------------------------- v2
+// The same weight gradient with every operand DMA'd (no register prefetch): bands of 2 output
+// rows; per band the raw dA and y tiles (224 px x 64 ch each) and the 9 input rows go global ->
+// LDS by LDS-DMA into one of two buffer sets, and the NEXT band's DMA is issued right after the
+// barrier that opens a band -- before this band's dA is turned into dy in place -- so the loads
+// stay in flight through the conversion and the MFMAs (v1 issued its register prefetch only
+// after staging: HBM idled for this CU while it converted). 4 waves: wave w = output row w & 1
+// of the band, k half w >> 1 (64 co x 112 k, 28 accumulators). The dy tile keeps v1's 32-B
+// segment swizzle: the DMA lane at physical chunk c of pixel row r loads logical chunk
+// swz(r, c) (the XOR is an involution), and the converter rewrites its own chunk in place.
+namespace {
+
+constexpr int V2B = 2;                  // output rows per band
+constexpr int V2PX = V2B * WO;          // 224 band pixels
+constexpr int V2RAW = V2PX * 128;       // one raw tile (dA or y): 28 KB
+constexpr int V2ROWS = 2 * V2B + 5;     // 9 input rows
+constexpr int V2PROWS = 10;             // allocated: 10 x 128 slots = 5 passes of 256 x 16 B
+constexpr int V2PATCH = V2PROWS * SLOTS * 16;
+constexpr int V2SET = 2 * V2RAW + V2PATCH;  // one buffer set: dA (-> dy), y, patch = 76 KB
+constexpr int V2LR = V2PX * 8 / WNTH;   // raw-tile DMA passes per tensor (7)
+constexpr int V2LP = V2PROWS * SLOTS / WNTH;  // patch DMA passes (5)
+static_assert(2 * V2SET <= 160 * 1024 - 2048, "two buffer sets in LDS");
+
+// logical 16-B chunk held by physical chunk c of dy-tile row r (dyt_off's segment swizzle)
+__device__ __forceinline__ int v2_chunk(int r, int c) { return ((((c >> 1) ^ ((r >> 1) & 3))) << 1) | (c & 1); }
+
+__global__ void __launch_bounds__(WNTH, 1) stem_wgrad2_kernel(StemWgParams p) {
+  __shared__ __attribute__((aligned(16))) char smem[2 * V2SET];
+  __shared__ float coef[5 * 64];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int Ho = p.H / 2, bands = Ho / V2B, Wp = p.W / 2;
+  for (int i = tid; i < 5 * 64; i += WNTH) coef[i] = p.bnc[i];
+
+  auto issue = [&](int tile, int set) __attribute__((always_inline)) {
+    const bool live = tile < p.ntiles;
+    const int n = live ? tile / bands : 0, band = live ? tile - (tile / bands) * bands : 0;
+    char* sa = smem + set * V2SET;
+    const size_t base = (((size_t)n * Ho + band * V2B) * WO) * 64;
+#pragma unroll
+    for (int l = 0; l < V2LR; ++l) {
+      const int q = tid + WNTH * l;
+      const int px = q >> 3, c = v2_chunk(px, q & 7);
+      const size_t off = base + (size_t)px * 64 + c * 8;
+      const void* sd = live ? (const void*)(p.dA + off) : p.zero;
+      const void* sy = live ? (const void*)(p.y + off) : p.zero;
+      __builtin_amdgcn_global_load_lds(sd, (__attribute__((address_space(3))) void*)(sa + (64 * wave + WNTH * l) * 16),
+                                       16, 0, 0);
+      __builtin_amdgcn_global_load_lds(sy, (__attribute__((address_space(3))) void*)(sa + V2RAW +
+                                                                                      (64 * wave + WNTH * l) * 16),
+                                       16, 0, 0);
+    }
+    const int ih0 = 2 * band * V2B - 3;
+    char* sp = sa + 2 * V2RAW;
+#pragma unroll
+    for (int l = 0; l < V2LP; ++l) {
+      const int q = tid + WNTH * l;
+      const int r = q >> 7, s = q & (SLOTS - 1);
+      const int ih = ih0 + r, pr = s - 2;
+      const bool ok = live && r < V2ROWS && (unsigned)ih < (unsigned)p.H && (unsigned)pr < (unsigned)Wp;
+      const void* src = ok ? (const void*)(p.x + (((size_t)n * p.H + ih) * Wp + pr) * 8) : p.zero;
+      __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)(sp + (64 * wave + WNTH * l) * 16),
+                                       16, 0, 0);
+    }
+  };
+
+  const int wr = wave & 1, kh0 = (wave >> 1) * KB2;
+  f32x4 acc[4][KB2];
+#pragma unroll
+  for (int cb = 0; cb < 4; ++cb)
+#pragma unroll
+    for (int kb = 0; kb < KB2; ++kb) acc[cb][kb] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const int g = lane >> 4, q = (lane >> 2) & 3, pp = lane & 3;
+
+  int tile = blockIdx.x;
+  issue(tile, 0);
+  for (int it = 0; tile < p.ntiles; ++it, tile += gridDim.x) {
+    const int set = it & 1;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this band's raw tiles and patch (own DMA)
+    __builtin_amdgcn_s_barrier();                      // everyone's landed; the other set's readers are done
+    asm volatile("" ::: "memory");
+    issue(tile + gridDim.x, set ^ 1);                  // next band: in flight through convert + MFMAs
+    char* const dyt = smem + set * V2SET;
+    const char* const yt = dyt + V2RAW;
+    // dA -> dy in place (each thread its own chunks; channels from the swizzled chunk)
+#pragma unroll
+    for (int l = 0; l < V2LR; ++l) {
+      const int qq = tid + WNTH * l;
+      const int px = qq >> 3, c8 = v2_chunk(px, qq & 7) * 8;
+      u32x4* dp = reinterpret_cast<u32x4*>(dyt + qq * 16);
+      const u32x4 da = *dp, yy = *reinterpret_cast<const u32x4*>(yt + qq * 16);
+      u32x4 o;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        float v[2];
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          const int k = 2 * e + h;
+          const float d = h ? hi_bf(da[e]) : lo_bf(da[e]);
+          const float yv = h ? hi_bf(yy[e]) : lo_bf(yy[e]);
+          const float gk = (yv * coef[192 + c8 + k] + coef[256 + c8 + k]) > 0.f ? d : 0.f;
+          v[h] = coef[c8 + k] * gk + coef[64 + c8 + k] * yv + coef[128 + c8 + k];
+        }
+        o[e] = pack2bf(v[0], v[1]);
+      }
+      *dp = o;
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();  // dy tile complete
+    asm volatile("" ::: "memory");
+    const char* sp = dyt + 2 * V2RAW;
+#pragma unroll 1
+    for (int s = 0; s < WO / 16; ++s) {
+      const int m0 = wr * WO + 16 * s;
+      const int ow = 16 * s + 4 * g + q;
+      bf16x4 af[4];
+#pragma unroll
+      for (int cb = 0; cb < 4; ++cb) af[cb] = tr4(dyt + dyt_off(m0 + 4 * g + q, cb * 32 + pp * 8));
+#pragma unroll
+      for (int kb = 0; kb < KB2; ++kb) {
+        const int kh = (kh0 + kb) >> 1, t0 = 2 * ((kh0 + kb) & 1);
+        const bf16x4 xf = tr4(sp + (2 * wr + kh) * (SLOTS * 16) + (ow + t0 + (pp >> 1)) * 16 + (pp & 1) * 8);
+#pragma unroll
+        for (int cb = 0; cb < 4; ++cb)
+          acc[cb][kb] = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(af[cb], xf, acc[cb][kb], 0, 0, 0);
+      }
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  float* out = p.slab + (size_t)(blockIdx.x * 2 + wr) * 64 * 256;
+#pragma unroll
+  for (int cb = 0; cb < 4; ++cb)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int co = cb * 16 + 4 * (lane >> 4) + r;
+#pragma unroll
+      for (int kb = 0; kb < KB2; ++kb) out[co * 256 + (kh0 + kb) * 16 + (lane & 15)] = acc[cb][kb][r];
+      if (kh0 != 0) {
+        out[co * 256 + 224 + (lane & 15)] = 0.f;
+        out[co * 256 + 240 + (lane & 15)] = 0.f;
+      }
+    }
+}
+
+}  // namespace
+
+// v2 (variant 1 of pdt_stem_wgrad_v): slab rows = grid * 2
+PDT_API int pdt_stem_wgrad_splits_v(int N, int H, int W, int Cout, int variant) {
+  if (variant == 0) return pdt_stem_wgrad_splits_v1(N, H, W, Cout);
+  if (variant != 1 || Cout != 64 || H % (2 * V2B) != 0 || W != 2 * WO || N < 1) return -5;
+  const int ntiles = N * (H / 2 / V2B);
+  return (ntiles < 256 ? ntiles : 256) * 2;
+}
+
 // Slab rows (splits) of the halo stem weight gradient; -5 when the geometry is not covered.
-PDT_API int pdt_stem_wgrad_splits(int N, int H, int W, int Cout) {
+PDT_API int pdt_stem_wgrad_splits(int N, int H, int W, int Cout) { return pdt_stem_wgrad_splits_v(N, H, W, Cout, 0); }
+static int pdt_stem_wgrad_splits_v1(int N, int H, int W, int Cout) {
   if (Cout != 64 || H % (2 * WB) != 0 || W != 2 * WO || N < 1) return -5;
   const int ntiles = N * (H / 2 / WB);
   return (ntiles < 256 ? ntiles : 256) * WNW;
@@ -406,9 +563,18 @@ PDT_API int pdt_stem_wgrad_splits(int N, int H, int W, int Cout) {
 // slab[splits][64][256] = per-wave partials of the stem weight gradient (space-to-depth layout)
 // with the BN backward apply formed from dA, y and bnc = [k1; k2; k3; scale; shift] ([5][64]);
 // reduce with pdt_wgrad_reduce(slab, out, nullptr, nullptr, splits, 64, 256, ...).
+PDT_API int pdt_stem_wgrad_v(const void* x4, const void* dA, const void* y, const float* bnc, float* slab, int N,
+                             int H, int W, int Cout, int variant, hipStream_t stream);
+
 PDT_API int pdt_stem_wgrad(const void* x4, const void* dA, const void* y, const float* bnc, float* slab, int N, int H,
                            int W, int Cout, hipStream_t stream) {
-  const int splits = pdt_stem_wgrad_splits(N, H, W, Cout);
+  return pdt_stem_wgrad_v(x4, dA, y, bnc, slab, N, H, W, Cout, 0, stream);
+}
+
+// variant 0: v1 (register prefetch, 4-row bands), 1: v2 (all-DMA double-buffered, 2-row bands)
+PDT_API int pdt_stem_wgrad_v(const void* x4, const void* dA, const void* y, const float* bnc, float* slab, int N,
+                             int H, int W, int Cout, int variant, hipStream_t stream) {
+  const int splits = pdt_stem_wgrad_splits_v(N, H, W, Cout, variant);
   if (splits < 0) return splits;
   if ((long long)N * H * W * 4 >= (1LL << 31) || (long long)N * (H / 2) * (W / 2) * 64 >= (1LL << 31)) return -5;
   static const void* zcache[PDT_MAX_DEV] = {};
@@ -421,7 +587,12 @@ PDT_API int pdt_stem_wgrad(const void* x4, const void* dA, const void* y, const 
   p.zero = pdt_symbol_addr(HIP_SYMBOL(stem_zero), zcache);
   if (p.zero == nullptr) return PDT_ERR_SYMBOL;
   p.N = N; p.H = H; p.W = W;
-  p.ntiles = N * (H / 2 / WB);
-  hipLaunchKernelGGL(stem_wgrad_kernel, dim3(splits / WNW), dim3(WNTH), 0, stream, p);
+  if (variant == 1) {
+    p.ntiles = N * (H / 2 / V2B);
+    hipLaunchKernelGGL(stem_wgrad2_kernel, dim3(splits / 2), dim3(WNTH), 0, stream, p);
+  } else {
+    p.ntiles = N * (H / 2 / WB);
+    hipLaunchKernelGGL(stem_wgrad_kernel, dim3(splits / WNW), dim3(WNTH), 0, stream, p);
+  }
   PDT_RETURN_LAUNCH();
 }

@@ -37,6 +37,8 @@ _SIGS = {
     "pdt_stem_fwd": (c_int, [P, P, P, P, c_int, c_int, c_int, c_int, P]),
     "pdt_stem_wgrad_splits": (c_int, [c_int, c_int, c_int, c_int]),
     "pdt_stem_wgrad": (c_int, [P, P, P, P, P, c_int, c_int, c_int, c_int, P]),
+    "pdt_stem_wgrad_v": (c_int, [P, P, P, P, P, c_int, c_int, c_int, c_int, c_int, P]),
+    "pdt_stem_wgrad_splits_v": (c_int, [c_int, c_int, c_int, c_int, c_int]),
     "pdt_conv_nt_stat_rows": (c_int, [c_int, c_int, c_int, c_int]),
     "pdt_conv_nt_bnb_rows": (c_int, [c_int, c_int, c_int, c_int]),
     "pdt_conv_nt_num_variants": (c_int, []),
@@ -1979,37 +1981,45 @@ def _unit_fwd_s2d(x, w, gamma, beta, bna: _BNArgs):
 
 def _stem_wgrad_halo(u: _Unit, dA, coef, dw256, generic) -> bool:
     """The halo-patch stem weight gradient (csrc/stem.hip, the BN backward apply in its dY
-    staging) into ``dw256``; a tuned per-geometry choice against ``generic()`` (the generic
-    weight gradient path, itself tuned; key stem1w; ``PDT_STEM_HALO=0`` forces it). False:
-    not taken here (the caller runs ``generic``)."""
+    staging) into ``dw256``: variant 0 (register prefetch, 4-row bands) or 1 (all operands by
+    LDS-DMA, double-buffered 2-row bands), a tuned per-geometry choice against each other and
+    ``generic()`` (the generic weight-gradient path, itself tuned; key stem2w, value -1 =
+    generic; ``PDT_STEM_HALO=0`` forces generic). False: not taken here (the caller runs
+    ``generic``)."""
     lib = _load()
     N, H, W, Cout = u.N, u.H, u.W, u.Cout
-    splits = lib.pdt_stem_wgrad_splits(N, H, W, Cout)
-    if os.environ.get("PDT_STEM_HALO", "1") == "0" or splits < 0 or u.x.shape[1] != 4:
+    if os.environ.get("PDT_STEM_HALO", "1") == "0" or u.x.shape[1] != 4 or \
+            lib.pdt_stem_wgrad_splits_v(N, H, W, Cout, 0) < 0:
         return False
-    ws = torch.empty(lib.pdt_wgrad_workspace(splits, Cout, 256), dtype=torch.float32, device=dA.device)
+    ws = {}
 
-    def run_halo():
-        rc = lib.pdt_stem_wgrad(_p(u.x), _p(dA), _p(u.y), _p(coef), _p(ws), N, H, W, Cout, _s())
+    def run_halo(v):
+        splits = lib.pdt_stem_wgrad_splits_v(N, H, W, Cout, v)
+        if splits < 0:
+            return NOT_APPLICABLE
+        if v not in ws:
+            ws[v] = torch.empty(lib.pdt_wgrad_workspace(splits, Cout, 256), dtype=torch.float32, device=dA.device)
+        rc = lib.pdt_stem_wgrad_v(_p(u.x), _p(dA), _p(u.y), _p(coef), _p(ws[v]), N, H, W, Cout, v, _s())
         if rc == 0:
-            rc = lib.pdt_wgrad_reduce(_p(ws), _p(dw256), None, None, splits, Cout, 256, 1.0, 0, _s())
+            rc = lib.pdt_wgrad_reduce(_p(ws[v]), _p(dw256), None, None, splits, Cout, 256, 1.0, 0, _s())
         return rc
 
-    key = f"stem1w:{N},{H},{W},{Cout}"
+    key = f"stem2w:{N},{H},{W},{Cout}"
     table = _tuned()
     if key in table:
         choice = int(table[key])
     elif not _tune_allowed():
         choice = 1
     else:
-        _chk(run_halo(), "stem_wgrad")
+        choice = _time_variants(2, run_halo)
         generic()  # settles the generic path's own tuning before it is timed
-        choice = 1 if _time_fn(run_halo) < _time_fn(generic) else 0
+        if choice < 0 or _time_fn(generic) < _time_fn(lambda: run_halo(choice)):
+            choice = -1
         table[key] = choice
         _save_tuned()
-    if choice != 1:
+    if choice < 0:
         return False
-    _chk(run_halo(), "stem_wgrad")
+    _chk(run_halo(choice), "stem_wgrad")
     return True
 
 

@@ -9,4 +9,4 @@ run ${T}_bench_fused.txt 400 python bench.py || exit $?
 PDT_POOL_BNRED_BLOCKS=2048 run ${T}_bench_fused2048.txt 400 python bench.py || exit $?
 PDT_POOL_BNRED=0 run ${T}_bench_sep2.txt 400 python bench.py || exit $?
 run ${T}_bench_fused2.txt 400 python bench.py || exit $?
-bash scripts/gpu_job.sh $T ktrace
+bash scripts/gpu_job.sh $T ktrace bench:--model,vit_b_16,--fp8 ktrace:--model,vit_b_16,--fp8,--batch,1024

@@ -66,7 +66,14 @@ def _worker(port, hook, q):
         for p, r in zip(model.parameters(), ref.parameters()):
             want = r.grad if hook is None else r.grad.to(torch.bfloat16).float()
             errs.append(float((p.grad - want).abs().max() / want.abs().max().clamp_min(1e-12)))
-            views += int(p.grad._base is not None)  # gradient_as_bucket_view: grads live in the buckets
+            # gradients live in the buckets: torch DDP (gradient_as_bucket_view) hands out bucket
+            # views; the native reducer's slots are adopted by autograd through detach(), which
+            # shares the storage without keeping ``_base`` -- check the address instead
+            if hook is None:
+                views += int(any(b.flat.data_ptr() <= p.grad.data_ptr() <
+                                 b.flat.data_ptr() + b.flat.numel() * b.flat.element_size() for b in ddp.buckets))
+            else:
+                views += int(p.grad._base is not None)
         # FusedSGD on the bucket views == FusedSGD on plain gradients (same grads in)
         if hook is None:
             o1 = FusedSGD(list(model.parameters()), lr=0.1, momentum=0.9, weight_decay=1e-4)

@@ -63,15 +63,16 @@ def test_stem_halo_in_the_model_matches_generic(monkeypatch):
     assert nrmerr(outs[0][2], outs[1][2]) < 1e-3
 
 
+@pytest.mark.parametrize("variant", [0, 1])
 @pytest.mark.parametrize("N", [2, 40])
-def test_stem_halo_weight_gradient_with_bn_backward_apply(N):
+def test_stem_halo_weight_gradient_with_bn_backward_apply(N, variant):
     """pdt_stem_wgrad (+ pdt_wgrad_reduce) = the stem weight gradient of dy = k1 * relu_gate(dA)
     + k2 * y + k3 (gate from y * scale + shift > 0), dy rounded to bf16 as the kernel stages it."""
     lib = no._load()
     dev = "cuda"
     torch.manual_seed(13)
     H = W = 224
-    splits = lib.pdt_stem_wgrad_splits(N, H, W, 64)
+    splits = lib.pdt_stem_wgrad_splits_v(N, H, W, 64, variant)
     assert splits > 0
     x = torch.randn(N, 3, H, W, device=dev).to(torch.bfloat16)
     x4 = F.pad(x.permute(0, 2, 3, 1), (0, 1)).contiguous()
@@ -82,7 +83,8 @@ def test_stem_halo_weight_gradient_with_bn_backward_apply(N):
                         torch.randn(64, device=dev) * 0.2]).contiguous()
     ws = torch.full((lib.pdt_wgrad_workspace(splits, 64, 256),), float("nan"), device=dev)
     dw256 = torch.full((64, 256), float("nan"), device=dev)
-    assert lib.pdt_stem_wgrad(no._p(x4), no._p(dA), no._p(y), no._p(coef), no._p(ws), N, H, W, 64, no._s()) == 0
+    assert lib.pdt_stem_wgrad_v(no._p(x4), no._p(dA), no._p(y), no._p(coef), no._p(ws), N, H, W, 64, variant,
+                                no._s()) == 0
     assert lib.pdt_wgrad_reduce(no._p(ws), no._p(dw256), None, None, splits, 64, 256, 1.0, 0, no._s()) == 0
     torch.cuda.synchronize()
     k1, k2, k3, sc, sh = coef
