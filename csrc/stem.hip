@@ -464,6 +464,19 @@ __global__ void __launch_bounds__(WNTH, 1) stem_wgrad2_kernel(StemWgParams p) {
     }
   };
 
+  __syncthreads();  // coef table
+  float c_k1[8], c_k2[8], c_k3[8], c_sc[8], c_sh[8];
+  {
+    const int c8 = v2_chunk(tid >> 3, tid & 7) * 8;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      c_k1[k] = coef[c8 + k];
+      c_k2[k] = coef[64 + c8 + k];
+      c_k3[k] = coef[128 + c8 + k];
+      c_sc[k] = coef[192 + c8 + k];
+      c_sh[k] = coef[256 + c8 + k];
+    }
+  }
   const int wr = wave & 1, kh0 = (wave >> 1) * KB2;
   f32x4 acc[4][KB2];
 #pragma unroll
@@ -482,11 +495,12 @@ __global__ void __launch_bounds__(WNTH, 1) stem_wgrad2_kernel(StemWgParams p) {
     issue(tile + gridDim.x, set ^ 1);                  // next band: in flight through convert + MFMAs
     char* const dyt = smem + set * V2SET;
     const char* const yt = dyt + V2RAW;
-    // dA -> dy in place (each thread its own chunks; channels from the swizzled chunk)
+    // dA -> dy in place (each thread its own chunks: pixel rows (tid >> 3) + 32 l all share
+    // the swizzle bits (row >> 1) & 3, so the logical channel chunk -- and the coefficients,
+    // loaded once -- are the same for all of them)
 #pragma unroll
     for (int l = 0; l < V2LR; ++l) {
       const int qq = tid + WNTH * l;
-      const int px = qq >> 3, c8 = v2_chunk(px, qq & 7) * 8;
       u32x4* dp = reinterpret_cast<u32x4*>(dyt + qq * 16);
       const u32x4 da = *dp, yy = *reinterpret_cast<const u32x4*>(yt + qq * 16);
       u32x4 o;
@@ -498,8 +512,8 @@ __global__ void __launch_bounds__(WNTH, 1) stem_wgrad2_kernel(StemWgParams p) {
           const int k = 2 * e + h;
           const float d = h ? hi_bf(da[e]) : lo_bf(da[e]);
           const float yv = h ? hi_bf(yy[e]) : lo_bf(yy[e]);
-          const float gk = (yv * coef[192 + c8 + k] + coef[256 + c8 + k]) > 0.f ? d : 0.f;
-          v[h] = coef[c8 + k] * gk + coef[64 + c8 + k] * yv + coef[128 + c8 + k];
+          const float gk = (yv * c_sc[k] + c_sh[k]) > 0.f ? d : 0.f;
+          v[h] = c_k1[k] * gk + c_k2[k] * yv + c_k3[k];
         }
         o[e] = pack2bf(v[0], v[1]);
       }
