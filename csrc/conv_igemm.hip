@@ -537,9 +537,13 @@ PDT_API int pdt_fp8_meta_roll_partial(float* meta, const float* partial, int nbl
                                       hipStream_t st);
 
 namespace {
-constexpr int NVAR_F8 = 11;
-constexpr int VAR_F8_BM[NVAR_F8] = {128, 128, 256, 128, 64, 128, 256, 128, 256, 128, 256};
-constexpr int VAR_F8_BN[NVAR_F8] = {128, 128, 128, 256, 128, 64, 64, 128, 128, 256, 256};
+// id 11: the 256x256 tile on FOUR waves (2x2 of 128x128, 256 accumulators per lane, one wave
+// per SIMD): per K-tile a CU's fragment reads fall from 192 KB (8 waves of 128x64) to 128 KB
+// -- the fp8 MFMA consumes twice the bytes per cycle of the bf16 one, so the LDS read
+// bandwidth, not the matrix core, bounds the 8-wave tile.
+constexpr int NVAR_F8 = 12;
+constexpr int VAR_F8_BM[NVAR_F8] = {128, 128, 256, 128, 64, 128, 256, 128, 256, 128, 256, 256};
+constexpr int VAR_F8_BN[NVAR_F8] = {128, 128, 128, 256, 128, 64, 64, 128, 128, 256, 256, 256};
 
 template <int F8>
 int launch_f8(int v, const NTParams& p, hipStream_t st) {
@@ -555,6 +559,7 @@ int launch_f8(int v, const NTParams& p, hipStream_t st) {
     case 8: return launch<256, 128, 3, true, false, true, 512, 4, F8, true>(p, st);
     case 9: return launch<128, 256, 3, true, false, true, 512, 2, F8, true>(p, st);
     case 10: return launch<256, 256, 2, true, false, true, 512, 2, F8, true>(p, st);
+    case 11: return launch<256, 256, 2, true, false, true, 256, 2, F8, true>(p, st);
   }
   return -3;
 }

@@ -93,7 +93,7 @@ static __device__ __attribute__((aligned(64))) u32x4 wg8_zero_chunk[4];
 // flight across it). A wave instruction writes 1 KB of LDS lane-linearly, so the chunk
 // swizzle moves to the source address (the XOR is an involution).
 template <int BM, int BN, int NSTAGE, int NTH, int WM, bool BIAS, int KS = 1, bool GL = false>
-__global__ void __launch_bounds__(NTH, NTH == 256 && !GL ? 2 : 1) wgrad_f8_kernel(WG8Params p) {
+__global__ void __launch_bounds__(NTH, NTH == 256 && !GL && BM * BN < 65536 ? 2 : 1) wgrad_f8_kernel(WG8Params p) {
   constexpr int BK = BK1 * KS;
   constexpr int WN = NTH / 64 / WM;
   constexpr int RBA = BM, RBB = BN;  // bytes per LDS row
@@ -306,7 +306,9 @@ struct WG8Var {
 // 4-wave tiles (2x2 waves, two workgroups per CU) and 8-wave tiles; target = workgroups,
 // KS = MFMA k-steps (128 token rows each) per k-tile / barrier
 // GL = LDS-DMA ring (NS stages, one workgroup per CU)
-constexpr int WG8_NVAR = 21;
+// ids 21-24: 256x256 on FOUR waves (2x2 of 128x128, one wave per SIMD, accumulators in
+// AGPRs): a CU's fragment reads per k-step fall from 192 KB (8 waves of 128x64) to 128 KB
+constexpr int WG8_NVAR = 25;
 constexpr WG8Var WG8_VARS[WG8_NVAR] = {
     {128, 128, 2, 256, 1024, 1, 0}, {128, 128, 1, 256, 1024, 1, 0}, {128, 128, 2, 256, 512, 1, 0},
     {128, 128, 1, 256, 2048, 1, 0}, {256, 128, 2, 512, 512, 1, 0},  {128, 256, 2, 512, 512, 1, 0},
@@ -315,6 +317,8 @@ constexpr WG8Var WG8_VARS[WG8_NVAR] = {
     {256, 256, 1, 512, 512, 1, 0},  {128, 128, 3, 256, 1024, 1, 1}, {128, 128, 4, 256, 1024, 1, 1},
     {256, 128, 3, 512, 512, 1, 1},  {128, 256, 3, 512, 512, 1, 1},  {256, 128, 3, 512, 1024, 1, 1},
     {128, 128, 2, 256, 1024, 1, 1}, {256, 256, 2, 512, 256, 1, 1},  {256, 256, 2, 512, 512, 1, 1},
+    {256, 256, 2, 256, 512, 1, 0},  {256, 256, 2, 256, 256, 1, 0},  {256, 256, 2, 256, 256, 1, 1},
+    {256, 256, 2, 256, 512, 1, 1},
 };
 
 WG8Var wg8_variant(int v) { return (v < 0 || v >= WG8_NVAR) ? WG8_VARS[0] : WG8_VARS[v]; }
@@ -329,7 +333,8 @@ int launch8(const WG8Var& w, dim3 grid, const WG8Params& p_in, hipStream_t st) {
 #define G8(a, b, ns, t, wm) hipLaunchKernelGGL((wgrad_f8_kernel<a, b, ns, t, wm, BIAS, 1, true>), grid, dim3(t), 0, st, p)
   if (w.GL) {
     if (w.BM == 256 && w.BN == 256) {
-      G8(256, 256, 2, 512, 2);
+      if (w.NTH == 256) G8(256, 256, 2, 256, 2);
+      else G8(256, 256, 2, 512, 2);
     } else if (w.NTH == 512) {
       if (w.BM == 256) G8(256, 128, 3, 512, 4);
       else G8(128, 256, 3, 512, 2);
@@ -342,6 +347,8 @@ int launch8(const WG8Var& w, dim3 grid, const WG8Params& p_in, hipStream_t st) {
     }
   } else if (w.KS == 2) {
     hipLaunchKernelGGL((wgrad_f8_kernel<128, 128, 1, 256, 2, BIAS, 2>), grid, dim3(256), 0, st, p);
+  } else if (w.BM == 256 && w.BN == 256 && w.NTH == 256) {
+    L8(256, 256, 2, 256, 2);  // (single-stage: 620 B/lane of scratch, not built)
   } else if (w.BM == 256 && w.BN == 256) {
     if (w.NS == 2) L8(256, 256, 2, 512, 2);
     else L8(256, 256, 1, 512, 2);
