@@ -2375,6 +2375,29 @@ def fp8_weight(w: torch.Tensor):
     return val
 
 
+# Tuned-table id of the library path for PLAIN fp8 GEMMs (no activation / aux / addend / fp8
+# side output; bias allowed, added in bf16): hipBLASLt through torch._scaled_mm with the
+# device dequant scales as its scale operands (no host sync). On the ViT-B/16 batch-1024
+# data-gradient shapes and the qkv projection it measured 1.16-1.42x the native ring tiles
+# (profiles/vit_fp8_gemm_library_round4.txt); every fused-epilogue GEMM stays native.
+F8_LIB = 100
+
+
+def _f8_lib_ok(out, act, aux, addend, q8) -> bool:
+    return act == 0 and aux is None and addend is None and q8 is None and out.is_contiguous() and \
+        hasattr(torch, "_scaled_mm") and os.environ.get("PDT_FP8_LIB", "1") == "1"
+
+
+def _gemm_f8_lib(a, b, out, dq_a, dq_b, fmt_a, bias):
+    M, N = a.shape[0], b.shape[0]
+    A = a.view(torch.float8_e5m2 if fmt_a == E5M2 else torch.float8_e4m3fn)
+    B = b.view(torch.float8_e4m3fn).t()  # [K][N] column-major: the layout hipBLASLt takes
+    bb = bias.to(torch.bfloat16) if bias is not None else None
+    torch._scaled_mm(A, B, scale_a=dq_a.reshape(()), scale_b=dq_b.reshape(()), bias=bb, out_dtype=torch.bfloat16,
+                     out=out.view(M, N))
+    return 0
+
+
 def gemm_f8(a, b, out, dq_a, dq_b, *, fmt_a=E4M3, bias=None, act=0, aux=None, addend=None, variant=None,
             q8=None):
     """out[M, N] (bf16) = dq_a*dq_b * a[M, K] @ b[N, K]^T (+bias, act) (+ addend); a, b uint8 fp8
@@ -2394,9 +2417,22 @@ def gemm_f8(a, b, out, dq_a, dq_b, *, fmt_a=E4M3, bias=None, act=0, aux=None, ad
     if q8 is None:
         args = lambda v: (_p(a), _p(b), _p(out), _p(bias), _p(dq_a), _p(dq_b), M, N, K, K, K, N, fmt_a, act,  # noqa
                           _p(aux), _p(addend), v, _s())
+        lib_ok = _f8_lib_ok(out, act, aux, addend, q8)
         if variant is None:
             key = f"f8b:{M},{N},{K},{fmt_a},{act},{int(bias is not None)}"
-            variant = _autotune(key, lib.pdt_gemm_f8_num_variants(), lambda v: lib.pdt_gemm_f8(*args(v)))
+            nv = lib.pdt_gemm_f8_num_variants()
+            # candidate nv (tuning only) = the library path, stored as F8_LIB
+            run = lambda v: lib.pdt_gemm_f8(*args(v)) if v < nv else _gemm_f8_lib(a, b, out, dq_a, dq_b,  # noqa
+                                                                                  fmt_a, bias)
+            variant = _autotune(key, nv + int(lib_ok), run)
+            if variant == nv and lib_ok:
+                variant = F8_LIB
+                _tuned()[key] = F8_LIB
+                _save_tuned()
+        if variant == F8_LIB:
+            if lib_ok:
+                return _gemm_f8_lib(a, b, out, dq_a, dq_b, fmt_a, bias) or out
+            variant = -1  # (library path disabled / not applicable: the built-in native choice)
         _chk(lib.pdt_gemm_f8(*args(variant)), "gemm_f8")
         return out
     codes, meta, qfmt, only = q8
