@@ -29,6 +29,7 @@
 // bf16 kernels do. lse is the forward's (log2 domain), delta = rowsum(dO * O) is computed
 // here from the bf16 O and dO.
 #include "fp8_mfma.h"
+#include <stdlib.h>
 
 namespace {
 
@@ -66,29 +67,50 @@ __global__ void __launch_bounds__(512) attn_bwd_f8_kernel(AttnBwdF8Params p) {
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int col = lane & 31, hh = lane >> 5, g = lane >> 4, j = lane & 15;
-  const int bh = blockIdx.x, b = bh / p.H, h = bh % p.H;
-  const u16* Qg = p.qkv + (long)b * p.T * p.ld + h * D;
-  const u16* Kg = Qg + p.H * D;
-  const u16* Vg = Qg + 2 * p.H * D;
-  const u16* dOg = p.dout + (long)b * p.T * p.ldo + h * D;
-  const u16* Og = p.out + (long)b * p.T * p.ldo + h * D;
+  const int nbh = p.B * p.H;
+
+  // ---------------------------------------------------------------- head loads
+  // Persistent: a workgroup walks heads bh = blockIdx.x, + gridDim.x, ... (one 137-KB
+  // workgroup per CU, so nothing else would overlap a head's HBM loads). The next head's
+  // bf16 operands are fetched into registers while this head's dQ phase runs.
+  // chunk q = tid + 512 it: row q >> 3, 16-B column ch = q & 7 (the 8 lanes of a row adjacent)
+  u32x4 rq[NQP], rk[NQP], rv[NQP], rd[NQP], ro[NQP];
+  float rl[NQP];
+  // (always assigns every register -- zeros past the last head -- so no stale copy of the
+  // previous head's operands stays live through a phase)
+  auto load_head = [&](int bh) __attribute__((always_inline)) {
+    const bool hok = bh < nbh;
+    const int b = hok ? bh / p.H : 0, h = hok ? bh % p.H : 0;
+    const u16* Qg = p.qkv + (long)b * p.T * p.ld + h * D;
+    const u16* dOg = p.dout + (long)b * p.T * p.ldo + h * D;
+    const u16* Og = p.out + (long)b * p.T * p.ldo + h * D;
+#pragma unroll
+    for (int it = 0; it < NQP; ++it) {
+      const int q = tid + 512 * it, row = q >> 3, ch = q & 7;
+      const u32x4 z = {0, 0, 0, 0};
+      rq[it] = rk[it] = rv[it] = rd[it] = ro[it] = z;
+      rl[it] = INFINITY;  // rows >= T: -lse = -inf -> P = 0
+      if (hok && row < p.T) {
+        rq[it] = *reinterpret_cast<const u32x4*>(Qg + (long)row * p.ld + ch * 8);
+        rk[it] = *reinterpret_cast<const u32x4*>(Qg + p.H * D + (long)row * p.ld + ch * 8);
+        rv[it] = *reinterpret_cast<const u32x4*>(Qg + 2 * p.H * D + (long)row * p.ld + ch * 8);
+        rd[it] = *reinterpret_cast<const u32x4*>(dOg + (long)row * p.ldo + ch * 8);
+        ro[it] = *reinterpret_cast<const u32x4*>(Og + (long)row * p.ldo + ch * 8);
+        if (ch == 0) rl[it] = p.lse[(long)bh * p.T + row];
+      }
+    }
+  };
+  load_head(blockIdx.x);
+
+  for (int bh = blockIdx.x; bh < nbh; bh += gridDim.x) {
+  const int b = bh / p.H, h = bh % p.H;
 
   // ---------------------------------------------------------------- staging
-  // chunk q = tid + 512 it: row q >> 3, 16-B column ch = q & 7 (the 8 lanes of a row adjacent)
-  u32x4 rq[NQP], rk[NQP], rv[NQP], rd[NQP];
   float mx[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
   for (int it = 0; it < NQP; ++it) {
     const int q = tid + 512 * it, row = q >> 3, ch = q & 7;
-    u32x4 a = {0, 0, 0, 0}, k = a, v = a, d = a, o = a;
-    if (row < p.T) {
-      a = *reinterpret_cast<const u32x4*>(Qg + (long)row * p.ld + ch * 8);
-      k = *reinterpret_cast<const u32x4*>(Kg + (long)row * p.ld + ch * 8);
-      v = *reinterpret_cast<const u32x4*>(Vg + (long)row * p.ld + ch * 8);
-      d = *reinterpret_cast<const u32x4*>(dOg + (long)row * p.ldo + ch * 8);
-      o = *reinterpret_cast<const u32x4*>(Og + (long)row * p.ldo + ch * 8);
-    }
-    rq[it] = a; rk[it] = k; rv[it] = v; rd[it] = d;
+    const u32x4 a = rq[it], k = rk[it], v = rv[it], d = rd[it], o = ro[it];
     float dl = 0.f;
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
@@ -101,7 +123,7 @@ __global__ void __launch_bounds__(512) attn_bwd_f8_kernel(AttnBwdF8Params p) {
     dl = row8_sum(dl);  // delta of this row: the 8 lanes of the row (DPP)
     if (ch == 0) {
       dl_s[row] = dl;
-      nlse_s[row] = row < p.T ? -p.lse[(long)bh * p.T + row] : -INFINITY;  // rows >= T: P = 0
+      nlse_s[row] = -rl[it];
     }
   }
 #pragma unroll
@@ -246,6 +268,7 @@ __global__ void __launch_bounds__(512) attn_bwd_f8_kernel(AttnBwdF8Params p) {
     }
   }
   __syncthreads();
+  load_head(bh + gridDim.x);  // in flight across the dQ phase
 
   // ---------------------------------------------------------------- phase 2: dQ
   const int nqt = (p.T + 31) / 32;
@@ -280,6 +303,8 @@ __global__ void __launch_bounds__(512) attn_bwd_f8_kernel(AttnBwdF8Params p) {
       }
     }
   }
+  __syncthreads();  // every LDS image, scale and row statistic is restaged for the next head
+  }
 }
 
 }  // namespace
@@ -299,6 +324,18 @@ PDT_API int pdt_attn_bwd_f8_debug(const void* qkv, const void* out, const void* 
   return attn_bwd_f8(qkv, out, dout, lse, dqkv, B, T, H, scale, dbg, st);
 }
 
+// PDT_ATTN_BWD_PERSIST=0: one workgroup per head (the grid B*H, each running the head loop
+// once) instead of one per CU -- an A/B switch
+static int attn_bwd_grid(int nbh) {
+  static int persist = -1;
+  if (persist < 0) {
+    const char* e = getenv("PDT_ATTN_BWD_PERSIST");
+    persist = (e && e[0] == '0') ? 0 : 1;
+  }
+  const int g = persist ? pdt_num_cus() : nbh;
+  return nbh < g ? nbh : g;
+}
+
 static int attn_bwd_f8(const void* qkv, const void* out, const void* dout, const float* lse, void* dqkv, int B,
                        int T, int H, float scale, float* dbg, hipStream_t st) {
   if (T < 1 || T > 256) return -1;
@@ -315,7 +352,8 @@ static int attn_bwd_f8(const void* qkv, const void* out, const void* dout, const
   p.scale = scale;
   p.dbg = dbg;
   const int nqp = (T + 63) / 64;
-  dim3 g(B * H);
+  // one workgroup per CU (the LDS images hold 137 KB), each walking B*H / grid heads
+  dim3 g(attn_bwd_grid(B * H));
 #define BWD(N) hipLaunchKernelGGL((attn_bwd_f8_kernel<N>), g, dim3(512), 0, st, p)
   switch (nqp) {
     case 1: BWD(1); break;

@@ -168,3 +168,17 @@ static inline const void* pdt_symbol_addr(const void* sym, const void** cache) {
   }
   return cache[dev];
 }
+
+// compute units of the current device (cached per device id; 256 if the query fails) --
+// the grid of a persistent kernel
+static inline int pdt_num_cus() {
+  static int cache[PDT_MAX_DEV] = {};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= PDT_MAX_DEV) return 256;
+  if (cache[dev] == 0) {
+    int n = 0;
+    cache[dev] = (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && n > 0) ? n
+                                                                                                               : 256;
+  }
+  return cache[dev];
+}
