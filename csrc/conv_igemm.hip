@@ -342,7 +342,10 @@ static int conv_nt_impl(const void* src, const void* b, void* out, float* stats,
   if (Cs % 8 != 0 || K % 8 != 0 || Ncol % 8 != 0 || ldo % 8 != 0 || ldb % 8 != 0) return -1;
   if (pix != 0 && (pix % 4 != 0 || pix > Cs)) return -10;
   if (K != nth * ntw * Cs) return -2;
-  if (act == 3 && (addend == nullptr || addend_mask != nullptr || aux != nullptr || bias != nullptr)) return -4;
+  if ((act == 3 || act == 5) && (addend == nullptr || addend_mask != nullptr || aux != nullptr || bias != nullptr))
+    return -4;
+  if (act == 4 && (aux == nullptr || addend != nullptr)) return -4;  // dual GELU: aux = gelu'(z)
+  if (act < 0 || act > 5) return -4;
   NTParams p;
   p.src = (const u16*)src;
   p.b = (const u16*)b;
@@ -531,7 +534,8 @@ PDT_API int pdt_conv_nt_ax(const void* src, const void* b, void* out, float* sta
 // ---------------------------------------------------------------------------
 // fp8 GEMM  out[m, n] = dq_a * dq_b * sum_k A[m, k] B[n, k] (+ bias, act, aux)
 // A: [M][lda] fp8 (e4m3 if fmt_a == 0, e5m2 if 1), B: [N][ldb] e4m3, out bf16 [M][ldo],
-// optional bf16 addend [M][ldo] (residual add, or the GELU-backward operand with act 3).
+// optional bf16 addend [M][ldo] (residual add, or the GELU-backward operand with act 3 / the
+// stored GELU derivative with act 5); act 4 = GELU with its derivative written to aux.
 // K, lda, ldb in BYTES (= elements), multiples of 128 / 16 / 16.
 PDT_API int pdt_fp8_meta_roll_partial(float* meta, const float* partial, int nblk, int fmt, float* dq_out,
                                       hipStream_t st);
@@ -581,7 +585,9 @@ static int gemm_f8_impl(const void* a, const void* b, void* out, const float* bi
   p.bias = bias;
   p.addend = (const u16*)addend;  // [M][ldo] bf16: out += addend (act 3: out *= gelu'(addend))
   p.addend_mask = nullptr;
-  if (act == 3 && (addend == nullptr || aux != nullptr || bias != nullptr)) return -4;
+  if ((act == 3 || act == 5) && (addend == nullptr || aux != nullptr || bias != nullptr)) return -4;
+  if (act == 4 && (aux == nullptr || addend != nullptr)) return -4;
+  if (act < 0 || act > 5) return -4;
   p.Hs = 1; p.Ws = 1; p.Cs = K / 2;
   p.Hm = 1; p.Wm = 1;
   p.M = M;

@@ -588,7 +588,7 @@ def select_nt_variant(src, b, out, *, with_stats=False, bias=None, act=0, aux=No
     # partial-stat rows depend on the variant's BM and waves-along-M: size for the largest
     rows = max(lib.pdt_conv_nt_stat_rows(M, a["Ncol"], a["K"], v) for v in range(nvar))
     stats = torch.empty(2 * rows * a["Ncol"], dtype=torch.float32, device=src.device) if with_stats else None
-    tune_add = addend if act == 3 else None  # act 3 reads its operand through the addend pointer
+    tune_add = addend if act in (3, 5) else None  # acts 3 / 5 read their operand through the addend pointer
     best = _time_variants(nvar, lambda v: lib.pdt_conv_nt(*_nt_args(src, b, out, stats, bias, a, act, v, aux=aux,
                                                                     addend=tune_add)),
                           allowed if allowed is not None else _variant_filter())
@@ -598,6 +598,16 @@ def select_nt_variant(src, b, out, *, with_stats=False, bias=None, act=0, aux=No
 
 
 ACT = {None: 0, "none": 0, "relu": 1, "gelu": 2}
+# epilogue ids beyond ACT: 3 = out * gelu'(addend = z); 4 = GELU whose aux output is gelu'(z)
+# (not z) -- both from one tanh; 5 = out * addend (the stored derivative)
+ACT_GELU_GRAD, ACT_GELU_DUAL, ACT_MUL = 3, 4, 5
+
+
+def _gelu_dual() -> bool:
+    """The MLP stores gelu'(z) in the fc1 epilogue (act 4) and its backward multiplies by it
+    in the fc2 data-gradient epilogue (act 5) -- the derivative's tanh is not recomputed there.
+    PDT_GELU_DUAL=0: store z and recompute gelu'(z) in the backward epilogue (acts 2 / 3)."""
+    return os.environ.get("PDT_GELU_DUAL", "1") == "1"
 
 
 def conv_nt(src, b, out, *, stats=None, bias=None, relu=False, act=None, variant=None, addend=None, aux=None,
@@ -2630,6 +2640,8 @@ class _Mlp(torch.autograd.Function):
         bias1, bias2 = b1.float().contiguous(), b2.float().contiguous()
         cfg = fp8_settings()
         f8w = fp8 and cfg["dgrad"] and cfg["wgrad"]
+        dual = _gelu_dual()
+        act1 = ACT_GELU_DUAL if dual else ACT["gelu"]  # z holds gelu'(fc1 pre-activation) when dual
         if fp8:
             pre = _prequant(x, mlp.fc1)
             xq, dqx = pre if pre is not None else _quant_act(x2, mlp.fc1)
@@ -2637,15 +2649,14 @@ class _Mlp(torch.autograd.Function):
             meta2 = getattr(mlp.fc2, "_pdt_fp8_meta", None) if cfg["scaling"] == "delayed" else None
             if meta2 is not None:  # fc1's epilogue writes fc2's e4m3 input (bf16 a only if a bf16 wgrad needs it)
                 aq = torch.empty((Mrows, Hd), dtype=torch.uint8, device=dev)
-                dqa = gemm_f8(xq, w1q, a, dqx, dqw1, bias=bias1, act=ACT["gelu"], aux=z,
-                              q8=(aq, meta2, E4M3, f8w))
+                dqa = gemm_f8(xq, w1q, a, dqx, dqw1, bias=bias1, act=act1, aux=z, q8=(aq, meta2, E4M3, f8w))
             else:
-                gemm_f8(xq, w1q, a, dqx, dqw1, bias=bias1, act=ACT["gelu"], aux=z)
+                gemm_f8(xq, w1q, a, dqx, dqw1, bias=bias1, act=act1, aux=z)
                 aq, dqa = _quant_act(a, mlp.fc2)
             w2q, _, dqw2 = fp8_weight(w2)
             gemm_f8(aq, w2q, out, dqa, dqw2, bias=bias2, addend=res)
         else:
-            _gemm_bf16(x2, bf16_weight(w1), a, bias=bias1, act="gelu", aux=z)
+            _gemm_bf16(x2, bf16_weight(w1), a, bias=bias1, act=act1, aux=z)
             _gemm_bf16(a, bf16_weight(w2), out, bias=bias2, addend=res)
         if f8w:  # fp8 weight gradients: the e4m3 GEMM inputs replace the bf16 ones in the saved state
             ctx.f8 = (xq, dqx, aq, dqa)
@@ -2654,6 +2665,7 @@ class _Mlp(torch.autograd.Function):
             ctx.f8 = None
             ctx.save_for_backward(x2, a, z, w1, w2)
         ctx.shp, ctx.fp8, ctx.mlp = shp, fp8, mlp
+        ctx.act2 = ACT_MUL if dual else ACT_GELU_GRAD  # the fc2 data gradient's epilogue
         ctx.fp8_dgrad = fp8 and cfg["dgrad"]
         return out.reshape(*shp[:-1], Nout)
 
@@ -2675,11 +2687,12 @@ class _Mlp(torch.autograd.Function):
                 else None
             if gmeta1 is not None:  # the epilogue also writes fc1's e5m2 output gradient (bf16 dz: bias grad)
                 dzq = torch.empty((Mrows, Hd), dtype=torch.uint8, device=g.device)
-                dqdz = gemm_f8(gq, w2qt, dz, dqg, dqw2, fmt_a=E5M2, act=3, addend=z, q8=(dzq, gmeta1, E5M2, False))
+                dqdz = gemm_f8(gq, w2qt, dz, dqg, dqw2, fmt_a=E5M2, act=ctx.act2, addend=z,
+                               q8=(dzq, gmeta1, E5M2, False))
             else:
-                gemm_f8(gq, w2qt, dz, dqg, dqw2, fmt_a=E5M2, act=3, addend=z)
+                gemm_f8(gq, w2qt, dz, dqg, dqw2, fmt_a=E5M2, act=ctx.act2, addend=z)
         else:
-            _gemm_bf16(g2, bf16_weight_t(w2), dz, act=3, addend=z)  # dz = (g W2) * gelu'(z)
+            _gemm_bf16(g2, bf16_weight_t(w2), dz, act=ctx.act2, addend=z)  # dz = (g W2) * gelu'(z)
         if f8 is not None:
             dw2, db2 = linear_wgrad_f8(gq, f8[2], dqg, f8[3], dy16=g2, with_bias=need[4], w=w2,
                                        b=ctx.brefs[1]) if need[3] \

@@ -571,6 +571,54 @@ def test_gemm_f8_all_variants(M, N, K, fmt):
         assert relerr(out, ref) < 1e-2, (v, relerr(out, ref))
 
 
+def _gelu_and_grad(z):
+    u = 0.7978845608 * (z + 0.044715 * z ** 3)
+    t = torch.tanh(u)
+    return 0.5 * z * (1 + t), 0.5 * (1 + t) + 0.5 * z * (1 - t * t) * 0.7978845608 * (1 + 3 * 0.044715 * z * z)
+
+
+def test_gelu_dual_and_mul_epilogues_all_variants():
+    """act 4: out = gelu(z), aux = gelu'(z) from one tanh (z = the bf16-rounded GEMM + bias);
+    act 5: out = (A B^T) * addend -- on every bf16 conv_nt tile (staged and direct epilogues,
+    rings) and every fp8 tile."""
+    torch.manual_seed(31)
+    M, N, K = 300, 256, 128
+    x = torch.randn(M, K, device="cuda").to(torch.bfloat16)
+    w = (torch.randn(N, K, device="cuda") * 0.2).to(torch.bfloat16)
+    bias = torch.randn(N, device="cuda") * 0.5
+    z = x.float() @ w.float().t() + bias
+    zr = z.to(torch.bfloat16).float()
+    g_ref, d_ref = _gelu_and_grad(zr)
+    add = torch.rand(M, N, device="cuda").to(torch.bfloat16)
+    mul_ref = (x.float() @ w.float().t()) * add.float()
+    geo = dict(Hs=1, Ws=1, Cs=K, Nimg=M, Hm=1, Wm=1, Ncol=N, K=K, ldb=K, sh=1, sw=1, oh0=0, ow0=0, dh=1, dw=1,
+               nth=1, ntw=1, Ho=1, Wo=1, osh=1, osw=1, oph=0, opw=0, ldo=N)
+    lib = no._load()
+    for v in range(lib.pdt_conv_nt_num_variants()):
+        if lib.pdt_conv_nt_variant_kind(v) != 0:
+            continue  # halo / streaming kernels: no activation epilogue
+        y = torch.full((M, N), float("nan"), device="cuda").to(torch.bfloat16)
+        aux = torch.full_like(y, float("nan"))
+        no.conv_nt(x, w, y, bias=bias, act=no.ACT_GELU_DUAL, aux=aux, variant=v, **geo)
+        y2 = torch.full_like(y, float("nan"))
+        no.conv_nt(x, w, y2, act=no.ACT_MUL, addend=add, variant=v, **geo)
+        torch.cuda.synchronize()
+        assert relerr(y, g_ref) < 1e-2, (v, relerr(y, g_ref))
+        assert relerr(aux, d_ref) < 1e-2, (v, relerr(aux, d_ref))
+        assert relerr(y2, mul_ref) < 1e-2, (v, relerr(y2, mul_ref))
+    qa, dqa = no.quantize_fp8(x, 0)
+    qb, dqb = no.quantize_fp8(w.float(), 0)
+    z8 = (_f8(qa, 0) * dqa) @ (_f8(qb, 0) * dqb).t() + bias
+    g8, d8 = _gelu_and_grad(z8.to(torch.bfloat16).float())
+    for v in range(lib.pdt_gemm_f8_num_variants()):
+        y = torch.full((M, N), float("nan"), device="cuda").to(torch.bfloat16)
+        aux = torch.full_like(y, float("nan"))
+        no.gemm_f8(qa, qb, y, dqa, dqb, bias=bias, act=no.ACT_GELU_DUAL, aux=aux, variant=v)
+        torch.cuda.synchronize()
+        assert relerr(y, g8) < 1e-2, (v, relerr(y, g8))
+        assert relerr(aux, d8) < 1e-2, (v, relerr(aux, d8))
+
+
 @pytest.mark.parametrize("fmt", [0, 1])
 @pytest.mark.parametrize("with_bias", [False, True])
 def test_gemm_f8_library_path(fmt, with_bias):
