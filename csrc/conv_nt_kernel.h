@@ -115,13 +115,7 @@ __device__ __forceinline__ float gelu_grad(float z) {
 
 // act 4 (the MLP's fc1): gelu_tanh(z) AND its derivative from one tanh -- the derivative is
 // stored as the aux output so the fc2 data gradient's epilogue is a plain multiply (act 5)
-__device__ __forceinline__ void gelu_dual(float z, float& g, float& d) {
-  const float u = 0.7978845608f * (z + 0.044715f * z * z * z);
-  const float h = 0.5f * (1.f + pdt_tanh(u));
-  const float du = 0.7978845608f * (1.f + 3.f * 0.044715f * z * z);
-  g = z * h;
-  d = h + 2.f * z * h * (1.f - h) * du;  // 0.5 z (1 - t^2) du, t = 2h - 1
-}
+__device__ __forceinline__ void gelu_dual(float z, float& g, float& d) { pdt_gelu_dual(z, g, d); }
 
 __device__ __forceinline__ int swz(int row, int chunk) { return chunk ^ ((row >> 1) & 7); }
 

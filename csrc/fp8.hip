@@ -202,6 +202,51 @@ __global__ void __launch_bounds__(256) cast_fp8_delayed_kernel(const void* __res
   }
 }
 
+// The MLP fc1 epilogue as a pass after a library GEMM (hipBLASLt has no GELU-derivative or
+// fp8 side output): y = the bf16 pre-activation (bias included) ->
+//   aux = gelu'(y) (bf16), q = fp8(bf16(gelu(y)) * scale) with the delayed scale, amax recorded,
+//   a_out (optional, may alias y) = gelu(y) (bf16)
+// -- the same values the fused conv_nt act-4 + q8 epilogue writes. n % 8 == 0.
+template <int FMT>
+__global__ void __launch_bounds__(256) gelu_dual_cast_kernel(const u16* __restrict__ y, long n,
+                                                             float* __restrict__ meta, uint8_t* __restrict__ q,
+                                                             u16* __restrict__ aux, u16* a_out) {
+  __shared__ float red[4];
+  const float s = meta[0];
+  float m = 0.f;
+  const long stride = (long)gridDim.x * 256 * 8;
+  for (long base = ((long)blockIdx.x * 256 + threadIdx.x) * 8; base < n; base += stride) {
+    const u32x4 w = *reinterpret_cast<const u32x4*>(y + base);
+    u32x4 gq, dq;
+    float g[8];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      float g0, g1, d0, d1;
+      pdt_gelu_dual(lo_bf(w[e]), g0, d0);
+      pdt_gelu_dual(hi_bf(w[e]), g1, d1);
+      gq[e] = pack2bf(g0, g1);
+      dq[e] = pack2bf(d0, d1);
+      g[2 * e] = lo_bf(gq[e]);
+      g[2 * e + 1] = hi_bf(gq[e]);
+    }
+#pragma unroll
+    for (int e = 0; e < 8; ++e) m = fmaxf(m, fabsf(g[e]));
+    *reinterpret_cast<u32x4*>(aux + base) = dq;
+    if (a_out != nullptr) *reinterpret_cast<u32x4*>(a_out + base) = gq;
+    uint2 o;
+    o.x = cvt4<FMT>(g[0] * s, g[1] * s, g[2] * s, g[3] * s);
+    o.y = cvt4<FMT>(g[4] * s, g[5] * s, g[6] * s, g[7] * s);
+    *reinterpret_cast<uint2*>(q + base) = o;
+  }
+  m = warp_max(m);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = m;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const float bm = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
+    atomicMax(reinterpret_cast<unsigned int*>(meta) + 2, __float_as_uint(bm));
+  }
+}
+
 // history roll, one tiny launch after the cast (a last-block roll inside the
 // cast would need a device-scope release fence per block: an L2 write-back on
 // the multi-XCD part)
@@ -310,6 +355,25 @@ PDT_API int pdt_cast_fp8_delayed(const void* x, int bf16, long n, float* meta, i
 #undef CD
   if (fmt == 0) hipLaunchKernelGGL(fp8_meta_roll_kernel<0>, dim3(1), dim3(64), 0, st, meta, dq_out);
   else hipLaunchKernelGGL(fp8_meta_roll_kernel<1>, dim3(1), dim3(64), 0, st, meta, dq_out);
+  PDT_RETURN_LAUNCH();
+}
+
+// y [n] bf16 -> aux = gelu'(y), q = fp8 codes of gelu(y) (delayed scale, history rolled, dq_out =
+// this cast's dequant factor), a_out = gelu(y) if given (may be y itself)
+PDT_API int pdt_gelu_dual_cast_fp8(const void* y, long n, float* meta, int fmt, void* q, void* aux, void* a_out,
+                                   float* dq_out, hipStream_t st) {
+  if (n % 8 != 0 || !y || !meta || !q || !aux) return -1;
+  const int nb = nblocks(n);
+  const u16* Y = (const u16*)y;
+  if (fmt == 0) {
+    hipLaunchKernelGGL(gelu_dual_cast_kernel<0>, dim3(nb), dim3(256), 0, st, Y, n, meta, (uint8_t*)q, (u16*)aux,
+                       (u16*)a_out);
+    hipLaunchKernelGGL(fp8_meta_roll_kernel<0>, dim3(1), dim3(64), 0, st, meta, dq_out);
+  } else {
+    hipLaunchKernelGGL(gelu_dual_cast_kernel<1>, dim3(nb), dim3(256), 0, st, Y, n, meta, (uint8_t*)q, (u16*)aux,
+                       (u16*)a_out);
+    hipLaunchKernelGGL(fp8_meta_roll_kernel<1>, dim3(1), dim3(64), 0, st, meta, dq_out);
+  }
   PDT_RETURN_LAUNCH();
 }
 

@@ -21,6 +21,16 @@ __device__ __forceinline__ float pdt_tanh(float x) {
   return 1.f - 2.f * __builtin_amdgcn_rcpf(1.f + __expf(2.f * x));
 }
 
+// gelu_tanh(z) and its derivative from one tanh (the MLP's act-4 epilogue and its library-GEMM
+// twin in csrc/fp8.hip)
+__device__ __forceinline__ void pdt_gelu_dual(float z, float& g, float& d) {
+  const float u = 0.7978845608f * (z + 0.044715f * z * z * z);
+  const float h = 0.5f * (1.f + pdt_tanh(u));
+  const float du = 0.7978845608f * (1.f + 3.f * 0.044715f * z * z);
+  g = z * h;
+  d = h + 2.f * z * h * (1.f - h) * du;  // 0.5 z (1 - t^2) du, t = 2h - 1
+}
+
 // four floats -> four packed OCP fp8 codes (FMT 0 = e4m3fn, 1 = e5m2) with the gfx950
 // packed converts (round to nearest even); clamped to the finite range first
 template <int FMT>

@@ -111,6 +111,7 @@ _SIGS = {
     "pdt_attn_fwd_tiles": (c_int, [P, P, P, c_int, c_int, c_int, c_float, P]),
     "pdt_attn_set_bwd_single": (c_int, [c_int]),
     "pdt_gemm_f8_num_variants": (c_int, []),
+    "pdt_gelu_dual_cast_fp8": (c_int, [P, c_long, P, c_int, P, P, P, P, P]),
     "pdt_gemm_f8": (c_int, [P, P, P, P, P, P] + [c_int] * 8 + [P, P, c_int, P]),
     "pdt_bn_set_unroll": (c_int, [c_int]),
     "pdt_amax_blocks": (c_int, [c_long]),
@@ -2408,6 +2409,29 @@ def _gemm_f8_lib(a, b, out, dq_a, dq_b, fmt_a, bias):
     return 0
 
 
+def _fc1_lib(M, Hd, K) -> bool:
+    """The MLP's fp8 fc1 as the library GEMM (+bias) followed by one pass that writes gelu'(z),
+    the e4m3 codes of gelu(z) and their amax (pdt_gelu_dual_cast_fp8), instead of the native
+    GEMM with that epilogue fused (act 4 + fp8 side output). Tuned-table key ``fc1lib:M,Hd,K``
+    (1 = library); PDT_FP8_FC1_LIB=0/1 forces either."""
+    env = os.environ.get("PDT_FP8_FC1_LIB")
+    if env is not None:
+        return env == "1" and hasattr(torch, "_scaled_mm")
+    return bool(_tuned().get(f"fc1lib:{M},{Hd},{K}", 0)) and hasattr(torch, "_scaled_mm") and \
+        os.environ.get("PDT_FP8_LIB", "1") == "1"
+
+
+def _fc1_lib_forward(xq, w1q, a, z, aq, dqx, dqw1, bias1, meta, keep_a):
+    """a <- x W1^T + b1 (library GEMM), then z <- gelu'(a), aq <- e4m3(gelu(a)), and (keep_a) a <- gelu(a)
+    in place. Returns the codes' dequant factor (device [1])."""
+    lib = _load()
+    dqa = torch.empty(1, dtype=torch.float32, device=a.device)
+    _gemm_f8_lib(xq, w1q, a, dqx, dqw1, E4M3, bias1)
+    _chk(lib.pdt_gelu_dual_cast_fp8(_p(a), a.numel(), _p(meta), E4M3, _p(aq), _p(z), _p(a) if keep_a else None,
+                                    _p(dqa), _s()), "gelu_dual_cast_fp8")
+    return dqa
+
+
 def gemm_f8(a, b, out, dq_a, dq_b, *, fmt_a=E4M3, bias=None, act=0, aux=None, addend=None, variant=None,
             q8=None):
     """out[M, N] (bf16) = dq_a*dq_b * a[M, K] @ b[N, K]^T (+bias, act) (+ addend); a, b uint8 fp8
@@ -2649,7 +2673,10 @@ class _Mlp(torch.autograd.Function):
             meta2 = getattr(mlp.fc2, "_pdt_fp8_meta", None) if cfg["scaling"] == "delayed" else None
             if meta2 is not None:  # fc1's epilogue writes fc2's e4m3 input (bf16 a only if a bf16 wgrad needs it)
                 aq = torch.empty((Mrows, Hd), dtype=torch.uint8, device=dev)
-                dqa = gemm_f8(xq, w1q, a, dqx, dqw1, bias=bias1, act=act1, aux=z, q8=(aq, meta2, E4M3, f8w))
+                if dual and _fc1_lib(Mrows, Hd, K):
+                    dqa = _fc1_lib_forward(xq, w1q, a, z, aq, dqx, dqw1, bias1, meta2, keep_a=not f8w)
+                else:
+                    dqa = gemm_f8(xq, w1q, a, dqx, dqw1, bias=bias1, act=act1, aux=z, q8=(aq, meta2, E4M3, f8w))
             else:
                 gemm_f8(xq, w1q, a, dqx, dqw1, bias=bias1, act=act1, aux=z)
                 aq, dqa = _quant_act(a, mlp.fc2)
