@@ -367,6 +367,57 @@ int launch8(const WG8Var& w, dim3 grid, const WG8Params& p_in, hipStream_t st) {
   return 0;
 }
 
+// the kernel a variant launches (launch8's dispatch), for the occupancy query
+template <bool BIAS>
+const void* kernel8(const WG8Var& w) {
+#define K8(a, b, ns, t, wm) return reinterpret_cast<const void*>(&wgrad_f8_kernel<a, b, ns, t, wm, BIAS>)
+#define KG8(a, b, ns, t, wm) return reinterpret_cast<const void*>(&wgrad_f8_kernel<a, b, ns, t, wm, BIAS, 1, true>)
+  if (w.GL) {
+    if (w.BM == 256 && w.BN == 256) {
+      if (w.NTH == 256) KG8(256, 256, 2, 256, 2);
+      KG8(256, 256, 2, 512, 2);
+    }
+    if (w.NTH == 512) {
+      if (w.BM == 256) KG8(256, 128, 3, 512, 4);
+      KG8(128, 256, 3, 512, 2);
+    }
+    if (w.NS == 4) KG8(128, 128, 4, 256, 2);
+    if (w.NS == 3) KG8(128, 128, 3, 256, 2);
+    KG8(128, 128, 2, 256, 2);
+  }
+  if (w.KS == 2) return reinterpret_cast<const void*>(&wgrad_f8_kernel<128, 128, 1, 256, 2, BIAS, 2>);
+  if (w.BM == 256 && w.BN == 256 && w.NTH == 256) K8(256, 256, 2, 256, 2);
+  if (w.BM == 256 && w.BN == 256) {
+    if (w.NS == 2) K8(256, 256, 2, 512, 2);
+    K8(256, 256, 1, 512, 2);
+  }
+  if (w.NTH == 512) {
+    if (w.BM == 256) K8(256, 128, 2, 512, 4);
+    K8(128, 256, 2, 512, 2);
+  }
+  if (w.BM == 64) K8(64, 128, 2, 256, 2);
+  if (w.NS == 2) K8(128, 128, 2, 256, 2);
+  K8(128, 128, 1, 256, 2);
+#undef K8
+#undef KG8
+}
+
+// workgroups of variant v resident on the whole device at once (occupancy API, the smaller of
+// the bias / no-bias instantiations; cached per variant)
+int slots8(int v) {
+  static int cache[WG8_NVAR] = {};
+  const int vi = (v < 0 || v >= WG8_NVAR) ? 0 : v;
+  if (cache[vi] == 0) {
+    const WG8Var w = wg8_variant(vi);
+    int a = 0, b = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&a, kernel8<true>(w), w.NTH, 0) != hipSuccess) a = 1;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, kernel8<false>(w), w.NTH, 0) != hipSuccess) b = 1;
+    int n = a < b ? a : b;
+    cache[vi] = (n < 1 ? 1 : n) * pdt_num_cus();
+  }
+  return cache[vi];
+}
+
 int reduce_groups8(int splits, int Mo, int No) {
   long n4 = (long)Mo * No / 4;
   int xb = (int)((n4 + 255) / 256);
@@ -385,11 +436,41 @@ PDT_API int pdt_wgrad_f8_plan(int M, int Mo, int No, int variant, int* ktiles_pe
   const int tiles = ((Mo + w.BM - 1) / w.BM) * ((No + w.BN - 1) / w.BN);
   const int BK = BK1 * w.KS;
   const int nk = (M + BK - 1) / BK;
-  int splits = (w.target + tiles - 1) / tiles;
-  if (splits > nk) splits = nk;
-  if (splits < 1) splits = 1;
-  while (splits > 1 && (nk + splits - 1) / splits * BK < 512) --splits;  // >= 512 token rows per split
-  const int kps = (nk + splits - 1) / splits;
+  // Splits s <= ceil(target / tiles) minimising (dispatch waves) x (k-tiles per split): the
+  // device holds slots8(v) workgroups at once, and a grid one workgroup past a multiple of it
+  // runs a whole extra wave for that straggler (tiles = 27 at target 512: 513 workgroups, 3
+  // waves of 83 k-tiles; s = 9: 243 workgroups, 1 wave of 176). Ties keep fewer splits (less
+  // slab traffic). >= 512 token rows per split.
+  int smax = (w.target + tiles - 1) / tiles;
+  if (smax > nk) smax = nk;
+  if (smax < 1) smax = 1;
+  static int legacy = -1;  // PDT_WG8_PLAN=0: the previous plan, s = ceil(target / tiles) (A/B switch)
+  if (legacy < 0) {
+    const char* e = getenv("PDT_WG8_PLAN");
+    legacy = (e && e[0] == '0') ? 1 : 0;
+  }
+  if (legacy) {
+    int s = smax;
+    while (s > 1 && (nk + s - 1) / s * BK < 512) --s;
+    const int kps = (nk + s - 1) / s;
+    *ktiles_per_split = kps;
+    return (nk + kps - 1) / kps;
+  }
+  const long slots = slots8(variant);
+  int best_s = 1;
+  long best_cost = -1;
+  for (int s = 1; s <= smax; ++s) {
+    const int kps = (nk + s - 1) / s;
+    if (s > 1 && kps * BK < 512) break;
+    const int se = (nk + kps - 1) / kps;
+    const long waves = ((long)tiles * se + slots - 1) / slots;
+    const long cost = waves * kps;
+    if (best_cost < 0 || cost < best_cost) {
+      best_cost = cost;
+      best_s = s;
+    }
+  }
+  const int kps = (nk + best_s - 1) / best_s;
   *ktiles_per_split = kps;
   return (nk + kps - 1) / kps;
 }
