@@ -488,18 +488,98 @@ static void launch_wg(const WGVar& w, dim3 grid, const WGParams& p, hipStream_t 
 #undef WG_LAUNCH_PF
 }
 
-// Plan: number of splits so the grid covers the chip; returns splits and
-// writes ktiles_per_split.
+// the kernel launch_wg / launch_wg_bna start for a variant (for the occupancy query)
+template <bool BIAS, bool BNA>
+static const void* wg_kernel(const WGVar& w) {
+#define KP(a, b, c, t, wm, pf) return reinterpret_cast<const void*>(&wgrad_kernel<a, b, c, t, wm, pf, BIAS, BNA>)
+  const int BM = w.BM, BN = w.BN, NS = w.NS;
+  if constexpr (!BNA) {
+    if (NS == 3) {
+      if (w.NTH == 512) {
+        if (BM == 256 && BN == 256) KP(256, 256, 2, 512, 2, 2);
+        if (BM == 256) KP(256, 128, 2, 512, 4, 2);
+        KP(128, 256, 2, 512, 2, 2);
+      }
+      if (BM == 64 && BN == 64) KP(64, 64, 2, NT, 2, 2);
+      if (BM == 64) KP(64, 128, 2, NT, 2, 2);
+      if (BN == 64) KP(128, 64, 2, NT, 2, 2);
+      KP(128, 128, 2, NT, 2, 2);
+    }
+    if (w.NTH == 512) {
+      if (BM == 256 && BN == 256) KP(256, 256, 2, 512, 2, 1);
+      if (BM == 256) KP(256, 128, 2, 512, 4, 1);
+      KP(128, 256, 2, 512, 2, 1);
+    }
+  }
+  if (NS == 2) {
+    if (BM == 64 && BN == 64) KP(64, 64, 2, NT, 2, 1);
+    if (BM == 64) KP(64, 128, 2, NT, 2, 1);
+    if (BN == 64) KP(128, 64, 2, NT, 2, 1);
+    KP(128, 128, 2, NT, 2, 1);
+  }
+  if (BM == 64 && BN == 64) KP(64, 64, 1, NT, 2, 1);
+  if (BM == 64) KP(64, 128, 1, NT, 2, 1);
+  if (BN == 64) KP(128, 64, 1, NT, 2, 1);
+  KP(128, 128, 1, NT, 2, 1);
+#undef KP
+}
+
+// workgroups of variant v resident on the device at once: the occupancy API's minimum over
+// the instantiations the variant may launch (plain, bias, and -- variants 0..11 -- the BN
+// backward apply), cached per variant
+static long wg_slots(int v, const WGVar& w) {
+  static int cache[WG_NVAR] = {};
+  if (v < 0 || v >= WG_NVAR) return 2L * pdt_num_cus();
+  if (cache[v] == 0) {
+    int n = 1 << 20;
+    const void* ks[3] = {wg_kernel<false, false>(w), wg_kernel<true, false>(w),
+                         (w.NS <= 2 && w.NTH == NT) ? wg_kernel<false, true>(w) : nullptr};
+    for (const void* k : ks) {
+      int b = 0;
+      if (k == nullptr) continue;
+      if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, k, w.NTH, 0) != hipSuccess) b = 1;
+      n = b < n ? b : n;
+    }
+    cache[v] = n < 1 ? 1 : n;
+  }
+  return (long)cache[v] * pdt_num_cus();
+}
+
+// Plan: splits s <= ceil(target / tiles) minimising (dispatch waves) x (k-tiles per split), the
+// device holding wg_slots() workgroups at once (a grid a few workgroups past a multiple of it
+// runs a whole extra wave for them); ties keep fewer splits. At least 8 k-tiles per split so
+// the pipeline amortises. Returns splits and writes ktiles_per_split. PDT_WG_PLAN=0: the
+// previous plan, s = ceil(target / tiles) (A/B switch).
 PDT_API int pdt_wgrad_plan(int M, int Mo, int No, int variant, int* ktiles_per_split) {
   const WGVar w = wg_variant(variant, Mo, No);
   const int BM = w.BM, BN = w.BN, target = w.target;
   int tiles = ((Mo + BM - 1) / BM) * ((No + BN - 1) / BN);
   int nk = (M + BK - 1) / BK;
-  int splits = (target + tiles - 1) / tiles;
-  if (splits > nk) splits = nk;
-  if (splits < 1) splits = 1;
-  // at least 8 k-tiles per split so the pipeline amortises
-  while (splits > 1 && (nk + splits - 1) / splits < 8) --splits;
+  int smax = (target + tiles - 1) / tiles;
+  if (smax > nk) smax = nk;
+  if (smax < 1) smax = 1;
+  static int legacy = -1;
+  if (legacy < 0) {
+    const char* e = getenv("PDT_WG_PLAN");
+    legacy = (e && e[0] == '0') ? 1 : 0;
+  }
+  int splits = smax;
+  if (legacy) {
+    while (splits > 1 && (nk + splits - 1) / splits < 8) --splits;
+  } else {
+    const long slots = wg_slots(variant, w);
+    long best_cost = -1;
+    for (int s = 1; s <= smax; ++s) {
+      const int kps = (nk + s - 1) / s;
+      if (s > 1 && kps < 8) break;
+      const int se = (nk + kps - 1) / kps;
+      const long cost = (((long)tiles * se + slots - 1) / slots) * kps;
+      if (best_cost < 0 || cost < best_cost) {
+        best_cost = cost;
+        splits = s;
+      }
+    }
+  }
   int kps = (nk + splits - 1) / splits;
   splits = (nk + kps - 1) / kps;
   *ktiles_per_split = kps;
