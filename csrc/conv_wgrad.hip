@@ -689,6 +689,15 @@ PDT_API int pdt_conv_wgrad2(const void* dy, const void* x, float* slab, float* o
 
 // Deterministic reduction of the split-K slabs [splits][Mo][No] (+ the optional bias slab
 // [splits][Mo]) into out (= or += scale * sum); shared by the bf16 and fp8 weight gradients.
+// out[n] (= or +=) scale * sum of nrows rows of [nrows][n] (n % 4 == 0): the bias-gradient partial rows
+PDT_API int pdt_wgrad_reduce_rows(const float* rows, float* out, int nrows, int n, float scale, int accumulate,
+                                  hipStream_t stream) {
+  if (n % 4 != 0 || nrows < 1) return -1;
+  hipLaunchKernelGGL(wgrad_reduce1_kernel, dim3((n / 4 + 255) / 256, 1), dim3(256), 0, stream, rows, out,
+                     (long)(n / 4), nrows, 1, scale, accumulate, 1);
+  PDT_RETURN_LAUNCH();
+}
+
 PDT_API int pdt_wgrad_reduce(float* slab, float* out, const float* bslab, float* bias_out, int splits, int Mo, int No,
                              float scale, int accumulate, hipStream_t stream) {
   const int G = reduce_groups(splits, Mo, No);

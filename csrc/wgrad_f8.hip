@@ -24,6 +24,8 @@
 
 PDT_API int pdt_wgrad_reduce(float* slab, float* out, const float* bslab, float* bias_out, int splits, int Mo, int No,
                              float scale, int accumulate, hipStream_t stream);
+PDT_API int pdt_wgrad_reduce_rows(const float* rows, float* out, int nrows, int n, float scale, int accumulate,
+                                  hipStream_t stream);
 
 namespace {
 
@@ -241,14 +243,18 @@ __global__ void __launch_bounds__(NTH, NTH == 256 && !GL && BM * BN < 65536 ? 2 
   }
 
   if constexpr (BIAS) {
-    if (tn == 0) {  // bias gradient: column sums of the bf16 dY rows of this split (L2-resident)
+    {  // bias gradient: column sums of the bf16 dY rows of this split (L2-resident), the rows
+       // shared out among the split's ntn tile columns (one workgroup summing all of them
+       // was the critical path once splits grew long): partial row split * ntn + tn
       constexpr int CPR = BM / 8, RPP = NTH / CPR;
       const int cc = tid % CPR, rr = tid / CPR;
       const int co = co0 + cc * 8;
       float bs[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+      const int sm0 = kt_begin * BK, sm1 = min(p.M, kt_end * BK);
+      const int share = ((sm1 - sm0 + ntn - 1) / ntn + RPP - 1) / RPP * RPP;
       if (co < p.Mo) {
-        const int m1 = min(p.M, kt_end * BK);
-        int m = kt_begin * BK + rr;
+        const int m1 = min(sm1, sm0 + (tn + 1) * share);
+        int m = sm0 + tn * share + rr;
         for (; m + 3 * RPP < m1; m += 4 * RPP) {
           u32x4 v[4];
 #pragma unroll
@@ -280,7 +286,7 @@ __global__ void __launch_bounds__(NTH, NTH == 256 && !GL && BM * BN < 65536 ? 2 
         for (int j = 0; j < RPP; ++j)
 #pragma unroll
           for (int k = 0; k < 8; ++k) t8[k] += red[(j * CPR + tid) * 8 + k];
-        float* bo = p.bslab + (size_t)split * p.Mo + co;
+        float* bo = p.bslab + ((size_t)split * ntn + tn) * p.Mo + co;
         *reinterpret_cast<f32x4*>(bo) = f32x4{t8[0], t8[1], t8[2], t8[3]};
         *reinterpret_cast<f32x4*>(bo + 4) = f32x4{t8[4], t8[5], t8[6], t8[7]};
       }
@@ -475,10 +481,11 @@ PDT_API int pdt_wgrad_f8_plan(int M, int Mo, int No, int variant, int* ktiles_pe
   return (nk + kps - 1) / kps;
 }
 
-// floats of workspace: slabs + stage-1 partials (same layout as pdt_wgrad_workspace) + bias slab
+// floats of workspace: slabs + stage-1 partials (same layout as pdt_wgrad_workspace) + the
+// bias partial rows ([splits][tile columns][Mo]; tile columns <= ceil(No / 128) for every variant)
 PDT_API long pdt_wgrad_f8_workspace(int splits, int Mo, int No) {
   const long G = reduce_groups8(splits, Mo, No);
-  return (long)splits * Mo * No + (G > 1 ? G * Mo * No : 0) + (long)splits * Mo;
+  return (long)splits * Mo * No + (G > 1 ? G * Mo * No : 0) + (long)splits * ((No + 127) / 128) * Mo;
 }
 
 // dW[Mo][No] (fp32, = or +=) from e5m2 dY codes [M][ldy] and e4m3 X codes [M][ldx];
@@ -515,5 +522,10 @@ PDT_API int pdt_linear_wgrad_f8(const void* dy8, const void* x8, const float* dq
   if (lrc) return lrc;
   int e = (int)hipGetLastError();
   if (e) return e;
-  return pdt_wgrad_reduce(slab, out, p.bslab, bias_out, splits, Mo, No, 1.f, accumulate, stream);
+  if (bias_out) {
+    const int rc = pdt_wgrad_reduce_rows(p.bslab, bias_out, splits * ((No + w.BN - 1) / w.BN), Mo, 1.f, accumulate,
+                                         stream);
+    if (rc) return rc;
+  }
+  return pdt_wgrad_reduce(slab, out, nullptr, nullptr, splits, Mo, No, 1.f, accumulate, stream);
 }
