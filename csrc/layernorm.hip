@@ -33,7 +33,9 @@ __global__ void __launch_bounds__(64 * WPB) ln_fwd_kernel(const u16* __restrict_
                                                           float* __restrict__ mean_out, float* __restrict__ rstd_out,
                                                           int rows, float eps, uint8_t* __restrict__ q8 = nullptr,
                                                           const float* __restrict__ meta = nullptr,
-                                                          float* __restrict__ amax_part = nullptr) {
+                                                          float* __restrict__ amax_part = nullptr,
+                                                          const u16* __restrict__ radd = nullptr,
+                                                          u16* __restrict__ xsum = nullptr) {
   const int lane = threadIdx.x & 63;
   int row = blockIdx.x * WPB + (threadIdx.x >> 6);
   __shared__ float red[WPB];
@@ -49,6 +51,13 @@ __global__ void __launch_bounds__(64 * WPB) ln_fwd_kernel(const u16* __restrict_
 #pragma unroll
   for (int c = 0; c < CH; ++c) {
     ld4(xr + (c * 64 + lane) * 4, v[c]);
+    if (radd != nullptr) {  // residual add of a pre-norm block: xsum = bf16(x + r), normalised
+      float r[4];
+      ld4(radd + (long)row * D + (c * 64 + lane) * 4, r);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) v[c][e] = bf2f(f2bf(v[c][e] + r[e]));
+      st4(xsum + (long)row * D + (c * 64 + lane) * 4, v[c]);
+    }
     s += v[c][0] + v[c][1] + v[c][2] + v[c][3];
   }
   const float mean = warp_sum(s) * (1.f / D);
@@ -292,6 +301,41 @@ PDT_API int pdt_fp8_meta_roll_partial(float* meta, const float* partial, int nbl
                                       hipStream_t st);
 
 PDT_API int pdt_ln_fwd_f8_blocks(int rows) { return (rows + WPB - 1) / WPB; }
+
+// LayerNorm of xsum = bf16(x + r) (written to xsum): the residual add of a pre-norm block moved
+// out of the producing GEMM's epilogue (so a library GEMM can produce x). q (optional, with
+// meta / amax_part / dq_out as pdt_ln_fwd_f8): the e4m3 codes of the output as well.
+PDT_API int pdt_ln_add_fwd(const void* x, const void* r, void* xsum, const float* g, const float* b, void* y,
+                           float* mean, float* rstd, int rows, int D, float eps, void* q, float* meta,
+                           float* amax_part, float* dq_out, hipStream_t st) {
+  if (!r || !xsum || (q && (!meta || !amax_part))) return -1;
+  const int nb = (rows + WPB - 1) / WPB;
+  dim3 grid(nb), blk(64 * WPB);
+#define LA(CH_, F_) hipLaunchKernelGGL((ln_fwd_kernel<CH_, F_>), grid, blk, 0, st, (const u16*)x, g, b, (u16*)y, mean, \
+                                       rstd, rows, eps, (uint8_t*)q, (const float*)meta, amax_part, (const u16*)r,   \
+                                       (u16*)xsum)
+  if (q) {
+    switch (D) {
+      case 256: LA(1, true); break;
+      case 512: LA(2, true); break;
+      case 768: LA(3, true); break;
+      case 1024: LA(4, true); break;
+      default: return -1;
+    }
+  } else {
+    switch (D) {
+      case 256: LA(1, false); break;
+      case 512: LA(2, false); break;
+      case 768: LA(3, false); break;
+      case 1024: LA(4, false); break;
+      default: return -1;
+    }
+  }
+#undef LA
+  int e = (int)hipGetLastError();
+  if (e || !q) return e;
+  return pdt_fp8_meta_roll_partial(meta, amax_part, nb, 0, dq_out, st);
+}
 
 // LayerNorm forward that also emits the e4m3 codes of its output for the next fp8 GEMM
 // (delayed scale meta[0]) and rolls that GEMM's amax history; amax_part holds

@@ -27,6 +27,13 @@ def _fp8_attn() -> bool:
     return os.environ.get("PDT_FP8_ATTN", "1") == "1"
 
 
+def _ln_add() -> bool:
+    """fp8 models: the blocks' residual adds in the next LayerNorm kernel instead of the proj /
+    fc2 GEMM epilogues (PDT_LN_ADD=0 keeps them in the epilogues)."""
+    import os
+    return os.environ.get("PDT_LN_ADD", "1") == "1"
+
+
 class Attention(nn.Module):
     def __init__(self, dim, num_heads):
         super().__init__()
@@ -63,15 +70,28 @@ class Block(nn.Module):
         self.norm2 = nn.LayerNorm(dim, eps=1e-6)
         self.mlp = Mlp(dim, int(dim * mlp_ratio))
 
-    def forward(self, x, fp8=False, prev_fc2=None):
+    def forward(self, x, fp8=False, prev_fc2=None, pending=None, defer=False):
         # pre-norm residual block; the residual adds ride the proj / fc2 GEMM epilogues and
         # their gradients are summed inside the LayerNorm backward (fused.ln_fork)
         # (fp8: the LayerNorm forward kernels also write the e4m3 inputs of qkv / fc1, and
         # the LayerNorm backward kernels the e5m2 output gradients of the previous block's
-        # fc2 / this block's proj -- the layers that produced their inputs)
-        x, h = fused.ln_fork(x, self.norm1, self.attn.qkv if fp8 else None, prev_fc2 if fp8 else None)
-        x = self.attn(h, fp8=fp8, residual=x)
-        x, h = fused.ln_fork(x, self.norm2, self.mlp.fc1 if fp8 else None, self.attn.proj if fp8 else None)
+        # fc2 / this block's proj -- the layers that produced their inputs).
+        # fp8 with _ln_add(): the adds move into the next LayerNorm kernel (fused.ln_add_fork)
+        # so proj / fc2 are plain GEMMs the tuner may give to hipBLASLt; ``pending`` = the
+        # previous block's (fc2 output, residual) pair, ``defer``: return this block's pair.
+        if pending is not None:
+            x, h = fused.ln_add_fork(pending[0], pending[1], self.norm1, self.attn.qkv if fp8 else None,
+                                     prev_fc2 if fp8 else None)
+        else:
+            x, h = fused.ln_fork(x, self.norm1, self.attn.qkv if fp8 else None, prev_fc2 if fp8 else None)
+        if fp8 and _ln_add():
+            y = self.attn(h, fp8=fp8)
+            x, h = fused.ln_add_fork(y, x, self.norm2, self.mlp.fc1, self.attn.proj)
+        else:
+            x = self.attn(h, fp8=fp8, residual=x)
+            x, h = fused.ln_fork(x, self.norm2, self.mlp.fc1 if fp8 else None, self.attn.proj if fp8 else None)
+        if defer:
+            return self.mlp(h, fp8=fp8), x
         return self.mlp(h, fp8=fp8, residual=x)
 
 
@@ -103,8 +123,15 @@ class VisionTransformer(BaseModel):
         cls = self.cls_token.to(x.dtype).expand(B, -1, -1)
         x = torch.cat([cls, x], dim=1) + self.pos_embed.to(x.dtype)
         prev = None
-        for blk in self.blocks:
-            x = blk(x, fp8=self.fp8, prev_fc2=prev)
+        pending = None
+        defer = self.fp8 and _ln_add()
+        for i, blk in enumerate(self.blocks):
+            last = i == len(self.blocks) - 1
+            out = blk(x, fp8=self.fp8, prev_fc2=prev, pending=pending, defer=defer and not last)
+            if defer and not last:
+                pending, x = out, None
+            else:
+                x, pending = out, None
             prev = blk.mlp.fc2
         x = fused.layer_norm(x[:, 0], self.norm)
         return fused.linear(x, self.head)

@@ -178,6 +178,17 @@ def ln_fork(x, ln: nn.LayerNorm, fp8_for: nn.Linear | None = None, grad_fp8_for:
     return x, ln(x)
 
 
+def ln_add_fork(y, r, ln: nn.LayerNorm, fp8_for: nn.Linear | None = None, grad_fp8_for: nn.Linear | None = None):
+    """(y + r, ln(y + r)): :func:`ln_fork` with the block's residual add done by the native
+    LayerNorm kernel (it reads y and r and writes the sum) instead of the producing GEMM's
+    epilogue."""
+    if _use_native(y):
+        from . import native_ops
+        return native_ops.ln_add_fork(y, r, ln, fp8_for, grad_fp8_for)
+    s = y + r
+    return s, ln(s)
+
+
 def attention(q, k, v):
     """softmax(q k^T / sqrt(d)) v for [B,H,T,d] tensors (non-causal)."""
     if _use_native(q):

@@ -58,6 +58,7 @@ _SIGS = {
     "pdt_bn_bwd_apply_dual": (c_int, [P] * 12 + [c_long, c_int, P]),
     "pdt_bn_apply_res_affine": (c_int, [P] * 7 + [c_long, c_int, c_int, P, P]),
     "pdt_ln_fwd_f8": (c_int, [P, P, P, P, P, P, c_int, c_int, c_float, P, P, P, P, P]),
+    "pdt_ln_add_fwd": (c_int, [P] * 8 + [c_int, c_int, c_float] + [P] * 5),
     "pdt_ln_fwd_f8_blocks": (c_int, [c_int]),
     "pdt_fp8_meta_roll_partial": (c_int, [P, P, c_int, c_int, P, P]),
     "pdt_ln_bwd_blocks": (c_int, [c_int]),
@@ -2453,7 +2454,9 @@ def gemm_f8(a, b, out, dq_a, dq_b, *, fmt_a=E4M3, bias=None, act=0, aux=None, ad
                           _p(aux), _p(addend), v, _s())
         lib_ok = _f8_lib_ok(out, act, aux, addend, q8)
         if variant is None:
-            key = f"f8b:{M},{N},{K},{fmt_a},{act},{int(bias is not None)}"
+            # ",r": a residual addend in the epilogue (a different best tile, and no library path)
+            key = f"f8b:{M},{N},{K},{fmt_a},{act},{int(bias is not None)}" + (",r" if addend is not None and act == 0
+                                                                               else "")
             nv = lib.pdt_gemm_f8_num_variants()
             # candidate nv (tuning only) = the library path, stored as F8_LIB
             run = lambda v: lib.pdt_gemm_f8(*args(v)) if v < nv else _gemm_f8_lib(a, b, out, dq_a, dq_b,  # noqa
@@ -2841,34 +2844,103 @@ class _LNFork(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, g_res, dy):
-        x2, gf, stats = ctx.saved_tensors
-        rows, D = x2.shape
-        lib = _load()
-        dev = x2.device
         if dy is None:
-            return g_res, None, None, None
-        dy2 = dy.reshape(rows, D).to(torch.bfloat16).contiguous()
-        add = g_res.reshape(rows, D).to(torch.bfloat16).contiguous() if g_res is not None else None
-        dx = torch.empty_like(x2)
-        blocks = lib.pdt_ln_bwd_blocks(rows)
-        part = torch.empty(2 * blocks * D, dtype=torch.float32, device=dev)
-        dg, db = _grad_buf(ctx.refs[0], (D,)), _grad_buf(ctx.refs[1], (D,))
-        owner = ctx.grad_owner
-        gmeta = getattr(owner, "_pdt_fp8_gmeta", None) if owner is not None else None
-        if gmeta is not None and fp8_settings()["scaling"] == "delayed":
-            # also the e5m2 codes of dx for the fp8 GEMM that consumes this gradient
-            codes = torch.empty((rows, D), dtype=torch.uint8, device=dev)
-            qpart = torch.empty(blocks + 1, dtype=torch.float32, device=dev)
-            dq = qpart[-1:]
-            _chk(lib.pdt_ln_bwd_f8(_p(dy2), _p(x2), _p(gf), _p(stats[0]), _p(stats[1]), _p(dx), _p(dg), _p(db),
-                                   _p(part), rows, D, 0, _p(add), _p(codes), _p(gmeta), _p(qpart), _p(dq), _s()),
-                 "ln_bwd_f8")
-            out = dx.reshape(ctx.shp)
-            out._pdt_f8g = (codes, dq, owner)
-            return out, dg, db, None, None, None, None
-        _chk(lib.pdt_ln_bwd(_p(dy2), _p(x2), _p(gf), _p(stats[0]), _p(stats[1]), _p(dx), _p(dg), _p(db), _p(part),
-                            rows, D, 0, _p(add), _s()), "ln_bwd")
-        return dx.reshape(ctx.shp), dg, db, None, None, None, None
+            return g_res, None, None, None, None, None, None
+        dx, dg, db = _ln_fork_backward(ctx, g_res, dy)
+        return dx, dg, db, None, None, None, None
+
+
+def _ln_fork_backward(ctx, g_res, dy):
+    """LayerNorm backward of a fork (x -> (x, LN(x))) with the residual gradient g_res summed
+    in: (dx, dgamma, dbeta); dx carries the e5m2 codes for ctx.grad_owner (``_pdt_f8g``) when
+    that fp8 layer's gradient history exists."""
+    x2, gf, stats = ctx.saved_tensors
+    rows, D = x2.shape
+    lib = _load()
+    dev = x2.device
+    dy2 = dy.reshape(rows, D).to(torch.bfloat16).contiguous()
+    add = g_res.reshape(rows, D).to(torch.bfloat16).contiguous() if g_res is not None else None
+    dx = torch.empty_like(x2)
+    blocks = lib.pdt_ln_bwd_blocks(rows)
+    part = torch.empty(2 * blocks * D, dtype=torch.float32, device=dev)
+    dg, db = _grad_buf(ctx.refs[0], (D,)), _grad_buf(ctx.refs[1], (D,))
+    owner = ctx.grad_owner
+    gmeta = getattr(owner, "_pdt_fp8_gmeta", None) if owner is not None else None
+    if gmeta is not None and fp8_settings()["scaling"] == "delayed":
+        # also the e5m2 codes of dx for the fp8 GEMM that consumes this gradient
+        codes = torch.empty((rows, D), dtype=torch.uint8, device=dev)
+        qpart = torch.empty(blocks + 1, dtype=torch.float32, device=dev)
+        dq = qpart[-1:]
+        _chk(lib.pdt_ln_bwd_f8(_p(dy2), _p(x2), _p(gf), _p(stats[0]), _p(stats[1]), _p(dx), _p(dg), _p(db),
+                               _p(part), rows, D, 0, _p(add), _p(codes), _p(gmeta), _p(qpart), _p(dq), _s()),
+             "ln_bwd_f8")
+        out = dx.reshape(ctx.shp)
+        out._pdt_f8g = (codes, dq, owner)
+        return out, dg, db
+    _chk(lib.pdt_ln_bwd(_p(dy2), _p(x2), _p(gf), _p(stats[0]), _p(stats[1]), _p(dx), _p(dg), _p(db), _p(part),
+                        rows, D, 0, _p(add), _s()), "ln_bwd")
+    return dx.reshape(ctx.shp), dg, db
+
+
+class _LNAddFork(torch.autograd.Function):
+    """(s, LayerNorm(s)) with s = y + r: the pre-norm block's residual add done by the
+    LayerNorm kernel (it reads y and r, writes s) instead of the epilogue of the GEMM that
+    produced y -- so that GEMM can be a library one (the fp8 proj / fc2 on hipBLASLt). Backward
+    as _LNFork; y and r both receive the summed gradient."""
+
+    @staticmethod
+    def forward(ctx, y, r, g, b, eps, f8meta, f8box, grad_owner):
+        ctx.refs = (g, b)
+        shp = y.shape
+        D = shp[-1]
+        y2 = y.reshape(-1, D).contiguous()
+        r2 = r.reshape(-1, D).to(torch.bfloat16).contiguous()
+        rows = y2.shape[0]
+        xs = torch.empty_like(y2)
+        h = torch.empty_like(y2)
+        stats = torch.empty((2, rows), dtype=torch.float32, device=y.device)
+        gf, bf = g.float().contiguous(), b.float().contiguous()
+        lib = _load()
+        if f8meta is not None:
+            q = torch.empty((rows, D), dtype=torch.uint8, device=y.device)
+            part = torch.empty(lib.pdt_ln_fwd_f8_blocks(rows) + 1, dtype=torch.float32, device=y.device)
+            dq = part[-1:]
+            _chk(lib.pdt_ln_add_fwd(_p(y2), _p(r2), _p(xs), _p(gf), _p(bf), _p(h), _p(stats[0]), _p(stats[1]), rows, D,
+                                    float(eps), _p(q), _p(f8meta), _p(part), _p(dq), _s()), "ln_add_fwd_f8")
+            f8box.append((q, dq))
+        else:
+            _chk(lib.pdt_ln_add_fwd(_p(y2), _p(r2), _p(xs), _p(gf), _p(bf), _p(h), _p(stats[0]), _p(stats[1]), rows, D,
+                                    float(eps), None, None, None, None, _s()), "ln_add_fwd")
+        ctx.save_for_backward(xs, gf, stats)
+        ctx.shp = shp
+        ctx.grad_owner = grad_owner
+        return xs.reshape(shp), h.reshape(shp)
+
+    @staticmethod
+    def backward(ctx, g_res, dy):
+        if dy is None:
+            return g_res, g_res, None, None, None, None, None, None
+        dx, dg, db = _ln_fork_backward(ctx, g_res, dy)
+        return dx, dx, dg, db, None, None, None, None
+
+
+def ln_add_fork(y, r, ln, fp8_for=None, grad_fp8_for=None):
+    """(y + r, ln(y + r)) -- :func:`ln_fork` with the residual add done by the LayerNorm kernel
+    (``grad_fp8_for``: the fp8 layer that produced ``y``)."""
+    D = ln.normalized_shape[-1]
+    if (len(ln.normalized_shape) != 1 or D not in (256, 512, 768, 1024) or not ln.elementwise_affine
+            or y.dtype != torch.bfloat16 or r.shape != y.shape):
+        return ln_fork(y + r.to(y.dtype), ln, fp8_for, grad_fp8_for)
+    meta = None
+    if fp8_for is not None and fp8_settings()["scaling"] == "delayed" and D % 128 == 0:
+        meta = getattr(fp8_for, "_pdt_fp8_meta", None)
+    box: list = []
+    if os.environ.get("PDT_FP8_LN_GRAD", "1") == "0":
+        grad_fp8_for = None
+    xo, h = _LNAddFork.apply(y, r, ln.weight, ln.bias, ln.eps, meta, box, grad_fp8_for)
+    if box:
+        h._pdt_f8 = (box[0][0], box[0][1], fp8_for)
+    return xo, h
 
 
 def ln_fork(x, ln, fp8_for=None, grad_fp8_for=None):

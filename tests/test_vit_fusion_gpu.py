@@ -480,3 +480,49 @@ def test_fp8_attention_forward_and_backward(B, T, H, bwd, pv8, monkeypatch):
         ei = nrmerr(g[:, :, i], gr[:, :, i])
         # fp8 backward: its own e4m3 score recompute adds ~0.1 (tests/test_attention_bwd_f8_gpu.py)
         assert ei < (1.6e-1 if bwd == "f8" else 1e-1), (name, ei)
+
+
+@pytest.mark.parametrize("fp8", [False, True])
+def test_ln_add_fork_matches_add_then_fork(fp8):
+    """ln_add_fork(y, r) == ln_fork(bf16(y + r)): the summed residual stream, the normalised
+    output (and its e4m3 codes under delayed scaling), and both input gradients = the fork's
+    summed gradient (with the producer's e5m2 codes)."""
+    torch.manual_seed(41)
+    D, rows = 768, 394
+    ln = nn.LayerNorm(D, eps=1e-6).cuda()
+    with torch.no_grad():
+        ln.weight.uniform_(0.5, 1.5)
+        ln.bias.uniform_(-0.2, 0.2)
+    consumer, producer = nn.Linear(D, D).cuda(), nn.Linear(D, D).cuda()
+    if fp8:
+        no._quant_act(torch.randn(rows, D, device="cuda").to(torch.bfloat16), consumer)
+        no._quant_grad(torch.randn(rows, D, device="cuda").to(torch.bfloat16), producer, "_pdt_fp8_gmeta")
+    y0 = torch.randn(2, rows // 2, D, device="cuda").to(torch.bfloat16)
+    r0 = torch.randn(2, rows // 2, D, device="cuda").to(torch.bfloat16)
+    g_res = torch.randn_like(y0)
+    g_h = torch.randn_like(y0)
+    metas = [(getattr(consumer, "_pdt_fp8_meta", None), getattr(producer, "_pdt_fp8_gmeta", None))]
+
+    def run(fused_add):
+        if fp8:  # both runs start from the same scaling state
+            consumer._pdt_fp8_meta = metas[0][0].clone()
+            producer._pdt_fp8_gmeta = metas[0][1].clone()
+        y = y0.clone().requires_grad_(True)
+        r = r0.clone().requires_grad_(True)
+        cons, prod = (consumer, producer) if fp8 else (None, None)
+        if fused_add:
+            s, h = no.ln_add_fork(y, r, ln, cons, prod)
+        else:
+            s, h = no.ln_fork(y + r, ln, cons, prod)
+        torch.autograd.backward([s, h], [g_res, g_h])
+        return s, h, y.grad, r.grad
+
+    s1, h1, gy1, gr1 = run(True)
+    s0, h0, gy0, gr0 = run(False)
+    torch.cuda.synchronize()
+    assert torch.equal(s1, s0)
+    assert torch.equal(h1, h0)
+    assert torch.equal(gy1, gy0) and torch.equal(gr1, gy1)
+    if fp8:
+        assert torch.equal(h1._pdt_f8[0], h0._pdt_f8[0])
+        assert torch.equal(gy1._pdt_f8g[0], gy0._pdt_f8g[0]) if hasattr(gy0, "_pdt_f8g") else True
