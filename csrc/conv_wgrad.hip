@@ -545,11 +545,14 @@ static long wg_slots(int v, const WGVar& w) {
   return (long)cache[v] * pdt_num_cus();
 }
 
-// Plan: splits s <= ceil(target / tiles) minimising (dispatch waves) x (k-tiles per split), the
-// device holding wg_slots() workgroups at once (a grid a few workgroups past a multiple of it
-// runs a whole extra wave for them); ties keep fewer splits. At least 8 k-tiles per split so
-// the pipeline amortises. Returns splits and writes ktiles_per_split. PDT_WG_PLAN=0: the
-// previous plan, s = ceil(target / tiles) (A/B switch).
+// Plan: splits s = ceil(target / tiles), at least 8 k-tiles per split so the pipeline
+// amortises. Returns splits and writes ktiles_per_split.
+// PDT_WG_PLAN=1: s <= ceil(target / tiles) minimising (dispatch waves) x (k-tiles per split)
+// with wg_slots() workgroups resident -- the plan that took the fp8 weight gradient's
+// one-workgroup-per-CU tiles from 3 dispatch waves to 1 (csrc/wgrad_f8.hip); on these
+// multi-workgroup-per-CU tiles it picked grids of ~512 workgroups where ~2048 cycling through
+// the resident slots hide latency better (ResNet-50: 290-650 vs 262-582 us per call,
+// gpurun_out r4t vs r4w), so it is off by default here.
 PDT_API int pdt_wgrad_plan(int M, int Mo, int No, int variant, int* ktiles_per_split) {
   const WGVar w = wg_variant(variant, Mo, No);
   const int BM = w.BM, BN = w.BN, target = w.target;
@@ -561,7 +564,7 @@ PDT_API int pdt_wgrad_plan(int M, int Mo, int No, int variant, int* ktiles_per_s
   static int legacy = -1;
   if (legacy < 0) {
     const char* e = getenv("PDT_WG_PLAN");
-    legacy = (e && e[0] == '0') ? 1 : 0;
+    legacy = (e && e[0] == '1') ? 0 : 1;
   }
   int splits = smax;
   if (legacy) {
