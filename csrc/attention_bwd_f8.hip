@@ -147,8 +147,8 @@ __global__ void __launch_bounds__(512) attn_bwd_f8_kernel(AttnBwdF8Params p) {
     const int off = k8_off(row, ch >> 1) + (ch & 1) * 8;
     auto put = [&](char* img, const u32x4& x, float s) __attribute__((always_inline)) {
       uint2 w;
-      w.x = e4m3x4(lo_bf(x[0]) * s, hi_bf(x[0]) * s, lo_bf(x[1]) * s, hi_bf(x[1]) * s);
-      w.y = e4m3x4(lo_bf(x[2]) * s, hi_bf(x[2]) * s, lo_bf(x[3]) * s, hi_bf(x[3]) * s);
+      w.x = e4m3x4_ir(lo_bf(x[0]) * s, hi_bf(x[0]) * s, lo_bf(x[1]) * s, hi_bf(x[1]) * s);
+      w.y = e4m3x4_ir(lo_bf(x[2]) * s, hi_bf(x[2]) * s, lo_bf(x[3]) * s, hi_bf(x[3]) * s);
       *reinterpret_cast<uint2*>(img + off) = w;
     };
     put(Qi, rq[it], sq);
@@ -226,8 +226,8 @@ __global__ void __launch_bounds__(512) attn_bwd_f8_kernel(AttnBwdF8Params p) {
         const float sds = ldexpf(1.f, e);
 #pragma unroll
         for (int w = 0; w < 4; ++w) {
-          pc[u][w] = e4m3x4(pv[4 * w] * 256.f, pv[4 * w + 1] * 256.f, pv[4 * w + 2] * 256.f, pv[4 * w + 3] * 256.f);
-          dc[u][w] = e4m3x4(ds[4 * w] * sds, ds[4 * w + 1] * sds, ds[4 * w + 2] * sds, ds[4 * w + 3] * sds);
+          pc[u][w] = e4m3x4_ir(pv[4 * w] * 256.f, pv[4 * w + 1] * 256.f, pv[4 * w + 2] * 256.f, pv[4 * w + 3] * 256.f);
+          dc[u][w] = e4m3x4_ir(ds[4 * w] * sds, ds[4 * w + 1] * sds, ds[4 * w + 2] * sds, ds[4 * w + 3] * sds);
           // dS^T image [key][q]: 4 consecutive queries 32 qt + 8 w + 4 hh of this key
           *reinterpret_cast<uint32_t*>(dSt + key * DSR + 32 * qt + 8 * w + 4 * hh) = dc[u][w];
         }

@@ -61,8 +61,9 @@ __device__ __forceinline__ uint32_t cvt4_e4m3(float a, float b, float c, float d
 // power-of-two quantization scale for |x|max = amax: largest 2^e with amax * 2^e <= 448
 __device__ __forceinline__ float pow2_scale(float amax) {
   if (!(amax > 0.f)) return 1.f;
-  const int e = (int)floorf(__log2f(448.f / amax));
-  return ldexpf(1.f, max(min(e, 100), -100));
+  int e = max(min((int)floorf(__log2f(448.f / amax)), 100), -100);
+  if (ldexpf(amax, e) > 448.f) --e;  // (the fast log2 may round up at an exact power of two)
+  return ldexpf(1.f, e);
 }
 
 struct AttnF8Params {
@@ -149,8 +150,8 @@ __global__ void __launch_bounds__(256) attn_fwd_f8_kernel(AttnF8Params p) {
         const int row = q >> 3, ch = q & 7;
         const u32x4 v = vv[it];
         uint2 w;
-        w.x = cvt4_e4m3(lo_bf(v[0]) * sv, hi_bf(v[0]) * sv, lo_bf(v[1]) * sv, hi_bf(v[1]) * sv);
-        w.y = cvt4_e4m3(lo_bf(v[2]) * sv, hi_bf(v[2]) * sv, lo_bf(v[3]) * sv, hi_bf(v[3]) * sv);
+        w.x = pdt_cvt4_e4m3_inrange(lo_bf(v[0]) * sv, hi_bf(v[0]) * sv, lo_bf(v[1]) * sv, hi_bf(v[1]) * sv);
+        w.y = pdt_cvt4_e4m3_inrange(lo_bf(v[2]) * sv, hi_bf(v[2]) * sv, lo_bf(v[3]) * sv, hi_bf(v[3]) * sv);
         *reinterpret_cast<uint2*>(Vs + k8_off(row, ch >> 1) + (ch & 1) * 8) = w;
       }
     }
@@ -165,8 +166,8 @@ __global__ void __launch_bounds__(256) attn_fwd_f8_kernel(AttnF8Params p) {
       const int row = q >> 3, ch = q & 7;  // 8 bf16 -> 8 fp8 bytes: half of a 16-B fp8 chunk
       const u32x4 k = kv[it];
       uint2 w;
-      w.x = cvt4_e4m3(lo_bf(k[0]) * sk, hi_bf(k[0]) * sk, lo_bf(k[1]) * sk, hi_bf(k[1]) * sk);
-      w.y = cvt4_e4m3(lo_bf(k[2]) * sk, hi_bf(k[2]) * sk, lo_bf(k[3]) * sk, hi_bf(k[3]) * sk);
+      w.x = pdt_cvt4_e4m3_inrange(lo_bf(k[0]) * sk, hi_bf(k[0]) * sk, lo_bf(k[1]) * sk, hi_bf(k[1]) * sk);
+      w.y = pdt_cvt4_e4m3_inrange(lo_bf(k[2]) * sk, hi_bf(k[2]) * sk, lo_bf(k[3]) * sk, hi_bf(k[3]) * sk);
       *reinterpret_cast<uint2*>(Ks + k8_off(row, ch >> 1) + (ch & 1) * 8) = w;
     }
   }
@@ -204,9 +205,9 @@ __global__ void __launch_bounds__(256) attn_fwd_f8_kernel(AttnF8Params p) {
     i32x8 qf;
 #pragma unroll
     for (int c = 0; c < (F8 ? 4 : 0); ++c) {
-      qf[2 * c] = (int)cvt4_e4m3(lo_bf(qv[c][0]) * sq, hi_bf(qv[c][0]) * sq, lo_bf(qv[c][1]) * sq,
+      qf[2 * c] = (int)pdt_cvt4_e4m3_inrange(lo_bf(qv[c][0]) * sq, hi_bf(qv[c][0]) * sq, lo_bf(qv[c][1]) * sq,
                                  hi_bf(qv[c][1]) * sq);
-      qf[2 * c + 1] = (int)cvt4_e4m3(lo_bf(qv[c][2]) * sq, hi_bf(qv[c][2]) * sq, lo_bf(qv[c][3]) * sq,
+      qf[2 * c + 1] = (int)pdt_cvt4_e4m3_inrange(lo_bf(qv[c][2]) * sq, hi_bf(qv[c][2]) * sq, lo_bf(qv[c][3]) * sq,
                                      hi_bf(qv[c][3]) * sq);
     }
     // scores in the log2 domain: c * S = (c / (sk sq)) * S_fp8
@@ -262,7 +263,7 @@ __global__ void __launch_bounds__(256) attn_fwd_f8_kernel(AttnF8Params p) {
           }
 #pragma unroll
           for (int w = 0; w < 4; ++w)
-            pc[u][w] = cvt4_e4m3(s2[u][4 * w] * 256.f, s2[u][4 * w + 1] * 256.f, s2[u][4 * w + 2] * 256.f,
+            pc[u][w] = pdt_cvt4_e4m3_inrange(s2[u][4 * w] * 256.f, s2[u][4 * w + 1] * 256.f, s2[u][4 * w + 2] * 256.f,
                                  s2[u][4 * w + 3] * 256.f);
         }
         ls = xor32_reduce(ls, AddOp{});

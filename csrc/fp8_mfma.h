@@ -19,11 +19,16 @@ __device__ __forceinline__ int k8_off(int row, int chunk) { return row * 64 + ((
 // largest e with amax * 2^e <= 448 (0 for an all-zero block)
 __device__ __forceinline__ int pow2_exp(float amax) {
   if (!(amax > 0.f)) return 0;
-  const int e = (int)floorf(__log2f(448.f / amax));
-  return max(min(e, 100), -100);
+  int e = max(min((int)floorf(__log2f(448.f / amax)), 100), -100);
+  if (ldexpf(amax, e) > 448.f) --e;  // (the fast log2 may round up at an exact power of two)
+  return e;
 }
 
 __device__ __forceinline__ uint32_t e4m3x4(float a, float b, float c, float d) { return pdt_cvt4_f8<0>(a, b, c, d); }
+// in range by construction (pow2-scaled from the block's own |max|, or 256 P): no clamp
+__device__ __forceinline__ uint32_t e4m3x4_ir(float a, float b, float c, float d) {
+  return pdt_cvt4_e4m3_inrange(a, b, c, d);
+}
 
 // the 32-byte A / B fragment of a row image: row `row`, bytes 32 hh .. 32 hh + 31
 __device__ __forceinline__ i32x8 row_frag(const char* img, int row, int hh) {
