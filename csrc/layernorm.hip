@@ -120,18 +120,21 @@ __global__ void __launch_bounds__(64 * WPB) ln_bwd_kernel(const u16* __restrict_
                                                           const u16* __restrict__ addend,
                                                           uint8_t* __restrict__ q8 = nullptr,
                                                           const float* __restrict__ q8_meta = nullptr,
-                                                          float* __restrict__ q8_part = nullptr) {
+                                                          float* __restrict__ q8_part = nullptr,
+                                                          float* __restrict__ cpart = nullptr) {
+  // cpart (optional): per-block column sums of dx as stored (bf16) -> cpart[blockIdx.x][D]: the
+  // bias gradient of the layer whose output gradient dx is, formed where dx is written
   constexpr int D = 256 * CH;
   __shared__ float red[2][WPB][D];
   __shared__ float q8red[WPB];
   float q8max = 0.f;
   const float q8s = F8 ? q8_meta[0] : 0.f;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  float dg[CH][4], db[CH][4];
+  float dg[CH][4], db[CH][4], cs[CH][4];
 #pragma unroll
   for (int c = 0; c < CH; ++c)
 #pragma unroll
-    for (int e = 0; e < 4; ++e) dg[c][e] = db[c][e] = 0.f;
+    for (int e = 0; e < 4; ++e) dg[c][e] = db[c][e] = cs[c][e] = 0.f;
   const int r0 = blockIdx.x * rows_per_block;
   const int r1 = min(rows, r0 + rows_per_block);
   for (int row = r0 + w; row < r1; row += WPB) {
@@ -170,6 +173,10 @@ __global__ void __launch_bounds__(64 * WPB) ln_bwd_kernel(const u16* __restrict_
         for (int e = 0; e < 4; ++e) o[e] += ad[c][e];
       }
       st4(dx + (long)row * D + (c * 64 + lane) * 4, o);
+      if (cpart != nullptr) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) cs[c][e] += bf2f(f2bf(o[e]));
+      }
       if (F8) {
         float r[4];
 #pragma unroll
@@ -203,6 +210,20 @@ __global__ void __launch_bounds__(64 * WPB) ln_bwd_kernel(const u16* __restrict_
     }
     part[(long)blockIdx.x * D + col] = a;
     part[(long)(gridDim.x + blockIdx.x) * D + col] = bsum;
+  }
+  if (cpart != nullptr) {
+    __syncthreads();  // red[0] is read above
+#pragma unroll
+    for (int c = 0; c < CH; ++c)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) red[0][w][(c * 64 + lane) * 4 + e] = cs[c][e];
+    __syncthreads();
+    for (int col = threadIdx.x; col < D; col += 64 * WPB) {
+      float a = 0.f;
+#pragma unroll
+      for (int k = 0; k < WPB; ++k) a += red[0][k][col];
+      cpart[(long)blockIdx.x * D + col] = a;
+    }
   }
   if (F8 && threadIdx.x == 0) {  // q8red was written before the barrier above
     float m = q8red[0];
@@ -423,6 +444,43 @@ PDT_API int pdt_ln_bwd_f8(const void* dy, const void* x, const float* g, const f
   if (e) return e;
   hipLaunchKernelGGL(colsum_f32_kernel, dim3((D + 63) / 64), dim3(64 * CS_RG), 0, st, part, dg, db, blocks, D,
                      accumulate);
+  return pdt_fp8_meta_roll_partial(q8_meta, q8_part, blocks, 1, q8_dq, st);
+}
+
+PDT_API int pdt_wgrad_reduce_rows(const float* rows, float* out, int nrows, int n, float scale, int accumulate,
+                                  hipStream_t stream);
+
+// pdt_ln_bwd_f8 + the column sums of dx (bf16 as stored) into bias_out [D] (= or += with
+// bias_acc): the bias gradient of the fp8 layer that produced the LayerNorm's input, so its
+// weight-gradient kernel does not re-read dx for it. cpart: pdt_ln_bwd_blocks(rows) * D floats.
+PDT_API int pdt_ln_bwd_f8_db(const void* dy, const void* x, const float* g, const float* mean, const float* rstd,
+                             void* dx, float* dg, float* db, float* part, int rows, int D, int accumulate,
+                             const void* addend, void* q8, float* q8_meta, float* q8_part, float* q8_dq,
+                             float* cpart, float* bias_out, int bias_acc, hipStream_t st) {
+  if (!cpart || !bias_out) return -1;
+  const int blocks = pdt_ln_bwd_blocks(rows);
+  const int rpb = ln_rows_per_block(rows);
+  dim3 grid(blocks), blk(64 * WPB);
+  const u16 *DY = (const u16*)dy, *X = (const u16*)x;
+  u16* DX = (u16*)dx;
+  const u16* AD = (const u16*)addend;
+  uint8_t* Q = (uint8_t*)q8;
+#define LB8(CH_) hipLaunchKernelGGL((ln_bwd_kernel<CH_, true>), grid, blk, 0, st, DY, X, g, mean, rstd, DX, part, rows, \
+                                    rpb, AD, Q, (const float*)q8_meta, q8_part, cpart)
+  switch (D) {
+    case 256: LB8(1); break;
+    case 512: LB8(2); break;
+    case 768: LB8(3); break;
+    case 1024: LB8(4); break;
+    default: return -1;
+  }
+#undef LB8
+  int e = (int)hipGetLastError();
+  if (e) return e;
+  hipLaunchKernelGGL(colsum_f32_kernel, dim3((D + 63) / 64), dim3(64 * CS_RG), 0, st, part, dg, db, blocks, D,
+                     accumulate);
+  e = pdt_wgrad_reduce_rows(cpart, bias_out, blocks, D, 1.f, bias_acc, st);
+  if (e) return e;
   return pdt_fp8_meta_roll_partial(q8_meta, q8_part, blocks, 1, q8_dq, st);
 }
 

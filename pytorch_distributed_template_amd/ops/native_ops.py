@@ -51,6 +51,7 @@ _SIGS = {
     "pdt_gemm_f8_q8": (c_int, [P] * 6 + [c_int] * 8 + [P, P, c_int, P, P, P, c_int, c_int, P, P]),
     "pdt_gemm_f8_q8_part": (c_long, [c_int, c_int]),
     "pdt_ln_bwd_f8": (c_int, [P] * 9 + [c_int, c_int, c_int] + [P] * 6),
+    "pdt_ln_bwd_f8_db": (c_int, [P] * 9 + [c_int, c_int, c_int] + [P] * 7 + [c_int, P]),
     "pdt_wgrad_f8_num_variants": (c_int, []),
     "pdt_wgrad_f8_plan": (c_int, [c_int, c_int, c_int, c_int, ctypes.POINTER(c_int)]),
     "pdt_wgrad_f8_workspace": (c_long, [c_int, c_int, c_int]),
@@ -2530,6 +2531,13 @@ def linear_wgrad_f8(dyq, xq, dq_dy, dq_x, dy16=None, with_bias=False, variant=No
     return dw, db
 
 
+def _pre_bias_grad(g, owner):
+    """The bias gradient of ``owner`` if the producer of its output gradient ``g`` (a LayerNorm
+    backward, :func:`_ln_fork_backward`) already formed it, else None."""
+    pre = getattr(g, "_pdt_db", None) if g is not None else None
+    return pre[0] if pre is not None and pre[1] is owner else None
+
+
 def _fp8_wgrad_on() -> bool:
     return fp8_settings()["wgrad"]
 
@@ -2618,8 +2626,12 @@ class _LinearF8(torch.autograd.Function):
                 dx = _linear_dgrad(dy2, w)
             dx = dx.reshape(*shp[:-1], K)
         want_db = has_b and need[2]
+        pre_db = _pre_bias_grad(dy, ctx.fc) if act is None and want_db else None
         if ctx.f8w and need[1]:
-            dw, db = linear_wgrad_f8(dyq, ctx.xq, dqdy, ctx.dqx, dy16=dy2, with_bias=want_db, w=w, b=ctx.bref)
+            dw, db = linear_wgrad_f8(dyq, ctx.xq, dqdy, ctx.dqx, dy16=dy2, with_bias=want_db and pre_db is None, w=w,
+                                     b=ctx.bref)
+            if pre_db is not None:
+                db = pre_db
         elif ctx.f8w:
             dw, db = None, (colsum(dy2, Mrows, Nout) if want_db else None)
         else:
@@ -2723,10 +2735,13 @@ class _Mlp(torch.autograd.Function):
                 gemm_f8(gq, w2qt, dz, dqg, dqw2, fmt_a=E5M2, act=ctx.act2, addend=z)
         else:
             _gemm_bf16(g2, bf16_weight_t(w2), dz, act=ctx.act2, addend=z)  # dz = (g W2) * gelu'(z)
+        pre_db2 = _pre_bias_grad(g, ctx.mlp.fc2) if need[4] else None
         if f8 is not None:
-            dw2, db2 = linear_wgrad_f8(gq, f8[2], dqg, f8[3], dy16=g2, with_bias=need[4], w=w2,
+            dw2, db2 = linear_wgrad_f8(gq, f8[2], dqg, f8[3], dy16=g2, with_bias=need[4] and pre_db2 is None, w=w2,
                                        b=ctx.brefs[1]) if need[3] \
-                else (None, colsum(g2, Mrows, Nout) if need[4] else None)
+                else (None, colsum(g2, Mrows, Nout) if need[4] and pre_db2 is None else None)
+            if pre_db2 is not None:
+                db2 = pre_db2
         else:
             dw2, db2 = _linear_grads(g2, a, w2, need[4], need[3], bias=ctx.brefs[1])
         dx = None
@@ -2871,11 +2886,24 @@ def _ln_fork_backward(ctx, g_res, dy):
         codes = torch.empty((rows, D), dtype=torch.uint8, device=dev)
         qpart = torch.empty(blocks + 1, dtype=torch.float32, device=dev)
         dq = qpart[-1:]
-        _chk(lib.pdt_ln_bwd_f8(_p(dy2), _p(x2), _p(gf), _p(stats[0]), _p(stats[1]), _p(dx), _p(dg), _p(db),
-                               _p(part), rows, D, 0, _p(add), _p(codes), _p(gmeta), _p(qpart), _p(dq), _s()),
-             "ln_bwd_f8")
+        bias = getattr(owner, "bias", None)
+        if bias is not None and bias.requires_grad and os.environ.get("PDT_LN_DB", "1") == "1":
+            # the producer's bias gradient = column sums of dx, formed here (the weight-gradient
+            # kernel of that layer would re-read dx for them); picked up through ``_pdt_db``
+            pdb = _grad_buf(bias, (D,))
+            cpart = torch.empty(blocks * D, dtype=torch.float32, device=dev)
+            _chk(lib.pdt_ln_bwd_f8_db(_p(dy2), _p(x2), _p(gf), _p(stats[0]), _p(stats[1]), _p(dx), _p(dg), _p(db),
+                                      _p(part), rows, D, 0, _p(add), _p(codes), _p(gmeta), _p(qpart), _p(dq),
+                                      _p(cpart), _p(pdb), 0, _s()), "ln_bwd_f8_db")
+        else:
+            pdb = None
+            _chk(lib.pdt_ln_bwd_f8(_p(dy2), _p(x2), _p(gf), _p(stats[0]), _p(stats[1]), _p(dx), _p(dg), _p(db),
+                                   _p(part), rows, D, 0, _p(add), _p(codes), _p(gmeta), _p(qpart), _p(dq), _s()),
+                 "ln_bwd_f8")
         out = dx.reshape(ctx.shp)
         out._pdt_f8g = (codes, dq, owner)
+        if pdb is not None:
+            out._pdt_db = (pdb, owner)
         return out, dg, db
     _chk(lib.pdt_ln_bwd(_p(dy2), _p(x2), _p(gf), _p(stats[0]), _p(stats[1]), _p(dx), _p(dg), _p(db), _p(part),
                         rows, D, 0, _p(add), _s()), "ln_bwd")

@@ -41,6 +41,7 @@ def main():
     ap.add_argument("--iters", type=int, default=10)
     ap.add_argument("--fwd", default="8,9,10,11")
     ap.add_argument("--wgrad", default="10,12,19,20,21,22,23,24")
+    ap.add_argument("--bias", action="store_true", help="weight gradients with the bias gradient (bf16 dY column sums)")
     a = ap.parse_args()
     torch.manual_seed(0)
     fv = [int(v) for v in a.fwd.split(",") if v]
@@ -67,6 +68,7 @@ def main():
         fl = 2.0 * M * Nout * K
         dyq, dqd = no.quantize_fp8(torch.randn(M, Nout, device="cuda").to(torch.bfloat16), no.E5M2)
         xq, dqx = no.quantize_fp8(torch.randn(M, K, device="cuda").to(torch.bfloat16))
+        dy16 = torch.randn(M, Nout, device="cuda").to(torch.bfloat16) if a.bias else None
         ref, _ = no.linear_wgrad_f8(dyq, xq, dqd, dqx, variant=10)
         ref = ref.clone()
         parts = []
@@ -74,7 +76,7 @@ def main():
             out = {}
 
             def run():
-                out["dw"], _ = no.linear_wgrad_f8(dyq, xq, dqd, dqx, variant=v)
+                out["dw"], _ = no.linear_wgrad_f8(dyq, xq, dqd, dqx, dy16=dy16, with_bias=a.bias, variant=v)
 
             t = timeit(run, a.iters)
             parts.append(f"v{v} {t * 1e3:6.1f} us {fl / t / 1e9:5.0f} TF err {nrmerr(out['dw'], ref):.1e}")
