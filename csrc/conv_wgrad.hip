@@ -567,10 +567,12 @@ PDT_API int pdt_wgrad_plan(int M, int Mo, int No, int variant, int* ktiles_per_s
     legacy = (e && e[0] == '1') ? 0 : 1;
   }
   int splits = smax;
-  if (legacy) {
+  // the wave model fits one-workgroup-per-CU tiles (every resident workgroup runs at the same
+  // rate): those always take it; multi-workgroup tiles only with PDT_WG_PLAN=1
+  const long slots = wg_slots(variant, w);
+  if (legacy && slots > pdt_num_cus()) {
     while (splits > 1 && (nk + splits - 1) / splits < 8) --splits;
   } else {
-    const long slots = wg_slots(variant, w);
     long best_cost = -1;
     for (int s = 1; s <= smax; ++s) {
       const int kps = (nk + s - 1) / s;

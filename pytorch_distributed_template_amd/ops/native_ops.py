@@ -726,6 +726,13 @@ def conv_wgrad(dy, x, out, *, scale=1.0, accumulate=False, variant=None, bias_ou
                 key += f",p{a['pix']}"
             _WG_KEYS[gt] = key
         table = _tuned()
+        spec = os.environ.get("PDT_RETUNE_WG")  # targeted re-tune of shipped keys against these ids
+        if key in table and spec and key not in _RETUNED and _tune_allowed():
+            _RETUNED.add(key)
+            allowed = _id_set(spec) | {int(table[key])}
+            table[key] = _time_variants(lib.pdt_wgrad_num_variants(),
+                                        lambda v: _wgrad_launch(lib, dy, x, out, v, scale, False, a), allowed)
+            _save_tuned()
         if key in table:
             variant = int(table[key])
         elif not _tune_allowed():
