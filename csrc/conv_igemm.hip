@@ -574,7 +574,7 @@ PDT_API int pdt_gemm_f8_num_variants() { return NVAR_F8; }
 static int gemm_f8_impl(const void* a, const void* b, void* out, const float* bias, const float* dq_a,
                         const float* dq_b, int M, int N, int K, int lda, int ldb, int ldo, int fmt_a, int act,
                         void* aux, const void* addend, int variant, void* q8, float* q8_meta, float* q8_part,
-                        int q8_fmt, int q8_only, float* q8_dq, hipStream_t stream) {
+                        int q8_fmt, int q8_only, float* q8_dq, hipStream_t stream, float* colsum = nullptr) {
   if (K % 128 != 0 || lda % 16 != 0 || ldb % 16 != 0 || N % 8 != 0 || ldo % 8 != 0) return -1;
   if (lda != K) return -2;  // rows of A are dense (the gather's source row stride is Cs)
   NTParams p;
@@ -614,7 +614,8 @@ static int gemm_f8_impl(const void* a, const void* b, void* out, const float* bi
   p.q8_part = q8_part;
   p.q8_fmt = q8_fmt;
   p.q8_only = q8_only;
-  if (q8 != nullptr && v == 7) return -5;  // the direct-store epilogue has no fp8 output (NOT_APPLICABLE)
+  if ((q8 != nullptr || colsum != nullptr) && v == 7) return -5;  // the direct-store epilogue has neither
+  p.colsum = colsum;
   const int rc = fmt_a == 1 ? launch_f8<2>(v, p, stream) : launch_f8<1>(v, p, stream);
   if (rc || q8 == nullptr) return rc;
   const int nblk = ((M + VAR_F8_BM[v] - 1) / VAR_F8_BM[v]) * ((N + VAR_F8_BN[v] - 1) / VAR_F8_BN[v]);
@@ -627,6 +628,9 @@ PDT_API int pdt_gemm_f8(const void* a, const void* b, void* out, const float* bi
   return gemm_f8_impl(a, b, out, bias, dq_a, dq_b, M, N, K, lda, ldb, ldo, fmt_a, act, aux, addend, variant, nullptr,
                       nullptr, nullptr, 0, 0, nullptr, stream);
 }
+
+// M-tile rows of variant v (the colsum partial rows of pdt_gemm_f8_q8_cs)
+PDT_API int pdt_gemm_f8_bm(int variant) { return VAR_F8_BM[(variant >= 0 && variant < NVAR_F8) ? variant : 1]; }
 
 // floats of amax workspace pdt_gemm_f8_q8 needs (any variant)
 PDT_API long pdt_gemm_f8_q8_part(int M, int N) { return (long)((M + 63) / 64) * ((N + 63) / 64); }
@@ -641,4 +645,16 @@ PDT_API int pdt_gemm_f8_q8(const void* a, const void* b, void* out, const float*
   if (!q8 || !q8_meta || !q8_part || ldo != N) return -1;
   return gemm_f8_impl(a, b, out, bias, dq_a, dq_b, M, N, K, lda, ldb, ldo, fmt_a, act, aux, addend, variant, q8,
                       q8_meta, q8_part, q8_fmt, q8_only, q8_dq, stream);
+}
+
+// pdt_gemm_f8_q8 that also writes the column sums of the final bf16 output (whether or not
+// q8_only skips storing it) per M-tile: colsum[ceil(M / pdt_gemm_f8_bm(v))][N] -- the bias
+// gradient of the layer whose output gradient this is, with no pass over that gradient
+PDT_API int pdt_gemm_f8_q8_cs(const void* a, const void* b, void* out, const float* bias, const float* dq_a,
+                              const float* dq_b, int M, int N, int K, int lda, int ldb, int ldo, int fmt_a, int act,
+                              void* aux, const void* addend, int variant, void* q8, float* q8_meta, float* q8_part,
+                              int q8_fmt, int q8_only, float* q8_dq, float* colsum, hipStream_t stream) {
+  if (!q8 || !q8_meta || !q8_part || ldo != N || !colsum) return -1;
+  return gemm_f8_impl(a, b, out, bias, dq_a, dq_b, M, N, K, lda, ldb, ldo, fmt_a, act, aux, addend, variant, q8,
+                      q8_meta, q8_part, q8_fmt, q8_only, q8_dq, stream, colsum);
 }

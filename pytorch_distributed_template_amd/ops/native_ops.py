@@ -49,6 +49,9 @@ _SIGS = {
     "pdt_conv_nt_bnb2": (c_int, [P] * 5 + [c_int] * 25 + [P] * 6 + [c_int] * 3 + [P] * 3 + [P]),
     "pdt_ln_fwd": (c_int, [P, P, P, P, P, P, c_int, c_int, c_float, P]),
     "pdt_gemm_f8_q8": (c_int, [P] * 6 + [c_int] * 8 + [P, P, c_int, P, P, P, c_int, c_int, P, P]),
+    "pdt_gemm_f8_q8_cs": (c_int, [P] * 6 + [c_int] * 8 + [P, P, c_int, P, P, P, c_int, c_int, P, P, P]),
+    "pdt_gemm_f8_bm": (c_int, [c_int]),
+    "pdt_wgrad_reduce_rows": (c_int, [P, P, c_int, c_int, c_float, c_int, P]),
     "pdt_gemm_f8_q8_part": (c_long, [c_int, c_int]),
     "pdt_ln_bwd_f8": (c_int, [P] * 9 + [c_int, c_int, c_int] + [P] * 6),
     "pdt_ln_bwd_f8_db": (c_int, [P] * 9 + [c_int, c_int, c_int] + [P] * 7 + [c_int, P]),
@@ -2442,14 +2445,16 @@ def _fc1_lib_forward(xq, w1q, a, z, aq, dqx, dqw1, bias1, meta, keep_a):
 
 
 def gemm_f8(a, b, out, dq_a, dq_b, *, fmt_a=E4M3, bias=None, act=0, aux=None, addend=None, variant=None,
-            q8=None):
+            q8=None, colsum_out=None):
     """out[M, N] (bf16) = dq_a*dq_b * a[M, K] @ b[N, K]^T (+bias, act) (+ addend); a, b uint8 fp8
     codes. ``act=3``: GELU backward, out = (a @ b^T) * gelu'(addend).
 
     ``q8 = (codes, meta, fmt, only)``: the epilogue also writes the fp8 codes (format fmt) of
     the output for the NEXT fp8 GEMM with that GEMM's delayed scale ``meta`` and rolls its
     amax history (no separate quantisation pass); ``only`` skips the bf16 output. Returns
-    the codes' dequant factor (device [1]) in that case, else ``out``."""
+    the codes' dequant factor (device [1]) in that case, else ``out``. ``colsum_out`` (with q8,
+    fp32 [N]): also the column sums of the final bf16 output (written or not), formed in the
+    epilogue -- the bias gradient of the layer whose output gradient this GEMM produces."""
     M, K = a.shape
     N = b.shape[0]
     assert a.dtype == torch.uint8 and b.dtype == torch.uint8 and b.shape[1] == K and K % 128 == 0
@@ -2487,11 +2492,21 @@ def gemm_f8(a, b, out, dq_a, dq_b, *, fmt_a=E4M3, bias=None, act=0, aux=None, ad
     args = lambda v: (_p(a), _p(b), _p(out), _p(bias), _p(dq_a), _p(dq_b), M, N, K, K, K, N, fmt_a, act,  # noqa
                       _p(aux), _p(addend), v, _p(codes), _p(meta), _p(part), int(qfmt), int(only), _p(dq), _s())
     if variant is None:
-        key = f"f8b:{M},{N},{K},{fmt_a},{act},{int(bias is not None)},q{qfmt}{int(only)}"
+        key = f"f8b:{M},{N},{K},{fmt_a},{act},{int(bias is not None)},q{qfmt}{int(only)}" + \
+            (",cs" if colsum_out is not None else "")
         # (tuning launches roll the history too: tune on a scratch copy of the state)
         scratch = meta.clone()
         targs = lambda v: args(v)[:17] + (_p(codes), _p(scratch)) + args(v)[19:]  # noqa: E731
         variant = _autotune(key, lib.pdt_gemm_f8_num_variants(), lambda v: lib.pdt_gemm_f8_q8(*targs(v)))
+    if colsum_out is not None:
+        assert colsum_out.dtype == torch.float32 and colsum_out.numel() == N and colsum_out.is_contiguous()
+        if variant == 7 or variant < 0:  # the direct-store tile has no staged epilogue
+            variant = 10
+        ntm = -(-M // lib.pdt_gemm_f8_bm(variant))
+        cpart = torch.empty(ntm * N, dtype=torch.float32, device=a.device)
+        _chk(lib.pdt_gemm_f8_q8_cs(*args(variant)[:-1], _p(cpart), _s()), "gemm_f8_q8_cs")
+        _chk(lib.pdt_wgrad_reduce_rows(_p(cpart), _p(colsum_out), ntm, N, 1.0, 0, _s()), "colsum rows")
+        return dq
     _chk(lib.pdt_gemm_f8_q8(*args(variant)), "gemm_f8_q8")
     return dq
 
@@ -2728,7 +2743,7 @@ class _Mlp(torch.autograd.Function):
         g2 = g.reshape(Mrows, Nout).to(torch.bfloat16).contiguous()
         dz = torch.empty((Mrows, Hd), dtype=torch.bfloat16, device=g.device)
         f8 = ctx.f8
-        dzq = dqdz = None
+        dzq = dqdz = pre_db1 = None
         if ctx.fp8_dgrad:
             gq, dqg = _quant_grad(g2, ctx.mlp.fc2, "_pdt_fp8_gmeta", src=g)
             _, w2qt, dqw2 = fp8_weight(w2)
@@ -2736,8 +2751,15 @@ class _Mlp(torch.autograd.Function):
                 else None
             if gmeta1 is not None:  # the epilogue also writes fc1's e5m2 output gradient (bf16 dz: bias grad)
                 dzq = torch.empty((Mrows, Hd), dtype=torch.uint8, device=g.device)
-                dqdz = gemm_f8(gq, w2qt, dz, dqg, dqw2, fmt_a=E5M2, act=ctx.act2, addend=z,
-                               q8=(dzq, gmeta1, E5M2, False))
+                if f8 is not None and need[1] and need[2] and os.environ.get("PDT_F8_DB_EPI", "1") == "1":
+                    # fc1's bias gradient = column sums of dz formed in this epilogue: the bf16 dz
+                    # (only ever read for it) is not written at all
+                    pre_db1 = _grad_buf(ctx.brefs[0], (Hd,))
+                    dqdz = gemm_f8(gq, w2qt, dz, dqg, dqw2, fmt_a=E5M2, act=ctx.act2, addend=z,
+                                   q8=(dzq, gmeta1, E5M2, True), colsum_out=pre_db1)
+                else:
+                    dqdz = gemm_f8(gq, w2qt, dz, dqg, dqw2, fmt_a=E5M2, act=ctx.act2, addend=z,
+                                   q8=(dzq, gmeta1, E5M2, False))
             else:
                 gemm_f8(gq, w2qt, dz, dqg, dqw2, fmt_a=E5M2, act=ctx.act2, addend=z)
         else:
@@ -2763,9 +2785,11 @@ class _Mlp(torch.autograd.Function):
                 _gemm_bf16(dz, bf16_weight_t(w1), dx)
             dx = dx.reshape(ctx.shp)
         if f8 is not None:
-            dw1, db1 = linear_wgrad_f8(dzq, f8[0], dqdz, f8[1], dy16=dz, with_bias=need[2], w=w1,
-                                       b=ctx.brefs[0]) if need[1] \
+            dw1, db1 = linear_wgrad_f8(dzq, f8[0], dqdz, f8[1], dy16=dz, with_bias=need[2] and pre_db1 is None,
+                                       w=w1, b=ctx.brefs[0]) if need[1] \
                 else (None, colsum(dz, Mrows, Hd) if need[2] else None)
+            if pre_db1 is not None:
+                db1 = pre_db1
         else:
             dw1, db1 = _linear_grads(dz, x2, w1, need[2], need[1], bias=ctx.brefs[0])
         ctx.f8 = None

@@ -548,3 +548,34 @@ def test_ln_backward_bias_grads_match_wgrad_bias(monkeypatch):
     assert grads["1"].keys() == grads["0"].keys() and len(grads["1"]) == 4
     for n in grads["1"]:
         assert nrmerr(grads["1"][n], grads["0"][n]) < 1e-3, n
+
+
+@pytest.mark.parametrize("variant", [8, 9, 10])
+def test_gemm_f8_epilogue_column_sums(variant):
+    """gemm_f8(..., q8=(codes, meta, fmt, only=True), colsum_out=...): the column sums of the
+    final bf16 output (act 5: out * addend) formed in the epilogue equal the sums of the output
+    a plain call writes, and the codes / dequant factor are the same."""
+    torch.manual_seed(61)
+    M, N, K = 1000, 768, 256
+    a = torch.randn(M, K, device="cuda").to(torch.bfloat16)
+    b = torch.randn(N, K, device="cuda")
+    qa, dqa = no.quantize_fp8(a, no.E5M2)
+    qb, dqb = no.quantize_fp8(b, no.E4M3)
+    add = torch.rand(M, N, device="cuda").to(torch.bfloat16)
+    meta = no.quantize_fp8_delayed(torch.randn(M, N, device="cuda").to(torch.bfloat16), None, no.E5M2)[2]
+    out = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
+    codes = torch.empty(M, N, device="cuda", dtype=torch.uint8)
+    m0 = meta.clone()
+    dq0 = no.gemm_f8(qa, qb, out, dqa, dqb, fmt_a=no.E5M2, act=no.ACT_MUL, addend=add, variant=variant,
+                     q8=(codes, m0, no.E5M2, False))
+    cs = torch.full((N,), float("nan"), device="cuda")
+    codes1 = torch.empty_like(codes)
+    m1 = meta.clone()
+    out1 = torch.full_like(out, float("nan"))
+    dq1 = no.gemm_f8(qa, qb, out1, dqa, dqb, fmt_a=no.E5M2, act=no.ACT_MUL, addend=add, variant=variant,
+                     q8=(codes1, m1, no.E5M2, True), colsum_out=cs)
+    torch.cuda.synchronize()
+    assert torch.isnan(out1.float()).all()  # q8 only: the bf16 output is not written
+    assert torch.equal(codes1, codes) and torch.equal(dq1, dq0) and torch.equal(m1, m0)
+    ref = out.float().sum(0)
+    assert nrmerr(cs, ref) < 1e-5, nrmerr(cs, ref)
