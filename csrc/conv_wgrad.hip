@@ -694,12 +694,35 @@ PDT_API int pdt_conv_wgrad2(const void* dy, const void* x, float* slab, float* o
 
 // Deterministic reduction of the split-K slabs [splits][Mo][No] (+ the optional bias slab
 // [splits][Mo]) into out (= or += scale * sum); shared by the bf16 and fp8 weight gradients.
-// out[n] (= or +=) scale * sum of nrows rows of [nrows][n] (n % 4 == 0): the bias-gradient partial rows
+// row groups of the two-stage reduce of nrows partial rows (0: one stage)
+static int reduce_rows_groups(int nrows) {
+  if (nrows <= 32) return 0;
+  int G = 1;
+  while (G * G < nrows) ++G;
+  return G > 64 ? 64 : G;
+}
+
+// floats of workspace pdt_wgrad_reduce_rows needs for nrows partial rows of n columns
+PDT_API long pdt_reduce_rows_work(int nrows, int n) { return (long)reduce_rows_groups(nrows) * n; }
+
+// out[n] (= or +=) scale * sum of nrows rows of [nrows][n] (n % 4 == 0): partial rows of a
+// column sum (bias gradients). Many rows (an epilogue's per-tile rows, a LayerNorm backward's
+// per-block rows) are summed in two stages through `work` (pdt_reduce_rows_work floats):
+// the single-stage pass has only n / 1024 workgroups, each walking every row.
 PDT_API int pdt_wgrad_reduce_rows(const float* rows, float* out, int nrows, int n, float scale, int accumulate,
-                                  hipStream_t stream) {
+                                  float* work, hipStream_t stream) {
   if (n % 4 != 0 || nrows < 1) return -1;
-  hipLaunchKernelGGL(wgrad_reduce1_kernel, dim3((n / 4 + 255) / 256, 1), dim3(256), 0, stream, rows, out,
-                     (long)(n / 4), nrows, 1, scale, accumulate, 1);
+  const long n4 = n / 4;
+  const int xb = (int)((n4 + 255) / 256);
+  const int G = reduce_rows_groups(nrows);
+  if (G > 1 && work != nullptr) {
+    hipLaunchKernelGGL(wgrad_reduce1_kernel, dim3(xb, G), dim3(256), 0, stream, rows, work, n4, nrows, G, 1.f, 0, 0);
+    hipLaunchKernelGGL(wgrad_reduce1_kernel, dim3(xb, 1), dim3(256), 0, stream, work, out, n4, G, 1, scale,
+                       accumulate, 1);
+  } else {
+    hipLaunchKernelGGL(wgrad_reduce1_kernel, dim3(xb, 1), dim3(256), 0, stream, rows, out, n4, nrows, 1, scale,
+                       accumulate, 1);
+  }
   PDT_RETURN_LAUNCH();
 }
 

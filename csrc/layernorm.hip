@@ -448,11 +448,13 @@ PDT_API int pdt_ln_bwd_f8(const void* dy, const void* x, const float* g, const f
 }
 
 PDT_API int pdt_wgrad_reduce_rows(const float* rows, float* out, int nrows, int n, float scale, int accumulate,
-                                  hipStream_t stream);
+                                  float* work, hipStream_t stream);
+PDT_API long pdt_reduce_rows_work(int nrows, int n);
 
 // pdt_ln_bwd_f8 + the column sums of dx (bf16 as stored) into bias_out [D] (= or += with
 // bias_acc): the bias gradient of the fp8 layer that produced the LayerNorm's input, so its
-// weight-gradient kernel does not re-read dx for it. cpart: pdt_ln_bwd_blocks(rows) * D floats.
+// weight-gradient kernel does not re-read dx for it. cpart: pdt_ln_bwd_blocks(rows) * D floats
+// + pdt_reduce_rows_work(pdt_ln_bwd_blocks(rows), D) behind them (the reduce's workspace).
 PDT_API int pdt_ln_bwd_f8_db(const void* dy, const void* x, const float* g, const float* mean, const float* rstd,
                              void* dx, float* dg, float* db, float* part, int rows, int D, int accumulate,
                              const void* addend, void* q8, float* q8_meta, float* q8_part, float* q8_dq,
@@ -479,7 +481,7 @@ PDT_API int pdt_ln_bwd_f8_db(const void* dy, const void* x, const float* g, cons
   if (e) return e;
   hipLaunchKernelGGL(colsum_f32_kernel, dim3((D + 63) / 64), dim3(64 * CS_RG), 0, st, part, dg, db, blocks, D,
                      accumulate);
-  e = pdt_wgrad_reduce_rows(cpart, bias_out, blocks, D, 1.f, bias_acc, st);
+  e = pdt_wgrad_reduce_rows(cpart, bias_out, blocks, D, 1.f, bias_acc, cpart + (long)blocks * D, st);
   if (e) return e;
   return pdt_fp8_meta_roll_partial(q8_meta, q8_part, blocks, 1, q8_dq, st);
 }

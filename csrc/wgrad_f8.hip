@@ -25,7 +25,7 @@
 PDT_API int pdt_wgrad_reduce(float* slab, float* out, const float* bslab, float* bias_out, int splits, int Mo, int No,
                              float scale, int accumulate, hipStream_t stream);
 PDT_API int pdt_wgrad_reduce_rows(const float* rows, float* out, int nrows, int n, float scale, int accumulate,
-                                  hipStream_t stream);
+                                  float* work, hipStream_t stream);
 
 namespace {
 
@@ -524,7 +524,7 @@ PDT_API int pdt_linear_wgrad_f8(const void* dy8, const void* x8, const float* dq
   if (e) return e;
   if (bias_out) {
     const int rc = pdt_wgrad_reduce_rows(p.bslab, bias_out, splits * ((No + w.BN - 1) / w.BN), Mo, 1.f, accumulate,
-                                         stream);
+                                         nullptr, stream);
     if (rc) return rc;
   }
   return pdt_wgrad_reduce(slab, out, nullptr, nullptr, splits, Mo, No, 1.f, accumulate, stream);

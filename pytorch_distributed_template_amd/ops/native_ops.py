@@ -51,7 +51,8 @@ _SIGS = {
     "pdt_gemm_f8_q8": (c_int, [P] * 6 + [c_int] * 8 + [P, P, c_int, P, P, P, c_int, c_int, P, P]),
     "pdt_gemm_f8_q8_cs": (c_int, [P] * 6 + [c_int] * 8 + [P, P, c_int, P, P, P, c_int, c_int, P, P, P]),
     "pdt_gemm_f8_bm": (c_int, [c_int]),
-    "pdt_wgrad_reduce_rows": (c_int, [P, P, c_int, c_int, c_float, c_int, P]),
+    "pdt_wgrad_reduce_rows": (c_int, [P, P, c_int, c_int, c_float, c_int, P, P]),
+    "pdt_reduce_rows_work": (c_long, [c_int, c_int]),
     "pdt_gemm_f8_q8_part": (c_long, [c_int, c_int]),
     "pdt_ln_bwd_f8": (c_int, [P] * 9 + [c_int, c_int, c_int] + [P] * 6),
     "pdt_ln_bwd_f8_db": (c_int, [P] * 9 + [c_int, c_int, c_int] + [P] * 7 + [c_int, P]),
@@ -2503,9 +2504,10 @@ def gemm_f8(a, b, out, dq_a, dq_b, *, fmt_a=E4M3, bias=None, act=0, aux=None, ad
         if variant == 7 or variant < 0:  # the direct-store tile has no staged epilogue
             variant = 10
         ntm = -(-M // lib.pdt_gemm_f8_bm(variant))
-        cpart = torch.empty(ntm * N, dtype=torch.float32, device=a.device)
+        cpart = torch.empty(ntm * N + lib.pdt_reduce_rows_work(ntm, N), dtype=torch.float32, device=a.device)
         _chk(lib.pdt_gemm_f8_q8_cs(*args(variant)[:-1], _p(cpart), _s()), "gemm_f8_q8_cs")
-        _chk(lib.pdt_wgrad_reduce_rows(_p(cpart), _p(colsum_out), ntm, N, 1.0, 0, _s()), "colsum rows")
+        _chk(lib.pdt_wgrad_reduce_rows(_p(cpart), _p(colsum_out), ntm, N, 1.0, 0, _p(cpart[ntm * N:]), _s()),
+             "colsum rows")
         return dq
     _chk(lib.pdt_gemm_f8_q8(*args(variant)), "gemm_f8_q8")
     return dq
@@ -2922,7 +2924,7 @@ def _ln_fork_backward(ctx, g_res, dy):
             # the producer's bias gradient = column sums of dx, formed here (the weight-gradient
             # kernel of that layer would re-read dx for them); picked up through ``_pdt_db``
             pdb = _grad_buf(bias, (D,))
-            cpart = torch.empty(blocks * D, dtype=torch.float32, device=dev)
+            cpart = torch.empty(blocks * D + lib.pdt_reduce_rows_work(blocks, D), dtype=torch.float32, device=dev)
             _chk(lib.pdt_ln_bwd_f8_db(_p(dy2), _p(x2), _p(gf), _p(stats[0]), _p(stats[1]), _p(dx), _p(dg), _p(db),
                                       _p(part), rows, D, 0, _p(add), _p(codes), _p(gmeta), _p(qpart), _p(dq),
                                       _p(cpart), _p(pdb), 0, _s()), "ln_bwd_f8_db")
