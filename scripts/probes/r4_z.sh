@@ -2,7 +2,7 @@
 # Round 4: fc1's bias gradient from the fc2 data-gradient epilogue's column sums (the bf16 dz is
 # no longer written) -- tests, ViT A/B.
 source "$(dirname "$0")/../gpurun_lib.sh"
-T=r4zz
+T=r4z3
 run ${T}_tests.txt 400 python -u -m pytest tests/test_vit_fusion_gpu.py tests/test_kernels_gpu.py -k "vit or mlp or fp8 or f8 or gelu" -x -v --timeout 120 --timeout-method thread || exit $?
 grep -q " passed" gpurun_out/${T}_tests.txt && ! grep -q "failed" gpurun_out/${T}_tests.txt || { echo "tests failed"; exit 1; }
 for i in 1 2; do
