@@ -247,6 +247,62 @@ __global__ void __launch_bounds__(256) gelu_dual_cast_kernel(const u16* __restri
   }
 }
 
+// cast_fp8_delayed_kernel of a bf16 [rows][cols] gradient that also forms its column sums
+// (the producing nn.Linear's bias gradient) from the bf16 values it reads anyway: block b owns
+// rows [b * rpb, (b + 1) * rpb), a thread owns 8-column chunks (every chunk of the band is one
+// thread's, so no in-block combine) -> cpart[b][cols]. cols % 8 == 0.
+template <int FMT>
+__global__ void __launch_bounds__(1024) cast_fp8_delayed_cs_kernel(const u16* __restrict__ x, int rows, int cols,
+                                                                   int rpb, float* __restrict__ meta,
+                                                                   uint8_t* __restrict__ q, float* __restrict__ cpart) {
+  __shared__ float red[16];
+  const float s = meta[0];
+  const int c8n = cols / 8;
+  const int r0 = blockIdx.x * rpb, r1 = min(rows, r0 + rpb);
+  float m = 0.f;
+  for (int c8 = threadIdx.x; c8 < c8n; c8 += blockDim.x) {  // (one trip when cols <= 8 * blockDim)
+    float cs[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    int r = r0;
+    auto row = [&](const u32x4& w, long base) __attribute__((always_inline)) {
+      float v[8];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        v[2 * e] = lo_bf(w[e]);
+        v[2 * e + 1] = hi_bf(w[e]);
+      }
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        m = fmaxf(m, fabsf(v[e]));
+        cs[e] += v[e];
+      }
+      uint2 o;
+      o.x = cvt4<FMT>(v[0] * s, v[1] * s, v[2] * s, v[3] * s);
+      o.y = cvt4<FMT>(v[4] * s, v[5] * s, v[6] * s, v[7] * s);
+      *reinterpret_cast<uint2*>(q + base) = o;
+    };
+    for (; r + 3 < r1; r += 4) {  // four rows' loads in flight before any is used
+      u32x4 w[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) w[u] = *reinterpret_cast<const u32x4*>(x + (long)(r + u) * cols + c8 * 8);
+#pragma unroll
+      for (int u = 0; u < 4; ++u) row(w[u], (long)(r + u) * cols + c8 * 8);
+    }
+    for (; r < r1; ++r) row(*reinterpret_cast<const u32x4*>(x + (long)r * cols + c8 * 8), (long)r * cols + c8 * 8);
+    float* cp = cpart + (long)blockIdx.x * cols + c8 * 8;
+    *reinterpret_cast<f32x4*>(cp) = f32x4{cs[0], cs[1], cs[2], cs[3]};
+    *reinterpret_cast<f32x4*>(cp + 4) = f32x4{cs[4], cs[5], cs[6], cs[7]};
+  }
+  m = warp_max(m);
+  const int nw = (blockDim.x + 63) / 64;
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = m;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float bm = red[0];
+    for (int k = 1; k < nw; ++k) bm = fmaxf(bm, red[k]);
+    atomicMax(reinterpret_cast<unsigned int*>(meta) + 2, __float_as_uint(bm));  // order-free -> deterministic
+  }
+}
+
 // history roll, one tiny launch after the cast (a last-block roll inside the
 // cast would need a device-scope release fence per block: an L2 write-back on
 // the multi-XCD part)
@@ -375,6 +431,41 @@ PDT_API int pdt_gelu_dual_cast_fp8(const void* y, long n, float* meta, int fmt, 
     hipLaunchKernelGGL(fp8_meta_roll_kernel<1>, dim3(1), dim3(64), 0, st, meta, dq_out);
   }
   PDT_RETURN_LAUNCH();
+}
+
+PDT_API int pdt_wgrad_reduce_rows(const float* rows, float* out, int nrows, int n, float scale, int accumulate,
+                                  float* work, hipStream_t stream);
+PDT_API long pdt_reduce_rows_work(int nrows, int n);
+
+// row bands of pdt_cast_fp8_delayed_cs (its cpart holds that many rows of cols floats, followed
+// by pdt_reduce_rows_work(bands, cols) floats of reduce workspace)
+PDT_API int pdt_cast_cs_bands(int rows) {
+  int rpb = 64;
+  while ((rows + rpb - 1) / rpb > 2048) rpb *= 2;
+  return (rows + rpb - 1) / rpb;
+}
+
+// pdt_cast_fp8_delayed for a bf16 [rows][cols] gradient + its column sums into bias_out (=)
+PDT_API int pdt_cast_fp8_delayed_cs(const void* x, int rows, int cols, float* meta, int fmt, void* q, float* dq_out,
+                                    float* cpart, float* bias_out, hipStream_t st) {
+  if (cols % 8 != 0 || rows < 1 || !cpart || !bias_out) return -1;
+  const int nb = pdt_cast_cs_bands(rows);
+  const int rpb = (rows + nb - 1) / nb;
+  const u16* X = (const u16*)x;
+  // one thread per 8-column chunk (wave-rounded, at most 1024)
+  int nt = ((cols / 8 + 63) / 64) * 64;
+  if (nt > 1024) nt = 1024;
+  if (fmt == 0)
+    hipLaunchKernelGGL(cast_fp8_delayed_cs_kernel<0>, dim3(nb), dim3(nt), 0, st, X, rows, cols, rpb, meta,
+                       (uint8_t*)q, cpart);
+  else
+    hipLaunchKernelGGL(cast_fp8_delayed_cs_kernel<1>, dim3(nb), dim3(nt), 0, st, X, rows, cols, rpb, meta,
+                       (uint8_t*)q, cpart);
+  if (fmt == 0) hipLaunchKernelGGL(fp8_meta_roll_kernel<0>, dim3(1), dim3(64), 0, st, meta, dq_out);
+  else hipLaunchKernelGGL(fp8_meta_roll_kernel<1>, dim3(1), dim3(64), 0, st, meta, dq_out);
+  const int e = (int)hipGetLastError();
+  if (e) return e;
+  return pdt_wgrad_reduce_rows(cpart, bias_out, nb, cols, 1.f, 0, cpart + (long)nb * cols, st);
 }
 
 // roll after a fused producer (pdt_ln_fwd_f8): partial[nblk] holds its per-block amaxes

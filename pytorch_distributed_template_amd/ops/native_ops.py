@@ -51,6 +51,8 @@ _SIGS = {
     "pdt_gemm_f8_q8": (c_int, [P] * 6 + [c_int] * 8 + [P, P, c_int, P, P, P, c_int, c_int, P, P]),
     "pdt_gemm_f8_q8_cs": (c_int, [P] * 6 + [c_int] * 8 + [P, P, c_int, P, P, P, c_int, c_int, P, P, P]),
     "pdt_gemm_f8_bm": (c_int, [c_int]),
+    "pdt_cast_cs_bands": (c_int, [c_int]),
+    "pdt_cast_fp8_delayed_cs": (c_int, [P, c_int, c_int, P, c_int, P, P, P, P, P]),
     "pdt_wgrad_reduce_rows": (c_int, [P, P, c_int, c_int, c_float, c_int, P, P]),
     "pdt_reduce_rows_work": (c_long, [c_int, c_int]),
     "pdt_gemm_f8_q8_part": (c_long, [c_int, c_int]),
@@ -2555,6 +2557,27 @@ def linear_wgrad_f8(dyq, xq, dq_dy, dq_x, dy16=None, with_bias=False, variant=No
     return dw, db
 
 
+def _quant_grad_db(g2, owner, attr, bias):
+    """(e5m2 codes, dequant, bias gradient) of a bf16 [rows][cols] output gradient in ONE pass
+    (pdt_cast_fp8_delayed_cs: the delayed-scaling cast that also sums the columns it reads),
+    or None when that path does not apply (current scaling, no history yet, PDT_CAST_DB=0)."""
+    meta = getattr(owner, attr, None)
+    if meta is None or fp8_settings()["scaling"] != "delayed" or os.environ.get("PDT_CAST_DB", "1") != "1":
+        return None
+    rows, cols = g2.shape
+    if cols % 8:
+        return None
+    lib = _load()
+    nb = lib.pdt_cast_cs_bands(rows)
+    q = torch.empty((rows, cols), dtype=torch.uint8, device=g2.device)
+    dq = torch.empty(1, dtype=torch.float32, device=g2.device)
+    cpart = torch.empty(nb * cols + lib.pdt_reduce_rows_work(nb, cols), dtype=torch.float32, device=g2.device)
+    db = _grad_buf(bias, (cols,))
+    _chk(lib.pdt_cast_fp8_delayed_cs(_p(g2), rows, cols, _p(meta), E5M2, _p(q), _p(dq), _p(cpart), _p(db), _s()),
+         "cast_fp8_delayed_cs")
+    return q, dq, db
+
+
 def _pre_bias_grad(g, owner):
     """The bias gradient of ``owner`` if the producer of its output gradient ``g`` (a LayerNorm
     backward, :func:`_ln_fork_backward`) already formed it, else None."""
@@ -2639,8 +2662,15 @@ class _LinearF8(torch.autograd.Function):
         need = ctx.needs_input_grad
         dx = None
         dyq = dqdy = None
+        cast_db = None
         if ctx.fp8_dgrad and (need[0] or (ctx.f8w and need[1])):
-            dyq, dqdy = _quant_grad(dy2, ctx.fc, "_pdt_fp8_gmeta", src=dy if act is None else None)
+            pre = getattr(dy, "_pdt_f8g", None) if act is None else None
+            if act is None and has_b and need[2] and ctx.f8w and need[1] and (pre is None or pre[2] is not ctx.fc):
+                cast_db = _quant_grad_db(dy2, ctx.fc, "_pdt_fp8_gmeta", ctx.bref)
+            if cast_db is not None:
+                dyq, dqdy = cast_db[0], cast_db[1]
+            else:
+                dyq, dqdy = _quant_grad(dy2, ctx.fc, "_pdt_fp8_gmeta", src=dy if act is None else None)
         if need[0]:
             if ctx.fp8_dgrad:
                 _, wqt, dqw = fp8_weight(w)
@@ -2651,6 +2681,8 @@ class _LinearF8(torch.autograd.Function):
             dx = dx.reshape(*shp[:-1], K)
         want_db = has_b and need[2]
         pre_db = _pre_bias_grad(dy, ctx.fc) if act is None and want_db else None
+        if pre_db is None and cast_db is not None:
+            pre_db = cast_db[2]
         if ctx.f8w and need[1]:
             dw, db = linear_wgrad_f8(dyq, ctx.xq, dqdy, ctx.dqx, dy16=dy2, with_bias=want_db and pre_db is None, w=w,
                                      b=ctx.bref)

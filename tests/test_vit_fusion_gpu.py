@@ -529,13 +529,16 @@ def test_ln_add_fork_matches_add_then_fork(fp8):
 
 
 def test_ln_backward_bias_grads_match_wgrad_bias(monkeypatch):
-    """PDT_LN_DB: the proj / fc2 bias gradients formed as column sums of dx inside the
-    LayerNorm backward equal the ones the fp8 weight-gradient kernel sums from the same bf16
-    gradient (2-block fp8 ViT, second step so the delayed-scaling state exists)."""
+    """Bias gradients formed where the gradient is written -- proj / fc2 in the LayerNorm
+    backward (PDT_LN_DB), fc1 in the fc2 data-gradient epilogue (PDT_F8_DB_EPI), qkv in the
+    e5m2 cast of its output gradient (PDT_CAST_DB) -- equal the ones the fp8 weight-gradient
+    kernel sums from the same bf16 gradients (2-block fp8 ViT, second step so the
+    delayed-scaling state exists)."""
     from pytorch_distributed_template_amd.models import vit_b_16
     grads = {}
     for mode in ("0", "1"):
-        monkeypatch.setenv("PDT_LN_DB", mode)
+        for var in ("PDT_LN_DB", "PDT_F8_DB_EPI", "PDT_CAST_DB"):
+            monkeypatch.setenv(var, mode)
         torch.manual_seed(51)
         m = vit_b_16(num_classes=16, fp8=True, depth=2).cuda()
         x = torch.randn(4, 3, 224, 224, device="cuda")
@@ -544,8 +547,8 @@ def test_ln_backward_bias_grads_match_wgrad_bias(monkeypatch):
             m(x).float().square().mean().backward()
         torch.cuda.synchronize()
         grads[mode] = {n: p.grad.detach().clone() for n, p in m.named_parameters()
-                       if n.endswith("bias") and ("proj" in n or "fc2" in n)}
-    assert grads["1"].keys() == grads["0"].keys() and len(grads["1"]) == 4
+                       if n.endswith("bias") and any(k in n for k in ("qkv", "proj", "fc1", "fc2"))}
+    assert grads["1"].keys() == grads["0"].keys() and len(grads["1"]) == 8
     for n in grads["1"]:
         assert nrmerr(grads["1"][n], grads["0"][n]) < 1e-3, n
 
