@@ -561,16 +561,16 @@ PDT_API int pdt_wgrad_plan(int M, int Mo, int No, int variant, int* ktiles_per_s
   int smax = (target + tiles - 1) / tiles;
   if (smax > nk) smax = nk;
   if (smax < 1) smax = 1;
-  static int legacy = -1;
-  if (legacy < 0) {
+  static int mode = -1;  // PDT_WG_PLAN: 0 legacy for every tile, 1 wave plan for every tile, unset: by tile
+  if (mode < 0) {
     const char* e = getenv("PDT_WG_PLAN");
-    legacy = (e && e[0] == '1') ? 0 : 1;
+    mode = (e && e[0] == '0') ? 0 : (e && e[0] == '1') ? 1 : 2;
   }
   int splits = smax;
   // the wave model fits one-workgroup-per-CU tiles (every resident workgroup runs at the same
-  // rate): those always take it; multi-workgroup tiles only with PDT_WG_PLAN=1
+  // rate): those take it by default; multi-workgroup tiles only with PDT_WG_PLAN=1
   const long slots = wg_slots(variant, w);
-  if (legacy && slots > pdt_num_cus()) {
+  if (mode == 0 || (mode == 2 && slots > pdt_num_cus())) {
     while (splits > 1 && (nk + splits - 1) / splits < 8) --splits;
   } else {
     long best_cost = -1;
