@@ -615,7 +615,7 @@ static int gemm_f8_impl(const void* a, const void* b, void* out, const float* bi
   p.q8_fmt = q8_fmt;
   p.q8_only = q8_only;
   if ((q8 != nullptr || colsum != nullptr) && v == 7) return -5;  // the direct-store epilogue has neither
-  p.colsum = colsum;
+  p.stats = colsum;  // fp8 instantiations: the column-sum output (conv_nt_kernel.h)
   const int rc = fmt_a == 1 ? launch_f8<2>(v, p, stream) : launch_f8<1>(v, p, stream);
   if (rc || q8 == nullptr) return rc;
   const int nblk = ((M + VAR_F8_BM[v] - 1) / VAR_F8_BM[v]) * ((N + VAR_F8_BN[v] - 1) / VAR_F8_BN[v]);
