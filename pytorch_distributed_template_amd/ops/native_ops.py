@@ -3186,8 +3186,11 @@ def qkv_attention(qkv, num_heads, fp8=False, fp8_for=None, grad_fp8_for=None):
     # Off by default (PDT_FP8_ATTN_Q8=1 enables): the attention kernels write O / d(qkv) one
     # row per lane, so the extra 4-byte code stores are uncoalesced and cost more than the
     # separate cast passes they replace (same-box A/B: 6.32k vs 6.40k img/s, runs r4e-r4h)
-    if os.environ.get("PDT_FP8_ATTN_Q8", "0") != "1":
-        fp8_for = grad_fp8_for = None
+    q8 = os.environ.get("PDT_FP8_ATTN_Q8", "0")  # "fwd": only the forward's e4m3 output codes
+    if q8 != "1":
+        grad_fp8_for = None
+        if q8 != "fwd":
+            fp8_for = None
     if fp8 and fp8_for is not None and fp8_settings()["scaling"] == "delayed":
         meta = getattr(fp8_for, "_pdt_fp8_meta", None)
     box: list = []
