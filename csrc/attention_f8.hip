@@ -87,14 +87,15 @@ __device__ __forceinline__ int k16_off(int row, int chunk) { return row * 128 + 
 // score GEMM in bf16 (4 x mfma_f32_32x32x16_bf16 per 32 x 32 tile, K kept as bf16) -- the
 // bf16 forward of ViT (126 VGPRs, 3 workgroups per CU, vs 248 VGPRs / 1 wave per SIMD
 // for the whole-sequence kernel in csrc/attention.hip)
-template <int NKT, bool F8, bool PV8 = false>
-__global__ void __launch_bounds__(256) attn_fwd_f8_kernel(AttnF8Params p) {
+template <int NKT, bool F8, bool PV8 = false, int NW = 4>
+__global__ void __launch_bounds__(64 * NW) attn_fwd_f8_kernel(AttnF8Params p) {
+  constexpr int NTH = 64 * NW;
   static_assert(F8 || !PV8, "the fp8 PV rides on the fp8 score kernel");
   constexpr int ROWS = NKT * 32;
   constexpr int VROWS = PV8 ? 64 * ((NKT + 1) / 2) : ROWS;         // fp8 V: whole key-tile pairs
   __shared__ __attribute__((aligned(16))) char Ks[ROWS * (F8 ? 64 : 128)];  // fp8 or bf16 K
   __shared__ __attribute__((aligned(16))) char Vs[VROWS * (PV8 ? 64 : 128)];  // fp8 rows / bf16 tr image
-  __shared__ float red[4], vred[4];
+  __shared__ float red[NW], vred[NW];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int bh = blockIdx.x, b = bh / p.H, h = bh % p.H;
   const u16* base = p.qkv + (long)b * p.T * p.ld + h * D;
@@ -104,12 +105,12 @@ __global__ void __launch_bounds__(256) attn_fwd_f8_kernel(AttnF8Params p) {
   // ---- stage V (bf16 transposed-read image, or e4m3 rows) and K (registers first: |K|max)
   constexpr int CH = ROWS * 8;  // 16-B chunks of one [ROWS][64] bf16 matrix
   constexpr int VCH = VROWS * 8;
-  constexpr int NIT = (VCH + 255) / 256;
+  constexpr int NIT = (VCH + NTH - 1) / NTH;
   u32x4 kv[NIT], vv[PV8 ? NIT : 1];
   float kmax = 0.f, vmax = 0.f;
 #pragma unroll
   for (int it = 0; it < NIT; ++it) {
-    const int q = tid + it * 256;
+    const int q = tid + it * NTH;
     const int row = q >> 3, ch = q & 7;
     u32x4 v = {0, 0, 0, 0}, k = {0, 0, 0, 0};
     if (q < VCH && row < p.T) {
@@ -137,15 +138,20 @@ __global__ void __launch_bounds__(256) attn_fwd_f8_kernel(AttnF8Params p) {
       vred[wave] = vmax;
     }
     __syncthreads();
-    kmax = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
+    kmax = red[0];
+#pragma unroll
+    for (int w = 1; w < NW; ++w) kmax = fmaxf(kmax, red[w]);
     sk = pow2_scale(kmax);
   }
   if constexpr (PV8) {
-    ev = pdt_f8::pow2_exp(fmaxf(fmaxf(vred[0], vred[1]), fmaxf(vred[2], vred[3])));
+    float vm = vred[0];
+#pragma unroll
+    for (int w = 1; w < NW; ++w) vm = fmaxf(vm, vred[w]);
+    ev = pdt_f8::pow2_exp(vm);
     sv = ldexpf(1.f, ev);
 #pragma unroll
     for (int it = 0; it < NIT; ++it) {  // e4m3 V rows (zero rows up to the tile pair)
-      const int q = tid + it * 256;
+      const int q = tid + it * NTH;
       if (q < VCH) {
         const int row = q >> 3, ch = q & 7;
         const u32x4 v = vv[it];
@@ -158,7 +164,7 @@ __global__ void __launch_bounds__(256) attn_fwd_f8_kernel(AttnF8Params p) {
   }
 #pragma unroll
   for (int it = 0; it < NIT; ++it) {
-    const int q = tid + it * 256;
+    const int q = tid + it * NTH;
     if (!F8 && q < CH) {
       const int row = q >> 3, ch = q & 7;
       *reinterpret_cast<u32x4*>(Ks + k16_off(row, ch)) = kv[it];
@@ -178,7 +184,7 @@ __global__ void __launch_bounds__(256) attn_fwd_f8_kernel(AttnF8Params p) {
   const int grp = lane >> 4, i16 = lane & 15;  // 16-lane group of the transposed V reads
   const int nqt = (p.T + 31) / 32;
   float q8max = 0.f;
-  for (int qt = wave; qt < nqt; qt += 4) {
+  for (int qt = wave; qt < nqt; qt += NW) {
     // ---- Q tile -> e4m3 B fragment: lane (q = col, hh) holds Q[q][32 hh .. 32 hh + 31]
     const int q = qt * 32 + col;
     // fp8: qv[c] = Q[q][32 hh + 8 c .. +7] (one 32-B fp8 fragment); bf16: qb[kk] = Q[q][16 kk + 8 hh .. +7]
@@ -376,7 +382,12 @@ __global__ void __launch_bounds__(256) attn_fwd_f8_kernel(AttnF8Params p) {
     __syncthreads();
     if (lane == 0) red[wave] = q8max;
     __syncthreads();
-    if (tid == 0) p.q8_part[bh] = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
+    if (tid == 0) {
+      float m8 = red[0];
+#pragma unroll
+      for (int w = 1; w < NW; ++w) m8 = fmaxf(m8, red[w]);
+      p.q8_part[bh] = m8;
+    }
   }
 }
 
@@ -394,6 +405,17 @@ static int attn_pv8() {
   }
   return g_attn_pv8;
 }
+// PDT_ATTN_FWD_NW8=0: the 4-wave forward for T > 128 as well (A/B switch; 8 waves give each of
+// the 7 query tiles of T = 197 its own wave instead of 2 rounds with one wave idle)
+static int attn_fwd_nw8() {
+  static int v = -1;
+  if (v < 0) {
+    const char* e = getenv("PDT_ATTN_FWD_NW8");
+    v = (e && e[0] == '0') ? 0 : 1;
+  }
+  return v;
+}
+
 PDT_API int pdt_attn_set_pv8(int on) {
   g_attn_pv8 = on ? 1 : 0;
   return 0;
@@ -414,6 +436,15 @@ PDT_API int pdt_attn_fwd_f8(const void* qkv, void* out, float* lse, int B, int T
   p.q8 = nullptr; p.q8_meta = nullptr; p.q8_part = nullptr;
   const int nkt = (T + 31) / 32;
   dim3 g(B * H);
+  if (nkt >= 5 && !attn_pv8() && attn_fwd_nw8()) {  // 8 waves: one 32-query tile each (T = 197: 7)
+    switch (nkt) {
+      case 5: hipLaunchKernelGGL((attn_fwd_f8_kernel<5, true, false, 8>), g, dim3(512), 0, st, p); break;
+      case 6: hipLaunchKernelGGL((attn_fwd_f8_kernel<6, true, false, 8>), g, dim3(512), 0, st, p); break;
+      case 7: hipLaunchKernelGGL((attn_fwd_f8_kernel<7, true, false, 8>), g, dim3(512), 0, st, p); break;
+      default: hipLaunchKernelGGL((attn_fwd_f8_kernel<8, true, false, 8>), g, dim3(512), 0, st, p); break;
+    }
+    PDT_RETURN_LAUNCH();
+  }
 #define F8(N)                                                                         \
   if (attn_pv8()) hipLaunchKernelGGL((attn_fwd_f8_kernel<N, true, true>), g, dim3(256), 0, st, p); \
   else hipLaunchKernelGGL((attn_fwd_f8_kernel<N, true, false>), g, dim3(256), 0, st, p)
