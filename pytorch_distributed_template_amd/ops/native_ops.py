@@ -2414,11 +2414,27 @@ def _f8_lib_ok(out, act, aux, addend, q8) -> bool:
         hasattr(torch, "_scaled_mm") and os.environ.get("PDT_FP8_LIB", "1") == "1"
 
 
+_BIAS16: dict = {}
+
+
+def _bias_bf16(bias):
+    """bf16 copy of an fp32 bias for the library GEMM, cached per tensor version (the same
+    parameter serves every step's forward until the optimizer updates it)."""
+    if not isinstance(bias, torch.nn.Parameter):  # (a temporary: nothing to reuse)
+        return bias.to(torch.bfloat16)
+    ent = _BIAS16.get(id(bias))
+    if ent is not None and ent[0] == bias._version and ent[1] == bias.data_ptr() and _same_tensor(ent[3], bias):
+        return ent[2]
+    bb = bias.detach().to(torch.bfloat16)
+    _BIAS16[id(bias)] = (bias._version, bias.data_ptr(), bb, _weak(bias))
+    return bb
+
+
 def _gemm_f8_lib(a, b, out, dq_a, dq_b, fmt_a, bias):
     M, N = a.shape[0], b.shape[0]
     A = a.view(torch.float8_e5m2 if fmt_a == E5M2 else torch.float8_e4m3fn)
     B = b.view(torch.float8_e4m3fn).t()  # [K][N] column-major: the layout hipBLASLt takes
-    bb = bias.to(torch.bfloat16) if bias is not None else None
+    bb = _bias_bf16(bias) if bias is not None else None
     torch._scaled_mm(A, B, scale_a=dq_a.reshape(()), scale_b=dq_b.reshape(()), bias=bb, out_dtype=torch.bfloat16,
                      out=out.view(M, N))
     return 0
