@@ -2513,10 +2513,14 @@ def gemm_f8(a, b, out, dq_a, dq_b, *, fmt_a=E4M3, bias=None, act=0, aux=None, ad
     if variant is None:
         key = f"f8b:{M},{N},{K},{fmt_a},{act},{int(bias is not None)},q{qfmt}{int(only)}" + \
             (",cs" if colsum_out is not None else "")
-        # (tuning launches roll the history too: tune on a scratch copy of the state)
-        scratch = meta.clone()
-        targs = lambda v: args(v)[:17] + (_p(codes), _p(scratch)) + args(v)[19:]  # noqa: E731
-        variant = _autotune(key, lib.pdt_gemm_f8_num_variants(), lambda v: lib.pdt_gemm_f8_q8(*targs(v)))
+        table = _tuned()
+        if key in table:
+            variant = int(table[key])
+        else:
+            # (tuning launches roll the history too: tune on a scratch copy of the state)
+            scratch = meta.clone()
+            targs = lambda v: args(v)[:17] + (_p(codes), _p(scratch)) + args(v)[19:]  # noqa: E731
+            variant = _autotune(key, lib.pdt_gemm_f8_num_variants(), lambda v: lib.pdt_gemm_f8_q8(*targs(v)))
     if colsum_out is not None:
         assert colsum_out.dtype == torch.float32 and colsum_out.numel() == N and colsum_out.is_contiguous()
         if variant == 7 or variant < 0:  # the direct-store tile has no staged epilogue
