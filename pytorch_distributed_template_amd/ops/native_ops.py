@@ -2407,6 +2407,7 @@ def fp8_weight(w: torch.Tensor):
 # data-gradient shapes and the qkv projection it measured 1.16-1.42x the native ring tiles
 # (profiles/vit_fp8_gemm_library_round4.txt); every fused-epilogue GEMM stays native.
 F8_LIB = 100
+_F8_LIB_BROKEN: list = []  # set once torch._scaled_mm refused a call: every library id runs native
 
 
 def _f8_lib_ok(out, act, aux, addend, q8) -> bool:
@@ -2440,11 +2441,13 @@ def _gemm_f8_lib(a, b, out, dq_a, dq_b, fmt_a, bias):
     return 0
 
 
-def _fc1_lib(M, Hd, K) -> bool:
+def _fc1_lib(M, Hd, K) -> bool:  # noqa: D401
     """The MLP's fp8 fc1 as the library GEMM (+bias) followed by one pass that writes gelu'(z),
     the e4m3 codes of gelu(z) and their amax (pdt_gelu_dual_cast_fp8), instead of the native
     GEMM with that epilogue fused (act 4 + fp8 side output). Tuned-table key ``fc1lib:M,Hd,K``
     (1 = library); PDT_FP8_FC1_LIB=0/1 forces either."""
+    if _F8_LIB_BROKEN:
+        return False
     env = os.environ.get("PDT_FP8_FC1_LIB")
     if env is not None:
         return env == "1" and hasattr(torch, "_scaled_mm")
@@ -2499,8 +2502,13 @@ def gemm_f8(a, b, out, dq_a, dq_b, *, fmt_a=E4M3, bias=None, act=0, aux=None, ad
                 _tuned()[key] = F8_LIB
                 _save_tuned()
         if variant == F8_LIB:
-            if lib_ok:
-                return _gemm_f8_lib(a, b, out, dq_a, dq_b, fmt_a, bias) or out
+            if lib_ok and not _F8_LIB_BROKEN:
+                try:
+                    return _gemm_f8_lib(a, b, out, dq_a, dq_b, fmt_a, bias) or out
+                except RuntimeError as e:  # a hipBLASLt without this fp8 layout / bias combination
+                    _F8_LIB_BROKEN.append(str(e))
+                    import warnings
+                    warnings.warn(f"fp8 library GEMM unavailable ({e}); using the native tiles")
             variant = -1  # (library path disabled / not applicable: the built-in native choice)
         _chk(lib.pdt_gemm_f8(*args(variant)), "gemm_f8")
         return out
