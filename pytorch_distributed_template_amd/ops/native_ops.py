@@ -2441,7 +2441,7 @@ def _gemm_f8_lib(a, b, out, dq_a, dq_b, fmt_a, bias):
     return 0
 
 
-def _fc1_lib(M, Hd, K) -> bool:  # noqa: D401
+def _fc1_lib(M, Hd, K) -> bool:
     """The MLP's fp8 fc1 as the library GEMM (+bias) followed by one pass that writes gelu'(z),
     the e4m3 codes of gelu(z) and their amax (pdt_gelu_dual_cast_fp8), instead of the native
     GEMM with that epilogue fused (act 4 + fp8 side output). Tuned-table key ``fc1lib:M,Hd,K``
@@ -2772,9 +2772,13 @@ class _Mlp(torch.autograd.Function):
             meta2 = getattr(mlp.fc2, "_pdt_fp8_meta", None) if cfg["scaling"] == "delayed" else None
             if meta2 is not None:  # fc1's epilogue writes fc2's e4m3 input (bf16 a only if a bf16 wgrad needs it)
                 aq = torch.empty((Mrows, Hd), dtype=torch.uint8, device=dev)
+                dqa = None
                 if dual and _fc1_lib(Mrows, Hd, K):
-                    dqa = _fc1_lib_forward(xq, w1q, a, z, aq, dqx, dqw1, bias1, meta2, keep_a=not f8w)
-                else:
+                    try:
+                        dqa = _fc1_lib_forward(xq, w1q, a, z, aq, dqx, dqw1, bias1, meta2, keep_a=not f8w)
+                    except RuntimeError as e:  # (see gemm_f8: the native tiles from here on)
+                        _F8_LIB_BROKEN.append(str(e))
+                if dqa is None:
                     dqa = gemm_f8(xq, w1q, a, dqx, dqw1, bias=bias1, act=act1, aux=z, q8=(aq, meta2, E4M3, f8w))
             else:
                 gemm_f8(xq, w1q, a, dqx, dqw1, bias=bias1, act=act1, aux=z)
