@@ -3284,6 +3284,67 @@ class _PatchEmbed(torch.autograd.Function):
         return dx, dw, db, None
 
 
+class _PatchLinear(torch.autograd.Function):
+    """Non-overlapping patch conv as patchify + plain GEMM: one strided copy forms the
+    [B*N_patches, C*KH*KW] patch matrix (bf16, in the weight's own element order), then the
+    bf16 GEMM (bias in its epilogue) writes the token matrix and the weight gradient + bias
+    sums are one plain wgrad call on the same patch matrix. For 3-channel images this is
+    K = 768 instead of the implicit GEMM's channel-padded K = 2048 (ViT-B/16), and no pad pass.
+    The reference runs torch's conv (torchvision vit_b_16 ``conv_proj``)."""
+
+    @staticmethod
+    def forward(ctx, x, w, b, conv):
+        N, C, H, W = x.shape
+        Cout, _, KH, KW = w.shape
+        nh, nw = H // KH, W // KW
+        K = C * KH * KW
+        kkc = w.is_contiguous(memory_format=torch.channels_last) and not w.is_contiguous()
+        xv = x.view(N, C, nh, KH, nw, KW)
+        pm = torch.empty((N * nh * nw, K), dtype=torch.bfloat16, device=x.device)
+        if kkc:  # weight memory order (kh, kw, c)
+            pm.view(N, nh, nw, KH, KW, C).copy_(xv.permute(0, 2, 4, 3, 5, 1))
+            wb = bf16_weight(w).permute(0, 2, 3, 1).reshape(Cout, K)
+        else:    # (c, kh, kw)
+            pm.view(N, nh, nw, C, KH, KW).copy_(xv.permute(0, 2, 4, 1, 3, 5))
+            wb = w.detach().reshape(Cout, K).to(torch.bfloat16).contiguous()
+        y = torch.empty((N * nh * nw, Cout), dtype=torch.bfloat16, device=x.device)
+        _gemm_bf16(pm, wb, y, bias=b.float().contiguous() if b is not None else None)
+        ctx.save_for_backward(pm)
+        ctx.meta = (w, b, kkc, N, nh * nw)
+        return y.view(N, nh * nw, Cout)
+
+    @staticmethod
+    def backward(ctx, dtok):
+        (pm,) = ctx.saved_tensors
+        w, b, kkc, N, npatch = ctx.meta
+        Cout = w.shape[0]
+        K = pm.shape[1]
+        want_dw, want_db = ctx.needs_input_grad[1], b is not None and ctx.needs_input_grad[2]
+        dy2 = dtok.reshape(-1, Cout).to(torch.bfloat16).contiguous()
+        dw = db = None
+        if want_dw:
+            if kkc:
+                dw = _grad_buf(w, tuple(w.shape), torch.channels_last)
+                dw2 = dw.permute(0, 2, 3, 1).reshape(Cout, K)
+            else:
+                dw = _grad_buf(w, tuple(w.shape))
+                dw2 = dw.view(Cout, K)
+            db = _grad_buf(b, (Cout,)) if want_db else None
+            conv_wgrad(dy2, pm, dw2, M=dy2.shape[0], Mo=Cout, No=K, ldy=Cout, Hs=1, Ws=1, C=K, Hm=1, Wm=1, sh=1,
+                       sw=1, oh0=0, ow0=0, dh=1, dw=1, ntw=1, bias_out=db)
+            dw = dw.to(w.dtype) if dw.dtype != w.dtype else dw
+        elif want_db:
+            db = colsum(dy2, dy2.shape[0], Cout)
+        return None, dw, db, None
+
+
+def _patch_linear_ok(x, conv) -> bool:
+    if os.environ.get("PDT_PATCH_LINEAR", "1") != "1" or x.requires_grad:
+        return False
+    K = conv.in_channels * conv.kernel_size[0] * conv.kernel_size[1]
+    return K % 8 == 0 and x.dtype in (torch.bfloat16, torch.float32)
+
+
 def patch_embed(x, conv):
     KH, KW = conv.kernel_size
     if (conv.stride != conv.kernel_size or conv.padding != (0, 0) or conv.out_channels % 8 or conv.groups != 1
@@ -3293,6 +3354,8 @@ def patch_embed(x, conv):
                                 "(kernel: non-overlapping patches, bias-any, channels <= 8 or % 8 == 0)")
         y = conv(x)
         return y.flatten(2).transpose(1, 2)
+    if _patch_linear_ok(x, conv):
+        return _PatchLinear.apply(x, conv.weight, conv.bias, conv)
     return _PatchEmbed.apply(x, conv.weight, conv.bias, conv)
 
 

@@ -324,8 +324,11 @@ def test_vit_fp8_steps_track_torch_fp32():
         worst = max((nrmerr(out["native"][1][n], out["torch"][1][n]), n) for n in out["torch"][1])
         errs.append((it, el, worst))
     print(errs)
+    # 128 logits of a random-init model: the fp8 quantisation noise realised in them moves with
+    # bit-level rounding of the bf16 inputs (0.073 with the implicit-GEMM patch embedding, 0.083
+    # with patchify + GEMM, whose tokens are as accurate: scripts/probe_patch_embed.py)
     for it, el, worst in errs:
-        assert el < 8e-2, errs
+        assert el < 0.1, errs
         assert worst[0] < 0.25, errs
     assert m.blocks[0].attn.qkv._pdt_fp8_meta is not None and m.blocks[0].mlp.fc2._pdt_fp8_gmeta is not None
 
@@ -582,3 +585,28 @@ def test_gemm_f8_epilogue_column_sums(variant):
     assert torch.equal(codes1, codes) and torch.equal(dq1, dq0) and torch.equal(m1, m0)
     ref = out.float().sum(0)
     assert nrmerr(cs, ref) < 1e-5, nrmerr(cs, ref)
+
+
+@pytest.mark.parametrize("layout", ["channels_last", "contiguous"])
+@pytest.mark.parametrize("path", ["linear", "implicit"])
+def test_patch_embedding_matches_conv_fp32(layout, path, monkeypatch):
+    """Patch embedding (patchify + plain GEMM, or the channel-padded implicit GEMM) vs an fp32
+    conv: tokens, weight gradient and bias gradient, for both weight memory layouts."""
+    monkeypatch.setenv("PDT_PATCH_LINEAR", "1" if path == "linear" else "0")
+    torch.manual_seed(0)
+    conv = nn.Conv2d(3, 768, 16, stride=16).cuda()
+    mf = torch.channels_last if layout == "channels_last" else torch.contiguous_format
+    conv = conv.to(memory_format=mf)
+    x = torch.randn(4, 3, 224, 224, device="cuda").to(torch.bfloat16)
+    g = torch.randn(4, 196, 768, device="cuda")
+    ref = nn.Conv2d(3, 768, 16, stride=16).cuda()
+    ref.load_state_dict(conv.state_dict())
+    yr = ref(x.float()).flatten(2).transpose(1, 2)
+    yr.backward(g)
+    y = no.patch_embed(x, conv)
+    y.backward(g.to(torch.bfloat16))
+    assert y.shape == (4, 196, 768)
+    assert nrmerr(y, yr) < 1e-2
+    assert conv.weight.grad.shape == ref.weight.grad.shape
+    assert nrmerr(conv.weight.grad, ref.weight.grad) < 1e-2
+    assert nrmerr(conv.bias.grad, ref.bias.grad) < 1e-2
