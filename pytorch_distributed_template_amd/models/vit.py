@@ -119,9 +119,7 @@ class VisionTransformer(BaseModel):
 
     def forward(self, x):
         x = fused.patch_embed(x, self.patch_embed)                 # [B, N, D]
-        B = x.shape[0]
-        cls = self.cls_token.to(x.dtype).expand(B, -1, -1)
-        x = torch.cat([cls, x], dim=1) + self.pos_embed.to(x.dtype)
+        x = fused.embed_tokens(x, self.cls_token, self.pos_embed)  # [B, N+1, D]
         prev = None
         pending = None
         defer = self.fp8 and _ln_add()

@@ -222,6 +222,16 @@ def patch_embed(x, conv: nn.Conv2d):
     return y.flatten(2).transpose(1, 2)
 
 
+def embed_tokens(tok, cls_token, pos_embed):
+    """[cls; tok] + pos for [B, N, D] patch tokens -> [B, N+1, D]. Native path: one pass
+    writing the token buffer (no concatenated intermediate); torch path: cat + add."""
+    if _use_native(tok):
+        from . import native_ops
+        return native_ops.embed_tokens(tok, cls_token, pos_embed)
+    cls = cls_token.to(tok.dtype).expand(tok.shape[0], -1, -1)
+    return torch.cat([cls, tok], dim=1) + pos_embed.to(tok.dtype)
+
+
 def softmax_cross_entropy(logits, target, label_smoothing: float = 0.0):
     """Mean softmax cross-entropy (fused fwd/bwd kernel on the native path)."""
     if _use_native(logits):

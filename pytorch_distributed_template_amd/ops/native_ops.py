@@ -3338,6 +3338,44 @@ class _PatchLinear(torch.autograd.Function):
         return None, dw, db, None
 
 
+class _EmbedTokens(torch.autograd.Function):
+    """x[:, 0] = cls + pos[0], x[:, 1:] = tok + pos[1:] written straight into the [B, N+1, D]
+    buffer (one pass over the tokens instead of torch.cat then the broadcast add). Backward:
+    d_pos = sum over the batch, d_cls = d_pos[0] (cls and pos[0] add to the same token of every
+    image), d_tok a view of the incoming gradient. The reference gets its token assembly from
+    torchvision's vit_b_16 (class token concat + pos-embedding add)."""
+
+    @staticmethod
+    def forward(ctx, tok, cls_token, pos_embed):
+        B, N, D = tok.shape
+        x = torch.empty((B, N + 1, D), dtype=tok.dtype, device=tok.device)
+        pos = pos_embed.detach().to(tok.dtype).reshape(N + 1, D)
+        torch.add(tok, pos[1:], out=x[:, 1:])
+        x[:, 0] = (cls_token.detach().reshape(D) + pos_embed.detach().reshape(N + 1, D)[0]).to(tok.dtype)
+        ctx.meta = (cls_token.shape, cls_token.dtype, pos_embed.shape, pos_embed.dtype)
+        return x
+
+    @staticmethod
+    def backward(ctx, dx):
+        cshape, cdtype, pshape, pdtype = ctx.meta
+        need_pos = ctx.needs_input_grad[1] or ctx.needs_input_grad[2]
+        dpos = dx.sum(0, dtype=torch.float32) if need_pos else None
+        dcls = dpos[0].reshape(cshape).to(cdtype) if ctx.needs_input_grad[1] else None
+        dp = dpos.reshape(pshape).to(pdtype) if ctx.needs_input_grad[2] else None
+        dtok = dx[:, 1:] if ctx.needs_input_grad[0] else None
+        return dtok, dcls, dp
+
+
+def embed_tokens(tok, cls_token, pos_embed):
+    B, N, D = tok.shape
+    if os.environ.get("PDT_EMBED_FUSED", "1") != "1":  # A/B switch: torch.cat + add
+        return torch.cat([cls_token.to(tok.dtype).expand(B, -1, -1), tok], dim=1) + pos_embed.to(tok.dtype)
+    if cls_token.numel() != D or pos_embed.numel() != (N + 1) * D:
+        fallback("embed_tokens", f"cls {tuple(cls_token.shape)} pos {tuple(pos_embed.shape)} for tokens {tuple(tok.shape)}")
+        return torch.cat([cls_token.to(tok.dtype).expand(B, -1, -1), tok], dim=1) + pos_embed.to(tok.dtype)
+    return _EmbedTokens.apply(tok, cls_token, pos_embed)
+
+
 def _patch_linear_ok(x, conv) -> bool:
     if os.environ.get("PDT_PATCH_LINEAR", "1") != "1" or x.requires_grad:
         return False

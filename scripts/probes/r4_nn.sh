@@ -1,0 +1,10 @@
+#!/bin/bash
+# Round 4: ViT token assembly ([cls; tok] + pos) in one pass -- tests, ViT A/B.
+source "$(dirname "$0")/../gpurun_lib.sh"
+T=r4nn
+run ${T}_tests.txt 400 python -u -m pytest tests/test_vit_fusion_gpu.py tests/test_fallback_gpu.py -k "patch or vit or embed" -x -v --timeout 120 --timeout-method thread || exit $?
+grep -q " passed" gpurun_out/${T}_tests.txt && ! grep -q "failed" gpurun_out/${T}_tests.txt || { echo "tests failed"; exit 1; }
+for i in 1 2; do
+PDT_EMBED_FUSED=0 run ${T}_vit_off$i.txt 400 python bench.py --model vit_b_16 --fp8 || exit $?
+run ${T}_vit_on$i.txt 400 python bench.py --model vit_b_16 --fp8 || exit $?
+done

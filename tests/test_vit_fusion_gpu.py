@@ -610,3 +610,23 @@ def test_patch_embedding_matches_conv_fp32(layout, path, monkeypatch):
     assert conv.weight.grad.shape == ref.weight.grad.shape
     assert nrmerr(conv.weight.grad, ref.weight.grad) < 1e-2
     assert nrmerr(conv.bias.grad, ref.bias.grad) < 1e-2
+
+
+def test_embed_tokens_matches_cat_add():
+    """Token assembly ([cls; tok] + pos in one pass) vs torch.cat + add in fp32: values and
+    the gradients of the tokens, the class token and the position embedding."""
+    torch.manual_seed(0)
+    B, N, D = 6, 196, 768
+    tok = torch.randn(B, N, D, device="cuda").to(torch.bfloat16).requires_grad_()
+    cls = (0.02 * torch.randn(1, 1, D, device="cuda")).requires_grad_()
+    pos = (0.02 * torch.randn(1, N + 1, D, device="cuda")).requires_grad_()
+    g = torch.randn(B, N + 1, D, device="cuda")
+    x = no.embed_tokens(tok, cls, pos)
+    gt, gc, gp = torch.autograd.grad(x, (tok, cls, pos), g.to(torch.bfloat16))
+    t32 = tok.detach().float().requires_grad_()
+    xr = torch.cat([cls.expand(B, -1, -1), t32], dim=1) + pos
+    rt, rc, rp = torch.autograd.grad(xr, (t32, cls, pos), g)
+    assert x.shape == (B, N + 1, D) and x.dtype == torch.bfloat16
+    assert nrmerr(x, xr) < 5e-3
+    assert nrmerr(gt, rt) < 5e-3 and nrmerr(gc, rc) < 5e-3 and nrmerr(gp, rp) < 5e-3
+    assert gc.shape == cls.shape and gp.shape == pos.shape
