@@ -231,7 +231,7 @@ __global__ void __launch_bounds__(256) gelu_dual_cast_kernel(const u16* __restri
     }
 #pragma unroll
     for (int e = 0; e < 8; ++e) m = fmaxf(m, fabsf(g[e]));
-    *reinterpret_cast<u32x4*>(aux + base) = dq;
+    if (aux != nullptr) *reinterpret_cast<u32x4*>(aux + base) = dq;
     if (a_out != nullptr) *reinterpret_cast<u32x4*>(a_out + base) = gq;
     uint2 o;
     o.x = cvt4<FMT>(g[0] * s, g[1] * s, g[2] * s, g[3] * s);
@@ -414,11 +414,12 @@ PDT_API int pdt_cast_fp8_delayed(const void* x, int bf16, long n, float* meta, i
   PDT_RETURN_LAUNCH();
 }
 
-// y [n] bf16 -> aux = gelu'(y), q = fp8 codes of gelu(y) (delayed scale, history rolled, dq_out =
-// this cast's dequant factor), a_out = gelu(y) if given (may be y itself)
+// y [n] bf16 -> aux = gelu'(y) if given, q = fp8 codes of gelu(y) (delayed scale, history rolled,
+// dq_out = this cast's dequant factor), a_out = gelu(y) if given (may be y itself). Without aux the
+// caller keeps y itself (the pre-activation) for the backward's act-3 epilogue.
 PDT_API int pdt_gelu_dual_cast_fp8(const void* y, long n, float* meta, int fmt, void* q, void* aux, void* a_out,
                                    float* dq_out, hipStream_t st) {
-  if (n % 8 != 0 || !y || !meta || !q || !aux) return -1;
+  if (n % 8 != 0 || !y || !meta || !q) return -1;
   const int nb = nblocks(n);
   const u16* Y = (const u16*)y;
   if (fmt == 0) {

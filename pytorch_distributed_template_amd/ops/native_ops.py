@@ -2456,14 +2456,22 @@ def _fc1_lib(M, Hd, K) -> bool:
 
 
 def _fc1_lib_forward(xq, w1q, a, z, aq, dqx, dqw1, bias1, meta, keep_a):
-    """a <- x W1^T + b1 (library GEMM), then z <- gelu'(a), aq <- e4m3(gelu(a)), and (keep_a) a <- gelu(a)
-    in place. Returns the codes' dequant factor (device [1])."""
+    """a <- x W1^T + b1 (library GEMM), then z <- gelu'(a) (z None: not formed -- the caller keeps
+    the pre-activation a), aq <- e4m3(gelu(a)), and (keep_a) a <- gelu(a) in place. Returns the
+    codes' dequant factor (device [1])."""
     lib = _load()
     dqa = torch.empty(1, dtype=torch.float32, device=a.device)
     _gemm_f8_lib(xq, w1q, a, dqx, dqw1, E4M3, bias1)
-    _chk(lib.pdt_gelu_dual_cast_fp8(_p(a), a.numel(), _p(meta), E4M3, _p(aq), _p(z), _p(a) if keep_a else None,
-                                    _p(dqa), _s()), "gelu_dual_cast_fp8")
+    _chk(lib.pdt_gelu_dual_cast_fp8(_p(a), a.numel(), _p(meta), E4M3, _p(aq), _p(z) if z is not None else None,
+                                    _p(a) if keep_a else None, _p(dqa), _s()), "gelu_dual_cast_fp8")
     return dqa
+
+
+def _fc1_keep_pre() -> bool:
+    """Library fc1 with fp8 weight gradients: keep the GEMM's own pre-activation output for the
+    backward (whose fc2 data-gradient epilogue then forms gelu'(z) itself, act 3) instead of
+    writing gelu'(z) in the cast pass -- one bf16 [M, 4D] store fewer per block."""
+    return os.environ.get("PDT_FC1_KEEP_PRE", "1") == "1"
 
 
 def gemm_f8(a, b, out, dq_a, dq_b, *, fmt_a=E4M3, bias=None, act=0, aux=None, addend=None, variant=None,
@@ -2756,8 +2764,8 @@ class _Mlp(torch.autograd.Function):
         Mrows, K = x2.shape
         Hd, Nout = w1.shape[0], w2.shape[0]
         dev = x.device
-        z = torch.empty((Mrows, Hd), dtype=torch.bfloat16, device=dev)
-        a = torch.empty_like(z)
+        a = torch.empty((Mrows, Hd), dtype=torch.bfloat16, device=dev)
+        z = None
         out = torch.empty((Mrows, Nout), dtype=torch.bfloat16, device=dev)
         res = _residual2d(residual, Mrows, Nout)
         bias1, bias2 = b1.float().contiguous(), b2.float().contiguous()
@@ -2765,6 +2773,7 @@ class _Mlp(torch.autograd.Function):
         f8w = fp8 and cfg["dgrad"] and cfg["wgrad"]
         dual = _gelu_dual()
         act1 = ACT_GELU_DUAL if dual else ACT["gelu"]  # z holds gelu'(fc1 pre-activation) when dual
+        act2 = ACT_MUL if dual else ACT_GELU_GRAD      # the fc2 data gradient's epilogue
         if fp8:
             pre = _prequant(x, mlp.fc1)
             xq, dqx = pre if pre is not None else _quant_act(x2, mlp.fc1)
@@ -2774,18 +2783,25 @@ class _Mlp(torch.autograd.Function):
                 aq = torch.empty((Mrows, Hd), dtype=torch.uint8, device=dev)
                 dqa = None
                 if dual and _fc1_lib(Mrows, Hd, K):
+                    pre = f8w and _fc1_keep_pre()
+                    z = None if pre else torch.empty_like(a)
                     try:
                         dqa = _fc1_lib_forward(xq, w1q, a, z, aq, dqx, dqw1, bias1, meta2, keep_a=not f8w)
+                        if pre:  # a holds the pre-activation (its gelu lives only as the e4m3 codes)
+                            z, act2 = a, ACT_GELU_GRAD
                     except RuntimeError as e:  # (see gemm_f8: the native tiles from here on)
                         _F8_LIB_BROKEN.append(str(e))
                 if dqa is None:
+                    z = torch.empty_like(a)
                     dqa = gemm_f8(xq, w1q, a, dqx, dqw1, bias=bias1, act=act1, aux=z, q8=(aq, meta2, E4M3, f8w))
             else:
+                z = torch.empty_like(a)
                 gemm_f8(xq, w1q, a, dqx, dqw1, bias=bias1, act=act1, aux=z)
                 aq, dqa = _quant_act(a, mlp.fc2)
             w2q, _, dqw2 = fp8_weight(w2)
             gemm_f8(aq, w2q, out, dqa, dqw2, bias=bias2, addend=res)
         else:
+            z = torch.empty_like(a)
             _gemm_bf16(x2, bf16_weight(w1), a, bias=bias1, act=act1, aux=z)
             _gemm_bf16(a, bf16_weight(w2), out, bias=bias2, addend=res)
         if f8w:  # fp8 weight gradients: the e4m3 GEMM inputs replace the bf16 ones in the saved state
@@ -2795,7 +2811,7 @@ class _Mlp(torch.autograd.Function):
             ctx.f8 = None
             ctx.save_for_backward(x2, a, z, w1, w2)
         ctx.shp, ctx.fp8, ctx.mlp = shp, fp8, mlp
-        ctx.act2 = ACT_MUL if dual else ACT_GELU_GRAD  # the fc2 data gradient's epilogue
+        ctx.act2 = act2
         ctx.fp8_dgrad = fp8 and cfg["dgrad"]
         return out.reshape(*shp[:-1], Nout)
 
