@@ -251,10 +251,14 @@ __global__ void __launch_bounds__(256) gelu_dual_cast_kernel(const u16* __restri
 // (the producing nn.Linear's bias gradient) from the bf16 values it reads anyway: block b owns
 // rows [b * rpb, (b + 1) * rpb), a thread owns 8-column chunks (every chunk of the band is one
 // thread's, so no in-block combine) -> cpart[b][cols]. cols % 8 == 0.
-template <int FMT>
+// GG: x is a GEMM's (g W) and zz the GELU pre-activation of the same shape -- the values cast
+// and summed are x * gelu'(zz) (the MLP fc1 output gradient, when the fc2 data gradient runs on
+// the library GEMM without the act-3 epilogue).
+template <int FMT, bool GG = false>
 __global__ void __launch_bounds__(1024) cast_fp8_delayed_cs_kernel(const u16* __restrict__ x, int rows, int cols,
                                                                    int rpb, float* __restrict__ meta,
-                                                                   uint8_t* __restrict__ q, float* __restrict__ cpart) {
+                                                                   uint8_t* __restrict__ q, float* __restrict__ cpart,
+                                                                   const u16* __restrict__ zz = nullptr) {
   __shared__ float red[16];
   const float s = meta[0];
   const int c8n = cols / 8;
@@ -263,12 +267,22 @@ __global__ void __launch_bounds__(1024) cast_fp8_delayed_cs_kernel(const u16* __
   for (int c8 = threadIdx.x; c8 < c8n; c8 += blockDim.x) {  // (one trip when cols <= 8 * blockDim)
     float cs[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
     int r = r0;
-    auto row = [&](const u32x4& w, long base) __attribute__((always_inline)) {
+    auto row = [&](const u32x4& w, const u32x4& zw, long base) __attribute__((always_inline)) {
       float v[8];
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
         v[2 * e] = lo_bf(w[e]);
         v[2 * e + 1] = hi_bf(w[e]);
+      }
+      if constexpr (GG) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          float g0, g1, d0, d1;
+          pdt_gelu_dual(lo_bf(zw[e]), g0, d0);
+          pdt_gelu_dual(hi_bf(zw[e]), g1, d1);
+          v[2 * e] *= d0;
+          v[2 * e + 1] *= d1;
+        }
       }
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
@@ -281,13 +295,21 @@ __global__ void __launch_bounds__(1024) cast_fp8_delayed_cs_kernel(const u16* __
       *reinterpret_cast<uint2*>(q + base) = o;
     };
     for (; r + 3 < r1; r += 4) {  // four rows' loads in flight before any is used
-      u32x4 w[4];
+      u32x4 w[4], zw[4];
 #pragma unroll
-      for (int u = 0; u < 4; ++u) w[u] = *reinterpret_cast<const u32x4*>(x + (long)(r + u) * cols + c8 * 8);
+      for (int u = 0; u < 4; ++u) {
+        w[u] = *reinterpret_cast<const u32x4*>(x + (long)(r + u) * cols + c8 * 8);
+        if constexpr (GG) zw[u] = *reinterpret_cast<const u32x4*>(zz + (long)(r + u) * cols + c8 * 8);
+      }
 #pragma unroll
-      for (int u = 0; u < 4; ++u) row(w[u], (long)(r + u) * cols + c8 * 8);
+      for (int u = 0; u < 4; ++u) row(w[u], zw[u], (long)(r + u) * cols + c8 * 8);
     }
-    for (; r < r1; ++r) row(*reinterpret_cast<const u32x4*>(x + (long)r * cols + c8 * 8), (long)r * cols + c8 * 8);
+    for (; r < r1; ++r) {
+      const long base = (long)r * cols + c8 * 8;
+      u32x4 zw{};
+      if constexpr (GG) zw = *reinterpret_cast<const u32x4*>(zz + base);
+      row(*reinterpret_cast<const u32x4*>(x + base), zw, base);
+    }
     float* cp = cpart + (long)blockIdx.x * cols + c8 * 8;
     *reinterpret_cast<f32x4*>(cp) = f32x4{cs[0], cs[1], cs[2], cs[3]};
     *reinterpret_cast<f32x4*>(cp + 4) = f32x4{cs[4], cs[5], cs[6], cs[7]};
@@ -462,6 +484,28 @@ PDT_API int pdt_cast_fp8_delayed_cs(const void* x, int rows, int cols, float* me
   else
     hipLaunchKernelGGL(cast_fp8_delayed_cs_kernel<1>, dim3(nb), dim3(nt), 0, st, X, rows, cols, rpb, meta,
                        (uint8_t*)q, cpart);
+  if (fmt == 0) hipLaunchKernelGGL(fp8_meta_roll_kernel<0>, dim3(1), dim3(64), 0, st, meta, dq_out);
+  else hipLaunchKernelGGL(fp8_meta_roll_kernel<1>, dim3(1), dim3(64), 0, st, meta, dq_out);
+  const int e = (int)hipGetLastError();
+  if (e) return e;
+  return pdt_wgrad_reduce_rows(cpart, bias_out, nb, cols, 1.f, 0, cpart + (long)nb * cols, st);
+}
+
+// pdt_cast_fp8_delayed_cs of x * gelu'(z) (x, z bf16 [rows][cols]): the MLP fc1 output gradient
+// from the fc2 data gradient's plain GEMM output, cast + bias sums in the same pass
+PDT_API int pdt_cast_fp8_gelu_grad_cs(const void* x, const void* z, int rows, int cols, float* meta, int fmt,
+                                      void* q, float* dq_out, float* cpart, float* bias_out, hipStream_t st) {
+  if (cols % 8 != 0 || rows < 1 || !z || !cpart || !bias_out) return -1;
+  const int nb = pdt_cast_cs_bands(rows);
+  const int rpb = (rows + nb - 1) / nb;
+  int nt = ((cols / 8 + 63) / 64) * 64;
+  if (nt > 1024) nt = 1024;
+  if (fmt == 0)
+    hipLaunchKernelGGL((cast_fp8_delayed_cs_kernel<0, true>), dim3(nb), dim3(nt), 0, st, (const u16*)x, rows, cols,
+                       rpb, meta, (uint8_t*)q, cpart, (const u16*)z);
+  else
+    hipLaunchKernelGGL((cast_fp8_delayed_cs_kernel<1, true>), dim3(nb), dim3(nt), 0, st, (const u16*)x, rows, cols,
+                       rpb, meta, (uint8_t*)q, cpart, (const u16*)z);
   if (fmt == 0) hipLaunchKernelGGL(fp8_meta_roll_kernel<0>, dim3(1), dim3(64), 0, st, meta, dq_out);
   else hipLaunchKernelGGL(fp8_meta_roll_kernel<1>, dim3(1), dim3(64), 0, st, meta, dq_out);
   const int e = (int)hipGetLastError();

@@ -120,6 +120,7 @@ _SIGS = {
     "pdt_attn_set_bwd_single": (c_int, [c_int]),
     "pdt_gemm_f8_num_variants": (c_int, []),
     "pdt_gelu_dual_cast_fp8": (c_int, [P, c_long, P, c_int, P, P, P, P, P]),
+    "pdt_cast_fp8_gelu_grad_cs": (c_int, [P, P, c_int, c_int, P, c_int, P, P, P, P, P]),
     "pdt_gemm_f8": (c_int, [P, P, P, P, P, P] + [c_int] * 8 + [P, P, c_int, P]),
     "pdt_bn_set_unroll": (c_int, [c_int]),
     "pdt_amax_blocks": (c_int, [c_long]),
@@ -2467,6 +2468,29 @@ def _fc1_lib_forward(xq, w1q, a, z, aq, dqx, dqw1, bias1, meta, keep_a):
     return dqa
 
 
+def _fc2_dgrad_lib_on() -> bool:
+    """The MLP's fc2 data gradient as the plain library GEMM (bf16 g W2) followed by one pass that
+    multiplies by gelu'(z), casts to e5m2 and sums fc1's bias gradient
+    (pdt_cast_fp8_gelu_grad_cs), instead of the native GEMM with that epilogue (act 3 + e5m2 +
+    column sums). PDT_FC2_DGRAD_LIB=0 turns it off."""
+    return not _F8_LIB_BROKEN and hasattr(torch, "_scaled_mm") and os.environ.get("PDT_FP8_LIB", "1") == "1" \
+        and os.environ.get("PDT_FC2_DGRAD_LIB", "1") == "1"
+
+
+def _fc2_dgrad_lib(gq, w2qt, dz, dqg, dqw2, z, dzq, gmeta, db):
+    """dz <- g W2 (library), then dzq <- e5m2(dz * gelu'(z)) and db <- column sums of dz * gelu'(z).
+    Returns the codes' dequant factor (device [1])."""
+    lib = _load()
+    rows, cols = dz.shape
+    _gemm_f8_lib(gq, w2qt, dz, dqg, dqw2, E5M2, None)
+    nb = lib.pdt_cast_cs_bands(rows)
+    cpart = torch.empty(nb * cols + lib.pdt_reduce_rows_work(nb, cols), dtype=torch.float32, device=dz.device)
+    dq = torch.empty(1, dtype=torch.float32, device=dz.device)
+    _chk(lib.pdt_cast_fp8_gelu_grad_cs(_p(dz), _p(z), rows, cols, _p(gmeta), E5M2, _p(dzq), _p(dq), _p(cpart),
+                                       _p(db), _s()), "cast_fp8_gelu_grad_cs")
+    return dq
+
+
 def _fc1_keep_pre() -> bool:
     """Library fc1 with fp8 weight gradients: keep the GEMM's own pre-activation output for the
     backward (whose fc2 data-gradient epilogue then forms gelu'(z) itself, act 3) instead of
@@ -2837,8 +2861,14 @@ class _Mlp(torch.autograd.Function):
                     # fc1's bias gradient = column sums of dz formed in this epilogue: the bf16 dz
                     # (only ever read for it) is not written at all
                     pre_db1 = _grad_buf(ctx.brefs[0], (Hd,))
-                    dqdz = gemm_f8(gq, w2qt, dz, dqg, dqw2, fmt_a=E5M2, act=ctx.act2, addend=z,
-                                   q8=(dzq, gmeta1, E5M2, True), colsum_out=pre_db1)
+                    if ctx.act2 == ACT_GELU_GRAD and _fc2_dgrad_lib_on():  # z: the pre-activation
+                        try:
+                            dqdz = _fc2_dgrad_lib(gq, w2qt, dz, dqg, dqw2, z, dzq, gmeta1, pre_db1)
+                        except RuntimeError as e:  # (see gemm_f8: the native tiles from here on)
+                            _F8_LIB_BROKEN.append(str(e))
+                    if dqdz is None:
+                        dqdz = gemm_f8(gq, w2qt, dz, dqg, dqw2, fmt_a=E5M2, act=ctx.act2, addend=z,
+                                       q8=(dzq, gmeta1, E5M2, True), colsum_out=pre_db1)
                 else:
                     dqdz = gemm_f8(gq, w2qt, dz, dqg, dqw2, fmt_a=E5M2, act=ctx.act2, addend=z,
                                    q8=(dzq, gmeta1, E5M2, False))

@@ -333,18 +333,22 @@ def test_vit_fp8_steps_track_torch_fp32():
     assert m.blocks[0].attn.qkv._pdt_fp8_meta is not None and m.blocks[0].mlp.fc2._pdt_fp8_gmeta is not None
 
 
-@pytest.mark.parametrize("mode", ["bf16", "fp8", "fp8_lib", "fp8_lib_aux", "bf16_nodual", "fp8_nodual"])
+@pytest.mark.parametrize("mode", ["bf16", "fp8", "fp8_lib", "fp8_lib_natdgrad", "fp8_lib_aux", "bf16_nodual",
+                                  "fp8_nodual"])
 def test_fused_mlp_node(mode, monkeypatch):
     """The MLP node vs fp32 autograd. fp8: delayed scaling, so a first step seeds the amax
     histories and the checked step runs the fused fc1 epilogue (act 4 + e4m3 side output);
     fp8_lib: fc1 on the library GEMM + pdt_gelu_dual_cast_fp8 keeping the GEMM's pre-activation
     (the fc2 data gradient forms gelu'(z), act 3); fp8_lib_aux: the cast pass writes gelu'(z)
-    (act 5); *_nodual: z stored, gelu'(z) recomputed in the fc2 data-gradient epilogue (acts 2 / 3)."""
+    (act 5); fp8_lib runs the fc2 data gradient on the library GEMM + the gelu'-multiplying e5m2
+    cast with bias sums, fp8_lib_natdgrad on the native tile's act-3 epilogue; *_nodual: z
+    stored, gelu'(z) recomputed in the fc2 data-gradient epilogue (acts 2 / 3)."""
     from pytorch_distributed_template_amd.models.vit import Mlp
     fp8 = mode.startswith("fp8")
     monkeypatch.setenv("PDT_GELU_DUAL", "0" if mode.endswith("nodual") else "1")
     monkeypatch.setenv("PDT_FP8_FC1_LIB", "1" if mode.startswith("fp8_lib") else "0")
     monkeypatch.setenv("PDT_FC1_KEEP_PRE", "0" if mode == "fp8_lib_aux" else "1")
+    monkeypatch.setenv("PDT_FC2_DGRAD_LIB", "0" if mode == "fp8_lib_natdgrad" else "1")
     torch.manual_seed(24)
     m = Mlp(768, 3072).cuda()
     x = torch.randn(4, 197, 768, device="cuda").to(torch.bfloat16).requires_grad_(True)
