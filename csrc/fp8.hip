@@ -11,6 +11,8 @@
 // The conversions are the gfx950 packed converts v_cvt_pk_fp8_f32 /
 // v_cvt_pk_bf8_f32 (round to nearest even); inputs are clamped to the format's
 // finite range first, so nothing overflows to NaN.
+#include <cstdlib>
+
 #include "pdt_common.h"
 
 namespace {
@@ -46,7 +48,7 @@ __global__ void __launch_bounds__(256) amax_partial_kernel(const void* __restric
 
 // amax from the partials; every thread of the block gets it
 __device__ __forceinline__ float block_amax(const float* __restrict__ partial, int nblk) {
-  __shared__ float red[4];
+  __shared__ float red[16];  // up to 1024 threads
   float m = 0.f, m1 = 0.f, m2 = 0.f, m3 = 0.f;
   const int B = blockDim.x;
   int i = threadIdx.x;
@@ -62,7 +64,9 @@ __device__ __forceinline__ float block_amax(const float* __restrict__ partial, i
   __syncthreads();
   if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = m;
   __syncthreads();
-  return fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
+  float r = red[0];
+  for (int w = 1; w < (B + 63) / 64; ++w) r = fmaxf(r, red[w]);
+  return r;
 }
 
 template <int FMT>
@@ -349,7 +353,7 @@ __global__ void fp8_meta_roll_kernel(float* __restrict__ meta, float* __restrict
 // the same roll for a producer kernel that wrote per-block amax partials instead of
 // the atomicMax slot (the LayerNorm forward's fused fp8 output)
 template <int FMT>
-__global__ void __launch_bounds__(256) fp8_meta_roll_part_kernel(float* __restrict__ meta,
+__global__ void __launch_bounds__(1024) fp8_meta_roll_part_kernel(float* __restrict__ meta,
                                                                 const float* __restrict__ partial, int nblk,
                                                                 float* __restrict__ dq_out) {
   const float a = block_amax(partial, nblk);
@@ -513,13 +517,26 @@ PDT_API int pdt_cast_fp8_gelu_grad_cs(const void* x, const void* z, int rows, in
   return pdt_wgrad_reduce_rows(cpart, bias_out, nb, cols, 1.f, 0, cpart + (long)nb * cols, st);
 }
 
+// threads of the one-block partial-amax roll: 1024 for the long partial lists of the LayerNorm
+// forward (a 256-thread block walked them in ~24 us); PDT_ROLL_NT overrides (256 / 512 / 1024)
+static int roll_threads(int nblk) {
+  static const int nt = [] {
+    const char* e = getenv("PDT_ROLL_NT");
+    const int v = e ? atoi(e) : 1024;
+    return (v == 256 || v == 512) ? v : 1024;
+  }();
+  return nblk <= 1024 ? 256 : nt;
+}
+
 // roll after a fused producer (pdt_ln_fwd_f8): partial[nblk] holds its per-block amaxes
 PDT_API int pdt_fp8_meta_roll_partial(float* meta, const float* partial, int nblk, int fmt, float* dq_out,
                                       hipStream_t st) {
   if (fmt == 0)
-    hipLaunchKernelGGL(fp8_meta_roll_part_kernel<0>, dim3(1), dim3(256), 0, st, meta, partial, nblk, dq_out);
+    hipLaunchKernelGGL(fp8_meta_roll_part_kernel<0>, dim3(1), dim3(roll_threads(nblk)), 0, st, meta, partial, nblk,
+                       dq_out);
   else
-    hipLaunchKernelGGL(fp8_meta_roll_part_kernel<1>, dim3(1), dim3(256), 0, st, meta, partial, nblk, dq_out);
+    hipLaunchKernelGGL(fp8_meta_roll_part_kernel<1>, dim3(1), dim3(roll_threads(nblk)), 0, st, meta, partial, nblk,
+                       dq_out);
   PDT_RETURN_LAUNCH();
 }
 
