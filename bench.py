@@ -70,6 +70,75 @@ STOCK_BEST_1GPU_IMG_S = {"resnet50": (6969.13, 2048), "resnet152": (2842.36, 204
 DEFAULT_BATCH = {"resnet50": 2048, "resnet152": 2560, "vit_b_16": 1024}
 # --graph: batches run eagerly and replayed (lr 0) before the timed run; losses must agree
 GRAPH_CHECK_STEPS = 3
+# --graph: relative difference allowed between the weight updates of one eager step and one
+# replay from the same state (atomics in the split-K reductions reorder fp32 sums; a doubled
+# or dropped gradient is a difference of ~0.5-1)
+GRAPH_UPDATE_TOL = 2e-2
+
+
+def _train_state(model, opt):
+    """Every tensor a training step mutates: parameters, buffers (BN running statistics),
+    the fp8 delayed-scaling states of the native ViT layers, optimizer state (momentum /
+    Adam moments), the fused optimizer's bf16 weight shadows and device [lr, t] scalars."""
+    ts = [p.detach() for p in model.parameters()] + list(model.buffers())
+    for m in model.modules():
+        for a in ("_pdt_fp8_meta", "_pdt_fp8_gmeta"):
+            if isinstance(getattr(m, a, None), torch.Tensor):
+                ts.append(getattr(m, a))
+    for st in opt.state.values():
+        ts += [v for v in st.values() if isinstance(v, torch.Tensor)]
+    ts += [v for v in getattr(opt, "_shadows", {}).values() if isinstance(v, torch.Tensor)]
+    ts += [v for v in getattr(opt, "_dev", {}).values() if isinstance(v, torch.Tensor)]
+    seen, out = set(), []
+    for t in ts:
+        if t.data_ptr() not in seen:
+            seen.add(t.data_ptr())
+            out.append(t)
+    return out
+
+
+class _UpdateCheck:
+    """The --graph preflight at the REAL lr: one eager step (before the capture, so the eager
+    activations are released before the graph's private pool is reserved) and one replay,
+    each from the same saved state on the same batch; ``rel`` = ||dW_eager - dW_replay|| /
+    ||dW_eager|| over all parameters. Every mutated tensor is restored after each."""
+
+    def __init__(self, model, opt, batch):
+        self.state = _train_state(model, opt)
+        self.saved = [t.clone() for t in self.state]
+        self.params = [p.detach() for p in model.parameters() if p.requires_grad]
+        self.p0 = [p.clone() for p in self.params]
+        self.batch = batch
+        self.de = None
+
+    @torch.no_grad()
+    def restore(self):
+        for t, s in zip(self.state, self.saved):
+            t.copy_(s)
+
+    def eager(self, side, gstep, sx, sy):
+        side.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(side):
+            sx.copy_(self.batch[0])
+            sy.copy_(self.batch[1])
+            gstep()
+        torch.cuda.current_stream().wait_stream(side)
+        with torch.no_grad():
+            self.de = [p - q for p, q in zip(self.params, self.p0)]
+        self.restore()
+        torch.cuda.synchronize()
+
+    @torch.no_grad()
+    def replay(self, graph, sx, sy) -> float:
+        self.restore()
+        sx.copy_(self.batch[0])
+        sy.copy_(self.batch[1])
+        graph.replay()
+        num = sum(float((p - q - d).double().pow(2).sum()) for p, q, d in zip(self.params, self.p0, self.de))
+        den = sum(float(d.double().pow(2).sum()) for d in self.de)
+        self.restore()
+        torch.cuda.synchronize()
+        return math.sqrt(num / den) if den > 0 else float("inf")
 
 
 def parse():
@@ -427,8 +496,12 @@ def main():
             sx = sbuf[:, :x0.shape[1]]
             sx.pdt_nhwc_pad = cp
 
+        static_slots = bool(getattr(model, "static_grad_slots", False))
+
         def gstep():
-            opt.zero_grad(set_to_none=False)
+            # fixed addresses for the capture: the reducer's bucket slots (gradients dropped,
+            # the kernels write the slots), else gradients kept allocated and zeroed in place
+            opt.zero_grad(set_to_none=static_slots)
             with torch.autocast(dev_type, dtype=torch.bfloat16, enabled=autocast):
                 out = model(sx)
                 loss = fused.softmax_cross_entropy(out, sy)
@@ -464,6 +537,13 @@ def main():
                 sy.copy_(yb)
                 eager_losses.append(gstep().detach().clone())
         torch.cuda.current_stream().wait_stream(side)
+        # the losses at lr 0 are blind to the gradient's SCALE (a doubled gradient gives the
+        # same loss): one eager step here and one replay after the capture, from the same
+        # state and batch at the real lr, must also move the weights by the same amount
+        set_lr(saved_lr)
+        upd = _UpdateCheck(model, opt, check_batches[0])
+        upd.eager(side, gstep, sx, sy)
+        set_lr([0.0] * len(saved_lr))
         # hand the warm-up's cached activation blocks back before the capture allocates the
         # graph's private pool: otherwise both stay reserved (2x the activations: ResNet-152
         # at 2048 images/GPU would not fit in 288 GB)
@@ -483,13 +563,16 @@ def main():
             graph.replay()
             graph_losses.append(static_loss.detach().clone())
         set_lr(saved_lr)
+        step_rel = upd.replay(graph, sx, sy)
+        del upd
         le = torch.stack(eager_losses).double().cpu()
         lg = torch.stack(graph_losses).double().cpu()
         rel = float(((le - lg).abs() / le.abs().clamp_min(1e-12)).max())
         graph_check = {"eager": [round(float(v), 6) for v in le], "replay": [round(float(v), 6) for v in lg],
-                       "max_rel_diff": rel}
+                       "max_rel_diff": rel, "param_update_rel_diff": step_rel}
         del check_batches
-        bad = not (torch.isfinite(le).all() and torch.isfinite(lg).all() and rel <= 1e-3)
+        bad = not (torch.isfinite(le).all() and torch.isfinite(lg).all() and rel <= 1e-3 and
+                   step_rel <= GRAPH_UPDATE_TOL)
 
         def step(i):  # noqa: F811
             xb, yb = next_batch(i)

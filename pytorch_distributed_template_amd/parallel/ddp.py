@@ -4,22 +4,28 @@ Reference: ``/root/reference/train.py:45-52`` wraps the model in
 ``DistributedDataParallel(device_ids=[local_rank], output_device=local_rank)``
 with the defaults (25 MiB buckets, ``broadcast_buffers=True``).
 
-Here the same DDP reducer (bucketed all-reduce issued from autograd hooks on
-RCCL's own HIP stream, overlapping the rest of backward) is configured for the
-MI355X node instead of NVSwitch defaults:
+``wrap_ddp`` picks one of two reducers:
 
-* ``bucket_cap_mb``: xGMI is a full mesh of 7 point-to-point links per GPU;
-  RCCL's ring/tree channels are per-link bound, so a handful of large buckets
-  keeps every channel streaming. Default 64 MiB for fp32 grads: ResNet-50's
-  97.5 MiB of gradients become 2 buckets (the tail bucket, issued when
-  backward finishes layer1/stem, is the only exposed one) instead of 5.
-* ``gradient_as_bucket_view=True``: gradients live inside the buckets -- no
-  per-step copy into/out of the flat buffers (saves 2x gradient bytes of HBM
-  traffic per step).
-* ``broadcast_buffers``: the reference broadcasts BN running stats from rank 0
-  every forward (its own comment says to remove it). Configurable; the
-  benchmark disables it (running stats are not used by training-mode BN).
-* ``comm_hook="bf16"``: optional bf16-compressed all-reduce (half the xGMI bytes).
+* ``impl="native"`` (the default on the native kernel backend): the framework's own
+  reducer, ``parallel/reducer.py`` -- the native weight-gradient kernels write straight
+  into 64-B-aligned bucket slots (no per-parameter copy kernels), ``ReduceOp.AVG``
+  all-reduces launched from post-accumulate-grad hooks on RCCL's stream while backward
+  continues, a small first bucket and a split last bucket (``docs/DDP_XGMI.md``);
+* ``impl="torch"`` (the default on the stock ``torch`` backend, i.e. the reference's
+  stack, and whenever a compression comm hook is asked for): torch's
+  ``DistributedDataParallel`` with ``gradient_as_bucket_view`` and the same bucket size.
+
+Either way the knobs are set for the MI355X node rather than NVSwitch defaults:
+
+* ``bucket_cap_mb``: xGMI is a full mesh of 7 point-to-point links per GPU; RCCL's
+  ring/tree channels are per-link bound, so a handful of large buckets keeps every
+  channel streaming. Default 64 MiB for fp32 grads.
+* ``broadcast_buffers``: the reference broadcasts BN running stats from rank 0 every
+  forward (its own comment says to remove it). Configurable; the benchmark disables it
+  (running stats are not used by training-mode BN).
+* ``comm_hook="bf16"``: optional bf16-compressed all-reduce (half the xGMI bytes; torch
+  DDP only).
+* ``PDT_DDP=native|torch`` overrides the choice (A/B runs).
 """
 from __future__ import annotations
 
@@ -46,14 +52,17 @@ def wrap_ddp(model: torch.nn.Module, device: torch.device, bucket_cap_mb: float 
     RCCL all-reduce then run at N = 1 exactly as at N > 1. Without a process group the model
     is returned unchanged.
 
-    ``impl``: ``"native"`` (default; ``PDT_DDP`` overrides) is the framework's reducer
-    (``parallel/reducer.py``: gradients written by the native kernels straight into aligned
-    bucket slots, ``ReduceOp.AVG`` all-reduce, a small first bucket); ``"torch"`` is torch's
-    ``DistributedDataParallel`` with the same bucket size (kept for A/B runs and for the
-    compression comm hooks, which only it implements)."""
+    ``impl``: ``"native"`` is the framework's reducer (``parallel/reducer.py``: gradients
+    written by the native kernels straight into aligned bucket slots, ``ReduceOp.AVG``
+    all-reduce, a small first bucket); ``"torch"`` is torch's ``DistributedDataParallel``
+    with the same bucket size -- the reference's wrapper, used by default on the stock
+    ``torch`` kernel backend (the reference-equivalent baseline) and for the compression
+    comm hooks, which only it implements. ``None``: ``PDT_DDP`` if set, else by backend."""
     if not is_dist_ready():
         return model
-    impl = impl or os.environ.get("PDT_DDP", "native")
+    if impl is None:
+        from ..ops import fused
+        impl = os.environ.get("PDT_DDP") or ("torch" if fused.get_backend() == "torch" else "native")
     if comm_hook in ("bf16", "fp16"):
         impl = "torch"
     if impl == "native":

@@ -20,7 +20,14 @@ What it does, per step:
   division launch at all. gloo has no AVG: sum, then one scale per bucket;
 * a callback queued on the autograd engine runs when backward finishes: buckets with a
   parameter that received no gradient get zeros in that slot and are reduced too (so an unused
-  parameter never hangs the job), then the compute stream waits for every bucket.
+  parameter never hangs the job), then the compute stream waits for every bucket. Such a
+  parameter's ``.grad`` becomes its reduced slot -- the other ranks' average when they used
+  it (torch DDP's ``find_unused_parameters=True`` behaviour for a locally unused parameter),
+  zeros when nobody did (torch DDP leaves ``None`` there, or errors with the reference's
+  ``find_unused_parameters=False``): a weight-decaying optimizer then still decays it.
+* a RETAINED gradient (``zero_grad(set_to_none=False)``, ``no_sync()``) is the slot itself;
+  the native kernels then write into a scratch buffer and autograd adds it into the slot
+  (``grad_out``), so accumulation sums as torch's does.
 
 Bucket sizes are chosen for MI355X's xGMI mesh, not NVSwitch: one ring all-reduce is bound
 by one ~153 GB/s link per direction and RCCL spreads channels over the 7 links, so a handful
@@ -79,10 +86,16 @@ def grad_slot(param: torch.Tensor) -> Optional[torch.Tensor]:
 
 
 def grad_out(param: torch.Tensor, *shape, memory_format=None) -> torch.Tensor:
-    """Output buffer for ``param``'s gradient: its reducer slot when there is one (and the
-    requested layout is the parameter's), else a new fp32 tensor of ``shape``."""
+    """Output buffer for ``param``'s gradient: its reducer slot when there is one, the requested
+    layout is the parameter's AND ``param.grad`` is None; else a new fp32 tensor of ``shape``.
+
+    The ``param.grad is None`` condition is what keeps accumulation right: a retained
+    gradient (``zero_grad(set_to_none=False)``, ``no_sync()`` micro-batches) already IS the
+    slot, and autograd's AccumulateGrad will add whatever the backward returns into it --
+    handing out the slot there would overwrite the retained value with g and then add g to
+    itself (2g). With a separate buffer AccumulateGrad computes ``slot += g`` in place."""
     s = grad_slot(param)
-    if s is not None and tuple(s.shape) == tuple(shape or param.shape) and \
+    if s is not None and param.grad is None and tuple(s.shape) == tuple(shape or param.shape) and \
             (memory_format is None or s.is_contiguous(memory_format=memory_format)):
         return s
     shape = shape or tuple(param.shape)
@@ -124,6 +137,10 @@ class DataParallel(torch.nn.Module):
     """Data-parallel wrapper over a process group (RCCL on GPUs, gloo on CPU): same contract as
     the torch DDP wrapper the reference uses -- ``.module``, forward passthrough, gradients
     averaged over the ranks when backward returns -- with the bucketing above."""
+
+    # every gradient ends in a fixed slot: a graph-captured step may drop the gradients
+    # (``zero_grad(set_to_none=True)``) and still see the same addresses on every replay
+    static_grad_slots = True
 
     def __init__(self, module: torch.nn.Module, device: torch.device | None = None, process_group=None,
                  bucket_cap_mb: float = 64.0, first_bucket_mb: float = 8.0, broadcast_buffers: bool = False,
@@ -180,6 +197,13 @@ class DataParallel(torch.nn.Module):
 
     # ------------------------------------------------------------------ forward
     def forward(self, *args, **kwargs):
+        if self._in_backward and torch.is_grad_enabled():
+            # the previous backward raised before its final callback (e.g. a caught OOM): the
+            # engine drops queued callbacks then, so the bucket state is reset here, as torch
+            # DDP prepares its reducer in forward
+            self._in_backward = False
+            for b in self.buckets:
+                b.ready, b.work, b.launched = 0, None, False
         if self.broadcast_buffers and self.world > 1:
             bufs = list(self.module.buffers())
             if bufs:

@@ -236,8 +236,11 @@ class Trainer(BaseTrainer):
 
     # ------------------------------------------------------------------ HIP graph
     def _step_body(self, data, target):
-        # grads stay allocated (set_to_none=False): the captured kernels write fixed addresses
-        self.optimizer.zero_grad(set_to_none=False)
+        # the captured kernels must write fixed addresses: under the framework's reducer every
+        # gradient lives in a fixed bucket slot anyway, so the gradients are dropped and the
+        # native kernels write the slots directly (no zero fill, no accumulate add); otherwise
+        # they stay allocated (set_to_none=False) and are zeroed in place
+        self.optimizer.zero_grad(set_to_none=bool(getattr(self.model, "static_grad_slots", False)))
         with self._autocast():
             output = self.model(data)
             loss = self.criterion(output, target)

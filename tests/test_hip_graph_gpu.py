@@ -120,25 +120,35 @@ def test_trainer_hip_graph_under_torchrun_ddp_rccl(tmp_path):
     """``trainer.hip_graph`` with DDP over a 1-rank RCCL group (torchrun): the reducer is
     built on the capture side stream, the RCCL watchdog is drained before the capture, the
     captured step (bucketed all-reduce included) is replayed, a scheduler changes the lr
-    between the epochs, checkpoints are written; then resume -> test."""
-    cfg = json.loads((ROOT / "config" / "resnet50_bf16.json").read_text())
-    cfg["trainer"].update(save_dir=str(tmp_path), len_epoch=14, epochs=2, monitor="off", save_period=2,
-                          hip_graph=True)
-    cfg["train_loader"]["args"].update(batch_size=16, num_samples=16 * 14)
-    cfg["lr_scheduler"] = {"type": "StepLR", "args": {"step_size": 1, "gamma": 0.5}}
+    between the epochs, checkpoints are written -- and the weights after 2 epochs equal those
+    of the same torchrun job stepped eagerly (a gradient the reducer doubled or dropped in
+    the captured step shows up here: the graph path keeps gradients across steps)."""
+    base = json.loads((ROOT / "config" / "resnet50_bf16.json").read_text())
+    base["trainer"].update(len_epoch=14, epochs=2, monitor="off", save_period=2)
+    base["train_loader"]["args"].update(batch_size=16, num_samples=16 * 14)
+    base["lr_scheduler"] = {"type": "StepLR", "args": {"step_size": 1, "gamma": 0.5}}
     for k in ("valid_loader", "test_loader"):
-        cfg[k]["args"].update(batch_size=16, num_samples=32)
-    p = tmp_path / "cfg.json"
-    p.write_text(json.dumps(cfg))
-    env = dict(os.environ, PYTHONPATH=str(ROOT), PDT_RUN_ID="gd", HSA_ENABLE_IPC_MODE_LEGACY="0")
-    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=1",
-           "--master-addr=127.0.0.1", f"--master-port={_free_port()}", "train.py", "-c", str(p), "--backend", "native"]
-    r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=900)
-    out = r.stdout + r.stderr
-    assert r.returncode == 0, out[-4000:]
-    assert "process group: nccl, world size 1" in out and "captured the training step as a HIP graph" in out, \
-        out[-3000:]
-    ck = tmp_path / cfg["name"] / "train" / "gd" / "checkpoint-epoch2.pth"
-    state = torch.load(ck, weights_only=True, map_location="cpu")
-    assert all(torch.isfinite(v).all() for v in state["state_dict"].values() if v.is_floating_point())
-    assert abs(state["optimizer"]["param_groups"][0]["lr"] - 0.1 * 0.25) < 1e-9  # two StepLR steps
+        base[k]["args"].update(batch_size=16, num_samples=32)
+    weights = {}
+    for mode in ("graph", "eager"):
+        cfg = json.loads(json.dumps(base))
+        cfg["trainer"].update(save_dir=str(tmp_path / mode), hip_graph=mode == "graph")
+        p = tmp_path / f"{mode}.json"
+        p.write_text(json.dumps(cfg))
+        env = dict(os.environ, PYTHONPATH=str(ROOT), PDT_RUN_ID=mode, HSA_ENABLE_IPC_MODE_LEGACY="0")
+        cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=1",
+               "--master-addr=127.0.0.1", f"--master-port={_free_port()}", "train.py", "-c", str(p),
+               "--backend", "native", "--seed", "0", "--deterministic"]
+        r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=900)
+        out = r.stdout + r.stderr
+        assert r.returncode == 0, out[-4000:]
+        assert "process group: nccl, world size 1" in out, out[-3000:]
+        assert ("captured the training step as a HIP graph" in out) == (mode == "graph"), out[-3000:]
+        ck = tmp_path / mode / cfg["name"] / "train" / mode / "checkpoint-epoch2.pth"
+        state = torch.load(ck, weights_only=True, map_location="cpu")
+        assert abs(state["optimizer"]["param_groups"][0]["lr"] - 0.1 * 0.25) < 1e-9  # two StepLR steps
+        weights[mode] = state["state_dict"]
+    for k, v in weights["eager"].items():
+        if v.is_floating_point():
+            assert torch.isfinite(weights["graph"][k]).all(), k
+            torch.testing.assert_close(weights["graph"][k].float(), v.float(), rtol=1e-3, atol=1e-4, msg=k)

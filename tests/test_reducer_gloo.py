@@ -88,6 +88,73 @@ def _w_reducer(rank, world, port, q):
         q.put((rank, repr(e) + traceback.format_exc()))
 
 
+def _w_accumulate(rank, world, port, q):
+    """Retained gradients: ``zero_grad(set_to_none=False)`` and ``no_sync`` micro-batches on
+    DIFFERENT batches must sum exactly as a single process does -- checked on the slot-written
+    ``w`` (the native-kernel path) as well as on the stock-op parameters."""
+    try:
+        pdist = _init(rank, world, port)
+        from pytorch_distributed_template_amd.parallel.reducer import DataParallel
+        torch.manual_seed(0)
+        model, ref = Net(), Net()
+        ref.load_state_dict(model.state_dict())
+        for m in (model, ref):
+            m.bn.eval()  # batch-independent normalisation: sums over micro-batches are exact
+        dp = DataParallel(model, torch.device("cpu"), bucket_cap_mb=0.0001, first_bucket_mb=0.00001)
+        torch.manual_seed(1)
+        batches = [(torch.randn(8, 3, 6, 6), torch.randint(0, 3, (8,))) for _ in range(3)]
+        shard = lambda b: (b[0][rank * 4:(rank + 1) * 4], b[1][rank * 4:(rank + 1) * 4])  # noqa: E731
+        ce = torch.nn.functional.cross_entropy
+
+        def ref_grads(bs):
+            for p in ref.parameters():
+                p.grad = None
+            for X, Y in bs:
+                (sum(ce(ref(X[r * 4:(r + 1) * 4]), Y[r * 4:(r + 1) * 4]) for r in range(world)) / world).backward()
+            return {n: p.grad.clone() for n, p in ref.named_parameters() if n != "unused"}
+
+        def diff(want):
+            return max(float((p.grad - want[n]).abs().max()) for n, p in model.named_parameters() if n != "unused")
+
+        out = {}
+        # (a) retained gradients zeroed in place between steps (the HIP-graph trainer's old path)
+        opt = torch.optim.SGD(model.parameters(), lr=0.0)
+        ce(dp(shard(batches[0])[0]), shard(batches[0])[1]).backward()
+        opt.zero_grad(set_to_none=False)
+        ce(dp(shard(batches[1])[0]), shard(batches[1])[1]).backward()
+        out["zero_inplace"] = diff(ref_grads([batches[1]]))
+        out["w_ratio"] = float(model.w.grad.norm() / ref.w.grad.norm())
+        # (b) no_sync accumulation over three different batches
+        for p in model.parameters():
+            p.grad = None
+        with dp.no_sync():
+            ce(dp(shard(batches[0])[0]), shard(batches[0])[1]).backward()
+            ce(dp(shard(batches[1])[0]), shard(batches[1])[1]).backward()
+        ce(dp(shard(batches[2])[0]), shard(batches[2])[1]).backward()
+        out["nosync"] = diff(ref_grads(batches))
+        # (c) a backward that raised before its final callback does not wedge the next step
+        dp._in_backward = True
+        for p in model.parameters():
+            p.grad = None
+        ce(dp(shard(batches[2])[0]), shard(batches[2])[1]).backward()
+        out["after_abort"] = diff(ref_grads([batches[2]]))
+        q.put((rank, out))
+        pdist.cleanup()
+    except Exception as e:  # pragma: no cover
+        import traceback
+        q.put((rank, repr(e) + traceback.format_exc()))
+
+
+def test_reducer_accumulates_into_retained_gradients():
+    res = _run(_w_accumulate)
+    for r in (0, 1):
+        o = res[r]
+        assert isinstance(o, dict), o
+        assert o["zero_inplace"] < 1e-6 and abs(o["w_ratio"] - 1) < 1e-6, o
+        assert o["nosync"] < 1e-6, o
+        assert o["after_abort"] < 1e-6, o
+
+
 def test_reducer_matches_single_process_and_uses_slots():
     res = _run(_w_reducer)
     for r in (0, 1):
