@@ -545,9 +545,12 @@ namespace {
 // per SIMD): per K-tile a CU's fragment reads fall from 192 KB (8 waves of 128x64) to 128 KB
 // -- the fp8 MFMA consumes twice the bytes per cycle of the bf16 one, so the LDS read
 // bandwidth, not the matrix core, bounds the 8-wave tile.
-constexpr int NVAR_F8 = 12;
-constexpr int VAR_F8_BM[NVAR_F8] = {128, 128, 256, 128, 64, 128, 256, 128, 256, 128, 256, 256};
-constexpr int VAR_F8_BN[NVAR_F8] = {128, 128, 128, 256, 128, 64, 64, 128, 128, 256, 256, 256};
+// ids 12 / 13: the dense 256x256 ping-pong ring (csrc/gemm_ring.hip, tile groupings GM 4 / 8)
+// for the plain GEMMs (optional bias, no activation / aux / addend / fp8 side output)
+constexpr int NVAR_F8 = 14;
+constexpr int F8_RING0 = 12;
+constexpr int VAR_F8_BM[NVAR_F8] = {128, 128, 256, 128, 64, 128, 256, 128, 256, 128, 256, 256, 256, 256};
+constexpr int VAR_F8_BN[NVAR_F8] = {128, 128, 128, 256, 128, 64, 64, 128, 128, 256, 256, 256, 256, 256};
 
 template <int F8>
 int launch_f8(int v, const NTParams& p, hipStream_t st) {
@@ -571,12 +574,21 @@ int launch_f8(int v, const NTParams& p, hipStream_t st) {
 
 PDT_API int pdt_gemm_f8_num_variants() { return NVAR_F8; }
 
+PDT_API int pdt_gemm_ring(const void* a, const void* b, void* c, const float* bias, const float* dq_a,
+                          const float* dq_b, int M, int N, int K, int lda, int ldb, int ldc, int dt, int sub,
+                          hipStream_t st);
+
 static int gemm_f8_impl(const void* a, const void* b, void* out, const float* bias, const float* dq_a,
                         const float* dq_b, int M, int N, int K, int lda, int ldb, int ldo, int fmt_a, int act,
                         void* aux, const void* addend, int variant, void* q8, float* q8_meta, float* q8_part,
                         int q8_fmt, int q8_only, float* q8_dq, hipStream_t stream, float* colsum = nullptr) {
   if (K % 128 != 0 || lda % 16 != 0 || ldb % 16 != 0 || N % 8 != 0 || ldo % 8 != 0) return -1;
   if (lda != K) return -2;  // rows of A are dense (the gather's source row stride is Cs)
+  if (variant >= F8_RING0 && variant < NVAR_F8) {  // the plain-epilogue dense ring
+    if (act != 0 || aux != nullptr || addend != nullptr || q8 != nullptr || colsum != nullptr) return -5;
+    return pdt_gemm_ring(a, b, out, bias, dq_a, dq_b, M, N, K, lda, ldb, ldo, fmt_a == 1 ? 2 : 1,
+                         variant - F8_RING0, stream);
+  }
   NTParams p;
   p.src = (const u16*)a;
   p.b = (const u16*)b;

@@ -479,6 +479,16 @@ def _restore_fp8_meta(snap):
 NOT_APPLICABLE = -5  # kernel return code: this variant cannot run this geometry
 
 
+class NotApplicable(RuntimeError):
+    """An explicitly requested kernel variant cannot run this geometry / epilogue."""
+
+
+def _chk_v(rc, name):
+    if rc == NOT_APPLICABLE:
+        raise NotApplicable(f"{name}: variant not applicable")
+    _chk(rc, name)
+
+
 def _time_variants(nvar, launch, allowed=None):
     """Fastest variant id: one warm launch each, then two interleaved rounds over all
     variants of a 3-launch HIP-event trial, best trial per variant (interleaving keeps a
@@ -2404,16 +2414,21 @@ def fp8_weight(w: torch.Tensor):
 
 # Tuned-table id of the library path for PLAIN fp8 GEMMs (no activation / aux / addend / fp8
 # side output; bias allowed, added in bf16): hipBLASLt through torch._scaled_mm with the
-# device dequant scales as its scale operands (no host sync). On the ViT-B/16 batch-1024
-# data-gradient shapes and the qkv projection it measured 1.16-1.42x the native ring tiles
-# (profiles/vit_fp8_gemm_library_round4.txt); every fused-epilogue GEMM stays native.
+# device dequant scales as its scale operands (no host sync). OFF by default: every fp8 GEMM
+# of the framework runs on its own CDNA4 tiles; ``PDT_FP8_LIB=1`` enables the library path as
+# an A/B reference (it measured 1.16-1.42x the round-4 native ring tiles on the ViT-B/16
+# batch-1024 data-gradient shapes, profiles/vit_fp8_gemm_library_round4.txt).
 F8_LIB = 100
+
+
+def _fp8_lib_enabled() -> bool:
+    return os.environ.get("PDT_FP8_LIB", "0") == "1"
 _F8_LIB_BROKEN: list = []  # set once torch._scaled_mm refused a call: every library id runs native
 
 
 def _f8_lib_ok(out, act, aux, addend, q8) -> bool:
     return act == 0 and aux is None and addend is None and q8 is None and out.is_contiguous() and \
-        hasattr(torch, "_scaled_mm") and os.environ.get("PDT_FP8_LIB", "1") == "1"
+        hasattr(torch, "_scaled_mm") and _fp8_lib_enabled()
 
 
 _BIAS16: dict = {}
@@ -2453,7 +2468,7 @@ def _fc1_lib(M, Hd, K) -> bool:
     if env is not None:
         return env == "1" and hasattr(torch, "_scaled_mm")
     return bool(_tuned().get(f"fc1lib:{M},{Hd},{K}", 0)) and hasattr(torch, "_scaled_mm") and \
-        os.environ.get("PDT_FP8_LIB", "1") == "1"
+        _fp8_lib_enabled()
 
 
 def _fc1_lib_forward(xq, w1q, a, z, aq, dqx, dqw1, bias1, meta, keep_a):
@@ -2473,7 +2488,7 @@ def _fc2_dgrad_lib_on() -> bool:
     multiplies by gelu'(z), casts to e5m2 and sums fc1's bias gradient
     (pdt_cast_fp8_gelu_grad_cs), instead of the native GEMM with that epilogue (act 3 + e5m2 +
     column sums). PDT_FC2_DGRAD_LIB=0 turns it off."""
-    return not _F8_LIB_BROKEN and hasattr(torch, "_scaled_mm") and os.environ.get("PDT_FP8_LIB", "1") == "1" \
+    return not _F8_LIB_BROKEN and hasattr(torch, "_scaled_mm") and _fp8_lib_enabled() \
         and os.environ.get("PDT_FC2_DGRAD_LIB", "1") == "1"
 
 
@@ -2525,6 +2540,8 @@ def gemm_f8(a, b, out, dq_a, dq_b, *, fmt_a=E4M3, bias=None, act=0, aux=None, ad
             key = f"f8b:{M},{N},{K},{fmt_a},{act},{int(bias is not None)}" + (",r" if addend is not None and act == 0
                                                                                else "")
             nv = lib.pdt_gemm_f8_num_variants()
+            if not lib_ok and int(_tuned().get(key, -1)) == F8_LIB:
+                key += ",nat"  # the table chose the (now disabled) library path: the best native tile
             # candidate nv (tuning only) = the library path, stored as F8_LIB
             run = lambda v: lib.pdt_gemm_f8(*args(v)) if v < nv else _gemm_f8_lib(a, b, out, dq_a, dq_b,  # noqa
                                                                                   fmt_a, bias)
@@ -2542,7 +2559,7 @@ def gemm_f8(a, b, out, dq_a, dq_b, *, fmt_a=E4M3, bias=None, act=0, aux=None, ad
                     import warnings
                     warnings.warn(f"fp8 library GEMM unavailable ({e}); using the native tiles")
             variant = -1  # (library path disabled / not applicable: the built-in native choice)
-        _chk(lib.pdt_gemm_f8(*args(variant)), "gemm_f8")
+        _chk_v(lib.pdt_gemm_f8(*args(variant)), "gemm_f8")
         return out
     codes, meta, qfmt, only = q8
     assert codes.dtype == torch.uint8 and codes.numel() == M * N and codes.is_contiguous()
@@ -2567,11 +2584,11 @@ def gemm_f8(a, b, out, dq_a, dq_b, *, fmt_a=E4M3, bias=None, act=0, aux=None, ad
             variant = 10
         ntm = -(-M // lib.pdt_gemm_f8_bm(variant))
         cpart = torch.empty(ntm * N + lib.pdt_reduce_rows_work(ntm, N), dtype=torch.float32, device=a.device)
-        _chk(lib.pdt_gemm_f8_q8_cs(*args(variant)[:-1], _p(cpart), _s()), "gemm_f8_q8_cs")
+        _chk_v(lib.pdt_gemm_f8_q8_cs(*args(variant)[:-1], _p(cpart), _s()), "gemm_f8_q8_cs")
         _chk(lib.pdt_wgrad_reduce_rows(_p(cpart), _p(colsum_out), ntm, N, 1.0, 0, _p(cpart[ntm * N:]), _s()),
              "colsum rows")
         return dq
-    _chk(lib.pdt_gemm_f8_q8(*args(variant)), "gemm_f8_q8")
+    _chk_v(lib.pdt_gemm_f8_q8(*args(variant)), "gemm_f8_q8")
     return dq
 
 

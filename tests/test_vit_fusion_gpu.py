@@ -155,7 +155,10 @@ def test_gemm_f8_fp8_output_epilogue(act, qfmt):
     lib = no._load()
     for v in range(lib.pdt_gemm_f8_num_variants()):
         out = torch.empty(M, N, dtype=torch.bfloat16, device="cuda")
-        no.gemm_f8(a8, b8, out, dqa, dqb, variant=v, **kw)
+        try:
+            no.gemm_f8(a8, b8, out, dqa, dqb, variant=v, **kw)
+        except no.NotApplicable:  # (the dense ring: plain epilogue, N % 256 == 0)
+            continue
         q_ref, dq_ref, meta_ref = no.quantize_fp8_delayed(out, meta0.clone(), qfmt)
         out2 = torch.empty_like(out)
         codes = torch.empty(M, N, dtype=torch.uint8, device="cuda")
