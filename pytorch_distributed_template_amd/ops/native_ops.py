@@ -2448,6 +2448,12 @@ def _bias_bf16(bias):
 
 
 def _gemm_f8_lib(a, b, out, dq_a, dq_b, fmt_a, bias):
+    """The plain fp8 GEMM of the split-epilogue paths below (fc1 forward, fc2 data gradient):
+    the framework's own tiles (tuned per shape; the 256x256 ring, csrc/gemm_ring.hip, on the
+    ViT shapes) -- or hipBLASLt through torch._scaled_mm when PDT_FP8_LIB=1."""
+    if not _fp8_lib_enabled():
+        gemm_f8(a, b, out, dq_a, dq_b, fmt_a=fmt_a, bias=bias)
+        return 0
     M, N = a.shape[0], b.shape[0]
     A = a.view(torch.float8_e5m2 if fmt_a == E5M2 else torch.float8_e4m3fn)
     B = b.view(torch.float8_e4m3fn).t()  # [K][N] column-major: the layout hipBLASLt takes
@@ -2458,17 +2464,16 @@ def _gemm_f8_lib(a, b, out, dq_a, dq_b, fmt_a, bias):
 
 
 def _fc1_lib(M, Hd, K) -> bool:
-    """The MLP's fp8 fc1 as the library GEMM (+bias) followed by one pass that writes gelu'(z),
-    the e4m3 codes of gelu(z) and their amax (pdt_gelu_dual_cast_fp8), instead of the native
-    GEMM with that epilogue fused (act 4 + fp8 side output). Tuned-table key ``fc1lib:M,Hd,K``
-    (1 = library); PDT_FP8_FC1_LIB=0/1 forces either."""
+    """The MLP's fp8 fc1 as a plain GEMM (+bias; ``_gemm_f8_lib``) followed by one pass that
+    writes gelu'(z), the e4m3 codes of gelu(z) and their amax (pdt_gelu_dual_cast_fp8), instead
+    of one GEMM with that epilogue fused (act 4 + fp8 side output). Tuned-table key
+    ``fc1lib:M,Hd,K`` (1 = split); PDT_FP8_FC1_LIB=0/1 forces either."""
     if _F8_LIB_BROKEN:
         return False
     env = os.environ.get("PDT_FP8_FC1_LIB")
     if env is not None:
-        return env == "1" and hasattr(torch, "_scaled_mm")
-    return bool(_tuned().get(f"fc1lib:{M},{Hd},{K}", 0)) and hasattr(torch, "_scaled_mm") and \
-        _fp8_lib_enabled()
+        return env == "1"
+    return bool(_tuned().get(f"fc1lib:{M},{Hd},{K}", 0))
 
 
 def _fc1_lib_forward(xq, w1q, a, z, aq, dqx, dqw1, bias1, meta, keep_a):
@@ -2484,12 +2489,11 @@ def _fc1_lib_forward(xq, w1q, a, z, aq, dqx, dqw1, bias1, meta, keep_a):
 
 
 def _fc2_dgrad_lib_on() -> bool:
-    """The MLP's fc2 data gradient as the plain library GEMM (bf16 g W2) followed by one pass that
-    multiplies by gelu'(z), casts to e5m2 and sums fc1's bias gradient
-    (pdt_cast_fp8_gelu_grad_cs), instead of the native GEMM with that epilogue (act 3 + e5m2 +
-    column sums). PDT_FC2_DGRAD_LIB=0 turns it off."""
-    return not _F8_LIB_BROKEN and hasattr(torch, "_scaled_mm") and _fp8_lib_enabled() \
-        and os.environ.get("PDT_FC2_DGRAD_LIB", "1") == "1"
+    """The MLP's fc2 data gradient as a plain GEMM (bf16 g W2; ``_gemm_f8_lib``) followed by one
+    pass that multiplies by gelu'(z), casts to e5m2 and sums fc1's bias gradient
+    (pdt_cast_fp8_gelu_grad_cs), instead of one GEMM with that epilogue (act 3 + e5m2 + column
+    sums). PDT_FC2_DGRAD_LIB=0 turns it off."""
+    return not _F8_LIB_BROKEN and os.environ.get("PDT_FC2_DGRAD_LIB", "1") == "1"
 
 
 def _fc2_dgrad_lib(gq, w2qt, dz, dqg, dqw2, z, dzq, gmeta, db):
