@@ -577,6 +577,10 @@ PDT_API int pdt_gemm_f8_num_variants() { return NVAR_F8; }
 PDT_API int pdt_gemm_ring(const void* a, const void* b, void* c, const float* bias, const float* dq_a,
                           const float* dq_b, int M, int N, int K, int lda, int ldb, int ldc, int dt, int sub,
                           hipStream_t st);
+PDT_API int pdt_gemm_ring_epi(const void* a, const void* b, void* c, const float* bias, const float* dq_a,
+                              const float* dq_b, int M, int N, int K, int lda, int ldb, int ldc, int dt, int act,
+                              void* aux, const void* addend, void* q8, const float* q8_meta, float* q8_part,
+                              int q8_fmt, int q8_only, float* colsum, hipStream_t st);
 
 static int gemm_f8_impl(const void* a, const void* b, void* out, const float* bias, const float* dq_a,
                         const float* dq_b, int M, int N, int K, int lda, int ldb, int ldo, int fmt_a, int act,
@@ -584,10 +588,19 @@ static int gemm_f8_impl(const void* a, const void* b, void* out, const float* bi
                         int q8_fmt, int q8_only, float* q8_dq, hipStream_t stream, float* colsum = nullptr) {
   if (K % 128 != 0 || lda % 16 != 0 || ldb % 16 != 0 || N % 8 != 0 || ldo % 8 != 0) return -1;
   if (lda != K) return -2;  // rows of A are dense (the gather's source row stride is Cs)
-  if (variant >= F8_RING0 && variant < NVAR_F8) {  // the plain-epilogue dense ring
-    if (act != 0 || aux != nullptr || addend != nullptr || q8 != nullptr || colsum != nullptr) return -5;
-    return pdt_gemm_ring(a, b, out, bias, dq_a, dq_b, M, N, K, lda, ldb, ldo, fmt_a == 1 ? 2 : 1,
-                         variant - F8_RING0, stream);
+  if (variant >= F8_RING0 && variant < NVAR_F8) {  // the dense ring (csrc/gemm_ring.hip)
+    const int dt = fmt_a == 1 ? 2 : 1;
+    int rc;
+    if (act != 0 || aux != nullptr || addend != nullptr || q8 != nullptr || colsum != nullptr) {
+      if (variant != F8_RING0) return -5;  // the fused epilogue: grouping GM 4 only
+      rc = pdt_gemm_ring_epi(a, b, out, bias, dq_a, dq_b, M, N, K, lda, ldb, ldo, dt, act, aux, addend, q8, q8_meta,
+                             q8_part, q8_fmt, q8_only, colsum, stream);
+    } else {
+      rc = pdt_gemm_ring(a, b, out, bias, dq_a, dq_b, M, N, K, lda, ldb, ldo, dt, variant - F8_RING0, stream);
+    }
+    if (rc || q8 == nullptr) return rc;
+    const int nblk = ((M + 255) / 256) * (N / 256);
+    return pdt_fp8_meta_roll_partial(q8_meta, q8_part, nblk, q8_fmt, q8_dq, stream);
   }
   NTParams p;
   p.src = (const u16*)a;

@@ -47,7 +47,25 @@ struct RingParams {
   const void* zero;   // 16 zero bytes (DMA source of rows past M)
   int M, N, nk;       // nk = K-tiles (K bytes / 128)
   int lda, ldb, ldc;  // lda / ldb in bytes, ldc in elements
+  // fused epilogue (EPI instantiations; conv_nt_kernel.h's staged-epilogue semantics, on the
+  // bf16-rounded values): act 0 out = z (+ addend); act 3 out = z * gelu'(addend);
+  // act 4 out = gelu(z), aux = gelu'(z); act 5 out = z * addend -- z = bf16(alpha acc + bias)
+  int act;
+  u16* aux;             // [M][ldc]
+  const u16* addend;    // [M][ldc]
+  uint8_t* q8;          // [M][ldc] fp8 codes of out (x q8_meta[0]); nullptr = none
+  const float* q8_meta;
+  float* q8_part;       // [grid]: the workgroup's max |out|
+  int q8_fmt, q8_only;  // 0 e4m3 / 1 e5m2; 1: out itself is not stored
+  float* colsum;        // [ceil(M / 256)][N]: column sums of out per 256-row tile; nullptr = none
 };
+
+__device__ __forceinline__ float ring_gelu_grad(float z) {  // d gelu_tanh(z) / dz
+  const float u = 0.7978845608f * (z + 0.044715f * z * z * z);
+  const float t = pdt_tanh(u);
+  const float du = 0.7978845608f * (1.f + 3.f * 0.044715f * z * z);
+  return 0.5f * (1.f + t) + 0.5f * z * (1.f - t * t) * du;
+}
 
 __device__ __forceinline__ int rswz(int row, int chunk) { return chunk ^ ((row >> 1) & 7); }
 
@@ -72,7 +90,7 @@ __device__ __forceinline__ void ring_tile_of(uint32_t bid, int ntm, int ntn, int
 }
 
 // DT 0: bf16 x bf16; 1: e4m3 A x e4m3 B; 2: e5m2 A x e4m3 B (OCP fp8, unit block scales)
-template <int DT, bool BIAS, int GM>
+template <int DT, bool BIAS, int GM, bool EPI>
 __global__ void __launch_bounds__(RNTH, 1) gemm_ring_kernel(RingParams p) {
   constexpr int WM = 2, WN = 4;
   constexpr int MI = RBM / WM / 16;  // 8 row blocks per wave
@@ -237,6 +255,16 @@ __global__ void __launch_bounds__(RNTH, 1) gemm_ring_kernel(RingParams p) {
 #pragma unroll
     for (int e = 0; e < 4; ++e) bv[j][e] = BIAS ? p.bias[n0 + wcol(j) + lcol + e] : 0.f;
   const bool odd = (lane >> 4) & 1;
+  // EPI: this lane's 8 columns of each column pair are fixed (colsum partials), its max |out|
+  float csum[EPI ? 2 : 1][EPI ? 8 : 1];
+  float q8max = 0.f;
+  const float q8s = (EPI && p.q8 != nullptr) ? p.q8_meta[0] : 0.f;
+  if constexpr (EPI) {
+#pragma unroll
+    for (int jp = 0; jp < 2; ++jp)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) csum[jp][e] = 0.f;
+  }
 #pragma unroll
   for (int i = 0; i < MI; ++i) {
     const int m = m0 + wm * (RBM / WM) + i * 16 + lrow;
@@ -252,39 +280,134 @@ __global__ void __launch_bounds__(RNTH, 1) gemm_ring_kernel(RingParams p) {
       // j's 8 columns and the odd lane block j + 1's
       const auto r0 = __builtin_amdgcn_permlane16_swap(a0, b0, false, false);
       const auto r1 = __builtin_amdgcn_permlane16_swap(a1, b1, false, false);
-      const u32x4 v = {r0[0], r1[0], r0[1], r1[1]};
+      u32x4 v = {r0[0], r1[0], r0[1], r1[1]};
       const int col = n0 + wcol(odd ? j + 1 : j) + ((lane >> 5) * 8);
-      if (m < p.M) *reinterpret_cast<u32x4*>(p.C + (size_t)m * p.ldc + col) = v;
+      if constexpr (!EPI) {
+        if (m < p.M) *reinterpret_cast<u32x4*>(p.C + (size_t)m * p.ldc + col) = v;
+      } else {
+        if (m < p.M) {
+          const size_t e0 = (size_t)m * p.ldc + col;
+          if (p.addend != nullptr) {
+            const u32x4 ad = *reinterpret_cast<const u32x4*>(p.addend + e0);
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              if (p.act == 3)
+                v[e] = pack2bf(lo_bf(v[e]) * ring_gelu_grad(lo_bf(ad[e])), hi_bf(v[e]) * ring_gelu_grad(hi_bf(ad[e])));
+              else if (p.act == 5)
+                v[e] = pack2bf(lo_bf(v[e]) * lo_bf(ad[e]), hi_bf(v[e]) * hi_bf(ad[e]));
+              else
+                v[e] = pack2bf(lo_bf(v[e]) + lo_bf(ad[e]), hi_bf(v[e]) + hi_bf(ad[e]));
+            }
+          }
+          if (p.act == 4) {
+            u32x4 gd;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              float g0, g1, d0, d1;
+              pdt_gelu_dual(lo_bf(v[e]), g0, d0);
+              pdt_gelu_dual(hi_bf(v[e]), g1, d1);
+              v[e] = pack2bf(g0, g1);
+              gd[e] = pack2bf(d0, d1);
+            }
+            *reinterpret_cast<u32x4*>(p.aux + e0) = gd;
+          }
+          float f[8];
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            f[2 * e] = lo_bf(v[e]);
+            f[2 * e + 1] = hi_bf(v[e]);
+          }
+#pragma unroll
+          for (int e = 0; e < 8; ++e) csum[j >> 1][e] += f[e];
+          if (p.q8 != nullptr) {
+#pragma unroll
+            for (int e = 0; e < 8; ++e) q8max = fmaxf(q8max, fabsf(f[e]));
+            uint2 c8;
+            if (p.q8_fmt == 0) {
+              c8.x = pdt_cvt4_f8<0>(f[0] * q8s, f[1] * q8s, f[2] * q8s, f[3] * q8s);
+              c8.y = pdt_cvt4_f8<0>(f[4] * q8s, f[5] * q8s, f[6] * q8s, f[7] * q8s);
+            } else {
+              c8.x = pdt_cvt4_f8<1>(f[0] * q8s, f[1] * q8s, f[2] * q8s, f[3] * q8s);
+              c8.y = pdt_cvt4_f8<1>(f[4] * q8s, f[5] * q8s, f[6] * q8s, f[7] * q8s);
+            }
+            *reinterpret_cast<uint2*>(p.q8 + e0) = c8;
+          }
+          if (!(p.q8 != nullptr && p.q8_only)) *reinterpret_cast<u32x4*>(p.C + e0) = v;
+        }
+      }
+    }
+  }
+  if constexpr (EPI) {
+    // every LDS fragment read finished before the loop's last barrier: smem is free here
+    float* red = reinterpret_cast<float*>(smem);
+    if (p.colsum != nullptr) {
+      // lanes of one 16-lane row hold 16 rows of the same 8 columns: DPP row sums, then the
+      // two wave rows (wm) with the same columns through LDS: [wm][wn][jp][g][8]
+#pragma unroll
+      for (int jp = 0; jp < 2; ++jp)
+#pragma unroll
+        for (int e = 0; e < 8; ++e) csum[jp][e] = row16_sum(csum[jp][e]);
+      if (lrow == 0) {
+#pragma unroll
+        for (int jp = 0; jp < 2; ++jp)
+#pragma unroll
+          for (int e = 0; e < 8; ++e) red[((wm * WN + wn) * 2 + jp) * 32 + (lane >> 4) * 8 + e] = csum[jp][e];
+      }
+    }
+    if (p.q8 != nullptr) {
+      q8max = warp_max(q8max);
+      if (lane == 0) red[2 * WN * 2 * 32 + wave] = q8max;
+    }
+    __syncthreads();
+    if (p.colsum != nullptr && wm == 0 && lrow == 0) {
+#pragma unroll
+      for (int jp = 0; jp < 2; ++jp) {
+        const int base = ((wn)*2 + jp) * 32 + (lane >> 4) * 8;
+        const int cl = wcol(2 * jp + (odd ? 1 : 0)) + ((lane >> 5) * 8);
+        f32x4 s0, s1;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          s0[e] = red[base + e] + red[WN * 2 * 32 + base + e];
+          s1[e] = red[base + 4 + e] + red[WN * 2 * 32 + base + 4 + e];
+        }
+        float* dst = p.colsum + (size_t)tm * p.N + n0 + cl;
+        *reinterpret_cast<f32x4*>(dst) = s0;
+        *reinterpret_cast<f32x4*>(dst + 4) = s1;
+      }
+    }
+    if (p.q8 != nullptr && tid == 0) {
+      float mx = 0.f;
+#pragma unroll
+      for (int w = 0; w < RNTH / 64; ++w) mx = fmaxf(mx, red[2 * WN * 2 * 32 + w]);
+      p.q8_part[blockIdx.x] = mx;
     }
   }
 }
 
 static __device__ __attribute__((aligned(64))) u32x4 ring_zero_chunk[4];
 
-template <int DT, bool BIAS, int GM>
+template <int DT, bool BIAS, int GM, bool EPI>
 int ring_launch(const RingParams& p, hipStream_t st) {
   const int ntm = (p.M + RBM - 1) / RBM, ntn = p.N / RBN;
-  hipLaunchKernelGGL((gemm_ring_kernel<DT, BIAS, GM>), dim3(ntm * ntn), dim3(RNTH), 0, st, p);
+  hipLaunchKernelGGL((gemm_ring_kernel<DT, BIAS, GM, EPI>), dim3(ntm * ntn), dim3(RNTH), 0, st, p);
   PDT_RETURN_LAUNCH();
 }
 
 template <int DT>
-int ring_dispatch(int sub, bool bias, const RingParams& p, hipStream_t st) {
-  if (sub == 0) return bias ? ring_launch<DT, true, 4>(p, st) : ring_launch<DT, false, 4>(p, st);
-  return bias ? ring_launch<DT, true, 8>(p, st) : ring_launch<DT, false, 8>(p, st);
+int ring_dispatch(int sub, bool bias, bool epi, const RingParams& p, hipStream_t st) {
+  if constexpr (DT != 0) {
+    if (epi) return bias ? ring_launch<DT, true, 4, true>(p, st) : ring_launch<DT, false, 4, true>(p, st);
+  } else if (epi) {
+    return -5;  // (the fused epilogue is built for the fp8 GEMMs only)
+  }
+  if (sub == 0) return bias ? ring_launch<DT, true, 4, false>(p, st) : ring_launch<DT, false, 4, false>(p, st);
+  return bias ? ring_launch<DT, true, 8, false>(p, st) : ring_launch<DT, false, 8, false>(p, st);
 }
 
-}  // namespace
-
-// Number of ring sub-variants (tile-order groupings GM = 4, 8).
-PDT_API int pdt_gemm_ring_num_variants() { return 2; }
-
-// C[M][N] = dq_a*dq_b * A[M][K] . B[N][K]^T (+ bias), bf16 out. dt: 0 bf16 operands (K in
-// elements, a multiple of 64), 1 / 2 e4m3 / e5m2 A with e4m3 B (K a multiple of 128).
-// Returns -5 (not applicable) for N not a multiple of 256 or unaligned strides.
-PDT_API int pdt_gemm_ring(const void* a, const void* b, void* c, const float* bias, const float* dq_a,
-                          const float* dq_b, int M, int N, int K, int lda, int ldb, int ldc, int dt, int sub,
-                          hipStream_t st) {
+int ring_run(const void* a, const void* b, void* c, const float* bias, const float* dq_a, const float* dq_b, int M,
+             int N, int K, int lda, int ldb, int ldc, int dt, int sub, int act, void* aux, const void* addend,
+             void* q8, const float* q8_meta, float* q8_part, int q8_fmt, int q8_only, float* colsum,
+             hipStream_t st) {
   static const void* zcache[PDT_MAX_DEV] = {};
   const int esz = dt == 0 ? 2 : 1;
   const long kbytes = (long)K * esz;
@@ -293,6 +416,10 @@ PDT_API int pdt_gemm_ring(const void* a, const void* b, void* c, const float* bi
       lda < K || ldb < K || ldc < N)
     return -5;
   if ((long)M * lda * esz >= (1L << 40)) return -1;
+  if (!(act == 0 || act == 3 || act == 4 || act == 5)) return -5;
+  if ((act == 3 || act == 5) && addend == nullptr) return -4;
+  if (act == 4 && (aux == nullptr || addend != nullptr)) return -4;
+  if (q8 != nullptr && (q8_meta == nullptr || q8_part == nullptr || ldc != N)) return -4;
   RingParams p;
   p.A = (const char*)a;
   p.B = (const char*)b;
@@ -308,11 +435,51 @@ PDT_API int pdt_gemm_ring(const void* a, const void* b, void* c, const float* bi
   p.lda = lda * esz;
   p.ldb = ldb * esz;
   p.ldc = ldc;
+  p.act = act;
+  p.aux = (u16*)aux;
+  p.addend = (const u16*)addend;
+  p.q8 = (uint8_t*)q8;
+  p.q8_meta = q8_meta;
+  p.q8_part = q8_part;
+  p.q8_fmt = q8_fmt;
+  p.q8_only = q8_only;
+  p.colsum = colsum;
+  const bool epi = act != 0 || aux != nullptr || addend != nullptr || q8 != nullptr || colsum != nullptr;
   if (sub < 0 || sub > 1) sub = 0;
   switch (dt) {
-    case 0: return ring_dispatch<0>(sub, bias != nullptr, p, st);
-    case 1: return ring_dispatch<1>(sub, bias != nullptr, p, st);
-    case 2: return ring_dispatch<2>(sub, bias != nullptr, p, st);
+    case 0: return ring_dispatch<0>(sub, bias != nullptr, epi, p, st);
+    case 1: return ring_dispatch<1>(sub, bias != nullptr, epi, p, st);
+    case 2: return ring_dispatch<2>(sub, bias != nullptr, epi, p, st);
   }
   return -1;
+}
+
+}  // namespace
+
+// Number of ring sub-variants (tile-order groupings GM = 4, 8).
+PDT_API int pdt_gemm_ring_num_variants() { return 2; }
+
+// Rows of the ring's M tile (the colsum partial rows).
+PDT_API int pdt_gemm_ring_bm() { return RBM; }
+
+// C[M][N] = dq_a*dq_b * A[M][K] . B[N][K]^T (+ bias), bf16 out. dt: 0 bf16 operands (K in
+// elements, a multiple of 64), 1 / 2 e4m3 / e5m2 A with e4m3 B (K a multiple of 128).
+// Returns -5 (not applicable) for N not a multiple of 256 or unaligned strides.
+PDT_API int pdt_gemm_ring(const void* a, const void* b, void* c, const float* bias, const float* dq_a,
+                          const float* dq_b, int M, int N, int K, int lda, int ldb, int ldc, int dt, int sub,
+                          hipStream_t st) {
+  return ring_run(a, b, c, bias, dq_a, dq_b, M, N, K, lda, ldb, ldc, dt, sub, 0, nullptr, nullptr, nullptr, nullptr,
+                  nullptr, 0, 0, nullptr, st);
+}
+
+// The same with the fused fp8 epilogue (RingParams: act / aux / addend, the fp8 codes of the
+// output with the next GEMM's delayed scale and the workgroup amax partials, per-tile column
+// sums); dt 1 / 2 only (the fused instantiation is grouping GM = 4).
+PDT_API int pdt_gemm_ring_epi(const void* a, const void* b, void* c, const float* bias, const float* dq_a,
+                              const float* dq_b, int M, int N, int K, int lda, int ldb, int ldc, int dt, int act,
+                              void* aux, const void* addend, void* q8, const float* q8_meta, float* q8_part,
+                              int q8_fmt, int q8_only, float* colsum, hipStream_t st) {
+  if (dt == 0) return -5;
+  return ring_run(a, b, c, bias, dq_a, dq_b, M, N, K, lda, ldb, ldc, dt, 0, act, aux, addend, q8, q8_meta, q8_part,
+                  q8_fmt, q8_only, colsum, st);
 }

@@ -2540,8 +2540,9 @@ def gemm_f8(a, b, out, dq_a, dq_b, *, fmt_a=E4M3, bias=None, act=0, aux=None, ad
                           _p(aux), _p(addend), v, _s())
         lib_ok = _f8_lib_ok(out, act, aux, addend, q8)
         if variant is None:
-            # ",r": a residual addend in the epilogue (a different best tile, and no library path)
-            key = f"f8b:{M},{N},{K},{fmt_a},{act},{int(bias is not None)}" + (",r" if addend is not None and act == 0
+            # ",r": a residual addend in the epilogue (a different best tile, and no library path);
+            # "f8c": the variant set with the dense ring (ids 12 / 13) -- "f8b" choices predate it
+            key = f"f8c:{M},{N},{K},{fmt_a},{act},{int(bias is not None)}" + (",r" if addend is not None and act == 0
                                                                                else "")
             nv = lib.pdt_gemm_f8_num_variants()
             if not lib_ok and int(_tuned().get(key, -1)) == F8_LIB:
@@ -2572,7 +2573,7 @@ def gemm_f8(a, b, out, dq_a, dq_b, *, fmt_a=E4M3, bias=None, act=0, aux=None, ad
     args = lambda v: (_p(a), _p(b), _p(out), _p(bias), _p(dq_a), _p(dq_b), M, N, K, K, K, N, fmt_a, act,  # noqa
                       _p(aux), _p(addend), v, _p(codes), _p(meta), _p(part), int(qfmt), int(only), _p(dq), _s())
     if variant is None:
-        key = f"f8b:{M},{N},{K},{fmt_a},{act},{int(bias is not None)},q{qfmt}{int(only)}" + \
+        key = f"f8c:{M},{N},{K},{fmt_a},{act},{int(bias is not None)},q{qfmt}{int(only)}" + \
             (",cs" if colsum_out is not None else "")
         table = _tuned()
         if key in table:

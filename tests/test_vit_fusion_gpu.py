@@ -639,3 +639,45 @@ def test_embed_tokens_matches_cat_add():
     assert nrmerr(x, xr) < 5e-3
     assert nrmerr(gt, rt) < 5e-3 and nrmerr(gc, rc) < 5e-3 and nrmerr(gp, rp) < 5e-3
     assert gc.shape == cls.shape and gp.shape == pos.shape
+
+
+@pytest.mark.parametrize("act,qfmt,cs", [(4, 0, False), (3, 1, True), (5, 1, True), (0, 0, False)])
+def test_ring_fused_epilogues(act, qfmt, cs):
+    """The dense 256x256 ring (fp8 variant 12, csrc/gemm_ring.hip) with the fused epilogues of
+    the ViT MLP: fc1's GELU + gelu' (act 4) with fc2's e4m3 input codes, the fc2 data gradient's
+    gelu' multiply (act 3 / 5) with fc1's e5m2 gradient codes and bias-gradient column sums, a
+    residual addend (act 0): the bf16 output against the staged native tile (variant 1), the
+    codes / dequant factor / amax history against the separate cast of the ring's own output
+    (bit-exact), the column sums against a sum of that output; M has a partial 256-row tile."""
+    torch.manual_seed(60 + act)
+    M, N, K = 1100, 512, 384
+    fmt_a = no.E5M2 if act in (3, 5) else no.E4M3
+    a8, dqa = no.quantize_fp8(torch.randn(M, K, device="cuda").to(torch.bfloat16), fmt_a)
+    b8, dqb = no.quantize_fp8(torch.randn(N, K, device="cuda").to(torch.bfloat16) * 0.1, no.E4M3)
+    z = torch.randn(M, N, device="cuda").to(torch.bfloat16)
+    bias = torch.randn(N, device="cuda") if act in (0, 4) else None
+    kw = dict(fmt_a=fmt_a, bias=bias, act=act, addend=z if act != 4 else None)
+    aux_r = torch.empty(M, N, dtype=torch.bfloat16, device="cuda") if act == 4 else None
+    aux_1 = torch.empty_like(aux_r) if act == 4 else None
+    ref = torch.empty(M, N, dtype=torch.bfloat16, device="cuda")
+    no.gemm_f8(a8, b8, ref, dqa, dqb, variant=1, aux=aux_1, **kw)
+    out = torch.full((M, N), float("nan"), device="cuda").to(torch.bfloat16)
+    no.gemm_f8(a8, b8, out, dqa, dqb, variant=12, aux=aux_r, **kw)
+    torch.cuda.synchronize()
+    assert nrmerr(out, ref) < 1e-2, nrmerr(out, ref)
+    if act == 4:
+        assert nrmerr(aux_r, aux_1) < 1e-2
+    _, _, meta0 = no.quantize_fp8_delayed(torch.randn(M, N, device="cuda").to(torch.bfloat16), None, qfmt)
+    q_ref, dq_ref, meta_ref = no.quantize_fp8_delayed(out, meta0.clone(), qfmt)
+    codes = torch.empty(M, N, dtype=torch.uint8, device="cuda")
+    meta = meta0.clone()
+    out2 = torch.full_like(out, float("nan"))
+    csum = torch.empty(N, dtype=torch.float32, device="cuda") if cs else None
+    dq = no.gemm_f8(a8, b8, out2, dqa, dqb, variant=12, aux=torch.empty_like(out) if act == 4 else None,
+                    q8=(codes, meta, qfmt, False), colsum_out=csum, **kw)
+    torch.cuda.synchronize()
+    assert torch.equal(out2, out)
+    assert torch.equal(codes, q_ref), (codes != q_ref).sum().item()
+    assert torch.equal(dq, dq_ref) and torch.equal(meta, meta_ref)
+    if cs:
+        assert nrmerr(csum, out.float().sum(0)) < 1e-3, nrmerr(csum, out.float().sum(0))
