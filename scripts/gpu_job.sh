@@ -12,6 +12,7 @@
 #   testss:EXPR      the same with -s and a 600 s per-test limit (long numerics tests)
 #   smoke            __graft_entry__.smoke()
 #   bench[:ARGS]     python bench.py ARGS   (ARGS: commas become spaces)
+#   benchenv:K=V+K2=V2[:ARGS]  the same with extra environment variables
 #   ktrace[:ARGS]    rocprofv3 kernel trace of bench.py --steps 3 --warmup 3 ARGS,
 #                    per-step summary via scripts/step_profile.py
 #   hiptrace[:ARGS]  rocprofv3 HIP-API + kernel trace (host-sync hunting)
@@ -35,6 +36,9 @@ for job in "$@"; do
       PDT_SLOW_TESTS=1 run ${TAG}_testss_$(echo "$args" | tr -c 'a-zA-Z0-9_\n' '_' | cut -c1-40).txt 1100 python -u -m pytest tests -m gpu -x -v -s --timeout 600 --timeout-method thread -k "$args" ;;
     smoke) run ${TAG}_smoke.txt 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) run ${TAG}_bench_$(echo "$args" | tr -c 'a-zA-Z0-9_\n' '_').txt 400 python bench.py $args ;;
+    benchenv)  # benchenv:K=V+K2=V2:ARGS -- bench.py with extra environment variables
+      envs=${rest%%:*}; bargs=""; [[ "$rest" == *:* ]] && bargs=${rest#*:}
+      run ${TAG}_benchenv_$(echo "$envs$bargs" | tr -c 'a-zA-Z0-9_\n' '_' | cut -c1-60).txt 400 env ${envs//+/ } python bench.py ${bargs//,/ } ;;
     benchlong)  # stock-stack runs whose MIOpen find takes minutes; find results kept in gpurun_out/miopen_db,
                 # seeded from the find db of earlier runs (profiles/miopen_db_bs2048: MIOpen's own text db)
       mkdir -p gpurun_out/miopen_db
