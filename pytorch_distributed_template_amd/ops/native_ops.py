@@ -2466,14 +2466,16 @@ def _gemm_f8_lib(a, b, out, dq_a, dq_b, fmt_a, bias):
 def _fc1_lib(M, Hd, K) -> bool:
     """The MLP's fp8 fc1 as a plain GEMM (+bias; ``_gemm_f8_lib``) followed by one pass that
     writes gelu'(z), the e4m3 codes of gelu(z) and their amax (pdt_gelu_dual_cast_fp8), instead
-    of one GEMM with that epilogue fused (act 4 + fp8 side output). Tuned-table key
-    ``fc1lib:M,Hd,K`` (1 = split); PDT_FP8_FC1_LIB=0/1 forces either."""
+    of one GEMM with that epilogue fused (act 4 + fp8 side output). Off by default: the dense
+    ring's fused epilogue (csrc/gemm_ring.hip) measured faster than the split (ViT-B/16 fp8 bs
+    1024: 9 404 vs 9 175 img/s with the fc2 data gradient below, same box, r5b). Tuned-table
+    key ``fc1split:M,Hd,K`` (1 = split); PDT_FP8_FC1_LIB=0/1 forces either."""
     if _F8_LIB_BROKEN:
         return False
     env = os.environ.get("PDT_FP8_FC1_LIB")
     if env is not None:
         return env == "1"
-    return bool(_tuned().get(f"fc1lib:{M},{Hd},{K}", 0))
+    return bool(_tuned().get(f"fc1split:{M},{Hd},{K}", 0))
 
 
 def _fc1_lib_forward(xq, w1q, a, z, aq, dqx, dqw1, bias1, meta, keep_a):
@@ -2492,8 +2494,9 @@ def _fc2_dgrad_lib_on() -> bool:
     """The MLP's fc2 data gradient as a plain GEMM (bf16 g W2; ``_gemm_f8_lib``) followed by one
     pass that multiplies by gelu'(z), casts to e5m2 and sums fc1's bias gradient
     (pdt_cast_fp8_gelu_grad_cs), instead of one GEMM with that epilogue (act 3 + e5m2 + column
-    sums). PDT_FC2_DGRAD_LIB=0 turns it off."""
-    return not _F8_LIB_BROKEN and os.environ.get("PDT_FC2_DGRAD_LIB", "1") == "1"
+    sums). Off by default (the fused ring epilogue is faster, see ``_fc1_lib``);
+    PDT_FC2_DGRAD_LIB=1 turns it on."""
+    return not _F8_LIB_BROKEN and os.environ.get("PDT_FC2_DGRAD_LIB", "0") == "1"
 
 
 def _fc2_dgrad_lib(gq, w2qt, dz, dqg, dqw2, z, dzq, gmeta, db):
