@@ -27,6 +27,17 @@ def _fp8_attn() -> bool:
     return os.environ.get("PDT_FP8_ATTN", "1") == "1"
 
 
+def _cls_prune(x, setting) -> bool:
+    """Whether the last block computes the class token's row only (see Block.forward).
+    ``setting`` None: on the native kernel path (the stock torch path stays the plain model, as
+    the reference-equivalent baseline); PDT_VIT_CLS_PRUNE=0/1 overrides."""
+    import os
+    env = os.environ.get("PDT_VIT_CLS_PRUNE")
+    if env is not None:
+        return env == "1"
+    return fused.use_native(x) if setting is None else bool(setting)
+
+
 def _ln_add() -> bool:
     """fp8 models: the blocks' residual adds in the next LayerNorm kernel instead of the proj /
     fc2 GEMM epilogues (PDT_LN_ADD=0 keeps them in the epilogues)."""
@@ -70,7 +81,7 @@ class Block(nn.Module):
         self.norm2 = nn.LayerNorm(dim, eps=1e-6)
         self.mlp = Mlp(dim, int(dim * mlp_ratio))
 
-    def forward(self, x, fp8=False, prev_fc2=None, pending=None, defer=False):
+    def forward(self, x, fp8=False, prev_fc2=None, pending=None, defer=False, cls_only=False):
         # pre-norm residual block; the residual adds ride the proj / fc2 GEMM epilogues and
         # their gradients are summed inside the LayerNorm backward (fused.ln_fork)
         # (fp8: the LayerNorm forward kernels also write the e4m3 inputs of qkv / fc1, and
@@ -84,6 +95,8 @@ class Block(nn.Module):
                                      prev_fc2 if fp8 else None)
         else:
             x, h = fused.ln_fork(x, self.norm1, self.attn.qkv if fp8 else None, prev_fc2 if fp8 else None)
+        if cls_only:
+            return self._forward_cls(x, h, fp8)
         if fp8 and _ln_add():
             y = self.attn(h, fp8=fp8)
             x, h = fused.ln_add_fork(y, x, self.norm2, self.mlp.fc1, self.attn.proj)
@@ -94,13 +107,32 @@ class Block(nn.Module):
             return self.mlp(h, fp8=fp8), x
         return self.mlp(h, fp8=fp8, residual=x)
 
+    def _forward_cls(self, x, h, fp8):
+        """The block for a consumer that reads token 0 only (the classifier after the LAST
+        block): keys and values of every token (qkv over all rows), but the attention output,
+        projection, residual, LayerNorm 2 and MLP of the class token's row alone -> [B, 1, D].
+        The model's output and every parameter gradient are those of the full block (the other
+        196 output rows feed nothing); it removes ~1/12 of the proj + MLP GEMM work and the
+        block's element passes over the other rows."""
+        qkv = fused.linear(h, self.attn.qkv, fp8=fp8)
+        o = fused.cls_attention(qkv, self.attn.num_heads)          # [B, 1, D]
+        x0 = x[:, :1].contiguous()
+        if fp8 and _ln_add():
+            y = fused.linear(o, self.attn.proj, fp8=fp8)
+            x0, h0 = fused.ln_add_fork(y, x0, self.norm2, self.mlp.fc1, self.attn.proj)
+        else:
+            x0 = fused.linear(o, self.attn.proj, fp8=fp8, residual=x0)
+            x0, h0 = fused.ln_fork(x0, self.norm2, self.mlp.fc1 if fp8 else None, self.attn.proj if fp8 else None)
+        return self.mlp(h0, fp8=fp8, residual=x0)
+
 
 class VisionTransformer(BaseModel):
     def __init__(self, image_size=224, patch_size=16, in_chans=3, num_classes=1000, embed_dim=768,
-                 depth=12, num_heads=12, mlp_ratio=4.0, fp8=False):
+                 depth=12, num_heads=12, mlp_ratio=4.0, fp8=False, cls_prune=None):
         super().__init__()
         self.patch_size = patch_size
         self.fp8 = fp8
+        self.cls_prune = cls_prune  # None: on the native path (_cls_prune)
         self.patch_embed = nn.Conv2d(in_chans, embed_dim, patch_size, stride=patch_size)
         n_patches = (image_size // patch_size) ** 2
         self.cls_token = nn.Parameter(torch.zeros(1, 1, embed_dim))
@@ -123,9 +155,11 @@ class VisionTransformer(BaseModel):
         prev = None
         pending = None
         defer = self.fp8 and _ln_add()
+        prune = _cls_prune(x, self.cls_prune)
         for i, blk in enumerate(self.blocks):
             last = i == len(self.blocks) - 1
-            out = blk(x, fp8=self.fp8, prev_fc2=prev, pending=pending, defer=defer and not last)
+            out = blk(x, fp8=self.fp8, prev_fc2=prev, pending=pending, defer=defer and not last,
+                      cls_only=prune and last)
             if defer and not last:
                 pending, x = out, None
             else:

@@ -213,6 +213,23 @@ def qkv_attention(qkv, num_heads: int, fp8: bool = False, fp8_for: nn.Linear | N
     return o.transpose(1, 2).reshape(B, T, num_heads * hd)
 
 
+def cls_attention(qkv, num_heads: int):
+    """Attention of token 0's query only (against every key / value) on a packed qkv
+    [B, T, 3*H*hd] -> [B, 1, H*hd]: what a classifier that reads token 0 needs from the last
+    block. Native path: one small kernel per direction (hd = 64, T <= 256); torch path: the
+    same math in fp32."""
+    B, T, D3 = qkv.shape
+    hd = D3 // (3 * num_heads)
+    if _use_native(qkv):
+        from . import native_ops
+        if hd == 64 and qkv.dtype == torch.bfloat16 and T <= 256:
+            return native_ops.cls_attention(qkv, num_heads)
+        native_ops.fallback("cls_attention", f"head dim {hd}, {qkv.dtype}, T {T} (kernel: 64, bf16, T <= 256)")
+    q, k, v = qkv.view(B, T, 3, num_heads, hd).permute(2, 0, 3, 1, 4)
+    o = F.scaled_dot_product_attention(q[:, :, :1], k, v)
+    return o.transpose(1, 2).reshape(B, 1, num_heads * hd)
+
+
 def patch_embed(x, conv: nn.Conv2d):
     """Non-overlapping patch conv -> [B, N, D] tokens."""
     if _use_native(x):

@@ -115,6 +115,8 @@ _SIGS = {
     "pdt_wt_dgrad_multi": (c_int, [P, c_int, c_long, P]),
     "pdt_add_bf16": (c_int, [P, P, P, c_long, P]),
     "pdt_attn_fwd": (c_int, [P, P, P, c_int, c_int, c_int, c_float, P]),
+    "pdt_cls_attn_fwd": (c_int, [P, P, P, c_int, c_int, c_int, P]),
+    "pdt_cls_attn_bwd": (c_int, [P, P, P, P, P, c_int, c_int, c_int, P]),
     "pdt_attn_fwd_f8": (c_int, [P, P, P, c_int, c_int, c_int, c_float, P]),
     "pdt_attn_fwd_tiles": (c_int, [P, P, P, c_int, c_int, c_int, c_float, P]),
     "pdt_attn_set_bwd_single": (c_int, [c_int]),
@@ -3275,6 +3277,37 @@ class _QKVAttention(torch.autograd.Function):
         _chk(_load().pdt_attn_bwd(_p(qkv), _p(out), _p(dout), _p(lse), _p(delta), _p(dqkv), B, T, ctx.H,
                                   ctx.scale, _s()), "attn_bwd")
         return dqkv, None, None, None, None, None
+
+
+class _ClsAttention(torch.autograd.Function):
+    """Attention of token 0's query against all T keys of a packed qkv [B, T, 3*H*64]
+    (csrc/attention_cls.hip): the output [B, 1, H*64] and, in backward, the full dqkv (token 0's
+    q gradient, every token's k / v gradients, zeros for the other queries)."""
+
+    @staticmethod
+    def forward(ctx, qkv, H):
+        B, T, D3 = qkv.shape
+        qkv = qkv.contiguous()
+        o = torch.empty((B, 1, D3 // 3), dtype=torch.bfloat16, device=qkv.device)
+        lse = torch.empty(B * H, dtype=torch.float32, device=qkv.device)
+        _chk(_load().pdt_cls_attn_fwd(_p(qkv), _p(o), _p(lse), B, T, H, _s()), "cls_attn_fwd")
+        ctx.save_for_backward(qkv, o, lse)
+        ctx.H = H
+        return o
+
+    @staticmethod
+    def backward(ctx, do):
+        qkv, o, lse = ctx.saved_tensors
+        B, T, _ = qkv.shape
+        do = do.to(torch.bfloat16).contiguous()
+        dqkv = torch.empty_like(qkv)
+        _chk(_load().pdt_cls_attn_bwd(_p(qkv), _p(o), _p(do), _p(lse), _p(dqkv), B, T, ctx.H, _s()), "cls_attn_bwd")
+        return dqkv, None
+
+
+def cls_attention(qkv, num_heads):
+    assert qkv.dtype == torch.bfloat16 and qkv.shape[-1] == 3 * 64 * num_heads and qkv.shape[1] <= 256
+    return _ClsAttention.apply(qkv, num_heads)
 
 
 def qkv_attention(qkv, num_heads, fp8=False, fp8_for=None, grad_fp8_for=None):

@@ -681,3 +681,55 @@ def test_ring_fused_epilogues(act, qfmt, cs):
     assert torch.equal(dq, dq_ref) and torch.equal(meta, meta_ref)
     if cs:
         assert nrmerr(csum, out.float().sum(0)) < 1e-3, nrmerr(csum, out.float().sum(0))
+
+
+@pytest.mark.parametrize("T", [197, 50])
+def test_cls_attention_kernel_matches_fp32(T):
+    """csrc/attention_cls.hip: token 0's attention output and the full dqkv against an fp32
+    torch reference of the same op."""
+    torch.manual_seed(70 + T)
+    B, H = 5, 12
+    qkv = (torch.randn(B, T, 3 * H * 64, device="cuda") * 0.5).to(torch.bfloat16).requires_grad_(True)
+    o = fused.cls_attention(qkv, H)
+    do = torch.randn_like(o)
+    o.backward(do)
+    ref_in = qkv.detach().float().requires_grad_(True)
+    q, k, v = ref_in.view(B, T, 3, H, 64).permute(2, 0, 3, 1, 4)
+    p = torch.softmax((q[:, :, :1] @ k.transpose(-1, -2)) / 8.0, dim=-1)
+    ref = (p @ v).transpose(1, 2).reshape(B, 1, H * 64)
+    ref.backward(do.float())
+    torch.cuda.synchronize()
+    assert o.shape == (B, 1, H * 64)
+    assert nrmerr(o, ref) < 1e-2, nrmerr(o, ref)
+    g, gr = qkv.grad.view(B, T, 3, H * 64), ref_in.grad.view(B, T, 3, H * 64)
+    assert torch.count_nonzero(g[:, 1:, 0]) == 0  # no query gradient except token 0's
+    for i, name in enumerate("qkv"):
+        e = nrmerr(g[:, :, i], gr[:, :, i])
+        assert e < 2e-2, (name, e)
+
+
+def test_vit_cls_prune_native_matches_full(monkeypatch):
+    """The native fp8 ViT with the class-token-only last block: loss and every parameter
+    gradient close to the same model computing all 197 rows of the last block."""
+    from pytorch_distributed_template_amd.models.vit import VisionTransformer
+    torch.manual_seed(3)
+    m = VisionTransformer(depth=2, fp8=True).cuda().to(memory_format=torch.channels_last)
+    x = torch.randn(8, 3, 224, 224, device="cuda")
+    y = torch.randint(0, 1000, (8,), device="cuda")
+    res = {}
+    for prune in ("0", "1"):
+        monkeypatch.setenv("PDT_VIT_CLS_PRUNE", prune)
+        for mod in m.modules():  # fresh fp8 scaling state for each arm
+            for a in ("_pdt_fp8_meta", "_pdt_fp8_gmeta"):
+                if hasattr(mod, a):
+                    delattr(mod, a)
+        m.zero_grad(set_to_none=True)
+        out = m(x)
+        loss = fused.softmax_cross_entropy(out, y)
+        loss.backward()
+        torch.cuda.synchronize()
+        res[prune] = (float(loss), {n: p.grad.float().clone() for n, p in m.named_parameters()})
+    assert abs(res["1"][0] - res["0"][0]) < 2e-2 * abs(res["0"][0]), (res["1"][0], res["0"][0])
+    for n, g in res["0"][1].items():
+        e = nrmerr(res["1"][1][n], g)
+        assert e < 0.1, (n, e)
