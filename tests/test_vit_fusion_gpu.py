@@ -708,12 +708,15 @@ def test_cls_attention_kernel_matches_fp32(T):
         assert e < 2e-2, (name, e)
 
 
-def test_vit_cls_prune_native_matches_full(monkeypatch):
-    """The native fp8 ViT with the class-token-only last block: loss and every parameter
-    gradient close to the same model computing all 197 rows of the last block."""
+@pytest.mark.parametrize("fp8", [False, True])
+def test_vit_cls_prune_native_matches_full(fp8, monkeypatch):
+    """The native ViT with the class-token-only last block: loss and every parameter gradient
+    close to the same model computing all 197 rows of the last block (bf16: tight; fp8: the
+    delayed scales of the last block's GEMMs see the class rows only, so its e4m3 / e5m2
+    rounding differs -- looser)."""
     from pytorch_distributed_template_amd.models.vit import VisionTransformer
     torch.manual_seed(3)
-    m = VisionTransformer(depth=2, fp8=True).cuda().to(memory_format=torch.channels_last)
+    m = VisionTransformer(depth=2, fp8=fp8).cuda().to(memory_format=torch.channels_last)
     x = torch.randn(8, 3, 224, 224, device="cuda")
     y = torch.randint(0, 1000, (8,), device="cuda")
     res = {}
@@ -730,6 +733,7 @@ def test_vit_cls_prune_native_matches_full(monkeypatch):
         torch.cuda.synchronize()
         res[prune] = (float(loss), {n: p.grad.float().clone() for n, p in m.named_parameters()})
     assert abs(res["1"][0] - res["0"][0]) < 2e-2 * abs(res["0"][0]), (res["1"][0], res["0"][0])
+    tol = 0.25 if fp8 else 2e-2
     for n, g in res["0"][1].items():
         e = nrmerr(res["1"][1][n], g)
-        assert e < 0.1, (n, e)
+        assert e < tol, (n, e)
