@@ -116,6 +116,7 @@ _SIGS = {
     "pdt_add_bf16": (c_int, [P, P, P, c_long, P]),
     "pdt_attn_fwd": (c_int, [P, P, P, c_int, c_int, c_int, c_float, P]),
     "pdt_cls_attn_fwd": (c_int, [P, P, P, c_int, c_int, c_int, P]),
+    "pdt_gemm_ring": (c_int, [P] * 6 + [c_int] * 8 + [P]),
     "pdt_cls_attn_bwd": (c_int, [P, P, P, P, P, c_int, c_int, c_int, P]),
     "pdt_attn_fwd_f8": (c_int, [P, P, P, c_int, c_int, c_int, c_float, P]),
     "pdt_attn_fwd_tiles": (c_int, [P, P, P, c_int, c_int, c_int, c_float, P]),

@@ -69,10 +69,24 @@ def main():
         wq, dqw = no.quantize_fp8(w)
         best8 = (1e9, -1)
         for v in range(lib.pdt_gemm_f8_num_variants()):
-            t = timeit(lambda: no.gemm_f8(xq, wq, y, dqx, dqw, variant=v), a.iters)
+            try:
+                t = timeit(lambda: no.gemm_f8(xq, wq, y, dqx, dqw, variant=v), a.iters)
+            except no.NotApplicable:  # (the dense ring: N % 256 == 0)
+                continue
             best8 = min(best8, (t, v))
+        # the dense bf16 ring (csrc/gemm_ring.hip, groupings GM 4 / 8)
+        ring = (1e9, -1)
+        for sub in range(2):
+            if lib.pdt_gemm_ring(no._p(x), no._p(w), no._p(y), None, None, None, M, N, K, K, K, N, 0, sub,
+                                 no._s()) != 0:
+                continue
+            t = timeit(lambda: lib.pdt_gemm_ring(no._p(x), no._p(w), no._p(y), None, None, None, M, N, K, K, K, N, 0,
+                                                 sub, no._s()), a.iters)
+            ring = min(ring, (t, sub))
         t_q = timeit(lambda: no.quantize_fp8(x), a.iters)
         line = (f"M={M} N={N} K={K}: native bf16 {best[0] * 1e3:7.1f} us ({fl / best[0] / 1e9:6.0f} TF, v{best[1]})"
+                f" | ring bf16 " + (f"{ring[0] * 1e3:7.1f} us ({fl / ring[0] / 1e9:6.0f} TF, gm{4 * (1 + ring[1])})"
+                                      if ring[1] >= 0 else "n/a") +
                 f" | hipBLASLt bf16 {t_lib * 1e3:7.1f} us ({fl / t_lib / 1e9:6.0f} TF)"
                 f" | native fp8 {best8[0] * 1e3:7.1f} us ({fl / best8[0] / 1e9:6.0f} TF, v{best8[1]})"
                 f" | quantize x {t_q * 1e3:6.1f} us")
