@@ -42,18 +42,20 @@ sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 
 BASELINE_METRIC = "images/sec (whole node) ResNet-50 synthetic 3x224x224 at 1/2/4/8 MI355X"
 # Reference-equivalent stack (stock PyTorch-ROCm: autocast bf16, channels_last,
-# MIOpen convs/BN, torch SGD, DDP over a 1-rank RCCL group) measured on one MI355X
-# with this same harness (`bench.py --backend torch --batch B`), keyed by (model,
-# per-GPU batch), see BASELINE.md. Scaled by N for N GPUs (weak scaling). The bs 2048
-# point needs MIOpen's find db (profiles/miopen_db_bs2048, scripts/gpu_job.sh benchlong):
-# a cold find at that batch runs ~20 min, and immediate mode without it falls back to
-# naive kernels.
-STOCK_1GPU_IMG_S = {("resnet50", 256): 6605.4, ("resnet50", 512): 6863.8, ("resnet50", 2048): 6969.13,
-                    ("resnet152", 2048): 2842.36,
-                    ("vit_b_16", 256): 3547.25, ("vit_b_16", 1024): 4059.96}
+# MIOpen convs/BN, torch optimizers, torch.nn.parallel.DistributedDataParallel over a
+# 1-rank RCCL group -- the reference's wrapper, train.py:45-52) measured on one MI355X with
+# this same harness (`bench.py --backend torch --batch B`, 20 timed steps), keyed by (model,
+# per-GPU batch), see BASELINE.md. Scaled by N for N GPUs (weak scaling). The bs 2048 points
+# need MIOpen's find db (profiles/miopen_db_bs2048, scripts/gpu_job.sh benchlong): a cold
+# find at that batch runs ~20 min, and immediate mode without it falls back to naive kernels.
+# Round 5 (profiles/bench_runs_round5.jsonl, r5e / r5f): resnet50 2048, resnet152 2048,
+# vit_b_16 1024; the bs 256 / 512 points are round 2-3 measurements.
+STOCK_1GPU_IMG_S = {("resnet50", 256): 6605.4, ("resnet50", 512): 6863.8, ("resnet50", 2048): 6936.44,
+                    ("resnet152", 2048): 2852.86,
+                    ("vit_b_16", 256): 3547.25, ("vit_b_16", 1024): 4089.11}
 # The stock stack's BEST measured per-GPU throughput (and its batch): reported as
 # ``vs_best_stock``, never as ``vs_baseline``.
-STOCK_BEST_1GPU_IMG_S = {"resnet50": (6969.13, 2048), "resnet152": (2842.36, 2048), "vit_b_16": (4059.96, 1024)}
+STOCK_BEST_1GPU_IMG_S = {"resnet50": (6936.44, 2048), "resnet152": (2852.86, 2048), "vit_b_16": (4089.11, 1024)}
 # Per-GPU batch: 2048 images (82 GiB of the 288 GiB HBM3E; weak scaling, so the
 # 8-GPU job holds 16384 images). The stage-3/4 GEMMs (M = N*14*14, N*7*7) fill all
 # 256 CUs only from ~512 images up and every per-launch cost amortises over more
