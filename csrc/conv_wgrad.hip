@@ -432,7 +432,38 @@ static WGVar wg_variant(int v, int Mo, int No) {
 }
 
 // + 1: the 3x3 halo-patch kernel (id WG_NVAR; NOT_APPLICABLE (-5) outside stride-1 3x3 geometry)
-PDT_API int pdt_wgrad_num_variants() { return WG_NVAR + 1; }
+// + 2: the 256x256 ping-pong ring (id WG_RING, csrc/wgrad_ring.hip; Mo, No multiples of 256)
+constexpr int WG_RING = WG_NVAR + 1;
+PDT_API int pdt_wgrad_num_variants() { return WG_NVAR + 2; }
+PDT_API int pdt_wgrad_halo_id() { return WG_NVAR; }
+PDT_API int pdt_wgrad_ring_id() { return WG_RING; }
+PDT_API int pdt_wgrad_ring_ok(int Mo, int No, int C, int pix);
+PDT_API int pdt_wgrad_ring_launch(const void* dy, const void* x, float* slab, int M, int Mo, int No, int ldy,
+                                  int Hs, int Ws, int C, int Hm, int Wm, int sh, int sw, int oh0, int ow0, int dh,
+                                  int dw, int ntw, int splits, int ktiles_per_split, int pix, hipStream_t st);
+
+// the ring's split plan: one workgroup per CU, so the dispatch-wave model -- splits s <= the
+// k-tiles / 8 minimising (waves of tiles*s over the CUs) x (k-tiles per split)
+static int wgrad_ring_plan(int M, int Mo, int No, int* ktiles_per_split) {
+  const int tiles = (Mo / 256) * (No / 256);
+  const int nk = (M + BK - 1) / BK;
+  const long slots = pdt_num_cus();
+  int splits = 1;
+  long best_cost = -1;
+  for (int s = 1; s <= nk; ++s) {
+    const int kps = (nk + s - 1) / s;
+    if (s > 1 && kps < 8) break;
+    const int se = (nk + kps - 1) / kps;
+    const long cost = (((long)tiles * se + slots - 1) / slots) * kps;
+    if (best_cost < 0 || cost < best_cost) {
+      best_cost = cost;
+      splits = s;
+    }
+  }
+  const int kps = (nk + splits - 1) / splits;
+  *ktiles_per_split = kps;
+  return (nk + kps - 1) / kps;
+}
 
 // the BN-backward-apply instantiations: the 4-wave, 1/2-stage tiles (variants 0..11)
 static void launch_wg_bna(const WGVar& w, dim3 grid, const WGParams& p, hipStream_t stream) {
@@ -599,6 +630,10 @@ PDT_API int pdt_wgrad_plan2(int M, int Mo, int No, int Hs, int Ws, int C, int va
     const int rc = pdt_nt::halo_wgrad_plan(M, Mo, C, Hs, Ws, &splits, per_split);
     return rc ? rc : splits;
   }
+  if (variant == WG_RING) {
+    if (pdt_wgrad_ring_ok(Mo, No, C, 0) != 0) return -5;
+    return wgrad_ring_plan(M, Mo, No, per_split);
+  }
   return pdt_wgrad_plan(M, Mo, No, variant, per_split);
 }
 
@@ -652,6 +687,13 @@ PDT_API int pdt_conv_wgrad2(const void* dy, const void* x, float* slab, float* o
         Hm != Hs || Wm != Ws || (pix != 0 && pix != C) || ldy != Mo || bias_out != nullptr || M % Wm != 0)
       return -5;
     const int rc = pdt_nt::run_halo_wgrad(dy, x, slab, M, Mo, C, Hs, Ws, splits, ktiles_per_split, stream);
+    if (rc) return rc;
+    return pdt_wgrad_reduce(slab, out, nullptr, nullptr, splits, Mo, No, scale, accumulate, stream);
+  }
+  if (variant == WG_RING) {  // the 256x256 ping-pong ring (plain dY, no bias)
+    if (bna || bias_out != nullptr) return -5;
+    const int rc = pdt_wgrad_ring_launch(dy, x, slab, M, Mo, No, ldy, Hs, Ws, C, Hm, Wm, sh, sw, oh0, ow0, dh, dw, ntw,
+                                         splits, ktiles_per_split, pix, stream);
     if (rc) return rc;
     return pdt_wgrad_reduce(slab, out, nullptr, nullptr, splits, Mo, No, scale, accumulate, stream);
   }

@@ -74,6 +74,8 @@ _SIGS = {
     "pdt_wgrad_plan": (c_int, [c_int, c_int, c_int, c_int, ctypes.POINTER(c_int)]),
     "pdt_wgrad_plan2": (c_int, [c_int] * 7 + [ctypes.POINTER(c_int)]),
     "pdt_wgrad_num_variants": (c_int, []),
+    "pdt_wgrad_halo_id": (c_int, []),
+    "pdt_wgrad_ring_id": (c_int, []),
     "pdt_wgrad_workspace": (c_long, [c_int, c_int, c_int]),
     "pdt_wgrad_reduce": (c_int, [P, P, P, P, c_int, c_int, c_int, c_float, c_int, P]),
     "pdt_conv_wgrad": (c_int, [P, P, P, P] + [c_int] * 16 + [c_int, c_int, c_float, c_int, c_int, c_int, P, P]),

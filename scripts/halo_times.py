@@ -89,7 +89,7 @@ def main():
             assert rc == 0, ("wgrad", v, rc)
             res.append((timeit(fn), v))
         res.sort()
-        hv = lib.pdt_wgrad_num_variants() - 1
+        hv = lib.pdt_wgrad_halo_id()
         gen = [r for r in res if r[1] != hv]
         halo = [r for r in res if r[1] == hv]
         line = f"n={n} C={C:3d} H={H:2d} {'wgrad':10s} | generic v{gen[0][1]:2d} {gen[0][0]:8.1f} us " \

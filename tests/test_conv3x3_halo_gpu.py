@@ -120,7 +120,7 @@ def test_halo_wgrad(shape):
     ref = torch.nn.grad.conv2d_weight(x.float(), (Cout, Cin, 3, 3), dy.float(), 1, 1)
     wa = dict(M=N * H * W, Mo=Cout, No=9 * Cin, ldy=Cout, Hs=H, Ws=W, C=Cin, Hm=H, Wm=W, sh=1, sw=1, oh0=-1, ow0=-1,
               dh=1, dw=1, ntw=3)
-    hv = lib.pdt_wgrad_num_variants() - 1  # the halo variant is the last id
+    hv = lib.pdt_wgrad_halo_id()
     dw = torch.full((Cout, Cin, 3, 3), float("nan"), device="cuda").contiguous(memory_format=torch.channels_last)
     rc = no._wgrad_launch(lib, dy, x, dw, hv, 1.0, False, wa)
     assert rc == 0, rc

@@ -31,7 +31,10 @@ def _w_collectives(rank, world, port, q):
         pdist = _init(rank, world, port)
         out = {}
         out["rank"] = pdist.get_rank()
-        out["gather_obj"] = pdist.all_gather({"r": rank, "t": torch.tensor([rank])})
+        # tensors leave the rank as lists: a tensor in the result queue travels as a shared fd that
+        # the parent may try to fetch after this process has exited (EOFError under load)
+        out["gather_obj"] = [{"r": d["r"], "t": d["t"].tolist()}
+                             for d in pdist.all_gather({"r": rank, "t": torch.tensor([rank])})]
         t = torch.arange(rank + 2, dtype=torch.float32)  # variable length
         g = pdist.gather_tensors(t, dst=0)
         out["gather_t"] = None if g is None else [x.tolist() for x in g]
@@ -80,6 +83,7 @@ def test_collectives():
     res = _run(_w_collectives)
     r0, r1 = res[0], res[1]
     assert [d["r"] for d in r0["gather_obj"]] == [0, 1]
+    assert [d["t"] for d in r0["gather_obj"]] == [[0], [1]]
     assert r0["gather_t"] == [[0.0, 1.0], [0.0, 1.0, 2.0]] and r1["gather_t"] is None
     assert r0["reduce"] == 1.5      # (1+2)/2 on rank 0
     assert r1["bcast"] == {"x": 5}
