@@ -386,14 +386,14 @@ static int conv_nt_impl(const void* src, const void* b, void* out, float* stats,
   const int v = pdt_conv_nt_resolve_variant(variant, p.M, Ncol, K);
   p.nstat_rows = pdt_conv_nt_stat_rows(p.M, Ncol, K, v);
   if (ax.mode != 0) {
-    // the A-staging BN apply: stride-1 source walk, 64-channel k-tiles, dense pixels, 32-bit
-    // element offsets into the source
+    // the A-staging BN apply: stride-1 source walk, 64-channel k-tiles, dense pixels, unsigned
+    // 32-bit element offsets into the source (AX_NONE excluded)
     if (sh != 1 || sw != 1 || p.pix != Cs || Cs % 64 != 0 || bias != nullptr || aux != nullptr || act != 0 ||
         (addend != nullptr && bnb.part == nullptr) || ax.c1 == nullptr || ax.c2 == nullptr ||
         (ax.mode == 2 && (ax.y2 == nullptr || ax.c3 == nullptr || ax.mask_in == nullptr)) ||
         (ax.mode == 3 && (ax.y2 == nullptr || ax.c3 == nullptr || ax.rsc == nullptr || ax.rsh == nullptr)) ||
         (ax.mode == 1 && ax.y2 == nullptr && ax.rsc != nullptr) ||
-        (long long)Nimg * Hs * Ws * Cs >= (1LL << 31) || v >= NVAR)
+        (long long)Nimg * Hs * Ws * Cs >= (1LL << 32) - 8 || v >= NVAR)
       return -5;
     p.ax.ctr = -1;
     if (ax.dst != nullptr || ax.mask_out != nullptr) {
@@ -441,7 +441,7 @@ PDT_API int pdt_conv_nt_bnb(const void* src, const void* b, void* out, const voi
                             const void* bn_y, const float* bn_mean, const float* bn_scale, const float* bn_shift,
                             const void* bn_mask, float* part, int relu, int row0, int R, hipStream_t stream) {
   if (part == nullptr || bn_y == nullptr || bn_mean == nullptr) return -8;
-  if ((long long)Nimg * Ho * Wo * ldo >= (1LL << 31)) return -9;  // 32-bit element offsets in the epilogue
+  if ((long long)Nimg * Ho * Wo * ldo >= (1LL << 32)) return -9;  // unsigned 32-bit offsets in the BN-backward epilogue
   if (relu && bn_mask == nullptr && (bn_scale == nullptr || bn_shift == nullptr)) return -8;
   BnbArgs bnb{(const u16*)bn_y, bn_mean, bn_scale, bn_shift, (const uint8_t*)bn_mask, part, relu, row0, R};
   return conv_nt_impl(src, b, out, nullptr, nullptr, addend, addend_mask, Hs, Ws, Cs, Nimg, Hm, Wm, Ncol, K, ldb, sh,
@@ -462,7 +462,7 @@ PDT_API int pdt_conv_nt_bnb2(const void* src, const void* b, void* out, const vo
   if (part == nullptr || bn_y == nullptr || bn_mean == nullptr || bn_y2 == nullptr || bn_mean2 == nullptr ||
       part2 == nullptr)
     return -8;
-  if ((long long)Nimg * Ho * Wo * ldo >= (1LL << 31)) return -9;
+  if ((long long)Nimg * Ho * Wo * ldo >= (1LL << 32)) return -9;
   if (relu && bn_mask == nullptr && (bn_scale == nullptr || bn_shift == nullptr)) return -8;
   BnbArgs bnb{(const u16*)bn_y, bn_mean, bn_scale, bn_shift, (const uint8_t*)bn_mask, part, relu, row0, R,
               (const u16*)bn_y2, bn_mean2, part2};
@@ -493,7 +493,7 @@ PDT_API int pdt_conv_nt_ax3(const void* src, const void* b, void* out, float* st
   if (addend != nullptr && (ax_mode == 1 || part == nullptr)) return -8;
   if (part != nullptr && (bn_y == nullptr || bn_mean == nullptr)) return -8;
   if (part != nullptr && relu && bn_mask == nullptr && (bn_scale == nullptr || bn_shift == nullptr)) return -8;
-  if ((long long)Nimg * Ho * Wo * ldo >= (1LL << 31)) return -9;
+  if ((long long)Nimg * Ho * Wo * ldo >= (1LL << 32)) return -9;
   BnbArgs bnb{(const u16*)bn_y, bn_mean, bn_scale, bn_shift, (const uint8_t*)bn_mask, part, relu, row0, R};
   AXArgs ax{ax_mode, -1, (const u16*)ax_y2, ax_c1, ax_c2, ax_c3, ax_rsc, ax_rsh, (const uint8_t*)ax_mask_in,
             (uint8_t*)ax_mask_out, (u16*)ax_dst};

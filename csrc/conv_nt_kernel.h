@@ -49,6 +49,10 @@ struct BnbArgs {
 // from the k-tiles of tap `ctr`, the one that maps every output row onto its own source pixel.
 //   mode 2 (backward, conv3's dgrad):  A = c1*gate(src) + c2*y2 + c3   (src = dout, y2 = y3,
 //                                      gate = mask_in bit), dst = dy3 (the wgrad operand)
+// staged-chunk sentinel of the AX path (padding / rows past M); valid element offsets of the
+// source are < 2^32 - 8 (conv_nt_impl refuses larger sources for AX)
+constexpr uint32_t AX_NONE = 0xffffffffu;
+
 struct AXArgs {
   int mode;
   int ctr;  // the tap whose A chunks are the source pixels themselves (dst / mask_out written there)

@@ -385,8 +385,8 @@ PDT_API int pdt_avgpool_bwd(const void* dy, void* dx, int N, int HW, int C, hipS
 PDT_API int pdt_maxpool_bwd_bnred(const void* dy, const void* idx, void* dx, const void* y, const float* mean,
                                   const float* scale, const float* shift, float* part, int N, int H, int W, int C,
                                   int Ho, int Wo, int blocks, hipStream_t st) {
-  if (C != 64 || Ho != (H + 1) / 2 || Wo != (W + 1) / 2 || blocks < 1 || (long)N * ((H + 1) / 2) >= (1L << 31) ||
-      (long)N * H * W * C >= (1L << 31))
+  // (64-bit offsets: no element-count limit)
+  if (C != 64 || Ho != (H + 1) / 2 || Wo != (W + 1) / 2 || blocks < 1 || (long)N * ((H + 1) / 2) >= (1L << 31))
     return -5;
   hipLaunchKernelGGL(maxpool_bwd_k3s2_bnred_kernel, dim3(blocks), dim3(NT), 0, st, (const u16*)dy, (const uint8_t*)idx,
                      (u16*)dx, (const u16*)y, mean, scale, shift, part, N, H, W, Ho, Wo);

@@ -201,7 +201,7 @@ PDT_API int pdt_stem_fwd(const void* x4, const void* w256, void* y, float* part,
                          hipStream_t stream) {
   const int R = pdt_stem_fwd_rows(N, H, W, Cout);
   if (R < 0) return R;
-  if ((long long)N * H * W * 4 >= (1LL << 31) || (long long)N * (H / 2) * (W / 2) * 64 >= (1LL << 31)) return -5;
+  // (every global offset is 64-bit: no element-count limit)
   static const void* zcache[PDT_MAX_DEV] = {};
   StemParams p;
   p.x = (const u16*)x4;
@@ -590,7 +590,7 @@ PDT_API int pdt_stem_wgrad_v(const void* x4, const void* dA, const void* y, cons
                              int H, int W, int Cout, int variant, hipStream_t stream) {
   const int splits = pdt_stem_wgrad_splits_v(N, H, W, Cout, variant);
   if (splits < 0) return splits;
-  if ((long long)N * H * W * 4 >= (1LL << 31) || (long long)N * (H / 2) * (W / 2) * 64 >= (1LL << 31)) return -5;
+  // (every global offset is 64-bit: no element-count limit)
   static const void* zcache[PDT_MAX_DEV] = {};
   StemWgParams p;
   p.x = (const u16*)x4;

@@ -570,6 +570,12 @@ def _nt_args(src, b, out, stats, bias, a, act, variant, addend=None, aux=None, a
             int(a.get("pix", 0)), _s())
 
 
+# element-count limit of the unsigned 32-bit offsets in the A-staging BN apply (AX) and the fused
+# BN-backward epilogue (csrc/conv_nt_tile.inc): ResNet-152 stage-1 activations at 3072 images per
+# GPU (N x 56 x 56 x 256 = 2.47e9) are inside it; the rest of the conv path indexes in 64 bits
+_AX_MAX_ELEMS = 2 ** 32 - 8
+
+
 def _check_nt(src, b, out, a):
     assert src.dtype == torch.bfloat16 and b.dtype == torch.bfloat16 and out.dtype == torch.bfloat16
     Cs, K, Ncol, ldo, ldb = a["Cs"], a["K"], a["Ncol"], a["ldo"], a["ldb"]
@@ -582,7 +588,10 @@ def _check_nt(src, b, out, a):
     assert b.numel() >= Ncol * ldb or K == 0, "B too small"
     assert out.numel() >= a["Nimg"] * a["Ho"] * a["Wo"] * ldo, "out too small"
     assert a["Hm"] * a["osh"] <= a["Ho"] and a["Wm"] * a["osw"] <= a["Wo"]
-    assert a["Nimg"] * a["Hs"] * a["Ws"] * Cs < 2 ** 31 and a["Nimg"] * a["Ho"] * a["Wo"] < 2 ** 31
+    # pixel indices are 32-bit; element offsets are 64-bit except the A-staging BN apply and the
+    # BN-backward epilogue, which use unsigned 32-bit offsets (limit _AX_MAX_ELEMS, checked by the
+    # library: it refuses those paths beyond it)
+    assert a["Nimg"] * a["Hs"] * a["Ws"] < 2 ** 31 and a["Nimg"] * a["Ho"] * a["Wo"] < 2 ** 31
 
 
 _NT_KEYS: dict = {}  # geometry tuple -> tuned-table key string (built once per geometry)
@@ -1455,7 +1464,7 @@ def _conv_fwd_ax(pu: _Unit, xbuf, wb, N, H, W, Cs, Cout, g, with_stats):
     Ho, Wo = g["Ho"], g["Wo"]
     M = N * Ho * Wo
     if g["sh"] != 1 or g["sw"] != 1 or Ho != H or Wo != W or Cs != pu.Cout or Cs % 64 or Cout % 8 or \
-            N * H * W * Cs >= 2 ** 31 or not pu.relu:
+            N * H * W * Cs >= _AX_MAX_ELEMS or not pu.relu:
         return None
     lib = _load()
     y = _empty_cl(N, Cout, Ho, Wo, torch.bfloat16, xbuf.device)
@@ -1506,7 +1515,7 @@ def _conv2_dgrad_bn_bwd(da2, u2, k1, k2, k3, dy2, u1, bnb_mask=None, addend=None
     N, Cout, Ho, Wo = u2.y.shape
     Cin = u2.C
     if g["sh"] != 1 or g["sw"] != 1 or Ho != u2.H or Wo != u2.W or u2.Cs != Cin or Cout % 64 or u1.Cout != Cin or \
-            u2.mask is not None or not u2.relu or N * Ho * Wo * Cout >= 2 ** 31:
+            u2.mask is not None or not u2.relu or N * Ho * Wo * Cout >= _AX_MAX_ELEMS:
         return None
     KH, KW, ph, pw = g["KH"], g["KW"], g["ph"], g["pw"]
     lib = _load()

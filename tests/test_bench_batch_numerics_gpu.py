@@ -7,10 +7,13 @@ bench geometry. The fp32 references are computed with the convolutions chunked
 along the batch (per-image ops, so chunking is exact) and BatchNorm over the FULL
 batch, which keeps MIOpen on small, fast problems.
 
-* the stem node (conv 7x7/2 + BN + ReLU + max-pool) and layer1.0 (bottleneck with
-  downsample), forward and backward, vs fp32: relative Frobenius error no worse than
-  max(3 x the stock bf16 autocast error, 0.03) (the yardstick of
-  tests/test_bench_geometry_gpu.py);
+* the stem node (conv 7x7/2 + BN + ReLU + max-pool) and layer1.0 -> layer1.1 (bottleneck
+  with downsample, then one whose conv1 applies layer1.0's BN in its A staging), forward and
+  backward, vs fp32: relative Frobenius error no worse than max(3 x the stock bf16 autocast
+  error, 0.03) (the yardstick of tests/test_bench_geometry_gpu.py); also at 2752 images,
+  where the stem output and every 256-channel stage-1 tensor hold 2752 x 802 816 = 2.21e9
+  elements -- past 2^31 (the unsigned 32-bit offsets of the A-staging BN apply and of the
+  BN-backward epilogue, 64-bit everywhere else: ResNet-152 at 3072 images per GPU);
 * 3 SGD steps of the whole ResNet-50 at bs 2048 on the native kernels vs the same
   steps in fp32 on the stock ops: the loss trajectory agrees to 1 %.
 """
@@ -107,26 +110,33 @@ def _compare(name, fn, x, params, tol=0.03, need_dx=True):
     return out_n
 
 
-def _batch(i):
+def _batch(i, bs=BS):
     """The bench's batch: SyntheticImageNet samples, NHWC padded to 4 channels (pdt_nhwc_pad)."""
     from pytorch_distributed_template_amd.data.synthetic import SyntheticImageNet
-    x, y = SyntheticImageNet(BS * 4, seed=5, device="cuda").collate(list(range(i * BS, (i + 1) * BS)))
+    x, y = SyntheticImageNet(bs * 4, seed=5, device="cuda").collate(list(range(i * bs, (i + 1) * bs)))
     assert getattr(x, "pdt_nhwc_pad", None) == 4
     return x
 
 
-@pytest.mark.timeout(300)
-def test_resnet50_stem_and_layer1_0_at_bs2048_vs_fp32():
+@pytest.mark.timeout(900)
+@pytest.mark.parametrize("bs", [BS, 2752])
+def test_resnet50_stem_and_layer1_at_bench_batch_vs_fp32(bs):
     from pytorch_distributed_template_amd.models import resnet50
     torch.manual_seed(41)
     m = resnet50(num_classes=1000).cuda().to(memory_format=torch.channels_last)
-    x = _batch(0)
-    assert BS * 64 * 112 * 112 > 1.6e9  # the stem activation is within 24 % of 2^31 elements
-    stem = _compare("stem bs2048", lambda t: fused.conv_bn_relu_maxpool(t, m.conv1, m.bn1), x,
+    x = _batch(0, bs)
+    if bs == BS:
+        assert bs * 64 * 112 * 112 > 1.6e9  # the stem activation is within 24 % of 2^31 elements
+    else:
+        assert bs * 64 * 112 * 112 > 2 ** 31 and bs * 256 * 56 * 56 > 2 ** 31
+    stem = _compare(f"stem bs{bs}", lambda t: fused.conv_bn_relu_maxpool(t, m.conv1, m.bn1), x,
                     [m.conv1.weight, m.bn1.weight, m.bn1.bias], need_dx=False)
-    blk = m.layer1[0]
-    _compare("layer1.0 bs2048", lambda t: fused.bottleneck(t, blk), _cl(stem.to(torch.bfloat16)),
-             [blk.conv1.weight, blk.conv2.weight, blk.conv3.weight, blk.bn3.weight, blk.downsample[0].weight])
+    del x
+    b0, b1 = m.layer1[0], m.layer1[1]
+    _compare(f"layer1.0-1 bs{bs}", lambda t: fused.bottleneck_chain(t, [b0, b1]),
+             _cl(stem.to(torch.bfloat16)),
+             [b0.conv1.weight, b0.conv3.weight, b0.bn3.weight, b0.downsample[0].weight, b1.conv1.weight,
+              b1.conv2.weight, b1.bn1.weight])
 
 
 @pytest.mark.timeout(600)
