@@ -48,10 +48,10 @@ BASELINE_METRIC = "images/sec (whole node) ResNet-50 synthetic 3x224x224 at 1/2/
 # per-GPU batch), see BASELINE.md. Scaled by N for N GPUs (weak scaling). The bs 2048 points
 # need MIOpen's find db (profiles/miopen_db_bs2048, scripts/gpu_job.sh benchlong): a cold
 # find at that batch runs ~20 min, and immediate mode without it falls back to naive kernels.
-# Round 5 (profiles/bench_runs_round5.jsonl, r5e / r5f): resnet50 2048, resnet152 2048,
-# vit_b_16 1024; the bs 256 / 512 points are round 2-3 measurements.
+# Round 5 (profiles/bench_runs_round5.jsonl, r5e / r5f / r5n): resnet50 2048, resnet152 2048 and
+# 3072 (258.7 GiB), vit_b_16 1024; the bs 256 / 512 points are round 2-3 measurements.
 STOCK_1GPU_IMG_S = {("resnet50", 256): 6605.4, ("resnet50", 512): 6863.8, ("resnet50", 2048): 6936.44,
-                    ("resnet152", 2048): 2852.86,
+                    ("resnet152", 2048): 2852.86, ("resnet152", 3072): 2828.03,
                     ("vit_b_16", 256): 3547.25, ("vit_b_16", 1024): 4089.11}
 # The stock stack's BEST measured per-GPU throughput (and its batch): reported as
 # ``vs_best_stock``, never as ``vs_baseline``.
@@ -65,11 +65,11 @@ STOCK_BEST_1GPU_IMG_S = {"resnet50": (6936.44, 2048), "resnet152": (2852.86, 204
 # fp8: 6.46k img/s at 256, 6.96k at 512, 7.31k at 1024, 7.49k at 2048; bf16 5.38k at
 # 1024 (stock autocast: 3.55k at 256, 4.06k at 1024). At 256 the host-side issue
 # time (~35 ms) is close to the 40 ms step: the GPU idles between kernels.
-# ResNet-152 (BASELINE config 4, "per-GPU batch sized to 288 GB HBM"): 2560 images, 213 GiB --
-# the largest multiple of 256 whose stem activation (N x 112 x 112 x 64) stays under the kernels'
-# 2^31-element index limit (2730 images); 5.96k img/s vs 5.88k at 2048 (170.6 GiB), the stock stack
-# 2.84k at 2048 with the seeded MIOpen find db (profiles/bench_runs_round4.jsonl)
-DEFAULT_BATCH = {"resnet50": 2048, "resnet152": 2560, "vit_b_16": 1024}
+# ResNet-152 (BASELINE config 4, "per-GPU batch sized to 288 GB HBM"): 3072 images, 255.8 GiB of
+# the 268 GiB: 6.17k img/s (2560: 6.11k, 213 GiB; profiles/bench_runs_round5.jsonl r5l, r5f). The
+# stem and stage-1 tensors then hold 2.47e9 elements -- past 2^31: the conv path's offsets are
+# 64-bit or unsigned 32-bit (README "Performance")
+DEFAULT_BATCH = {"resnet50": 2048, "resnet152": 3072, "vit_b_16": 1024}
 # --graph: batches run eagerly and replayed (lr 0) before the timed run; losses must agree
 GRAPH_CHECK_STEPS = 3
 # --graph: relative difference allowed between the weight updates of one eager step and one
