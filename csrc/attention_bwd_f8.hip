@@ -106,21 +106,21 @@ __global__ void __launch_bounds__(512) attn_bwd_f8_kernel(AttnBwdF8Params p) {
   const int b = bh / p.H, h = bh % p.H;
 
   // ---------------------------------------------------------------- staging
-  float mx[4] = {0.f, 0.f, 0.f, 0.f};
+  // |x|max on the packed bf16 bits (2 magnitudes per v_pk_max_u16), delta with v_dot2 on the
+  // packed pairs: no unpacking in the staging pass
+  uint32_t mxb[4] = {0u, 0u, 0u, 0u};
 #pragma unroll
   for (int it = 0; it < NQP; ++it) {
     const int q = tid + 512 * it, row = q >> 3, ch = q & 7;
     const u32x4 a = rq[it], k = rk[it], v = rv[it], d = rd[it], o = ro[it];
-    float dl = 0.f;
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
-      mx[0] = fmaxf(mx[0], fmaxf(fabsf(lo_bf(a[e])), fabsf(hi_bf(a[e]))));
-      mx[1] = fmaxf(mx[1], fmaxf(fabsf(lo_bf(k[e])), fabsf(hi_bf(k[e]))));
-      mx[2] = fmaxf(mx[2], fmaxf(fabsf(lo_bf(v[e])), fabsf(hi_bf(v[e]))));
-      mx[3] = fmaxf(mx[3], fmaxf(fabsf(lo_bf(d[e])), fabsf(hi_bf(d[e]))));
-      dl += lo_bf(d[e]) * lo_bf(o[e]) + hi_bf(d[e]) * hi_bf(o[e]);
+      mxb[0] = absmax_bf16x2(mxb[0], a[e]);
+      mxb[1] = absmax_bf16x2(mxb[1], k[e]);
+      mxb[2] = absmax_bf16x2(mxb[2], v[e]);
+      mxb[3] = absmax_bf16x2(mxb[3], d[e]);
     }
-    dl = row8_sum(dl);  // delta of this row: the 8 lanes of the row (DPP)
+    const float dl = row8_sum(dot8_bf16(d, o, 0.f));  // delta of this row: the 8 lanes of the row (DPP)
     if (ch == 0) {
       dl_s[row] = dl;
       nlse_s[row] = -rl[it];
@@ -128,7 +128,7 @@ __global__ void __launch_bounds__(512) attn_bwd_f8_kernel(AttnBwdF8Params p) {
   }
 #pragma unroll
   for (int m = 0; m < 4; ++m) {
-    const float w = warp_max(mx[m]);
+    const float w = warp_max(absmax_bf16x2_value(mxb[m]));
     if (lane == 0) red[wave][m] = w;
   }
   __syncthreads();
@@ -140,15 +140,16 @@ __global__ void __launch_bounds__(512) attn_bwd_f8_kernel(AttnBwdF8Params p) {
     for (int w = 1; w < 8; ++w) a = fmaxf(a, red[w][m]);
     ex[m] = pow2_exp(a);
   }
-  const float sq = ldexpf(1.f, ex[0]), sk = ldexpf(1.f, ex[1]), sv = ldexpf(1.f, ex[2]), sd = ldexpf(1.f, ex[3]);
+  // quantisation divisors 2^-e (the scaled converts divide): codes of x * 2^e
+  const float sq = ldexpf(1.f, -ex[0]), sk = ldexpf(1.f, -ex[1]), sv = ldexpf(1.f, -ex[2]), sd = ldexpf(1.f, -ex[3]);
 #pragma unroll
   for (int it = 0; it < NQP; ++it) {
     const int q = tid + 512 * it, row = q >> 3, ch = q & 7;
     const int off = k8_off(row, ch >> 1) + (ch & 1) * 8;
-    auto put = [&](char* img, const u32x4& x, float s) __attribute__((always_inline)) {
+    auto put = [&](char* img, const u32x4& x, float sdiv) __attribute__((always_inline)) {
       uint2 w;
-      w.x = e4m3x4_ir(lo_bf(x[0]) * s, hi_bf(x[0]) * s, lo_bf(x[1]) * s, hi_bf(x[1]) * s);
-      w.y = e4m3x4_ir(lo_bf(x[2]) * s, hi_bf(x[2]) * s, lo_bf(x[3]) * s, hi_bf(x[3]) * s);
+      w.x = e4m3x4_bf16(x[0], x[1], sdiv);
+      w.y = e4m3x4_bf16(x[2], x[3], sdiv);
       *reinterpret_cast<uint2*>(img + off) = w;
     };
     put(Qi, rq[it], sq);
@@ -177,6 +178,10 @@ __global__ void __launch_bounds__(512) attn_bwd_f8_kernel(AttnBwdF8Params p) {
     const bool kok = key < p.T;
     const i32x8 kf = row_frag(Ki, key, hh);
     const i32x8 vf = row_frag(Vi, key, hh);
+    // Keys past T (lanes with !kok) are not masked per element: their K / V rows are zero, so
+    // their P / dS only reach dV / dK columns that are never stored and the phase-2 products
+    // with their zero K rows. What must hold: their dS codes are finite -- they are excluded
+    // from the tile's |dS|max and converted with a 2^127 divisor (code 0).
     f32x16 dvT[2], dkT[2];
 #pragma unroll
     for (int dn = 0; dn < 2; ++dn)
@@ -208,7 +213,7 @@ __global__ void __launch_bounds__(512) attn_bwd_f8_kernel(AttnBwdF8Params p) {
 #pragma unroll
           for (int e = 0; e < 4; ++e) {
             const int r = 4 * jj + e;
-            const float pr = kok ? __builtin_amdgcn_exp2f(fmaf(s[r], p.c, nl[e])) : 0.f;
+            const float pr = __builtin_amdgcn_exp2f(fmaf(s[r], p.c, nl[e]));
             pv[r] = pr;
             ds[r] = pr * (dp[r] - dl[e]);
             am = fmaxf(am, fabsf(ds[r]));
@@ -221,13 +226,15 @@ __global__ void __launch_bounds__(512) attn_bwd_f8_kernel(AttnBwdF8Params p) {
             p.dbg[((long)bh * ROWS + q) * ROWS + key] = ds[r];
           }
         }
-        const int e = pow2_exp(warp_max(am));  // one scale per 32 x 32 dS tile
+        const int e = pow2_exp(warp_max(kok ? am : 0.f));  // one scale per 32 x 32 dS tile
         de[u] = e;
-        const float sds = ldexpf(1.f, e);
+        // convert divisor: codes of dS * 2^e; 2^127 (codes 0) for the padded keys -- not inf: the
+        // scaled convert takes the divisor's exponent as an E8M0 scale, and inf's is the NaN code
+        const float sds = kok ? ldexpf(1.f, -e) : 0x1p127f;
 #pragma unroll
         for (int w = 0; w < 4; ++w) {
-          pc[u][w] = e4m3x4_ir(pv[4 * w] * 256.f, pv[4 * w + 1] * 256.f, pv[4 * w + 2] * 256.f, pv[4 * w + 3] * 256.f);
-          dc[u][w] = e4m3x4_ir(ds[4 * w] * sds, ds[4 * w + 1] * sds, ds[4 * w + 2] * sds, ds[4 * w + 3] * sds);
+          pc[u][w] = e4m3x4_div(pv[4 * w], pv[4 * w + 1], pv[4 * w + 2], pv[4 * w + 3], 1.f / 256.f);
+          dc[u][w] = e4m3x4_div(ds[4 * w], ds[4 * w + 1], ds[4 * w + 2], ds[4 * w + 3], sds);
           // dS^T image [key][q]: 4 consecutive queries 32 qt + 8 w + 4 hh of this key
           *reinterpret_cast<uint32_t*>(dSt + key * DSR + 32 * qt + 8 * w + 4 * hh) = dc[u][w];
         }

@@ -30,6 +30,48 @@ __device__ __forceinline__ uint32_t e4m3x4_ir(float a, float b, float c, float d
   return pdt_cvt4_e4m3_inrange(a, b, c, d);
 }
 
+// gfx950 scaled converts: v_cvt_scalef32_pk_fp8_{bf16,f32} round x / sdiv to e4m3 (they DIVIDE
+// by the scale operand: scripts/probes/cvt_scale_probe.hip; bit-identical to cvt(x * 2^e) for
+// sdiv = 2^-e). One instruction per pair instead of unpack + multiply + convert.
+typedef __bf16 bf16x2v __attribute__((ext_vector_type(2)));
+typedef short s16x2 __attribute__((ext_vector_type(2)));
+typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+// four bf16 (two packed words) -> four e4m3 codes of x / sdiv, element order kept
+__device__ __forceinline__ uint32_t e4m3x4_bf16(uint32_t w0, uint32_t w1, float sdiv) {
+  s16x2 r = __builtin_amdgcn_cvt_scalef32_pk_fp8_bf16(s16x2{0, 0}, __builtin_bit_cast(bf16x2v, w0), sdiv, false);
+  r = __builtin_amdgcn_cvt_scalef32_pk_fp8_bf16(r, __builtin_bit_cast(bf16x2v, w1), sdiv, true);
+  return __builtin_bit_cast(uint32_t, r);
+}
+// four floats -> four e4m3 codes of x / sdiv (in range by construction)
+__device__ __forceinline__ uint32_t e4m3x4_div(float a, float b, float c, float d, float sdiv) {
+  s16x2 r = __builtin_amdgcn_cvt_scalef32_pk_fp8_f32(s16x2{0, 0}, a, b, sdiv, false);
+  r = __builtin_amdgcn_cvt_scalef32_pk_fp8_f32(r, c, d, sdiv, true);
+  return __builtin_bit_cast(uint32_t, r);
+}
+// running |x|max of packed bf16 pairs on the bits: magnitudes compare as u16 (v_pk_max_u16)
+__device__ __forceinline__ uint32_t absmax_bf16x2(uint32_t m, uint32_t w) {
+  return __builtin_bit_cast(uint32_t, __builtin_elementwise_max(__builtin_bit_cast(u16x2, m),
+                                                                __builtin_bit_cast(u16x2, w & 0x7fff7fffu)));
+}
+// acc + sum over the 8 bf16 of a * b (fp32 products and sums, v_dot2c_f32_bf16 x 4). The operands
+// are bit-cast as WHOLE vectors and split with swizzles: hipcc 7.2 miscompiles
+// __builtin_amdgcn_fdot2_f32_bf16(__builtin_bit_cast(bf16x2, v[e]), ...) in an unrolled loop --
+// it loads one dword and feeds element 0 to all four calls. (An inline-asm v_dot2c also works
+// but hides its latency from the hazard recognizer: a following DPP read got 1 nop, not 2.)
+typedef __bf16 bf16x8v __attribute__((ext_vector_type(8)));
+__device__ __forceinline__ float dot8_bf16(const u32x4& a, const u32x4& b, float acc) {
+  const bf16x8v x = __builtin_bit_cast(bf16x8v, a), y = __builtin_bit_cast(bf16x8v, b);
+  acc = __builtin_amdgcn_fdot2_f32_bf16(x.s01, y.s01, acc, false);
+  acc = __builtin_amdgcn_fdot2_f32_bf16(x.s23, y.s23, acc, false);
+  acc = __builtin_amdgcn_fdot2_f32_bf16(x.s45, y.s45, acc, false);
+  return __builtin_amdgcn_fdot2_f32_bf16(x.s67, y.s67, acc, false);
+}
+// the float value of the larger of the two magnitudes
+__device__ __forceinline__ float absmax_bf16x2_value(uint32_t m) {
+  const uint32_t hi = m >> 16, lo = m & 0xffffu;
+  return __uint_as_float((hi > lo ? hi : lo) << 16);
+}
+
 // the 32-byte A / B fragment of a row image: row `row`, bytes 32 hh .. 32 hh + 31
 __device__ __forceinline__ i32x8 row_frag(const char* img, int row, int hh) {
   const u32x4 a = *reinterpret_cast<const u32x4*>(img + k8_off(row, 2 * hh));
