@@ -107,7 +107,8 @@ __global__ void __launch_bounds__(64 * NW) attn_fwd_f8_kernel(AttnF8Params p) {
   constexpr int VCH = VROWS * 8;
   constexpr int NIT = (VCH + NTH - 1) / NTH;
   u32x4 kv[NIT], vv[PV8 ? NIT : 1];
-  float kmax = 0.f, vmax = 0.f;
+  // |K|max / |V|max on the packed bf16 bits (pdt_f8::absmax_bf16x2: two magnitudes per u16 max)
+  uint32_t kmb = 0u, vmb = 0u;
 #pragma unroll
   for (int it = 0; it < NIT; ++it) {
     const int q = tid + it * NTH;
@@ -120,14 +121,15 @@ __global__ void __launch_bounds__(64 * NW) attn_fwd_f8_kernel(AttnF8Params p) {
     if constexpr (PV8) {
       vv[it] = v;
 #pragma unroll
-      for (int e = 0; e < 4; ++e) vmax = fmaxf(vmax, fmaxf(fabsf(lo_bf(v[e])), fabsf(hi_bf(v[e]))));
+      for (int e = 0; e < 4; ++e) vmb = pdt_f8::absmax_bf16x2(vmb, v[e]);
     } else if (q < CH) {
       *reinterpret_cast<u32x4*>(Vs + vt_off(row, ch * 16)) = v;
     }
     kv[it] = k;
 #pragma unroll
-    for (int e = 0; e < 4; ++e) kmax = fmaxf(kmax, fmaxf(fabsf(lo_bf(k[e])), fabsf(hi_bf(k[e]))));
+    for (int e = 0; e < 4; ++e) kmb = pdt_f8::absmax_bf16x2(kmb, k[e]);
   }
+  float kmax = pdt_f8::absmax_bf16x2_value(kmb), vmax = pdt_f8::absmax_bf16x2_value(vmb);
   float sk = 1.f, sv = 1.f;
   int ev = 0;
   if constexpr (F8) {
@@ -149,6 +151,7 @@ __global__ void __launch_bounds__(64 * NW) attn_fwd_f8_kernel(AttnF8Params p) {
     for (int w = 1; w < NW; ++w) vm = fmaxf(vm, vred[w]);
     ev = pdt_f8::pow2_exp(vm);
     sv = ldexpf(1.f, ev);
+    const float vdiv = ldexpf(1.f, -ev);  // the scaled converts divide: codes of V * 2^ev
 #pragma unroll
     for (int it = 0; it < NIT; ++it) {  // e4m3 V rows (zero rows up to the tile pair)
       const int q = tid + it * NTH;
@@ -156,8 +159,8 @@ __global__ void __launch_bounds__(64 * NW) attn_fwd_f8_kernel(AttnF8Params p) {
         const int row = q >> 3, ch = q & 7;
         const u32x4 v = vv[it];
         uint2 w;
-        w.x = pdt_cvt4_e4m3_inrange(lo_bf(v[0]) * sv, hi_bf(v[0]) * sv, lo_bf(v[1]) * sv, hi_bf(v[1]) * sv);
-        w.y = pdt_cvt4_e4m3_inrange(lo_bf(v[2]) * sv, hi_bf(v[2]) * sv, lo_bf(v[3]) * sv, hi_bf(v[3]) * sv);
+        w.x = pdt_f8::e4m3x4_bf16(v[0], v[1], vdiv);
+        w.y = pdt_f8::e4m3x4_bf16(v[2], v[3], vdiv);
         *reinterpret_cast<uint2*>(Vs + k8_off(row, ch >> 1) + (ch & 1) * 8) = w;
       }
     }
@@ -172,8 +175,8 @@ __global__ void __launch_bounds__(64 * NW) attn_fwd_f8_kernel(AttnF8Params p) {
       const int row = q >> 3, ch = q & 7;  // 8 bf16 -> 8 fp8 bytes: half of a 16-B fp8 chunk
       const u32x4 k = kv[it];
       uint2 w;
-      w.x = pdt_cvt4_e4m3_inrange(lo_bf(k[0]) * sk, hi_bf(k[0]) * sk, lo_bf(k[1]) * sk, hi_bf(k[1]) * sk);
-      w.y = pdt_cvt4_e4m3_inrange(lo_bf(k[2]) * sk, hi_bf(k[2]) * sk, lo_bf(k[3]) * sk, hi_bf(k[3]) * sk);
+      w.x = pdt_f8::e4m3x4_bf16(k[0], k[1], 1.f / sk);  // (sk a power of two: exact divisor)
+      w.y = pdt_f8::e4m3x4_bf16(k[2], k[3], 1.f / sk);
       *reinterpret_cast<uint2*>(Ks + k8_off(row, ch >> 1) + (ch & 1) * 8) = w;
     }
   }
@@ -200,21 +203,19 @@ __global__ void __launch_bounds__(64 * NW) attn_fwd_f8_kernel(AttnF8Params p) {
     }
     float sq = 1.f;
     if constexpr (F8) {
-      float qm = 0.f;
+      uint32_t qmb = 0u;
 #pragma unroll
       for (int c = 0; c < 4; ++c)
 #pragma unroll
-        for (int e = 0; e < 4; ++e) qm = fmaxf(qm, fmaxf(fabsf(lo_bf(qv[c][e])), fabsf(hi_bf(qv[c][e]))));
-      qm = warp_max(qm);
+        for (int e = 0; e < 4; ++e) qmb = pdt_f8::absmax_bf16x2(qmb, qv[c][e]);
+      const float qm = warp_max(pdt_f8::absmax_bf16x2_value(qmb));
       sq = pow2_scale(qm);
     }
     i32x8 qf;
 #pragma unroll
     for (int c = 0; c < (F8 ? 4 : 0); ++c) {
-      qf[2 * c] = (int)pdt_cvt4_e4m3_inrange(lo_bf(qv[c][0]) * sq, hi_bf(qv[c][0]) * sq, lo_bf(qv[c][1]) * sq,
-                                 hi_bf(qv[c][1]) * sq);
-      qf[2 * c + 1] = (int)pdt_cvt4_e4m3_inrange(lo_bf(qv[c][2]) * sq, hi_bf(qv[c][2]) * sq, lo_bf(qv[c][3]) * sq,
-                                     hi_bf(qv[c][3]) * sq);
+      qf[2 * c] = (int)pdt_f8::e4m3x4_bf16(qv[c][0], qv[c][1], 1.f / sq);
+      qf[2 * c + 1] = (int)pdt_f8::e4m3x4_bf16(qv[c][2], qv[c][3], 1.f / sq);
     }
     // scores in the log2 domain: c * S = (c / (sk sq)) * S_fp8
     const float cs = p.c / (sk * sq);
@@ -269,8 +270,8 @@ __global__ void __launch_bounds__(64 * NW) attn_fwd_f8_kernel(AttnF8Params p) {
           }
 #pragma unroll
           for (int w = 0; w < 4; ++w)
-            pc[u][w] = pdt_cvt4_e4m3_inrange(s2[u][4 * w] * 256.f, s2[u][4 * w + 1] * 256.f, s2[u][4 * w + 2] * 256.f,
-                                 s2[u][4 * w + 3] * 256.f);
+            pc[u][w] = pdt_f8::e4m3x4_div(s2[u][4 * w], s2[u][4 * w + 1], s2[u][4 * w + 2], s2[u][4 * w + 3],
+                                          1.f / 256.f);
         }
         ls = xor32_reduce(ls, AddOp{});
         l = l * alpha + ls;
