@@ -258,19 +258,26 @@ __global__ void __launch_bounds__(256) gelu_dual_cast_kernel(const u16* __restri
 // GG: x is a GEMM's (g W) and zz the GELU pre-activation of the same shape -- the values cast
 // and summed are x * gelu'(zz) (the MLP fc1 output gradient, when the fc2 data gradient runs on
 // the library GEMM without the act-3 epilogue).
+// RG > 1 row groups (RG * cols / 8 <= blockDim): thread (g, c8) walks rows r0 + g, r0 + g + RG,
+// ... -- a block keeps RG times the loads in flight (96 threads per band at cols = 768 left the
+// cast latency-bound at ~1.7 TB/s); the groups' column sums are added in group order through LDS.
 template <int FMT, bool GG = false>
 __global__ void __launch_bounds__(1024) cast_fp8_delayed_cs_kernel(const u16* __restrict__ x, int rows, int cols,
                                                                    int rpb, float* __restrict__ meta,
                                                                    uint8_t* __restrict__ q, float* __restrict__ cpart,
-                                                                   const u16* __restrict__ zz = nullptr) {
+                                                                   const u16* __restrict__ zz = nullptr, int RG = 1) {
   __shared__ float red[16];
+  __shared__ f32x4 csh[1024 * 2];  // [RG][c8n][8] column partials (RG * c8n <= 1024)
   const float s = meta[0];
   const int c8n = cols / 8;
   const int r0 = blockIdx.x * rpb, r1 = min(rows, r0 + rpb);
   float m = 0.f;
-  for (int c8 = threadIdx.x; c8 < c8n; c8 += blockDim.x) {  // (one trip when cols <= 8 * blockDim)
+  const int g = RG > 1 ? (int)threadIdx.x / c8n : 0;
+  const int c8first = RG > 1 ? (int)threadIdx.x - g * c8n : (int)threadIdx.x;
+  const int c8step = RG > 1 ? c8n : (int)blockDim.x;  // RG > 1: one chunk per thread
+  for (int c8 = c8first; c8 < c8n && g < RG; c8 += c8step) {  // (one trip when cols <= 8 * blockDim)
     float cs[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-    int r = r0;
+    int r = r0 + g;
     auto row = [&](const u32x4& w, const u32x4& zw, long base) __attribute__((always_inline)) {
       float v[8];
 #pragma unroll
@@ -298,25 +305,43 @@ __global__ void __launch_bounds__(1024) cast_fp8_delayed_cs_kernel(const u16* __
       o.y = cvt4<FMT>(v[4] * s, v[5] * s, v[6] * s, v[7] * s);
       *reinterpret_cast<uint2*>(q + base) = o;
     };
-    for (; r + 3 < r1; r += 4) {  // four rows' loads in flight before any is used
+    for (; r + 3 * RG < r1; r += 4 * RG) {  // four rows' loads in flight before any is used
       u32x4 w[4], zw[4];
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
-        w[u] = *reinterpret_cast<const u32x4*>(x + (long)(r + u) * cols + c8 * 8);
-        if constexpr (GG) zw[u] = *reinterpret_cast<const u32x4*>(zz + (long)(r + u) * cols + c8 * 8);
+        w[u] = *reinterpret_cast<const u32x4*>(x + (long)(r + u * RG) * cols + c8 * 8);
+        if constexpr (GG) zw[u] = *reinterpret_cast<const u32x4*>(zz + (long)(r + u * RG) * cols + c8 * 8);
       }
 #pragma unroll
-      for (int u = 0; u < 4; ++u) row(w[u], zw[u], (long)(r + u) * cols + c8 * 8);
+      for (int u = 0; u < 4; ++u) row(w[u], zw[u], (long)(r + u * RG) * cols + c8 * 8);
     }
-    for (; r < r1; ++r) {
+    for (; r < r1; r += RG) {
       const long base = (long)r * cols + c8 * 8;
       u32x4 zw{};
       if constexpr (GG) zw = *reinterpret_cast<const u32x4*>(zz + base);
       row(*reinterpret_cast<const u32x4*>(x + base), zw, base);
     }
-    float* cp = cpart + (long)blockIdx.x * cols + c8 * 8;
-    *reinterpret_cast<f32x4*>(cp) = f32x4{cs[0], cs[1], cs[2], cs[3]};
-    *reinterpret_cast<f32x4*>(cp + 4) = f32x4{cs[4], cs[5], cs[6], cs[7]};
+    if (RG > 1) {
+      csh[2 * threadIdx.x] = f32x4{cs[0], cs[1], cs[2], cs[3]};
+      csh[2 * threadIdx.x + 1] = f32x4{cs[4], cs[5], cs[6], cs[7]};
+    } else {
+      float* cp = cpart + (long)blockIdx.x * cols + c8 * 8;
+      *reinterpret_cast<f32x4*>(cp) = f32x4{cs[0], cs[1], cs[2], cs[3]};
+      *reinterpret_cast<f32x4*>(cp + 4) = f32x4{cs[4], cs[5], cs[6], cs[7]};
+    }
+  }
+  if (RG > 1) {  // the band's column sums: row groups added in group order
+    __syncthreads();
+    if ((int)threadIdx.x < c8n) {
+      f32x4 a = csh[2 * threadIdx.x], b = csh[2 * threadIdx.x + 1];
+      for (int k = 1; k < RG; ++k) {
+        a += csh[2 * (k * c8n + threadIdx.x)];
+        b += csh[2 * (k * c8n + threadIdx.x) + 1];
+      }
+      float* cp = cpart + (long)blockIdx.x * cols + threadIdx.x * 8;
+      *reinterpret_cast<f32x4*>(cp) = a;
+      *reinterpret_cast<f32x4*>(cp + 4) = b;
+    }
   }
   m = warp_max(m);
   const int nw = (blockDim.x + 63) / 64;
@@ -464,6 +489,25 @@ PDT_API int pdt_wgrad_reduce_rows(const float* rows, float* out, int nrows, int 
                                   float* work, hipStream_t stream);
 PDT_API long pdt_reduce_rows_work(int nrows, int n);
 
+// block shape of the column-summing casts: one thread per 8-column chunk, times up to 8 row groups
+// (PDT_CAST_CS_RG=1: the previous one-row-walker-per-chunk shape, for A/B runs)
+static void cs_block(int cols, int* nt, int* rg) {
+  static int env = -1;
+  if (env < 0) {
+    const char* e = getenv("PDT_CAST_CS_RG");
+    env = e ? atoi(e) : 0;
+  }
+  const int c8n = cols / 8;
+  int g = c8n <= 1024 ? 1024 / c8n : 1;
+  if (g > 8) g = 8;
+  if (env >= 1 && env < g) g = env;
+  if (g < 1) g = 1;
+  const int n = g > 1 ? c8n * g : c8n;
+  *nt = ((n + 63) / 64) * 64;
+  if (*nt > 1024) *nt = 1024;
+  *rg = g;
+}
+
 // row bands of pdt_cast_fp8_delayed_cs (its cpart holds that many rows of cols floats, followed
 // by pdt_reduce_rows_work(bands, cols) floats of reduce workspace)
 PDT_API int pdt_cast_cs_bands(int rows) {
@@ -479,15 +523,14 @@ PDT_API int pdt_cast_fp8_delayed_cs(const void* x, int rows, int cols, float* me
   const int nb = pdt_cast_cs_bands(rows);
   const int rpb = (rows + nb - 1) / nb;
   const u16* X = (const u16*)x;
-  // one thread per 8-column chunk (wave-rounded, at most 1024)
-  int nt = ((cols / 8 + 63) / 64) * 64;
-  if (nt > 1024) nt = 1024;
+  int nt, rg;
+  cs_block(cols, &nt, &rg);
   if (fmt == 0)
     hipLaunchKernelGGL(cast_fp8_delayed_cs_kernel<0>, dim3(nb), dim3(nt), 0, st, X, rows, cols, rpb, meta,
-                       (uint8_t*)q, cpart);
+                       (uint8_t*)q, cpart, nullptr, rg);
   else
     hipLaunchKernelGGL(cast_fp8_delayed_cs_kernel<1>, dim3(nb), dim3(nt), 0, st, X, rows, cols, rpb, meta,
-                       (uint8_t*)q, cpart);
+                       (uint8_t*)q, cpart, nullptr, rg);
   if (fmt == 0) hipLaunchKernelGGL(fp8_meta_roll_kernel<0>, dim3(1), dim3(64), 0, st, meta, dq_out);
   else hipLaunchKernelGGL(fp8_meta_roll_kernel<1>, dim3(1), dim3(64), 0, st, meta, dq_out);
   const int e = (int)hipGetLastError();
@@ -502,14 +545,14 @@ PDT_API int pdt_cast_fp8_gelu_grad_cs(const void* x, const void* z, int rows, in
   if (cols % 8 != 0 || rows < 1 || !z || !cpart || !bias_out) return -1;
   const int nb = pdt_cast_cs_bands(rows);
   const int rpb = (rows + nb - 1) / nb;
-  int nt = ((cols / 8 + 63) / 64) * 64;
-  if (nt > 1024) nt = 1024;
+  int nt, rg;
+  cs_block(cols, &nt, &rg);
   if (fmt == 0)
     hipLaunchKernelGGL((cast_fp8_delayed_cs_kernel<0, true>), dim3(nb), dim3(nt), 0, st, (const u16*)x, rows, cols,
-                       rpb, meta, (uint8_t*)q, cpart, (const u16*)z);
+                       rpb, meta, (uint8_t*)q, cpart, (const u16*)z, rg);
   else
     hipLaunchKernelGGL((cast_fp8_delayed_cs_kernel<1, true>), dim3(nb), dim3(nt), 0, st, (const u16*)x, rows, cols,
-                       rpb, meta, (uint8_t*)q, cpart, (const u16*)z);
+                       rpb, meta, (uint8_t*)q, cpart, (const u16*)z, rg);
   if (fmt == 0) hipLaunchKernelGGL(fp8_meta_roll_kernel<0>, dim3(1), dim3(64), 0, st, meta, dq_out);
   else hipLaunchKernelGGL(fp8_meta_roll_kernel<1>, dim3(1), dim3(64), 0, st, meta, dq_out);
   const int e = (int)hipGetLastError();

@@ -737,3 +737,32 @@ def test_vit_cls_prune_native_matches_full(fp8, monkeypatch):
     for n, g in res["0"][1].items():
         e = nrmerr(res["1"][1][n], g)
         assert e < tol, (n, e)
+
+
+@pytest.mark.parametrize("rows,cols,fmt", [(50432, 768, 1), (4001, 2304, 1), (1000, 3072, 0), (777, 8, 1)])
+def test_cast_fp8_delayed_colsum(rows, cols, fmt):
+    """pdt_cast_fp8_delayed_cs (row-grouped blocks, csrc/fp8.hip): codes bit-identical to the plain
+    delayed cast from the same scaling state, the same amax-history roll, and column sums of
+    the bf16 input (the bias gradient) against fp32."""
+    torch.manual_seed(rows + cols)
+    lib = no._load()
+    x = (torch.randn(rows, cols, device="cuda") * 3).to(torch.bfloat16)
+    _, _, meta = no.quantize_fp8_delayed(x, None, fmt)
+    meta_a, meta_b = meta.clone(), meta.clone()
+    q_ref = torch.empty(rows, cols, dtype=torch.uint8, device="cuda")
+    dq_ref = torch.empty(1, dtype=torch.float32, device="cuda")
+    no._chk(lib.pdt_cast_fp8_delayed(no._p(x), 1, x.numel(), no._p(meta_a), fmt, no._p(q_ref), no._p(dq_ref),
+                                     no._s()), "cast_fp8_delayed")
+    nb = lib.pdt_cast_cs_bands(rows)
+    cpart = torch.empty(nb * cols + lib.pdt_reduce_rows_work(nb, cols), dtype=torch.float32, device="cuda")
+    q = torch.empty(rows, cols, dtype=torch.uint8, device="cuda")
+    dq = torch.empty(1, dtype=torch.float32, device="cuda")
+    db = torch.empty(cols, dtype=torch.float32, device="cuda")
+    no._chk(lib.pdt_cast_fp8_delayed_cs(no._p(x), rows, cols, no._p(meta_b), fmt, no._p(q), no._p(dq), no._p(cpart),
+                                        no._p(db), no._s()), "cast_fp8_delayed_cs")
+    torch.cuda.synchronize()
+    assert torch.equal(q, q_ref)
+    assert torch.equal(dq, dq_ref)
+    assert torch.equal(meta_a, meta_b)
+    ref = x.float().sum(0)
+    assert ((db - ref).norm() / ref.norm()).item() < 1e-5
