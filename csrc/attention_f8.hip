@@ -354,28 +354,44 @@ __global__ void __launch_bounds__(64 * NW) attn_fwd_f8_kernel(AttnF8Params p) {
         }
       }
     }
-    // o[dt][r] = O^T[d = 32 dt + (r & 3) + 8 (r >> 2) + 4 hh][query q]
-    if (q < p.T) {
+    // o[dt][r] = O^T[d = 32 dt + (r & 3) + 8 (r >> 2) + 4 hh][query q]: lane (q, hh) holds 4 of
+    // each 8-column chunk, lane (q, 1 - hh) = lane ^ 32 the other 4. One v_permlane32_swap per
+    // dword of two chunks g4 (even), g4 + 1 gives lane hh = 0 chunk g4's 8 columns and lane
+    // hh = 1 chunk g4 + 1's: 16-B O stores and 8-B code stores instead of 8-B / 4-B ones (a
+    // row-per-lane epilogue is store-issue-bound). The swaps run with the full EXEC (lanes
+    // q >= T hold finite values: their Q rows are zero); only the stores are predicated.
+    {
+      const bool qok = q < p.T;
       const float inv = 1.f / l;
-      const long orow_off = ((long)b * p.T + q) * p.ldo + h * D;
+      const long orow_off = ((long)b * p.T + (qok ? q : 0)) * p.ldo + h * D;
       u16* orow = p.out + orow_off;
+      const float s8 = p.q8 != nullptr ? p.q8_meta[0] : 0.f;
 #pragma unroll
       for (int dt = 0; dt < 2; ++dt)
 #pragma unroll
-        for (int g4 = 0; g4 < 4; ++g4) {
-          uint2 w;
-          w.x = pack2bf(o[dt][4 * g4] * inv, o[dt][4 * g4 + 1] * inv);
-          w.y = pack2bf(o[dt][4 * g4 + 2] * inv, o[dt][4 * g4 + 3] * inv);
-          *reinterpret_cast<uint2*>(orow + 32 * dt + 8 * g4 + 4 * hh) = w;
+        for (int g2 = 0; g2 < 4; g2 += 2) {
+          uint32_t w[2][2], c8[2];
+#pragma unroll
+          for (int u = 0; u < 2; ++u) {
+            const int g4 = g2 + u;
+            w[u][0] = pack2bf(o[dt][4 * g4] * inv, o[dt][4 * g4 + 1] * inv);
+            w[u][1] = pack2bf(o[dt][4 * g4 + 2] * inv, o[dt][4 * g4 + 3] * inv);
+            if (p.q8 != nullptr) {
+              const float f0 = lo_bf(w[u][0]), f1 = hi_bf(w[u][0]), f2 = lo_bf(w[u][1]), f3 = hi_bf(w[u][1]);
+              if (qok) q8max = fmaxf(q8max, fmaxf(fmaxf(fabsf(f0), fabsf(f1)), fmaxf(fabsf(f2), fabsf(f3))));
+              c8[u] = cvt4_e4m3(f0 * s8, f1 * s8, f2 * s8, f3 * s8);
+            }
+          }
+          const auto r0 = __builtin_amdgcn_permlane32_swap(w[0][0], w[1][0], false, false);
+          const auto r1 = __builtin_amdgcn_permlane32_swap(w[0][1], w[1][1], false, false);
+          const int col0 = 32 * dt + 8 * (g2 + hh);
+          if (qok) *reinterpret_cast<u32x4*>(orow + col0) = u32x4{r0[0], r1[0], r0[1], r1[1]};
           if (p.q8 != nullptr) {
-            const float s8 = p.q8_meta[0];
-            const float f0 = lo_bf(w.x), f1 = hi_bf(w.x), f2 = lo_bf(w.y), f3 = hi_bf(w.y);
-            q8max = fmaxf(q8max, fmaxf(fmaxf(fabsf(f0), fabsf(f1)), fmaxf(fabsf(f2), fabsf(f3))));
-            *reinterpret_cast<uint32_t*>(p.q8 + orow_off + 32 * dt + 8 * g4 + 4 * hh) =
-                cvt4_e4m3(f0 * s8, f1 * s8, f2 * s8, f3 * s8);
+            const auto rc = __builtin_amdgcn_permlane32_swap(c8[0], c8[1], false, false);
+            if (qok) *reinterpret_cast<uint2*>(p.q8 + orow_off + col0) = uint2{rc[0], rc[1]};
           }
         }
-      if (hh == 0) p.lse[(long)bh * p.T + q] = m + log2f(l);
+      if (qok && hh == 0) p.lse[(long)bh * p.T + q] = m + log2f(l);
     }
   }
   if (p.q8 != nullptr) {  // workgroup max |O| (all waves reach this after their query tiles)
