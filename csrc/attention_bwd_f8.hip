@@ -256,21 +256,34 @@ __global__ void __launch_bounds__(512) attn_bwd_f8_kernel(AttnBwdF8Params p) {
         dkT[dn] = mfma8(qa, sf, dkT[dn], dq_q, sb_ds);
       }
     }
-    // dK^T / dV^T[d = 32 dn + 8 jj + 4 hh + e][key]: 4 consecutive d per store
-    if (kok) {
-      u16* drow = p.dqkv + ((long)b * p.T + key) * p.ld + h * D;
+    // dK^T / dV^T[d = 32 dn + 8 jj + 4 hh + e][key]: lane (key, hh) holds 4 of each 8-d chunk,
+    // lane ^ 32 the other 4; a v_permlane32_swap per dword of chunks jj (even), jj + 1 gives
+    // lane hh chunk jj + hh whole: 16-B stores (the swaps run with the full EXEC; only the
+    // stores of keys past T are predicated off)
+    {
+      u16* drow = p.dqkv + ((long)b * p.T + (kok ? key : 0)) * p.ld + h * D;
 #pragma unroll
       for (int dn = 0; dn < 2; ++dn)
 #pragma unroll
-        for (int jj = 0; jj < 4; ++jj) {
-          const int d0 = 32 * dn + 8 * jj + 4 * hh;
-          uint2 wk, wv;
-          wk.x = pack2bf(dkT[dn][4 * jj] * p.scale, dkT[dn][4 * jj + 1] * p.scale);
-          wk.y = pack2bf(dkT[dn][4 * jj + 2] * p.scale, dkT[dn][4 * jj + 3] * p.scale);
-          wv.x = pack2bf(dvT[dn][4 * jj], dvT[dn][4 * jj + 1]);
-          wv.y = pack2bf(dvT[dn][4 * jj + 2], dvT[dn][4 * jj + 3]);
-          *reinterpret_cast<uint2*>(drow + p.H * D + d0) = wk;
-          *reinterpret_cast<uint2*>(drow + 2 * p.H * D + d0) = wv;
+        for (int j2 = 0; j2 < 4; j2 += 2) {
+          uint32_t wk[2][2], wv[2][2];
+#pragma unroll
+          for (int u = 0; u < 2; ++u) {
+            const int jj = j2 + u;
+            wk[u][0] = pack2bf(dkT[dn][4 * jj] * p.scale, dkT[dn][4 * jj + 1] * p.scale);
+            wk[u][1] = pack2bf(dkT[dn][4 * jj + 2] * p.scale, dkT[dn][4 * jj + 3] * p.scale);
+            wv[u][0] = pack2bf(dvT[dn][4 * jj], dvT[dn][4 * jj + 1]);
+            wv[u][1] = pack2bf(dvT[dn][4 * jj + 2], dvT[dn][4 * jj + 3]);
+          }
+          const auto k0 = __builtin_amdgcn_permlane32_swap(wk[0][0], wk[1][0], false, false);
+          const auto k1 = __builtin_amdgcn_permlane32_swap(wk[0][1], wk[1][1], false, false);
+          const auto v0 = __builtin_amdgcn_permlane32_swap(wv[0][0], wv[1][0], false, false);
+          const auto v1 = __builtin_amdgcn_permlane32_swap(wv[0][1], wv[1][1], false, false);
+          const int d0 = 32 * dn + 8 * (j2 + hh);
+          if (kok) {
+            *reinterpret_cast<u32x4*>(drow + p.H * D + d0) = u32x4{k0[0], k1[0], k0[1], k1[1]};
+            *reinterpret_cast<u32x4*>(drow + 2 * p.H * D + d0) = u32x4{v0[0], v1[0], v0[1], v1[1]};
+          }
         }
     }
   }
@@ -299,14 +312,21 @@ __global__ void __launch_bounds__(512) attn_bwd_f8_kernel(AttnBwdF8Params p) {
       acc = mfma8(ka, sb, acc, dq_k, tsc[qt * NT2 + kt]);
     }
     const int q = 32 * qt + col;
-    if (q < p.T) {
-      u16* drow = p.dqkv + ((long)b * p.T + q) * p.ld + h * D;
+    {  // dQ^T[d = 32 dn + 8 jj + 4 hh + e][q]: the same lane-pair exchange, 16-B stores
+      const bool qok = q < p.T;
+      u16* drow = p.dqkv + ((long)b * p.T + (qok ? q : 0)) * p.ld + h * D;
 #pragma unroll
-      for (int jj = 0; jj < 4; ++jj) {
-        uint2 w;
-        w.x = pack2bf(acc[4 * jj] * p.scale, acc[4 * jj + 1] * p.scale);
-        w.y = pack2bf(acc[4 * jj + 2] * p.scale, acc[4 * jj + 3] * p.scale);
-        *reinterpret_cast<uint2*>(drow + 32 * dn + 8 * jj + 4 * hh) = w;
+      for (int j2 = 0; j2 < 4; j2 += 2) {
+        uint32_t w[2][2];
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+          const int jj = j2 + u;
+          w[u][0] = pack2bf(acc[4 * jj] * p.scale, acc[4 * jj + 1] * p.scale);
+          w[u][1] = pack2bf(acc[4 * jj + 2] * p.scale, acc[4 * jj + 3] * p.scale);
+        }
+        const auto r0 = __builtin_amdgcn_permlane32_swap(w[0][0], w[1][0], false, false);
+        const auto r1 = __builtin_amdgcn_permlane32_swap(w[0][1], w[1][1], false, false);
+        if (qok) *reinterpret_cast<u32x4*>(drow + 32 * dn + 8 * (j2 + hh)) = u32x4{r0[0], r1[0], r0[1], r1[1]};
       }
     }
   }
