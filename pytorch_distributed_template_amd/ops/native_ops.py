@@ -3300,6 +3300,8 @@ class _ClsAttention(torch.autograd.Function):
     def forward(ctx, qkv, H):
         B, T, D3 = qkv.shape
         qkv = qkv.contiguous()
+        if qkv.data_ptr() % 16:  # the kernels read 16-B chunks
+            qkv = qkv.clone()
         o = torch.empty((B, 1, D3 // 3), dtype=torch.bfloat16, device=qkv.device)
         lse = torch.empty(B * H, dtype=torch.float32, device=qkv.device)
         _chk(_load().pdt_cls_attn_fwd(_p(qkv), _p(o), _p(lse), B, T, H, _s()), "cls_attn_fwd")
@@ -3312,6 +3314,8 @@ class _ClsAttention(torch.autograd.Function):
         qkv, o, lse = ctx.saved_tensors
         B, T, _ = qkv.shape
         do = do.to(torch.bfloat16).contiguous()
+        if do.data_ptr() % 16:  # the kernel reads 16-B chunks
+            do = do.clone()
         dqkv = torch.empty_like(qkv)
         _chk(_load().pdt_cls_attn_bwd(_p(qkv), _p(o), _p(do), _p(lse), _p(dqkv), B, T, ctx.H, _s()), "cls_attn_bwd")
         return dqkv, None

@@ -683,7 +683,7 @@ def test_ring_fused_epilogues(act, qfmt, cs):
         assert nrmerr(csum, out.float().sum(0)) < 1e-3, nrmerr(csum, out.float().sum(0))
 
 
-@pytest.mark.parametrize("T", [197, 50])
+@pytest.mark.parametrize("T", [197, 50, 256, 7])
 def test_cls_attention_kernel_matches_fp32(T):
     """csrc/attention_cls.hip: token 0's attention output and the full dqkv against an fp32
     torch reference of the same op."""
