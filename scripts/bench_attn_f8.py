@@ -30,8 +30,16 @@ lse = torch.empty(B * H, T, dtype=torch.float32, device=dev)
 dout = torch.randn(B, T, H * 64, device=dev, generator=g).to(torch.bfloat16)
 dqkv = torch.empty_like(qkv)
 P, st, sc = no._p, no._s(), 64 ** -0.5
+# the ViT step's forward: the same kernel that also writes the e4m3 codes of O for the
+# projection GEMM and rolls that GEMM's amax history (pdt_attn_fwd_f8_q8)
+codes = torch.empty(B * T, H * 64, dtype=torch.uint8, device=dev)
+meta = torch.zeros(lib.pdt_fp8_meta_words(), dtype=torch.float32, device=dev)
+meta[0] = 1.0
+part = torch.empty(B * H + 1, dtype=torch.float32, device=dev)
 arms = {
     "fwd f8": lambda: lib.pdt_attn_fwd_f8(P(qkv), P(out), P(lse), B, T, H, sc, st),
+    "fwd q8": lambda: lib.pdt_attn_fwd_f8_q8(P(qkv), P(out), P(lse), B, T, H, sc, P(codes), P(meta), P(part),
+                                             P(part[-1:]), st),
     "bwd f8": lambda: lib.pdt_attn_bwd_f8(P(qkv), P(out), P(dout), P(lse), P(dqkv), B, T, H, sc, st),
 }
 ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)

@@ -18,6 +18,7 @@
 #   hiptrace[:ARGS]  rocprofv3 HIP-API + kernel trace (host-sync hunting)
 #   pmc:CTRS:ARGS    one counter pass (CTRS: commas -> spaces) over bench.py ARGS
 #   py:SCRIPT[:ARGS] python SCRIPT ARGS
+#   pyenv:K=V+K2=V2:SCRIPT[:ARGS]  the same with extra environment variables
 #   retunewith:NAME:IDS[:ARGS]  targeted re-tune of the shipped conv_nt keys against ids IDS
 #                    (e.g. 45-48+50: '+' separates ranges) -> gpurun_out/tune_NAME.json
 source "$(dirname "$0")/gpurun_lib.sh"
@@ -67,6 +68,9 @@ for job in "$@"; do
     py)
       scr=${rest%%:*}; sargs=""; [[ "$rest" == *:* ]] && sargs=${rest#*:}
       run ${TAG}_py_$(basename $scr .py)$(echo "$sargs" | tr -c 'a-zA-Z0-9_\n' '_' | cut -c1-30).txt 600 python -u $scr ${sargs//,/ } ;;
+    pyenv)  # pyenv:K=V+K2=V2:SCRIPT[:ARGS] -- a python script with extra environment variables
+      envs=${rest%%:*}; r2=${rest#*:}; scr=${r2%%:*}; sargs=""; [[ "$r2" == *:* ]] && sargs=${r2#*:}
+      run ${TAG}_pyenv_$(echo "$envs$(basename $scr .py)$sargs" | tr -c 'a-zA-Z0-9_\n' '_' | cut -c1-60).txt 600 env ${envs//+/ } python -u $scr ${sargs//,/ } ;;
     *) echo "unknown job $job"; exit 2 ;;
   esac
 done
