@@ -106,18 +106,39 @@ __global__ void __launch_bounds__(64 * NW) attn_fwd_f8_kernel(AttnF8Params p) {
   constexpr int CH = ROWS * 8;  // 16-B chunks of one [ROWS][64] bf16 matrix
   constexpr int VCH = VROWS * 8;
   constexpr int NIT = (VCH + NTH - 1) / NTH;
-  u32x4 kv[NIT], vv[PV8 ? NIT : 1];
+  u32x4 kv[NIT], vv[NIT];
+  // Every staging load is issued before any is consumed, from a clamped (always valid) row:
+  // with the bounds test around the loads, hipcc waited for each iteration's pair before the
+  // next one's issue (vmcnt(1) between pairs), serialising ~NIT + 1 HBM latencies per head.
+#pragma unroll
+  for (int it = 0; it < NIT; ++it) {
+    const int q = tid + it * NTH;
+    const int rr = min(q >> 3, p.T - 1), ch = q & 7;
+    vv[it] = *reinterpret_cast<const u32x4*>(Vg + (long)rr * p.ld + ch * 8);
+    kv[it] = *reinterpret_cast<const u32x4*>(Kg + (long)rr * p.ld + ch * 8);
+  }
+  // fp8: this wave's first query tile is loaded here too, so its latency overlaps the staging
+  // loads' instead of following the staging barrier (with 8 waves and T <= 256 it is the wave's
+  // only tile). Same lane layout as the in-loop load below.
+  u32x4 qpre[F8 ? 4 : 1];
+  if constexpr (F8) {
+    const int q = wave * 32 + (lane & 31);
+    const int qr = min(q, p.T - 1);
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      const u32x4 t = *reinterpret_cast<const u32x4*>(base + (long)qr * p.ld + 32 * (lane >> 5) + 8 * c);
+      qpre[c] = q < p.T ? t : u32x4{0, 0, 0, 0};
+    }
+  }
   // |K|max / |V|max on the packed bf16 bits (pdt_f8::absmax_bf16x2: two magnitudes per u16 max)
   uint32_t kmb = 0u, vmb = 0u;
 #pragma unroll
   for (int it = 0; it < NIT; ++it) {
     const int q = tid + it * NTH;
     const int row = q >> 3, ch = q & 7;
-    u32x4 v = {0, 0, 0, 0}, k = {0, 0, 0, 0};
-    if (q < VCH && row < p.T) {
-      v = *reinterpret_cast<const u32x4*>(Vg + (long)row * p.ld + ch * 8);
-      k = *reinterpret_cast<const u32x4*>(Kg + (long)row * p.ld + ch * 8);
-    }
+    const bool ok = q < VCH && row < p.T;
+    const u32x4 v = ok ? vv[it] : u32x4{0, 0, 0, 0};
+    const u32x4 k = ok ? kv[it] : u32x4{0, 0, 0, 0};
     if constexpr (PV8) {
       vv[it] = v;
 #pragma unroll
@@ -196,7 +217,9 @@ __global__ void __launch_bounds__(64 * NW) attn_fwd_f8_kernel(AttnF8Params p) {
     for (int c = 0; c < 4; ++c) {
       qv[c] = u32x4{0, 0, 0, 0};
       qb[c] = u32x4{0, 0, 0, 0};
-      if (q < p.T) {
+      if (F8 && qt == wave) {
+        qv[c] = qpre[F8 ? c : 0];
+      } else if (q < p.T) {
         if (F8) qv[c] = *reinterpret_cast<const u32x4*>(base + (long)q * p.ld + 32 * hh + 8 * c);
         else qb[c] = *reinterpret_cast<const u32x4*>(base + (long)q * p.ld + 16 * c + 8 * hh);
       }
@@ -499,20 +522,29 @@ PDT_API int pdt_attn_fwd_f8_q8(const void* qkv, void* out, float* lse, int B, in
   p.q8 = (uint8_t*)q8; p.q8_meta = q8_meta; p.q8_part = q8_part;
   const int nkt = (T + 31) / 32;
   dim3 g(B * H);
+  if (nkt >= 5 && !attn_pv8() && attn_fwd_nw8()) {  // 8 waves, as in pdt_attn_fwd_f8
+    switch (nkt) {
+      case 5: hipLaunchKernelGGL((attn_fwd_f8_kernel<5, true, false, 8>), g, dim3(512), 0, st, p); break;
+      case 6: hipLaunchKernelGGL((attn_fwd_f8_kernel<6, true, false, 8>), g, dim3(512), 0, st, p); break;
+      case 7: hipLaunchKernelGGL((attn_fwd_f8_kernel<7, true, false, 8>), g, dim3(512), 0, st, p); break;
+      default: hipLaunchKernelGGL((attn_fwd_f8_kernel<8, true, false, 8>), g, dim3(512), 0, st, p); break;
+    }
+  } else {
 #define F8(N)                                                                         \
   if (attn_pv8()) hipLaunchKernelGGL((attn_fwd_f8_kernel<N, true, true>), g, dim3(256), 0, st, p); \
   else hipLaunchKernelGGL((attn_fwd_f8_kernel<N, true, false>), g, dim3(256), 0, st, p)
-  switch (nkt) {
-    case 1: F8(1); break;
-    case 2: F8(2); break;
-    case 3: F8(3); break;
-    case 4: F8(4); break;
-    case 5: F8(5); break;
-    case 6: F8(6); break;
-    case 7: F8(7); break;
-    default: F8(8); break;
-  }
+    switch (nkt) {
+      case 1: F8(1); break;
+      case 2: F8(2); break;
+      case 3: F8(3); break;
+      case 4: F8(4); break;
+      case 5: F8(5); break;
+      case 6: F8(6); break;
+      case 7: F8(7); break;
+      default: F8(8); break;
+    }
 #undef F8
+  }
   int e = (int)hipGetLastError();
   if (e) return e;
   return pdt_fp8_meta_roll_partial(q8_meta, q8_part, B * H, 0, q8_dq, st);

@@ -48,18 +48,35 @@ __global__ void __launch_bounds__(64 * WPB) ln_fwd_kernel(const u16* __restrict_
   const u16* xr = x + (long)row * D;
   float v[CH][4];
   float s = 0.f;
+  // all of the row's x (and residual) chunks are loaded before any is used, each path in one
+  // block: with the residual branch inside the chunk loop (or between the x and r loads) hipcc
+  // waited for the x loads before issuing the r loads
+  uint2 xw[CH], rw[CH];
+  if (radd != nullptr) {  // residual add of a pre-norm block: xsum = bf16(x + r), normalised
 #pragma unroll
-  for (int c = 0; c < CH; ++c) {
-    ld4(xr + (c * 64 + lane) * 4, v[c]);
-    if (radd != nullptr) {  // residual add of a pre-norm block: xsum = bf16(x + r), normalised
-      float r[4];
-      ld4(radd + (long)row * D + (c * 64 + lane) * 4, r);
+    for (int c = 0; c < CH; ++c) {
+      xw[c] = *reinterpret_cast<const uint2*>(xr + (c * 64 + lane) * 4);
+      rw[c] = *reinterpret_cast<const uint2*>(radd + (long)row * D + (c * 64 + lane) * 4);
+    }
 #pragma unroll
-      for (int e = 0; e < 4; ++e) v[c][e] = bf2f(f2bf(v[c][e] + r[e]));
+    for (int c = 0; c < CH; ++c) {
+      const float r[4] = {lo_bf(rw[c].x), hi_bf(rw[c].x), lo_bf(rw[c].y), hi_bf(rw[c].y)};
+      const float xv[4] = {lo_bf(xw[c].x), hi_bf(xw[c].x), lo_bf(xw[c].y), hi_bf(xw[c].y)};
+#pragma unroll
+      for (int e = 0; e < 4; ++e) v[c][e] = bf2f(f2bf(xv[e] + r[e]));
       st4(xsum + (long)row * D + (c * 64 + lane) * 4, v[c]);
     }
-    s += v[c][0] + v[c][1] + v[c][2] + v[c][3];
+  } else {
+#pragma unroll
+    for (int c = 0; c < CH; ++c) xw[c] = *reinterpret_cast<const uint2*>(xr + (c * 64 + lane) * 4);
+#pragma unroll
+    for (int c = 0; c < CH; ++c) {
+      v[c][0] = lo_bf(xw[c].x); v[c][1] = hi_bf(xw[c].x);
+      v[c][2] = lo_bf(xw[c].y); v[c][3] = hi_bf(xw[c].y);
+    }
   }
+#pragma unroll
+  for (int c = 0; c < CH; ++c) s += v[c][0] + v[c][1] + v[c][2] + v[c][3];
   const float mean = warp_sum(s) * (1.f / D);
   float q = 0.f;
 #pragma unroll
