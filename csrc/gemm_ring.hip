@@ -265,6 +265,26 @@ __global__ void __launch_bounds__(RNTH, 1) gemm_ring_kernel(RingParams p) {
 #pragma unroll
       for (int e = 0; e < 8; ++e) csum[jp][e] = 0.f;
   }
+  // EPI addend: every chunk of the tile is loaded (from clamped rows: no branch) before the first
+  // store. Loaded next to its use, each row block's wait was a vmcnt(0): with loads and stores both
+  // in flight hipcc treats vmcnt as out of order and waits for zero, which drained the previous
+  // row block's stores as well (16 serialised round trips per tile; a one-ahead prefetch hit the
+  // same drain). The MFMA fragments are dead here, so the 64 registers fit.
+  const bool has_add = EPI && p.addend != nullptr;
+  u32x4 adv[EPI ? MI : 1][EPI ? 2 : 1];
+  if constexpr (EPI) {
+    if (has_add) {
+#pragma unroll
+      for (int i = 0; i < MI; ++i) {
+        const int mc = min(m0 + wm * (RBM / WM) + i * 16 + lrow, p.M - 1);
+#pragma unroll
+        for (int jp = 0; jp < 2; ++jp) {
+          const int col = n0 + wcol(odd ? 2 * jp + 1 : 2 * jp) + ((lane >> 5) * 8);
+          adv[i][jp] = *reinterpret_cast<const u32x4*>(p.addend + (size_t)mc * p.ldc + col);
+        }
+      }
+    }
+  }
 #pragma unroll
   for (int i = 0; i < MI; ++i) {
     const int m = m0 + wm * (RBM / WM) + i * 16 + lrow;
@@ -287,8 +307,8 @@ __global__ void __launch_bounds__(RNTH, 1) gemm_ring_kernel(RingParams p) {
       } else {
         if (m < p.M) {
           const size_t e0 = (size_t)m * p.ldc + col;
-          if (p.addend != nullptr) {
-            const u32x4 ad = *reinterpret_cast<const u32x4*>(p.addend + e0);
+          if (has_add) {
+            const u32x4 ad = adv[EPI ? i : 0][EPI ? (j >> 1) : 0];
 #pragma unroll
             for (int e = 0; e < 4; ++e) {
               if (p.act == 3)
