@@ -31,6 +31,7 @@
 //
 // Developed in scripts/gemm_lab/gemm_lab.hip (v4: 1.28-1.33 PF/s bf16 at 4096^3).
 #include "pdt_common.h"
+#include <type_traits>
 
 namespace {
 
@@ -271,91 +272,121 @@ __global__ void __launch_bounds__(RNTH, 1) gemm_ring_kernel(RingParams p) {
   // row block's stores as well (16 serialised round trips per tile; a one-ahead prefetch hit the
   // same drain). The MFMA fragments are dead here, so the 64 registers fit.
   const bool has_add = EPI && p.addend != nullptr;
-  u32x4 adv[EPI ? MI : 1][EPI ? 2 : 1];
+  // The EPI loop nest is compiled per configuration (compile-time act / fp8 code format): the
+  // ViT MLP runs two -- fc1 forward (GELU + GELU', e4m3 codes, no addend) and fc2's data gradient
+  // (x gelu' addend, e5m2 codes) -- and with run-time fields every element group branched on
+  // act, q8 and the format (~450 branches and ~320 exec moves per tile); anything else takes the
+  // run-time path.
+  auto run = [&](auto act_c, auto q8_c) __attribute__((always_inline)) {
+    constexpr int CA = decltype(act_c)::value;  // -1: p.act at run time
+    constexpr int CQ = decltype(q8_c)::value;   // -1: p.q8 / p.q8_fmt at run time; 1 e4m3, 2 e5m2
+    const int act = CA >= 0 ? CA : p.act;
+    const bool q8on = CQ > 0 ? true : (EPI && p.q8 != nullptr);
+    const int fmt = CQ > 0 ? CQ - 1 : p.q8_fmt;
+    const bool hadd = CA == 4 ? false : (CA == 5 ? true : has_add);
+    const bool cstore = !(q8on && p.q8_only);
+    (void)act; (void)fmt; (void)hadd; (void)cstore;
+    // EPI addend: every chunk of the tile is loaded (from clamped rows: no branch) before the first
+    // store. Loaded next to its use, each row block's wait was a vmcnt(0): with loads and stores
+    // both in flight hipcc treats vmcnt as out of order and waits for zero, which drained the
+    // previous row block's stores as well (16 serialised round trips per tile; a one-ahead
+    // prefetch hit the same drain). The MFMA fragments are dead here, so the 64 registers fit.
+    u32x4 adv[EPI ? MI : 1][EPI ? 2 : 1];
+    if constexpr (EPI) {
+      if (hadd) {
+#pragma unroll
+        for (int i = 0; i < MI; ++i) {
+          const int mc = min(m0 + wm * (RBM / WM) + i * 16 + lrow, p.M - 1);
+#pragma unroll
+          for (int jp = 0; jp < 2; ++jp) {
+            const int col = n0 + wcol(odd ? 2 * jp + 1 : 2 * jp) + ((lane >> 5) * 8);
+            adv[i][jp] = *reinterpret_cast<const u32x4*>(p.addend + (size_t)mc * p.ldc + col);
+          }
+        }
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < MI; ++i) {
+      const int m = m0 + wm * (RBM / WM) + i * 16 + lrow;
+#pragma unroll
+      for (int j = 0; j < NI; j += 2) {
+        const f32x4 x = acc[i][j], y = acc[i][j + 1];
+        const uint32_t a0 = pack2bf(x[0] * alpha + bv[j][0], x[1] * alpha + bv[j][1]);
+        const uint32_t a1 = pack2bf(x[2] * alpha + bv[j][2], x[3] * alpha + bv[j][3]);
+        const uint32_t b0 = pack2bf(y[0] * alpha + bv[j + 1][0], y[1] * alpha + bv[j + 1][1]);
+        const uint32_t b1 = pack2bf(y[2] * alpha + bv[j + 1][2], y[3] * alpha + bv[j + 1][3]);
+        // lanes l (group g = l >> 4 even) and l + 16 (g odd) hold the low / high 4 columns of
+        // one 8-column half of blocks j and j + 1: one swap per dword gives the even lane block
+        // j's 8 columns and the odd lane block j + 1's
+        const auto r0 = __builtin_amdgcn_permlane16_swap(a0, b0, false, false);
+        const auto r1 = __builtin_amdgcn_permlane16_swap(a1, b1, false, false);
+        u32x4 v = {r0[0], r1[0], r0[1], r1[1]};
+        const int col = n0 + wcol(odd ? j + 1 : j) + ((lane >> 5) * 8);
+        if constexpr (!EPI) {
+          if (m < p.M) *reinterpret_cast<u32x4*>(p.C + (size_t)m * p.ldc + col) = v;
+        } else {
+          if (m < p.M) {
+            const size_t e0 = (size_t)m * p.ldc + col;
+            if (hadd) {
+              const u32x4 ad = adv[EPI ? i : 0][EPI ? (j >> 1) : 0];
+#pragma unroll
+              for (int e = 0; e < 4; ++e) {
+                if (act == 3)
+                  v[e] = pack2bf(lo_bf(v[e]) * ring_gelu_grad(lo_bf(ad[e])), hi_bf(v[e]) * ring_gelu_grad(hi_bf(ad[e])));
+                else if (act == 5)
+                  v[e] = pack2bf(lo_bf(v[e]) * lo_bf(ad[e]), hi_bf(v[e]) * hi_bf(ad[e]));
+                else
+                  v[e] = pack2bf(lo_bf(v[e]) + lo_bf(ad[e]), hi_bf(v[e]) + hi_bf(ad[e]));
+              }
+            }
+            if (act == 4) {
+              u32x4 gd;
+#pragma unroll
+              for (int e = 0; e < 4; ++e) {
+                float g0, g1, d0, d1;
+                pdt_gelu_dual(lo_bf(v[e]), g0, d0);
+                pdt_gelu_dual(hi_bf(v[e]), g1, d1);
+                v[e] = pack2bf(g0, g1);
+                gd[e] = pack2bf(d0, d1);
+              }
+              *reinterpret_cast<u32x4*>(p.aux + e0) = gd;
+            }
+            float f[8];
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              f[2 * e] = lo_bf(v[e]);
+              f[2 * e + 1] = hi_bf(v[e]);
+            }
+#pragma unroll
+            for (int e = 0; e < 8; ++e) csum[j >> 1][e] += f[e];
+            if (q8on) {
+#pragma unroll
+              for (int e = 0; e < 8; ++e) q8max = fmaxf(q8max, fabsf(f[e]));
+              uint2 c8;
+              if (fmt == 0) {
+                c8.x = pdt_cvt4_f8<0>(f[0] * q8s, f[1] * q8s, f[2] * q8s, f[3] * q8s);
+                c8.y = pdt_cvt4_f8<0>(f[4] * q8s, f[5] * q8s, f[6] * q8s, f[7] * q8s);
+              } else {
+                c8.x = pdt_cvt4_f8<1>(f[0] * q8s, f[1] * q8s, f[2] * q8s, f[3] * q8s);
+                c8.y = pdt_cvt4_f8<1>(f[4] * q8s, f[5] * q8s, f[6] * q8s, f[7] * q8s);
+              }
+              *reinterpret_cast<uint2*>(p.q8 + e0) = c8;
+            }
+            if (cstore) *reinterpret_cast<u32x4*>(p.C + e0) = v;
+          }
+        }
+      }
+    }
+  };
   if constexpr (EPI) {
-    if (has_add) {
-#pragma unroll
-      for (int i = 0; i < MI; ++i) {
-        const int mc = min(m0 + wm * (RBM / WM) + i * 16 + lrow, p.M - 1);
-#pragma unroll
-        for (int jp = 0; jp < 2; ++jp) {
-          const int col = n0 + wcol(odd ? 2 * jp + 1 : 2 * jp) + ((lane >> 5) * 8);
-          adv[i][jp] = *reinterpret_cast<const u32x4*>(p.addend + (size_t)mc * p.ldc + col);
-        }
-      }
-    }
-  }
-#pragma unroll
-  for (int i = 0; i < MI; ++i) {
-    const int m = m0 + wm * (RBM / WM) + i * 16 + lrow;
-#pragma unroll
-    for (int j = 0; j < NI; j += 2) {
-      const f32x4 x = acc[i][j], y = acc[i][j + 1];
-      const uint32_t a0 = pack2bf(x[0] * alpha + bv[j][0], x[1] * alpha + bv[j][1]);
-      const uint32_t a1 = pack2bf(x[2] * alpha + bv[j][2], x[3] * alpha + bv[j][3]);
-      const uint32_t b0 = pack2bf(y[0] * alpha + bv[j + 1][0], y[1] * alpha + bv[j + 1][1]);
-      const uint32_t b1 = pack2bf(y[2] * alpha + bv[j + 1][2], y[3] * alpha + bv[j + 1][3]);
-      // lanes l (group g = l >> 4 even) and l + 16 (g odd) hold the low / high 4 columns of
-      // one 8-column half of blocks j and j + 1: one swap per dword gives the even lane block
-      // j's 8 columns and the odd lane block j + 1's
-      const auto r0 = __builtin_amdgcn_permlane16_swap(a0, b0, false, false);
-      const auto r1 = __builtin_amdgcn_permlane16_swap(a1, b1, false, false);
-      u32x4 v = {r0[0], r1[0], r0[1], r1[1]};
-      const int col = n0 + wcol(odd ? j + 1 : j) + ((lane >> 5) * 8);
-      if constexpr (!EPI) {
-        if (m < p.M) *reinterpret_cast<u32x4*>(p.C + (size_t)m * p.ldc + col) = v;
-      } else {
-        if (m < p.M) {
-          const size_t e0 = (size_t)m * p.ldc + col;
-          if (has_add) {
-            const u32x4 ad = adv[EPI ? i : 0][EPI ? (j >> 1) : 0];
-#pragma unroll
-            for (int e = 0; e < 4; ++e) {
-              if (p.act == 3)
-                v[e] = pack2bf(lo_bf(v[e]) * ring_gelu_grad(lo_bf(ad[e])), hi_bf(v[e]) * ring_gelu_grad(hi_bf(ad[e])));
-              else if (p.act == 5)
-                v[e] = pack2bf(lo_bf(v[e]) * lo_bf(ad[e]), hi_bf(v[e]) * hi_bf(ad[e]));
-              else
-                v[e] = pack2bf(lo_bf(v[e]) + lo_bf(ad[e]), hi_bf(v[e]) + hi_bf(ad[e]));
-            }
-          }
-          if (p.act == 4) {
-            u32x4 gd;
-#pragma unroll
-            for (int e = 0; e < 4; ++e) {
-              float g0, g1, d0, d1;
-              pdt_gelu_dual(lo_bf(v[e]), g0, d0);
-              pdt_gelu_dual(hi_bf(v[e]), g1, d1);
-              v[e] = pack2bf(g0, g1);
-              gd[e] = pack2bf(d0, d1);
-            }
-            *reinterpret_cast<u32x4*>(p.aux + e0) = gd;
-          }
-          float f[8];
-#pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            f[2 * e] = lo_bf(v[e]);
-            f[2 * e + 1] = hi_bf(v[e]);
-          }
-#pragma unroll
-          for (int e = 0; e < 8; ++e) csum[j >> 1][e] += f[e];
-          if (p.q8 != nullptr) {
-#pragma unroll
-            for (int e = 0; e < 8; ++e) q8max = fmaxf(q8max, fabsf(f[e]));
-            uint2 c8;
-            if (p.q8_fmt == 0) {
-              c8.x = pdt_cvt4_f8<0>(f[0] * q8s, f[1] * q8s, f[2] * q8s, f[3] * q8s);
-              c8.y = pdt_cvt4_f8<0>(f[4] * q8s, f[5] * q8s, f[6] * q8s, f[7] * q8s);
-            } else {
-              c8.x = pdt_cvt4_f8<1>(f[0] * q8s, f[1] * q8s, f[2] * q8s, f[3] * q8s);
-              c8.y = pdt_cvt4_f8<1>(f[4] * q8s, f[5] * q8s, f[6] * q8s, f[7] * q8s);
-            }
-            *reinterpret_cast<uint2*>(p.q8 + e0) = c8;
-          }
-          if (!(p.q8 != nullptr && p.q8_only)) *reinterpret_cast<u32x4*>(p.C + e0) = v;
-        }
-      }
-    }
+    if (p.act == 4 && p.q8 != nullptr && p.q8_fmt == 0 && !has_add)
+      run(std::integral_constant<int, 4>{}, std::integral_constant<int, 1>{});
+    else if (p.act == 5 && p.q8 != nullptr && p.q8_fmt == 1 && has_add)
+      run(std::integral_constant<int, 5>{}, std::integral_constant<int, 2>{});
+    else
+      run(std::integral_constant<int, -1>{}, std::integral_constant<int, -1>{});
+  } else {
+    run(std::integral_constant<int, -1>{}, std::integral_constant<int, -1>{});
   }
   if constexpr (EPI) {
     // every LDS fragment read finished before the loop's last barrier: smem is free here
