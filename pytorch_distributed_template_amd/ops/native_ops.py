@@ -246,7 +246,7 @@ def _chk(rc, name):
         raise RuntimeError(f"{name} failed with code {rc}")
 
 
-def _grad_buf(param, shape, memory_format=None):
+def _grad_buf(param, shape, memory_format=None, device=None):
     """fp32 output buffer for ``param``'s gradient: its slot in the data-parallel reducer's
     bucket when it has one (``parallel/reducer.py``: the kernel then writes the gradient where
     the all-reduce reads it, and autograd adopts that view as ``param.grad`` with no copy),
@@ -254,7 +254,11 @@ def _grad_buf(param, shape, memory_format=None):
     if param is not None and getattr(param, "_pdt_grad_slot", None) is not None:
         from ..parallel.reducer import grad_out
         return grad_out(param, *shape, memory_format=memory_format)
-    dev = param.device if param is not None else None
+    # no parameter (e.g. a bias gradient asked for without its bias tensor): the current GPU --
+    # device=None would allocate on the HOST, and the kernel that fills the buffer would then
+    # write through a host pointer (the illegal access of round 5's r5z variant sweep)
+    dev = param.device if param is not None else device if device is not None else (
+        torch.device("cuda", torch.cuda.current_device()) if torch.cuda.is_available() else None)
     if memory_format is not None:
         return torch.empty(shape, dtype=torch.float32, device=dev, memory_format=memory_format)
     return torch.empty(shape, dtype=torch.float32, device=dev)
@@ -747,6 +751,8 @@ def conv_wgrad(dy, x, out, *, scale=1.0, accumulate=False, variant=None, bias_ou
     assert a["ntw"] >= 1 and No % C == 0
     if bias_out is not None:
         assert bias_out.dtype == torch.float32 and bias_out.numel() >= Mo and bias_out.is_contiguous()
+        assert bias_out.device == dy.device, "bias gradient buffer on another device than dY"
+    assert out.device == dy.device == x.device, "weight gradient operands on different devices"
     lib = _load()
     if variant is None:
         gt = (a["M"], a["Mo"], a["No"], a["Hs"], a["Ws"], a["C"], a["Hm"], a["Wm"], a["sh"], a["ntw"], a.get("pix", 0))
@@ -2274,8 +2280,8 @@ def _linear_dgrad(dy2, w):
 def _linear_wgrad(dy2, x2, w, with_bias=False, bias=None):
     """(dW fp32 [Nout][K], db fp32 [Nout] or None): db comes out of the same kernel."""
     Nout, K = w.shape
-    dw = _grad_buf(w, (Nout, K))
-    db = _grad_buf(bias, (Nout,)) if with_bias else None
+    dw = _grad_buf(w, (Nout, K), device=dy2.device)
+    db = _grad_buf(bias, (Nout,), device=dy2.device) if with_bias else None
     conv_wgrad(dy2, x2, dw, M=dy2.shape[0], Mo=Nout, No=K, ldy=Nout, Hs=1, Ws=1, C=K, Hm=1, Wm=1, sh=1, sw=1,
                oh0=0, ow0=0, dh=1, dw=1, ntw=1, bias_out=db)
     return dw, db

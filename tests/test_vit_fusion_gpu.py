@@ -766,3 +766,20 @@ def test_cast_fp8_delayed_colsum(rows, cols, fmt):
     assert torch.equal(meta_a, meta_b)
     ref = x.float().sum(0)
     assert ((db - ref).norm() / ref.norm()).item() < 1e-5
+
+
+def test_linear_wgrad_bias_without_param():
+    """_linear_wgrad(..., with_bias=True) without a bias tensor: the bias-gradient buffer is
+    allocated on the GPU (ops/native_ops.py _grad_buf). With device=None it landed on the host
+    and the weight-gradient kernel wrote through a host pointer -- the illegal access that
+    faulted round 5's r5z variant sweep."""
+    torch.manual_seed(3)
+    M, Nout, K = 1000, 256, 128
+    dy = torch.randn(M, Nout, device="cuda").to(torch.bfloat16)
+    x = torch.randn(M, K, device="cuda").to(torch.bfloat16)
+    w = torch.empty(Nout, K, device="cuda")
+    dw, db = no._linear_wgrad(dy, x, w, with_bias=True)
+    torch.cuda.synchronize()
+    assert db.is_cuda and dw.is_cuda
+    assert nrmerr(db, dy.float().sum(0)) < 1e-5
+    assert nrmerr(dw, dy.float().t() @ x.float()) < 1e-3
