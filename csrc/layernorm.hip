@@ -154,21 +154,56 @@ __global__ void __launch_bounds__(64 * WPB) ln_bwd_kernel(const u16* __restrict_
     for (int e = 0; e < 4; ++e) dg[c][e] = db[c][e] = cs[c][e] = 0.f;
   const int r0 = blockIdx.x * rows_per_block;
   const int r1 = min(rows, r0 + rows_per_block);
-  for (int row = r0 + w; row < r1; row += WPB) {
-    const float mean = mean_in[row], rstd = rstd_in[row];
-    float xh[CH][4], gy[CH][4], ad[CH][4];
-    float s1 = 0.f, s2 = 0.f;
-    if (addend != nullptr) {  // issued with the row's other loads (latency overlapped)
-#pragma unroll
-      for (int c = 0; c < CH; ++c) ld4(addend + (long)row * D + (c * 64 + lane) * 4, ad[c]);
-    }
+  // Rows are software-pipelined: the next row's operands are loaded at the top of this row's
+  // iteration and stay in flight through its arithmetic and stores. The empty asm with the
+  // loaded registers as "+v" operands is the one wait per row: after it every use sees plain
+  // registers, so hipcc does not fold the in-flight next-row loads into a later wait (with
+  // loads and stores both pending it waits for zero -- which, at a wait for this row's data
+  // placed after the prefetch, would have drained the prefetch too).
+  uint2 nx[CH], ndy[CH], nad[CH];
+  float nmean = 0.f, nrstd = 0.f;
+  // (without an addend the third stream re-reads dy -- a valid address, its values unused --
+  // so the prefetch is one branch-free block of loads)
+  const u16* aptr = addend != nullptr ? addend : dy;
+  auto fetch = [&](int rr) __attribute__((always_inline)) {
 #pragma unroll
     for (int c = 0; c < CH; ++c) {
-      const int col = (c * 64 + lane) * 4;
-      float xv[4], dv[4];
-      ld4(x + (long)row * D + col, xv);
-      ld4(dy + (long)row * D + col, dv);
-      f32x4 gg = *reinterpret_cast<const f32x4*>(g + col);
+      const long off = (long)rr * D + (c * 64 + lane) * 4;
+      nx[c] = *reinterpret_cast<const uint2*>(x + off);
+      ndy[c] = *reinterpret_cast<const uint2*>(dy + off);
+      nad[c] = *reinterpret_cast<const uint2*>(aptr + off);
+    }
+    nmean = mean_in[rr];
+    nrstd = rstd_in[rr];
+  };
+  // gamma is per column: loaded once (a load issued after the prefetch and waited for inside
+  // the row would retire the prefetch with it -- vmcnt counts in order)
+  f32x4 gv[CH];
+#pragma unroll
+  for (int c = 0; c < CH; ++c) gv[c] = *reinterpret_cast<const f32x4*>(g + (c * 64 + lane) * 4);
+  if (r0 + w < r1) fetch(r0 + w);
+  for (int row = r0 + w; row < r1; row += WPB) {
+#pragma unroll
+    for (int c = 0; c < CH; ++c) asm volatile("" : "+v"(nx[c]), "+v"(ndy[c]), "+v"(nad[c])::"memory");
+    asm volatile("" : "+v"(nmean), "+v"(nrstd)::"memory");
+    uint2 cx[CH], cdy[CH], cad[CH];
+#pragma unroll
+    for (int c = 0; c < CH; ++c) {
+      cx[c] = nx[c];
+      cdy[c] = ndy[c];
+      cad[c] = nad[c];
+    }
+    const float mean = nmean, rstd = nrstd;
+    if (row + WPB < r1) fetch(row + WPB);
+    float xh[CH][4], gy[CH][4], ad[CH][4];
+    float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+    for (int c = 0; c < CH; ++c) {
+      const float xv[4] = {lo_bf(cx[c].x), hi_bf(cx[c].x), lo_bf(cx[c].y), hi_bf(cx[c].y)};
+      const float dv[4] = {lo_bf(cdy[c].x), hi_bf(cdy[c].x), lo_bf(cdy[c].y), hi_bf(cdy[c].y)};
+      ad[c][0] = lo_bf(cad[c].x); ad[c][1] = hi_bf(cad[c].x);
+      ad[c][2] = lo_bf(cad[c].y); ad[c][3] = hi_bf(cad[c].y);
+      const f32x4 gg = gv[c];
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
         xh[c][e] = (xv[e] - mean) * rstd;
