@@ -49,7 +49,9 @@ struct AttnBwdF8Params {
 };
 
 // NQP query-tile pairs: images of ROWS = 64 NQP rows (zero beyond T); 8 waves
-template <int NQP>
+// DBG: the tests' fp32 dS dump (p.dbg) -- compiled only into the debug entry point: in the
+// production kernel its address arithmetic held registers across phase 1 (NQP = 4 sits at 256)
+template <int NQP, bool DBG = false>
 __global__ void __launch_bounds__(512) attn_bwd_f8_kernel(AttnBwdF8Params p) {
   constexpr int NT2 = 2 * NQP;  // 32-row tiles (queries and keys)
   constexpr int ROWS = 32 * NT2;
@@ -219,7 +221,7 @@ __global__ void __launch_bounds__(512) attn_bwd_f8_kernel(AttnBwdF8Params p) {
             am = fmaxf(am, fabsf(ds[r]));
           }
         }
-        if (p.dbg != nullptr) {
+        if constexpr (DBG) {
 #pragma unroll
           for (int r = 0; r < 16; ++r) {
             const int q = 32 * qt + 8 * (r >> 2) + 4 * hh + (r & 3);
@@ -381,7 +383,9 @@ static int attn_bwd_f8(const void* qkv, const void* out, const void* dout, const
   const int nqp = (T + 63) / 64;
   // one workgroup per CU (the LDS images hold 137 KB), each walking B*H / grid heads
   dim3 g(attn_bwd_grid(B * H));
-#define BWD(N) hipLaunchKernelGGL((attn_bwd_f8_kernel<N>), g, dim3(512), 0, st, p)
+#define BWD(N)                                                                        \
+  if (dbg != nullptr) hipLaunchKernelGGL((attn_bwd_f8_kernel<N, true>), g, dim3(512), 0, st, p); \
+  else hipLaunchKernelGGL((attn_bwd_f8_kernel<N>), g, dim3(512), 0, st, p)
   switch (nqp) {
     case 1: BWD(1); break;
     case 2: BWD(2); break;
