@@ -87,8 +87,11 @@ __device__ __forceinline__ int k16_off(int row, int chunk) { return row * 128 + 
 // score GEMM in bf16 (4 x mfma_f32_32x32x16_bf16 per 32 x 32 tile, K kept as bf16) -- the
 // bf16 forward of ViT (126 VGPRs, 3 workgroups per CU, vs 248 VGPRs / 1 wave per SIMD
 // for the whole-sequence kernel in csrc/attention.hip)
-template <int NKT, bool F8, bool PV8 = false, int NW = 4>
+// Q8: the e4m3 codes of O for the projection GEMM -- -1 decided by p.q8 at run time, 0 / 1
+// compiled out / in (the 8-wave launches: no per-chunk branches in the epilogue)
+template <int NKT, bool F8, bool PV8 = false, int NW = 4, int Q8 = -1>
 __global__ void __launch_bounds__(64 * NW) attn_fwd_f8_kernel(AttnF8Params p) {
+  const bool q8on = Q8 >= 0 ? Q8 == 1 : p.q8 != nullptr;
   constexpr int NTH = 64 * NW;
   static_assert(F8 || !PV8, "the fp8 PV rides on the fp8 score kernel");
   constexpr int ROWS = NKT * 32;
@@ -388,7 +391,7 @@ __global__ void __launch_bounds__(64 * NW) attn_fwd_f8_kernel(AttnF8Params p) {
       const float inv = 1.f / l;
       const long orow_off = ((long)b * p.T + (qok ? q : 0)) * p.ldo + h * D;
       u16* orow = p.out + orow_off;
-      const float s8 = p.q8 != nullptr ? p.q8_meta[0] : 0.f;
+      const float s8 = q8on ? p.q8_meta[0] : 0.f;
 #pragma unroll
       for (int dt = 0; dt < 2; ++dt)
 #pragma unroll
@@ -399,7 +402,7 @@ __global__ void __launch_bounds__(64 * NW) attn_fwd_f8_kernel(AttnF8Params p) {
             const int g4 = g2 + u;
             w[u][0] = pack2bf(o[dt][4 * g4] * inv, o[dt][4 * g4 + 1] * inv);
             w[u][1] = pack2bf(o[dt][4 * g4 + 2] * inv, o[dt][4 * g4 + 3] * inv);
-            if (p.q8 != nullptr) {
+            if (q8on) {
               const float f0 = lo_bf(w[u][0]), f1 = hi_bf(w[u][0]), f2 = lo_bf(w[u][1]), f3 = hi_bf(w[u][1]);
               if (qok) q8max = fmaxf(q8max, fmaxf(fmaxf(fabsf(f0), fabsf(f1)), fmaxf(fabsf(f2), fabsf(f3))));
               c8[u] = cvt4_e4m3(f0 * s8, f1 * s8, f2 * s8, f3 * s8);
@@ -409,7 +412,7 @@ __global__ void __launch_bounds__(64 * NW) attn_fwd_f8_kernel(AttnF8Params p) {
           const auto r1 = __builtin_amdgcn_permlane32_swap(w[0][1], w[1][1], false, false);
           const int col0 = 32 * dt + 8 * (g2 + hh);
           if (qok) *reinterpret_cast<u32x4*>(orow + col0) = u32x4{r0[0], r1[0], r0[1], r1[1]};
-          if (p.q8 != nullptr) {
+          if (q8on) {
             const auto rc = __builtin_amdgcn_permlane32_swap(c8[0], c8[1], false, false);
             if (qok) *reinterpret_cast<uint2*>(p.q8 + orow_off + col0) = uint2{rc[0], rc[1]};
           }
@@ -417,7 +420,7 @@ __global__ void __launch_bounds__(64 * NW) attn_fwd_f8_kernel(AttnF8Params p) {
       if (qok && hh == 0) p.lse[(long)bh * p.T + q] = m + log2f(l);
     }
   }
-  if (p.q8 != nullptr) {  // workgroup max |O| (all waves reach this after their query tiles)
+  if (q8on) {  // workgroup max |O| (all waves reach this after their query tiles)
     q8max = warp_max(q8max);
     __syncthreads();
     if (lane == 0) red[wave] = q8max;
@@ -478,10 +481,10 @@ PDT_API int pdt_attn_fwd_f8(const void* qkv, void* out, float* lse, int B, int T
   dim3 g(B * H);
   if (nkt >= 5 && !attn_pv8() && attn_fwd_nw8()) {  // 8 waves: one 32-query tile each (T = 197: 7)
     switch (nkt) {
-      case 5: hipLaunchKernelGGL((attn_fwd_f8_kernel<5, true, false, 8>), g, dim3(512), 0, st, p); break;
-      case 6: hipLaunchKernelGGL((attn_fwd_f8_kernel<6, true, false, 8>), g, dim3(512), 0, st, p); break;
-      case 7: hipLaunchKernelGGL((attn_fwd_f8_kernel<7, true, false, 8>), g, dim3(512), 0, st, p); break;
-      default: hipLaunchKernelGGL((attn_fwd_f8_kernel<8, true, false, 8>), g, dim3(512), 0, st, p); break;
+      case 5: hipLaunchKernelGGL((attn_fwd_f8_kernel<5, true, false, 8, 0>), g, dim3(512), 0, st, p); break;
+      case 6: hipLaunchKernelGGL((attn_fwd_f8_kernel<6, true, false, 8, 0>), g, dim3(512), 0, st, p); break;
+      case 7: hipLaunchKernelGGL((attn_fwd_f8_kernel<7, true, false, 8, 0>), g, dim3(512), 0, st, p); break;
+      default: hipLaunchKernelGGL((attn_fwd_f8_kernel<8, true, false, 8, 0>), g, dim3(512), 0, st, p); break;
     }
     PDT_RETURN_LAUNCH();
   }
@@ -524,10 +527,10 @@ PDT_API int pdt_attn_fwd_f8_q8(const void* qkv, void* out, float* lse, int B, in
   dim3 g(B * H);
   if (nkt >= 5 && !attn_pv8() && attn_fwd_nw8()) {  // 8 waves, as in pdt_attn_fwd_f8
     switch (nkt) {
-      case 5: hipLaunchKernelGGL((attn_fwd_f8_kernel<5, true, false, 8>), g, dim3(512), 0, st, p); break;
-      case 6: hipLaunchKernelGGL((attn_fwd_f8_kernel<6, true, false, 8>), g, dim3(512), 0, st, p); break;
-      case 7: hipLaunchKernelGGL((attn_fwd_f8_kernel<7, true, false, 8>), g, dim3(512), 0, st, p); break;
-      default: hipLaunchKernelGGL((attn_fwd_f8_kernel<8, true, false, 8>), g, dim3(512), 0, st, p); break;
+      case 5: hipLaunchKernelGGL((attn_fwd_f8_kernel<5, true, false, 8, 1>), g, dim3(512), 0, st, p); break;
+      case 6: hipLaunchKernelGGL((attn_fwd_f8_kernel<6, true, false, 8, 1>), g, dim3(512), 0, st, p); break;
+      case 7: hipLaunchKernelGGL((attn_fwd_f8_kernel<7, true, false, 8, 1>), g, dim3(512), 0, st, p); break;
+      default: hipLaunchKernelGGL((attn_fwd_f8_kernel<8, true, false, 8, 1>), g, dim3(512), 0, st, p); break;
     }
   } else {
 #define F8(N)                                                                         \
