@@ -516,15 +516,34 @@ PDT_API int pdt_cast_cs_bands(int rows) {
   return (rows + rpb - 1) / rpb;
 }
 
+// bands actually launched: pdt_cast_cs_bands(rows) is the bound the caller sized cpart for;
+// above one round of resident blocks it is rounded DOWN to whole rounds (the ViT qkv gradient,
+// 201 728 x 2304: 1 576 bands of 896 threads at 2 per CU = 3.08 rounds, the fourth 8 % full).
+// Fewer bands never need more cpart: the reduce workspace grows with the band count.
+// PDT_CAST_CS_ROUNDS=0: the bound itself (A/B runs).
+static int cs_launch_bands(const void* kern, int rows, int nt) {
+  static int env = -1;
+  if (env < 0) {
+    const char* e = getenv("PDT_CAST_CS_ROUNDS");
+    env = e ? atoi(e) : 1;
+  }
+  const int nb = pdt_cast_cs_bands(rows);
+  int per = 0;
+  if (env == 0 || hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, kern, nt, 0) != hipSuccess || per < 1) return nb;
+  const int slots = per * pdt_num_cus();
+  return nb > slots ? nb / slots * slots : nb;
+}
+
 // pdt_cast_fp8_delayed for a bf16 [rows][cols] gradient + its column sums into bias_out (=)
 PDT_API int pdt_cast_fp8_delayed_cs(const void* x, int rows, int cols, float* meta, int fmt, void* q, float* dq_out,
                                     float* cpart, float* bias_out, hipStream_t st) {
   if (cols % 8 != 0 || rows < 1 || !cpart || !bias_out) return -1;
-  const int nb = pdt_cast_cs_bands(rows);
-  const int rpb = (rows + nb - 1) / nb;
   const u16* X = (const u16*)x;
   int nt, rg;
   cs_block(cols, &nt, &rg);
+  const int nb = cs_launch_bands(
+      fmt == 0 ? (const void*)cast_fp8_delayed_cs_kernel<0> : (const void*)cast_fp8_delayed_cs_kernel<1>, rows, nt);
+  const int rpb = (rows + nb - 1) / nb;
   if (fmt == 0)
     hipLaunchKernelGGL(cast_fp8_delayed_cs_kernel<0>, dim3(nb), dim3(nt), 0, st, X, rows, cols, rpb, meta,
                        (uint8_t*)q, cpart, nullptr, rg);
@@ -543,10 +562,12 @@ PDT_API int pdt_cast_fp8_delayed_cs(const void* x, int rows, int cols, float* me
 PDT_API int pdt_cast_fp8_gelu_grad_cs(const void* x, const void* z, int rows, int cols, float* meta, int fmt,
                                       void* q, float* dq_out, float* cpart, float* bias_out, hipStream_t st) {
   if (cols % 8 != 0 || rows < 1 || !z || !cpart || !bias_out) return -1;
-  const int nb = pdt_cast_cs_bands(rows);
-  const int rpb = (rows + nb - 1) / nb;
   int nt, rg;
   cs_block(cols, &nt, &rg);
+  const int nb = cs_launch_bands(fmt == 0 ? (const void*)cast_fp8_delayed_cs_kernel<0, true>
+                                          : (const void*)cast_fp8_delayed_cs_kernel<1, true>,
+                                 rows, nt);
+  const int rpb = (rows + nb - 1) / nb;
   if (fmt == 0)
     hipLaunchKernelGGL((cast_fp8_delayed_cs_kernel<0, true>), dim3(nb), dim3(nt), 0, st, (const u16*)x, rows, cols,
                        rpb, meta, (uint8_t*)q, cpart, (const u16*)z, rg);

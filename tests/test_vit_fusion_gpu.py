@@ -739,11 +739,13 @@ def test_vit_cls_prune_native_matches_full(fp8, monkeypatch):
         assert e < tol, (n, e)
 
 
-@pytest.mark.parametrize("rows,cols,fmt", [(50432, 768, 1), (4001, 2304, 1), (1000, 3072, 0), (777, 8, 1)])
+@pytest.mark.parametrize("rows,cols,fmt", [(50432, 768, 1), (4001, 2304, 1), (1000, 3072, 0), (777, 8, 1),
+                                           (201728, 2304, 1)])
 def test_cast_fp8_delayed_colsum(rows, cols, fmt):
     """pdt_cast_fp8_delayed_cs (row-grouped blocks, csrc/fp8.hip): codes bit-identical to the plain
     delayed cast from the same scaling state, the same amax-history roll, and column sums of
-    the bf16 input (the bias gradient) against fp32."""
+    the bf16 input (the bias gradient) against fp32. 50 432 and 201 728 rows (the ViT bs1024 qkv
+    gradient) launch fewer bands than pdt_cast_cs_bands (whole rounds of resident blocks)."""
     torch.manual_seed(rows + cols)
     lib = no._load()
     x = (torch.randn(rows, cols, device="cuda") * 3).to(torch.bfloat16)
