@@ -432,9 +432,16 @@ PDT_API int pdt_ln_fwd_f8(const void* x, const float* g, const float* b, void* y
   return pdt_fp8_meta_roll_partial(meta, amax_part, nb, 0, dq_out, st);
 }
 
+// rows per LayerNorm-backward block: 64, doubled until at most PDT_LN_BWD_MAXB (512) blocks
 static int ln_rows_per_block(int rows) {
+  static int maxb = -1;
+  if (maxb < 0) {
+    const char* e = getenv("PDT_LN_BWD_MAXB");
+    maxb = e ? atoi(e) : 512;
+    if (maxb < 64) maxb = 512;
+  }
   int rpb = 64;
-  while ((rows + rpb - 1) / rpb > 512) rpb *= 2;
+  while ((rows + rpb - 1) / rpb > maxb) rpb *= 2;
   return rpb;
 }
 
