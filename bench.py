@@ -171,6 +171,10 @@ def parse():
     ap.add_argument("--no-ddp", action="store_true",
                     help="N=1 only: no process group and no DDP wrapper (A/B against the default 1-rank "
                          "RCCL group + DDP reducer that every N>1 rank also runs)")
+    ap.add_argument("--ddp-impl", default=None, choices=[None, "native", "torch"],
+                    help="data-parallel wrapper: native = the framework's BucketedDDP reducer (default, the CPU "
+                         "rehearsal too), torch = torch.nn.parallel.DistributedDataParallel (default for the stock "
+                         "--backend torch on the GPU, the reference's stack)")
     ap.add_argument("--device", default="cuda", choices=["cuda", "cpu"],
                     help="cpu: gloo ranks on the host with stock torch ops (launcher/plumbing rehearsal)")
     ap.add_argument("--image-size", type=int, default=224, help="only for --device cpu rehearsals")
@@ -187,6 +191,10 @@ def parse():
         ap.error("--graph needs the native backend on the GPU with RCCL collectives")
     if a.device == "cpu":
         a.backend, a.dist_backend, a.graph = "torch", "gloo", False
+    if a.ddp_impl is None:
+        # the CPU rehearsal runs stock ops but the framework's reducer (what every GPU rank of
+        # the native stack runs); only the stock GPU baseline uses torch's DDP
+        a.ddp_impl = "torch" if (a.backend == "torch" and a.device == "cuda") or a.comm_hook else "native"
     elif a.image_size != 224:
         ap.error("--image-size is a CPU-rehearsal knob; GPU runs measure 224x224")
     return a
@@ -326,6 +334,24 @@ def allreduce_probe(model, device, world, iters=10):
     nbytes = n * 4
     return {"bytes": nbytes, "median_ms": round(ms, 3),
             "busbw_GBps": round(2 * (world - 1) / world * nbytes / (ms / 1e3) / 1e9, 1)}
+
+
+@torch.no_grad()
+def rank_consistency(model, device, world):
+    """Do all ranks hold the same weights after the timed steps? Every rank applies the same
+    averaged gradient with the same optimizer, so the parameters must be bitwise equal: per
+    parameter an fp64 sum and sum of squares, all-reduced MAX and MIN over the ranks; any
+    difference is rank divergence (a bucket reduced on some ranks only, a slot mix-up, a
+    rank-local update). Reported in the JSON (``ranks_in_sync``), not hidden."""
+    ps = [p.detach() for p in model.parameters()]
+    v = torch.stack([p.double().sum() for p in ps] + [p.double().square().sum() for p in ps])
+    hi, lo = v.clone(), v.clone()
+    if pdist_ready() and world > 1:
+        torch.distributed.all_reduce(hi, op=torch.distributed.ReduceOp.MAX)
+        torch.distributed.all_reduce(lo, op=torch.distributed.ReduceOp.MIN)
+    diff = float((hi - lo).abs().max())
+    return {"ranks_in_sync": diff == 0.0, "param_checksum": float(v[:len(ps)].sum()),
+            "param_checksum_max_rank_diff": diff, "ranks_checked": world}
 
 
 def any_rank(flag: bool, device) -> bool:
@@ -472,10 +498,10 @@ def main():
         side.wait_stream(torch.cuda.current_stream())
         with torch.cuda.stream(side):
             model = wrap_ddp(model, device, bucket_cap_mb=args.bucket_mb, broadcast_buffers=False,
-                             gradient_as_bucket_view=True, comm_hook=args.comm_hook)
+                             gradient_as_bucket_view=True, comm_hook=args.comm_hook, impl=args.ddp_impl)
     else:
         model = wrap_ddp(model, device, bucket_cap_mb=args.bucket_mb, broadcast_buffers=False,
-                         gradient_as_bucket_view=True, comm_hook=args.comm_hook)
+                         gradient_as_bucket_view=True, comm_hook=args.comm_hook, impl=args.ddp_impl)
 
     def step(i):
         x, y = next_batch(i)
@@ -665,6 +691,10 @@ def main():
     if any_rank(not (math.isfinite(loss_first) and math.isfinite(loss_last)), device):
         refuse(rank, record(None, ms, losses), f"non-finite training loss (first {loss_first}, last {loss_last})",
                args.json_out)
+    sync_rec = rank_consistency(model, device, world)
+    if not sync_rec["ranks_in_sync"] and rank == 0:
+        print(f"bench.py: WARNING ranks diverged after the timed steps: {sync_rec}", file=sys.stderr, flush=True)
+    losses.update(sync_rec)
     # host enqueue cost of one step with an idle GPU (cpu_issue above includes the time the
     # host waits on a full submission queue while the GPU is busy)
     sync()

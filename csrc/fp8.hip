@@ -12,6 +12,7 @@
 // v_cvt_pk_bf8_f32 (round to nearest even); inputs are clamped to the format's
 // finite range first, so nothing overflows to NaN.
 #include <cstdlib>
+#include <mutex>
 
 #include "pdt_common.h"
 
@@ -267,7 +268,9 @@ __global__ void __launch_bounds__(1024) cast_fp8_delayed_cs_kernel(const u16* __
                                                                    uint8_t* __restrict__ q, float* __restrict__ cpart,
                                                                    const u16* __restrict__ zz = nullptr, int RG = 1) {
   __shared__ float red[16];
-  __shared__ f32x4 csh[1024 * 2];  // [RG][c8n][8] column partials (RG * c8n <= 1024)
+  // [RG][c8n][8] column partials (RG * c8n <= 1024): dynamic, sized by the launcher only when
+  // RG > 1 -- an RG == 1 launch reserves no LDS for it (a static 32 KB array cost them occupancy)
+  extern __shared__ f32x4 csh[];
   const float s = meta[0];
   const int c8n = cols / 8;
   const int r0 = blockIdx.x * rpb, r1 = min(rows, r0 + rpb);
@@ -521,15 +524,39 @@ PDT_API int pdt_cast_cs_bands(int rows) {
 // 201 728 x 2304: 1 576 bands of 896 threads at 2 per CU = 3.08 rounds, the fourth 8 % full).
 // Fewer bands never need more cpart: the reduce workspace grows with the band count.
 // PDT_CAST_CS_ROUNDS=0: the bound itself (A/B runs).
-static int cs_launch_bands(const void* kern, int rows, int nt) {
+// The occupancy answer is cached per (kernel, threads, LDS bytes): the query is host time on
+// every cast launch otherwise (the step is partly host-issue-bound).
+static int cs_blocks_per_cu(const void* kern, int nt, size_t sh) {
+  struct Ent {
+    const void* k;
+    int nt;
+    size_t sh;
+    int per;
+  };
+  static Ent cache[32];
+  static int n = 0;
+  static std::mutex mu;
+  std::lock_guard<std::mutex> lk(mu);
+  for (int i = 0; i < n; ++i)
+    if (cache[i].k == kern && cache[i].nt == nt && cache[i].sh == sh) return cache[i].per;
+  int per = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, kern, nt, sh) != hipSuccess) per = 0;
+  if (n < 32) cache[n++] = Ent{kern, nt, sh, per};
+  return per;
+}
+
+static size_t cs_lds_bytes(int cols, int rg) { return rg > 1 ? (size_t)rg * (cols / 8) * 2 * sizeof(f32x4) : 0; }
+
+static int cs_launch_bands(const void* kern, int rows, int nt, size_t sh) {
   static int env = -1;
   if (env < 0) {
     const char* e = getenv("PDT_CAST_CS_ROUNDS");
     env = e ? atoi(e) : 1;
   }
   const int nb = pdt_cast_cs_bands(rows);
-  int per = 0;
-  if (env == 0 || hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, kern, nt, 0) != hipSuccess || per < 1) return nb;
+  if (env == 0) return nb;
+  const int per = cs_blocks_per_cu(kern, nt, sh);
+  if (per < 1) return nb;
   const int slots = per * pdt_num_cus();
   return nb > slots ? nb / slots * slots : nb;
 }
@@ -541,14 +568,16 @@ PDT_API int pdt_cast_fp8_delayed_cs(const void* x, int rows, int cols, float* me
   const u16* X = (const u16*)x;
   int nt, rg;
   cs_block(cols, &nt, &rg);
+  const size_t sh = cs_lds_bytes(cols, rg);
   const int nb = cs_launch_bands(
-      fmt == 0 ? (const void*)cast_fp8_delayed_cs_kernel<0> : (const void*)cast_fp8_delayed_cs_kernel<1>, rows, nt);
+      fmt == 0 ? (const void*)cast_fp8_delayed_cs_kernel<0> : (const void*)cast_fp8_delayed_cs_kernel<1>, rows, nt,
+      sh);
   const int rpb = (rows + nb - 1) / nb;
   if (fmt == 0)
-    hipLaunchKernelGGL(cast_fp8_delayed_cs_kernel<0>, dim3(nb), dim3(nt), 0, st, X, rows, cols, rpb, meta,
+    hipLaunchKernelGGL(cast_fp8_delayed_cs_kernel<0>, dim3(nb), dim3(nt), sh, st, X, rows, cols, rpb, meta,
                        (uint8_t*)q, cpart, nullptr, rg);
   else
-    hipLaunchKernelGGL(cast_fp8_delayed_cs_kernel<1>, dim3(nb), dim3(nt), 0, st, X, rows, cols, rpb, meta,
+    hipLaunchKernelGGL(cast_fp8_delayed_cs_kernel<1>, dim3(nb), dim3(nt), sh, st, X, rows, cols, rpb, meta,
                        (uint8_t*)q, cpart, nullptr, rg);
   if (fmt == 0) hipLaunchKernelGGL(fp8_meta_roll_kernel<0>, dim3(1), dim3(64), 0, st, meta, dq_out);
   else hipLaunchKernelGGL(fp8_meta_roll_kernel<1>, dim3(1), dim3(64), 0, st, meta, dq_out);
@@ -564,15 +593,16 @@ PDT_API int pdt_cast_fp8_gelu_grad_cs(const void* x, const void* z, int rows, in
   if (cols % 8 != 0 || rows < 1 || !z || !cpart || !bias_out) return -1;
   int nt, rg;
   cs_block(cols, &nt, &rg);
+  const size_t sh = cs_lds_bytes(cols, rg);
   const int nb = cs_launch_bands(fmt == 0 ? (const void*)cast_fp8_delayed_cs_kernel<0, true>
                                           : (const void*)cast_fp8_delayed_cs_kernel<1, true>,
-                                 rows, nt);
+                                 rows, nt, sh);
   const int rpb = (rows + nb - 1) / nb;
   if (fmt == 0)
-    hipLaunchKernelGGL((cast_fp8_delayed_cs_kernel<0, true>), dim3(nb), dim3(nt), 0, st, (const u16*)x, rows, cols,
+    hipLaunchKernelGGL((cast_fp8_delayed_cs_kernel<0, true>), dim3(nb), dim3(nt), sh, st, (const u16*)x, rows, cols,
                        rpb, meta, (uint8_t*)q, cpart, (const u16*)z, rg);
   else
-    hipLaunchKernelGGL((cast_fp8_delayed_cs_kernel<1, true>), dim3(nb), dim3(nt), 0, st, (const u16*)x, rows, cols,
+    hipLaunchKernelGGL((cast_fp8_delayed_cs_kernel<1, true>), dim3(nb), dim3(nt), sh, st, (const u16*)x, rows, cols,
                        rpb, meta, (uint8_t*)q, cpart, (const u16*)z, rg);
   if (fmt == 0) hipLaunchKernelGGL(fp8_meta_roll_kernel<0>, dim3(1), dim3(64), 0, st, meta, dq_out);
   else hipLaunchKernelGGL(fp8_meta_roll_kernel<1>, dim3(1), dim3(64), 0, st, meta, dq_out);

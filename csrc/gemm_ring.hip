@@ -467,6 +467,11 @@ int ring_run(const void* a, const void* b, void* c, const float* bias, const flo
       lda < K || ldb < K || ldc < N)
     return -5;
   if ((long)M * lda * esz >= (1L << 40)) return -1;
+  // 16-B LDS-DMA / global loads and 16-B / 8-B epilogue stores go through these pointers: a
+  // view with an offset is "not applicable" (-5) here, not a fault
+  if ((((uintptr_t)a | (uintptr_t)b | (uintptr_t)c | (uintptr_t)addend | (uintptr_t)aux) & 15) != 0 ||
+      ((uintptr_t)q8 & 7) != 0)
+    return -5;
   if (!(act == 0 || act == 3 || act == 4 || act == 5)) return -5;
   if ((act == 3 || act == 5) && addend == nullptr) return -4;
   if (act == 4 && (aux == nullptr || addend != nullptr)) return -4;

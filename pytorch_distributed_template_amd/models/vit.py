@@ -88,7 +88,7 @@ class Block(nn.Module):
         # the LayerNorm backward kernels the e5m2 output gradients of the previous block's
         # fc2 / this block's proj -- the layers that produced their inputs).
         # fp8 with _ln_add(): the adds move into the next LayerNorm kernel (fused.ln_add_fork)
-        # so proj / fc2 are plain GEMMs the tuner may give to hipBLASLt; ``pending`` = the
+        # so proj / fc2 are plain GEMMs (no addend epilogue); ``pending`` = the
         # previous block's (fc2 output, residual) pair, ``defer``: return this block's pair.
         if pending is not None:
             x, h = fused.ln_add_fork(pending[0], pending[1], self.norm1, self.attn.qkv if fp8 else None,

@@ -2432,99 +2432,48 @@ def fp8_weight(w: torch.Tensor):
     return val
 
 
-# Tuned-table id of the library path for PLAIN fp8 GEMMs (no activation / aux / addend / fp8
-# side output; bias allowed, added in bf16): hipBLASLt through torch._scaled_mm with the
-# device dequant scales as its scale operands (no host sync). OFF by default: every fp8 GEMM
-# of the framework runs on its own CDNA4 tiles; ``PDT_FP8_LIB=1`` enables the library path as
-# an A/B reference (it measured 1.16-1.42x the round-4 native ring tiles on the ViT-B/16
-# batch-1024 data-gradient shapes, profiles/vit_fp8_gemm_library_round4.txt).
-F8_LIB = 100
-
-
-def _fp8_lib_enabled() -> bool:
-    return os.environ.get("PDT_FP8_LIB", "0") == "1"
-_F8_LIB_BROKEN: list = []  # set once torch._scaled_mm refused a call: every library id runs native
-
-
-def _f8_lib_ok(out, act, aux, addend, q8) -> bool:
-    return act == 0 and aux is None and addend is None and q8 is None and out.is_contiguous() and \
-        hasattr(torch, "_scaled_mm") and _fp8_lib_enabled()
-
-
-_BIAS16: dict = {}
-
-
-def _bias_bf16(bias):
-    """bf16 copy of an fp32 bias for the library GEMM, cached per tensor version (the same
-    parameter serves every step's forward until the optimizer updates it)."""
-    if not isinstance(bias, torch.nn.Parameter):  # (a temporary: nothing to reuse)
-        return bias.to(torch.bfloat16)
-    ent = _BIAS16.get(id(bias))
-    if ent is not None and ent[0] == bias._version and ent[1] == bias.data_ptr() and _same_tensor(ent[3], bias):
-        return ent[2]
-    bb = bias.detach().to(torch.bfloat16)
-    _BIAS16[id(bias)] = (bias._version, bias.data_ptr(), bb, _weak(bias))
-    return bb
-
-
-def _gemm_f8_lib(a, b, out, dq_a, dq_b, fmt_a, bias):
-    """The plain fp8 GEMM of the split-epilogue paths below (fc1 forward, fc2 data gradient):
-    the framework's own tiles (tuned per shape; the 256x256 ring, csrc/gemm_ring.hip, on the
-    ViT shapes) -- or hipBLASLt through torch._scaled_mm when PDT_FP8_LIB=1."""
-    if not _fp8_lib_enabled():
-        gemm_f8(a, b, out, dq_a, dq_b, fmt_a=fmt_a, bias=bias)
-        return 0
-    M, N = a.shape[0], b.shape[0]
-    A = a.view(torch.float8_e5m2 if fmt_a == E5M2 else torch.float8_e4m3fn)
-    B = b.view(torch.float8_e4m3fn).t()  # [K][N] column-major: the layout hipBLASLt takes
-    bb = _bias_bf16(bias) if bias is not None else None
-    torch._scaled_mm(A, B, scale_a=dq_a.reshape(()), scale_b=dq_b.reshape(()), bias=bb, out_dtype=torch.bfloat16,
-                     out=out.view(M, N))
-    return 0
-
-
-def _fc1_lib(M, Hd, K) -> bool:
-    """The MLP's fp8 fc1 as a plain GEMM (+bias; ``_gemm_f8_lib``) followed by one pass that
-    writes gelu'(z), the e4m3 codes of gelu(z) and their amax (pdt_gelu_dual_cast_fp8), instead
-    of one GEMM with that epilogue fused (act 4 + fp8 side output). Off by default: the dense
-    ring's fused epilogue (csrc/gemm_ring.hip) measured faster than the split (ViT-B/16 fp8 bs
-    1024: 9 404 vs 9 175 img/s with the fc2 data gradient below, same box, r5b). Tuned-table
-    key ``fc1split:M,Hd,K`` (1 = split); PDT_FP8_FC1_LIB=0/1 forces either."""
-    if _F8_LIB_BROKEN:
-        return False
-    env = os.environ.get("PDT_FP8_FC1_LIB")
+def _fc1_split(M, Hd, K) -> bool:
+    """The MLP's fp8 fc1 as a plain GEMM (+bias) followed by one pass that writes gelu'(z), the
+    e4m3 codes of gelu(z) and their amax (pdt_gelu_dual_cast_fp8), instead of one GEMM with that
+    epilogue fused (act 4 + fp8 side output). Off by default: the dense ring's fused epilogue
+    (csrc/gemm_ring.hip) measured faster than the split (ViT-B/16 fp8 bs 1024: 9 404 vs 9 175
+    img/s with the fc2 data gradient below, same box, r5b). Tuned-table key
+    ``fc1split:M,Hd,K`` (1 = split); PDT_FP8_FC1_SPLIT=0/1 forces either. (The hipBLASLt A/B
+    of these plain GEMMs lives in ``scripts/probe_scaled_mm.py`` / ``scripts/bench_f8.py``,
+    not in the product.)"""
+    env = os.environ.get("PDT_FP8_FC1_SPLIT")
     if env is not None:
         return env == "1"
     return bool(_tuned().get(f"fc1split:{M},{Hd},{K}", 0))
 
 
-def _fc1_lib_forward(xq, w1q, a, z, aq, dqx, dqw1, bias1, meta, keep_a):
-    """a <- x W1^T + b1 (library GEMM), then z <- gelu'(a) (z None: not formed -- the caller keeps
+def _fc1_split_forward(xq, w1q, a, z, aq, dqx, dqw1, bias1, meta, keep_a):
+    """a <- x W1^T + b1 (plain fp8 GEMM), then z <- gelu'(a) (z None: not formed -- the caller keeps
     the pre-activation a), aq <- e4m3(gelu(a)), and (keep_a) a <- gelu(a) in place. Returns the
     codes' dequant factor (device [1])."""
     lib = _load()
     dqa = torch.empty(1, dtype=torch.float32, device=a.device)
-    _gemm_f8_lib(xq, w1q, a, dqx, dqw1, E4M3, bias1)
+    gemm_f8(xq, w1q, a, dqx, dqw1, fmt_a=E4M3, bias=bias1)
     _chk(lib.pdt_gelu_dual_cast_fp8(_p(a), a.numel(), _p(meta), E4M3, _p(aq), _p(z) if z is not None else None,
                                     _p(a) if keep_a else None, _p(dqa), _s()), "gelu_dual_cast_fp8")
     return dqa
 
 
-def _fc2_dgrad_lib_on() -> bool:
-    """The MLP's fc2 data gradient as a plain GEMM (bf16 g W2; ``_gemm_f8_lib``) followed by one
-    pass that multiplies by gelu'(z), casts to e5m2 and sums fc1's bias gradient
+def _fc2_dgrad_split_on() -> bool:
+    """The MLP's fc2 data gradient as a plain GEMM (bf16 g W2) followed by one pass that
+    multiplies by gelu'(z), casts to e5m2 and sums fc1's bias gradient
     (pdt_cast_fp8_gelu_grad_cs), instead of one GEMM with that epilogue (act 3 + e5m2 + column
-    sums). Off by default (the fused ring epilogue is faster, see ``_fc1_lib``);
-    PDT_FC2_DGRAD_LIB=1 turns it on."""
-    return not _F8_LIB_BROKEN and os.environ.get("PDT_FC2_DGRAD_LIB", "0") == "1"
+    sums). Off by default (the fused ring epilogue is faster, see ``_fc1_split``);
+    PDT_FC2_DGRAD_SPLIT=1 turns it on."""
+    return os.environ.get("PDT_FC2_DGRAD_SPLIT", "0") == "1"
 
 
-def _fc2_dgrad_lib(gq, w2qt, dz, dqg, dqw2, z, dzq, gmeta, db):
-    """dz <- g W2 (library), then dzq <- e5m2(dz * gelu'(z)) and db <- column sums of dz * gelu'(z).
+def _fc2_dgrad_split(gq, w2qt, dz, dqg, dqw2, z, dzq, gmeta, db):
+    """dz <- g W2 (plain fp8 GEMM), then dzq <- e5m2(dz * gelu'(z)) and db <- column sums of dz * gelu'(z).
     Returns the codes' dequant factor (device [1])."""
     lib = _load()
     rows, cols = dz.shape
-    _gemm_f8_lib(gq, w2qt, dz, dqg, dqw2, E5M2, None)
+    gemm_f8(gq, w2qt, dz, dqg, dqw2, fmt_a=E5M2)
     nb = lib.pdt_cast_cs_bands(rows)
     cpart = torch.empty(nb * cols + lib.pdt_reduce_rows_work(nb, cols), dtype=torch.float32, device=dz.device)
     dq = torch.empty(1, dtype=torch.float32, device=dz.device)
@@ -2534,7 +2483,7 @@ def _fc2_dgrad_lib(gq, w2qt, dz, dqg, dqw2, z, dzq, gmeta, db):
 
 
 def _fc1_keep_pre() -> bool:
-    """Library fc1 with fp8 weight gradients: keep the GEMM's own pre-activation output for the
+    """Split fc1 with fp8 weight gradients: keep the GEMM's own pre-activation output for the
     backward (whose fc2 data-gradient epilogue then forms gelu'(z) itself, act 3) instead of
     writing gelu'(z) in the cast pass -- one bf16 [M, 4D] store fewer per block."""
     return os.environ.get("PDT_FC1_KEEP_PRE", "1") == "1"
@@ -2561,32 +2510,15 @@ def gemm_f8(a, b, out, dq_a, dq_b, *, fmt_a=E4M3, bias=None, act=0, aux=None, ad
     if q8 is None:
         args = lambda v: (_p(a), _p(b), _p(out), _p(bias), _p(dq_a), _p(dq_b), M, N, K, K, K, N, fmt_a, act,  # noqa
                           _p(aux), _p(addend), v, _s())
-        lib_ok = _f8_lib_ok(out, act, aux, addend, q8)
+        nv = lib.pdt_gemm_f8_num_variants()
         if variant is None:
-            # ",r": a residual addend in the epilogue (a different best tile, and no library path);
-            # "f8c": the variant set with the dense ring (ids 12 / 13) -- "f8b" choices predate it
+            # ",r": a residual addend in the epilogue (a different best tile); "f8c": the variant
+            # set with the dense ring (ids 12 / 13)
             key = f"f8c:{M},{N},{K},{fmt_a},{act},{int(bias is not None)}" + (",r" if addend is not None and act == 0
                                                                                else "")
-            nv = lib.pdt_gemm_f8_num_variants()
-            if not lib_ok and int(_tuned().get(key, -1)) == F8_LIB:
-                key += ",nat"  # the table chose the (now disabled) library path: the best native tile
-            # candidate nv (tuning only) = the library path, stored as F8_LIB
-            run = lambda v: lib.pdt_gemm_f8(*args(v)) if v < nv else _gemm_f8_lib(a, b, out, dq_a, dq_b,  # noqa
-                                                                                  fmt_a, bias)
-            variant = _autotune(key, nv + int(lib_ok), run)
-            if variant == nv and lib_ok:
-                variant = F8_LIB
-                _tuned()[key] = F8_LIB
-                _save_tuned()
-        if variant == F8_LIB:
-            if lib_ok and not _F8_LIB_BROKEN:
-                try:
-                    return _gemm_f8_lib(a, b, out, dq_a, dq_b, fmt_a, bias) or out
-                except RuntimeError as e:  # a hipBLASLt without this fp8 layout / bias combination
-                    _F8_LIB_BROKEN.append(str(e))
-                    import warnings
-                    warnings.warn(f"fp8 library GEMM unavailable ({e}); using the native tiles")
-            variant = -1  # (library path disabled / not applicable: the built-in native choice)
+            variant = _autotune(key, nv, lambda v: lib.pdt_gemm_f8(*args(v)))
+        if variant >= nv:
+            variant = -1  # (a stale table entry: the built-in native choice)
         _chk_v(lib.pdt_gemm_f8(*args(variant)), "gemm_f8")
         return out
     codes, meta, qfmt, only = q8
@@ -2851,15 +2783,12 @@ class _Mlp(torch.autograd.Function):
             if meta2 is not None:  # fc1's epilogue writes fc2's e4m3 input (bf16 a only if a bf16 wgrad needs it)
                 aq = torch.empty((Mrows, Hd), dtype=torch.uint8, device=dev)
                 dqa = None
-                if dual and _fc1_lib(Mrows, Hd, K):
+                if dual and _fc1_split(Mrows, Hd, K):
                     pre = f8w and _fc1_keep_pre()
                     z = None if pre else torch.empty_like(a)
-                    try:
-                        dqa = _fc1_lib_forward(xq, w1q, a, z, aq, dqx, dqw1, bias1, meta2, keep_a=not f8w)
-                        if pre:  # a holds the pre-activation (its gelu lives only as the e4m3 codes)
-                            z, act2 = a, ACT_GELU_GRAD
-                    except RuntimeError as e:  # (see gemm_f8: the native tiles from here on)
-                        _F8_LIB_BROKEN.append(str(e))
+                    dqa = _fc1_split_forward(xq, w1q, a, z, aq, dqx, dqw1, bias1, meta2, keep_a=not f8w)
+                    if pre:  # a holds the pre-activation (its gelu lives only as the e4m3 codes)
+                        z, act2 = a, ACT_GELU_GRAD
                 if dqa is None:
                     z = torch.empty_like(a)
                     dqa = gemm_f8(xq, w1q, a, dqx, dqw1, bias=bias1, act=act1, aux=z, q8=(aq, meta2, E4M3, f8w))
@@ -2906,11 +2835,8 @@ class _Mlp(torch.autograd.Function):
                     # fc1's bias gradient = column sums of dz formed in this epilogue: the bf16 dz
                     # (only ever read for it) is not written at all
                     pre_db1 = _grad_buf(ctx.brefs[0], (Hd,))
-                    if ctx.act2 == ACT_GELU_GRAD and _fc2_dgrad_lib_on():  # z: the pre-activation
-                        try:
-                            dqdz = _fc2_dgrad_lib(gq, w2qt, dz, dqg, dqw2, z, dzq, gmeta1, pre_db1)
-                        except RuntimeError as e:  # (see gemm_f8: the native tiles from here on)
-                            _F8_LIB_BROKEN.append(str(e))
+                    if ctx.act2 == ACT_GELU_GRAD and _fc2_dgrad_split_on():  # z: the pre-activation
+                        dqdz = _fc2_dgrad_split(gq, w2qt, dz, dqg, dqw2, z, dzq, gmeta1, pre_db1)
                     if dqdz is None:
                         dqdz = gemm_f8(gq, w2qt, dz, dqg, dqw2, fmt_a=E5M2, act=ctx.act2, addend=z,
                                        q8=(dzq, gmeta1, E5M2, True), colsum_out=pre_db1)
@@ -3101,7 +3027,7 @@ def _ln_fork_backward(ctx, g_res, dy):
 class _LNAddFork(torch.autograd.Function):
     """(s, LayerNorm(s)) with s = y + r: the pre-norm block's residual add done by the
     LayerNorm kernel (it reads y and r, writes s) instead of the epilogue of the GEMM that
-    produced y -- so that GEMM can be a library one (the fp8 proj / fc2 on hipBLASLt). Backward
+    produced y -- so that GEMM is a plain ring GEMM (no residual addend in its epilogue). Backward
     as _LNFork; y and r both receive the summed gradient."""
 
     @staticmethod

@@ -66,8 +66,8 @@ def wrap_ddp(model: torch.nn.Module, device: torch.device, bucket_cap_mb: float 
     if comm_hook in ("bf16", "fp16"):
         impl = "torch"
     if impl == "native":
-        from .reducer import DataParallel
-        return DataParallel(model, device, bucket_cap_mb=bucket_cap_mb, first_bucket_mb=first_bucket_mb,
+        from .reducer import BucketedDDP
+        return BucketedDDP(model, device, bucket_cap_mb=bucket_cap_mb, first_bucket_mb=first_bucket_mb,
                             broadcast_buffers=broadcast_buffers)
     kwargs = dict(bucket_cap_mb=bucket_cap_mb, broadcast_buffers=broadcast_buffers,
                   gradient_as_bucket_view=gradient_as_bucket_view, static_graph=static_graph,
@@ -83,8 +83,8 @@ def wrap_ddp(model: torch.nn.Module, device: torch.device, bucket_cap_mb: float 
 
 
 def is_data_parallel(model) -> bool:
-    from .reducer import DataParallel
-    return isinstance(model, (DistributedDataParallel, DataParallel))
+    from .reducer import BucketedDDP
+    return isinstance(model, (DistributedDataParallel, BucketedDDP))
 
 
 def pretune_for_ddp(model: torch.nn.Module, step_fn) -> None:

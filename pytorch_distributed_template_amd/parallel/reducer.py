@@ -49,6 +49,7 @@ like any other work on the capture stream.
 from __future__ import annotations
 
 import contextlib
+import hashlib
 from typing import List, Optional
 
 import torch
@@ -133,7 +134,7 @@ def plan_buckets(params: List[torch.Tensor], bucket_cap_mb: float, first_bucket_
     return buckets
 
 
-class DataParallel(torch.nn.Module):
+class BucketedDDP(torch.nn.Module):
     """Data-parallel wrapper over a process group (RCCL on GPUs, gloo on CPU): same contract as
     the torch DDP wrapper the reference uses -- ``.module``, forward passthrough, gradients
     averaged over the ranks when backward returns -- with the bucketing above."""
@@ -171,7 +172,7 @@ class DataParallel(torch.nn.Module):
             for i, off in zip(idx, offs):
                 p = self.params[i]
                 if not _dense(p):
-                    raise ValueError("DataParallel: every parameter must be dense (no overlapping strides)")
+                    raise ValueError("BucketedDDP: every parameter must be dense (no overlapping strides)")
                 p._pdt_grad_slot = (flat, off)
                 self._bucket_of[id(p)] = bi
                 bparams.append(p)
@@ -180,14 +181,24 @@ class DataParallel(torch.nn.Module):
 
     # ------------------------------------------------------------------ setup
     def _verify_shapes(self):
-        """Every rank must hold the same parameter list (else the buckets would not line up)."""
-        sig = torch.tensor([len(self.params)] + [p.numel() for p in self.params][:4096], dtype=torch.int64)
+        """Every rank must hold the same parameter list (else the buckets would not line up):
+        [count, total elements, a digest of every parameter's shape and dtype in order] --
+        fixed size whatever the parameter count -- must be equal on all ranks."""
+        h = hashlib.sha256()
+        for p in self.params:
+            h.update(repr((tuple(p.shape), str(p.dtype))).encode())
+        d = h.digest()
+        sig = torch.tensor([len(self.params), sum(p.numel() for p in self.params),
+                            int.from_bytes(d[:7], "little"), int.from_bytes(d[7:14], "little")], dtype=torch.int64)
         dev = self.device if self.device.type == "cuda" else torch.device("cpu")
-        mine = sig.to(dev)
-        ref = mine.clone()
-        dist.broadcast(ref, src=0, group=self.process_group)
-        if not torch.equal(mine, ref):
-            raise RuntimeError("DataParallel: parameter shapes differ between ranks")
+        # MAX of (sig, -sig): every rank learns the max AND the min, so a mismatch raises on
+        # EVERY rank (a broadcast from rank 0 would let rank 0 continue into the parameter
+        # broadcast and wait there for the ranks that raised)
+        t = torch.cat([sig, -sig]).to(dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX, group=self.process_group)
+        t = t.cpu()
+        if not (torch.equal(t[:4], sig) and torch.equal(-t[4:], sig)):
+            raise RuntimeError("BucketedDDP: parameter shapes differ between ranks")
 
     @torch.no_grad()
     def _broadcast_state(self):
@@ -203,6 +214,11 @@ class DataParallel(torch.nn.Module):
             # DDP prepares its reducer in forward
             self._in_backward = False
             for b in self.buckets:
+                if b.work is not None:
+                    # an all-reduce launched before the failure may still be running on RCCL's
+                    # stream over b.flat: make the compute stream wait for it before the next
+                    # backward's kernels write into the same slots
+                    b.work.wait()
                 b.ready, b.work, b.launched = 0, None, False
         if self.broadcast_buffers and self.world > 1:
             bufs = list(self.module.buffers())

@@ -19,6 +19,31 @@ from pathlib import Path
 import torch
 
 
+def set_deterministic(on: bool):
+    """``--deterministic``: MIOpen/torch deterministic algorithms AND fixed native
+    kernel variants (no autotune timing: the shipped table or the heuristic, the
+    same on every run and rank; every reduction in csrc/ is atomic-free)."""
+    if on:
+        import os
+        torch.backends.cudnn.deterministic = True
+        torch.backends.cudnn.benchmark = False
+        os.environ["PDT_DETERMINISTIC"] = "1"
+
+
+def seed_everything(seed, deterministic=False):
+    """``--seed`` (reference train.py:101-106 / test.py:120-125, whose test.py seeds numpy
+    without importing it): torch, numpy and Python RNGs, then ``set_deterministic``."""
+    import random
+
+    import numpy as np
+    torch.manual_seed(seed)
+    np.random.seed(seed)
+    random.seed(seed)
+    torch.backends.cudnn.deterministic = deterministic
+    torch.backends.cudnn.benchmark = False
+    set_deterministic(deterministic)
+
+
 def ensure_dir(dirname):
     dirname = Path(dirname)
     if not dirname.is_dir():

@@ -11,9 +11,7 @@ rank 0 as fixed-shape tensors and logs
 Fixes ``--seed`` (the reference hit a NameError).
 """
 import argparse
-import random
 
-import numpy as np
 import torch
 
 from pytorch_distributed_template_amd.base.base_trainer import load_checkpoint, strip_module_prefix
@@ -21,6 +19,7 @@ from pytorch_distributed_template_amd.config import ConfigParser
 from pytorch_distributed_template_amd.runtime import (autocast_dtype, build_criterion_metrics, build_loader,
                                                       build_model)
 from pytorch_distributed_template_amd.utils import dist as pdist
+from pytorch_distributed_template_amd.utils.util import seed_everything, set_deterministic
 
 
 @torch.no_grad()
@@ -84,11 +83,9 @@ def cli(argv=None):
     if ns.backend:
         config["trainer"]["backend"] = ns.backend
     if ns.seed is not None:
-        torch.manual_seed(ns.seed)
-        np.random.seed(ns.seed)
-        random.seed(ns.seed)
-        torch.backends.cudnn.deterministic = ns.deterministic
-        torch.backends.cudnn.benchmark = False
+        seed_everything(ns.seed, ns.deterministic)
+    elif ns.deterministic:
+        set_deterministic(True)
     try:
         return main(ns, config, device)
     finally:

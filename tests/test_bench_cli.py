@@ -43,6 +43,8 @@ def test_bench_self_launches_two_cpu_ranks():
     assert rec["config"]["dist_backend"] == "gloo"
     assert rec["steps"] == 1 and rec["warmup"] == 1
     assert rec["value"] > 0
+    assert rec["config"]["ddp_impl"] == "BucketedDDP"  # the framework's reducer, not torch DDP
+    assert rec["config"]["ranks_in_sync"] is True and rec["config"]["ranks_checked"] == 2
 
 
 @pytest.mark.skipif(__import__("torch").cuda.device_count() >= 2, reason="host has >= 2 GPUs")
@@ -90,6 +92,10 @@ def test_bench_eight_cpu_ranks_one_json_line():
     assert rec["config"]["global_batch"] == 16
     assert rec["config"]["loss_first"] is not None and rec["config"]["loss_last"] is not None
     assert rec["config"]["grad_allreduce_probe"] is None  # CPU ranks: no RCCL probe
+    # the framework's reducer over 8 ranks, 3 optimizer steps: every rank holds the same weights
+    assert rec["config"]["ddp_impl"] == "BucketedDDP"
+    assert rec["config"]["ranks_in_sync"] is True and rec["config"]["ranks_checked"] == 8
+    assert rec["config"]["param_checksum_max_rank_diff"] == 0.0
 
 
 def test_bench_refuses_a_nan_step():

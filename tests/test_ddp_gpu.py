@@ -69,3 +69,27 @@ def test_ddp_two_ranks_native_kernels():
     for r, v in res.items():
         assert not isinstance(v, str), v
         assert v < 1e-3, (r, v)
+
+
+def test_bench_two_gloo_ranks_native_kernels_reducer_in_sync():
+    """bench.py at N = 2 on the one GPU: two ranks (gloo transport, RCCL needs a GPU per rank)
+    running the native kernels and the framework's reducer for several optimizer steps; the
+    JSON line must report a finite loss and ``ranks_in_sync`` (bitwise-equal weights)."""
+    import json
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1", HSA_ENABLE_IPC_MODE_LEGACY="0", OMP_NUM_THREADS="2")
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK"):
+        env.pop(k, None)
+    r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "2", "--dist-backend", "gloo",
+                        "--batch", "64", "--steps", "3", "--warmup", "1"], cwd=root, env=env, capture_output=True,
+                       text=True, timeout=600)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{") and '"metric"' in ln]
+    assert len(lines) == 1, r.stdout[-2000:]
+    rec = json.loads(lines[0])
+    c = rec["config"]
+    assert rec["n_gpus"] == 2 and c["backend"] == "native" and c["ddp_impl"] == "BucketedDDP"
+    assert c["loss_first"] is not None and c["loss_last"] is not None
+    assert c["ranks_in_sync"] is True and c["ranks_checked"] == 2, c

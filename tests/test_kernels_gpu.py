@@ -634,36 +634,6 @@ def test_gelu_dual_and_mul_epilogues_all_variants():
         assert relerr(aux, d8) < 1e-2, (v, relerr(aux, d8))
 
 
-@pytest.mark.parametrize("fmt", [0, 1])
-@pytest.mark.parametrize("with_bias", [False, True])
-def test_gemm_f8_library_path(fmt, with_bias, monkeypatch):
-    """The tuned-table library id (F8_LIB: hipBLASLt through torch._scaled_mm, device dequant
-    scales; off unless PDT_FP8_LIB=1) computes the plain fp8 GEMM the native tiles do -- e5m2
-    x e4m3 (data gradient) included; with a bias it is added in bf16, and an epilogue the
-    library lacks falls back to the native kernel."""
-    monkeypatch.setenv("PDT_FP8_LIB", "1")
-    torch.manual_seed(21 + fmt)
-    M, N, K = 1000, 768, 384
-    a = torch.randn(M, K, device="cuda").to(torch.bfloat16)
-    b = torch.randn(N, K, device="cuda")
-    qa, dqa = no.quantize_fp8(a, fmt)
-    qb, dqb = no.quantize_fp8(b, 0)
-    bias = torch.randn(N, device="cuda") if with_bias else None
-    ref = (_f8(qa, fmt) * dqa) @ (_f8(qb, 0) * dqb).t() + (bias if with_bias else 0)
-    out = torch.full((M, N), float("nan"), device="cuda").to(torch.bfloat16)
-    nat = torch.empty_like(out)
-    no.gemm_f8(qa, qb, out, dqa, dqb, fmt_a=fmt, bias=bias, variant=no.F8_LIB)
-    no.gemm_f8(qa, qb, nat, dqa, dqb, fmt_a=fmt, bias=bias, variant=10)
-    torch.cuda.synchronize()
-    assert relerr(out, ref) < 1e-2, relerr(out, ref)
-    assert relerr(out, nat) < 1e-2
-    # GELU epilogue requested with the library id: the native kernel runs instead
-    z = torch.empty_like(out)
-    no.gemm_f8(qa, qb, out, dqa, dqb, fmt_a=fmt, bias=bias, act=2, aux=z, variant=no.F8_LIB)
-    torch.cuda.synchronize()
-    assert relerr(z, ref) < 1e-2
-
-
 def test_linear_fp8_autograd():
     torch.manual_seed(12)
     fc = nn.Linear(768, 3072).cuda()

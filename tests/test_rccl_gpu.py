@@ -59,7 +59,7 @@ def _worker(port, hook, q):
         fused.softmax_cross_entropy(ref(x), y).backward()
         ddp = wrap_ddp(model, dev, bucket_cap_mb=8, broadcast_buffers=True, gradient_as_bucket_view=True,
                        comm_hook=hook)
-        assert type(ddp).__name__ == ("DistributedDataParallel" if hook else "DataParallel")
+        assert type(ddp).__name__ == ("DistributedDataParallel" if hook else "BucketedDDP")
         fused.softmax_cross_entropy(ddp(x), y).backward()
         torch.cuda.synchronize()
         errs, views = [], 0
@@ -137,7 +137,7 @@ def test_resnet50_config_torchrun_rccl_train_resume_test(tmp_path):
 
     out = run(["train.py", "-c", str(p), "--backend", "native"])
     assert "process group: nccl, world size 1" in out, out[-3000:]
-    assert "DataParallel(" in out  # the model print is the data-parallel wrapper
+    assert "BucketedDDP(" in out  # the model print is the data-parallel wrapper
     ck = tmp_path / cfg["name"] / "train" / "t1" / "checkpoint-epoch1.pth"
     assert ck.exists(), out[-3000:]
     state = torch.load(ck, weights_only=True, map_location="cpu")

@@ -45,11 +45,11 @@ class Net(torch.nn.Module):
 def _w_reducer(rank, world, port, q):
     try:
         pdist = _init(rank, world, port)
-        from pytorch_distributed_template_amd.parallel.reducer import DataParallel, SLOT_ALIGN
+        from pytorch_distributed_template_amd.parallel.reducer import BucketedDDP, SLOT_ALIGN
         torch.manual_seed(0)
         model, ref = Net(), Net()
         ref.load_state_dict(model.state_dict())
-        dp = DataParallel(model, torch.device("cpu"), bucket_cap_mb=0.0001, first_bucket_mb=0.00001)
+        dp = BucketedDDP(model, torch.device("cpu"), bucket_cap_mb=0.0001, first_bucket_mb=0.00001)
         torch.manual_seed(1)
         X = torch.randn(8, 3, 6, 6)
         Y = torch.randint(0, 3, (8,))
@@ -94,13 +94,13 @@ def _w_accumulate(rank, world, port, q):
     ``w`` (the native-kernel path) as well as on the stock-op parameters."""
     try:
         pdist = _init(rank, world, port)
-        from pytorch_distributed_template_amd.parallel.reducer import DataParallel
+        from pytorch_distributed_template_amd.parallel.reducer import BucketedDDP
         torch.manual_seed(0)
         model, ref = Net(), Net()
         ref.load_state_dict(model.state_dict())
         for m in (model, ref):
             m.bn.eval()  # batch-independent normalisation: sums over micro-batches are exact
-        dp = DataParallel(model, torch.device("cpu"), bucket_cap_mb=0.0001, first_bucket_mb=0.00001)
+        dp = BucketedDDP(model, torch.device("cpu"), bucket_cap_mb=0.0001, first_bucket_mb=0.00001)
         torch.manual_seed(1)
         batches = [(torch.randn(8, 3, 6, 6), torch.randint(0, 3, (8,))) for _ in range(3)]
         shard = lambda b: (b[0][rank * 4:(rank + 1) * 4], b[1][rank * 4:(rank + 1) * 4])  # noqa: E731
@@ -132,12 +132,18 @@ def _w_accumulate(rank, world, port, q):
             ce(dp(shard(batches[1])[0]), shard(batches[1])[1]).backward()
         ce(dp(shard(batches[2])[0]), shard(batches[2])[1]).backward()
         out["nosync"] = diff(ref_grads(batches))
-        # (c) a backward that raised before its final callback does not wedge the next step
+        # (c) a backward that raised before its final callback does not wedge the next step,
+        # and an all-reduce it left in flight on a bucket finishes before the next backward
+        # writes that bucket's slots (forward waits for it)
         dp._in_backward = True
+        for b in dp.buckets:
+            b.flat.fill_(1e6)
+            b.work = torch.distributed.all_reduce(b.flat, async_op=True)
         for p in model.parameters():
             p.grad = None
         ce(dp(shard(batches[2])[0]), shard(batches[2])[1]).backward()
         out["after_abort"] = diff(ref_grads([batches[2]]))
+        out["works_cleared"] = all(b.work is None for b in dp.buckets)
         q.put((rank, out))
         pdist.cleanup()
     except Exception as e:  # pragma: no cover
@@ -152,7 +158,39 @@ def test_reducer_accumulates_into_retained_gradients():
         assert isinstance(o, dict), o
         assert o["zero_inplace"] < 1e-6 and abs(o["w_ratio"] - 1) < 1e-6, o
         assert o["nosync"] < 1e-6, o
-        assert o["after_abort"] < 1e-6, o
+        assert o["after_abort"] < 1e-6 and o["works_cleared"], o
+
+
+class _ManyParams(torch.nn.Module):
+    """More than 4 096 parameters; on rank 1 the LAST one has another shape (same numel)."""
+
+    def __init__(self, odd):
+        super().__init__()
+        self.ps = torch.nn.ParameterList([torch.nn.Parameter(torch.zeros(2)) for _ in range(5000)])
+        self.ps.append(torch.nn.Parameter(torch.zeros(1, 2) if odd else torch.zeros(2)))
+
+
+def _w_shape_mismatch(rank, world, port, q):
+    try:
+        pdist = _init(rank, world, port)
+        from pytorch_distributed_template_amd.parallel.reducer import BucketedDDP
+        try:
+            BucketedDDP(_ManyParams(odd=rank == 1), torch.device("cpu"))
+            q.put((rank, {"msg": "constructed"}))
+        except RuntimeError as e:
+            q.put((rank, {"msg": "raised: " + str(e)}))
+        pdist.cleanup()
+    except Exception as e:  # pragma: no cover
+        import traceback
+        q.put((rank, repr(e) + traceback.format_exc()))
+
+
+def test_reducer_shape_check_covers_every_parameter_and_raises_on_every_rank():
+    """The signature covers all parameters (a mismatch at index 5 000 is found) and a mismatch
+    raises on EVERY rank, rank 0 included (else rank 0 would wait in the parameter broadcast)."""
+    res = _run(_w_shape_mismatch)
+    for r in (0, 1):
+        assert res[r]["msg"].startswith("raised: BucketedDDP: parameter shapes differ"), res[r]
 
 
 def test_reducer_matches_single_process_and_uses_slots():

@@ -12,10 +12,7 @@ config/run dir so all ranks agree on ONE run dir (Q5); ``--local-rank``,
 """
 import argparse
 import collections
-import os
-import random
 
-import numpy as np
 import torch
 
 from pytorch_distributed_template_amd.config import ConfigParser
@@ -24,25 +21,7 @@ from pytorch_distributed_template_amd.runtime import (autocast_dtype, build_crit
                                                       wrap_model)
 from pytorch_distributed_template_amd.trainer import Trainer
 from pytorch_distributed_template_amd.utils import dist as pdist
-
-
-def seed_everything(seed, deterministic=False):
-    torch.manual_seed(seed)
-    np.random.seed(seed)
-    random.seed(seed)
-    torch.backends.cudnn.deterministic = deterministic
-    torch.backends.cudnn.benchmark = False
-    set_deterministic(deterministic)
-
-
-def set_deterministic(on: bool):
-    """``--deterministic``: MIOpen/torch deterministic algorithms AND fixed native
-    kernel variants (no autotune timing: the shipped table or the heuristic, the
-    same on every run and rank; every reduction in csrc/ is atomic-free)."""
-    if on:
-        torch.backends.cudnn.deterministic = True
-        torch.backends.cudnn.benchmark = False
-        os.environ["PDT_DETERMINISTIC"] = "1"
+from pytorch_distributed_template_amd.utils.util import seed_everything, set_deterministic
 
 
 def main(args, config, device):
