@@ -106,6 +106,7 @@ class _UpdateCheck:
     ||dW_eager|| over all parameters. Every mutated tensor is restored after each."""
 
     def __init__(self, model, opt, batch):
+        self.opt = opt
         self.state = _train_state(model, opt)
         self.saved = [t.clone() for t in self.state]
         self.params = [p.detach() for p in model.parameters() if p.requires_grad]
@@ -117,6 +118,11 @@ class _UpdateCheck:
     def restore(self):
         for t, s in zip(self.state, self.saved):
             t.copy_(s)
+        if hasattr(self.opt, "sync_shadows"):
+            # the bf16 weight shadows of the restored weights, registered under the new
+            # parameter versions: else the capture below records a weight cast per layer that
+            # every replay repeats, and a replay after a restore reads stale shadows
+            self.opt.sync_shadows()
 
     def eager(self, side, gstep, sx, sy):
         side.wait_stream(torch.cuda.current_stream())

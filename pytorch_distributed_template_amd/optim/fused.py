@@ -132,6 +132,27 @@ class _FusedBase(Optimizer):
             self._dev_lr[gi] = float(group["lr"])
         return d
 
+    @torch.no_grad()
+    def sync_shadows(self):
+        """Re-form every bf16 weight shadow from its fp32 parameter and register it again.
+
+        After parameters were written outside ``step()`` (a state restore, a checkpoint load)
+        the registered shadows no longer match the parameters' versions, so the next forward
+        casts each weight into a NEW buffer -- and a HIP graph captured at that point records
+        those casts and repeats them on every replay (53 extra cast kernels, 0.33 ms, per
+        ResNet-50 replay: ``profiles/graph_vs_eager_resnet50_round6.txt``). Called before a
+        capture, the captured forward reads the shadows the captured ``step()`` rewrites."""
+        if not self.write_bf16_shadow:
+            return
+        from ..ops import native_ops
+        for group in self.param_groups:
+            for p in group["params"]:
+                sh = self._shadows.get(id(p))
+                if sh is None or sh.data_ptr() == 0 or sh.shape != p.shape:
+                    continue
+                sh.copy_(p.detach())
+                native_ops.register_shadow(p, sh)
+
     def refresh_scalars(self):
         """Write each group's current lr into its device scalars (capturable mode): call it
         before replaying a graph that captured ``step()`` -- an LR scheduler changes only the
