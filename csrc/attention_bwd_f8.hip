@@ -46,12 +46,29 @@ struct AttnBwdF8Params {
   long ld, ldo;
   float c, scale;
   float* dbg;  // optional (tests): dS [B*H][ROWS][ROWS] fp32 as phase 1 computes it
+  // Q8 instantiations (pdt_attn_bwd_f8_q8): the qkv projection's e5m2 output gradient and
+  // its bias gradient come out of this kernel instead of a cast pass over bf16 d(qkv):
+  uint8_t* q8;            // [B*T][3*H*64] e5m2 codes of bf16(d(qkv)) * q8_meta[0]
+  const float* q8_meta;   // the projection's delayed-scaling state (scale in [0])
+  float* q8_part;         // [gridDim.x] per-workgroup max |bf16(d(qkv))|
+  float* colpart;         // [B][3*H*64] per-image column sums (the bias gradient's partial rows)
+  int wbf;                // 1: also write the bf16 d(qkv) (0: nothing reads it)
 };
 
 // NQP query-tile pairs: images of ROWS = 64 NQP rows (zero beyond T); 8 waves
 // DBG: the tests' fp32 dS dump (p.dbg) -- compiled only into the debug entry point: in the
 // production kernel its address arithmetic held registers across phase 1 (NQP = 4 sits at 256)
-template <int NQP, bool DBG = false>
+//
+// Q8 (the fused qkv-gradient epilogue): every dK / dV / dQ chunk a lane stores is also
+// converted to e5m2 with the projection's delayed scale (amax over the bf16-rounded values,
+// per workgroup), and the bias gradient's per-image column sums are formed from identities
+// of the attention backward instead of a reduction over the written gradient:
+//   sum_keys dV[key] = sum_q dO[q] (sum_keys P[q][key])         = sum_q dO[q]   (rows of P sum to 1)
+//   sum_keys dK[key] = scale sum_q Q[q] (sum_keys dS[q][key])   = 0             (sum_k P (dP - delta) = 0)
+//   sum_q dQ[q]      : reduced over the 32 query lanes of each dQ unit (DPP + permlane16)
+// (exact in real arithmetic; the dV / dK sums of the fp8-rounded gradients differ from these
+// by their quantisation noise only).
+template <int NQP, bool DBG = false, bool Q8 = false>
 __global__ void __launch_bounds__(512) attn_bwd_f8_kernel(AttnBwdF8Params p) {
   constexpr int NT2 = 2 * NQP;  // 32-row tiles (queries and keys)
   constexpr int ROWS = 32 * NT2;
@@ -61,6 +78,27 @@ __global__ void __launch_bounds__(512) attn_bwd_f8_kernel(AttnBwdF8Params p) {
   __shared__ float nlse_s[ROWS], dl_s[ROWS];
   __shared__ int tsc[NT2 * NT2];  // E8M0 dequant of each dS tile [q tile][key tile]
   __shared__ float red[8][4];
+  // Q8: per head-parity buffers (the sums of head i are read after its closing barrier while
+  // head i + 1 writes the other buffer): dO column sums per wave, dQ column sums per query tile
+  __shared__ float vsum[Q8 ? 2 : 1][8][Q8 ? 64 : 1];
+  __shared__ float qsum[Q8 ? 2 : 1][NT2][Q8 ? 64 : 1];
+  float q8max = 0.f;
+  const float q8s = Q8 ? p.q8_meta[0] : 0.f;
+  // e5m2 codes (scale q8s) of 8 bf16 values -> dst; their |max| into q8max
+  auto q8_put = [&](uint8_t* dst, const u32x4& w) __attribute__((always_inline)) {
+    float f[8];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      f[2 * e] = lo_bf(w[e]);
+      f[2 * e + 1] = hi_bf(w[e]);
+    }
+#pragma unroll
+    for (int e = 0; e < 8; ++e) q8max = fmaxf(q8max, fabsf(f[e]));
+    uint2 c;
+    c.x = pdt_cvt4_f8<1>(f[0] * q8s, f[1] * q8s, f[2] * q8s, f[3] * q8s);
+    c.y = pdt_cvt4_f8<1>(f[4] * q8s, f[5] * q8s, f[6] * q8s, f[7] * q8s);
+    *reinterpret_cast<uint2*>(dst) = c;
+  };
   char* Qi = smem;
   char* Ki = smem + IMG;
   char* Vi = smem + 2 * IMG;
@@ -106,6 +144,28 @@ __global__ void __launch_bounds__(512) attn_bwd_f8_kernel(AttnBwdF8Params p) {
 
   for (int bh = blockIdx.x; bh < nbh; bh += gridDim.x) {
   const int b = bh / p.H, h = bh % p.H;
+  const int hb = Q8 ? ((bh - (int)blockIdx.x) / (int)gridDim.x) & 1 : 0;  // head-parity buffer
+
+  if constexpr (Q8) {  // column sums of this head's dO (the V bias gradient, see above)
+    float cs[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int it = 0; it < NQP; ++it)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        cs[2 * e] += lo_bf(rd[it][e]);
+        cs[2 * e + 1] += hi_bf(rd[it][e]);
+      }
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {  // lanes of one 16-B column chunk: lane & 7 equal
+      cs[e] += __shfl_xor(cs[e], 8, 64);
+      cs[e] += __shfl_xor(cs[e], 16, 64);
+      cs[e] += __shfl_xor(cs[e], 32, 64);
+    }
+    if (lane < 8) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) vsum[hb][wave][lane * 8 + e] = cs[e];
+    }
+  }
 
   // ---------------------------------------------------------------- staging
   // |x|max on the packed bf16 bits (2 magnitudes per v_pk_max_u16), delta with v_dot2 on the
@@ -283,8 +343,16 @@ __global__ void __launch_bounds__(512) attn_bwd_f8_kernel(AttnBwdF8Params p) {
           const auto v1 = __builtin_amdgcn_permlane32_swap(wv[0][1], wv[1][1], false, false);
           const int d0 = 32 * dn + 8 * (j2 + hh);
           if (kok) {
-            *reinterpret_cast<u32x4*>(drow + p.H * D + d0) = u32x4{k0[0], k1[0], k0[1], k1[1]};
-            *reinterpret_cast<u32x4*>(drow + 2 * p.H * D + d0) = u32x4{v0[0], v1[0], v0[1], v1[1]};
+            const u32x4 kw = {k0[0], k1[0], k0[1], k1[1]}, vw = {v0[0], v1[0], v0[1], v1[1]};
+            if (!Q8 || p.wbf) {
+              *reinterpret_cast<u32x4*>(drow + p.H * D + d0) = kw;
+              *reinterpret_cast<u32x4*>(drow + 2 * p.H * D + d0) = vw;
+            }
+            if constexpr (Q8) {
+              uint8_t* crow = p.q8 + ((long)b * p.T + key) * p.ld + h * D;
+              q8_put(crow + p.H * D + d0, kw);
+              q8_put(crow + 2 * p.H * D + d0, vw);
+            }
           }
         }
     }
@@ -328,11 +396,52 @@ __global__ void __launch_bounds__(512) attn_bwd_f8_kernel(AttnBwdF8Params p) {
         }
         const auto r0 = __builtin_amdgcn_permlane32_swap(w[0][0], w[1][0], false, false);
         const auto r1 = __builtin_amdgcn_permlane32_swap(w[0][1], w[1][1], false, false);
-        if (qok) *reinterpret_cast<u32x4*>(drow + 32 * dn + 8 * (j2 + hh)) = u32x4{r0[0], r1[0], r0[1], r1[1]};
+        const u32x4 qw = {r0[0], r1[0], r0[1], r1[1]};
+        const int d0 = 32 * dn + 8 * (j2 + hh);
+        if (qok && (!Q8 || p.wbf)) *reinterpret_cast<u32x4*>(drow + d0) = qw;
+        if constexpr (Q8) {
+          if (qok) q8_put(p.q8 + ((long)b * p.T + q) * p.ld + h * D + d0, qw);
+          // column sums over the tile's 32 queries (lanes of one half; queries past T hold 0)
+          float cs[8];
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            cs[2 * e] = lo_bf(qw[e]);
+            cs[2 * e + 1] = hi_bf(qw[e]);
+          }
+#pragma unroll
+          for (int e = 0; e < 8; ++e) cs[e] = xor16_reduce(row16_sum(cs[e]), AddOp{});
+          if (col == 0) {
+#pragma unroll
+            for (int e = 0; e < 8; ++e) qsum[hb][qt][d0 + e] = cs[e];
+          }
+        }
       }
     }
   }
   __syncthreads();  // every LDS image, scale and row statistic is restaged for the next head
+  if constexpr (Q8) {  // this head's bias-gradient partials into image b's row: [q | k | v][h][d]
+    if (tid < D) {
+      float qs = 0.f, vs = 0.f;
+      for (int t = 0; t < nqt; ++t) qs += qsum[hb][t][tid];
+#pragma unroll
+      for (int w = 0; w < 8; ++w) vs += vsum[hb][w][tid];
+      float* cr = p.colpart + (long)b * p.ld + h * D + tid;
+      cr[0] = qs;
+      cr[p.H * D] = 0.f;
+      cr[2 * p.H * D] = vs;
+    }
+  }
+  }
+  if constexpr (Q8) {  // workgroup max |bf16 d(qkv)| -> q8_part[blockIdx.x]
+    q8max = warp_max(q8max);
+    if (lane == 0) red[wave][0] = q8max;
+    __syncthreads();
+    if (tid == 0) {
+      float m = red[0][0];
+#pragma unroll
+      for (int w = 1; w < 8; ++w) m = fmaxf(m, red[w][0]);
+      p.q8_part[blockIdx.x] = m;
+    }
   }
 }
 
@@ -340,17 +449,53 @@ __global__ void __launch_bounds__(512) attn_bwd_f8_kernel(AttnBwdF8Params p) {
 
 // fused fp8 backward for T <= 256, head dim 64 (d(qkv) bf16); -1 when not covered
 static int attn_bwd_f8(const void* qkv, const void* out, const void* dout, const float* lse, void* dqkv, int B,
-                       int T, int H, float scale, float* dbg, hipStream_t st);
+                       int T, int H, float scale, float* dbg, const AttnBwdF8Params* q8, hipStream_t st);
+
+PDT_API int pdt_fp8_meta_roll_partial(float* meta, const float* partial, int nblk, int fmt, float* dq_out,
+                                      hipStream_t st);
+PDT_API long pdt_reduce_rows_work(int nrows, int n);
+PDT_API int pdt_wgrad_reduce_rows(const float* rows, float* out, int nrows, int n, float scale, int accumulate,
+                                  float* work, hipStream_t st);
+
+// Workgroups of the backward launch: the length of the q8_part the caller passes to
+// pdt_attn_bwd_f8_q8.
+static int attn_bwd_grid(int nbh);
+PDT_API int pdt_attn_bwd_f8_grid(int B, int H) { return attn_bwd_grid(B * H); }
+
+// pdt_attn_bwd_f8 with the qkv projection's gradient epilogue (Q8 above): the e5m2 codes of
+// d(qkv) with the delayed scale q8_meta[0] -> q8 ([B*T][3*H*64]), the amax history rolled
+// from the workgroups' partial maxima (q8_part: pdt_attn_bwd_f8_grid floats) with the new
+// dequant factor -> q8_dq, and the bias gradient -> bias_out ([3*H*64] fp32, =) through the
+// per-image partial rows colpart ([B][3*H*64] + pdt_reduce_rows_work(B, 3*H*64) floats).
+// dqkv (bf16) is written only when it is not null.
+PDT_API int pdt_attn_bwd_f8_q8(const void* qkv, const void* out, const void* dout, const float* lse, void* dqkv,
+                               int B, int T, int H, float scale, void* q8, const float* q8_meta, float* q8_part,
+                               float* q8_dq, float* colpart, float* bias_out, hipStream_t st) {
+  if (!q8 || !q8_meta || !q8_part || !q8_dq || !colpart || !bias_out) return -1;
+  if (((uintptr_t)q8 & 7) != 0) return -5;  // 8-B code stores
+  AttnBwdF8Params e{};
+  e.q8 = (uint8_t*)q8;
+  e.q8_meta = q8_meta;
+  e.q8_part = q8_part;
+  e.colpart = colpart;
+  e.wbf = dqkv != nullptr;
+  int rc = attn_bwd_f8(qkv, out, dout, lse, dqkv, B, T, H, scale, nullptr, &e, st);
+  if (rc) return rc;
+  rc = pdt_fp8_meta_roll_partial(const_cast<float*>(q8_meta), q8_part, attn_bwd_grid(B * H), 1, q8_dq, st);
+  if (rc) return rc;
+  const int n = 3 * H * D;
+  return pdt_wgrad_reduce_rows(colpart, bias_out, B, n, 1.f, 0, colpart + (long)B * n, st);
+}
 
 PDT_API int pdt_attn_bwd_f8(const void* qkv, const void* out, const void* dout, const float* lse, void* dqkv,
                             int B, int T, int H, float scale, hipStream_t st) {
-  return attn_bwd_f8(qkv, out, dout, lse, dqkv, B, T, H, scale, nullptr, st);
+  return attn_bwd_f8(qkv, out, dout, lse, dqkv, B, T, H, scale, nullptr, nullptr, st);
 }
 
 // the same, also writing phase 1's fp32 dS to dbg ([B*H][R][R], R = 64 ceil(T / 64)) for tests
 PDT_API int pdt_attn_bwd_f8_debug(const void* qkv, const void* out, const void* dout, const float* lse, void* dqkv,
                                   int B, int T, int H, float scale, float* dbg, hipStream_t st) {
-  return attn_bwd_f8(qkv, out, dout, lse, dqkv, B, T, H, scale, dbg, st);
+  return attn_bwd_f8(qkv, out, dout, lse, dqkv, B, T, H, scale, dbg, nullptr, st);
 }
 
 // PDT_ATTN_BWD_PERSIST=0: one workgroup per head (the grid B*H, each running the head loop
@@ -366,9 +511,9 @@ static int attn_bwd_grid(int nbh) {
 }
 
 static int attn_bwd_f8(const void* qkv, const void* out, const void* dout, const float* lse, void* dqkv, int B,
-                       int T, int H, float scale, float* dbg, hipStream_t st) {
+                       int T, int H, float scale, float* dbg, const AttnBwdF8Params* q8, hipStream_t st) {
   if (T < 1 || T > 256) return -1;
-  AttnBwdF8Params p;
+  AttnBwdF8Params p = q8 ? *q8 : AttnBwdF8Params{};
   p.qkv = (const u16*)qkv;
   p.out = (const u16*)out;
   p.dout = (const u16*)dout;
@@ -383,8 +528,9 @@ static int attn_bwd_f8(const void* qkv, const void* out, const void* dout, const
   const int nqp = (T + 63) / 64;
   // one workgroup per CU (the LDS images hold 137 KB), each walking B*H / grid heads
   dim3 g(attn_bwd_grid(B * H));
-#define BWD(N)                                                                        \
-  if (dbg != nullptr) hipLaunchKernelGGL((attn_bwd_f8_kernel<N, true>), g, dim3(512), 0, st, p); \
+#define BWD(N)                                                                                  \
+  if (dbg != nullptr) hipLaunchKernelGGL((attn_bwd_f8_kernel<N, true>), g, dim3(512), 0, st, p);            \
+  else if (q8 != nullptr) hipLaunchKernelGGL((attn_bwd_f8_kernel<N, false, true>), g, dim3(512), 0, st, p); \
   else hipLaunchKernelGGL((attn_bwd_f8_kernel<N>), g, dim3(512), 0, st, p)
   switch (nqp) {
     case 1: BWD(1); break;

@@ -140,6 +140,8 @@ _SIGS = {
     "pdt_fp8_meta_seed": (c_int, [P, c_long, c_int, P, P]),
     "pdt_attn_bwd": (c_int, [P, P, P, P, P, P, c_int, c_int, c_int, c_float, P]),
     "pdt_attn_bwd_f8": (c_int, [P, P, P, P, P, c_int, c_int, c_int, c_float, P]),
+    "pdt_attn_bwd_f8_grid": (c_int, [c_int, c_int]),
+    "pdt_attn_bwd_f8_q8": (c_int, [P, P, P, P, P, c_int, c_int, c_int, c_float, P, P, P, P, P, P, P]),
     "pdt_attn_set_pv8": (c_int, [c_int]),
     "pdt_attn_bwd_f8_debug": (c_int, [P, P, P, P, P, c_int, c_int, c_int, c_float, P, P]),
     "pdt_lenet_grad_row": (c_int, [c_int]),
@@ -2336,6 +2338,12 @@ class _Linear(torch.autograd.Function):
     def backward(ctx, dy):
         x2, w, saved = ctx.saved_tensors
         shp, act, has_b = ctx.meta
+        only = getattr(dy, "_pdt_f8g_only", None)
+        if only is not None and (only is not ctx.fc or act is not None or not ctx.fp8_dgrad or not ctx.f8w):
+            # the producer (the fp8 attention backward) wrote the e5m2 codes and the bias
+            # gradient but not the bf16 values this configuration would read
+            raise RuntimeError("this output gradient carries fp8 codes only (PDT_ATTN_BWD_Q8); its layer needs "
+                               "the bf16 values: set PDT_ATTN_BWD_Q8_BF16=1 or PDT_ATTN_BWD_Q8=0")
         lib = _load()
         st = _s()
         Nout, K = w.shape
@@ -2686,6 +2694,12 @@ class _LinearF8(torch.autograd.Function):
     def backward(ctx, dy):
         x2, w, saved = ctx.saved_tensors
         shp, act, has_b = ctx.meta
+        only = getattr(dy, "_pdt_f8g_only", None)
+        if only is not None and (only is not ctx.fc or act is not None or not ctx.fp8_dgrad or not ctx.f8w):
+            # the producer (the fp8 attention backward) wrote the e5m2 codes and the bias
+            # gradient but not the bf16 values this configuration would read
+            raise RuntimeError("this output gradient carries fp8 codes only (PDT_ATTN_BWD_Q8); its layer needs "
+                               "the bf16 values: set PDT_ATTN_BWD_Q8_BF16=1 or PDT_ATTN_BWD_Q8=0")
         lib = _load()
         Nout, K = w.shape
         dy2 = dy.reshape(-1, Nout).to(torch.bfloat16).contiguous()
@@ -3163,6 +3177,21 @@ def softmax_cross_entropy(logits, target, label_smoothing=0.0):
 # =============================================================================
 # ViT ops (torch path for now on GPU as well; native kernels land in ops/vit_ops)
 # =============================================================================
+def _attn_bwd_q8_target(ctx):
+    """(owner, gmeta) when the fp8 attention backward should also write the qkv projection's
+    e5m2 gradient codes and bias gradient: delayed scaling with an amax history on the
+    projection (``grad_fp8_for`` = the fp8 layer whose output is this attention's only input)
+    whose backward is fp8 in both GEMMs. PDT_ATTN_BWD_Q8=0: the separate cast pass."""
+    owner = ctx.grad_owner
+    if owner is None or os.environ.get("PDT_ATTN_BWD_Q8", "1") != "1":
+        return None
+    cfg = fp8_settings()
+    gmeta = getattr(owner, "_pdt_fp8_gmeta", None)
+    if gmeta is None or cfg["scaling"] != "delayed" or not (cfg["dgrad"] and cfg["wgrad"]):
+        return None
+    return owner, gmeta
+
+
 class _QKVAttention(torch.autograd.Function):
     """Fused multi-head attention straight off the qkv projection output
     (csrc/attention.hip): qkv [B, T, 3*H*64] -> out [B, T, H*64] (the proj
@@ -3203,7 +3232,7 @@ class _QKVAttention(torch.autograd.Function):
         dqkv = torch.empty_like(qkv)
         owner = ctx.grad_owner
         gmeta = getattr(owner, "_pdt_fp8_gmeta", None) if owner is not None else None
-        if gmeta is not None and T <= 256 and fp8_settings()["scaling"] == "delayed":
+        if not ctx.fp8 and gmeta is not None and T <= 256 and fp8_settings()["scaling"] == "delayed":
             # also the e5m2 codes of d(qkv) for the qkv projection's fp8 gradient GEMMs
             codes = torch.empty((B * T, qkv.shape[2]), dtype=torch.uint8, device=qkv.device)
             part = torch.empty(2 * B * ctx.H + 1, dtype=torch.float32, device=qkv.device)
@@ -3215,6 +3244,31 @@ class _QKVAttention(torch.autograd.Function):
                 return dqkv, None, None, None, None, None
         if ctx.fp8 and T <= 256 and os.environ.get("PDT_FP8_ATTN_BWD", "1") == "1":
             # fused fp8 backward (csrc/attention_bwd_f8.hip): dQ, dK, dV in one kernel on e4m3 MFMA
+            q8 = _attn_bwd_q8_target(ctx)
+            if q8 is not None:
+                # ... that also writes the qkv projection's e5m2 output gradient (its delayed
+                # scale) and bias gradient; the bf16 d(qkv) is then never read (the projection's
+                # backward consumes the codes and the bias gradient: _LinearF8), so it is not
+                # written unless PDT_ATTN_BWD_Q8_BF16=1
+                owner, gmeta = q8
+                lib = _load()
+                n = qkv.shape[2]
+                codes = torch.empty((B * T, n), dtype=torch.uint8, device=qkv.device)
+                grid = lib.pdt_attn_bwd_f8_grid(B, ctx.H)
+                part = torch.empty(grid + 1, dtype=torch.float32, device=qkv.device)
+                dq = part[-1:]
+                colpart = torch.empty(B * n + lib.pdt_reduce_rows_work(B, n), dtype=torch.float32,
+                                      device=qkv.device)
+                db = _grad_buf(getattr(owner, "bias", None), (n,))
+                wbf = os.environ.get("PDT_ATTN_BWD_Q8_BF16", "0") == "1"
+                _chk(lib.pdt_attn_bwd_f8_q8(_p(qkv), _p(out), _p(dout), _p(lse), _p(dqkv) if wbf else None, B, T,
+                                            ctx.H, ctx.scale, _p(codes), _p(gmeta), _p(part), _p(dq), _p(colpart),
+                                            _p(db), _s()), "attn_bwd_f8_q8")
+                dqkv._pdt_f8g = (codes, dq, owner)
+                dqkv._pdt_db = (db, owner)
+                if not wbf:
+                    dqkv._pdt_f8g_only = owner  # (the values were not written: see _LinearF8)
+                return dqkv, None, None, None, None, None
             _chk(_load().pdt_attn_bwd_f8(_p(qkv), _p(out), _p(dout), _p(lse), _p(dqkv), B, T, ctx.H, ctx.scale,
                                          _s()), "attn_bwd_f8")
             return dqkv, None, None, None, None, None
@@ -3272,7 +3326,8 @@ def qkv_attention(qkv, num_heads, fp8=False, fp8_for=None, grad_fp8_for=None):
     # separate cast passes they replace (same-box A/B: 6.32k vs 6.40k img/s, runs r4e-r4h)
     q8 = os.environ.get("PDT_FP8_ATTN_Q8", "0")  # "fwd": only the forward's e4m3 output codes
     if q8 != "1":
-        grad_fp8_for = None
+        if not fp8:  # (the fp8 backward's epilogue writes the gradient codes: _attn_bwd_q8_target)
+            grad_fp8_for = None
         if q8 != "fwd":
             fp8_for = None
     if fp8 and fp8_for is not None and fp8_settings()["scaling"] == "delayed":

@@ -111,3 +111,67 @@ def test_attention_bwd_f8(B, T, H):
         # ~0.1 logit moves P by ~10 % at these x1.5 Gaussian inputs; the fp8 forward's own
         # output error is 6.5 %, tests/test_vit_fusion_gpu.py)
         assert e8 < 1.6e-1, (name, e8)
+
+
+@pytest.mark.parametrize("B,T,H", [(3, 197, 4), (40, 197, 12), (2, 64, 2), (1, 50, 12)])
+def test_attention_bwd_f8_q8_epilogue(B, T, H):
+    """pdt_attn_bwd_f8_q8: the qkv projection's e5m2 output-gradient codes, amax-history roll
+    and dequant factor equal the separate delayed cast of the kernel's own bf16 d(qkv) bit for
+    bit; the bf16 d(qkv) (when written) equals the plain kernel's; the bias gradient -- q part
+    reduced in-kernel, k part 0 and v part sum_q dO (identities of the attention backward) --
+    is at least as close to the exact fp32 bias gradient as the column sums of the written
+    fp8-path gradient are."""
+    torch.manual_seed(B * 7 + T)
+    lib = no._load()
+    n = 3 * H * 64
+    qkv = (torch.randn(B, T, n, device="cuda") * 1.5).to(torch.bfloat16)
+    dout = torch.randn(B, T, H * 64, device="cuda").to(torch.bfloat16)
+    out, lse = _bf16_forward(qkv, H)
+    d8 = torch.empty_like(qkv)
+    no._chk(lib.pdt_attn_bwd_f8(no._p(qkv), no._p(out), no._p(dout), no._p(lse), no._p(d8), B, T, H, 0.125,
+                                no._s()), "attn_bwd_f8")
+    # the delayed-scaling state of a projection that has seen a few gradients
+    _, _, meta = no.quantize_fp8_delayed((torch.randn(B * T, n, device="cuda") * 3e-3).to(torch.bfloat16), None,
+                                         no.E5M2)
+    meta_a, meta_b = meta.clone(), meta.clone()
+    # reference: the separate cast with column sums over the bf16 gradient
+    nb = lib.pdt_cast_cs_bands(B * T)
+    cpart = torch.empty(nb * n + lib.pdt_reduce_rows_work(nb, n), device="cuda")
+    q_ref = torch.empty(B * T, n, dtype=torch.uint8, device="cuda")
+    dq_ref = torch.empty(1, device="cuda")
+    db_ref = torch.empty(n, device="cuda")
+    no._chk(lib.pdt_cast_fp8_delayed_cs(no._p(d8), B * T, n, no._p(meta_a), no.E5M2, no._p(q_ref), no._p(dq_ref),
+                                        no._p(cpart), no._p(db_ref), no._s()), "cast_cs")
+    # fused
+    grid = lib.pdt_attn_bwd_f8_grid(B, H)
+    part = torch.empty(grid, device="cuda")
+    colpart = torch.empty(B * n + lib.pdt_reduce_rows_work(B, n), device="cuda")
+    codes = torch.empty(B * T, n, dtype=torch.uint8, device="cuda")
+    dq = torch.empty(1, device="cuda")
+    db = torch.full((n,), float("nan"), device="cuda")
+    d8b = torch.full_like(qkv, float("nan"))
+    no._chk(lib.pdt_attn_bwd_f8_q8(no._p(qkv), no._p(out), no._p(dout), no._p(lse), no._p(d8b), B, T, H, 0.125,
+                                   no._p(codes), no._p(meta_b), no._p(part), no._p(dq), no._p(colpart), no._p(db),
+                                   no._s()), "attn_bwd_f8_q8")
+    # without the bf16 output: the same codes
+    codes2 = torch.empty_like(codes)
+    meta_c = meta.clone()
+    no._chk(lib.pdt_attn_bwd_f8_q8(no._p(qkv), no._p(out), no._p(dout), no._p(lse), None, B, T, H, 0.125,
+                                   no._p(codes2), no._p(meta_c), no._p(part), no._p(dq), no._p(colpart), no._p(db),
+                                   no._s()), "attn_bwd_f8_q8 (codes only)")
+    torch.cuda.synchronize()
+    assert torch.equal(d8b, d8)
+    assert torch.equal(codes, q_ref) and torch.equal(codes2, q_ref)
+    assert torch.equal(dq, dq_ref)
+    assert torch.equal(meta_b, meta_a) and torch.equal(meta_c, meta_a)
+    # exact fp32 bias gradient of the same attention
+    qf = qkv.float().requires_grad_(True)
+    q, k, v = qf.view(B, T, 3, H, 64).permute(2, 0, 3, 1, 4)
+    o = torch.softmax((q @ k.transpose(-1, -2)) * 0.125, -1) @ v
+    o.transpose(1, 2).reshape(B, T, H * 64).backward(dout.float())
+    exact = qf.grad.sum((0, 1))
+    hd = H * 64
+    assert nrmerr(db[:hd], d8.float().sum((0, 1))[:hd]) < 1e-5  # q: the same sums, another order
+    assert db[hd:2 * hd].abs().max().item() == 0.0
+    assert nrmerr(db[2 * hd:], exact[2 * hd:]) < 1e-5
+    assert nrmerr(db, exact) <= nrmerr(db_ref, exact) + 1e-4, (nrmerr(db, exact), nrmerr(db_ref, exact))
