@@ -94,7 +94,14 @@ static __device__ __attribute__((aligned(64))) u32x4 wg8_zero_chunk[4];
 // counted vmcnt before the barrier retires only tile t's DMA (later tiles stay in
 // flight across it). A wave instruction writes 1 KB of LDS lane-linearly, so the chunk
 // swizzle moves to the source address (the XOR is an involution).
-template <int BM, int BN, int NSTAGE, int NTH, int WM, bool BIAS, int KS = 1, bool GL = false>
+//
+// SP (software-pipelined fragment reads): within a k-step the B fragments and the first A
+// fragment are read, then every A row block's MFMAs run while the NEXT row block's fragment
+// reads are in flight (two A fragment registers sets; scheduling barriers keep hipcc from
+// regrouping them). Without it hipcc reads a row block's fragment and waits for it right
+// before its 4 MFMAs, so the matrix pipe idles for an LDS round trip per 4 MFMAs (the
+// counter pass measured it busy 37 % of the kernel: profiles/vit_b16_fp8_pmc_round5_r6p.txt).
+template <int BM, int BN, int NSTAGE, int NTH, int WM, bool BIAS, int KS = 1, bool GL = false, bool SP = false>
 __global__ void __launch_bounds__(NTH, NTH == 256 && !GL && BM * BN < 65536 ? 2 : 1) wgrad_f8_kernel(WG8Params p) {
   constexpr int BK = BK1 * KS;
   constexpr int WN = NTH / 64 / WM;
@@ -188,6 +195,30 @@ __global__ void __launch_bounds__(NTH, NTH == 256 && !GL && BM * BN < 65536 ? 2 
 
   auto compute = [&](const char* sa) {
     const char* sb = sa + A_BYTES;
+    if constexpr (SP) {
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) {
+        i32x8 bfr[NI], af[2];
+#pragma unroll
+        for (int j = 0; j < NI; ++j) bfr[j] = frag8<RBB>(sb, wn * (BN / WN) + j * 16, lane, ks * BK1);
+        af[0] = frag8<RBA>(sa, wm * (BM / WM), lane, ks * BK1);
+#pragma unroll
+        for (int i = 0; i < MI; ++i) {
+          if (i + 1 < MI) af[(i + 1) & 1] = frag8<RBA>(sa, wm * (BM / WM) + (i + 1) * 16, lane, ks * BK1);
+          __builtin_amdgcn_sched_barrier(0);
+          // retire row block i's fragment (and, at i = 0, the B fragments); the next row
+          // block's 4 reads stay in flight across the MFMAs
+          if (i + 1 < MI) asm volatile("s_waitcnt lgkmcnt(4)" ::: "memory");
+          else asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+          for (int j = 0; j < NI; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(bfr[j], af[i & 1], acc[i][j], 0, 1, 0, 127,
+                                                                           0, 127);
+          __builtin_amdgcn_sched_barrier(0);
+        }
+      }
+      return;
+    }
 #pragma unroll
     for (int ks = 0; ks < KS; ++ks) {
       i32x8 bfr[NI];
@@ -307,14 +338,16 @@ __global__ void __launch_bounds__(NTH, NTH == 256 && !GL && BM * BN < 65536 ? 2 
 }
 
 struct WG8Var {
-  int BM, BN, NS, NTH, target, KS, GL;
+  int BM, BN, NS, NTH, target, KS, GL, SP;
 };
 // 4-wave tiles (2x2 waves, two workgroups per CU) and 8-wave tiles; target = workgroups,
 // KS = MFMA k-steps (128 token rows each) per k-tile / barrier
 // GL = LDS-DMA ring (NS stages, one workgroup per CU)
 // ids 21-24: 256x256 on FOUR waves (2x2 of 128x128, one wave per SIMD, accumulators in
 // AGPRs): a CU's fragment reads per k-step fall from 192 KB (8 waves of 128x64) to 128 KB
-constexpr int WG8_NVAR = 25;
+// ids 25-28: the software-pipelined fragment reads (SP) on the 256x256 8-wave tiles (1 / 2
+// register-staged stages, the 2-stage LDS-DMA ring) and the 128x128 2-stage tile
+constexpr int WG8_NVAR = 29;
 constexpr WG8Var WG8_VARS[WG8_NVAR] = {
     {128, 128, 2, 256, 1024, 1, 0}, {128, 128, 1, 256, 1024, 1, 0}, {128, 128, 2, 256, 512, 1, 0},
     {128, 128, 1, 256, 2048, 1, 0}, {256, 128, 2, 512, 512, 1, 0},  {128, 256, 2, 512, 512, 1, 0},
@@ -325,6 +358,8 @@ constexpr WG8Var WG8_VARS[WG8_NVAR] = {
     {128, 128, 2, 256, 1024, 1, 1}, {256, 256, 2, 512, 256, 1, 1},  {256, 256, 2, 512, 512, 1, 1},
     {256, 256, 2, 256, 512, 1, 0},  {256, 256, 2, 256, 256, 1, 0},  {256, 256, 2, 256, 256, 1, 1},
     {256, 256, 2, 256, 512, 1, 1},
+    {256, 256, 1, 512, 256, 1, 0, 1}, {256, 256, 2, 512, 256, 1, 0, 1}, {256, 256, 2, 512, 256, 1, 1, 1},
+    {128, 128, 2, 256, 1024, 1, 0, 1},
 };
 
 WG8Var wg8_variant(int v) { return (v < 0 || v >= WG8_NVAR) ? WG8_VARS[0] : WG8_VARS[v]; }
@@ -337,7 +372,14 @@ int launch8(const WG8Var& w, dim3 grid, const WG8Params& p_in, hipStream_t st) {
   if (p.zero == nullptr) return PDT_ERR_SYMBOL;
 #define L8(a, b, ns, t, wm) hipLaunchKernelGGL((wgrad_f8_kernel<a, b, ns, t, wm, BIAS>), grid, dim3(t), 0, st, p)
 #define G8(a, b, ns, t, wm) hipLaunchKernelGGL((wgrad_f8_kernel<a, b, ns, t, wm, BIAS, 1, true>), grid, dim3(t), 0, st, p)
-  if (w.GL) {
+#define S8(a, b, ns, t, wm, gl) \
+  hipLaunchKernelGGL((wgrad_f8_kernel<a, b, ns, t, wm, BIAS, 1, gl, true>), grid, dim3(t), 0, st, p)
+  if (w.SP) {
+    if (w.BM == 128) S8(128, 128, 2, 256, 2, false);
+    else if (w.GL) S8(256, 256, 2, 512, 2, true);
+    else if (w.NS == 2) S8(256, 256, 2, 512, 2, false);
+    else S8(256, 256, 1, 512, 2, false);
+  } else if (w.GL) {
     if (w.BM == 256 && w.BN == 256) {
       if (w.NTH == 256) G8(256, 256, 2, 256, 2);
       else G8(256, 256, 2, 512, 2);
@@ -370,6 +412,7 @@ int launch8(const WG8Var& w, dim3 grid, const WG8Params& p_in, hipStream_t st) {
   }
 #undef L8
 #undef G8
+#undef S8
   return 0;
 }
 
@@ -378,6 +421,14 @@ template <bool BIAS>
 const void* kernel8(const WG8Var& w) {
 #define K8(a, b, ns, t, wm) return reinterpret_cast<const void*>(&wgrad_f8_kernel<a, b, ns, t, wm, BIAS>)
 #define KG8(a, b, ns, t, wm) return reinterpret_cast<const void*>(&wgrad_f8_kernel<a, b, ns, t, wm, BIAS, 1, true>)
+#define KS8(a, b, ns, t, wm, gl) \
+  return reinterpret_cast<const void*>(&wgrad_f8_kernel<a, b, ns, t, wm, BIAS, 1, gl, true>)
+  if (w.SP) {
+    if (w.BM == 128) KS8(128, 128, 2, 256, 2, false);
+    if (w.GL) KS8(256, 256, 2, 512, 2, true);
+    if (w.NS == 2) KS8(256, 256, 2, 512, 2, false);
+    KS8(256, 256, 1, 512, 2, false);
+  }
   if (w.GL) {
     if (w.BM == 256 && w.BN == 256) {
       if (w.NTH == 256) KG8(256, 256, 2, 256, 2);
@@ -406,6 +457,7 @@ const void* kernel8(const WG8Var& w) {
   K8(128, 128, 1, 256, 2);
 #undef K8
 #undef KG8
+#undef KS8
 }
 
 // workgroups of variant v resident on the whole device at once (occupancy API, the smaller of
