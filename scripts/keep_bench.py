@@ -1,4 +1,4 @@
-"""Append the bench.py JSON records found in gpurun_out logs to profiles/bench_runs_round5.jsonl,
+"""Append the bench.py JSON records found in gpurun_out logs to profiles/bench_runs_round6.jsonl,
 tagged with the log name (the gpurun call tag) and a note.
 
     python scripts/keep_bench.py NOTE gpurun_out/r5a_bench_*.txt ...
@@ -7,7 +7,7 @@ import json
 import sys
 from pathlib import Path
 
-OUT = Path(__file__).resolve().parents[1] / "profiles" / "bench_runs_round5.jsonl"
+OUT = Path(__file__).resolve().parents[1] / "profiles" / "bench_runs_round6.jsonl"
 
 
 def main():

@@ -73,7 +73,11 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("dirs", nargs="+")
     ap.add_argument("--top", type=int, default=25)
+    ap.add_argument("--rate", default="", help="comma-separated SQ counters printed as %% of SIMD-cycles "
+                                                 "(counter / (1024 SIMDs x GRBM_GUI_ACTIVE / 8)), e.g. "
+                                                 "SQ_ACTIVE_INST_VALU,SQ_ACTIVE_INST_LDS")
     a = ap.parse_args()
+    rates = [r for r in a.rate.split(",") if r]
     fam = collections.defaultdict(collections.Counter)
     calls = collections.Counter()
     for d in a.dirs:
@@ -93,7 +97,7 @@ def main():
     tot_ns = sum(c.get("_ns", 0) for c in fam.values())
     print(f"step kernel time in the profiled pass: {tot_ns / 1e6:.2f} ms over {sum(calls.values())} dispatches")
     hdr = (f"{'kernel family':72s} {'calls':>5s} {'ms':>7s} {'GHz':>5s} {'MFMA%':>6s} {'TF/s':>6s} {'ldsconf':>7s} "
-           f"{'L2hit':>6s} {'fetchMB':>8s} {'writeMB':>8s}")
+           f"{'L2hit':>6s} {'fetchMB':>8s} {'writeMB':>8s}" + "".join(f" {r[-12:]:>12s}" for r in rates))
     print(hdr)
     for k in ranked[: a.top]:
         c = fam[k]
@@ -108,7 +112,8 @@ def main():
         h, m = c.get("TCC_HIT_sum", 0), c.get("TCC_MISS_sum", 0)
         hr = h / (h + m) if h + m else nan
         print(f"{k[:72]:72s} {calls[k]:5d} {ns / 1e6:7.3f} {ghz:5.2f} {mf:6.1f} {tf:6.0f} {lc:7.3f} {hr:6.3f} "
-              f"{c.get('FETCH_SIZE', 0) / 1024:8.1f} {c.get('WRITE_SIZE', 0) / 1024:8.1f}")
+              f"{c.get('FETCH_SIZE', 0) / 1024:8.1f} {c.get('WRITE_SIZE', 0) / 1024:8.1f}" +
+              "".join(f" {100 * c.get(r, 0) / (1024 * cyc) if cyc else nan:12.1f}" for r in rates))
     print("counters seen:", sorted({n for c in fam.values() for n in c}))
 
 
