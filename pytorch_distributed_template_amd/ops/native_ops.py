@@ -3232,7 +3232,9 @@ class _QKVAttention(torch.autograd.Function):
         dqkv = torch.empty_like(qkv)
         owner = ctx.grad_owner
         gmeta = getattr(owner, "_pdt_fp8_gmeta", None) if owner is not None else None
-        if not ctx.fp8 and gmeta is not None and T <= 256 and fp8_settings()["scaling"] == "delayed":
+        f8bwd = ctx.fp8 and T <= 256 and os.environ.get("PDT_FP8_ATTN_BWD", "1") == "1"
+        if not f8bwd and gmeta is not None and T <= 256 and fp8_settings()["scaling"] == "delayed" and \
+                os.environ.get("PDT_FP8_ATTN_Q8", "0") == "1":
             # also the e5m2 codes of d(qkv) for the qkv projection's fp8 gradient GEMMs
             codes = torch.empty((B * T, qkv.shape[2]), dtype=torch.uint8, device=qkv.device)
             part = torch.empty(2 * B * ctx.H + 1, dtype=torch.float32, device=qkv.device)
@@ -3242,7 +3244,7 @@ class _QKVAttention(torch.autograd.Function):
             if rc == 0:
                 dqkv._pdt_f8g = (codes, dq, owner)
                 return dqkv, None, None, None, None, None
-        if ctx.fp8 and T <= 256 and os.environ.get("PDT_FP8_ATTN_BWD", "1") == "1":
+        if f8bwd:
             # fused fp8 backward (csrc/attention_bwd_f8.hip): dQ, dK, dV in one kernel on e4m3 MFMA
             q8 = _attn_bwd_q8_target(ctx)
             if q8 is not None:
