@@ -57,8 +57,9 @@ for job in "$@"; do
       run ${TAG}_hiptrace.txt 400 rocprofv3 --hip-trace --kernel-trace --output-format csv -d $d -o run -- python3 bench.py --steps 3 --warmup 3 $args ;;
     pmc)
       ctrs=${rest%%:*}; bargs=""; [[ "$rest" == *:* ]] && bargs=${rest#*:}
-      d=gpurun_out/${TAG}_pmc_$(echo "$ctrs" | tr -c 'a-zA-Z0-9_\n' '_' | cut -c1-40)
-      run ${TAG}_pmc.txt 240 timeout -s KILL 200 rocprofv3 --pmc ${ctrs//,/ } --output-format csv -d $d -o run -- python3 bench.py --steps 2 --warmup 2 ${bargs//,/ } ;;
+      sfx=$(echo "$ctrs$bargs" | md5sum | cut -c1-8)  # (counters + bench args: one directory per pass)
+      d=gpurun_out/${TAG}_pmc_$sfx
+      run ${TAG}_pmc_$sfx.txt 240 timeout -s KILL 200 rocprofv3 --pmc ${ctrs//,/ } --output-format csv -d $d -o run -- python3 bench.py --steps 2 --warmup 2 ${bargs//,/ } ;;
     retune)  # fresh autotune of every kernel variant for a bench config -> gpurun_out/tune_NAME.json
       nm=${rest%%:*}; bargs=""; [[ "$rest" == *:* ]] && bargs=${rest#*:}
       PDT_AUTOTUNE_SHIPPED=0 PDT_AUTOTUNE_CACHE=$PWD/gpurun_out/tune_$nm.json run ${TAG}_retune_$nm.txt 600 python bench.py --steps 5 --warmup 3 ${bargs//,/ } ;;

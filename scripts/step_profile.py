@@ -1,5 +1,5 @@
-"""Per-step kernel breakdown from a rocprofv3 kernel-trace CSV: the last full
-training step is delimited by the optimizer kernel (adam_kernel / sgd_kernel).
+"""Per-step kernel breakdown from a rocprofv3 kernel-trace CSV: a full training step is
+delimited by the optimizer kernel (adam_kernel / sgd_kernel); --window picks which one.
 
 Usage: python scripts/step_profile.py <run_kernel_trace.csv> [--top 30]
 """
@@ -12,6 +12,9 @@ ap = argparse.ArgumentParser()
 ap.add_argument("csv")
 ap.add_argument("--top", type=int, default=30)
 ap.add_argument("--marker", default=r"(adam|sgd)_kernel")
+ap.add_argument("--window", type=int, default=2,
+                help="the step ending at the optimizer dispatch this many places from the end (bench.py's "
+                     "last window also holds the after-timing checksums)")
 a = ap.parse_args()
 
 rows = []
@@ -22,7 +25,8 @@ rows.sort()
 idx = [i for i, r in enumerate(rows) if re.search(a.marker, r[2])]
 if len(idx) < 2:
     raise SystemExit("need >= 2 optimizer steps in the trace")
-sel = rows[idx[-2] + 1: idx[-1] + 1]
+w = min(a.window, len(idx) - 1)
+sel = rows[idx[-w - 1] + 1: idx[-w] + 1]
 
 
 def short(n):
