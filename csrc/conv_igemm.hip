@@ -545,12 +545,13 @@ namespace {
 // per SIMD): per K-tile a CU's fragment reads fall from 192 KB (8 waves of 128x64) to 128 KB
 // -- the fp8 MFMA consumes twice the bytes per cycle of the bf16 one, so the LDS read
 // bandwidth, not the matrix core, bounds the 8-wave tile.
-// ids 12 / 13: the dense 256x256 ping-pong ring (csrc/gemm_ring.hip, tile groupings GM 4 / 8)
-// for the plain GEMMs (optional bias, no activation / aux / addend / fp8 side output)
-constexpr int NVAR_F8 = 14;
+// ids 12 / 13: the dense 256x256 ping-pong ring (csrc/gemm_ring.hip, tile groupings GM 4 / 8),
+// 14 / 15: the same ring persistent (one workgroup per CU walks the tiles, the next tile's first
+// K-tile loading under the current tile's epilogue); the fused epilogue on 12 and 14
+constexpr int NVAR_F8 = 16;
 constexpr int F8_RING0 = 12;
-constexpr int VAR_F8_BM[NVAR_F8] = {128, 128, 256, 128, 64, 128, 256, 128, 256, 128, 256, 256, 256, 256};
-constexpr int VAR_F8_BN[NVAR_F8] = {128, 128, 128, 256, 128, 64, 64, 128, 128, 256, 256, 256, 256, 256};
+constexpr int VAR_F8_BM[NVAR_F8] = {128, 128, 256, 128, 64, 128, 256, 128, 256, 128, 256, 256, 256, 256, 256, 256};
+constexpr int VAR_F8_BN[NVAR_F8] = {128, 128, 128, 256, 128, 64, 64, 128, 128, 256, 256, 256, 256, 256, 256, 256};
 
 template <int F8>
 int launch_f8(int v, const NTParams& p, hipStream_t st) {
@@ -581,6 +582,11 @@ PDT_API int pdt_gemm_ring_epi(const void* a, const void* b, void* c, const float
                               const float* dq_b, int M, int N, int K, int lda, int ldb, int ldc, int dt, int act,
                               void* aux, const void* addend, void* q8, const float* q8_meta, float* q8_part,
                               int q8_fmt, int q8_only, float* colsum, hipStream_t st);
+PDT_API int pdt_gemm_ring_epi_pers(const void* a, const void* b, void* c, const float* bias, const float* dq_a,
+                                   const float* dq_b, int M, int N, int K, int lda, int ldb, int ldc, int dt, int act,
+                                   void* aux, const void* addend, void* q8, const float* q8_meta, float* q8_part,
+                                   int q8_fmt, int q8_only, float* colsum, hipStream_t st);
+PDT_API int pdt_gemm_ring_grid(int M, int N, int sub);
 
 static int gemm_f8_impl(const void* a, const void* b, void* out, const float* bias, const float* dq_a,
                         const float* dq_b, int M, int N, int K, int lda, int ldb, int ldo, int fmt_a, int act,
@@ -591,16 +597,17 @@ static int gemm_f8_impl(const void* a, const void* b, void* out, const float* bi
   if (variant >= F8_RING0 && variant < NVAR_F8) {  // the dense ring (csrc/gemm_ring.hip)
     const int dt = fmt_a == 1 ? 2 : 1;
     int rc;
+    const int sub = variant - F8_RING0;
     if (act != 0 || aux != nullptr || addend != nullptr || q8 != nullptr || colsum != nullptr) {
-      if (variant != F8_RING0) return -5;  // the fused epilogue: grouping GM 4 only
-      rc = pdt_gemm_ring_epi(a, b, out, bias, dq_a, dq_b, M, N, K, lda, ldb, ldo, dt, act, aux, addend, q8, q8_meta,
-                             q8_part, q8_fmt, q8_only, colsum, stream);
+      if (sub != 0 && sub != 2) return -5;  // the fused epilogue: grouping GM 4 only
+      rc = (sub == 2 ? pdt_gemm_ring_epi_pers : pdt_gemm_ring_epi)(a, b, out, bias, dq_a, dq_b, M, N, K, lda, ldb, ldo,
+                                                                   dt, act, aux, addend, q8, q8_meta, q8_part, q8_fmt,
+                                                                   q8_only, colsum, stream);
     } else {
-      rc = pdt_gemm_ring(a, b, out, bias, dq_a, dq_b, M, N, K, lda, ldb, ldo, dt, variant - F8_RING0, stream);
+      rc = pdt_gemm_ring(a, b, out, bias, dq_a, dq_b, M, N, K, lda, ldb, ldo, dt, sub, stream);
     }
     if (rc || q8 == nullptr) return rc;
-    const int nblk = ((M + 255) / 256) * (N / 256);
-    return pdt_fp8_meta_roll_partial(q8_meta, q8_part, nblk, q8_fmt, q8_dq, stream);
+    return pdt_fp8_meta_roll_partial(q8_meta, q8_part, pdt_gemm_ring_grid(M, N, sub), q8_fmt, q8_dq, stream);
   }
   NTParams p;
   p.src = (const u16*)a;

@@ -91,7 +91,15 @@ __device__ __forceinline__ void ring_tile_of(uint32_t bid, int ntm, int ntn, int
 }
 
 // DT 0: bf16 x bf16; 1: e4m3 A x e4m3 B; 2: e5m2 A x e4m3 B (OCP fp8, unit block scales)
-template <int DT, bool BIAS, int GM, bool EPI>
+//
+// PERS (persistent): one workgroup per CU walks the tiles t = blockIdx.x, + gridDim.x, ... in the
+// one-tile launch's order (gridDim.x is a multiple of 8, so a workgroup's tiles keep its XCD).
+// Right after a tile's mainloop -- both LDS stages free, before the epilogue -- it issues the
+// LDS-DMA of the NEXT tile's first K-tile, so that load's HBM round trip runs under this tile's
+// epilogue (VALU, stores) instead of after a new workgroup's dispatch. Per-tile math and the
+// output bytes are those of the one-tile launch; the fp8 side output's max |out| is one
+// partial per workgroup (q8_part[blockIdx.x], the host rolls gridDim.x partials).
+template <int DT, bool BIAS, int GM, bool EPI, bool PERS = false>
 __global__ void __launch_bounds__(RNTH, 1) gemm_ring_kernel(RingParams p) {
   constexpr int WM = 2, WN = 4;
   constexpr int MI = RBM / WM / 16;  // 8 row blocks per wave
@@ -102,8 +110,12 @@ __global__ void __launch_bounds__(RNTH, 1) gemm_ring_kernel(RingParams p) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave / WN, wn = wave % WN;
   const int ntm = (p.M + RBM - 1) / RBM, ntn = p.N / RBN;
+  const int ntiles = ntm * ntn;
+  float q8all = 0.f;  // (EPI persistent: this workgroup's max |out| over all its tiles)
+  // one output tile (a lambda so the one-tile launch compiles to the straight-line kernel)
+  auto run_tile = [&](const int tile) __attribute__((always_inline)) {
   int tm, tn;
-  ring_tile_of<GM>(blockIdx.x, ntm, ntn, tm, tn);
+  ring_tile_of<GM>(PERS ? (uint32_t)tile : blockIdx.x, ntm, ntn, tm, tn);
   const int m0 = tm * RBM, n0 = tn * RBN;
   const int ca = tid & 7;
   const int nk = p.nk;
@@ -210,9 +222,13 @@ __global__ void __launch_bounds__(RNTH, 1) gemm_ring_kernel(RingParams p) {
     bar();
   };
   if (nk > 0) {
+    if (!PERS || tile == (int)blockIdx.x) {
 #pragma unroll
-    for (int q = 0; q < 4; ++q) issue(q, 0, 0);
-    asm volatile("s_waitcnt vmcnt(4)" ::: "memory");  // q0 q1 of K-tile 0
+      for (int q = 0; q < 4; ++q) issue(q, 0, 0);
+    }
+    // q0 q1 of K-tile 0 (a persistent walk issued them before the previous tile's epilogue:
+    // loads retire in order, so <= 4 outstanding -- stores included -- proves q0 and q1 landed)
+    asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
   }
   bar();
   if (wm == 1) bar();  // the stagger: group 1 runs one barrier behind group 0
@@ -255,6 +271,34 @@ __global__ void __launch_bounds__(RNTH, 1) gemm_ring_kernel(RingParams p) {
   for (int j = 0; j < NI; ++j)
 #pragma unroll
     for (int e = 0; e < 4; ++e) bv[j][e] = BIAS ? p.bias[n0 + wcol(j) + lcol + e] : 0.f;
+  if constexpr (PERS) {
+    // the next tile's K-tile 0 into stage 0 (every wave is past its last fragment read: the
+    // closing barrier above), in flight under this epilogue
+    const int nt = tile + (int)gridDim.x;
+    if (nt < ntiles && nk > 0) {
+      int tm2, tn2;
+      ring_tile_of<GM>((uint32_t)nt, ntm, ntn, tm2, tn2);
+      const char* An = p.A + (size_t)(tm2 * RBM) * p.lda;
+      const char* Bn = p.B + (size_t)(tn2 * RBN) * p.ldb;
+      const int mremn = p.M - tm2 * RBM;
+      auto na = [&](int i) __attribute__((always_inline)) {
+        const int r = (tid >> 3) + RS * i;
+        const void* g = r < mremn ? (const void*)(An + (size_t)r * p.lda + rswz(r, ca) * 16) : p.zero;
+        __builtin_amdgcn_global_load_lds(g, (__attribute__((address_space(3))) void*)(smem + (8 * wave + RS * i) * RKB),
+                                         16, 0, 0);
+      };
+      auto nb = [&](int j) __attribute__((always_inline)) {
+        const int r = (tid >> 3) + RS * j;
+        const char* g = Bn + (size_t)r * p.ldb + rswz(r, ca) * 16;
+        __builtin_amdgcn_global_load_lds(g, (__attribute__((address_space(3))) void*)(smem + RA_BYTES +
+                                                                                      (8 * wave + RS * j) * RKB),
+                                         16, 0, 0);
+      };
+      // quarter order q0 (A 0, 2), q1 (B 0, 1), q2 (B 2, 3), q3 (A 1, 3): the next tile's
+      // vmcnt(4) then covers q0 q1 exactly as the one-tile prologue's
+      na(0); na(2); nb(0); nb(1); nb(2); nb(3); na(1); na(3);
+    }
+  }
   const bool odd = (lane >> 4) & 1;
   // EPI: this lane's 8 columns of each column pair are fixed (colsum partials), its max |out|
   float csum[EPI ? 2 : 1][EPI ? 8 : 1];
@@ -390,7 +434,8 @@ __global__ void __launch_bounds__(RNTH, 1) gemm_ring_kernel(RingParams p) {
   }
   if constexpr (EPI) {
     // every LDS fragment read finished before the loop's last barrier: smem is free here
-    float* red = reinterpret_cast<float*>(smem);
+    // (a persistent walk prefetches into stage 0: the reductions use stage 1)
+    float* red = reinterpret_cast<float*>(smem + (PERS ? RSTAGE : 0));
     if (p.colsum != nullptr) {
       // lanes of one 16-lane row hold 16 rows of the same 8 columns: DPP row sums, then the
       // two wave rows (wm) with the same columns through LDS: [wm][wn][jp][g][8]
@@ -406,8 +451,12 @@ __global__ void __launch_bounds__(RNTH, 1) gemm_ring_kernel(RingParams p) {
       }
     }
     if (p.q8 != nullptr) {
-      q8max = warp_max(q8max);
-      if (lane == 0) red[2 * WN * 2 * 32 + wave] = q8max;
+      if constexpr (PERS) {
+        q8all = fmaxf(q8all, q8max);
+      } else {
+        q8max = warp_max(q8max);
+        if (lane == 0) red[2 * WN * 2 * 32 + wave] = q8max;
+      }
     }
     __syncthreads();
     if (p.colsum != nullptr && wm == 0 && lrow == 0) {
@@ -426,33 +475,72 @@ __global__ void __launch_bounds__(RNTH, 1) gemm_ring_kernel(RingParams p) {
         *reinterpret_cast<f32x4*>(dst + 4) = s1;
       }
     }
-    if (p.q8 != nullptr && tid == 0) {
+    if (p.q8 != nullptr && tid == 0 && !PERS) {
       float mx = 0.f;
 #pragma unroll
       for (int w = 0; w < RNTH / 64; ++w) mx = fmaxf(mx, red[2 * WN * 2 * 32 + w]);
       p.q8_part[blockIdx.x] = mx;
     }
   }
+  };
+  if constexpr (PERS) {
+    for (int tile = blockIdx.x; tile < ntiles; tile += gridDim.x) run_tile(tile);
+  } else {
+    run_tile(blockIdx.x);
+  }
+  if constexpr (EPI && PERS) {  // the workgroup's max |out| over its tiles -> q8_part[blockIdx.x]
+    if (p.q8 != nullptr) {
+      __syncthreads();  // (the last tile's reductions read stage 1)
+      float* red = reinterpret_cast<float*>(smem + RSTAGE);
+      const float w = warp_max(q8all);
+      if (lane == 0) red[wave] = w;
+      __syncthreads();
+      if (tid == 0) {
+        float mx = 0.f;
+#pragma unroll
+        for (int i = 0; i < RNTH / 64; ++i) mx = fmaxf(mx, red[i]);
+        p.q8_part[blockIdx.x] = mx;
+      }
+    }
+  }
 }
 
 static __device__ __attribute__((aligned(64))) u32x4 ring_zero_chunk[4];
 
-template <int DT, bool BIAS, int GM, bool EPI>
+// workgroups of a launch: one per tile, or (persistent sub-variants 2 / 3) one per CU -- a
+// multiple of 8 (whole XCD rounds) -- when there are more tiles than that
+int ring_grid(int M, int N, int sub) {
+  const int ntiles = ((M + RBM - 1) / RBM) * (N / RBN);
+  if (sub < 2) return ntiles;
+  const int g = pdt_num_cus() / 8 * 8;
+  return ntiles < g ? ntiles : g;
+}
+
+template <int DT, bool BIAS, int GM, bool EPI, bool PERS>
 int ring_launch(const RingParams& p, hipStream_t st) {
-  const int ntm = (p.M + RBM - 1) / RBM, ntn = p.N / RBN;
-  hipLaunchKernelGGL((gemm_ring_kernel<DT, BIAS, GM, EPI>), dim3(ntm * ntn), dim3(RNTH), 0, st, p);
+  hipLaunchKernelGGL((gemm_ring_kernel<DT, BIAS, GM, EPI, PERS>), dim3(ring_grid(p.M, p.N, PERS ? 2 : 0)),
+                     dim3(RNTH), 0, st, p);
   PDT_RETURN_LAUNCH();
 }
 
+// sub: 0 / 1 tile groupings GM 4 / 8, one tile per workgroup; 2 / 3 the same, persistent
 template <int DT>
 int ring_dispatch(int sub, bool bias, bool epi, const RingParams& p, hipStream_t st) {
   if constexpr (DT != 0) {
-    if (epi) return bias ? ring_launch<DT, true, 4, true>(p, st) : ring_launch<DT, false, 4, true>(p, st);
+    if (epi) {
+      if (sub == 0) return bias ? ring_launch<DT, true, 4, true, false>(p, st) : ring_launch<DT, false, 4, true, false>(p, st);
+      if (sub == 2) return bias ? ring_launch<DT, true, 4, true, true>(p, st) : ring_launch<DT, false, 4, true, true>(p, st);
+      return -5;  // (the fused epilogue: grouping GM 4 only)
+    }
   } else if (epi) {
     return -5;  // (the fused epilogue is built for the fp8 GEMMs only)
   }
-  if (sub == 0) return bias ? ring_launch<DT, true, 4, false>(p, st) : ring_launch<DT, false, 4, false>(p, st);
-  return bias ? ring_launch<DT, true, 8, false>(p, st) : ring_launch<DT, false, 8, false>(p, st);
+  switch (sub) {
+    case 0: return bias ? ring_launch<DT, true, 4, false, false>(p, st) : ring_launch<DT, false, 4, false, false>(p, st);
+    case 1: return bias ? ring_launch<DT, true, 8, false, false>(p, st) : ring_launch<DT, false, 8, false, false>(p, st);
+    case 2: return bias ? ring_launch<DT, true, 4, false, true>(p, st) : ring_launch<DT, false, 4, false, true>(p, st);
+    default: return bias ? ring_launch<DT, true, 8, false, true>(p, st) : ring_launch<DT, false, 8, false, true>(p, st);
+  }
 }
 
 int ring_run(const void* a, const void* b, void* c, const float* bias, const float* dq_a, const float* dq_b, int M,
@@ -501,7 +589,7 @@ int ring_run(const void* a, const void* b, void* c, const float* bias, const flo
   p.q8_only = q8_only;
   p.colsum = colsum;
   const bool epi = act != 0 || aux != nullptr || addend != nullptr || q8 != nullptr || colsum != nullptr;
-  if (sub < 0 || sub > 1) sub = 0;
+  if (sub < 0 || sub > 3) sub = 0;
   switch (dt) {
     case 0: return ring_dispatch<0>(sub, bias != nullptr, epi, p, st);
     case 1: return ring_dispatch<1>(sub, bias != nullptr, epi, p, st);
@@ -512,8 +600,11 @@ int ring_run(const void* a, const void* b, void* c, const float* bias, const flo
 
 }  // namespace
 
-// Number of ring sub-variants (tile-order groupings GM = 4, 8).
-PDT_API int pdt_gemm_ring_num_variants() { return 2; }
+// Number of ring sub-variants (tile-order groupings GM = 4, 8; one-tile / persistent).
+PDT_API int pdt_gemm_ring_num_variants() { return 4; }
+
+// Workgroups a launch of sub-variant `sub` runs (the fp8 side output's partial-max count).
+PDT_API int pdt_gemm_ring_grid(int M, int N, int sub) { return ring_grid(M, N, sub); }
 
 // Rows of the ring's M tile (the colsum partial rows).
 PDT_API int pdt_gemm_ring_bm() { return RBM; }
@@ -537,5 +628,16 @@ PDT_API int pdt_gemm_ring_epi(const void* a, const void* b, void* c, const float
                               int q8_fmt, int q8_only, float* colsum, hipStream_t st) {
   if (dt == 0) return -5;
   return ring_run(a, b, c, bias, dq_a, dq_b, M, N, K, lda, ldb, ldc, dt, 0, act, aux, addend, q8, q8_meta, q8_part,
+                  q8_fmt, q8_only, colsum, st);
+}
+
+// pdt_gemm_ring_epi on the persistent walk (sub-variant 2): q8_part receives
+// pdt_gemm_ring_grid(M, N, 2) partial maxima
+PDT_API int pdt_gemm_ring_epi_pers(const void* a, const void* b, void* c, const float* bias, const float* dq_a,
+                                   const float* dq_b, int M, int N, int K, int lda, int ldb, int ldc, int dt, int act,
+                                   void* aux, const void* addend, void* q8, const float* q8_meta, float* q8_part,
+                                   int q8_fmt, int q8_only, float* colsum, hipStream_t st) {
+  if (dt == 0) return -5;
+  return ring_run(a, b, c, bias, dq_a, dq_b, M, N, K, lda, ldb, ldc, dt, 2, act, aux, addend, q8, q8_meta, q8_part,
                   q8_fmt, q8_only, colsum, st);
 }

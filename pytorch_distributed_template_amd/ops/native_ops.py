@@ -1650,52 +1650,10 @@ def _take_bnb(u, grad):
     return st[3]
 
 
-# Weight gradients on a side HIP stream. Inside a block's backward the
-# data-gradient chain (dgrad GEMM -> BN reduce/finalize -> BN apply -> next
-# dgrad) is serial and full of small, latency-bound launches (BN finalize runs
-# on a handful of workgroups); the weight-gradient GEMMs depend only on dy and
-# the saved input, so they run beside that chain and fill the idle CUs. The
-# block joins the side stream before returning its gradients (DDP's bucket
-# hooks and the optimizer see finished tensors on the current stream).
-# Opt-in (PDT_WGRAD_STREAM=1): measured on one MI355X the kernels do overlap
-# (53.5 ms of kernel time in a 44.0 ms ResNet-50 bs512 step) but they then
-# contend for HBM bandwidth -- the BN element passes beside a wgrad GEMM run
-# 2.5x longer -- so the step is within noise of the single-stream order
-# (+0.4 % at bs512, -0.3 % at bs256; profiles/resnet50_native_bs512_step_r44_sidestream.txt).
-_SIDE_STREAMS: dict = {}
-
-
-def _wgrad_stream_enabled() -> bool:
-    return os.environ.get("PDT_WGRAD_STREAM", "0") == "1" and not torch.cuda.is_current_stream_capturing()
-
-
-class _SideWgrad:
-    def __init__(self):
-        self.on = _wgrad_stream_enabled()
-        self.used = False
-        if self.on:
-            dev = torch.cuda.current_device()
-            if dev not in _SIDE_STREAMS:
-                _SIDE_STREAMS[dev] = torch.cuda.Stream(device=dev)
-            self.side = _SIDE_STREAMS[dev]
-            self.main = torch.cuda.current_stream()
-
-    def dw(self, dy, u):
-        if not self.on:
-            return _unit_dw(dy, u)
-        self.side.wait_stream(self.main)  # dy (and everything before it) is ready
-        with torch.cuda.stream(self.side):
-            dw = _unit_dw(dy, u)
-        # the allocator must not recycle these while the side stream still reads / writes them
-        dy.record_stream(self.side)
-        u.x.record_stream(self.side)
-        dw.record_stream(self.main)
-        self.used = True
-        return dw
-
-    def join(self):
-        if self.used:
-            self.main.wait_stream(self.side)
+# (Weight gradients on a side HIP stream beside the data-gradient chain were an opt-in switch
+# through round 5: +0.4 % / -0.3 % at bs 512 / 256, and at bs 2048 on the round-6 tree 1 163 vs
+# 14 573 img/s -- the stream-recorded blocks of the 85-GiB step kept the caching allocator from
+# reusing memory (profiles/bench_runs_round6.jsonl, call q04). Removed: one stream.)
 
 
 class _Bottleneck(torch.autograd.Function):
@@ -1775,8 +1733,7 @@ class _Bottleneck(torch.autograd.Function):
             da2, pre2 = _unit_dx(dy3, u3, bnb_unit=u2)
         else:
             da2, pre2 = _unit_dx(dy3, u3), None
-        wg = _SideWgrad()
-        dw3 = wg.dw(dy3, u3)
+        dw3 = _unit_dw(dy3, u3)
         fused2 = None
         if fuse and _ax_enabled():
             # bn2's backward apply inside conv2's data gradient (stride-1 conv2; tuned per shape)
@@ -1795,7 +1752,7 @@ class _Bottleneck(torch.autograd.Function):
             da1, pre1 = _unit_dx(dy2, u2, bnb_unit=u1)
         else:
             da1, pre1 = _unit_dx(dy2, u2), None
-        dw2 = wg.dw(dy2, u2)
+        dw2 = _unit_dw(dy2, u2)
         prev = ctx.prev() if ctx.prev is not None else None
         fold1 = fuse and _ax_enabled() and need[0] and prev is not None and prev.mask is not None and \
             prev.Cout == u1.C and u1.Cs == u1.C and _conv1_fold_enabled()
@@ -1813,7 +1770,7 @@ class _Bottleneck(torch.autograd.Function):
             if not dual:
                 dyd, _, dgd, dbd = _bn_bwd(dout, ud, False, mask=u3.mask, pre=pre_d)
             addend = _unit_dx(dyd, ud) if need[0] else None
-            dwd = wg.dw(dyd, ud)
+            dwd = _unit_dw(dyd, ud)
             grads_ds = (dwd, dgd, dbd)
         else:
             addend, addend_mask = dout, u3.mask
@@ -1838,8 +1795,7 @@ class _Bottleneck(torch.autograd.Function):
             prev.bnb_pre = (dx.data_ptr(), dx._version, tuple(dx.shape), pre)
         elif need[0]:
             dx = _unit_dx(dy1, u1, addend=addend, addend_mask=addend_mask)
-        dw1 = wg.dw(dy1, u1)
-        wg.join()
+        dw1 = _unit_dw(dy1, u1)
         del ctx.units
         return (dx, None, None, None, None, None, dw1, dg1, db1, dw2, dg2, db2, dw3, dg3, db3) + grads_ds
 

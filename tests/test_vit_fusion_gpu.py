@@ -683,6 +683,50 @@ def test_ring_fused_epilogues(act, qfmt, cs):
         assert nrmerr(csum, out.float().sum(0)) < 1e-3, nrmerr(csum, out.float().sum(0))
 
 
+@pytest.mark.parametrize("act,qfmt,cs,K", [(None, 0, False, 384), (None, 1, False, 256), (4, 0, False, 384),
+                                           (5, 1, True, 256), (0, 0, False, 256)])
+def test_ring_persistent_matches_one_tile(act, qfmt, cs, K):
+    """The persistent ring walk (fp8 variants 14 / 15: one workgroup per CU walks the tiles, the
+    next tile's first K-tile prefetched under the current tile's epilogue) writes exactly the
+    bytes of the one-tile launch (12 / 13): the plain GEMM (with / without bias, e4m3 / e5m2 A),
+    and with the fused epilogues the bf16 output, gelu' side output, fp8 codes, dequant factor,
+    amax history and column sums. 260 tiles (more than one per workgroup), a partial last tile
+    row, an odd and an even K-tile count."""
+    torch.manual_seed(80 + K)
+    M, N = 16500, 1024
+    fmt_a = no.E5M2 if (act in (3, 5) or (act is None and qfmt == 1)) else no.E4M3
+    a8, dqa = no.quantize_fp8(torch.randn(M, K, device="cuda").to(torch.bfloat16), fmt_a)
+    b8, dqb = no.quantize_fp8(torch.randn(N, K, device="cuda").to(torch.bfloat16) * 0.1, no.E4M3)
+    if act is None:
+        bias = torch.randn(N, device="cuda") if qfmt == 0 else None
+        outs = {}
+        for v in (12, 13, 14, 15):
+            o = torch.full((M, N), float("nan"), device="cuda").to(torch.bfloat16)
+            no.gemm_f8(a8, b8, o, dqa, dqb, fmt_a=fmt_a, bias=bias, variant=v)
+            outs[v] = o
+        torch.cuda.synchronize()
+        assert torch.equal(outs[14], outs[12]) and torch.equal(outs[15], outs[13])
+        assert torch.isfinite(outs[12].float()).all()
+        return
+    z = torch.randn(M, N, device="cuda").to(torch.bfloat16)
+    bias = torch.randn(N, device="cuda") if act in (0, 4) else None
+    kw = dict(fmt_a=fmt_a, bias=bias, act=act, addend=z if act != 4 else None)
+    _, _, meta0 = no.quantize_fp8_delayed(torch.randn(M, N, device="cuda").to(torch.bfloat16), None, qfmt)
+    res = {}
+    for v in (12, 14):
+        out = torch.full((M, N), float("nan"), device="cuda").to(torch.bfloat16)
+        aux = torch.full_like(out, float("nan")) if act == 4 else None
+        codes = torch.empty(M, N, dtype=torch.uint8, device="cuda")
+        meta = meta0.clone()
+        csum = torch.empty(N, dtype=torch.float32, device="cuda") if cs else None
+        dq = no.gemm_f8(a8, b8, out, dqa, dqb, variant=v, aux=aux, q8=(codes, meta, qfmt, False), colsum_out=csum,
+                        **kw)
+        res[v] = [out, codes, dq, meta] + ([aux] if aux is not None else []) + ([csum] if cs else [])
+    torch.cuda.synchronize()
+    for x, y in zip(res[14], res[12]):
+        assert torch.equal(x, y)
+
+
 @pytest.mark.parametrize("T", [197, 50, 256, 7])
 def test_cls_attention_kernel_matches_fp32(T):
     """csrc/attention_cls.hip: token 0's attention output and the full dqkv against an fp32
