@@ -114,6 +114,12 @@ __global__ void __launch_bounds__(RNTH, 1) gemm_ring_kernel(RingParams p) {
   float q8all = 0.f;  // (EPI persistent: this workgroup's max |out| over all its tiles)
   // one output tile (a lambda so the one-tile launch compiles to the straight-line kernel)
   auto run_tile = [&](const int tile) __attribute__((always_inline)) {
+  // (persistent: the lane-dependent values are re-derived per tile from an opaque copy of the
+  // thread id -- hoisted out of the tile loop they stayed live across the mainloop and spilled)
+  int tid = (int)threadIdx.x;
+  if constexpr (PERS) asm volatile("" : "+v"(tid));
+  const int lane = tid & 63, wave = tid >> 6;
+  const int wm = wave / WN, wn = wave % WN;
   int tm, tn;
   ring_tile_of<GM>(PERS ? (uint32_t)tile : blockIdx.x, ntm, ntn, tm, tn);
   const int m0 = tm * RBM, n0 = tn * RBN;
