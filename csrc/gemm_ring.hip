@@ -114,10 +114,12 @@ __global__ void __launch_bounds__(RNTH, 1) gemm_ring_kernel(RingParams p) {
   float q8all = 0.f;  // (EPI persistent: this workgroup's max |out| over all its tiles)
   // one output tile (a lambda so the one-tile launch compiles to the straight-line kernel)
   auto run_tile = [&](const int tile) __attribute__((always_inline)) {
-  // (persistent: the lane-dependent values are re-derived per tile from an opaque copy of the
-  // thread id -- hoisted out of the tile loop they stayed live across the mainloop and spilled)
+  // (persistent fused epilogue: the lane-dependent values are re-derived per tile from an
+  // opaque copy of the thread id -- hoisted out of the tile loop they stayed live across the
+  // mainloop and spilled 120-192 B; the plain persistent walk keeps them hoisted, 245 VGPRs, no
+  // scratch, and measured faster so on the long-K shapes: profiles/ring_persistent_ab_round6.txt)
   int tid = (int)threadIdx.x;
-  if constexpr (PERS) asm volatile("" : "+v"(tid));
+  if constexpr (PERS && EPI) asm volatile("" : "+v"(tid));
   const int lane = tid & 63, wave = tid >> 6;
   const int wm = wave / WN, wn = wave % WN;
   int tm, tn;
