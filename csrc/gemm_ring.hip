@@ -329,9 +329,10 @@ __global__ void __launch_bounds__(RNTH, 1) gemm_ring_kernel(RingParams p) {
   // (x gelu' addend, e5m2 codes) -- and with run-time fields every element group branched on
   // act, q8 and the format (~450 branches and ~320 exec moves per tile); anything else takes the
   // run-time path.
-  auto run = [&](auto act_c, auto q8_c) __attribute__((always_inline)) {
+  auto run = [&](auto act_c, auto q8_c, auto cs_c) __attribute__((always_inline)) {
     constexpr int CA = decltype(act_c)::value;  // -1: p.act at run time
     constexpr int CQ = decltype(q8_c)::value;   // -1: p.q8 / p.q8_fmt at run time; 1 e4m3, 2 e5m2
+    constexpr int CC = decltype(cs_c)::value;   // column sums: -1 run time (summed, used if p.colsum), 0 no, 1 yes
     const int act = CA >= 0 ? CA : p.act;
     const bool q8on = CQ > 0 ? true : (EPI && p.q8 != nullptr);
     const int fmt = CQ > 0 ? CQ - 1 : p.q8_fmt;
@@ -394,12 +395,11 @@ __global__ void __launch_bounds__(RNTH, 1) gemm_ring_kernel(RingParams p) {
             if (act == 4) {
               u32x4 gd;
 #pragma unroll
-              for (int e = 0; e < 4; ++e) {
-                float g0, g1, d0, d1;
-                pdt_gelu_dual(lo_bf(v[e]), g0, d0);
-                pdt_gelu_dual(hi_bf(v[e]), g1, d1);
-                v[e] = pack2bf(g0, g1);
-                gd[e] = pack2bf(d0, d1);
+              for (int e = 0; e < 4; ++e) {  // (the pair on the packed VALU)
+                pdt_f32x2 g, d;
+                pdt_gelu_dual2(pdt_f32x2{lo_bf(v[e]), hi_bf(v[e])}, g, d);
+                v[e] = pack2bf(g.x, g.y);
+                gd[e] = pack2bf(d.x, d.y);
               }
               *reinterpret_cast<u32x4*>(p.aux + e0) = gd;
             }
@@ -409,8 +409,10 @@ __global__ void __launch_bounds__(RNTH, 1) gemm_ring_kernel(RingParams p) {
               f[2 * e] = lo_bf(v[e]);
               f[2 * e + 1] = hi_bf(v[e]);
             }
+            if constexpr (CC != 0) {
 #pragma unroll
-            for (int e = 0; e < 8; ++e) csum[j >> 1][e] += f[e];
+              for (int e = 0; e < 8; ++e) csum[j >> 1][e] += f[e];
+            }
             if (q8on) {
 #pragma unroll
               for (int e = 0; e < 8; ++e) q8max = fmaxf(q8max, fabsf(f[e]));
@@ -431,14 +433,15 @@ __global__ void __launch_bounds__(RNTH, 1) gemm_ring_kernel(RingParams p) {
     }
   };
   if constexpr (EPI) {
-    if (p.act == 4 && p.q8 != nullptr && p.q8_fmt == 0 && !has_add)
-      run(std::integral_constant<int, 4>{}, std::integral_constant<int, 1>{});
-    else if (p.act == 5 && p.q8 != nullptr && p.q8_fmt == 1 && has_add)
-      run(std::integral_constant<int, 5>{}, std::integral_constant<int, 2>{});
+    // fc1 forward (no column sums) and fc2's data gradient (with them: fc1's bias gradient)
+    if (p.act == 4 && p.q8 != nullptr && p.q8_fmt == 0 && !has_add && p.colsum == nullptr)
+      run(std::integral_constant<int, 4>{}, std::integral_constant<int, 1>{}, std::integral_constant<int, 0>{});
+    else if (p.act == 5 && p.q8 != nullptr && p.q8_fmt == 1 && has_add && p.colsum != nullptr)
+      run(std::integral_constant<int, 5>{}, std::integral_constant<int, 2>{}, std::integral_constant<int, 1>{});
     else
-      run(std::integral_constant<int, -1>{}, std::integral_constant<int, -1>{});
+      run(std::integral_constant<int, -1>{}, std::integral_constant<int, -1>{}, std::integral_constant<int, -1>{});
   } else {
-    run(std::integral_constant<int, -1>{}, std::integral_constant<int, -1>{});
+    run(std::integral_constant<int, -1>{}, std::integral_constant<int, -1>{}, std::integral_constant<int, -1>{});
   }
   if constexpr (EPI) {
     // every LDS fragment read finished before the loop's last barrier: smem is free here

@@ -37,6 +37,25 @@ __device__ __forceinline__ void pdt_gelu_dual(float z, float& g, float& d) {
   d = fmaf(g * (1.f - h), fmaf(C3, z2, C1), h);  // h + 0.5 z (1 - t^2) 2du, t = 2h - 1
 }
 
+// pdt_gelu_dual of two values on the packed fp32 VALU (v_pk_mul / v_pk_fma / v_pk_add: one
+// instruction per pair; exp2 / rcp stay scalar) -- the same operations in the same order, so
+// the results are those of two pdt_gelu_dual calls
+typedef float pdt_f32x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ void pdt_gelu_dual2(pdt_f32x2 z, pdt_f32x2& g, pdt_f32x2& d) {
+  constexpr float K1 = -2.f * 0.7978845608f * 1.4426950409f;
+  constexpr float K3 = K1 * 0.044715f;
+  constexpr float C1 = 2.f * 0.7978845608f;
+  constexpr float C3 = C1 * 3.f * 0.044715f;
+  const pdt_f32x2 z2 = z * z;
+  const pdt_f32x2 a = z * __builtin_elementwise_fma(pdt_f32x2{K3, K3}, z2, pdt_f32x2{K1, K1});
+  pdt_f32x2 h;
+  h.x = __builtin_amdgcn_rcpf(1.f + __builtin_amdgcn_exp2f(a.x));
+  h.y = __builtin_amdgcn_rcpf(1.f + __builtin_amdgcn_exp2f(a.y));
+  g = z * h;
+  d = __builtin_elementwise_fma(g * (pdt_f32x2{1.f, 1.f} - h),
+                                __builtin_elementwise_fma(pdt_f32x2{C3, C3}, z2, pdt_f32x2{C1, C1}), h);
+}
+
 // four floats already within +-448 -> four packed e4m3fn codes, no clamp (8 VALU ops fewer
 // than pdt_cvt4_f8<0>): values scaled by a power of two from their own |max| (attention's
 // per-head / per-tile scales) or bounded by construction (256 P, P <= 1)
