@@ -7,7 +7,7 @@ variant and of every applicable variant, and a streaming reference from the same
 (``torch.add(y, addend, out=o)``: 2 reads + 1 write of the output size). Prints one line per
 (shape, variant) with GB/s and the fraction of the streaming reference.
 
-    python scripts/bnb_roofline.py [--batch 2048] [--variants 2,7,12,17,22,27,38-41]
+    python scripts/bnb_roofline.py [--batch 2048] [--variants 2,7,12,17,22,27,38-41] [--shapes 14:256:1024]
 """
 import argparse
 import os
@@ -53,11 +53,16 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--batch", type=int, default=2048)
     ap.add_argument("--variants", default="2,7,12,17,22,27,38-41")
+    ap.add_argument("--shapes", default="", help="H:K:N[,H:K:N...] subset of SHAPES (e.g. for a counter pass)")
+    ap.add_argument("--no-ref", action="store_true", help="skip the streaming reference (counter passes)")
     a = ap.parse_args()
     lib = no._load()
     table = no._tuned()
     torch.manual_seed(0)
+    keep = {tuple(int(x) for x in t.split(":")) for t in a.shapes.split(",") if t}
     for H, K, N, boundary in SHAPES:
+        if keep and (H, K, N) not in keep:
+            continue
         M = a.batch * H * H
         dy = (torch.randn(M, K, device="cuda") * 0.1).to(torch.bfloat16)
         wt = (torch.randn(N, K, device="cuda") * 0.05).to(torch.bfloat16)
@@ -84,7 +89,7 @@ def main():
 
         o2 = torch.empty_like(out)
         ref_b = 3 * M * N * 2
-        t_ref = timeit(lambda: torch.add(y, out if addend is None else addend, out=o2))
+        t_ref = 1.0 if a.no_ref else timeit(lambda: torch.add(y, out if addend is None else addend, out=o2))
         ref_bw = ref_b / t_ref
         print(f"H{H} K{K} N{N} {'boundary' if boundary else 'inner'}: M={M} bytes={nbytes / 1e9:.2f} GB  "
               f"stream ref {ref_bw / 1e12:.2f} TB/s  tuned v{tuned}", flush=True)

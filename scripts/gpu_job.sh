@@ -17,6 +17,7 @@
 #                    per-step summary via scripts/step_profile.py
 #   hiptrace[:ARGS]  rocprofv3 HIP-API + kernel trace (host-sync hunting)
 #   pmc:CTRS:ARGS    one counter pass (CTRS: commas -> spaces) over bench.py ARGS
+#   pmcpy:CTRS:SCRIPT[:ARGS]  one counter pass over python3 SCRIPT ARGS
 #   py:SCRIPT[:ARGS] python SCRIPT ARGS
 #   pyenv:K=V+K2=V2:SCRIPT[:ARGS]  the same with extra environment variables
 #   retunewith:NAME:IDS[:ARGS]  targeted re-tune of the shipped conv_nt keys against ids IDS
@@ -60,6 +61,11 @@ for job in "$@"; do
       sfx=$(echo "$ctrs$bargs" | md5sum | cut -c1-8)  # (counters + bench args: one directory per pass)
       d=gpurun_out/${TAG}_pmc_$sfx
       run ${TAG}_pmc_$sfx.txt 240 timeout -s KILL 200 rocprofv3 --pmc ${ctrs//,/ } --output-format csv -d $d -o run -- python3 bench.py --steps 2 --warmup 2 ${bargs//,/ } ;;
+    pmcpy)  # pmcpy:CTRS:SCRIPT[:ARGS] -- one counter pass over a python script
+      ctrs=${rest%%:*}; r2=${rest#*:}; scr=${r2%%:*}; sargs=""; [[ "$r2" == *:* ]] && sargs=${r2#*:}
+      sfx=$(echo "$ctrs$scr$sargs" | md5sum | cut -c1-8)
+      d=gpurun_out/${TAG}_pmc_$sfx
+      run ${TAG}_pmc_$sfx.txt 240 timeout -s KILL 200 rocprofv3 --pmc ${ctrs//,/ } --output-format csv -d $d -o run -- python3 -u $scr ${sargs//,/ } ;;
     retune)  # fresh autotune of every kernel variant for a bench config -> gpurun_out/tune_NAME.json
       nm=${rest%%:*}; bargs=""; [[ "$rest" == *:* ]] && bargs=${rest#*:}
       PDT_AUTOTUNE_SHIPPED=0 PDT_AUTOTUNE_CACHE=$PWD/gpurun_out/tune_$nm.json run ${TAG}_retune_$nm.txt 600 python bench.py --steps 5 --warmup 3 ${bargs//,/ } ;;
