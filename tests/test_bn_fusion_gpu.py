@@ -235,12 +235,17 @@ def test_stem_bn_backward_gathers_pool_gradient(monkeypatch):
         assert torch.isfinite(a).all() and e < 1e-2, (a.shape, e)
 
 
-@pytest.mark.parametrize("ncol,use_mask,use_add", [(128, False, True), (512, True, False)])
-def test_bnb_epilogue_every_variant(ncol, use_mask, use_add):
+@pytest.mark.parametrize("ncol,use_mask,use_add,use_amask,two", [
+    (128, False, True, True, False), (512, True, False, False, False),  # run-time flags (generic walk)
+    (256, False, False, False, False),                 # a block's inner unit: ReLU gate from y
+    (256, True, True, True, False), (384, True, True, False, False),  # block input: addend, ReLU bits
+    (256, True, True, True, True), (384, True, True, False, True)])   # + a second unit's partials
+def test_bnb_epilogue_every_variant(ncol, use_mask, use_add, use_amask, two):
     """Every conv_nt tile variant (and stream variant) with the fused BN-backward
     epilogue, on a 1x1 data-gradient geometry: the output (+ ReLU-masked addend)
     and the partial sums (sum of the gated gradient g, sum of g * (y - mean)) vs
-    an fp32 reference."""
+    an fp32 reference. The configurations cover the epilogue's compiled walks
+    (csrc/conv_nt_tile.inc) and its run-time-flag one."""
     torch.manual_seed(21)
     dev = "cuda"
     N, H, K = 4, 28, 256
@@ -253,25 +258,32 @@ def test_bnb_epilogue_every_variant(ncol, use_mask, use_add):
     scale = torch.rand(ncol, device=dev) + 0.5
     shift = torch.randn(ncol, device=dev) * 0.2
     add = torch.randn(M, ncol, device=dev).to(torch.bfloat16) if use_add else None
-    amask = torch.randint(0, 256, (M * ncol // 8,), dtype=torch.uint8, device=dev) if use_add else None
+    amask = torch.randint(0, 256, (M * ncol // 8,), dtype=torch.uint8, device=dev) if use_amask else None
     mask = torch.randint(0, 256, (M * ncol // 8,), dtype=torch.uint8, device=dev) if use_mask else None
+
+    y2 = torch.randn(M, ncol, device=dev).to(torch.bfloat16) if two else None
+    mean2 = torch.randn(ncol, device=dev) * 0.1 if two else None
 
     def bits(m):
         return ((m.view(-1, 1).int() >> torch.arange(8, device=dev)) & 1).view(M, ncol).float()
 
     ref = dy.float() @ wt.float().t()
     if use_add:
-        ref = ref + add.float() * bits(amask)
+        ref = ref + add.float() * (bits(amask) if use_amask else 1.0)
     gate = bits(mask) if use_mask else ((y.float() * scale + shift) > 0).float()
     ran = 0
     for v in range(lib.pdt_conv_nt_num_variants()):
         R = lib.pdt_conv_nt_bnb_rows(M, ncol, K, v)
         part = torch.full((2 * max(R, 1) * ncol,), float("nan"), device=dev)
+        part2 = torch.full_like(part, float("nan")) if two else None
         out = torch.empty(M, ncol, device=dev, dtype=torch.bfloat16)
-        rc = lib.pdt_conv_nt_bnb(no._p(dy), no._p(wt), no._p(out), no._p(add), no._p(amask),
-                                 H, H, K, N, H, H, ncol, K, K, 1, 1, 0, 0, 1, 1, 1, 1,
-                                 H, H, 1, 1, 0, 0, ncol, v, no._p(y), no._p(mean), no._p(scale), no._p(shift),
-                                 no._p(mask), no._p(part), 1, 0, R, no._s())
+        args = (no._p(dy), no._p(wt), no._p(out), no._p(add), no._p(amask), H, H, K, N, H, H, ncol, K, K, 1, 1, 0,
+                0, 1, 1, 1, 1, H, H, 1, 1, 0, 0, ncol, v, no._p(y), no._p(mean), no._p(scale), no._p(shift),
+                no._p(mask), no._p(part), 1, 0, R)
+        if two:
+            rc = lib.pdt_conv_nt_bnb2(*args, no._p(y2), no._p(mean2), no._p(part2), no._s())
+        else:
+            rc = lib.pdt_conv_nt_bnb(*args, no._s())
         if rc == no.NOT_APPLICABLE:
             continue
         assert rc == 0, (v, rc)
@@ -281,4 +293,8 @@ def test_bnb_epilogue_every_variant(ncol, use_mask, use_add):
         ps = part.view(2, R, ncol).sum(1)
         assert nrmerr(ps[0], g.sum(0)) < 1e-3, v
         assert nrmerr(ps[1], (g * (y.float() - mean)).sum(0)) < 1e-3, v
-    assert ran >= 30
+        if two:
+            ps2 = part2.view(2, R, ncol).sum(1)
+            assert torch.equal(ps2[0], ps[0]), v
+            assert nrmerr(ps2[1], (g * (y2.float() - mean2)).sum(0)) < 1e-3, v
+    assert ran >= (20 if two else 30)
