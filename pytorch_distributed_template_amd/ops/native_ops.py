@@ -561,9 +561,12 @@ _RETUNED: set = set()
 def _retune_candidates(key, table):
     """PDT_RETUNE_WITH="45-48": a targeted re-tune of the table -- every conv_nt key already in
     it is timed once more against these new variant ids only (its current choice included),
-    and switches when one of them is faster. Returns the allowed id set, or None (no re-tune)."""
+    and switches when one of them is faster (PDT_RETUNE_PREFIX: only the keys of one family).
+    Returns the allowed id set, or None (no re-tune)."""
     spec = os.environ.get("PDT_RETUNE_WITH")
     if not spec or key in _RETUNED or key not in table or not _tune_allowed():
+        return None
+    if not key.startswith(os.environ.get("PDT_RETUNE_PREFIX", "")):  # e.g. "ntb2:" (one key family)
         return None
     _RETUNED.add(key)
     return _id_set(spec) | {int(table[key])}
