@@ -406,8 +406,13 @@ static int conv_nt_impl(const void* src, const void* b, void* out, float* stats,
     }
     return launch_variant_ax(v, p, stream);
   }
-  // ring tiles: no second-unit partials
-  if (bnb.part2 != nullptr && ((v >= 34 && v < NVAR) || v >= PERS0)) return -5;
+  // ring tiles: only the BN-backward walks they compile (conv_nt_tile.inc) -- a block's inner unit
+  // (ReLU recomputed from y) or a block input (addend + ReLU bit mask); no second-unit partials
+  if (bnb.part != nullptr && ((v >= 34 && v < NVAR) || v >= PERS0)) {
+    const bool inner = addend == nullptr && bnb.mask == nullptr && bnb.relu;
+    const bool input = addend != nullptr && bnb.mask != nullptr && bnb.relu;
+    if (bnb.part2 != nullptr || !(inner || input)) return -5;
+  }
   const bool cs64 = (Cs % 64) == 0;
   if (v >= PERS0) {
     if (bnb.part != nullptr) return launch_variant_pers_bnb(v - PERS0, cs64, p, stream);

@@ -1018,18 +1018,19 @@ def _conv_dgrad(dy, w32, N, H, W, Cin, Cout, g, addend=None, addend_mask=None, b
             return lib.pdt_conv_nt_bnb(*args, _s())
         return lib.pdt_conv_nt_bnb2(*args, _p(u2.y), _p(u2.mean), _p(part2), _s())
 
-    plan, R = [], 0
-    for wt, a in launches:
-        _check_nt(dy, wt, dx, a)
-        v = _select_bnb_variant(lambda v, part, rows, wt=wt, a=a: launch(wt, a, v, part, 0, rows), a,
-                                addend is not None, bnb_mask is not None, dy.device)
-        rows = lib.pdt_conv_nt_bnb_rows(a["Nimg"] * a["Hm"] * a["Wm"], Cin, a["K"], v)
-        plan.append((wt, a, v, R))
-        R += rows
     u2 = bnb_unit2
     if u2 is not None and (bnb_mask is None or u2.Cout != Cin or u2.y.shape != u.y.shape or
                            not u2.y.is_contiguous(memory_format=torch.channels_last)):
         u2 = None
+    plan, R = [], 0
+    for wt, a in launches:
+        _check_nt(dy, wt, dx, a)
+        # with a second unit the tile is tuned with its partials (own key: the ring tiles cannot)
+        v = _select_bnb_variant(lambda v, part, rows, part2, wt=wt, a=a: launch(wt, a, v, part, 0, rows, part2), a,
+                                addend is not None, bnb_mask is not None, dy.device, two=u2 is not None)
+        rows = lib.pdt_conv_nt_bnb_rows(a["Nimg"] * a["Hm"] * a["Wm"], Cin, a["K"], v)
+        plan.append((wt, a, v, R))
+        R += rows
     one = 2 * R * Cin + lib.pdt_rows_reduce_workspace(R, Cin)
     if u2 is None:
         part = torch.empty(one, dtype=torch.float32, device=dy.device)
@@ -1055,15 +1056,16 @@ def _conv_dgrad(dy, w32, N, H, W, Cin, Cout, g, addend=None, addend_mask=None, b
 _NTB_KEYS: dict = {}
 
 
-def _select_bnb_variant(launch, a, has_addend, has_mask, device):
+def _select_bnb_variant(launch, a, has_addend, has_mask, device, two=False):
     """Variant for a data gradient with the fused BN-backward epilogue: its own
-    tuned-table key (the epilogue's extra loads / registers shift the best tile)."""
+    tuned-table key (the epilogue's extra loads / registers shift the best tile);
+    ``two``: also a second unit's partials (key suffix ",2", timed with them)."""
     gt = (a["Hs"], a["Ws"], a["Cs"], a["Nimg"], a["Hm"], a["Wm"], a["Ncol"], a["K"], a["sh"], a["sw"], a["nth"],
-          a["ntw"], a["osh"], int(has_addend), int(has_mask))
+          a["ntw"], a["osh"], int(has_addend), int(has_mask)) + ((2,) if two else ())
     key = _NTB_KEYS.get(gt)
     if key is None:
         key = _NTB_KEYS[gt] = "ntb2:" + ",".join(str(x) for x in gt)
-    geom = key[5:].rsplit(",", 2)[0]
+    geom = ",".join(str(x) for x in gt[:13])
     table = _tuned()
     allowed = _retune_candidates(key, table)
     if key in table and allowed is None:
@@ -1076,7 +1078,9 @@ def _select_bnb_variant(launch, a, has_addend, has_mask, device):
     nvar = lib.pdt_conv_nt_num_variants()
     rows = max(lib.pdt_conv_nt_bnb_rows(M, a["Ncol"], a["K"], v) for v in range(nvar))
     part = torch.empty(2 * rows * a["Ncol"], dtype=torch.float32, device=device)
-    table[key] = _time_variants(nvar, lambda v: launch(v, part, lib.pdt_conv_nt_bnb_rows(M, a["Ncol"], a["K"], v)),
+    part2 = torch.empty_like(part) if two else None
+    table[key] = _time_variants(nvar, lambda v: launch(v, part, lib.pdt_conv_nt_bnb_rows(M, a["Ncol"], a["K"], v),
+                                                       part2),
                                 allowed if allowed is not None else _variant_filter())
     _save_tuned()
     return table[key]

@@ -28,7 +28,7 @@ SHAPES = [(56, 64, 256, 1), (56, 128, 256, 1), (28, 128, 512, 1), (14, 256, 1024
 
 def _ids(spec):
     out = []
-    for part in spec.split(","):
+    for part in spec.replace("+", ",").split(","):  # ('+' too: gpu_job.sh turns commas into spaces)
         lo, _, hi = part.partition("-")
         out += list(range(int(lo), int(hi or lo) + 1))
     return out

@@ -297,4 +297,7 @@ def test_bnb_epilogue_every_variant(ncol, use_mask, use_add, use_amask, two):
             ps2 = part2.view(2, R, ncol).sum(1)
             assert torch.equal(ps2[0], ps[0]), v
             assert nrmerr(ps2[1], (g * (y2.float() - mean2)).sum(0)) < 1e-3, v
-    assert ran >= (20 if two else 30)
+    # the ring tiles (ids 34-37, persistent 45-46) take only the inner / block-input walks
+    compiled = (not use_add and not use_mask) or (use_add and use_mask)
+    print(f"variants run: {ran}")
+    assert ran >= (30 if compiled and not two else 20)
