@@ -54,7 +54,9 @@ constexpr int PMAX = 384;          // patch pixels per buffer
 constexpr int PBYTES = PMAX * 128;
 constexpr int ZBYTES = 1024;       // zero region (reads land at ZOFF +- 256 B)
 
-template <int BN, int NTH, int SGN, bool BNB>
+// BNB: 0 plain output; the fused BN-backward partials with the ReLU gate 1 off, 2 recomputed
+// from y, 3 from the unit's bit mask (compiled per gate: a run-time gate branched per element)
+template <int BN, int NTH, int SGN, int BNB>
 __global__ void __launch_bounds__(NTH, 1) conv3x3_halo_kernel(NTParams p, int rs_log2, int ntm, int ntn, int ncc) {
   constexpr int WN = NTH / 64 / HWM;
   constexpr int MI = HBM / (HWM * 16);  // 7
@@ -266,42 +268,50 @@ __global__ void __launch_bounds__(NTH, 1) conv3x3_halo_kernel(NTParams p, int rs
       }
     } else {
       // fused BN-backward partials of the unit this gradient feeds: g = relu_gate(dA) on the
-      // bf16-rounded stored dA (exactly what the separate reduce pass would read)
-      const bool gate_y = p.bnb.relu && p.bnb.mask == nullptr;
+      // bf16-rounded stored dA (exactly what the separate reduce pass would read); a gated-off
+      // element is cleared in its packed word, the sums run on the packed fp32 VALU
+      typedef float f32x2 __attribute__((ext_vector_type(2)));
 #pragma unroll
       for (int j = 0; j < NI; ++j) {
         const int col = n0 + wn * (BN / WN) + j * 16 + lc;
-        float mu[4], sc[4], sh[4], s[4], q[4];
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          mu[r] = p.bnb.mean[col + r];
-          sc[r] = gate_y ? p.bnb.scale[col + r] : 0.f;
-          sh[r] = gate_y ? p.bnb.shift[col + r] : 0.f;
-          s[r] = q[r] = 0.f;
+        const f32x4 mu = *reinterpret_cast<const f32x4*>(p.bnb.mean + col);
+        f32x4 sc = {0.f, 0.f, 0.f, 0.f}, sh = sc;
+        if constexpr (BNB == 2) {
+          sc = *reinterpret_cast<const f32x4*>(p.bnb.scale + col);
+          sh = *reinterpret_cast<const f32x4*>(p.bnb.shift + col);
         }
+        f32x2 s01 = {0.f, 0.f}, s23 = s01, q01 = s01, q23 = s01;
 #pragma unroll
         for (int i = 0; i < MI; ++i) {
           const int m = m0 + wm * (HBM / HWM) + i * 16 + lr16;
           const bool rok = m < p.M;
           const size_t e = (size_t)(rok ? m : 0) * p.ldo + col;
           const uint2 yy = *reinterpret_cast<const uint2*>(p.bnb.y + e);
-          const uint32_t mk = p.bnb.mask != nullptr ? (uint32_t)(p.bnb.mask[e >> 3] >> (e & 7)) : 0xfu;
+          // (col is a multiple of 4: this lane's 4 mask bits are the byte's low or high nibble)
+          const uint32_t mk = BNB == 3 ? (uint32_t)(p.bnb.mask[e >> 3] >> (e & 7)) : 0xfu;
           const uint32_t w0 = pack2bf(acc[i][j][0], acc[i][j][1]), w1 = pack2bf(acc[i][j][2], acc[i][j][3]);
           if (rok) {
             typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
             *reinterpret_cast<u32x2*>(p.out + e) = u32x2{w0, w1};
           }
-          const float g0[4] = {lo_bf(w0), hi_bf(w0), lo_bf(w1), hi_bf(w1)};
-          const float yv[4] = {lo_bf(yy.x), hi_bf(yy.x), lo_bf(yy.y), hi_bf(yy.y)};
-#pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            bool on = rok;
-            if (p.bnb.relu) on = on && (gate_y ? (yv[r] * sc[r] + sh[r]) > 0.f : ((mk >> r) & 1u) != 0);
-            const float g = on ? g0[r] : 0.f;
-            s[r] += g;
-            q[r] += g * (yv[r] - mu[r]);
+          const uint32_t kb = rok ? mk : 0u;
+          const uint32_t g0w = w0 & pdt_bf16_pair_keep(kb, 0), g1w = w1 & pdt_bf16_pair_keep(kb, 1);
+          f32x2 ga = {lo_bf(g0w), hi_bf(g0w)}, gb = {lo_bf(g1w), hi_bf(g1w)};
+          const f32x2 ya = {lo_bf(yy.x), hi_bf(yy.x)}, yb = {lo_bf(yy.y), hi_bf(yy.y)};
+          if constexpr (BNB == 2) {
+            const f32x2 za = __builtin_elementwise_fma(ya, f32x2{sc[0], sc[1]}, f32x2{sh[0], sh[1]});
+            const f32x2 zb = __builtin_elementwise_fma(yb, f32x2{sc[2], sc[3]}, f32x2{sh[2], sh[3]});
+            ga.x = za.x > 0.f ? ga.x : 0.f;
+            ga.y = za.y > 0.f ? ga.y : 0.f;
+            gb.x = zb.x > 0.f ? gb.x : 0.f;
+            gb.y = zb.y > 0.f ? gb.y : 0.f;
           }
+          s01 += ga;
+          s23 += gb;
+          q01 = __builtin_elementwise_fma(ga, ya - f32x2{mu[0], mu[1]}, q01);
+          q23 = __builtin_elementwise_fma(gb, yb - f32x2{mu[2], mu[3]}, q23);
         }
+        float s[4] = {s01.x, s01.y, s23.x, s23.y}, q[4] = {q01.x, q01.y, q23.x, q23.y};
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           s[r] = row16_sum(s[r]);
@@ -327,13 +337,22 @@ int launch_halo(const NTParams& p, int sgn, int rs_log2, hipStream_t st) {
   const int ntm = (p.M + HBM - 1) / HBM, ntn = p.Ncol / BN, ncc = p.Cs / 64;
   int grid = ntm * ntn;
   if (grid > 256) grid = 256;  // persistent: one workgroup per CU (LDS-bound residency)
-  const bool bnb = p.bnb.part != nullptr;
+  const int bnb = p.bnb.part == nullptr ? 0 : !p.bnb.relu ? 1 : p.bnb.mask == nullptr ? 2 : 3;
+  auto go = [&](auto sgn_c, auto bnb_c) {
+    hipLaunchKernelGGL((conv3x3_halo_kernel<BN, NTH, decltype(sgn_c)::value, decltype(bnb_c)::value>), dim3(grid),
+                       dim3(NTH), 0, st, p, rs_log2, ntm, ntn, ncc);
+  };
+  using std::integral_constant;
   if (sgn > 0) {
-    if (bnb) hipLaunchKernelGGL((conv3x3_halo_kernel<BN, NTH, 1, true>), dim3(grid), dim3(NTH), 0, st, p, rs_log2, ntm, ntn, ncc);
-    else hipLaunchKernelGGL((conv3x3_halo_kernel<BN, NTH, 1, false>), dim3(grid), dim3(NTH), 0, st, p, rs_log2, ntm, ntn, ncc);
+    if (bnb == 0) go(integral_constant<int, 1>{}, integral_constant<int, 0>{});
+    else if (bnb == 1) go(integral_constant<int, 1>{}, integral_constant<int, 1>{});
+    else if (bnb == 2) go(integral_constant<int, 1>{}, integral_constant<int, 2>{});
+    else go(integral_constant<int, 1>{}, integral_constant<int, 3>{});
   } else {
-    if (bnb) hipLaunchKernelGGL((conv3x3_halo_kernel<BN, NTH, -1, true>), dim3(grid), dim3(NTH), 0, st, p, rs_log2, ntm, ntn, ncc);
-    else hipLaunchKernelGGL((conv3x3_halo_kernel<BN, NTH, -1, false>), dim3(grid), dim3(NTH), 0, st, p, rs_log2, ntm, ntn, ncc);
+    if (bnb == 0) go(integral_constant<int, -1>{}, integral_constant<int, 0>{});
+    else if (bnb == 1) go(integral_constant<int, -1>{}, integral_constant<int, 1>{});
+    else if (bnb == 2) go(integral_constant<int, -1>{}, integral_constant<int, 2>{});
+    else go(integral_constant<int, -1>{}, integral_constant<int, 3>{});
   }
   PDT_RETURN_LAUNCH();
 }

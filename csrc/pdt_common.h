@@ -103,6 +103,14 @@ __device__ __forceinline__ uint32_t pack2bf(float lo, float hi) {
 __device__ __forceinline__ float lo_bf(uint32_t w) { return __uint_as_float(w << 16); }
 __device__ __forceinline__ float hi_bf(uint32_t w) { return __uint_as_float(w & 0xffff0000u); }
 
+// keep mask of packed bf16 word e from a bit mask: bit 2e keeps its low half, bit 2e + 1 its
+// high half (0 / 0xffff / 0xffff0000 / ~0: a gated-off element becomes +0 under AND)
+__device__ __forceinline__ uint32_t pdt_bf16_pair_keep(uint32_t bits, int e) {
+  const uint32_t lo = (uint32_t)((int)(bits << (31 - 2 * e)) >> 31);
+  const uint32_t hi = (uint32_t)((int)(bits << (30 - 2 * e)) >> 31);
+  return (lo & 0x0000ffffu) | (hi & 0xffff0000u);
+}
+
 // DPP row reductions: a DPP "row" is 16 lanes; the operand permutes ride on the
 // VALU add (no LDS round trip, unlike __shfl_xor's ds_bpermute).
 //   quad_perm [1,0,3,2] (0xB1) = lane ^ 1, quad_perm [2,3,0,1] (0x4E) = lane ^ 2,

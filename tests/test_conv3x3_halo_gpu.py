@@ -45,6 +45,7 @@ def test_halo_forward_and_stats(shape):
     g = dict(KH=3, KW=3, sh=1, sw=1, ph=1, pw=1, Ho=H, Wo=W)
     a = no._fwd_nt_geom(N, H, W, Cin, Cout, g)
     M = N * H * W
+    bmask = torch.randint(0, 256, (M * Cin // 8,), dtype=torch.uint8, device="cuda") if gate_mode == "mask" else None
     ran = 0
     for v in _halo_variants():
         rows = lib.pdt_conv_nt_stat_rows(M, Cout, a["K"], v)
@@ -62,8 +63,11 @@ def test_halo_forward_and_stats(shape):
     assert ran >= 1
 
 
+@pytest.mark.parametrize("gate_mode", ["y", "mask", "none"])
 @pytest.mark.parametrize("shape", SHAPES)
-def test_halo_dgrad_and_fused_bn_backward_partials(shape):
+def test_halo_dgrad_and_fused_bn_backward_partials(shape, gate_mode):
+    """The halo data gradient with the fused BN-backward partials, for each compiled ReLU gate
+    (recomputed from y, the unit's bit mask, no ReLU) vs fp32."""
     torch.manual_seed(1)
     N, Cin, H, W, Cout = shape
     lib = no._load()
@@ -82,6 +86,7 @@ def test_halo_dgrad_and_fused_bn_backward_partials(shape):
     scale = torch.rand(Cin, device="cuda") + 0.5
     shift = torch.randn(Cin, device="cuda") * 0.1
     M = N * H * W
+    bmask = torch.randint(0, 256, (M * Cin // 8,), dtype=torch.uint8, device="cuda") if gate_mode == "mask" else None
     ran = 0
     for v in _halo_variants():
         dx = torch.full_like(yb, float("nan"))
@@ -98,11 +103,17 @@ def test_halo_dgrad_and_fused_bn_backward_partials(shape):
             no._p(dy), no._p(wt), no._p(dx2), None, None, a["Hs"], a["Ws"], a["Cs"], a["Nimg"], a["Hm"], a["Wm"],
             a["Ncol"], a["K"], a["ldb"], a["sh"], a["sw"], a["oh0"], a["ow0"], a["dh"], a["dw"], a["nth"], a["ntw"],
             a["Ho"], a["Wo"], a["osh"], a["osw"], a["oph"], a["opw"], a["ldo"], v, no._p(yb), no._p(mean),
-            no._p(scale), no._p(shift), None, no._p(part), 1, 0, R, no._s())
+            no._p(scale), no._p(shift), no._p(bmask), no._p(part), int(gate_mode != "none"), 0, R, no._s())
         assert rc == 0, (v, rc)
         assert torch.equal(dx2, dx), v  # same stored gradient
         yf = yb.float()
-        gate = (yf * scale.view(1, -1, 1, 1) + shift.view(1, -1, 1, 1)) > 0
+        if gate_mode == "y":
+            gate = (yf * scale.view(1, -1, 1, 1) + shift.view(1, -1, 1, 1)) > 0
+        elif gate_mode == "mask":  # bit k of byte i gates element 8 i + k of the NHWC storage
+            bits = ((bmask.view(-1, 1).int() >> torch.arange(8, device="cuda")) & 1).view(N, H, W, Cin)
+            gate = bits.permute(0, 3, 1, 2).bool()
+        else:
+            gate = torch.ones_like(yf, dtype=torch.bool)
         gq = dx.float() * gate
         ps = part.view(2, R, Cin).sum(1)
         assert relerr(ps[0], gq.sum((0, 2, 3))) < 2e-3, v
