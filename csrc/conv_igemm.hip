@@ -322,6 +322,20 @@ PDT_API int pdt_conv_nt_bnb_rows(int M, int Ncol, int K, int variant) {
   return (M + VAR_BM[v] - 1) / VAR_BM[v];
 }
 
+// 1 when a variant's BN-backward epilogue compiles this configuration: the ring tiles (ids
+// 34-37 and the persistent ones) carry only a block's inner unit (ReLU recomputed from y) and a
+// block input (addend + ReLU bit mask), without a second unit; the halo tiles no second unit.
+PDT_API int pdt_conv_nt_bnb_supports(int variant, int has_addend, int has_mask, int relu, int two) {
+  const int v = variant;
+  if ((v >= 34 && v < NVAR) || v >= PERS0) {
+    const bool inner = !has_addend && !has_mask && relu;
+    const bool input = has_addend && has_mask && relu;
+    return !two && (inner || input);
+  }
+  if (v >= HALO0 && v < PERS0) return !two;
+  return 1;
+}
+
 PDT_API int pdt_conv_nt_stat_rows(int M, int Ncol, int K, int variant) {
   int v = pdt_conv_nt_resolve_variant(variant, M, Ncol, K);
   if (v >= HALO0 && v < PERS0) return halo_rows(M);
@@ -408,11 +422,9 @@ static int conv_nt_impl(const void* src, const void* b, void* out, float* stats,
   }
   // ring tiles: only the BN-backward walks they compile (conv_nt_tile.inc) -- a block's inner unit
   // (ReLU recomputed from y) or a block input (addend + ReLU bit mask); no second-unit partials
-  if (bnb.part != nullptr && ((v >= 34 && v < NVAR) || v >= PERS0)) {
-    const bool inner = addend == nullptr && bnb.mask == nullptr && bnb.relu;
-    const bool input = addend != nullptr && bnb.mask != nullptr && bnb.relu;
-    if (bnb.part2 != nullptr || !(inner || input)) return -5;
-  }
+  if (bnb.part != nullptr && ((v >= 34 && v < NVAR) || v >= PERS0) &&
+      !pdt_conv_nt_bnb_supports(v, addend != nullptr, bnb.mask != nullptr, bnb.relu, bnb.part2 != nullptr))
+    return -5;
   const bool cs64 = (Cs % 64) == 0;
   if (v >= PERS0) {
     if (bnb.part != nullptr) return launch_variant_pers_bnb(v - PERS0, cs64, p, stream);

@@ -47,6 +47,7 @@ _SIGS = {
     "pdt_conv_nt": (c_int, [P, P, P, P, P, P, P] + [c_int] * 25 + [P, c_int, c_int, P]),
     "pdt_conv_nt_bnb": (c_int, [P] * 5 + [c_int] * 25 + [P] * 6 + [c_int] * 3 + [P]),
     "pdt_conv_nt_bnb2": (c_int, [P] * 5 + [c_int] * 25 + [P] * 6 + [c_int] * 3 + [P] * 3 + [P]),
+    "pdt_conv_nt_bnb_supports": (c_int, [c_int] * 5),
     "pdt_ln_fwd": (c_int, [P, P, P, P, P, P, c_int, c_int, c_float, P]),
     "pdt_gemm_f8_q8": (c_int, [P] * 6 + [c_int] * 8 + [P, P, c_int, P, P, P, c_int, c_int, P, P]),
     "pdt_gemm_f8_q8_cs": (c_int, [P] * 6 + [c_int] * 8 + [P, P, c_int, P, P, P, c_int, c_int, P, P, P]),
@@ -1023,11 +1024,19 @@ def _conv_dgrad(dy, w32, N, H, W, Cin, Cout, g, addend=None, addend_mask=None, b
                            not u2.y.is_contiguous(memory_format=torch.channels_last)):
         u2 = None
     plan, R = [], 0
+    has_add, has_mask = int(addend is not None), int(bnb_mask is not None)
     for wt, a in launches:
         _check_nt(dy, wt, dx, a)
         # with a second unit the tile is tuned with its partials (own key: the ring tiles cannot)
         v = _select_bnb_variant(lambda v, part, rows, part2, wt=wt, a=a: launch(wt, a, v, part, 0, rows, part2), a,
                                 addend is not None, bnb_mask is not None, dy.device, two=u2 is not None)
+        # a table / heuristic choice whose epilogue does not compile this configuration (a ring
+        # tile): without the second unit if that is all it lacks, else the generic 64x128 tile
+        if not lib.pdt_conv_nt_bnb_supports(v, has_add, has_mask, int(relu), int(u2 is not None)):
+            if u2 is not None and lib.pdt_conv_nt_bnb_supports(v, has_add, has_mask, int(relu), 0):
+                u2 = None
+            else:
+                v = _BNB_GENERIC_VARIANT
         rows = lib.pdt_conv_nt_bnb_rows(a["Nimg"] * a["Hm"] * a["Wm"], Cin, a["K"], v)
         plan.append((wt, a, v, R))
         R += rows
@@ -1054,6 +1063,7 @@ def _conv_dgrad(dy, w32, N, H, W, Cin, Cout, g, addend=None, addend_mask=None, b
 
 
 _NTB_KEYS: dict = {}
+_BNB_GENERIC_VARIANT = 17  # 64x128 LDS tile, direct store: every BN-backward epilogue configuration
 
 
 def _select_bnb_variant(launch, a, has_addend, has_mask, device, two=False):

@@ -256,12 +256,15 @@ class _FakeUnit:
         self.Cout = y.shape[1]
 
 
-@pytest.mark.parametrize("v", [5, 15, 25, 27, 38, 40, 37])
-def test_dgrad_epilogue_second_unit_partials(monkeypatch, v):
+@pytest.mark.parametrize("v,with_add", [(5, False), (15, False), (25, False), (27, False), (38, False), (40, False),
+                                        (37, False), (37, True), (36, True)])
+def test_dgrad_epilogue_second_unit_partials(monkeypatch, v, with_add):
     """A data-gradient epilogue producing the BN-backward partials of TWO units fed by the
     same ReLU-gated gradient (a downsample block's bn3 and shortcut BN): both partial sets
-    against fp32 sums over the stored gradient; variant 37 (a ring tile) falls back to
-    the single-unit epilogue (second = None)."""
+    against fp32 sums over the stored gradient. A ring tile (36, 37) compiles no second unit:
+    given a block input (addend + mask) it runs the single-unit epilogue (second = None);
+    given a configuration it does not compile at all (mask without addend) the launch moves
+    to the generic tile, which carries both units."""
     torch.manual_seed(v)
     N, Cin, Cm, H = 4, 256, 64, 14
     dy = _cl(torch.randn(N, Cm, H, H, device="cuda").to(torch.bfloat16))
@@ -273,9 +276,12 @@ def test_dgrad_epilogue_second_unit_partials(monkeypatch, v):
     u3, ud = _FakeUnit(y3, m3), _FakeUnit(yd, md, relu=False)
     monkeypatch.setattr(no, "_select_bnb_variant", lambda *a, **k: v)
     g = {"KH": 1, "KW": 1, "sh": 1, "sw": 1, "ph": 0, "pw": 0, "Ho": H, "Wo": H}
-    dx, pre = no._conv_dgrad(dy, w, N, H, H, Cin, Cm, g, bnb_unit=u3, bnb_mask=mask, bnb_unit2=ud)
+    add = _cl(torch.randn(N, Cin, H, H, device="cuda").to(torch.bfloat16)) if with_add else None
+    dx, pre = no._conv_dgrad(dy, w, N, H, H, Cin, Cm, g, addend=add, bnb_unit=u3, bnb_mask=mask, bnb_unit2=ud)
     torch.cuda.synchronize()
     ref = torch.nn.functional.conv2d(dy.float(), w.to(torch.bfloat16).float().transpose(0, 1))
+    if with_add:
+        ref = ref + add.float()
     assert nrmerr(dx, ref) < 1e-2
     bits = torch.stack([(mask >> k) & 1 for k in range(8)], 1).reshape(-1).bool()
     gate = dx.float().permute(0, 2, 3, 1).reshape(-1, Cin) * bits.view(-1, Cin)
@@ -285,7 +291,7 @@ def test_dgrad_epilogue_second_unit_partials(monkeypatch, v):
     R = pre.R
     p3 = pre.part[:2 * R * Cin].view(2, R, Cin).sum(1)
     assert nrmerr(p3[0], s_ref) < 1e-3 and nrmerr(p3[1], q3_ref) < 1e-3
-    if v == 37:
+    if v in (36, 37) and with_add:
         assert pre.second is None
         return
     assert pre.second is not None and pre.second.unit is ud
