@@ -45,7 +45,6 @@ def test_halo_forward_and_stats(shape):
     g = dict(KH=3, KW=3, sh=1, sw=1, ph=1, pw=1, Ho=H, Wo=W)
     a = no._fwd_nt_geom(N, H, W, Cin, Cout, g)
     M = N * H * W
-    bmask = torch.randint(0, 256, (M * Cin // 8,), dtype=torch.uint8, device="cuda") if gate_mode == "mask" else None
     ran = 0
     for v in _halo_variants():
         rows = lib.pdt_conv_nt_stat_rows(M, Cout, a["K"], v)
