@@ -62,9 +62,12 @@ def test_persistent_ring_tiles_forward_and_stats(M, N, K):
         assert torch.equal(part, part1), v
 
 
-def test_persistent_ring_tiles_bn_backward_epilogue():
+@pytest.mark.parametrize("block_input", [False, True])
+def test_persistent_ring_tiles_bn_backward_epilogue(block_input):
     """The fused BN-backward partials (pdt_conv_nt_bnb) from the persistent tiles: every tile
-    writes its own partial row, with a ReLU-masked addend."""
+    writes its own partial row, in the two configurations the ring tiles compile -- a block's
+    inner unit (ReLU gate recomputed from y) and a block input (ReLU-masked addend, the
+    unit's ReLU bit mask)."""
     lib = no._load()
     torch.manual_seed(6)
     dev = "cuda"
@@ -75,14 +78,19 @@ def test_persistent_ring_tiles_bn_backward_epilogue():
     mean = torch.randn(N, device=dev) * 0.1
     scale = torch.rand(N, device=dev) + 0.5
     shift = torch.randn(N, device=dev) * 0.1
-    add = torch.randn(M, N, device=dev).to(torch.bfloat16)
-    amask = torch.randint(0, 256, (M * N // 8,), dtype=torch.uint8, device=dev)
+    add = torch.randn(M, N, device=dev).to(torch.bfloat16) if block_input else None
+    amask = torch.randint(0, 256, (M * N // 8,), dtype=torch.uint8, device=dev) if block_input else None
+    bmask = torch.randint(0, 256, (M * N // 8,), dtype=torch.uint8, device=dev) if block_input else None
 
     def bits(m):
         return ((m.view(-1, 1).int() >> torch.arange(8, device=dev)) & 1).view(M, N).float()
 
-    ref = dy.float() @ wt.float().t() + add.float() * bits(amask)
-    gate = ((y.float() * scale + shift) > 0).float()
+    ref = dy.float() @ wt.float().t()
+    if block_input:
+        ref = ref + add.float() * bits(amask)
+        gate = bits(bmask)
+    else:
+        gate = ((y.float() * scale + shift) > 0).float()
     for v in _pers_ids(lib):
         R = lib.pdt_conv_nt_bnb_rows(M, N, K, v)
         part = torch.full((2 * R * N,), float("nan"), device=dev)
@@ -90,7 +98,7 @@ def test_persistent_ring_tiles_bn_backward_epilogue():
         rc = lib.pdt_conv_nt_bnb(no._p(dy), no._p(wt), no._p(out), no._p(add), no._p(amask),
                                  1, 1, K, M, 1, 1, N, K, K, 1, 1, 0, 0, 1, 1, 1, 1,
                                  1, 1, 1, 1, 0, 0, N, v, no._p(y), no._p(mean), no._p(scale), no._p(shift),
-                                 None, no._p(part), 1, 0, R, no._s())
+                                 no._p(bmask), no._p(part), 1, 0, R, no._s())
         assert rc == 0, (v, rc)
         torch.cuda.synchronize()
         assert nrmerr(out, ref) < 1e-2, v
