@@ -48,10 +48,11 @@ BASELINE_METRIC = "images/sec (whole node) ResNet-50 synthetic 3x224x224 at 1/2/
 # per-GPU batch), see BASELINE.md. Scaled by N for N GPUs (weak scaling). The bs 2048 points
 # need MIOpen's find db (profiles/miopen_db_bs2048, scripts/gpu_job.sh benchlong): a cold
 # find at that batch runs ~20 min, and immediate mode without it falls back to naive kernels.
-# Round 5 (profiles/bench_runs_round5.jsonl, r5e / r5f / r5n): resnet50 2048, resnet152 2048 and
-# 3072 (258.7 GiB), vit_b_16 1024; the bs 256 / 512 points are round 2-3 measurements.
+# Round 5 (profiles/bench_runs_round5.jsonl, r5e / r5f): resnet50 2048, resnet152 2048, vit_b_16
+# 1024; round 6 (profiles/bench_runs_round6.jsonl, q01): resnet152 3072 (258.7 GiB), 20 timed
+# steps; the bs 256 / 512 points are round 2-3 measurements.
 STOCK_1GPU_IMG_S = {("resnet50", 256): 6605.4, ("resnet50", 512): 6863.8, ("resnet50", 2048): 6936.44,
-                    ("resnet152", 2048): 2852.86, ("resnet152", 3072): 2828.03,
+                    ("resnet152", 2048): 2852.86, ("resnet152", 3072): 2838.07,
                     ("vit_b_16", 256): 3547.25, ("vit_b_16", 1024): 4089.11}
 # The stock stack's BEST measured per-GPU throughput (and its batch): reported as
 # ``vs_best_stock``, never as ``vs_baseline``.
