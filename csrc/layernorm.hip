@@ -96,7 +96,7 @@ __global__ void __launch_bounds__(64 * WPB) ln_fwd_kernel(const u16* __restrict_
     float o[4];
 #pragma unroll
     for (int e = 0; e < 4; ++e) o[e] = (v[c][e] - mean) * rstd * gg[e] + bb[e];
-    st4(yr + col, o);
+    if (!F8 || y != nullptr) st4(yr + col, o);  // (F8: y == nullptr -- the codes are the only consumer's input)
     if (F8) {
       const float s = meta[0];
       float r[4];
@@ -377,11 +377,12 @@ PDT_API int pdt_ln_fwd_f8_blocks(int rows) { return (rows + WPB - 1) / WPB; }
 
 // LayerNorm of xsum = bf16(x + r) (written to xsum): the residual add of a pre-norm block moved
 // out of the producing GEMM's epilogue (so a library GEMM can produce x). q (optional, with
-// meta / amax_part / dq_out as pdt_ln_fwd_f8): the e4m3 codes of the output as well.
+// meta / amax_part / dq_out as pdt_ln_fwd_f8): the e4m3 codes of the output as well; with q,
+// y may be null (codes only: the consuming fp8 GEMM reads nothing else).
 PDT_API int pdt_ln_add_fwd(const void* x, const void* r, void* xsum, const float* g, const float* b, void* y,
                            float* mean, float* rstd, int rows, int D, float eps, void* q, float* meta,
                            float* amax_part, float* dq_out, hipStream_t st) {
-  if (!r || !xsum || (q && (!meta || !amax_part))) return -1;
+  if (!r || !xsum || (q && (!meta || !amax_part)) || (!q && !y)) return -1;
   const int nb = (rows + WPB - 1) / WPB;
   dim3 grid(nb), blk(64 * WPB);
 #define LA(CH_, F_) hipLaunchKernelGGL((ln_fwd_kernel<CH_, F_>), grid, blk, 0, st, (const u16*)x, g, b, (u16*)y, mean, \
@@ -412,7 +413,8 @@ PDT_API int pdt_ln_add_fwd(const void* x, const void* r, void* xsum, const float
 
 // LayerNorm forward that also emits the e4m3 codes of its output for the next fp8 GEMM
 // (delayed scale meta[0]) and rolls that GEMM's amax history; amax_part holds
-// pdt_ln_fwd_f8_blocks(rows) floats; dq_out receives the codes' dequant factor.
+// pdt_ln_fwd_f8_blocks(rows) floats; dq_out receives the codes' dequant factor. y may be null
+// (codes only).
 PDT_API int pdt_ln_fwd_f8(const void* x, const float* g, const float* b, void* y, float* mean, float* rstd, int rows,
                           int D, float eps, void* q, float* meta, float* amax_part, float* dq_out, hipStream_t st) {
   const int nb = (rows + WPB - 1) / WPB;

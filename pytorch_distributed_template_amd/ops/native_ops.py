@@ -2932,7 +2932,7 @@ class _LNFork(torch.autograd.Function):
     the LayerNorm backward kernel (no add pass)."""
 
     @staticmethod
-    def forward(ctx, x, g, b, eps, f8meta, f8box, grad_owner):
+    def forward(ctx, x, g, b, eps, f8meta, f8box, grad_owner, codes_only=False):
         ctx.refs = (g, b)
         shp = x.shape
         D = shp[-1]
@@ -2947,8 +2947,10 @@ class _LNFork(torch.autograd.Function):
             q = torch.empty((rows, D), dtype=torch.uint8, device=x.device)
             part = torch.empty(lib.pdt_ln_fwd_f8_blocks(rows) + 1, dtype=torch.float32, device=x.device)
             dq = part[-1:]  # the codes' dequant factor (written by the history roll)
-            _chk(lib.pdt_ln_fwd_f8(_p(x2), _p(gf), _p(bf), _p(y), _p(stats[0]), _p(stats[1]), rows, D, float(eps),
-                                   _p(q), _p(f8meta), _p(part), _p(dq), _s()), "ln_fwd_f8")
+            # codes_only: the bf16 output is not written (y stays uninitialised; see _ln_codes_only)
+            _chk(lib.pdt_ln_fwd_f8(_p(x2), _p(gf), _p(bf), None if codes_only else _p(y), _p(stats[0]),
+                                   _p(stats[1]), rows, D, float(eps), _p(q), _p(f8meta), _p(part), _p(dq), _s()),
+                 "ln_fwd_f8")
             f8box.append((q, dq))
         else:
             _chk(lib.pdt_ln_fwd(_p(x2), _p(gf), _p(bf), _p(y), _p(stats[0]), _p(stats[1]), rows, D, float(eps),
@@ -2961,9 +2963,9 @@ class _LNFork(torch.autograd.Function):
     @staticmethod
     def backward(ctx, g_res, dy):
         if dy is None:
-            return g_res, None, None, None, None, None, None
+            return g_res, None, None, None, None, None, None, None
         dx, dg, db = _ln_fork_backward(ctx, g_res, dy)
-        return dx, dg, db, None, None, None, None
+        return dx, dg, db, None, None, None, None, None
 
 
 def _ln_fork_backward(ctx, g_res, dy):
@@ -3018,7 +3020,7 @@ class _LNAddFork(torch.autograd.Function):
     as _LNFork; y and r both receive the summed gradient."""
 
     @staticmethod
-    def forward(ctx, y, r, g, b, eps, f8meta, f8box, grad_owner):
+    def forward(ctx, y, r, g, b, eps, f8meta, f8box, grad_owner, codes_only=False):
         ctx.refs = (g, b)
         shp = y.shape
         D = shp[-1]
@@ -3034,8 +3036,9 @@ class _LNAddFork(torch.autograd.Function):
             q = torch.empty((rows, D), dtype=torch.uint8, device=y.device)
             part = torch.empty(lib.pdt_ln_fwd_f8_blocks(rows) + 1, dtype=torch.float32, device=y.device)
             dq = part[-1:]
-            _chk(lib.pdt_ln_add_fwd(_p(y2), _p(r2), _p(xs), _p(gf), _p(bf), _p(h), _p(stats[0]), _p(stats[1]), rows, D,
-                                    float(eps), _p(q), _p(f8meta), _p(part), _p(dq), _s()), "ln_add_fwd_f8")
+            _chk(lib.pdt_ln_add_fwd(_p(y2), _p(r2), _p(xs), _p(gf), _p(bf), None if codes_only else _p(h),
+                                    _p(stats[0]), _p(stats[1]), rows, D, float(eps), _p(q), _p(f8meta), _p(part),
+                                    _p(dq), _s()), "ln_add_fwd_f8")
             f8box.append((q, dq))
         else:
             _chk(lib.pdt_ln_add_fwd(_p(y2), _p(r2), _p(xs), _p(gf), _p(bf), _p(h), _p(stats[0]), _p(stats[1]), rows, D,
@@ -3048,9 +3051,9 @@ class _LNAddFork(torch.autograd.Function):
     @staticmethod
     def backward(ctx, g_res, dy):
         if dy is None:
-            return g_res, g_res, None, None, None, None, None, None
+            return g_res, g_res, None, None, None, None, None, None, None
         dx, dg, db = _ln_fork_backward(ctx, g_res, dy)
-        return dx, dx, dg, db, None, None, None, None
+        return dx, dx, dg, db, None, None, None, None, None
 
 
 def ln_add_fork(y, r, ln, fp8_for=None, grad_fp8_for=None):
@@ -3066,9 +3069,12 @@ def ln_add_fork(y, r, ln, fp8_for=None, grad_fp8_for=None):
     box: list = []
     if os.environ.get("PDT_FP8_LN_GRAD", "1") == "0":
         grad_fp8_for = None
-    xo, h = _LNAddFork.apply(y, r, ln.weight, ln.bias, ln.eps, meta, box, grad_fp8_for)
+    only = meta is not None and _ln_codes_only(fp8_for)
+    xo, h = _LNAddFork.apply(y, r, ln.weight, ln.bias, ln.eps, meta, box, grad_fp8_for, only)
     if box:
         h._pdt_f8 = (box[0][0], box[0][1], fp8_for)
+        if only:
+            h._pdt_f8_only = True
     return xo, h
 
 
@@ -3092,15 +3098,36 @@ def ln_fork(x, ln, fp8_for=None, grad_fp8_for=None):
     box: list = []
     if os.environ.get("PDT_FP8_LN_GRAD", "1") == "0":
         grad_fp8_for = None
-    xo, h = _LNFork.apply(x, ln.weight, ln.bias, ln.eps, meta, box, grad_fp8_for)
+    only = meta is not None and _ln_codes_only(fp8_for)
+    xo, h = _LNFork.apply(x, ln.weight, ln.bias, ln.eps, meta, box, grad_fp8_for, only)
     if box:
         h._pdt_f8 = (box[0][0], box[0][1], fp8_for)
+        if only:
+            h._pdt_f8_only = True
     return xo, h
 
 
+def _ln_codes_only(fp8_for) -> bool:
+    """The LayerNorm output's bf16 values are not written when its consumer (the fp8 layer
+    ``fp8_for``: ViT's qkv / fc1) reads only its e4m3 codes -- an fp8 forward GEMM on the
+    codes, and fp8 weight gradients that keep the codes instead of the bf16 input. The
+    returned tensor carries ``_pdt_f8_only``; a consumer that would read the values refuses it
+    (:func:`_prequant`). PDT_LN_CODES_ONLY=0 writes them anyway."""
+    cfg = fp8_settings()
+    return (os.environ.get("PDT_LN_CODES_ONLY", "1") == "1" and cfg["dgrad"] and cfg["wgrad"]
+            and fp8_for.in_features % 128 == 0 and fp8_for.out_features % 128 == 0)
+
+
 def _prequant(x, owner):
-    """(codes [rows, K], dq) if ``x`` carries fp8 codes made for ``owner`` (ln_fork), else None."""
+    """(codes [rows, K], dq) if ``x`` carries fp8 codes made for ``owner`` (ln_fork), else None.
+    A codes-only tensor (``_pdt_f8_only``: its bf16 values were never written) may be read by
+    ``owner`` alone, and only through an fp8 path that keeps the codes for its weight gradient."""
     pre = getattr(x, "_pdt_f8", None)
+    if getattr(x, "_pdt_f8_only", False):
+        cfg = fp8_settings()
+        if pre is None or pre[2] is not owner or not (cfg["dgrad"] and cfg["wgrad"]):
+            raise RuntimeError("this LayerNorm output carries fp8 codes only (its bf16 values were not written) "
+                               "and its consumer would read the values: set PDT_LN_CODES_ONLY=0")
     if pre is None or pre[2] is not owner:
         return None
     return pre[0], pre[1]

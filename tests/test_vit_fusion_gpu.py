@@ -857,3 +857,46 @@ def test_linear_wgrad_bias_without_param():
     assert db.is_cuda and dw.is_cuda
     assert nrmerr(db, dy.float().sum(0)) < 1e-5
     assert nrmerr(dw, dy.float().t() @ x.float()) < 1e-3
+
+
+def test_vit_ln_codes_only_output_bit_identical(monkeypatch):
+    """fp8 ViT with the LayerNorm outputs written as e4m3 codes only (their consumers, qkv and
+    fc1, read nothing else: ops/native_ops.py _ln_codes_only) against the same step with the bf16
+    outputs written too: loss and every parameter gradient bit-identical from the same weights
+    and fp8 scaling state, and the codes-only launches actually taken."""
+    from pytorch_distributed_template_amd.models.vit import VisionTransformer
+    torch.manual_seed(4)
+    m = VisionTransformer(depth=2, fp8=True).cuda().to(memory_format=torch.channels_last)
+    x = torch.randn(8, 3, 224, 224, device="cuda")
+    y = torch.randint(0, 1000, (8,), device="cuda")
+    monkeypatch.setenv("PDT_LN_CODES_ONLY", "0")
+    for _ in range(3):  # delayed-scaling histories exist from here on: the LayerNorms emit codes
+        m.zero_grad(set_to_none=True)
+        fused.softmax_cross_entropy(m(x), y).backward()
+    names = ("_pdt_fp8_meta", "_pdt_fp8_gmeta")
+    state = [(mod, a, getattr(mod, a).clone()) for mod in m.modules() for a in names if hasattr(mod, a)]
+    assert state
+    lib = no._load()
+    seen = {"null_y": 0}
+    for fn_name, y_arg in (("pdt_ln_fwd_f8", 3), ("pdt_ln_add_fwd", 5)):
+        orig = getattr(lib, fn_name)
+
+        def wrap(*a, orig=orig, y_arg=y_arg):
+            seen["null_y"] += a[y_arg] is None
+            return orig(*a)
+        monkeypatch.setattr(lib, fn_name, wrap)
+    res = {}
+    for only in ("0", "1"):
+        for mod, a, t in state:
+            getattr(mod, a).copy_(t)
+        monkeypatch.setenv("PDT_LN_CODES_ONLY", only)
+        seen["null_y"] = 0
+        m.zero_grad(set_to_none=True)
+        loss = fused.softmax_cross_entropy(m(x), y)
+        loss.backward()
+        torch.cuda.synchronize()
+        res[only] = (float(loss), {n: p.grad.clone() for n, p in m.named_parameters()}, seen["null_y"])
+    assert res["0"][2] == 0 and res["1"][2] >= 4, (res["0"][2], res["1"][2])  # 2 LayerNorms per block
+    assert res["1"][0] == res["0"][0]
+    for n, g in res["0"][1].items():
+        assert torch.equal(res["1"][1][n], g), n
