@@ -178,9 +178,11 @@ def test_gemm_f8_fp8_output_epilogue(act, qfmt):
         assert torch.equal(meta, meta_ref), v
 
 
-def test_ln_fork_fp8_codes_match_separate_cast():
+def test_ln_fork_fp8_codes_match_separate_cast(monkeypatch):
     """pdt_ln_fwd_f8: same e4m3 codes, dq and amax-history roll as LayerNorm followed by
-    the delayed-scaling cast (rows % 4 != 0 exercises the idle-wave path)."""
+    the delayed-scaling cast (rows % 4 != 0 exercises the idle-wave path); the codes-only
+    output (no bf16 values written) carries the same codes."""
+    monkeypatch.setenv("PDT_LN_CODES_ONLY", "0")  # the bf16 output is compared below
     torch.manual_seed(26)
     ln = nn.LayerNorm(768, eps=1e-6).cuda()
     with torch.no_grad():
@@ -201,6 +203,13 @@ def test_ln_fork_fp8_codes_match_separate_cast():
     assert torch.equal(q.view(-1, 768), q_ref), (q.view(-1, 768) != q_ref).sum().item()
     assert torch.equal(dq, dq_ref)
     assert torch.equal(meta1, meta_ref), (meta1, meta_ref)
+    monkeypatch.setenv("PDT_LN_CODES_ONLY", "1")
+    fc._pdt_fp8_meta = meta0.clone()
+    _, h1 = no.ln_fork(x, ln, fc)
+    assert getattr(h1, "_pdt_f8_only", False) and h1._pdt_f8[2] is fc
+    assert torch.equal(h1._pdt_f8[0], q) and torch.equal(h1._pdt_f8[1], dq)
+    with pytest.raises(RuntimeError, match="codes only"):
+        no._prequant(h1, nn.Linear(768, 256).cuda())  # any other consumer would read the values
 
 
 def test_ln_fork_backward_e5m2_codes_match_separate_cast():
@@ -494,11 +503,13 @@ def test_fp8_attention_forward_and_backward(B, T, H, bwd, pv8, monkeypatch):
         assert ei < (1.6e-1 if bwd == "f8" else 1e-1), (name, ei)
 
 
-@pytest.mark.parametrize("fp8", [False, True])
-def test_ln_add_fork_matches_add_then_fork(fp8):
+@pytest.mark.parametrize("fp8,codes_only", [(False, "0"), (True, "0"), (True, "1")])
+def test_ln_add_fork_matches_add_then_fork(fp8, codes_only, monkeypatch):
     """ln_add_fork(y, r) == ln_fork(bf16(y + r)): the summed residual stream, the normalised
     output (and its e4m3 codes under delayed scaling), and both input gradients = the fork's
-    summed gradient (with the producer's e5m2 codes)."""
+    summed gradient (with the producer's e5m2 codes). codes_only: the normalised output is
+    written as e4m3 codes alone (its values are then not compared)."""
+    monkeypatch.setenv("PDT_LN_CODES_ONLY", codes_only)
     torch.manual_seed(41)
     D, rows = 768, 394
     ln = nn.LayerNorm(D, eps=1e-6).cuda()
@@ -533,7 +544,10 @@ def test_ln_add_fork_matches_add_then_fork(fp8):
     s0, h0, gy0, gr0 = run(False)
     torch.cuda.synchronize()
     assert torch.equal(s1, s0)
-    assert torch.equal(h1, h0)
+    if codes_only == "1":
+        assert getattr(h1, "_pdt_f8_only", False) and getattr(h0, "_pdt_f8_only", False)
+    else:
+        assert torch.equal(h1, h0)
     assert torch.equal(gy1, gy0) and torch.equal(gr1, gy1)
     if fp8:
         assert torch.equal(h1._pdt_f8[0], h0._pdt_f8[0])
