@@ -95,7 +95,8 @@ __global__ void __launch_bounds__(64 * WPB) ln_fwd_kernel(const u16* __restrict_
     f32x4 bb = *reinterpret_cast<const f32x4*>(b + col);
     float o[4];
 #pragma unroll
-    for (int e = 0; e < 4; ++e) o[e] = (v[c][e] - mean) * rstd * gg[e] + bb[e];
+    // (explicit fma: every instantiation rounds alike, whatever hipcc would contract)
+    for (int e = 0; e < 4; ++e) o[e] = fmaf((v[c][e] - mean) * rstd, gg[e], bb[e]);
     if (!F8 || y != nullptr) st4(yr + col, o);  // (F8: y == nullptr -- the codes are the only consumer's input)
     if (F8) {
       const float s = meta[0];
