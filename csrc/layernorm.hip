@@ -83,10 +83,10 @@ __global__ void __launch_bounds__(64 * WPB) ln_fwd_kernel(const u16* __restrict_
   for (int c = 0; c < CH; ++c)
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
-      float d = v[c][e] - mean;
-      q += d * d;
+      const float d = v[c][e] - mean;
+      q = fmaf(d, d, q);  // (explicit: hipcc contracted some of these per instantiation, not all)
     }
-  const float rstd = rsqrtf(warp_sum(q) * (1.f / D) + eps);
+  const float rstd = rsqrtf(fmaf(warp_sum(q), 1.f / D, eps));
   u16* yr = y + (long)row * D;
 #pragma unroll
   for (int c = 0; c < CH; ++c) {
