@@ -71,7 +71,7 @@ for job in "$@"; do
       PDT_AUTOTUNE_SHIPPED=0 PDT_AUTOTUNE_CACHE=$PWD/gpurun_out/tune_$nm.json run ${TAG}_retune_$nm.txt 600 python bench.py --steps 5 --warmup 3 ${bargs//,/ } ;;
     retunewith)  # targeted re-tune: every shipped conv_nt key vs the ids IDS only -> gpurun_out/tune_NAME.json
       nm=${rest%%:*}; r2=${rest#*:}; ids=${r2%%:*}; bargs=""; [[ "$r2" == *:* ]] && bargs=${r2#*:}
-      PDT_TUNE_ROUNDS=4 PDT_RETUNE_WITH=${ids//+/,} PDT_RETUNE_AX=${PDT_RETUNE_AX:-} PDT_AUTOTUNE_CACHE=$PWD/gpurun_out/tune_$nm.json run ${TAG}_retunewith_$nm.txt 600 python bench.py --steps 5 --warmup 3 ${bargs//,/ } ;;
+      PDT_TUNE_ROUNDS=4 PDT_RETUNE_WITH=${ids//+/,} PDT_RETUNE_AX=${PDT_RETUNE_AX//+/,} PDT_AUTOTUNE_CACHE=$PWD/gpurun_out/tune_$nm.json run ${TAG}_retunewith_$nm.txt 600 python bench.py --steps 5 --warmup 3 ${bargs//,/ } ;;
     py)
       scr=${rest%%:*}; sargs=""; [[ "$rest" == *:* ]] && sargs=${rest#*:}
       run ${TAG}_py_$(basename $scr .py)$(echo "$sargs" | tr -c 'a-zA-Z0-9_\n' '_' | cut -c1-30).txt 600 python -u $scr ${sargs//,/ } ;;
