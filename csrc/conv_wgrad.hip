@@ -56,10 +56,13 @@ struct WGParams {
   const u16* bn_y;   // [M][ldy] the unit's pre-BN conv output
   const float* bn_c; // [5][Mo]: k1, k2, k3, scale, shift
   FastDiv div_Wm, div_HWm, div_C, div_ntw;
+  const void* zero;  // 16 zero bytes: the source of padding / out-of-range chunks (every load is issued)
 };
 
 constexpr int BK = 64;
 constexpr int NT = 256;
+
+static __device__ __attribute__((aligned(64))) u32x4 wg_zero_chunk[4];
 
 // XOR applied to the 32-B segment index of an LDS row. A transposed read's
 // 32-lane half touches rows {8g + q : g = 0,1, q = 0..3} (+4) in one logical
@@ -182,14 +185,14 @@ __global__ void __launch_bounds__(NTH, NTH == NT ? 2 : 1) wgrad_kernel(WGParams 
     const int k0 = kt * BK;
 #pragma unroll
     for (int i = 0; i < NA; ++i) {
+      // every load is issued (padding from the zero page): a load under a per-chunk condition
+      // is branched around and waited for one by one
       int m = k0 + rA0 + AROWS * i;
-      if (okA && m < p.M)
-        ra[i] = *reinterpret_cast<const u32x4*>(p.dy + (size_t)m * p.ldy + coA);
-      else
-        ra[i] = u32x4{0, 0, 0, 0};
+      const bool ok = okA && m < p.M;
+      ra[i] = *reinterpret_cast<const u32x4*>(ok ? (const void*)(p.dy + (size_t)m * p.ldy + coA) : p.zero);
       if constexpr (BNA) {
-        rv[i] = okA && m < p.M;
-        ry[i] = rv[i] ? *reinterpret_cast<const u32x4*>(p.bn_y + (size_t)m * p.ldy + coA) : u32x4{0, 0, 0, 0};
+        rv[i] = ok;
+        ry[i] = *reinterpret_cast<const u32x4*>(ok ? (const void*)(p.bn_y + (size_t)m * p.ldy + coA) : p.zero);
       }
     }
 #pragma unroll
@@ -203,10 +206,8 @@ __global__ void __launch_bounds__(NTH, NTH == NT ? 2 : 1) wgrad_kernel(WGParams 
       uint32_t ow = rem - oh * p.Wm;
       int ih = (int)(oh * p.sh) + offh, iw = (int)(ow * p.sw) + offw;
       ok = ok && (unsigned)ih < (unsigned)p.Hs && (unsigned)iw < (unsigned)p.Ws;
-      if (ok)
-        rb[i] = *reinterpret_cast<const u32x4*>(p.x + ((size_t)(img * p.Hs + ih) * p.Ws + iw) * p.pix + cB_ch);
-      else
-        rb[i] = u32x4{0, 0, 0, 0};
+      rb[i] = *reinterpret_cast<const u32x4*>(
+          ok ? (const void*)(p.x + ((size_t)(img * p.Hs + ih) * p.Ws + iw) * p.pix + cB_ch) : p.zero);
     }
   };
   auto load_tile = [&](int kt) { load_into(kt, ra, rb); };
@@ -723,6 +724,11 @@ PDT_API int pdt_conv_wgrad2(const void* dy, const void* x, float* slab, float* o
   p.div_HWm = make_fastdiv(Hm * Wm);
   p.div_C = make_fastdiv(C);
   p.div_ntw = make_fastdiv(ntw);
+  {
+    static const void* zc[PDT_MAX_DEV] = {};
+    p.zero = pdt_symbol_addr(HIP_SYMBOL(wg_zero_chunk), zc);
+    if (p.zero == nullptr) return PDT_ERR_SYMBOL;
+  }
   const WGVar w = wg_variant(variant, Mo, No);
   int tiles = ((Mo + w.BM - 1) / w.BM) * ((No + w.BN - 1) / w.BN);
   dim3 grid(tiles * splits);
