@@ -286,8 +286,10 @@ __global__ void __launch_bounds__(WNTH, 1) __attribute__((amdgpu_waves_per_eu(1,
 #pragma unroll
     for (int l = 0; l < WLC; ++l) {
       const int px = (tid >> 3) + (WNTH / 8) * l;
-      ra[l] = live ? *reinterpret_cast<const u32x4*>(p.dA + base + (size_t)px * 64) : u32x4{0u, 0u, 0u, 0u};
-      ry[l] = live ? *reinterpret_cast<const u32x4*>(p.y + base + (size_t)px * 64) : u32x4{0u, 0u, 0u, 0u};
+      // (loads issued unconditionally -- the zero page past the last tile: a load under even a
+      // wave-uniform condition is branched around and waited for on its own)
+      ra[l] = *reinterpret_cast<const u32x4*>(live ? (const void*)(p.dA + base + (size_t)px * 64) : p.zero);
+      ry[l] = *reinterpret_cast<const u32x4*>(live ? (const void*)(p.y + base + (size_t)px * 64) : p.zero);
     }
   };
   auto issue_patch = [&](int tile, int buf) __attribute__((always_inline)) {

@@ -139,12 +139,14 @@ __global__ void __launch_bounds__(NTH, NTH == 256 && !GL && BM * BN < 65536 ? 2 
 #pragma unroll
     for (int i = 0; i < NA; ++i) {
       const int m = k0 + rA0 + AROWS * i;
-      ra[i] = (okA && m < p.M) ? *reinterpret_cast<const u32x4*>(p.dy + (size_t)m * p.ldy + coA) : u32x4{0, 0, 0, 0};
+      // every load is issued (padding from the zero page): hipcc branches around a load under a
+      // per-chunk condition and waits for it alone
+      ra[i] = *reinterpret_cast<const u32x4*>((okA && m < p.M) ? (const void*)(p.dy + (size_t)m * p.ldy + coA) : p.zero);
     }
 #pragma unroll
     for (int i = 0; i < NB; ++i) {
       const int m = k0 + rB0 + BROWS * i;
-      rb[i] = (okB && m < p.M) ? *reinterpret_cast<const u32x4*>(p.x + (size_t)m * p.ldx + tcB) : u32x4{0, 0, 0, 0};
+      rb[i] = *reinterpret_cast<const u32x4*>((okB && m < p.M) ? (const void*)(p.x + (size_t)m * p.ldx + tcB) : p.zero);
     }
   };
   auto store_tile = [&](int buf) {
