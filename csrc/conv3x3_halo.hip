@@ -281,14 +281,24 @@ __global__ void __launch_bounds__(NTH, 1) conv3x3_halo_kernel(NTParams p, int rs
           sh = *reinterpret_cast<const f32x4*>(p.bnb.shift + col);
         }
         f32x2 s01 = {0.f, 0.f}, s23 = s01, q01 = s01, q23 = s01;
+        // every row's y (and mask byte) is loaded before the first is used: one wait, not MI
+        uint2 yv[MI];
+        uint32_t mv[MI];
+#pragma unroll
+        for (int i = 0; i < MI; ++i) {
+          const int m = m0 + wm * (HBM / HWM) + i * 16 + lr16;
+          const size_t e = (size_t)(m < p.M ? m : 0) * p.ldo + col;
+          yv[i] = *reinterpret_cast<const uint2*>(p.bnb.y + e);
+          // (col is a multiple of 4: this lane's 4 mask bits are the byte's low or high nibble)
+          mv[i] = BNB == 3 ? (uint32_t)(p.bnb.mask[e >> 3] >> (e & 7)) : 0xfu;
+        }
 #pragma unroll
         for (int i = 0; i < MI; ++i) {
           const int m = m0 + wm * (HBM / HWM) + i * 16 + lr16;
           const bool rok = m < p.M;
           const size_t e = (size_t)(rok ? m : 0) * p.ldo + col;
-          const uint2 yy = *reinterpret_cast<const uint2*>(p.bnb.y + e);
-          // (col is a multiple of 4: this lane's 4 mask bits are the byte's low or high nibble)
-          const uint32_t mk = BNB == 3 ? (uint32_t)(p.bnb.mask[e >> 3] >> (e & 7)) : 0xfu;
+          const uint2 yy = yv[i];
+          const uint32_t mk = mv[i];
           const uint32_t w0 = pack2bf(acc[i][j][0], acc[i][j][1]), w1 = pack2bf(acc[i][j][2], acc[i][j][3]);
           if (rok) {
             typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));

@@ -348,16 +348,20 @@ int launch_variant(int v, const NTParams& p, hipStream_t st) {
 
 // persistent ring tiles (variant ids PERS0 + i in conv_igemm.hip): the tiles of ids
 // PERS_BASE[i], one workgroup per CU walking the output tiles (conv_nt_kernel_pers).
-// Only the 256x128 / 128x256 rings: the 256x256 ones sit at exactly 256 VGPRs (two waves per
-// SIMD) one tile per workgroup, and around the tile loop they spilled 40-44 VGPRs.
-constexpr int NVAR_PERS = 2;
-constexpr int PERS_BASE[NVAR_PERS] = {34, 35};
+// The 256x128 / 128x256 rings, and the 256x256 one (id 36) with the BN-backward epilogue only:
+// its plain-store instantiation sits at 256 VGPRs one tile per workgroup and spilled 236 B
+// around the tile loop, while the compiled BN-backward walks fit in 255 without spilling.
+constexpr int NVAR_PERS = 3;
+constexpr int PERS_BASE[NVAR_PERS] = {34, 35, 36};
 
 template <bool CS64, bool BNB = false>
 int launch_variant_pers(int i, const NTParams& p, hipStream_t st) {
   switch (i) {
     case 0: return launch<256, 128, 3, CS64, false, true, 512, 4, 0, true, BNB, 0, true>(p, st);
     case 1: return launch<128, 256, 3, CS64, false, true, 512, 2, 0, true, BNB, 0, true>(p, st);
+    case 2:
+      if constexpr (BNB) return launch<256, 256, 2, CS64, false, true, 512, 2, 0, true, BNB, 0, true>(p, st);
+      else return -5;
   }
   return -3;
 }
