@@ -3323,10 +3323,12 @@ def qkv_attention(qkv, num_heads, fp8=False, fp8_for=None, grad_fp8_for=None):
     the fp8 layer that produced qkv -- the backward then also writes its e5m2 output
     gradient (``_pdt_f8g`` on d(qkv))."""
     meta = None
-    # Off by default (PDT_FP8_ATTN_Q8=1 enables): the attention kernels write O / d(qkv) one
-    # row per lane, so the extra 4-byte code stores are uncoalesced and cost more than the
-    # separate cast passes they replace (same-box A/B: 6.32k vs 6.40k img/s, runs r4e-r4h)
-    q8 = os.environ.get("PDT_FP8_ATTN_Q8", "0")  # "fwd": only the forward's e4m3 output codes
+    # Default "fwd": the fp8 attention forward also writes the projection's e4m3 input codes
+    # (same-box A/B, round 6 q29: 11 626 / 11 640 vs 11 546 / 11 558 img/s with the separate cast
+    # pass, "0"). "1" adds the bf16 backward's d(qkv) codes (the fp8 backward writes its own:
+    # _attn_bwd_q8_target); in round 4 (r4e-r4h) the then-kernels' uncoalesced code stores cost
+    # more than the casts (6.32k vs 6.40k img/s), which is why this was off until round 6.
+    q8 = os.environ.get("PDT_FP8_ATTN_Q8", "fwd")
     if q8 != "1":
         if not fp8:  # (the fp8 backward's epilogue writes the gradient codes: _attn_bwd_q8_target)
             grad_fp8_for = None
