@@ -40,21 +40,44 @@ __global__ void maxpool_fwd_kernel(const u16* __restrict__ x, u16* __restrict__ 
 #pragma unroll
       for (int j = 0; j < 8; ++j) { sc[j] = scale[cc * 8 + j]; sh[j] = shift[cc * 8 + j]; }
     }
-    for (int kh = 0; kh < k; ++kh) {
-      int ih = oh * s - p + kh;
-      if ((unsigned)ih >= (unsigned)H) continue;
-      for (int kw = 0; kw < k; ++kw) {
-        int iw = ow * s - p + kw;
-        if ((unsigned)iw >= (unsigned)W) continue;
-        float f[8];
-        unpack8(*reinterpret_cast<const u32x4*>(x + (((IdxT)n * H + ih) * W + iw) * C + cc * 8), f);
-        if (AFF) {
+    auto take = [&](const u32x4 v, int w) __attribute__((always_inline)) {
+      float f[8];
+      unpack8(v, f);
+      if (AFF) {
 #pragma unroll
-          for (int j = 0; j < 8; ++j) f[j] = fmaxf(f[j] * sc[j] + sh[j], 0.f);
+        for (int j = 0; j < 8; ++j) f[j] = fmaxf(f[j] * sc[j] + sh[j], 0.f);
+      }
+#pragma unroll
+      for (int j = 0; j < 8; ++j)
+        if (f[j] > best[j] || (f[j] != f[j])) { best[j] = f[j]; bi[j] = (uint8_t)w; }
+    };
+    if (k == 3) {
+      // the ResNet stem's window: all 9 loads issued before the first is used (out-of-window
+      // taps read the window's centre pixel and are skipped) -- a load under a per-tap
+      // condition is branched around and waited for on its own
+      const int ih0 = oh * s - p, iw0 = ow * s - p;
+      const int ihc = min(max(ih0 + 1, 0), H - 1), iwc = min(max(iw0 + 1, 0), W - 1);
+      u32x4 v[9];
+#pragma unroll
+      for (int w = 0; w < 9; ++w) {
+        const int ih = ih0 + w / 3, iw = iw0 + w % 3;
+        const bool ok = (unsigned)ih < (unsigned)H && (unsigned)iw < (unsigned)W;
+        v[w] = *reinterpret_cast<const u32x4*>(x + (((IdxT)n * H + (ok ? ih : ihc)) * W + (ok ? iw : iwc)) * C + cc * 8);
+      }
+#pragma unroll
+      for (int w = 0; w < 9; ++w) {
+        const int ih = ih0 + w / 3, iw = iw0 + w % 3;
+        if ((unsigned)ih < (unsigned)H && (unsigned)iw < (unsigned)W) take(v[w], w);
+      }
+    } else {
+      for (int kh = 0; kh < k; ++kh) {
+        int ih = oh * s - p + kh;
+        if ((unsigned)ih >= (unsigned)H) continue;
+        for (int kw = 0; kw < k; ++kw) {
+          int iw = ow * s - p + kw;
+          if ((unsigned)iw >= (unsigned)W) continue;
+          take(*reinterpret_cast<const u32x4*>(x + (((IdxT)n * H + ih) * W + iw) * C + cc * 8), kh * k + kw);
         }
-#pragma unroll
-        for (int j = 0; j < 8; ++j)
-          if (f[j] > best[j] || (f[j] != f[j])) { best[j] = f[j]; bi[j] = (uint8_t)(kh * k + kw); }
       }
     }
     reinterpret_cast<u32x4*>(y)[t] = pack8(best);
