@@ -635,6 +635,9 @@ def main():
                "vs_best_stock": ({"ratio": round(value / (best[0] * world), 4), "stock_img_s": best[0],
                                   "stock_per_gpu_batch": best[1]} if best and value else None),
                "grad_allreduce_probe": ar,
+               # gradients a stock op produced outside the reducer's slots (each one a device copy)
+               "ddp_fallback_copies": getattr(model, "fallback_copies", None),
+               "ddp_fallback_shapes": sorted(getattr(model, "fallback_shapes", ()))[:16] or None,
                "max_mem_gib": round(torch.cuda.max_memory_allocated() / 2 ** 30, 2) if not cpu else None}
         cfg.update(extra)
         return {

@@ -2600,7 +2600,13 @@ def _pre_bias_grad(g, owner):
     """The bias gradient of ``owner`` if the producer of its output gradient ``g`` (a LayerNorm
     backward, :func:`_ln_fork_backward`) already formed it, else None."""
     pre = getattr(g, "_pdt_db", None) if g is not None else None
-    return pre[0] if pre is not None and pre[1] is owner else None
+    if pre is None or pre[1] is not owner:
+        return None
+    # dropped from ``g``: a LayerNorm's dx also feeds the residual branch, so it outlives this
+    # backward, and a second reference to the bias gradient (a reducer slot view) would make
+    # autograd clone it instead of adopting it as ``bias.grad`` (and the reducer copy it back)
+    del g._pdt_db
+    return pre[0]
 
 
 def _fp8_wgrad_on() -> bool:

@@ -156,6 +156,7 @@ class BucketedDDP(torch.nn.Module):
         self._sync = True
         self._in_backward = False
         self.fallback_copies = 0  # gradients that had to be copied into their slot (stock ops)
+        self.fallback_shapes = set()  # their parameter shapes (bench.py records them)
         self.params = [p for p in module.parameters() if p.requires_grad]
         self._verify_shapes()
         self._broadcast_state()
@@ -252,6 +253,7 @@ class BucketedDDP(torch.nn.Module):
             slot.copy_(g)
             p.grad = slot
             self.fallback_copies += 1
+            self.fallback_shapes.add(tuple(p.shape))
         b = self.buckets[self._bucket_of[id(p)]]
         b.ready += 1
         if b.ready == len(b.params):

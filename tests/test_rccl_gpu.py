@@ -118,6 +118,50 @@ def test_rccl_one_rank_ddp_native_grads(hook):
         assert err < 1e-2, err      # bf16-compressed buckets
 
 
+def _vit_worker(port, q):
+    try:
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK="0", WORLD_SIZE="1",
+                          LOCAL_RANK="0")
+        from pytorch_distributed_template_amd.models.vit import VisionTransformer
+        from pytorch_distributed_template_amd.ops import fused
+        from pytorch_distributed_template_amd.parallel import wrap_ddp
+        from pytorch_distributed_template_amd.utils import dist as pdist
+        dev = pdist.init_distributed()
+        fused.set_backend("native")
+        torch.manual_seed(0)
+        model = VisionTransformer(depth=2, fp8=True).to(dev).to(memory_format=torch.channels_last)
+        ddp = wrap_ddp(model, dev, bucket_cap_mb=8, broadcast_buffers=True, gradient_as_bucket_view=True)
+        x = torch.randn(8, 3, 224, 224, device=dev)
+        y = torch.randint(0, 1000, (8,), device=dev)
+        for _ in range(3):  # the fp8 scaling state (and the fused bias-gradient paths) settle
+            model.zero_grad(set_to_none=True)
+            fused.softmax_cross_entropy(ddp(x), y).backward()
+        torch.cuda.synchronize()
+        q.put((ddp.fallback_copies, sorted(ddp.fallback_shapes)))
+        import torch.distributed as dist
+        dist.destroy_process_group()
+    except Exception:  # pragma: no cover
+        import traceback
+        q.put(traceback.format_exc())
+
+
+def test_rccl_one_rank_ddp_vit_fp8_grads_in_slots():
+    """The fp8 ViT under the native reducer: every gradient but the two the stock ops of the
+    patch-embedding assembly produce (class token, position embedding) is written into its
+    bucket slot -- including the bias gradients of the attention projection and fc2, which
+    the LayerNorm backward forms and hands over (``_pdt_db``)."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    p = ctx.Process(target=_vit_worker, args=(_port(), q))
+    p.start()
+    res = q.get(timeout=300)
+    p.join(60)
+    assert not isinstance(res, str), res
+    copies, shapes = res
+    assert set(shapes) <= {(1, 1, 768), (1, 197, 768)}, shapes
+    assert copies <= 2 * 3, copies
+
+
 def test_resnet50_config_torchrun_rccl_train_resume_test(tmp_path):
     cfg = json.loads((ROOT / "config" / "resnet50_bf16.json").read_text())
     cfg["trainer"].update(save_dir=str(tmp_path), len_epoch=2, epochs=1, monitor="max val_accuracy")
